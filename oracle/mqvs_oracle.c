@@ -1,0 +1,648 @@
+/*
+ * mqvs_oracle.c -- CPU restatement of MyScaleDB's brute-force vector scan.
+ *
+ * TEST INFRASTRUCTURE ONLY (see mqvs_oracle.h).  Parity status: pinned by the
+ * reference's SQL known-answer tests (tests/golden/kat_*.json); the reference
+ * itself is unbuildable here (faiss submodule contrib/search-index is empty).
+ *
+ * Build: oracle/Makefile (gcc -O2 -ffp-contract=off; explicit fmaf()).
+ */
+#include "mqvs_oracle.h"
+
+#include <float.h>
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+/* ------------------------------------------------------------------------ */
+/* Distance primitives: faiss fvec_L2sqr / fvec_inner_product / fvec_norm_L2sqr
+ * (third-party, absent).  Sequential order, product rounded then added (no
+ * fma): the reference's own KATs (00001, 00002, 00014) pin this -- an fma
+ * chain misses 00001 rows 3, 4 and 6 by one ulp.  Built -ffp-contract=off. */
+
+float orc_l2sqr(const float *x, const float *y, int64_t d) {
+    float res = 0.0f;
+    for (int64_t i = 0; i < d; i++) {
+        const float t = x[i] - y[i];
+        res = res + t * t;
+    }
+    return res;
+}
+
+float orc_inner_product(const float *x, const float *y, int64_t d) {
+    float res = 0.0f;
+    for (int64_t i = 0; i < d; i++) res = res + x[i] * y[i];
+    return res;
+}
+
+float orc_norm_l2sqr(const float *x, int64_t d) {
+    float res = 0.0f;
+    for (int64_t i = 0; i < d; i++) res = res + x[i] * x[i];
+    return res;
+}
+
+/* The sgemm of faiss's BLAS branch (nx >= 20, exhaustive_*_blas): no KAT
+ * pins it; assumed to be what FMA microkernels compute for one C element, a
+ * sequential fp32 fma chain over k (documented assumption). */
+float orc_gemm_dot(const float *x, const float *y, int64_t d) {
+    float res = 0.0f;
+    for (int64_t i = 0; i < d; i++) res = fmaf(x[i], y[i], res);
+    return res;
+}
+
+/* VectorDataset<Float>::normalize, VectorDataset.h:98-117:
+ *   sum += p[d]*p[d] (separate mul/add), skip if sum < FLT_EPSILON,
+ *   sum = sqrt(sum), p[d] /= sum. */
+void orc_normalize(float *data, int64_t n, int64_t d) {
+    for (int64_t r = 0; r < n; r++) {
+        float *p = data + r * d;
+        float sum = 0.0f;
+        /* built with -ffp-contract=off: separate multiply and add */
+        for (int64_t i = 0; i < d; i++) sum = sum + p[i] * p[i];
+        if (sum < FLT_EPSILON) continue;
+        sum = sqrtf(sum);
+        for (int64_t i = 0; i < d; i++) p[i] = p[i] / sum;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* faiss heap restated (faiss/utils/Heap.h, third-party, absent): 1-based
+ * binary heap whose top is the current worst element; ordering by (value, id)
+ * via cmp2; neutral = FLT_MAX for the L2 max-heap, -FLT_MAX (lowest) for the
+ * IP min-heap.  `is_max` selects CMax (L2) or CMin (IP). */
+
+static inline int cmp2(int is_max, float a1, float b1, int64_t a2, int64_t b2) {
+    if (is_max) return (a1 > b1) || ((a1 == b1) && (a2 > b2));
+    return (a1 < b1) || ((a1 == b1) && (a2 > b2));
+}
+
+static inline int cmp1(int is_max, float a, float b) {
+    return is_max ? (a > b) : (a < b);
+}
+
+static void heap_heapify(int is_max, int64_t k, float *val, int64_t *ids) {
+    const float neutral = is_max ? FLT_MAX : -FLT_MAX;
+    for (int64_t i = 0; i < k; i++) {
+        val[i] = neutral;
+        ids[i] = -1;
+    }
+}
+
+/* faiss heap_replace_top: replace the top with (v, id) and sift down. */
+static void heap_replace_top(int is_max, int64_t k, float *bh_val,
+                             int64_t *bh_ids, float v, int64_t id) {
+    float *val = bh_val - 1; /* 1-based */
+    int64_t *ids = bh_ids - 1;
+    int64_t i = 1;
+    for (;;) {
+        int64_t i1 = i << 1, i2 = i1 + 1;
+        if (i1 > k) break;
+        if (i2 == k + 1 || cmp2(is_max, val[i1], val[i2], ids[i1], ids[i2])) {
+            if (cmp2(is_max, v, val[i1], id, ids[i1])) break;
+            val[i] = val[i1];
+            ids[i] = ids[i1];
+            i = i1;
+        } else {
+            if (cmp2(is_max, v, val[i2], id, ids[i2])) break;
+            val[i] = val[i2];
+            ids[i] = ids[i2];
+            i = i2;
+        }
+    }
+    val[i] = v;
+    ids[i] = id;
+}
+
+static void heap_pop(int is_max, int64_t k, float *bh_val, int64_t *bh_ids) {
+    float *val = bh_val - 1;
+    int64_t *ids = bh_ids - 1;
+    float v = val[k];
+    int64_t id = ids[k];
+    int64_t i = 1;
+    k--;
+    for (;;) {
+        int64_t i1 = i << 1, i2 = i1 + 1;
+        if (i1 > k) break;
+        if (i2 == k + 1 || cmp2(is_max, val[i1], val[i2], ids[i1], ids[i2])) {
+            if (cmp2(is_max, v, val[i1], id, ids[i1])) break;
+            val[i] = val[i1];
+            ids[i] = ids[i1];
+            i = i1;
+        } else {
+            if (cmp2(is_max, v, val[i2], id, ids[i2])) break;
+            val[i] = val[i2];
+            ids[i] = ids[i2];
+            i = i2;
+        }
+    }
+    val[i] = v;
+    ids[i] = id;
+}
+
+/* faiss heap_reorder: sort the heap best-first, move real entries to the
+ * front and pad the tail with (neutral, -1). */
+static void heap_reorder(int is_max, int64_t k, float *val, int64_t *ids) {
+    int64_t i, ii;
+    for (i = 0, ii = 0; i < k; i++) {
+        float v = val[0];
+        int64_t id = ids[0];
+        heap_pop(is_max, k - i, val, ids);
+        val[k - ii - 1] = v;
+        ids[k - ii - 1] = id;
+        if (id != -1) ii++;
+    }
+    memmove(val, val + k - ii, ii * sizeof(*val));
+    memmove(ids, ids + k - ii, ii * sizeof(*ids));
+    const float neutral = is_max ? FLT_MAX : -FLT_MAX;
+    for (; ii < k; ii++) {
+        val[ii] = neutral;
+        ids[ii] = -1;
+    }
+}
+
+/* ------------------------------------------------------------------------ */
+/* knn: faiss knn_L2sqr / knn_inner_product restated.
+ *   nx <  20: exhaustive_*_seq  (direct per-pair formula)
+ *   nx >= 20: exhaustive_*_blas (L2 via norms: (xn + yn) - 2 ip, clamp >= 0)
+ * In both, y is scanned in ascending row order and an element replaces the
+ * heap top only when strictly better in value. */
+
+int orc_knn(const float *x, const float *y, int64_t d, int64_t k, int64_t nx,
+            int64_t ny, int metric, int64_t *ids, float *dist) {
+    if (metric != ORC_L2 && metric != ORC_IP) return -1;
+    const int is_max = (metric == ORC_L2);
+    if (k <= 0) return 0;
+    float *y_norms = NULL, *x_norms = NULL;
+    const int blas = nx >= ORC_BLAS_THRESHOLD;
+    if (blas && metric == ORC_L2) {
+        y_norms = (float *)malloc(sizeof(float) * (ny > 0 ? ny : 1));
+        x_norms = (float *)malloc(sizeof(float) * nx);
+        for (int64_t j = 0; j < ny; j++) y_norms[j] = orc_norm_l2sqr(y + j * d, d);
+        for (int64_t i = 0; i < nx; i++) x_norms[i] = orc_norm_l2sqr(x + i * d, d);
+    }
+    for (int64_t i = 0; i < nx; i++) {
+        float *simi = dist + i * k;
+        int64_t *idxi = ids + i * k;
+        const float *xi = x + i * d;
+        heap_heapify(is_max, k, simi, idxi);
+        for (int64_t j = 0; j < ny; j++) {
+            const float *yj = y + j * d;
+            float dis;
+            if (!blas) {
+                dis = (metric == ORC_IP) ? orc_inner_product(xi, yj, d) : orc_l2sqr(xi, yj, d);
+            } else if (metric == ORC_IP) {
+                dis = orc_gemm_dot(xi, yj, d);
+            } else {
+                const float ip = orc_gemm_dot(xi, yj, d);
+                dis = (x_norms[i] + y_norms[j]) - 2.0f * ip;
+                if (dis < 0) dis = 0;
+            }
+            if (cmp1(is_max, simi[0], dis)) heap_replace_top(is_max, k, simi, idxi, dis, j);
+        }
+        heap_reorder(is_max, k, simi, idxi);
+    }
+    free(y_norms);
+    free(x_norms);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Fast, bit-identical variant for CPU timing.  Distances for a block of rows
+ * are computed into a buffer with the same per-pair fma chain, then offered to
+ * the heap in ascending row order, exactly like orc_knn. */
+
+#define FB_ROWS 64   /* rows per block  */
+#define FB_Q 16      /* queries per block (BLAS-branch micro kernel) */
+
+static void seq_block_dist(const float *xi, const float *y, int64_t d,
+                           int64_t rows, int metric, float *out) {
+    /* Transpose-free: for each k, update all rows' chains (vectorises across
+     * rows via strided loads; each chain stays sequential in k). */
+    float acc[FB_ROWS];
+    for (int64_t r = 0; r < rows; r++) acc[r] = 0.0f;
+    for (int64_t kk = 0; kk < d; kk++) {
+        const float xv = xi[kk];
+        if (metric == ORC_L2) {
+            for (int64_t r = 0; r < rows; r++) {
+                const float t = xv - y[r * d + kk];
+                acc[r] = acc[r] + t * t;
+            }
+        } else {
+            for (int64_t r = 0; r < rows; r++) acc[r] = acc[r] + xv * y[r * d + kk];
+        }
+    }
+    for (int64_t r = 0; r < rows; r++) out[r] = acc[r];
+}
+
+int orc_knn_fast(const float *x, const float *y, int64_t d, int64_t k,
+                 int64_t nx, int64_t ny, int metric, int64_t *ids, float *dist) {
+    if (metric != ORC_L2 && metric != ORC_IP) return -1;
+    const int is_max = (metric == ORC_L2);
+    if (k <= 0) return 0;
+    const int blas = nx >= ORC_BLAS_THRESHOLD;
+    for (int64_t i = 0; i < nx; i++) heap_heapify(is_max, k, dist + i * k, ids + i * k);
+    float *buf = (float *)malloc(sizeof(float) * FB_ROWS * (nx > 0 ? nx : 1));
+    float *x_norms = NULL, *xt = NULL;
+    if (blas) {
+        /* queries transposed [d][nx_pad] so a block of FB_Q queries is
+         * contiguous for each k */
+        const int64_t nxp = (nx + FB_Q - 1) / FB_Q * FB_Q;
+        xt = (float *)calloc((size_t)d * nxp, sizeof(float));
+        for (int64_t i = 0; i < nx; i++)
+            for (int64_t kk = 0; kk < d; kk++) xt[kk * nxp + i] = x[i * d + kk];
+        if (metric == ORC_L2) {
+            x_norms = (float *)malloc(sizeof(float) * nx);
+            for (int64_t i = 0; i < nx; i++) x_norms[i] = orc_norm_l2sqr(x + i * d, d);
+        }
+    }
+    const int64_t nxp = (nx + FB_Q - 1) / FB_Q * FB_Q;
+    for (int64_t j0 = 0; j0 < ny; j0 += FB_ROWS) {
+        const int64_t rows = (ny - j0) < FB_ROWS ? (ny - j0) : FB_ROWS;
+        const float *yb = y + j0 * d;
+        if (!blas) {
+            for (int64_t i = 0; i < nx; i++)
+                seq_block_dist(x + i * d, yb, d, rows, metric, buf + i * FB_ROWS);
+        } else {
+            float y_norms[FB_ROWS];
+            if (metric == ORC_L2)
+                for (int64_t r = 0; r < rows; r++) y_norms[r] = orc_norm_l2sqr(yb + r * d, d);
+            for (int64_t q0 = 0; q0 < nx; q0 += FB_Q) {
+                for (int64_t r = 0; r < rows; r++) {
+                    float acc[FB_Q];
+                    for (int qq = 0; qq < FB_Q; qq++) acc[qq] = 0.0f;
+                    const float *yr = yb + r * d;
+                    for (int64_t kk = 0; kk < d; kk++) {
+                        const float yv = yr[kk];
+                        const float *xk = xt + kk * nxp + q0;
+                        for (int qq = 0; qq < FB_Q; qq++) acc[qq] = fmaf(xk[qq], yv, acc[qq]);
+                    }
+                    for (int qq = 0; qq < FB_Q && q0 + qq < nx; qq++) {
+                        float dis = acc[qq];
+                        if (metric == ORC_L2) {
+                            dis = (x_norms[q0 + qq] + y_norms[r]) - 2.0f * acc[qq];
+                            if (dis < 0) dis = 0;
+                        }
+                        buf[(q0 + qq) * FB_ROWS + r] = dis;
+                    }
+                }
+            }
+        }
+        for (int64_t i = 0; i < nx; i++) {
+            float *simi = dist + i * k;
+            int64_t *idxi = ids + i * k;
+            const float *bi = buf + i * FB_ROWS;
+            for (int64_t r = 0; r < rows; r++)
+                if (cmp1(is_max, simi[0], bi[r]))
+                    heap_replace_top(is_max, k, simi, idxi, bi[r], j0 + r);
+        }
+    }
+    for (int64_t i = 0; i < nx; i++) heap_reorder(is_max, k, dist + i * k, ids + i * k);
+    free(buf);
+    free(xt);
+    free(x_norms);
+    return 0;
+}
+
+/* ------------------------------------------------------------------------ */
+/* VIWithColumnInPart::searchWithoutIndex, VIWithDataPart.h:341-382. */
+
+typedef int (*knn_fn)(const float *, const float *, int64_t, int64_t, int64_t,
+                      int64_t, int, int64_t *, float *);
+
+static int search_without_index_impl(knn_fn knn, float *x, float *y, int64_t d,
+                                     int64_t k, int64_t nx, int64_t ny,
+                                     int metric, int64_t *ids, float *dist) {
+    int m = metric;
+    if (metric == ORC_COSINE) {
+        m = ORC_IP;
+        orc_normalize(x, nx, d);
+        orc_normalize(y, ny, d);
+    }
+    int rc = knn(x, y, d, k, nx, ny, m, ids, dist);
+    if (rc) return rc;
+    if (metric == ORC_COSINE)
+        for (int64_t i = 0; i < k * nx; i++) dist[i] = 1 - dist[i];
+    return 0;
+}
+
+int orc_search_without_index(float *x, float *y, int64_t d, int64_t k,
+                             int64_t nx, int64_t ny, int metric, int64_t *ids,
+                             float *dist) {
+    return search_without_index_impl(orc_knn, x, y, d, k, nx, ny, metric, ids, dist);
+}
+
+/* ------------------------------------------------------------------------ */
+/* MergeTreeVSManager::searchWrapper, MergeTreeVSManager.cpp:1538-1680. */
+
+static inline int bit_test(const uint8_t *bm, int64_t i) {
+    return (bm[i >> 3] >> (i & 7)) & 1;
+}
+
+static int search_wrapper(knn_fn knn, int prewhere, float *query, int64_t nq,
+                          float *base, int64_t nbase, int64_t d, int64_t k,
+                          int64_t num_rows_read, int64_t *final_id,
+                          float *final_dist, const int64_t *actual_id_in_range,
+                          int metric, const uint8_t *row_exists_chunk,
+                          int64_t delete_id_num) {
+    const float init = (metric == ORC_IP) ? FLT_MIN : FLT_MAX;
+    const int64_t kk = k + delete_id_num;
+    float *per_dist = (float *)malloc(sizeof(float) * k * nq);
+    int64_t *per_id = (int64_t *)malloc(sizeof(int64_t) * k * nq);
+    float *tmp_dist = (float *)malloc(sizeof(float) * kk * nq);
+    int64_t *tmp_id = (int64_t *)malloc(sizeof(int64_t) * kk * nq);
+    for (int64_t i = 0; i < k * nq; i++) {
+        per_dist[i] = init;
+        per_id[i] = -1;
+    }
+    float *dd = delete_id_num > 0 ? tmp_dist : per_dist;
+    int64_t *ii = delete_id_num > 0 ? tmp_id : per_id;
+    int rc = search_without_index_impl(knn, query, base, d, kk, nq, nbase, metric, ii, dd);
+    if (rc) goto out;
+    if (delete_id_num > 0) {
+        for (int64_t q = 0; q < nq; q++) {
+            int64_t cur = 0, tcur = 0;
+            while (cur < k && tcur < kk) {
+                const int64_t tid = tmp_id[q * kk + tcur];
+                if (tid >= 0 && bit_test(row_exists_chunk, tid)) {
+                    per_id[q * k + cur] = tid;
+                    per_dist[q * k + cur] = tmp_dist[q * kk + tcur];
+                    ++cur;
+                }
+                ++tcur;
+            }
+        }
+    }
+    if (prewhere)
+        for (int64_t i = 0; i < k * nq; i++)
+            if (per_id[i] > -1) per_id[i] = actual_id_in_range[per_id[i]];
+    {
+        float *inter_d = (float *)malloc(sizeof(float) * k * nq);
+        int64_t *inter_i = (int64_t *)malloc(sizeof(int64_t) * k * nq);
+        for (int64_t q = 0; q < nq; q++) {
+            int64_t j = q * k, z = q * k;
+            for (int64_t i = 0; i < k; i++) {
+                if ((metric != ORC_IP && final_dist[j] > per_dist[z]) ||
+                    (metric == ORC_IP && final_dist[j] < per_dist[z])) {
+                    inter_d[q * k + i] = per_dist[z];
+                    inter_i[q * k + i] = per_id[z] + num_rows_read;
+                    z++;
+                } else {
+                    inter_d[q * k + i] = final_dist[j];
+                    inter_i[q * k + i] = final_id[j];
+                    j++;
+                }
+            }
+        }
+        memcpy(final_dist, inter_d, sizeof(float) * k * nq);
+        memcpy(final_id, inter_i, sizeof(int64_t) * k * nq);
+        free(inter_d);
+        free(inter_i);
+    }
+out:
+    free(per_dist);
+    free(per_id);
+    free(tmp_dist);
+    free(tmp_id);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------ */
+/* MergeTreeVSManager::vectorScanWithoutIndex, MergeTreeVSManager.cpp:960-1536
+ * (FloatVector branch) with a single read range covering the whole part. */
+
+static int vector_scan_impl(knn_fn knn, const float *rows, const uint8_t *nonempty,
+                            int64_t n, int64_t d, const int64_t *mark_rows,
+                            int64_t n_marks, const float *queries, int64_t nq,
+                            int64_t k, int metric, const uint8_t *filter,
+                            const uint8_t *row_exists, int64_t *out_ids,
+                            float *out_dist) {
+    if (metric != ORC_L2 && metric != ORC_IP && metric != ORC_COSINE) return -1;
+    const float init = (metric == ORC_IP) ? FLT_MIN : FLT_MAX;
+    for (int64_t i = 0; i < k * nq; i++) {
+        out_dist[i] = init;
+        out_ids[i] = -1;
+    }
+    if (n == 0 || nq == 0 || k <= 0) return 0;
+    /* the query dataset object is shared across chunks (normalised in place
+     * on every cosine call, VIWithDataPart.h:358) */
+    float *query = (float *)malloc(sizeof(float) * nq * d);
+    memcpy(query, queries, sizeof(float) * nq * d);
+    int rc = 0;
+    if (filter) {
+        /* :1043-1331: one mark at a time; gather selected non-empty rows */
+        int64_t filter_parsed = 0, row0 = 0;
+        float *chunk = NULL;
+        int64_t *actual = NULL;
+        for (int64_t m = 0; m < n_marks && row0 < n; m++) {
+            int64_t rows_m = mark_rows[m];
+            if (row0 + rows_m > n) rows_m = n - row0;
+            chunk = (float *)realloc(chunk, sizeof(float) * (rows_m > 0 ? rows_m : 1) * d);
+            actual = (int64_t *)realloc(actual, sizeof(int64_t) * (rows_m > 0 ? rows_m : 1));
+            int64_t left = 0;
+            for (int64_t i = filter_parsed; i < filter_parsed + rows_m; i++) {
+                if (i == n) break;
+                if (bit_test(filter, i) && (!row_exists || bit_test(row_exists, i)) &&
+                    (!nonempty || nonempty[i])) {
+                    memcpy(chunk + left * d, rows + i * d, sizeof(float) * d);
+                    actual[left] = i; /* current_rows_in_range, single range */
+                    left++;
+                }
+            }
+            filter_parsed += rows_m;
+            row0 += rows_m;
+            if (left == 0) continue;
+            rc = search_wrapper(knn, 1, query, nq, chunk, left, d, k, 0, out_ids,
+                                out_dist, actual, metric, NULL, 0);
+            if (rc) break;
+        }
+        free(chunk);
+        free(actual);
+    } else {
+        /* :1332-1498: uniform chunks of getMarkRows(0) rows */
+        const int64_t chunk_rows = n_marks > 0 && mark_rows[0] > 0 ? mark_rows[0] : n;
+        float *chunk = (float *)malloc(sizeof(float) * chunk_rows * d);
+        uint8_t *exists = (uint8_t *)malloc((size_t)(chunk_rows + 7) / 8);
+        for (int64_t r0 = 0; r0 < n; r0 += chunk_rows) {
+            const int64_t rows_c = (n - r0) < chunk_rows ? (n - r0) : chunk_rows;
+            /* src_vec.empty(): every array in the chunk is empty -> skipped */
+            int any = 0;
+            for (int64_t r = 0; r < rows_c && !any; r++) any = !nonempty || nonempty[r0 + r];
+            if (!any) continue;
+            memcpy(chunk, rows + r0 * d, sizeof(float) * rows_c * d);
+            int64_t deleted = 0;
+            memset(exists, 0xff, (size_t)(rows_c + 7) / 8);
+            if (row_exists) {
+                for (int64_t r = 0; r < rows_c; r++)
+                    if (!bit_test(row_exists, r0 + r)) {
+                        exists[r >> 3] &= (uint8_t)~(1u << (r & 7));
+                        deleted++;
+                    }
+            }
+            rc = search_wrapper(knn, 0, query, nq, chunk, rows_c, d, k, r0, out_ids,
+                                out_dist, NULL, metric, exists, deleted);
+            if (rc) break;
+        }
+        free(chunk);
+        free(exists);
+    }
+    free(query);
+    return rc;
+}
+
+int orc_vector_scan(const float *rows, const uint8_t *nonempty, int64_t n,
+                    int64_t d, const int64_t *mark_rows, int64_t n_marks,
+                    const float *queries, int64_t nq, int64_t k, int metric,
+                    const uint8_t *filter, const uint8_t *row_exists,
+                    int64_t *out_ids, float *out_dist) {
+    return vector_scan_impl(orc_knn, rows, nonempty, n, d, mark_rows, n_marks, queries,
+                            nq, k, metric, filter, row_exists, out_ids, out_dist);
+}
+
+int orc_vector_scan_fast(const float *rows, const uint8_t *nonempty, int64_t n,
+                         int64_t d, const int64_t *mark_rows, int64_t n_marks,
+                         const float *queries, int64_t nq, int64_t k,
+                         int metric, const uint8_t *filter,
+                         const uint8_t *row_exists, int64_t *out_ids,
+                         float *out_dist) {
+    return vector_scan_impl(orc_knn_fast, rows, nonempty, n, d, mark_rows, n_marks,
+                            queries, nq, k, metric, filter, row_exists, out_ids,
+                            out_dist);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Cross-part merge, MergeTreeBaseSearchManager.cpp:207-297: a multimap keyed
+ * by score; equal scores keep insertion order (parts in order, labels in
+ * their list order).  ASC takes the first k; DESC (IP) iterates in reverse,
+ * so equal scores come out in reverse insertion order. */
+
+typedef struct {
+    float score;
+    int64_t seq; /* insertion order */
+    int64_t part, label;
+} mm_entry;
+
+static int mm_cmp(const void *a, const void *b) {
+    const mm_entry *x = (const mm_entry *)a, *y = (const mm_entry *)b;
+    if (x->score < y->score) return -1;
+    if (x->score > y->score) return 1;
+    return (x->seq < y->seq) ? -1 : (x->seq > y->seq);
+}
+
+void orc_merge_parts(int64_t nparts, int64_t k, int metric,
+                     const int64_t *labels, const float *dists,
+                     int64_t *out_part, int64_t *out_label, float *out_dist) {
+    mm_entry *e = (mm_entry *)malloc(sizeof(mm_entry) * (nparts * k + 1));
+    int64_t m = 0;
+    for (int64_t p = 0; p < nparts; p++)
+        for (int64_t i = 0; i < k; i++) {
+            const int64_t lab = labels[p * k + i];
+            if (lab < 0) continue;
+            e[m].score = dists[p * k + i];
+            e[m].seq = m;
+            e[m].part = p;
+            e[m].label = lab;
+            m++;
+        }
+    qsort(e, (size_t)m, sizeof(mm_entry), mm_cmp);
+    for (int64_t i = 0; i < k; i++) {
+        out_part[i] = -1;
+        out_label[i] = -1;
+        out_dist[i] = (metric == ORC_IP) ? FLT_MIN : FLT_MAX;
+    }
+    for (int64_t i = 0; i < k && i < m; i++) {
+        const mm_entry *s = (metric == ORC_IP) ? &e[m - 1 - i] : &e[i];
+        out_part[i] = s->part;
+        out_label[i] = s->label;
+        out_dist[i] = s->score;
+    }
+    free(e);
+}
+
+/* ------------------------------------------------------------------------ */
+/* Reference threading shape for CPU timing (see header). */
+
+int orc_scan_parts(const float *rows, int64_t n, int64_t d, int64_t granule,
+                   const float *queries, int64_t nq, int64_t k, int metric,
+                   int parts, int threads, int64_t *out_ids, float *out_dist) {
+    if (parts < 1) parts = 1;
+    int64_t *pid = (int64_t *)malloc(sizeof(int64_t) * parts * nq * k);
+    float *pdist = (float *)malloc(sizeof(float) * parts * nq * k);
+    int rc = 0;
+#ifdef _OPENMP
+#pragma omp parallel for num_threads(threads) schedule(dynamic, 1) reduction(| : rc)
+#endif
+    for (int p = 0; p < parts; p++) {
+        const int64_t r0 = n * p / parts, r1 = n * (p + 1) / parts;
+        const int64_t g = granule;
+        rc |= orc_vector_scan_fast(rows + r0 * d, NULL, r1 - r0, d, &g, 1, queries, nq, k,
+                                   metric, NULL, NULL, pid + (int64_t)p * nq * k,
+                                   pdist + (int64_t)p * nq * k);
+        /* labels are part-local; make them global for the merged output */
+        for (int64_t i = 0; i < nq * k; i++)
+            if (pid[(int64_t)p * nq * k + i] >= 0) pid[(int64_t)p * nq * k + i] += r0;
+    }
+    (void)threads;
+    int64_t *lab = (int64_t *)malloc(sizeof(int64_t) * parts * k);
+    float *dd = (float *)malloc(sizeof(float) * parts * k);
+    int64_t *opart = (int64_t *)malloc(sizeof(int64_t) * k);
+    for (int64_t q = 0; q < nq; q++) {
+        for (int p = 0; p < parts; p++) {
+            memcpy(lab + p * k, pid + ((int64_t)p * nq + q) * k, sizeof(int64_t) * k);
+            memcpy(dd + p * k, pdist + ((int64_t)p * nq + q) * k, sizeof(float) * k);
+        }
+        orc_merge_parts(parts, k, metric, lab, dd, opart, out_ids + q * k, out_dist + q * k);
+    }
+    free(lab);
+    free(dd);
+    free(opart);
+    free(pid);
+    free(pdist);
+    return rc;
+}
+
+/* ------------------------------------------------------------------------ */
+/* Counter-based synthetic generator. */
+
+static inline uint64_t splitmix64(uint64_t z) {
+    z += 0x9e3779b97f4a7c15ULL;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+
+static inline float gen_gauss(uint64_t seed, uint64_t idx) {
+    const uint64_t h = splitmix64(seed ^ idx);
+    const float u0 = (float)(h & 0xffff) * (1.0f / 65536.0f);
+    const float u1 = (float)((h >> 16) & 0xffff) * (1.0f / 65536.0f);
+    const float u2 = (float)((h >> 32) & 0xffff) * (1.0f / 65536.0f);
+    const float u3 = (float)((h >> 48) & 0xffff) * (1.0f / 65536.0f);
+    const float s = (u0 + u1) + (u2 + u3);
+    return (s - 2.0f) * 1.7320508f;
+}
+
+#define ORC_MIX_CENTERS 4096ULL
+
+void orc_generate(uint64_t seed, int mode, int64_t row0, int64_t n, int64_t d,
+                  float *out) {
+    for (int64_t r = 0; r < n; r++) {
+        const uint64_t row = (uint64_t)(row0 + r);
+        const uint64_t c = splitmix64(seed ^ 0xC0FFEEULL ^ (row * 0x100000001B3ULL)) % ORC_MIX_CENTERS;
+        for (int64_t j = 0; j < d; j++) {
+            const uint64_t idx = row * (uint64_t)d + (uint64_t)j;
+            float v;
+            if (mode == 0) {
+                v = (float)((int)(splitmix64(seed ^ idx) % 17ULL) - 8);
+            } else if (mode == 1) {
+                v = gen_gauss(seed, idx);
+            } else {
+                const float center = gen_gauss(seed ^ 0xCE17E5ULL, c * (uint64_t)d + (uint64_t)j);
+                v = center + 0.25f * gen_gauss(seed, idx);
+            }
+            out[r * d + j] = v;
+        }
+    }
+}

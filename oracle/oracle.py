@@ -1,0 +1,165 @@
+"""ctypes loader for the CPU oracle (oracle/_build/libmqvs_oracle.so).
+
+TEST INFRASTRUCTURE ONLY: imported by tests/, __graft_entry__.smoke() and the
+cpu_baseline leg of bench.py -- never by the product package (myscaledb_amd/).
+The C sources (mqvs_oracle.c) restate the reference functions they cite.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "_build", "libmqvs_oracle.so")
+
+L2, IP, COSINE = 0, 1, 2
+METRICS = {"L2": L2, "IP": IP, "Cosine": COSINE, "COSINE": COSINE}
+
+_lib = None
+
+
+def build(quiet: bool = True) -> str:
+    """Compile the oracle with the committed Makefile (gcc)."""
+    out = subprocess.run(["make", "-C", _HERE], capture_output=True, text=True)
+    if out.returncode != 0:
+        raise RuntimeError("oracle build failed:\n" + out.stdout + out.stderr)
+    return _LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        P = ctypes.c_void_p
+        I64 = ctypes.c_int64
+        L.orc_knn.argtypes = [P, P, I64, I64, I64, I64, ctypes.c_int, P, P]
+        L.orc_knn_fast.argtypes = L.orc_knn.argtypes
+        L.orc_search_without_index.argtypes = L.orc_knn.argtypes
+        L.orc_normalize.argtypes = [P, I64, I64]
+        L.orc_vector_scan.argtypes = [P, P, I64, I64, P, I64, P, I64, I64, ctypes.c_int, P, P, P, P]
+        L.orc_vector_scan_fast.argtypes = L.orc_vector_scan.argtypes
+        L.orc_scan_parts.argtypes = [P, I64, I64, I64, P, I64, I64, ctypes.c_int, ctypes.c_int,
+                                     ctypes.c_int, P, P]
+        L.orc_merge_parts.argtypes = [I64, I64, ctypes.c_int, P, P, P, P, P]
+        L.orc_generate.argtypes = [ctypes.c_uint64, ctypes.c_int, I64, I64, I64, P]
+        L.orc_l2sqr.argtypes = [P, P, I64]
+        L.orc_l2sqr.restype = ctypes.c_float
+        L.orc_inner_product.argtypes = [P, P, I64]
+        L.orc_inner_product.restype = ctypes.c_float
+        for f in ("orc_knn", "orc_knn_fast", "orc_search_without_index", "orc_vector_scan",
+                  "orc_vector_scan_fast", "orc_scan_parts"):
+            getattr(L, f).restype = ctypes.c_int
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def knn(x, y, k, metric, fast=False):
+    """tryBruteForceSearch (BruteForceSearch.h:62-111)."""
+    x, y = _f32(x), _f32(y)
+    nx, d = x.shape
+    ny = y.shape[0]
+    ids = np.empty((nx, k), np.int64)
+    dist = np.empty((nx, k), np.float32)
+    fn = lib().orc_knn_fast if fast else lib().orc_knn
+    rc = fn(_p(x), _p(y), d, k, nx, ny, metric, _p(ids), _p(dist))
+    if rc:
+        raise NotImplementedError("metric not implemented in brute force search")
+    return ids, dist
+
+
+def search_without_index(x, y, k, metric):
+    """VIWithColumnInPart::searchWithoutIndex; copies (the C function mutates)."""
+    x, y = _f32(x).copy(), _f32(y).copy()
+    nx, d = x.shape
+    ids = np.empty((nx, k), np.int64)
+    dist = np.empty((nx, k), np.float32)
+    rc = lib().orc_search_without_index(_p(x), _p(y), d, k, nx, y.shape[0], metric, _p(ids), _p(dist))
+    if rc:
+        raise NotImplementedError
+    return ids, dist
+
+
+def normalize(a):
+    a = _f32(a).copy()
+    lib().orc_normalize(_p(a), a.shape[0], a.shape[1])
+    return a
+
+
+def vector_scan(rows, queries, k, metric, mark_rows, nonempty=None, filter_bits=None,
+                row_exists_bits=None, fast=False):
+    """MergeTreeVSManager::vectorScanWithoutIndex over one part.
+
+    rows: (n, d) float32 (FLT_MAX-filled where the array is empty);
+    nonempty: (n,) uint8 or None; filter_bits/row_exists_bits: packed LSB-first
+    uint8 bitmaps (np.packbits(..., bitorder='little')) or None;
+    mark_rows: int or list of rows per mark.
+    """
+    rows, queries = _f32(rows), _f32(queries)
+    n, d = rows.shape
+    nq = queries.shape[0]
+    if np.isscalar(mark_rows):
+        mr = np.full(max(1, -(-n // int(mark_rows))), int(mark_rows), np.int64)
+    else:
+        mr = np.ascontiguousarray(mark_rows, np.int64)
+    ne = None if nonempty is None else np.ascontiguousarray(nonempty, np.uint8)
+    fb = None if filter_bits is None else np.ascontiguousarray(filter_bits, np.uint8)
+    rb = None if row_exists_bits is None else np.ascontiguousarray(row_exists_bits, np.uint8)
+    ids = np.empty((nq, k), np.int64)
+    dist = np.empty((nq, k), np.float32)
+    fn = lib().orc_vector_scan_fast if fast else lib().orc_vector_scan
+    rc = fn(_p(rows), _p(ne), n, d, _p(mr), len(mr), _p(queries), nq, k, metric, _p(fb), _p(rb),
+            _p(ids), _p(dist))
+    if rc:
+        raise NotImplementedError
+    return ids, dist
+
+
+def scan_parts(rows, queries, k, metric, granule, parts, threads):
+    rows, queries = _f32(rows), _f32(queries)
+    n, d = rows.shape
+    nq = queries.shape[0]
+    ids = np.empty((nq, k), np.int64)
+    dist = np.empty((nq, k), np.float32)
+    lib().orc_scan_parts(_p(rows), n, d, granule, _p(queries), nq, k, metric, parts, threads,
+                         _p(ids), _p(dist))
+    return ids, dist
+
+
+def merge_parts(labels, dists, metric):
+    labels = np.ascontiguousarray(labels, np.int64)
+    dists = _f32(dists)
+    nparts, k = labels.shape
+    op = np.empty(k, np.int64)
+    ol = np.empty(k, np.int64)
+    od = np.empty(k, np.float32)
+    lib().orc_merge_parts(nparts, k, metric, _p(labels), _p(dists), _p(op), _p(ol), _p(od))
+    return op, ol, od
+
+
+def generate(seed, mode, row0, n, d):
+    out = np.empty((n, d), np.float32)
+    lib().orc_generate(seed, mode, row0, n, d, _p(out))
+    return out
+
+
+def l2sqr(x, y):
+    x, y = _f32(x), _f32(y)
+    return lib().orc_l2sqr(_p(x), _p(y), x.shape[0])
+
+
+def inner_product(x, y):
+    x, y = _f32(x), _f32(y)
+    return lib().orc_inner_product(_p(x), _p(y), x.shape[0])
