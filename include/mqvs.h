@@ -1,0 +1,175 @@
+/*
+ * mqvs.h -- C-ABI of libmqvs.so, the MI355X (gfx950) vector-scan engine that
+ * sits behind MyScaleDB's brute-force distance() path.
+ *
+ * Every entry point is plain C (pointers, sizes, ints); no HIP, torch or C++
+ * types cross this boundary.  The reference-side C++ binding that a MyScaleDB
+ * maintainer drops in is include/mqvs_vector_index.hpp.
+ *
+ * Reference interfaces replaced (paths relative to the MyScaleDB tree):
+ *   mqvs_knn_raw        VectorIndex::tryBruteForceSearch<FloatVector>
+ *                       src/VectorIndex/Common/BruteForceSearch.h:62-111
+ *   mqvs_segment_*      the per-granule copy of the Array(Float32) column into
+ *                       `vector_raw_data` + VectorDataset construction,
+ *                       src/VectorIndex/Storages/MergeTreeVSManager.cpp:1366-1393,
+ *                       src/VectorIndex/Common/VectorDataset.h:31-60
+ *                       (a whole data part is registered once and stays in HBM)
+ *   mqvs_search         MergeTreeVSManager::vectorScanWithoutIndex<Float> +
+ *                       searchWrapper + VIWithColumnInPart::searchWithoutIndex,
+ *                       MergeTreeVSManager.cpp:960-1680, VIWithDataPart.h:341-382
+ *   mqvs_rerank         VIWithColumnInPart::computeTopDistanceSubset,
+ *                       src/VectorIndex/Common/VIWithDataPart.cpp:838-856
+ *   mqvs_merge_shards   MergeTreeBaseSearchManager::getTotalTopSearchResultImpl,
+ *                       src/VectorIndex/Storages/MergeTreeBaseSearchManager.cpp:207-297
+ *                       (and the Distributed engine's shard merge)
+ *   mqvs_last_error /   DB::Exception(code, message) thrown by the above
+ *   status codes        (ErrorCodes NOT_IMPLEMENTED, LOGICAL_ERROR, ...)
+ *
+ * Threading: re-entrant.  Each calling thread gets its own HIP stream and
+ * scratch workspace; segments are read-only after creation and may be searched
+ * from any number of threads (the reference admits 2 x physical cores
+ * concurrent scans, MergeTreeVSManager.cpp:974-975).
+ */
+#ifndef MQVS_H
+#define MQVS_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define MQVS_ABI_VERSION 1
+
+/* Metric ids (VICommon.h VIMetric; float vectors only in this version). */
+enum {
+    MQVS_METRIC_L2 = 0,     /* squared L2, ascending */
+    MQVS_METRIC_IP = 1,     /* inner product, descending */
+    MQVS_METRIC_COSINE = 2  /* 1 - <q/|q|, y/|y|>, ascending */
+};
+
+/* Status codes; each maps 1:1 onto the DB::ErrorCodes the reference throws. */
+enum {
+    MQVS_OK = 0,
+    MQVS_ERR_NOT_IMPLEMENTED = 1,   /* unsupported metric (BruteForceSearch.h:89) */
+    MQVS_ERR_LOGICAL = 2,           /* dim mismatch, wrong segment metric (LOGICAL_ERROR) */
+    MQVS_ERR_ILLEGAL_COLUMN = 3,    /* malformed column data */
+    MQVS_ERR_BAD_ARGUMENTS = 4,     /* null pointers, k <= 0, ... */
+    MQVS_ERR_MEMORY_LIMIT = 5,      /* HBM allocation failed (MEMORY_LIMIT_EXCEEDED) */
+    MQVS_ERR_DEVICE = 6             /* HIP runtime / kernel failure */
+};
+
+/* mqvs_search / mqvs_rerank flags */
+#define MQVS_F_DEVICE_PTRS 0x1u /* queries, bitmaps, candidates and outputs are
+                                   device pointers on the segment's GPU */
+#define MQVS_F_ASYNC 0x2u       /* with DEVICE_PTRS: do not synchronise the
+                                   stream before returning (results valid after
+                                   the stream drains); the candidate-overflow
+                                   fallback then reports MQVS_ERR_LOGICAL */
+
+typedef struct mqvs_segment *mqvs_segment_t;
+typedef void *mqvs_stream_t; /* a hipStream_t, or NULL for the caller thread's stream */
+
+/* ---- lifecycle ---------------------------------------------------------- */
+int mqvs_abi_version(void);
+/* Bind the calling thread to `device` (a HIP ordinal). */
+int mqvs_init(int device);
+int mqvs_device_count(int *count);
+/* Thread-local message of the last failing call on this thread. */
+const char *mqvs_last_error(void);
+/* Release this thread's stream/workspace (optional; freed at thread exit). */
+int mqvs_thread_release(void);
+
+/* ---- segments: one data part's Array(Float32) column resident in HBM ---- */
+/* host_rows: n*d row-major fp32; rows whose Array is empty must be FLT_MAX
+ *   filled (MergeTreeVSManager.cpp:1381) and flagged 0 in `nonempty`.
+ * nonempty: n bytes (1 = non-empty array) or NULL (all non-empty).
+ * metric: the column's metric; COSINE segments are normalised in HBM once
+ *   (VectorDataset.h:98-117 per row) and serve only cosine searches; L2/IP
+ *   segments serve both L2 and IP.
+ * granule_rows: index_granularity (rows per mark; reads are chunked by it).
+ * row_offset: id of row 0 (0 for a whole part; shard start for a row-range
+ *   shard of a part -- must be a multiple of granule_rows). */
+int mqvs_segment_create(const float *host_rows, int64_t n, int32_t d, int32_t metric,
+                        int64_t granule_rows, const uint8_t *nonempty, int64_t row_offset,
+                        mqvs_segment_t *out);
+/* Same from a device buffer on the current device (copied). */
+int mqvs_segment_create_device(const float *dev_rows, int64_t n, int32_t d, int32_t metric,
+                               int64_t granule_rows, const uint8_t *dev_nonempty,
+                               int64_t row_offset, mqvs_segment_t *out);
+/* Synthetic segment generated in HBM by the counter-based generator
+ * (mode 0 exact ints in [-8,8], 1 ~N(0,1), 2 Gaussian mixture); row r of the
+ * segment is generator row row_offset + r. */
+int mqvs_segment_generate(uint64_t seed, int32_t mode, int64_t n, int32_t d, int32_t metric,
+                          int64_t granule_rows, int64_t row_offset, mqvs_segment_t *out);
+int mqvs_segment_free(mqvs_segment_t seg);
+int mqvs_segment_info(mqvs_segment_t seg, int64_t *n, int32_t *d, int32_t *metric,
+                      int64_t *granule_rows, int64_t *row_offset, size_t *hbm_bytes);
+/* Device pointer of the resident rows (normalised rows for cosine). */
+int mqvs_segment_rows(mqvs_segment_t seg, const float **dev_rows);
+
+/* ---- search --------------------------------------------------------------
+ * Brute-force top-k over the whole segment, with the reference operator's
+ * exact output: k (id, distance) per query, ascending for L2/Cosine,
+ * descending for IP, ties by row order; ids are row_offset + row; slots past
+ * the last result hold id -1 and distance FLT_MAX (L2, Cosine) or FLT_MIN (IP).
+ * queries: nq*d fp32 (original, un-normalised).
+ * filter: PREWHERE bitmap, LSB-first, n bits, or NULL (no PREWHERE).
+ * row_exists: lightweight-delete mask, LSB-first, n bits (1 = live), or NULL.
+ * out_ids: nq*k int64; out_dist: nq*k fp32 (caller-owned). */
+int mqvs_search(mqvs_segment_t seg, const float *queries, int32_t nq, int32_t k,
+                int32_t metric, const uint8_t *filter, const uint8_t *row_exists,
+                int64_t *out_ids, float *out_dist, uint32_t flags, mqvs_stream_t stream);
+
+/* tryBruteForceSearch contract (BruteForceSearch.h:62-111): x nx*d queries,
+ * y ny*d base (host pointers), one pass with no granule chunking, metric L2 or
+ * IP only (anything else -> MQVS_ERR_NOT_IMPLEMENTED); result_id / distance
+ * nx*k, faiss layout (-1 / FLT_MAX or -FLT_MAX padding). */
+int mqvs_knn_raw(const float *x, const float *y, int64_t d, int64_t k, int64_t nx, int64_t ny,
+                 int32_t metric, int64_t *result_id, float *distance);
+
+/* Exact re-rank of candidate ids (computeTopDistanceSubset contract): for
+ * each query, distances to its ncand candidates (segment-local row ids, -1 =
+ * none) with the brute-force formula for nq, then top-k as mqvs_search. */
+int mqvs_rerank(mqvs_segment_t seg, const float *queries, int32_t nq, const int64_t *cand,
+                int32_t ncand, int32_t k, int32_t metric, int64_t *out_ids, float *out_dist,
+                uint32_t flags, mqvs_stream_t stream);
+
+/* Merge per-shard top-k lists (row-range shards of one part, shard s holding
+ * lower ids than shard s+1): in_ids/in_dist [nshards][nq][k] as returned by
+ * mqvs_search on each shard; out nq*k.  Order: distance (desc for IP), then
+ * shard, then position in the shard's list -- the reference's insertion-order
+ * multimap merge. */
+int mqvs_merge_shards(int32_t nshards, int32_t nq, int32_t k, int32_t metric,
+                      const int64_t *in_ids, const float *in_dist, int64_t *out_ids,
+                      float *out_dist, uint32_t flags, mqvs_stream_t stream);
+
+/* Fill a device buffer with generator rows [row0, row0+n) (for queries). */
+int mqvs_generate_device(uint64_t seed, int32_t mode, int64_t row0, int64_t n, int32_t d,
+                         float *dev_out, mqvs_stream_t stream);
+
+/* ---- observability -------------------------------------------------------
+ * Stats of the calling thread's last mqvs_search: kernel time of the scan
+ * launches (ms, HIP events on the search stream), rows scanned, candidates
+ * kept, and which path ran (0 = VALU direct formula nq<20, 1 = MFMA). */
+typedef struct {
+    double scan_ms;     /* probe + main scan kernels */
+    double select_ms;   /* radix select + final select */
+    double total_ms;    /* first to last event of the search */
+    int64_t rows_scanned;
+    int64_t probe_rows;
+    int64_t max_candidates;
+    int32_t path;
+    int32_t rescans;    /* candidate-overflow re-scans */
+    int32_t scan_launches;
+    int32_t reserved;
+} mqvs_search_stats;
+int mqvs_last_search_stats(mqvs_search_stats *out);
+/* Enable per-search HIP-event timing (off by default: one extra event pair). */
+int mqvs_set_timing(int enabled);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* MQVS_H */

@@ -1,0 +1,115 @@
+"""ctypes binding of libmqvs.so (include/mqvs.h).
+
+The shared library is built in-tree (myscaledb_amd/libmqvs.so, see
+__graft_entry__.build / myscaledb_amd/csrc/Makefile).  There is no fallback:
+if the library is missing or fails to load, importing this module raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmqvs.so")
+
+# include/mqvs.h
+METRIC_L2, METRIC_IP, METRIC_COSINE = 0, 1, 2
+METRICS = {"L2": METRIC_L2, "IP": METRIC_IP, "COSINE": METRIC_COSINE, "Cosine": METRIC_COSINE,
+           "cosine": METRIC_COSINE, "l2": METRIC_L2, "ip": METRIC_IP}
+OK = 0
+ERR_NOT_IMPLEMENTED, ERR_LOGICAL, ERR_ILLEGAL_COLUMN, ERR_BAD_ARGUMENTS, ERR_MEMORY_LIMIT, \
+    ERR_DEVICE = 1, 2, 3, 4, 5, 6
+F_DEVICE_PTRS = 0x1
+F_ASYNC = 0x2
+
+# Exported C symbols: every one of these is declared in include/mqvs.h.
+SYMBOLS = [
+    "mqvs_abi_version", "mqvs_init", "mqvs_device_count", "mqvs_last_error",
+    "mqvs_thread_release", "mqvs_segment_create", "mqvs_segment_create_device",
+    "mqvs_segment_generate", "mqvs_segment_free", "mqvs_segment_info", "mqvs_segment_rows",
+    "mqvs_search", "mqvs_knn_raw", "mqvs_rerank", "mqvs_merge_shards", "mqvs_generate_device",
+    "mqvs_last_search_stats", "mqvs_set_timing",
+]
+
+
+class SearchStats(ctypes.Structure):
+    _fields_ = [("scan_ms", ctypes.c_double), ("select_ms", ctypes.c_double),
+                ("total_ms", ctypes.c_double), ("rows_scanned", ctypes.c_int64),
+                ("probe_rows", ctypes.c_int64), ("max_candidates", ctypes.c_int64),
+                ("path", ctypes.c_int32), ("rescans", ctypes.c_int32),
+                ("scan_launches", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+def _load():
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(
+            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            " (the HIP path has no CPU fallback)")
+    L = ctypes.CDLL(LIB_PATH)
+    P, I32, I64, U32, U64 = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
+                             ctypes.c_uint64)
+    sig = {
+        "mqvs_abi_version": ([], ctypes.c_int),
+        "mqvs_init": ([ctypes.c_int], ctypes.c_int),
+        "mqvs_device_count": ([P], ctypes.c_int),
+        "mqvs_last_error": ([], ctypes.c_char_p),
+        "mqvs_thread_release": ([], ctypes.c_int),
+        "mqvs_segment_create": ([P, I64, I32, I32, I64, P, I64, P], ctypes.c_int),
+        "mqvs_segment_create_device": ([P, I64, I32, I32, I64, P, I64, P], ctypes.c_int),
+        "mqvs_segment_generate": ([U64, I32, I64, I32, I32, I64, I64, P], ctypes.c_int),
+        "mqvs_segment_free": ([P], ctypes.c_int),
+        "mqvs_segment_info": ([P, P, P, P, P, P, P], ctypes.c_int),
+        "mqvs_segment_rows": ([P, P], ctypes.c_int),
+        "mqvs_search": ([P, P, I32, I32, I32, P, P, P, P, U32, P], ctypes.c_int),
+        "mqvs_knn_raw": ([P, P, I64, I64, I64, I64, I32, P, P], ctypes.c_int),
+        "mqvs_rerank": ([P, P, I32, P, I32, I32, I32, P, P, U32, P], ctypes.c_int),
+        "mqvs_merge_shards": ([I32, I32, I32, I32, P, P, P, P, U32, P], ctypes.c_int),
+        "mqvs_generate_device": ([U64, I32, I64, I64, I32, P, P], ctypes.c_int),
+        "mqvs_last_search_stats": ([P], ctypes.c_int),
+        "mqvs_set_timing": ([ctypes.c_int], ctypes.c_int),
+    }
+    for name, (args, res) in sig.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    return L
+
+
+lib = _load()
+
+
+# DB::ErrorCodes the reference throws for the same conditions
+CLICKHOUSE_CODE = {ERR_NOT_IMPLEMENTED: 48, ERR_LOGICAL: 49, ERR_ILLEGAL_COLUMN: 44,
+                   ERR_BAD_ARGUMENTS: 36, ERR_MEMORY_LIMIT: 241, ERR_DEVICE: 1001}
+CODE_NAME = {ERR_NOT_IMPLEMENTED: "NOT_IMPLEMENTED", ERR_LOGICAL: "LOGICAL_ERROR",
+             ERR_ILLEGAL_COLUMN: "ILLEGAL_COLUMN", ERR_BAD_ARGUMENTS: "BAD_ARGUMENTS",
+             ERR_MEMORY_LIMIT: "MEMORY_LIMIT_EXCEEDED", ERR_DEVICE: "DEVICE_ERROR"}
+
+
+class MqvsError(RuntimeError):
+    """Mirror of DB::Exception(code, message) raised by the reference path."""
+
+    def __init__(self, status, message):
+        self.status = status
+        self.code = CLICKHOUSE_CODE.get(status, 1001)
+        self.name = CODE_NAME.get(status, "UNKNOWN")
+        super().__init__(f"{self.name} ({self.code}): {message}")
+
+
+class NotImplementedMetric(MqvsError):
+    pass
+
+
+def check(rc):
+    if rc != OK:
+        msg = lib.mqvs_last_error()
+        msg = msg.decode() if msg else ""
+        cls = NotImplementedMetric if rc == ERR_NOT_IMPLEMENTED else MqvsError
+        raise cls(rc, msg)
+    return rc
+
+
+def last_search_stats():
+    st = SearchStats()
+    check(lib.mqvs_last_search_stats(ctypes.byref(st)))
+    return {f: getattr(st, f) for f, _ in SearchStats._fields_}

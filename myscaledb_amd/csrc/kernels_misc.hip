@@ -1,0 +1,289 @@
+// kernels_misc.hip -- segment preparation, query preparation and helpers.
+#include "mqvs_internal.h"
+
+namespace mqvs {
+
+constexpr int NB_K = 32;
+constexpr int NB_LD = NB_K + 4;
+
+// Per-row squared norm, sequential fp32 with the product rounded then added
+// (VectorDataset.h:105-108 for normalize; fvec_norm_L2sqr for the BLAS branch
+// norms, the same order the KATs pin for fvec_*).  Rows staged through LDS so
+// the HBM reads stay coalesced while each lane walks its own row in order.
+__device__ void block_row_sumsq(const float *rows, int64_t r0, int64_t r1, int d,
+                                float (*tile)[256 * NB_LD], float &sum) {
+    const int t = threadIdx.x;
+    sum = 0.0f;
+    const int nst = (d + NB_K - 1) / NB_K;
+    for (int s = 0; s < nst; ++s) {
+        const int k0 = s * NB_K;
+        for (int i = 0; i < 8; ++i) {
+            const int f = t + 256 * i;
+            const int lr = f >> 3, c = (f & 7) * 4;
+            const int64_t gr = r0 + lr;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (gr < r1) {
+                const float *src = rows + gr * d + k0 + c;
+                if (k0 + c + 0 < d) v.x = src[0];
+                if (k0 + c + 1 < d) v.y = src[1];
+                if (k0 + c + 2 < d) v.z = src[2];
+                if (k0 + c + 3 < d) v.w = src[3];
+            }
+            *reinterpret_cast<float4 *>(&tile[0][lr * NB_LD + c]) = v;
+        }
+        __syncthreads();
+        const float *tl = &tile[0][t * NB_LD];
+        const int lim = (d - k0) < NB_K ? (d - k0) : NB_K;
+        for (int kk = 0; kk < lim; ++kk) sum = sum + tl[kk] * tl[kk];
+        __syncthreads();
+    }
+}
+
+__global__ __launch_bounds__(256) void k_row_norms(const float *rows, int64_t n, int d,
+                                                    float *norms) {
+    __shared__ __attribute__((aligned(16))) float tile[1][256 * NB_LD];
+    for (int64_t r0 = (int64_t)blockIdx.x * 256; r0 < n; r0 += (int64_t)gridDim.x * 256) {
+        const int64_t r1 = r0 + 256 < n ? r0 + 256 : n;
+        float sum;
+        block_row_sumsq(rows, r0, r1, d, tile, sum);
+        if (r0 + threadIdx.x < r1) norms[r0 + threadIdx.x] = sum;
+    }
+}
+
+// VectorDataset<Float>::normalize (VectorDataset.h:98-117), in place.
+__global__ __launch_bounds__(256) void k_normalize_rows(float *rows, int64_t n, int d) {
+    __shared__ __attribute__((aligned(16))) float tile[1][256 * NB_LD];
+    __shared__ float scale[256];
+    const float eps = 1.1920929e-07f;  // FLT_EPSILON
+    for (int64_t r0 = (int64_t)blockIdx.x * 256; r0 < n; r0 += (int64_t)gridDim.x * 256) {
+        const int64_t r1 = r0 + 256 < n ? r0 + 256 : n;
+        float sum;
+        block_row_sumsq(rows, r0, r1, d, tile, sum);
+        // 0 marks "skip" (sum < FLT_EPSILON): the row is left untouched
+        scale[threadIdx.x] = (sum < eps) ? 0.0f : sqrtf(sum);
+        __syncthreads();
+        const int64_t cnt = (r1 - r0) * d;
+        float *base = rows + r0 * d;
+        for (int64_t i = threadIdx.x; i < cnt; i += 256) {
+            const float s = scale[i / d];
+            if (s != 0.0f) base[i] = base[i] / s;
+        }
+        __syncthreads();
+    }
+}
+
+void launch_row_norms(const float *rows, int64_t n, int d, float *norms, hipStream_t s) {
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks < 1) return;
+    hipLaunchKernelGGL(k_row_norms, dim3((unsigned)blocks), dim3(256), 0, s, rows, n, d, norms);
+}
+
+void launch_normalize_rows(float *rows, int64_t n, int d, hipStream_t s) {
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 8192) blocks = 8192;
+    if (blocks < 1) return;
+    hipLaunchKernelGGL(k_normalize_rows, dim3((unsigned)blocks), dim3(256), 0, s, rows, n, d);
+}
+
+// Query preparation, one lane per query.  L2/IP: variant 0 = the query,
+// qnorm = |q|^2 (BLAS branch).  Cosine: the reference normalises the SAME
+// query object once per searched granule chunk (VIWithDataPart.h:358 on the
+// dataset shared across chunks, MergeTreeVSManager.cpp:1279-1292,1473-1486),
+// so chunk ordinal c uses normalize^(c+1)(q).  Variants are generated until a
+// repeat: variants [0, mu) are the transient, [mu, mu+lam) the cycle.
+__global__ void k_query_prep(const float *q, int nq, int d, int metric, int blas, float *qvars,
+                             int maxv, float *qnorms, int *qmu, int *qlam, int *status) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= nq) return;
+    const int64_t qs = (int64_t)((d + 31) / 32 * 32);
+    const float *src = q + (int64_t)j * d;
+    float *v0 = qvars + (int64_t)j * maxv * qs;
+    if (metric != MQVS_METRIC_COSINE) {
+        float sum = 0.0f;
+        for (int i = 0; i < d; ++i) {
+            v0[i] = src[i];
+            sum = sum + src[i] * src[i];
+        }
+        if (qnorms) qnorms[j] = blas ? sum : 0.0f;
+        qmu[j] = 0;
+        qlam[j] = 1;
+        return;
+    }
+    const float eps = 1.1920929e-07f;
+    const float *prev = src;
+    for (int v = 0; v < maxv; ++v) {
+        float *cur = v0 + (int64_t)v * qs;
+        float sum = 0.0f;
+        for (int i = 0; i < d; ++i) sum = sum + prev[i] * prev[i];
+        if (sum < eps) {
+            for (int i = 0; i < d; ++i) cur[i] = prev[i];
+        } else {
+            const float s = sqrtf(sum);
+            for (int i = 0; i < d; ++i) cur[i] = prev[i] / s;
+        }
+        for (int u = 0; u < v; ++u) {
+            const float *o = v0 + (int64_t)u * qs;
+            bool eq = true;
+            for (int i = 0; i < d && eq; ++i)
+                eq = __builtin_bit_cast(uint32_t, o[i]) == __builtin_bit_cast(uint32_t, cur[i]);
+            if (eq) {
+                qmu[j] = u;
+                qlam[j] = v - u;
+                if (qnorms) qnorms[j] = 0.0f;
+                return;
+            }
+        }
+        prev = cur;
+    }
+    atomicOr(status, 1);  // no repeat within maxv normalisations
+    qmu[j] = 0;
+    qlam[j] = 1;
+}
+
+void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, float *qvars,
+                       float *qnorms, int *qmu, int *qlam, int *status, hipStream_t s) {
+    const int maxv = metric == MQVS_METRIC_COSINE ? kMaxVariants : 1;
+    hipLaunchKernelGGL(k_query_prep, dim3((nq + 63) / 64), dim3(64), 0, s, q, nq, d, metric,
+                       blas ? 1 : 0, qvars, maxv, qnorms, qmu, qlam, status);
+}
+
+// Counter-based synthetic generator; bit-identical to oracle/mqvs_oracle.c
+// orc_generate (integer hash, exact 16-bit fractions, one rounding).
+__device__ __host__ inline uint64_t splitmix64(uint64_t z) {
+    z += 0x9e3779b97f4a7c15ULL;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ULL;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebULL;
+    return z ^ (z >> 31);
+}
+
+__device__ inline float gen_gauss(uint64_t seed, uint64_t idx) {
+    const uint64_t h = splitmix64(seed ^ idx);
+    const float u0 = (float)(h & 0xffff) * (1.0f / 65536.0f);
+    const float u1 = (float)((h >> 16) & 0xffff) * (1.0f / 65536.0f);
+    const float u2 = (float)((h >> 32) & 0xffff) * (1.0f / 65536.0f);
+    const float u3 = (float)((h >> 48) & 0xffff) * (1.0f / 65536.0f);
+    const float s = (u0 + u1) + (u2 + u3);
+    return (s - 2.0f) * 1.7320508f;
+}
+
+__global__ void k_generate(uint64_t seed, int mode, int64_t row0, int64_t n, int d, float *out) {
+    const int64_t total = n * d;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = e / d;
+        const int j = (int)(e - r * d);
+        const uint64_t row = (uint64_t)(row0 + r);
+        const uint64_t idx = row * (uint64_t)d + (uint64_t)j;
+        float v;
+        if (mode == 0) {
+            v = (float)((int)(splitmix64(seed ^ idx) % 17ULL) - 8);
+        } else if (mode == 1) {
+            v = gen_gauss(seed, idx);
+        } else {
+            const uint64_t c =
+                splitmix64(seed ^ 0xC0FFEEULL ^ (row * 0x100000001B3ULL)) % 4096ULL;
+            const float center = gen_gauss(seed ^ 0xCE17E5ULL, c * (uint64_t)d + (uint64_t)j);
+            v = center + 0.25f * gen_gauss(seed, idx);
+        }
+        out[e] = v;
+    }
+}
+
+void launch_generate(uint64_t seed, int mode, int64_t row0, int64_t n, int d, float *out,
+                     hipStream_t s) {
+    const int64_t total = n * d;
+    int64_t blocks = (total + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    if (blocks < 1) return;
+    hipLaunchKernelGGL(k_generate, dim3((unsigned)blocks), dim3(256), 0, s, seed, mode, row0, n, d,
+                       out);
+}
+
+// bytes (1 = nonempty) -> LSB-first bitmap
+__global__ void k_pack(const uint8_t *bytes, int64_t n, uint8_t *bits) {
+    const int64_t nb = (n + 7) / 8;
+    for (int64_t b = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; b < nb;
+         b += (int64_t)gridDim.x * blockDim.x) {
+        uint8_t v = 0;
+        for (int i = 0; i < 8; ++i) {
+            const int64_t r = b * 8 + i;
+            if (r < n && bytes[r]) v |= (uint8_t)(1u << i);
+        }
+        bits[b] = v;
+    }
+}
+
+void launch_pack_nonempty(const uint8_t *bytes, int64_t n, uint8_t *bits, hipStream_t s) {
+    int64_t blocks = ((n + 7) / 8 + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    if (blocks < 1) return;
+    hipLaunchKernelGGL(k_pack, dim3((unsigned)blocks), dim3(256), 0, s, bytes, n, bits);
+}
+
+// Chunk ordinals: which granule chunks the reference actually hands to
+// searchWrapper, and how many such calls came before each.
+//  no-filter mode (require_filter = 0): a chunk is searched iff one of its
+//    arrays is non-empty (MergeTreeVSManager.cpp:1364-1368 skips src_vec.empty());
+//  filter mode: a mark is searched iff it keeps >= 1 selected non-empty live
+//    row (:1179-1183).
+__global__ __launch_bounds__(256) void k_chunk_active(const uint8_t *filter,
+                                                       const uint8_t *nonempty,
+                                                       const uint8_t *exists, int64_t n,
+                                                       int64_t chunk_rows, int require_filter,
+                                                       int *flag) {
+    __shared__ int any;
+    const int64_t c = blockIdx.x;
+    if (threadIdx.x == 0) any = 0;
+    __syncthreads();
+    const int64_t r0 = c * chunk_rows;
+    const int64_t r1 = r0 + chunk_rows < n ? r0 + chunk_rows : n;
+    int mine = 0;
+    for (int64_t r = r0 + threadIdx.x; r < r1 && !mine; r += 256) {
+        bool ok = nonempty ? bit_test(nonempty, r) : true;
+        if (require_filter) {
+            ok = ok && bit_test(filter, r);
+            if (exists) ok = ok && bit_test(exists, r);
+        }
+        mine = ok ? 1 : 0;
+    }
+    if (mine) atomicOr(&any, 1);
+    __syncthreads();
+    if (threadIdx.x == 0) flag[c] = any;
+}
+
+__global__ __launch_bounds__(256) void k_exclusive_ord(int *flag_ord, int64_t nchunks) {
+    __shared__ int sums[256];
+    __shared__ int carry;
+    if (threadIdx.x == 0) carry = 0;
+    __syncthreads();
+    for (int64_t base = 0; base < nchunks; base += 256) {
+        const int64_t c = base + threadIdx.x;
+        const int f = c < nchunks ? flag_ord[c] : 0;
+        sums[threadIdx.x] = f;
+        __syncthreads();
+        for (int off = 1; off < 256; off <<= 1) {
+            int v = threadIdx.x >= off ? sums[threadIdx.x - off] : 0;
+            __syncthreads();
+            sums[threadIdx.x] += v;
+            __syncthreads();
+        }
+        const int incl = sums[threadIdx.x];
+        if (c < nchunks) flag_ord[c] = f ? carry + incl - 1 : -1;
+        __syncthreads();
+        if (threadIdx.x == 255) carry += incl;
+        __syncthreads();
+    }
+}
+
+void launch_chunk_ordinals(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists,
+                           int64_t n, int64_t chunk_rows, int require_filter, int *ord,
+                           hipStream_t s) {
+    const int64_t nchunks = (n + chunk_rows - 1) / chunk_rows;
+    if (nchunks < 1) return;
+    hipLaunchKernelGGL(k_chunk_active, dim3((unsigned)nchunks), dim3(256), 0, s, filter, nonempty,
+                       exists, n, chunk_rows, require_filter, ord);
+    hipLaunchKernelGGL(k_exclusive_ord, dim3(1), dim3(256), 0, s, ord, nchunks);
+}
+
+}  // namespace mqvs

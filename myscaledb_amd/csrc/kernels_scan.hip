@@ -1,0 +1,371 @@
+// kernels_scan.hip -- brute-force distance scan kernels for gfx950.
+//
+// Two kernels replace faiss knn_L2sqr / knn_inner_product as called from
+// VectorIndex::tryBruteForceSearch (BruteForceSearch.h:62-111):
+//
+//  * k_scan_small  (nq < 20, faiss exhaustive_*_seq): HBM-bound streaming scan.
+//    A 256-thread workgroup owns 256 rows; row tiles of 32 floats are staged
+//    through LDS with coalesced 16-B loads (double-buffered), then every lane
+//    walks ITS row sequentially -- (x-y)^2 or x*y rounded then added, exactly
+//    the fvec_* order the reference's KATs pin -- against up to 20 queries
+//    whose values are wave-uniform (scalar loads).
+//
+//  * k_scan_mfma   (nq >= 20, faiss exhaustive_*_blas): MFMA-bound batch
+//    contraction on v_mfma_f32_32x32x2_f32.  A 128x128 (rows x queries) tile
+//    per workgroup, 4 waves of 64x64, K staged 32 deep through padded LDS.
+//    The f32 MFMA is a k-ordered fma chain, i.e. the sgemm element the oracle
+//    assumes; L2 uses (|x|^2 + |y|^2) - 2<x,y> clamped at 0.
+//
+// Neither kernel materialises the nq x n distance matrix.  A scan runs in
+// one of two epilogue modes:
+//    PROBE  -- write raw values for a short prefix of rows (the probe), from
+//              which the k-th key per query gives an upper-bound threshold;
+//    APPEND -- append only (raw, row) with key <= threshold to a per-query
+//              candidate list (a few thousand entries).
+// Validity (PREWHERE bitmap, lightweight-delete mask, empty arrays, metric
+// quirks) is applied in the epilogue; see mqvs_internal.h key32().
+#include "mqvs_internal.h"
+
+namespace mqvs {
+
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+static __device__ inline float nan_f() { return __builtin_nanf(""); }
+
+template <int METRIC, bool PROBE>
+__device__ inline void emit(const ScanParams &p, int j, int64_t row, bool valid, float raw) {
+    if (PROBE) {
+        p.probe[(int64_t)j * p.probe_ld + (row - p.row_begin)] = valid ? raw : nan_f();
+    } else if (valid) {
+        const uint32_t key = key32<METRIC>(raw);
+        if (key != 0xFFFFFFFFu && key <= p.tau[j]) {
+            const int pos = atomicAdd(&p.cand_count[j], 1);
+            if (pos < p.cand_cap) {
+                Cand c;
+                c.raw = raw;
+                c.row = (uint32_t)row;
+                p.cand[(int64_t)j * p.cand_cap + pos] = c;
+            }
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// VALU scan, nq < 20.
+constexpr int SB_K = 32;            // floats per stage
+constexpr int SB_LD = SB_K + 4;     // padded LDS row (16-B aligned, conflict-free b128)
+
+template <int NQ, int METRIC, bool PROBE, bool VEC4>
+__global__ __launch_bounds__(256) void k_scan_small(ScanParams p) {
+    __shared__ __attribute__((aligned(16))) float tile[2][kSmallRows * SB_LD];
+    __shared__ __attribute__((aligned(16))) float qtile[2][NQ * SB_K];
+    const int t = threadIdx.x;
+    const int d = p.d;
+    const int nst = (d + SB_K - 1) / SB_K;
+    const int64_t qstride = (int64_t)((d + 31) / 32 * 32);
+    // threads t < NQ*8 stage one float4 of the query slice per stage
+    const int qj = t >> 3, qc = (t & 7) * 4;
+    const bool qload = qj < NQ && qj < p.nq;
+    for (int64_t ti = blockIdx.x; ti < p.tiles; ti += gridDim.x) {
+        int64_t r0, r1, chunk;
+        tile_range(p, ti, r0, r1, chunk);
+        const int ord = p.chunk_ord ? p.chunk_ord[chunk] : (int)chunk;
+        const int64_t row = r0 + t;
+        const bool have = row < r1;
+        if (ord < 0) {  // chunk never searched by the reference (all arrays empty)
+            if (PROBE && have)
+                for (int j = 0; j < p.nq; ++j) emit<METRIC, true>(p, j, row, false, 0.f);
+            continue;
+        }
+        const float *qsrc = qload
+            ? p.qvars + ((int64_t)qj * p.maxv + variant_of(p, qj, ord)) * qstride + qc
+            : nullptr;
+        float acc[NQ];
+#pragma unroll
+        for (int j = 0; j < NQ; ++j) acc[j] = 0.0f;
+
+        float4 reg[8], qreg = make_float4(0.f, 0.f, 0.f, 0.f);
+        auto load = [&](int s) {
+            const int k0 = s * SB_K;
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int f = t + 256 * i;
+                const int lr = f >> 3, c = (f & 7) * 4;
+                const int64_t gr = r0 + lr;
+                float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+                if (gr < r1) {
+                    const float *src = p.rows + gr * d + k0 + c;
+                    if (VEC4) {
+                        if (k0 + c < d) v = *reinterpret_cast<const float4 *>(src);
+                    } else {
+                        if (k0 + c + 0 < d) v.x = src[0];
+                        if (k0 + c + 1 < d) v.y = src[1];
+                        if (k0 + c + 2 < d) v.z = src[2];
+                        if (k0 + c + 3 < d) v.w = src[3];
+                    }
+                }
+                reg[i] = v;
+            }
+            if (qload) qreg = *reinterpret_cast<const float4 *>(qsrc + k0);
+        };
+        auto store = [&](int b) {
+#pragma unroll
+            for (int i = 0; i < 8; ++i) {
+                const int f = t + 256 * i;
+                const int lr = f >> 3, c = (f & 7) * 4;
+                *reinterpret_cast<float4 *>(&tile[b][lr * SB_LD + c]) = reg[i];
+            }
+            if (t < NQ * 8) *reinterpret_cast<float4 *>(&qtile[b][qj * SB_K + qc]) = qreg;
+        };
+        load(0);
+        store(0);
+        __syncthreads();
+        for (int s = 0; s < nst; ++s) {
+            if (s + 1 < nst) load(s + 1);
+            const float *tl = &tile[s & 1][t * SB_LD];
+            const float *ql = qtile[s & 1];
+#pragma unroll 2
+            for (int kk = 0; kk < SB_K; kk += 4) {
+                const float4 v = *reinterpret_cast<const float4 *>(tl + kk);
+#pragma unroll
+                for (int j = 0; j < NQ; ++j) {
+                    // same address in every lane: LDS broadcast
+                    const float4 q = *reinterpret_cast<const float4 *>(ql + j * SB_K + kk);
+                    if (METRIC == MQVS_METRIC_L2) {
+                        float e;
+                        e = v.x - q.x; acc[j] = acc[j] + e * e;
+                        e = v.y - q.y; acc[j] = acc[j] + e * e;
+                        e = v.z - q.z; acc[j] = acc[j] + e * e;
+                        e = v.w - q.w; acc[j] = acc[j] + e * e;
+                    } else {
+                        acc[j] = acc[j] + v.x * q.x;
+                        acc[j] = acc[j] + v.y * q.y;
+                        acc[j] = acc[j] + v.z * q.z;
+                        acc[j] = acc[j] + v.w * q.w;
+                    }
+                }
+            }
+            if (s + 1 < nst) store((s + 1) & 1);
+            __syncthreads();
+        }
+        if (have) {
+            const bool valid = row_valid(p, row);
+#pragma unroll
+            for (int j = 0; j < NQ; ++j)
+                if (j < p.nq) emit<METRIC, PROBE>(p, j, row, valid, acc[j]);
+        }
+    }
+}
+
+template <int NQ, int METRIC, bool PROBE>
+static void launch_small_t(const ScanParams &p, hipStream_t s) {
+    int64_t grid = p.tiles < 4096 ? p.tiles : 4096;
+    if (grid < 1) return;
+    if (p.d % 4 == 0)
+        hipLaunchKernelGGL((k_scan_small<NQ, METRIC, PROBE, true>), dim3((unsigned)grid), dim3(256),
+                           0, s, p);
+    else
+        hipLaunchKernelGGL((k_scan_small<NQ, METRIC, PROBE, false>), dim3((unsigned)grid), dim3(256),
+                           0, s, p);
+}
+
+template <int METRIC, bool PROBE>
+static void launch_small_m(const ScanParams &p, hipStream_t s) {
+    const int nq = p.nq;
+    if (nq <= 1) launch_small_t<1, METRIC, PROBE>(p, s);
+    else if (nq <= 2) launch_small_t<2, METRIC, PROBE>(p, s);
+    else if (nq <= 4) launch_small_t<4, METRIC, PROBE>(p, s);
+    else if (nq <= 8) launch_small_t<8, METRIC, PROBE>(p, s);
+    else if (nq <= 12) launch_small_t<12, METRIC, PROBE>(p, s);
+    else if (nq <= 16) launch_small_t<16, METRIC, PROBE>(p, s);
+    else launch_small_t<20, METRIC, PROBE>(p, s);
+}
+
+void launch_scan_small(const ScanParams &p, int metric, bool probe, hipStream_t s) {
+    switch (metric) {
+        case MQVS_METRIC_L2:
+            probe ? launch_small_m<MQVS_METRIC_L2, true>(p, s) : launch_small_m<MQVS_METRIC_L2, false>(p, s);
+            break;
+        case MQVS_METRIC_IP:
+            probe ? launch_small_m<MQVS_METRIC_IP, true>(p, s) : launch_small_m<MQVS_METRIC_IP, false>(p, s);
+            break;
+        case MQVS_METRIC_COSINE:
+            probe ? launch_small_m<MQVS_METRIC_COSINE, true>(p, s)
+                  : launch_small_m<MQVS_METRIC_COSINE, false>(p, s);
+            break;
+        default:
+            probe ? launch_small_m<kMetricIpRaw, true>(p, s) : launch_small_m<kMetricIpRaw, false>(p, s);
+            break;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// MFMA scan, nq >= 20.
+constexpr int MB_K = 32;          // K per stage
+constexpr int MB_LD = MB_K + 1;   // odd LDS row stride: conflict-free ds_read_b32 columns
+
+template <int METRIC, bool PROBE, bool VEC4>
+__global__ __launch_bounds__(256, 2) void k_scan_mfma(ScanParams p) {
+    __shared__ float Ys[2][kMfmaRows * MB_LD];
+    __shared__ float Qs[2][kMfmaQ * MB_LD];
+    // XCD-aware block -> (row tile, query block): the query blocks of one row
+    // tile are consecutive logical blocks and land on one XCD (same L2).
+    const int64_t L = p.tiles * p.num_qblocks;
+    const int64_t cpx = (L + 7) / 8;
+    const int64_t b = blockIdx.x;
+    const int64_t l = (b % 8) * cpx + b / 8;
+    if (l >= L) return;
+    const int64_t ti = l / p.num_qblocks;
+    const int qb = (int)(l % p.num_qblocks);
+
+    int64_t r0, r1, chunk;
+    tile_range(p, ti, r0, r1, chunk);
+    const int ord = p.chunk_ord ? p.chunk_ord[chunk] : (int)chunk;
+    const int t = threadIdx.x;
+    const int lane = t & 63, w = t >> 6;
+    const int wr = w >> 1, wq = w & 1;
+    const int h = lane >> 5, l32 = lane & 31;
+    const int q0 = qb * kMfmaQ;
+    const int d = p.d;
+    const int64_t qstride = (int64_t)((d + 31) / 32 * 32);
+
+    if (ord < 0) {
+        if (PROBE) {
+            for (int i = t; i < kMfmaRows * kMfmaQ; i += 256) {
+                const int64_t row = r0 + (i % kMfmaRows);
+                const int j = q0 + i / kMfmaRows;
+                if (row < r1 && j < p.nq) emit<METRIC, true>(p, j, row, false, 0.f);
+            }
+        }
+        return;
+    }
+
+    // per-thread global load slots: 4 float4 of Y and 4 of Q per stage
+    const float *qsrc[4];
+    bool qok[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int f = t + 256 * i;
+        const int lq = f >> 3;
+        const int j = q0 + lq;
+        qok[i] = j < p.nq;
+        const int jj = qok[i] ? j : 0;
+        qsrc[i] = p.qvars + ((int64_t)jj * p.maxv + variant_of(p, jj, ord)) * qstride + (f & 7) * 4;
+    }
+    float4 ry[4], rq[4];
+    auto load = [&](int s) {
+        const int k0 = s * MB_K;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int f = t + 256 * i;
+            const int lr = f >> 3, c = (f & 7) * 4;
+            const int64_t gr = r0 + lr;
+            float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
+            if (gr < r1) {
+                const float *src = p.rows + gr * d + k0 + c;
+                if (VEC4) {
+                    if (k0 + c < d) v = *reinterpret_cast<const float4 *>(src);
+                } else {
+                    if (k0 + c + 0 < d) v.x = src[0];
+                    if (k0 + c + 1 < d) v.y = src[1];
+                    if (k0 + c + 2 < d) v.z = src[2];
+                    if (k0 + c + 3 < d) v.w = src[3];
+                }
+            }
+            ry[i] = v;
+            rq[i] = qok[i] ? *reinterpret_cast<const float4 *>(qsrc[i] + k0)
+                           : make_float4(0.f, 0.f, 0.f, 0.f);
+        }
+    };
+    auto store = [&](int bf) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int f = t + 256 * i;
+            const int lr = f >> 3, c = (f & 7) * 4;
+            float *ys = &Ys[bf][lr * MB_LD + c];
+            ys[0] = ry[i].x; ys[1] = ry[i].y; ys[2] = ry[i].z; ys[3] = ry[i].w;
+            float *qs = &Qs[bf][lr * MB_LD + c];
+            qs[0] = rq[i].x; qs[1] = rq[i].y; qs[2] = rq[i].z; qs[3] = rq[i].w;
+        }
+    };
+
+    f32x16 acc00 = {0}, acc01 = {0}, acc10 = {0}, acc11 = {0};
+    const int nst = (d + MB_K - 1) / MB_K;
+    load(0);
+    store(0);
+    __syncthreads();
+    const int ya = (wr * 64 + l32) * MB_LD + h;
+    const int qa = (wq * 64 + l32) * MB_LD + h;
+    for (int s = 0; s < nst; ++s) {
+        if (s + 1 < nst) load(s + 1);
+        const float *ys = Ys[s & 1];
+        const float *qs = Qs[s & 1];
+#pragma unroll
+        for (int ks = 0; ks < MB_K / 2; ++ks) {
+            const float a0 = ys[ya + 2 * ks];
+            const float a1 = ys[ya + 32 * MB_LD + 2 * ks];
+            const float b0 = qs[qa + 2 * ks];
+            const float b1 = qs[qa + 32 * MB_LD + 2 * ks];
+            acc00 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b0, acc00, 0, 0, 0);
+            acc01 = __builtin_amdgcn_mfma_f32_32x32x2f32(a0, b1, acc01, 0, 0, 0);
+            acc10 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b0, acc10, 0, 0, 0);
+            acc11 = __builtin_amdgcn_mfma_f32_32x32x2f32(a1, b1, acc11, 0, 0, 0);
+        }
+        if (s + 1 < nst) store((s + 1) & 1);
+        __syncthreads();
+    }
+
+    // epilogue: lane holds query column l32 of each 32x32 block, 16 rows
+    auto epi = [&](const f32x16 &acc, int rb, int qb2) {
+        const int j = q0 + wq * 64 + qb2 * 32 + l32;
+        if (j >= p.nq) return;
+        const float qn = (METRIC == MQVS_METRIC_L2) ? p.qnorms[j] : 0.f;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) {
+            const int il = wr * 64 + rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
+            const int64_t row = r0 + il;
+            if (row >= r1) continue;
+            float raw = acc[r];
+            if (METRIC == MQVS_METRIC_L2) {
+                raw = (qn + p.row_norms[row]) - 2.0f * acc[r];
+                if (raw < 0) raw = 0;
+            }
+            emit<METRIC, PROBE>(p, j, row, row_valid(p, row), raw);
+        }
+    };
+    epi(acc00, 0, 0);
+    epi(acc01, 0, 1);
+    epi(acc10, 1, 0);
+    epi(acc11, 1, 1);
+}
+
+template <int METRIC, bool PROBE>
+static void launch_mfma_t(const ScanParams &p, hipStream_t s) {
+    const int64_t L = p.tiles * p.num_qblocks;
+    const int64_t grid = (L + 7) / 8 * 8;
+    if (L < 1) return;
+    if (p.d % 4 == 0)
+        hipLaunchKernelGGL((k_scan_mfma<METRIC, PROBE, true>), dim3((unsigned)grid), dim3(256), 0, s, p);
+    else
+        hipLaunchKernelGGL((k_scan_mfma<METRIC, PROBE, false>), dim3((unsigned)grid), dim3(256), 0, s, p);
+}
+
+void launch_scan_mfma(const ScanParams &p, int metric, bool probe, hipStream_t s) {
+    switch (metric) {
+        case MQVS_METRIC_L2:
+            probe ? launch_mfma_t<MQVS_METRIC_L2, true>(p, s) : launch_mfma_t<MQVS_METRIC_L2, false>(p, s);
+            break;
+        case MQVS_METRIC_IP:
+            probe ? launch_mfma_t<MQVS_METRIC_IP, true>(p, s) : launch_mfma_t<MQVS_METRIC_IP, false>(p, s);
+            break;
+        case MQVS_METRIC_COSINE:
+            probe ? launch_mfma_t<MQVS_METRIC_COSINE, true>(p, s)
+                  : launch_mfma_t<MQVS_METRIC_COSINE, false>(p, s);
+            break;
+        default:
+            probe ? launch_mfma_t<kMetricIpRaw, true>(p, s) : launch_mfma_t<kMetricIpRaw, false>(p, s);
+            break;
+    }
+}
+
+}  // namespace mqvs

@@ -1,0 +1,682 @@
+// mqvs.hip -- C-ABI of libmqvs.so: segments, workspaces, search orchestration.
+//
+// Search = the whole of MergeTreeVSManager::vectorScanWithoutIndex for one data
+// part (MergeTreeVSManager.cpp:960-1536) in a handful of launches:
+//   1. query prep        (norms; cosine re-normalisation variants)
+//   2. probe scan        dense values for rows [0, P) (P ~ 3k*n/4096)
+//   3. probe select      per-query k-th key -> threshold tau; first candidates
+//   4. main scan         rows [P, n), append rows with key <= tau
+//   5. final select      sort candidates by the reference's total order, emit k
+// If a candidate list overflows (adversarial ties), tau is tightened from the
+// stored candidates and the part is re-scanned (rare; counted in the stats).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstring>
+#include <map>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "mqvs_internal.h"
+
+struct mqvs_segment {
+    int device = 0;
+    int64_t n = 0;
+    int d = 0;
+    int metric = 0;
+    int64_t granule = 0;
+    int64_t row_offset = 0;
+    float *rows = nullptr;
+    float *norms = nullptr;          // |y|^2 (L2/IP segments)
+    uint8_t *nonempty_bits = nullptr;// null when every array is non-empty
+    int *chunk_ord = nullptr;        // no-filter chunk ordinals (null = identity)
+    size_t bytes = 0;
+};
+
+namespace mqvs {
+
+static thread_local std::string g_error;
+static thread_local mqvs_search_stats g_stats{};
+static int g_timing = 0;
+
+void set_error(const std::string &msg) { g_error = msg; }
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    void *get(size_t bytes) {
+        if (bytes == 0) bytes = 16;
+        if (bytes > cap) {
+            if (p) (void)hipFree(p);
+            p = nullptr;
+            cap = 0;
+            MQVS_HIP(hipMalloc(&p, bytes));
+            cap = bytes;
+        }
+        return p;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct Workspace {
+    hipStream_t stream = nullptr;
+    hipEvent_t ev[6] = {};
+    DevBuf queries, qvars, qnorms, qmu, qlam, status, filter, exists, ord, probe, tau, count, cand,
+        overflow, out_ids, out_dist, misc;
+    int *host_flags = nullptr;  // pinned
+    void init() {
+        if (stream) return;
+        MQVS_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
+        for (auto &e : ev) MQVS_HIP(hipEventCreate(&e));
+        MQVS_HIP(hipHostMalloc((void **)&host_flags, 64 * sizeof(int), hipHostMallocDefault));
+    }
+    void release() {
+        DevBuf *all[] = {&queries, &qvars, &qnorms, &qmu,  &qlam,   &status,  &filter,   &exists, &ord,
+                         &probe,   &tau,   &count,  &cand, &overflow, &out_ids, &out_dist, &misc};
+        for (auto *b : all) b->release();
+        if (host_flags) (void)hipHostFree(host_flags);
+        host_flags = nullptr;
+        for (auto &e : ev)
+            if (e) (void)hipEventDestroy(e);
+        if (stream) (void)hipStreamDestroy(stream);
+        stream = nullptr;
+    }
+};
+
+static thread_local std::map<int, Workspace> *g_ws = nullptr;
+
+static Workspace &workspace(int device) {
+    if (!g_ws) g_ws = new std::map<int, Workspace>();  // leaked at exit on purpose
+    Workspace &w = (*g_ws)[device];
+    w.init();
+    return w;
+}
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        MQVS_HIP(hipGetDevice(&prev));
+        if (prev != dev) MQVS_HIP(hipSetDevice(dev));
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (hipGetDevice(&cur) == hipSuccess && prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+template <typename F>
+static int guarded(F &&f) {
+    try {
+        f();
+        return MQVS_OK;
+    } catch (const Error &e) {
+        set_error(e.msg);
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        set_error("host allocation failed");
+        return MQVS_ERR_MEMORY_LIMIT;
+    } catch (...) {
+        set_error("unknown error");
+        return MQVS_ERR_DEVICE;
+    }
+}
+
+[[noreturn]] static void fail(int code, const std::string &msg) { throw Error{code, msg}; }
+
+static bool is_device_ptr(const void *p) {
+    hipPointerAttribute_t a;
+    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
+        (void)hipGetLastError();
+        return false;
+    }
+    return a.type == hipMemoryTypeDevice;
+}
+
+// ---------------------------------------------------------------------------
+// segments
+
+static void prepare_segment(mqvs_segment *s, const uint8_t *dev_nonempty_bytes,
+                            hipStream_t st) {
+    if (dev_nonempty_bytes) {
+        MQVS_HIP(hipMalloc((void **)&s->nonempty_bits, (size_t)(s->n + 7) / 8));
+        s->bytes += (size_t)(s->n + 7) / 8;
+        launch_pack_nonempty(dev_nonempty_bytes, s->n, s->nonempty_bits, st);
+        const int64_t nchunks = (s->n + s->granule - 1) / s->granule;
+        MQVS_HIP(hipMalloc((void **)&s->chunk_ord, sizeof(int) * std::max<int64_t>(nchunks, 1)));
+        s->bytes += sizeof(int) * nchunks;
+        launch_chunk_ordinals(nullptr, s->nonempty_bits, nullptr, s->n, s->granule, 0,
+                              s->chunk_ord, st);
+    }
+    if (s->metric == MQVS_METRIC_COSINE) {
+        launch_normalize_rows(s->rows, s->n, s->d, st);
+    } else {
+        MQVS_HIP(hipMalloc((void **)&s->norms, sizeof(float) * std::max<int64_t>(s->n, 1)));
+        s->bytes += sizeof(float) * s->n;
+        launch_row_norms(s->rows, s->n, s->d, s->norms, st);
+    }
+    MQVS_HIP(hipGetLastError());
+    MQVS_HIP(hipStreamSynchronize(st));
+}
+
+static void check_seg_args(int64_t n, int32_t d, int32_t metric, int64_t granule,
+                           int64_t row_offset) {
+    if (n < 0 || n >= ((int64_t)1 << 32)) fail(MQVS_ERR_BAD_ARGUMENTS, "segment rows must be in [0, 2^32)");
+    if (d <= 0) fail(MQVS_ERR_BAD_ARGUMENTS, "dimension must be positive");
+    if (metric != MQVS_METRIC_L2 && metric != MQVS_METRIC_IP && metric != MQVS_METRIC_COSINE)
+        fail(MQVS_ERR_NOT_IMPLEMENTED, "Metric not implemented in brute force search for Float32 Vector");
+    if (granule <= 0) fail(MQVS_ERR_BAD_ARGUMENTS, "granule_rows must be positive");
+    if (row_offset < 0 || row_offset % granule != 0)
+        fail(MQVS_ERR_BAD_ARGUMENTS, "row_offset must be a non-negative multiple of granule_rows");
+}
+
+static mqvs_segment *new_segment(int64_t n, int32_t d, int32_t metric, int64_t granule,
+                                 int64_t row_offset) {
+    auto *s = new mqvs_segment();
+    MQVS_HIP(hipGetDevice(&s->device));
+    s->n = n;
+    s->d = d;
+    s->metric = metric;
+    s->granule = granule;
+    s->row_offset = row_offset;
+    const size_t bytes = (size_t)std::max<int64_t>(n, 1) * d * sizeof(float);
+    hipError_t e = hipMalloc((void **)&s->rows, bytes);
+    if (e != hipSuccess) {
+        (void)hipGetLastError();
+        delete s;
+        fail(MQVS_ERR_MEMORY_LIMIT, "HBM allocation of " + std::to_string(bytes) + " bytes failed");
+    }
+    s->bytes = bytes;
+    return s;
+}
+
+static void free_segment(mqvs_segment *s) {
+    if (!s) return;
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    (void)hipSetDevice(s->device);
+    if (s->rows) (void)hipFree(s->rows);
+    if (s->norms) (void)hipFree(s->norms);
+    if (s->nonempty_bits) (void)hipFree(s->nonempty_bits);
+    if (s->chunk_ord) (void)hipFree(s->chunk_ord);
+    if (cur >= 0) (void)hipSetDevice(cur);
+    delete s;
+}
+
+static bool all_nonempty(const uint8_t *ne, int64_t n) {
+    for (int64_t i = 0; i < n; ++i)
+        if (!ne[i]) return false;
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// search
+
+struct Range {
+    int64_t begin, end, tiles, tiles_per_chunk;
+};
+
+static Range make_range(int64_t b, int64_t e, int64_t tile_rows, int64_t chunk_rows, bool aligned) {
+    Range r{b, e, 0, 0};
+    if (e <= b) return r;
+    if (aligned) {
+        r.tiles_per_chunk = (chunk_rows + tile_rows - 1) / tile_rows;
+        const int64_t nch = (e - b + chunk_rows - 1) / chunk_rows;
+        r.tiles = nch * r.tiles_per_chunk;
+    } else {
+        r.tiles = (e - b + tile_rows - 1) / tile_rows;
+    }
+    return r;
+}
+
+static void run_scan(ScanParams p, const Range &r, bool mfma, int metric, bool probe, hipStream_t st) {
+    if (r.tiles <= 0) return;
+    p.row_begin = r.begin;
+    p.row_end = r.end;
+    p.tiles = r.tiles;
+    p.tiles_per_chunk = r.tiles_per_chunk;
+    p.tile_rows = mfma ? kMfmaRows : kSmallRows;
+    if (mfma)
+        launch_scan_mfma(p, metric, probe, st);
+    else
+        launch_scan_small(p, metric, probe, st);
+    MQVS_HIP(hipGetLastError());
+}
+
+static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+// metric: public metric, or kMetricIpRaw for the faiss-contract entry point
+static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, int metric,
+                        const uint8_t *filter, const uint8_t *exists, int64_t *out_ids,
+                        float *out_dist, uint32_t flags, hipStream_t user_stream) {
+    if (!seg) fail(MQVS_ERR_BAD_ARGUMENTS, "null segment");
+    if (nq < 0 || k < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "nq and k must be non-negative");
+    if (nq > 0 && k > 0 && (!queries || !out_ids || !out_dist))
+        fail(MQVS_ERR_BAD_ARGUMENTS, "null query or output pointer");
+    const bool cos = metric == MQVS_METRIC_COSINE;
+    if (metric != MQVS_METRIC_L2 && metric != MQVS_METRIC_IP && !cos && metric != kMetricIpRaw)
+        fail(MQVS_ERR_NOT_IMPLEMENTED, "Metric not implemented in brute force search for Float32 Vector");
+    if (cos != (seg->metric == MQVS_METRIC_COSINE))
+        fail(MQVS_ERR_LOGICAL, "segment was prepared for a different metric (cosine segments are "
+                               "normalised in HBM and serve only cosine searches)");
+    if (k > kSortCap) fail(MQVS_ERR_BAD_ARGUMENTS, "k above " + std::to_string(kSortCap) + " not supported");
+    mqvs_search_stats st{};
+    g_stats = st;
+    if (nq == 0 || k == 0) return;
+
+    DeviceGuard guard(seg->device);
+    Workspace &ws = workspace(seg->device);
+    hipStream_t s = user_stream ? (hipStream_t)user_stream : ws.stream;
+    const bool dev = flags & MQVS_F_DEVICE_PTRS;
+    const int64_t n = seg->n;
+    const int d = seg->d;
+    const int64_t bm_bytes = (n + 7) / 8;
+    const bool timing = g_timing != 0;
+    if (timing) MQVS_HIP(hipEventRecord(ws.ev[0], s));
+
+    // ---- inputs on device
+    const float *dq = queries;
+    const uint8_t *dfilter = filter, *dexists = exists;
+    if (!dev) {
+        float *q = (float *)ws.queries.get(sizeof(float) * (size_t)nq * d);
+        MQVS_HIP(hipMemcpyAsync(q, queries, sizeof(float) * (size_t)nq * d, hipMemcpyHostToDevice, s));
+        dq = q;
+        if (filter) {
+            auto *f = (uint8_t *)ws.filter.get(bm_bytes);
+            MQVS_HIP(hipMemcpyAsync(f, filter, bm_bytes, hipMemcpyHostToDevice, s));
+            dfilter = f;
+        }
+        if (exists) {
+            auto *f = (uint8_t *)ws.exists.get(bm_bytes);
+            MQVS_HIP(hipMemcpyAsync(f, exists, bm_bytes, hipMemcpyHostToDevice, s));
+            dexists = f;
+        }
+    }
+    int64_t *dids = out_ids;
+    float *ddist = out_dist;
+    if (!dev) {
+        dids = (int64_t *)ws.out_ids.get(sizeof(int64_t) * (size_t)nq * k);
+        ddist = (float *)ws.out_dist.get(sizeof(float) * (size_t)nq * k);
+    }
+
+    // ---- query prep
+    const bool mfma = nq >= kBlasThreshold;
+    const int maxv = cos ? kMaxVariants : 1;
+    const int64_t qstride = round_up(d, 32);
+    float *qvars = (float *)ws.qvars.get(sizeof(float) * (size_t)nq * maxv * qstride);
+    MQVS_HIP(hipMemsetAsync(qvars, 0, sizeof(float) * (size_t)nq * maxv * qstride, s));
+    float *qnorms = (float *)ws.qnorms.get(sizeof(float) * nq);
+    int *qmu = (int *)ws.qmu.get(sizeof(int) * nq);
+    int *qlam = (int *)ws.qlam.get(sizeof(int) * nq);
+    int *status = (int *)ws.status.get(sizeof(int) * 4);
+    MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
+    launch_query_prep(dq, nq, d, cos ? MQVS_METRIC_COSINE : MQVS_METRIC_L2, mfma && metric == MQVS_METRIC_L2,
+                      qvars, qnorms, qmu, qlam, status, s);
+    MQVS_HIP(hipGetLastError());
+
+    // ---- chunk ordinals
+    const int *chunk_ord = nullptr;
+    if (dfilter) {
+        if (cos) {
+            const int64_t nch = (n + seg->granule - 1) / seg->granule;
+            int *o = (int *)ws.ord.get(sizeof(int) * std::max<int64_t>(nch, 1));
+            launch_chunk_ordinals(dfilter, seg->nonempty_bits, dexists, n, seg->granule, 1, o, s);
+            MQVS_HIP(hipGetLastError());
+            chunk_ord = o;
+        }
+    } else {
+        chunk_ord = seg->chunk_ord;
+    }
+    const bool aligned = cos || chunk_ord != nullptr;
+    const int64_t tile_rows = mfma ? kMfmaRows : kSmallRows;
+
+    // ---- probe size: expected candidates ~ k*n/P; aim at cap/3
+    int64_t P = n;
+    if (n > 32768) {
+        P = (int64_t)((3.0 * k * (double)n) / kSortCap) + 1;
+        P = std::max<int64_t>(P, 8 * (int64_t)k);
+        P = round_up(P, aligned ? seg->granule : tile_rows);
+        if (P > n) P = n;
+    }
+
+    ScanParams p{};
+    p.rows = seg->rows;
+    p.row_norms = seg->norms;
+    p.n = n;
+    p.d = d;
+    p.nq = nq;
+    p.qvars = qvars;
+    p.qnorms = qnorms;
+    p.qmu = qmu;
+    p.qlam = qlam;
+    p.maxv = maxv;
+    p.chunk_rows = seg->granule;
+    p.chunk_ord = chunk_ord;
+    p.filter = dfilter;
+    p.exists = dexists;
+    p.nonempty = seg->nonempty_bits;
+    p.num_qblocks = (nq + kMfmaQ - 1) / kMfmaQ;
+    const int cap = kSortCap;
+    uint32_t *tau = (uint32_t *)ws.tau.get(sizeof(uint32_t) * nq);
+    int *count = (int *)ws.count.get(sizeof(int) * nq);
+    Cand *cand = (Cand *)ws.cand.get(sizeof(Cand) * (size_t)nq * cap);
+    int *overflow = (int *)ws.overflow.get(sizeof(int) * 4);
+    p.tau = tau;
+    p.cand_count = count;
+    p.cand = cand;
+    p.cand_cap = cap;
+    float *probe = (float *)ws.probe.get(sizeof(float) * (size_t)nq * P);
+    p.probe = probe;
+    p.probe_ld = P;
+
+    const Range pr = make_range(0, P, tile_rows, seg->granule, aligned);
+    const Range mr = make_range(P, n, tile_rows, seg->granule, aligned);
+    run_scan(p, pr, mfma, metric, true, s);
+    MQVS_HIP(hipMemsetAsync(count, 0, sizeof(int) * nq, s));
+    if (timing) MQVS_HIP(hipEventRecord(ws.ev[1], s));
+    launch_probe_select(probe, P, P, nq, k, metric, tau, count, cand, cap, 0, s);
+    MQVS_HIP(hipGetLastError());
+    if (timing) MQVS_HIP(hipEventRecord(ws.ev[2], s));
+    run_scan(p, mr, mfma, metric, false, s);
+    if (timing) MQVS_HIP(hipEventRecord(ws.ev[3], s));
+    MQVS_HIP(hipMemsetAsync(overflow, 0, sizeof(int) * 4, s));
+    launch_final_select(cand, count, cap, nq, k, metric, seg->granule, seg->row_offset, dids, ddist,
+                        overflow, s);
+    MQVS_HIP(hipGetLastError());
+    if (timing) MQVS_HIP(hipEventRecord(ws.ev[4], s));
+
+    st.path = mfma ? 1 : 0;
+    st.probe_rows = P;
+    st.rows_scanned = n;
+    st.scan_launches = (pr.tiles > 0) + (mr.tiles > 0);
+
+    const bool async = dev && (flags & MQVS_F_ASYNC);
+    if (!async) {
+        MQVS_HIP(hipMemcpyAsync(ws.host_flags, overflow, sizeof(int), hipMemcpyDeviceToHost, s));
+        MQVS_HIP(hipMemcpyAsync(ws.host_flags + 1, status, sizeof(int), hipMemcpyDeviceToHost, s));
+        MQVS_HIP(hipStreamSynchronize(s));
+        if (ws.host_flags[1]) fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not reach a cycle");
+        int rescans = 0;
+        while (ws.host_flags[0]) {
+            if (++rescans > 3)
+                fail(MQVS_ERR_LOGICAL, "candidate overflow: more than " + std::to_string(cap) +
+                                           " rows tie at the k-th distance");
+            launch_cand_tau(cand, count, cap, nq, k, metric, tau, nullptr, s);
+            MQVS_HIP(hipMemsetAsync(count, 0, sizeof(int) * nq, s));
+            run_scan(p, make_range(0, n, tile_rows, seg->granule, aligned), mfma, metric, false, s);
+            MQVS_HIP(hipMemsetAsync(overflow, 0, sizeof(int) * 4, s));
+            launch_final_select(cand, count, cap, nq, k, metric, seg->granule, seg->row_offset, dids,
+                                ddist, overflow, s);
+            MQVS_HIP(hipGetLastError());
+            MQVS_HIP(hipMemcpyAsync(ws.host_flags, overflow, sizeof(int), hipMemcpyDeviceToHost, s));
+            MQVS_HIP(hipStreamSynchronize(s));
+        }
+        st.rescans = rescans;
+        if (!dev) {
+            MQVS_HIP(hipMemcpyAsync(out_ids, dids, sizeof(int64_t) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
+            MQVS_HIP(hipMemcpyAsync(out_dist, ddist, sizeof(float) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
+            MQVS_HIP(hipStreamSynchronize(s));
+        }
+        if (timing) {
+            float a = 0, b = 0, c = 0, e = 0;
+            MQVS_HIP(hipEventElapsedTime(&a, ws.ev[0], ws.ev[1]));
+            MQVS_HIP(hipEventElapsedTime(&b, ws.ev[1], ws.ev[2]));
+            MQVS_HIP(hipEventElapsedTime(&c, ws.ev[2], ws.ev[3]));
+            MQVS_HIP(hipEventElapsedTime(&e, ws.ev[3], ws.ev[4]));
+            st.scan_ms = a + c;
+            st.select_ms = b + e;
+            st.total_ms = a + b + c + e;
+        }
+    }
+    g_stats = st;
+}
+
+}  // namespace mqvs
+
+using namespace mqvs;
+
+// ---------------------------------------------------------------------------
+extern "C" {
+
+int mqvs_abi_version(void) { return MQVS_ABI_VERSION; }
+
+const char *mqvs_last_error(void) { return g_error.c_str(); }
+
+int mqvs_init(int device) {
+    return guarded([&] {
+        int n = 0;
+        MQVS_HIP(hipGetDeviceCount(&n));
+        if (device < 0 || device >= n) fail(MQVS_ERR_BAD_ARGUMENTS, "no such device");
+        MQVS_HIP(hipSetDevice(device));
+    });
+}
+
+int mqvs_device_count(int *count) {
+    return guarded([&] {
+        if (!count) fail(MQVS_ERR_BAD_ARGUMENTS, "null count");
+        MQVS_HIP(hipGetDeviceCount(count));
+    });
+}
+
+int mqvs_thread_release(void) {
+    return guarded([&] {
+        if (!g_ws) return;
+        for (auto &kv : *g_ws) {
+            (void)hipSetDevice(kv.first);
+            kv.second.release();
+        }
+        g_ws->clear();
+    });
+}
+
+int mqvs_segment_create(const float *host_rows, int64_t n, int32_t d, int32_t metric,
+                        int64_t granule_rows, const uint8_t *nonempty, int64_t row_offset,
+                        mqvs_segment_t *out) {
+    return guarded([&] {
+        if (!out) fail(MQVS_ERR_BAD_ARGUMENTS, "null output handle");
+        *out = nullptr;
+        check_seg_args(n, d, metric, granule_rows, row_offset);
+        if (n > 0 && !host_rows) fail(MQVS_ERR_BAD_ARGUMENTS, "null rows");
+        mqvs_segment *s = new_segment(n, d, metric, granule_rows, row_offset);
+        try {
+            Workspace &ws = workspace(s->device);
+            if (n > 0)
+                MQVS_HIP(hipMemcpyAsync(s->rows, host_rows, sizeof(float) * (size_t)n * d,
+                                        hipMemcpyHostToDevice, ws.stream));
+            const uint8_t *dne = nullptr;
+            if (nonempty && n > 0 && !all_nonempty(nonempty, n)) {
+                auto *b = (uint8_t *)ws.misc.get((size_t)n);
+                MQVS_HIP(hipMemcpyAsync(b, nonempty, (size_t)n, hipMemcpyHostToDevice, ws.stream));
+                dne = b;
+            }
+            prepare_segment(s, dne, ws.stream);
+        } catch (...) {
+            free_segment(s);
+            throw;
+        }
+        *out = s;
+    });
+}
+
+int mqvs_segment_create_device(const float *dev_rows, int64_t n, int32_t d, int32_t metric,
+                               int64_t granule_rows, const uint8_t *dev_nonempty,
+                               int64_t row_offset, mqvs_segment_t *out) {
+    return guarded([&] {
+        if (!out) fail(MQVS_ERR_BAD_ARGUMENTS, "null output handle");
+        *out = nullptr;
+        check_seg_args(n, d, metric, granule_rows, row_offset);
+        if (n > 0 && !dev_rows) fail(MQVS_ERR_BAD_ARGUMENTS, "null rows");
+        mqvs_segment *s = new_segment(n, d, metric, granule_rows, row_offset);
+        try {
+            Workspace &ws = workspace(s->device);
+            if (n > 0)
+                MQVS_HIP(hipMemcpyAsync(s->rows, dev_rows, sizeof(float) * (size_t)n * d,
+                                        hipMemcpyDeviceToDevice, ws.stream));
+            prepare_segment(s, dev_nonempty, ws.stream);
+        } catch (...) {
+            free_segment(s);
+            throw;
+        }
+        *out = s;
+    });
+}
+
+int mqvs_segment_generate(uint64_t seed, int32_t mode, int64_t n, int32_t d, int32_t metric,
+                          int64_t granule_rows, int64_t row_offset, mqvs_segment_t *out) {
+    return guarded([&] {
+        if (!out) fail(MQVS_ERR_BAD_ARGUMENTS, "null output handle");
+        *out = nullptr;
+        check_seg_args(n, d, metric, granule_rows, row_offset);
+        if (mode < 0 || mode > 2) fail(MQVS_ERR_BAD_ARGUMENTS, "generator mode must be 0, 1 or 2");
+        mqvs_segment *s = new_segment(n, d, metric, granule_rows, row_offset);
+        try {
+            Workspace &ws = workspace(s->device);
+            launch_generate(seed, mode, row_offset, n, d, s->rows, ws.stream);
+            MQVS_HIP(hipGetLastError());
+            prepare_segment(s, nullptr, ws.stream);
+        } catch (...) {
+            free_segment(s);
+            throw;
+        }
+        *out = s;
+    });
+}
+
+int mqvs_segment_free(mqvs_segment_t seg) {
+    return guarded([&] { free_segment(seg); });
+}
+
+int mqvs_segment_info(mqvs_segment_t seg, int64_t *n, int32_t *d, int32_t *metric,
+                      int64_t *granule_rows, int64_t *row_offset, size_t *hbm_bytes) {
+    return guarded([&] {
+        if (!seg) fail(MQVS_ERR_BAD_ARGUMENTS, "null segment");
+        if (n) *n = seg->n;
+        if (d) *d = seg->d;
+        if (metric) *metric = seg->metric;
+        if (granule_rows) *granule_rows = seg->granule;
+        if (row_offset) *row_offset = seg->row_offset;
+        if (hbm_bytes) *hbm_bytes = seg->bytes;
+    });
+}
+
+int mqvs_segment_rows(mqvs_segment_t seg, const float **dev_rows) {
+    return guarded([&] {
+        if (!seg || !dev_rows) fail(MQVS_ERR_BAD_ARGUMENTS, "null argument");
+        *dev_rows = seg->rows;
+    });
+}
+
+int mqvs_search(mqvs_segment_t seg, const float *queries, int32_t nq, int32_t k, int32_t metric,
+                const uint8_t *filter, const uint8_t *row_exists, int64_t *out_ids, float *out_dist,
+                uint32_t flags, mqvs_stream_t stream) {
+    return guarded([&] {
+        search_impl(seg, queries, nq, k, metric, filter, row_exists, out_ids, out_dist, flags,
+                    (hipStream_t)stream);
+    });
+}
+
+int mqvs_knn_raw(const float *x, const float *y, int64_t d, int64_t k, int64_t nx, int64_t ny,
+                 int32_t metric, int64_t *result_id, float *distance) {
+    return guarded([&] {
+        if (metric != MQVS_METRIC_L2 && metric != MQVS_METRIC_IP)
+            fail(MQVS_ERR_NOT_IMPLEMENTED, "Metric not implemented in brute force search for Float32 Vector");
+        if (d <= 0 || d > INT32_MAX || k < 0 || k > INT32_MAX || nx < 0 || nx > INT32_MAX || ny < 0)
+            fail(MQVS_ERR_BAD_ARGUMENTS, "bad sizes");
+        if (nx == 0 || k == 0) return;
+        if (ny == 0) {
+            for (int64_t i = 0; i < nx * k; ++i) {
+                result_id[i] = -1;
+                distance[i] = metric == MQVS_METRIC_L2 ? 3.40282347e+38f : -3.40282347e+38f;
+            }
+            return;
+        }
+        mqvs_segment *s = new_segment(ny, (int)d, metric, ny, 0);
+        try {
+            Workspace &ws = workspace(s->device);
+            MQVS_HIP(hipMemcpyAsync(s->rows, y, sizeof(float) * (size_t)ny * d, hipMemcpyHostToDevice,
+                                    ws.stream));
+            prepare_segment(s, nullptr, ws.stream);
+            search_impl(s, x, (int)nx, (int)k, metric == MQVS_METRIC_IP ? kMetricIpRaw : MQVS_METRIC_L2,
+                        nullptr, nullptr, result_id, distance, 0, nullptr);
+        } catch (...) {
+            free_segment(s);
+            throw;
+        }
+        free_segment(s);
+    });
+}
+
+int mqvs_merge_shards(int32_t nshards, int32_t nq, int32_t k, int32_t metric, const int64_t *in_ids,
+                      const float *in_dist, int64_t *out_ids, float *out_dist, uint32_t flags,
+                      mqvs_stream_t stream) {
+    return guarded([&] {
+        if (nshards <= 0 || nq < 0 || k < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "bad sizes");
+        if ((int64_t)nshards * k > kSortCap) fail(MQVS_ERR_BAD_ARGUMENTS, "nshards * k above sort capacity");
+        if (nq == 0 || k == 0) return;
+        int dev = 0;
+        MQVS_HIP(hipGetDevice(&dev));
+        Workspace &ws = workspace(dev);
+        hipStream_t s = stream ? (hipStream_t)stream : ws.stream;
+        const size_t nin = (size_t)nshards * nq * k, nout = (size_t)nq * k;
+        const int64_t *di = in_ids;
+        const float *dd = in_dist;
+        int64_t *oi = out_ids;
+        float *od = out_dist;
+        const bool devp = flags & MQVS_F_DEVICE_PTRS;
+        if (!devp) {
+            auto *b = (char *)ws.misc.get(nin * 12 + nout * 12 + 64);
+            auto *bi = (int64_t *)b;
+            auto *bd = (float *)(b + nin * 8);
+            oi = (int64_t *)(b + nin * 12 + 16 - (nin * 12) % 16);
+            od = (float *)((char *)oi + nout * 8);
+            MQVS_HIP(hipMemcpyAsync(bi, in_ids, nin * 8, hipMemcpyHostToDevice, s));
+            MQVS_HIP(hipMemcpyAsync(bd, in_dist, nin * 4, hipMemcpyHostToDevice, s));
+            di = bi;
+            dd = bd;
+        }
+        launch_merge_shards(nshards, nq, k, metric, di, dd, oi, od, s);
+        MQVS_HIP(hipGetLastError());
+        if (!devp) {
+            MQVS_HIP(hipMemcpyAsync(out_ids, oi, nout * 8, hipMemcpyDeviceToHost, s));
+            MQVS_HIP(hipMemcpyAsync(out_dist, od, nout * 4, hipMemcpyDeviceToHost, s));
+        }
+        if (!(devp && (flags & MQVS_F_ASYNC))) MQVS_HIP(hipStreamSynchronize(s));
+    });
+}
+
+int mqvs_generate_device(uint64_t seed, int32_t mode, int64_t row0, int64_t n, int32_t d,
+                         float *dev_out, mqvs_stream_t stream) {
+    return guarded([&] {
+        if (mode < 0 || mode > 2 || n < 0 || d <= 0) fail(MQVS_ERR_BAD_ARGUMENTS, "bad arguments");
+        int dev = 0;
+        MQVS_HIP(hipGetDevice(&dev));
+        Workspace &ws = workspace(dev);
+        hipStream_t s = stream ? (hipStream_t)stream : ws.stream;
+        launch_generate(seed, mode, row0, n, d, dev_out, s);
+        MQVS_HIP(hipGetLastError());
+        MQVS_HIP(hipStreamSynchronize(s));
+    });
+}
+
+int mqvs_rerank(mqvs_segment_t, const float *, int32_t, const int64_t *, int32_t, int32_t, int32_t,
+                int64_t *, float *, uint32_t, mqvs_stream_t) {
+    set_error("mqvs_rerank: not implemented in this build");
+    return MQVS_ERR_NOT_IMPLEMENTED;
+}
+
+int mqvs_last_search_stats(mqvs_search_stats *out) {
+    if (!out) return MQVS_ERR_BAD_ARGUMENTS;
+    *out = g_stats;
+    return MQVS_OK;
+}
+
+int mqvs_set_timing(int enabled) {
+    g_timing = enabled;
+    return MQVS_OK;
+}
+
+}  // extern "C"

@@ -1,0 +1,191 @@
+// mqvs_internal.h -- shared definitions of libmqvs (gfx950 only).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include <string>
+
+#include "../../include/mqvs.h"
+
+namespace mqvs {
+
+// ---------------------------------------------------------------------------
+// Tunables
+constexpr int kBlasThreshold = 20;   // faiss distance_compute_blas_threshold
+constexpr int kMaxVariants = 16;     // cosine query re-normalisation variants kept
+constexpr int kSortCap = 4096;       // candidates sorted in LDS per query
+constexpr int kSmallRows = 256;      // rows per tile, VALU scan
+constexpr int kMfmaRows = 128;       // rows per tile, MFMA scan
+constexpr int kMfmaQ = 128;          // queries per tile, MFMA scan
+// Internal metric id: raw faiss inner product (knn_inner_product: every
+// ip > -FLT_MAX enters the heap), used by mqvs_knn_raw only.  The operator
+// path (mqvs_search) applies searchWrapper's FLT_MIN cut instead.
+constexpr int kMetricIpRaw = 3;
+
+// Candidate record: raw metric value (d for L2, ip for IP/cosine) + local row.
+struct __attribute__((aligned(8))) Cand {
+    float raw;
+    uint32_t row;
+};
+
+// ---------------------------------------------------------------------------
+// Ordering keys.  key32(raw) is a monotone encoding of the primary sort key
+// (smaller = better) and 0xFFFFFFFF for rows the reference never returns:
+//   L2:     d < FLT_MAX (faiss neutral FLT_MAX is strict, NaN never enters)
+//   IP:     ip > FLT_MIN (searchWrapper's FLT_MIN init, MergeTreeVSManager.cpp:1033,1661)
+//   Cosine: ip > -FLT_MAX and 1 - ip < FLT_MAX; primary key 1 - ip
+__host__ __device__ inline uint32_t ord_asc(float f) {
+    uint32_t u = __builtin_bit_cast(uint32_t, f);
+    return (u & 0x80000000u) ? ~u : (u | 0x80000000u);
+}
+
+__host__ __device__ inline float cos_dist(float ip) {
+    // 1 - ip exactly as VIWithDataPart.h:376 computes it (one fp32 subtraction)
+    return 1.0f - ip;
+}
+
+template <int METRIC>
+__host__ __device__ inline uint32_t key32(float raw) {
+    const float FLTMAX = 3.40282347e+38f;
+    const float FLTMIN = 1.17549435e-38f;
+    if (METRIC == MQVS_METRIC_L2) {
+        if (!(raw < FLTMAX)) return 0xFFFFFFFFu;
+        return ord_asc(raw);
+    } else if (METRIC == MQVS_METRIC_IP) {
+        if (!(raw > FLTMIN)) return 0xFFFFFFFFu;
+        return ~ord_asc(raw);  // descending ip
+    } else if (METRIC == kMetricIpRaw) {
+        if (!(raw > -FLTMAX)) return 0xFFFFFFFFu;
+        return ~ord_asc(raw);
+    } else {
+        if (!(raw > -FLTMAX)) return 0xFFFFFFFFu;
+        const float d = cos_dist(raw);
+        if (!(d < FLTMAX)) return 0xFFFFFFFFu;
+        return ord_asc(d);
+    }
+}
+
+__host__ __device__ inline uint32_t key32_rt(int metric, float raw) {
+    return metric == MQVS_METRIC_L2       ? key32<MQVS_METRIC_L2>(raw)
+           : metric == MQVS_METRIC_IP     ? key32<MQVS_METRIC_IP>(raw)
+           : metric == MQVS_METRIC_COSINE ? key32<MQVS_METRIC_COSINE>(raw)
+                                          : key32<kMetricIpRaw>(raw);
+}
+
+__device__ inline bool bit_test(const uint8_t *bm, int64_t i) {
+    return (bm[i >> 3] >> (i & 7)) & 1;
+}
+
+// ---------------------------------------------------------------------------
+// Scan parameters shared by the VALU and MFMA scan kernels.
+struct ScanParams {
+    const float *rows;      // segment rows (normalised for cosine)
+    const float *row_norms; // |y|^2 per row (L2 BLAS branch), may be null
+    int64_t n;              // segment rows
+    int d;
+    int nq;
+    const float *qvars;     // [nq][maxv][d] query variants
+    const float *qnorms;    // [nq] |q|^2 (L2 BLAS branch)
+    const int *qmu;         // [nq] cosine variant cycle start
+    const int *qlam;        // [nq] cosine variant cycle length
+    int maxv;
+    int64_t chunk_rows;     // granule rows (chunking for cosine variants)
+    const int *chunk_ord;   // [nchunks] ordinal, -1 = chunk never searched; null = identity
+    const uint8_t *filter;  // PREWHERE bitmap or null
+    const uint8_t *exists;  // LWD bitmap or null
+    const uint8_t *nonempty;// nonempty bitmap or null (only consulted with a filter)
+    int64_t row_begin, row_end;  // scan range [row_begin, row_end)
+    int64_t tiles;          // number of row tiles in the range
+    int64_t tiles_per_chunk;// tiles per chunk (chunk-aligned tiling) or 0 = contiguous
+    int64_t tile_rows;
+    // PROBE output: dense raw values [nq][probe_ld], column = row - row_begin
+    float *probe;
+    int64_t probe_ld;
+    // APPEND output
+    const uint32_t *tau;    // [nq] key threshold (inclusive)
+    int *cand_count;        // [nq]
+    Cand *cand;             // [nq][cand_cap]
+    int cand_cap;
+    int num_qblocks;        // MFMA: query blocks
+};
+
+// Tile -> [r0, r1) and chunk index.
+__device__ inline void tile_range(const ScanParams &p, int64_t t, int64_t &r0, int64_t &r1,
+                                  int64_t &chunk) {
+    if (p.tiles_per_chunk > 0) {
+        const int64_t c0 = p.row_begin / p.chunk_rows;  // row_begin is chunk-aligned
+        chunk = c0 + t / p.tiles_per_chunk;
+        r0 = chunk * p.chunk_rows + (t % p.tiles_per_chunk) * p.tile_rows;
+        int64_t ce = (chunk + 1) * p.chunk_rows;
+        r1 = r0 + p.tile_rows;
+        if (r1 > ce) r1 = ce;
+    } else {
+        r0 = p.row_begin + t * p.tile_rows;
+        r1 = r0 + p.tile_rows;
+        chunk = p.chunk_rows > 0 ? r0 / p.chunk_rows : 0;
+    }
+    if (r1 > p.row_end) r1 = p.row_end;
+}
+
+__device__ inline int variant_of(const ScanParams &p, int q, int ord) {
+    if (p.maxv <= 1) return 0;
+    const int mu = p.qmu[q], lam = p.qlam[q];
+    return ord < mu ? ord : mu + (ord - mu) % lam;
+}
+
+__device__ inline bool row_valid(const ScanParams &p, int64_t r) {
+    if (p.filter) {
+        if (!bit_test(p.filter, r)) return false;
+        if (p.nonempty && !bit_test(p.nonempty, r)) return false;
+    }
+    if (p.exists && !bit_test(p.exists, r)) return false;
+    return true;
+}
+
+// ---------------------------------------------------------------------------
+// Launchers (kernels_*.hip)
+void launch_scan_small(const ScanParams &p, int metric, bool probe, hipStream_t s);
+void launch_scan_mfma(const ScanParams &p, int metric, bool probe, hipStream_t s);
+void launch_probe_select(const float *probe, int64_t P, int64_t ld, int nq, int k, int metric,
+                         uint32_t *tau, int *cand_count, Cand *cand, int cand_cap,
+                         int64_t row_base, hipStream_t s);
+void launch_cand_tau(const Cand *cand, const int *cand_count, int cand_cap, int nq, int k,
+                     int metric, uint32_t *tau, const int *overflow_q, hipStream_t s);
+void launch_final_select(const Cand *cand, const int *cand_count, int cand_cap, int nq, int k,
+                         int metric, int64_t chunk_rows, int64_t id_offset, int64_t *out_ids,
+                         float *out_dist, int *overflow, hipStream_t s);
+void launch_merge_shards(int nshards, int nq, int k, int metric, const int64_t *in_ids,
+                         const float *in_dist, int64_t *out_ids, float *out_dist, hipStream_t s);
+void launch_normalize_rows(float *rows, int64_t n, int d, hipStream_t s);
+void launch_row_norms(const float *rows, int64_t n, int d, float *norms, hipStream_t s);
+void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, float *qvars,
+                       float *qnorms, int *qmu, int *qlam, int *status, hipStream_t s);
+void launch_generate(uint64_t seed, int mode, int64_t row0, int64_t n, int d, float *out,
+                     hipStream_t s);
+void launch_pack_nonempty(const uint8_t *bytes, int64_t n, uint8_t *bits, hipStream_t s);
+void launch_chunk_ordinals(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists,
+                           int64_t n, int64_t chunk_rows, int require_filter, int *ord,
+                           hipStream_t s);
+void launch_rerank(const ScanParams &p, const int64_t *cand_ids, int ncand, int metric,
+                   bool blas, hipStream_t s);
+
+// ---------------------------------------------------------------------------
+// Error plumbing
+void set_error(const std::string &msg);
+
+struct Error {
+    int code;
+    std::string msg;
+};
+
+}  // namespace mqvs
+
+#define MQVS_HIP(call)                                                                 \
+    do {                                                                               \
+        hipError_t e_ = (call);                                                        \
+        if (e_ != hipSuccess)                                                          \
+            throw ::mqvs::Error{e_ == hipErrorOutOfMemory ? MQVS_ERR_MEMORY_LIMIT         \
+                                                          : MQVS_ERR_DEVICE,             \
+                                std::string(#call) + ": " + hipGetErrorString(e_)};    \
+    } while (0)

@@ -1,0 +1,231 @@
+"""Host-side mirror of MyScaleDB's brute-force vector-scan operator over libmqvs.
+
+Names and contracts follow the reference so the parity tests read like its own:
+
+* ``try_brute_force_search``  -- VectorIndex::tryBruteForceSearch<FloatVector>
+  (src/VectorIndex/Common/BruteForceSearch.h:62-111); faiss result layout.
+* ``VectorScanSegment``       -- one data part's Array(Float32) column, registered
+  once and resident in HBM (replaces the per-granule copy loop of
+  MergeTreeVSManager.cpp:1366-1393).
+* ``vector_scan_without_index`` -- MergeTreeVSManager::vectorScanWithoutIndex<Float>
+  (MergeTreeVSManager.cpp:960-1536) incl. searchWrapper (:1538-1680); returns
+  the same result columns (label UInt32, [vector_id UInt32,] distance Float32)
+  with the -1 labels dropped (:1502-1532).
+
+Inputs are numpy arrays (host) or torch tensors already on the GPU (device
+pointers passed straight through the C-ABI).  Every call runs the HIP kernels;
+there is no CPU path in this package.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+
+from . import _lib
+from ._lib import F_ASYNC, F_DEVICE_PTRS, METRICS, check, lib
+
+FLT_MAX = np.float32(3.4028235e38)
+FLT_MIN = np.float32(1.1754944e-38)
+DEFAULT_GRANULE = 8192  # MergeTreeSettings.h index_granularity
+
+
+def metric_id(metric) -> int:
+    if isinstance(metric, (int, np.integer)):
+        return int(metric)
+    try:
+        return METRICS[metric]
+    except KeyError:
+        raise _lib.NotImplementedMetric(_lib.ERR_NOT_IMPLEMENTED,
+                                        f"Metric {metric} not implemented in brute force search")
+
+
+def _is_torch(a):
+    return type(a).__module__.startswith("torch")
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if _is_torch(a):
+        return ctypes.c_void_p(a.data_ptr())
+    return a.ctypes.data_as(ctypes.c_void_p)
+
+
+def _host_f32(a):
+    return np.ascontiguousarray(a, dtype=np.float32)
+
+
+def _host_u8(a):
+    return None if a is None else np.ascontiguousarray(a, dtype=np.uint8)
+
+
+def pack_bitmap(mask) -> np.ndarray:
+    """bool/0-1 per row -> LSB-first uint8 bitmap (Search::DenseBitmap byte layout)."""
+    return np.packbits(np.asarray(mask, dtype=np.uint8), bitorder="little")
+
+
+def init(device: int = 0):
+    check(lib.mqvs_init(device))
+
+
+class VectorScanSegment:
+    """A data part's vector column resident in HBM.
+
+    rows: (n, d) float32 (numpy, or a torch CUDA tensor); rows whose Array is
+    empty must be FLT_MAX-filled and flagged 0 in ``nonempty``.
+    """
+
+    def __init__(self, handle, n, d, metric, granule, row_offset):
+        self._h = handle
+        self.n, self.d, self.metric, self.granule, self.row_offset = n, d, metric, granule, row_offset
+
+    @classmethod
+    def from_rows(cls, rows, metric="L2", granule=DEFAULT_GRANULE, nonempty=None, row_offset=0):
+        m = metric_id(metric)
+        h = ctypes.c_void_p()
+        if _is_torch(rows):
+            assert rows.is_cuda and rows.is_contiguous()
+            n, d = rows.shape
+            ne = None
+            if nonempty is not None:
+                ne = nonempty
+            check(lib.mqvs_segment_create_device(_ptr(rows), n, d, m, granule, _ptr(ne),
+                                                 row_offset, ctypes.byref(h)))
+        else:
+            rows = _host_f32(rows)
+            n, d = rows.shape
+            ne = _host_u8(nonempty)
+            check(lib.mqvs_segment_create(_ptr(rows), n, d, m, granule, _ptr(ne), row_offset,
+                                          ctypes.byref(h)))
+        return cls(h, n, d, m, granule, row_offset)
+
+    @classmethod
+    def generate(cls, seed, mode, n, d, metric="L2", granule=DEFAULT_GRANULE, row_offset=0):
+        """Synthetic part from the counter-based generator (mode 0 exact, 1 gauss, 2 mixture)."""
+        m = metric_id(metric)
+        h = ctypes.c_void_p()
+        check(lib.mqvs_segment_generate(seed, mode, n, d, m, granule, row_offset, ctypes.byref(h)))
+        return cls(h, n, d, m, granule, row_offset)
+
+    def info(self):
+        n, d, m, g, o = (ctypes.c_int64(), ctypes.c_int32(), ctypes.c_int32(), ctypes.c_int64(),
+                         ctypes.c_int64())
+        b = ctypes.c_size_t()
+        check(lib.mqvs_segment_info(self._h, ctypes.byref(n), ctypes.byref(d), ctypes.byref(m),
+                                    ctypes.byref(g), ctypes.byref(o), ctypes.byref(b)))
+        return dict(n=n.value, d=d.value, metric=m.value, granule=g.value, row_offset=o.value,
+                    hbm_bytes=b.value)
+
+    def device_rows_ptr(self) -> int:
+        p = ctypes.c_void_p()
+        check(lib.mqvs_segment_rows(self._h, ctypes.byref(p)))
+        return p.value
+
+    def search(self, queries, k, metric=None, filter_bitmap=None, row_exists=None, out=None,
+               async_=False, stream=None):
+        """Raw mqvs_search: (ids[nq,k] int64, dist[nq,k] float32), -1 padded."""
+        m = self.metric if metric is None else metric_id(metric)
+        if _is_torch(queries):
+            import torch
+            assert queries.is_cuda and queries.is_contiguous() and queries.dtype == torch.float32
+            nq = queries.shape[0]
+            if out is None:
+                ids = torch.empty((nq, k), dtype=torch.int64, device=queries.device)
+                dist = torch.empty((nq, k), dtype=torch.float32, device=queries.device)
+            else:
+                ids, dist = out
+            flags = F_DEVICE_PTRS | (F_ASYNC if async_ else 0)
+            check(lib.mqvs_search(self._h, _ptr(queries), nq, k, m, _ptr(filter_bitmap),
+                                  _ptr(row_exists), _ptr(ids), _ptr(dist), flags,
+                                  ctypes.c_void_p(stream) if stream else None))
+            return ids, dist
+        q = _host_f32(queries)
+        if q.ndim == 1:
+            q = q[None, :]
+        nq = q.shape[0]
+        if q.shape[1] != self.d:
+            raise _lib.MqvsError(_lib.ERR_LOGICAL,
+                                 f"query dimension {q.shape[1]} != column dimension {self.d}")
+        ids = np.empty((nq, k), np.int64)
+        dist = np.empty((nq, k), np.float32)
+        check(lib.mqvs_search(self._h, _ptr(q), nq, k, m, _ptr(_host_u8(filter_bitmap)),
+                              _ptr(_host_u8(row_exists)), _ptr(ids), _ptr(dist), 0, None))
+        return ids, dist
+
+    def free(self):
+        if self._h:
+            check(lib.mqvs_segment_free(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def try_brute_force_search(x, y, d, k, nx, ny, metric):
+    """VectorIndex::tryBruteForceSearch: returns (result_id[nx*k], distance[nx*k])."""
+    m = metric_id(metric)
+    x = _host_f32(x).reshape(-1)
+    y = _host_f32(y).reshape(-1)
+    ids = np.empty(nx * k, np.int64)
+    dist = np.empty(nx * k, np.float32)
+    check(lib.mqvs_knn_raw(_ptr(x), _ptr(y), d, k, nx, ny, m, _ptr(ids), _ptr(dist)))
+    return ids, dist
+
+
+def vector_scan_without_index(segment: VectorScanSegment, query_vector, k, metric=None,
+                              filter_bitmap=None, row_exists=None, is_batch=False):
+    """MergeTreeVSManager::vectorScanWithoutIndex result columns.
+
+    Returns (label, distance) or, for batch, (label, vector_id, distance) with
+    the reference's emission order: query-major, best first, -1 labels dropped.
+    """
+    q = _host_f32(query_vector)
+    if q.ndim == 1:
+        q = q[None, :]
+    ids, dist = segment.search(q, k, metric, filter_bitmap, row_exists)
+    flat_ids, flat_dist = ids.reshape(-1), dist.reshape(-1)
+    keep = flat_ids > -1
+    label = flat_ids[keep].astype(np.uint32)
+    distance = flat_dist[keep]
+    if is_batch:
+        vector_id = (np.arange(flat_ids.size) // k)[keep].astype(np.uint32)
+        return label, vector_id, distance
+    return label, distance
+
+
+def merge_shards(ids, dist, metric, out=None, async_=False, stream=None):
+    """Merge per-shard results [nshards, nq, k] -> [nq, k] (mqvs_merge_shards)."""
+    m = metric_id(metric)
+    nshards, nq, k = ids.shape
+    if _is_torch(ids):
+        import torch
+        if out is None:
+            oi = torch.empty((nq, k), dtype=torch.int64, device=ids.device)
+            od = torch.empty((nq, k), dtype=torch.float32, device=ids.device)
+        else:
+            oi, od = out
+        flags = F_DEVICE_PTRS | (F_ASYNC if async_ else 0)
+        check(lib.mqvs_merge_shards(nshards, nq, k, m, _ptr(ids.contiguous()), _ptr(dist.contiguous()),
+                                    _ptr(oi), _ptr(od), flags,
+                                    ctypes.c_void_p(stream) if stream else None))
+        return oi, od
+    ids = np.ascontiguousarray(ids, np.int64)
+    dist = _host_f32(dist)
+    oi = np.empty((nq, k), np.int64)
+    od = np.empty((nq, k), np.float32)
+    check(lib.mqvs_merge_shards(nshards, nq, k, m, _ptr(ids), _ptr(dist), _ptr(oi), _ptr(od), 0,
+                                None))
+    return oi, od
+
+
+def generate_device(seed, mode, row0, n, d, out_tensor, stream=None):
+    check(lib.mqvs_generate_device(seed, mode, row0, n, d, _ptr(out_tensor),
+                                   ctypes.c_void_p(stream) if stream else None))
+
+
+def set_timing(enabled: bool):
+    check(lib.mqvs_set_timing(1 if enabled else 0))
