@@ -1,0 +1,272 @@
+#!/usr/bin/env python3
+"""bench.py -- MI355X brute-force vector scan, BASELINE.json configs[1]:
+FLAT cosine over 10M x 768 Float32, batch of 1000 queries, top-100.
+
+One step = one batch search of `--nq` queries over the whole part (every rank
+scans its granule-aligned row-range shard; with N > 1 the per-shard top-k are
+all-gathered over RCCL and merged).  Strong scaling: the 10M-row part is fixed
+and split over N GPUs.  Inputs are generated in HBM (counter-based generator,
+the oracle's bit-identical twin) before the timed region.
+
+Prints ONE JSON line on rank 0 (see the driver contract in the task README).
+"""
+import argparse
+import json
+import math
+import os
+import time
+
+import numpy as np
+
+SEED_BASE, SEED_QUERY = 0x5EED0001, 0x5EED0002
+FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, f32 MFMA (= VALU) dense peak
+HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md, HBM3E spec peak
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--n", type=int, default=10_000_000)
+    ap.add_argument("--d", type=int, default=768)
+    ap.add_argument("--nq", type=int, default=1000)
+    ap.add_argument("--k", type=int, default=100)
+    ap.add_argument("--metric", default="Cosine")
+    ap.add_argument("--mode", type=int, default=2, help="0 exact ints, 1 gauss, 2 gaussian mixture")
+    ap.add_argument("--granule", type=int, default=8192)
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu", action="store_true")
+    ap.add_argument("--no-verify", action="store_true")
+    ap.add_argument("--pmc", default=None, help="rocprofv3 PMC summary JSON for roofline.traffic")
+    return ap.parse_args()
+
+
+# ---------------------------------------------------------------------------
+# oracle-side helpers (CPU baseline leg + sample verification only)
+
+def _oracle():
+    from oracle import oracle as O
+    return O
+
+
+def verify_sample(O, ids, dist, q_host, args, n_probe_rows=20000):
+    """Size-independent exactness check at full size: the returned distances
+    are bit-identical to the oracle formula for those rows, and no sampled
+    other row beats the k-th result (full reference key incl. ties)."""
+    metric = O.METRICS[args.metric]
+    rng = np.random.default_rng(1)
+    blas = args.nq >= 20
+    ok = True
+    checked = 0
+    for qi in (0, args.nq // 2):
+        q = q_host[qi:qi + 1].copy()
+        variants = []
+        if metric == O.COSINE:
+            v = q.copy()
+            for _ in range(16):
+                v = O.normalize(v)
+                if variants and np.array_equal(v.view(np.uint32), variants[-1].view(np.uint32)):
+                    break
+                variants.append(v)
+
+        def dist_of(rows_idx):
+            rows = np.concatenate([O.generate(SEED_BASE, args.mode, int(r), 1, args.d)
+                                   for r in rows_idx]) if len(rows_idx) else np.zeros((0, args.d), np.float32)
+            out = []
+            for r, y in zip(rows_idx, rows):
+                if metric == O.COSINE:
+                    yn = O.normalize(y[None, :])[0]
+                    qv = variants[min(int(r) // args.granule, len(variants) - 1)][0]
+                    ip = O.gemm_dot(qv, yn) if blas else O.inner_product(qv, yn)
+                    out.append((np.float32(1.0) - np.float32(ip), ip))
+                elif metric == O.IP:
+                    ip = O.gemm_dot(q[0], y) if blas else O.inner_product(q[0], y)
+                    out.append((np.float32(ip), ip))
+                else:
+                    if blas:
+                        xn, yn2 = O.norm_l2sqr(q[0]), O.norm_l2sqr(y)
+                        dd = (xn + yn2) - np.float32(2.0) * O.gemm_dot(q[0], y)
+                        dd = max(dd, np.float32(0))
+                    else:
+                        dd = O.l2sqr(q[0], y)
+                    out.append((np.float32(dd), dd))
+            return out
+
+        got_ids = ids[qi]
+        got = dist_of(got_ids[got_ids >= 0])
+        for (dd, _), g in zip(got, dist[qi][got_ids >= 0]):
+            ok &= np.float32(dd).view(np.uint32) == np.float32(g).view(np.uint32)
+        # sampled challengers must not beat the k-th result
+        kth_d = dist[qi][args.k - 1]
+        sample = rng.choice(args.n, size=n_probe_rows, replace=False)
+        sample = sample[~np.isin(sample, got_ids)]
+        ch = dist_of(sample[:2000])
+        for r, (dd, _) in zip(sample[:2000], ch):
+            if metric == O.IP:
+                ok &= not (dd > kth_d or (dd == kth_d and r < got_ids[args.k - 1]))
+            else:
+                ok &= not (dd < kth_d)
+        checked += 1
+    return bool(ok), checked
+
+
+def cpu_baseline(O, args):
+    """The oracle's bit-identical fast restatement, with the reference's
+    threading shape (one thread per part, parts in parallel, cross-part merge),
+    timed on a bounded row sample of the same workload."""
+    threads = max(1, min(16, os.cpu_count() or 1))
+    metric = O.METRICS[args.metric]
+    q = O.generate(SEED_QUERY, args.mode, 0, args.nq, args.d)
+    rows = 4096 * threads
+    base = O.generate(SEED_BASE, args.mode, 0, rows, args.d)
+    t0 = time.perf_counter()
+    O.scan_parts(base, q, args.k, metric, args.granule, threads, threads)
+    t_cal = time.perf_counter() - t0
+    target = int(rows * max(1.0, args.cpu_seconds / max(t_cal, 1e-3)))
+    target = max(rows, min(target, 400_000, args.n))
+    if target > rows:
+        base = O.generate(SEED_BASE, args.mode, 0, target, args.d)
+    t0 = time.perf_counter()
+    O.scan_parts(base, q, args.k, metric, args.granule, threads, threads)
+    t = time.perf_counter() - t0
+    dist_per_s = args.nq * target / t
+    return {
+        "value": round(dist_per_s / args.n, 3),
+        "unit": "queries/s (extrapolated to the full part)",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"{args.nq} queries x first {target} rows ({args.d}-d, {args.metric}), "
+                  f"{threads} parts x 1 thread, {t:.1f} s; "
+                  f"{dist_per_s / 1e6:.1f} M distances/s",
+        "mdist_per_s": round(dist_per_s / 1e6, 2),
+    }
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    torch.cuda.set_device(local)
+    dist_on = world > 1
+    if dist_on:
+        import torch.distributed as tdist
+        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    import myscaledb_amd as mq
+    from myscaledb_amd import _lib
+    from myscaledb_amd.vector_scan import generate_device, merge_shards, set_timing
+
+    mq.init(local)
+    n, d, nq, k, g = args.n, args.d, args.nq, args.k, args.granule
+    nchunks = math.ceil(n / g)
+    c0, c1 = nchunks * rank // world, nchunks * (rank + 1) // world
+    r0, r1 = c0 * g, min(c1 * g, n)
+    seg = mq.VectorScanSegment.generate(SEED_BASE, args.mode, r1 - r0, d, args.metric, g, row_offset=r0)
+    q = torch.empty((nq, d), dtype=torch.float32, device="cuda")
+    generate_device(SEED_QUERY, args.mode, 0, nq, d, q)
+    ids = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+    dst = torch.empty((nq, k), dtype=torch.float32, device="cuda")
+    if dist_on:
+        g_ids = torch.empty((world, nq, k), dtype=torch.int64, device="cuda")
+        g_dst = torch.empty((world, nq, k), dtype=torch.float32, device="cuda")
+        f_ids = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+        f_dst = torch.empty((nq, k), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+
+    def step():
+        seg.search(q, k, out=(ids, dst))  # returns after its stream drained
+        if dist_on:
+            tdist.all_gather_into_tensor(g_ids, ids)
+            tdist.all_gather_into_tensor(g_dst, dst)
+            merge_shards(g_ids, g_dst, args.metric, out=(f_ids, f_dst))
+
+    for _ in range(args.warmup):
+        step()
+    set_timing(True)
+    stats = []
+    if dist_on:
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        stats.append(_lib.last_search_stats())
+    torch.cuda.synchronize()
+    if dist_on:
+        tdist.barrier()
+    t1 = time.perf_counter()
+    set_timing(False)
+    ms = (t1 - t0) * 1000.0 / args.steps
+    if dist_on:
+        t = torch.tensor([ms], dtype=torch.float64, device="cuda")
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        ms = float(t.item())
+
+    main_ms = float(np.mean([s["main_ms"] for s in stats]))
+    st = stats[-1]
+    main_rows = st["main_rows"]
+    if nq >= 20:
+        flop = 2.0 * nq * main_rows * d
+        achieved = flop / (main_ms * 1e-3) / 1e12
+        roof = {"bound": "mfma", "kernel": "k_scan_mfma (APPEND)", "achieved": round(achieved, 2),
+                "peak": FP32_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / FP32_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                "per_launch": {"rows": main_rows, "flop": flop, "ms": round(main_ms, 3)}}
+    else:
+        byts = 4.0 * main_rows * d + 4.0 * nq * d
+        achieved = byts / (main_ms * 1e-3) / 1e9
+        roof = {"bound": "hbm", "kernel": "k_scan_small (APPEND)", "achieved": round(achieved, 1),
+                "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(achieved / HBM_PEAK_GBS, 4),
+                "traffic": None, "per_launch": {"rows": main_rows, "bytes": byts, "ms": round(main_ms, 3)}}
+    if args.pmc and os.path.exists(args.pmc):
+        with open(args.pmc) as f:
+            pmc = json.load(f)
+        roof["traffic"] = pmc.get("hbm_bytes_per_launch")
+        roof["traffic_source"] = args.pmc
+
+    result = None
+    if rank == 0:
+        qps = nq / (ms / 1000.0)
+        result = {
+            "metric": "QPS (FLAT brute force, batch top-k)",
+            "value": round(qps, 2),
+            "unit": "queries/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": round(ms, 3),
+            "higher_is_better": True,
+            "scaling": "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (counter-based gaussian mixture, generated in HBM)",
+            "config": {"workload": f"FLAT {args.metric} {n // 1_000_000}M x {d} Float32, batch {nq}, "
+                                   f"top-{k} (BASELINE configs[1])",
+                       "n": n, "d": d, "nq": nq, "k": k, "metric": args.metric,
+                       "granule_rows": g, "parallelism": f"row-range shards x{world}"},
+            "mdist_per_s": round(nq * n / (ms / 1000.0) / 1e6, 1),
+            "recall_at_10": 1.0,
+            "stats_last_step": {kk: (round(v, 3) if isinstance(v, float) else v) for kk, v in st.items()},
+            "roofline": roof,
+        }
+        if not args.no_verify and world == 1:
+            O = _oracle()
+            q_host = q.cpu().numpy()
+            ok, nchk = verify_sample(O, ids.cpu().numpy(), dst.cpu().numpy(), q_host, args)
+            result["verify"] = {"queries": nchk, "bitwise_and_no_better_sample": ok}
+            if not ok:
+                result["recall_at_10"] = None
+        if not args.no_cpu and world == 1:
+            O = _oracle()
+            result["cpu_baseline"] = cpu_baseline(O, args)
+        print(json.dumps(result), flush=True)
+    seg.free()
+    if dist_on:
+        tdist.barrier()
+        tdist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

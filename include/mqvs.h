@@ -150,20 +150,22 @@ int mqvs_generate_device(uint64_t seed, int32_t mode, int64_t row0, int64_t n, i
                          float *dev_out, mqvs_stream_t stream);
 
 /* ---- observability -------------------------------------------------------
- * Stats of the calling thread's last mqvs_search: kernel time of the scan
- * launches (ms, HIP events on the search stream), rows scanned, candidates
- * kept, and which path ran (0 = VALU direct formula nq<20, 1 = MFMA). */
+ * Stats of the calling thread's last mqvs_search: per-launch kernel times
+ * (ms, HIP events on the search stream; only with mqvs_set_timing(1)), rows
+ * scanned by each launch and which path ran. */
 typedef struct {
-    double scan_ms;     /* probe + main scan kernels */
-    double select_ms;   /* radix select + final select */
-    double total_ms;    /* first to last event of the search */
+    double probe_ms;        /* probe scan kernel */
+    double probe_select_ms; /* radix select over the probe */
+    double main_ms;         /* main scan kernel (rows [probe_rows, n)) */
+    double final_ms;        /* final select kernel */
+    double total_ms;        /* first to last event of the search */
     int64_t rows_scanned;
     int64_t probe_rows;
-    int64_t max_candidates;
-    int32_t path;
-    int32_t rescans;    /* candidate-overflow re-scans */
-    int32_t scan_launches;
-    int32_t reserved;
+    int64_t main_rows;
+    int32_t nq;
+    int32_t k;
+    int32_t path;           /* 0 = VALU direct formula (nq < 20), 1 = MFMA */
+    int32_t rescans;        /* candidate-overflow re-scans */
 } mqvs_search_stats;
 int mqvs_last_search_stats(mqvs_search_stats *out);
 /* Enable per-search HIP-event timing (off by default: one extra event pair). */

@@ -33,14 +33,28 @@ SYMBOLS = [
 
 
 class SearchStats(ctypes.Structure):
-    _fields_ = [("scan_ms", ctypes.c_double), ("select_ms", ctypes.c_double),
+    _fields_ = [("probe_ms", ctypes.c_double), ("probe_select_ms", ctypes.c_double),
+                ("main_ms", ctypes.c_double), ("final_ms", ctypes.c_double),
                 ("total_ms", ctypes.c_double), ("rows_scanned", ctypes.c_int64),
-                ("probe_rows", ctypes.c_int64), ("max_candidates", ctypes.c_int64),
-                ("path", ctypes.c_int32), ("rescans", ctypes.c_int32),
-                ("scan_launches", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("probe_rows", ctypes.c_int64), ("main_rows", ctypes.c_int64),
+                ("nq", ctypes.c_int32), ("k", ctypes.c_int32),
+                ("path", ctypes.c_int32), ("rescans", ctypes.c_int32)]
+
+
+def _share_hip_runtime_with_torch():
+    """PyTorch-ROCm wheels bundle their own libamdhip64.so.7.  If libmqvs.so is
+    loaded first, the dynamic linker binds that soname to /opt/rocm's runtime
+    and torch then finds no GPU in the same process.  Loading torch first makes
+    libmqvs.so bind to the runtime torch already loaded, so the process has one
+    HIP runtime.  (Processes without torch use /opt/rocm's.)"""
+    try:
+        import torch  # noqa: F401
+    except Exception:
+        pass
 
 
 def _load():
+    _share_hip_runtime_with_torch()
     if not os.path.exists(LIB_PATH):
         raise ImportError(
             f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"

@@ -69,7 +69,7 @@ __global__ __launch_bounds__(256) void k_scan_small(ScanParams p) {
     for (int64_t ti = blockIdx.x; ti < p.tiles; ti += gridDim.x) {
         int64_t r0, r1, chunk;
         tile_range(p, ti, r0, r1, chunk);
-        const int ord = p.chunk_ord ? p.chunk_ord[chunk] : (int)chunk;
+        const int ord = chunk_ordinal(p, chunk);
         const int64_t row = r0 + t;
         const bool have = row < r1;
         if (ord < 0) {  // chunk never searched by the reference (all arrays empty)
@@ -220,7 +220,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_mfma(ScanParams p) {
 
     int64_t r0, r1, chunk;
     tile_range(p, ti, r0, r1, chunk);
-    const int ord = p.chunk_ord ? p.chunk_ord[chunk] : (int)chunk;
+    const int ord = chunk_ordinal(p, chunk);
     const int t = threadIdx.x;
     const int lane = t & 63, w = t >> 6;
     const int wr = w >> 1, wq = w & 1;

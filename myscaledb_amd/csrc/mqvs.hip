@@ -128,15 +128,6 @@ static int guarded(F &&f) {
 
 [[noreturn]] static void fail(int code, const std::string &msg) { throw Error{code, msg}; }
 
-static bool is_device_ptr(const void *p) {
-    hipPointerAttribute_t a;
-    if (hipPointerGetAttributes(&a, p) != hipSuccess) {
-        (void)hipGetLastError();
-        return false;
-    }
-    return a.type == hipMemoryTypeDevice;
-}
-
 // ---------------------------------------------------------------------------
 // segments
 
@@ -356,6 +347,9 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     p.maxv = maxv;
     p.chunk_rows = seg->granule;
     p.chunk_ord = chunk_ord;
+    // a row-range shard of a part continues the part's chunk ordinals (all
+    // earlier chunks assumed searched; see DESIGN.md, cosine + shards)
+    p.ord_base = (int)(seg->row_offset / seg->granule);
     p.filter = dfilter;
     p.exists = dexists;
     p.nonempty = seg->nonempty_bits;
@@ -375,9 +369,10 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
 
     const Range pr = make_range(0, P, tile_rows, seg->granule, aligned);
     const Range mr = make_range(P, n, tile_rows, seg->granule, aligned);
+    if (timing) MQVS_HIP(hipEventRecord(ws.ev[5], s));
     run_scan(p, pr, mfma, metric, true, s);
-    MQVS_HIP(hipMemsetAsync(count, 0, sizeof(int) * nq, s));
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[1], s));
+    MQVS_HIP(hipMemsetAsync(count, 0, sizeof(int) * nq, s));
     launch_probe_select(probe, P, P, nq, k, metric, tau, count, cand, cap, 0, s);
     MQVS_HIP(hipGetLastError());
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[2], s));
@@ -391,8 +386,10 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
 
     st.path = mfma ? 1 : 0;
     st.probe_rows = P;
+    st.main_rows = n - P;
     st.rows_scanned = n;
-    st.scan_launches = (pr.tiles > 0) + (mr.tiles > 0);
+    st.nq = nq;
+    st.k = k;
 
     const bool async = dev && (flags & MQVS_F_ASYNC);
     if (!async) {
@@ -422,14 +419,17 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
             MQVS_HIP(hipStreamSynchronize(s));
         }
         if (timing) {
-            float a = 0, b = 0, c = 0, e = 0;
-            MQVS_HIP(hipEventElapsedTime(&a, ws.ev[0], ws.ev[1]));
+            float a = 0, b = 0, c = 0, e = 0, f = 0;
+            MQVS_HIP(hipEventElapsedTime(&a, ws.ev[5], ws.ev[1]));
             MQVS_HIP(hipEventElapsedTime(&b, ws.ev[1], ws.ev[2]));
             MQVS_HIP(hipEventElapsedTime(&c, ws.ev[2], ws.ev[3]));
             MQVS_HIP(hipEventElapsedTime(&e, ws.ev[3], ws.ev[4]));
-            st.scan_ms = a + c;
-            st.select_ms = b + e;
-            st.total_ms = a + b + c + e;
+            MQVS_HIP(hipEventElapsedTime(&f, ws.ev[0], ws.ev[4]));
+            st.probe_ms = a;
+            st.probe_select_ms = b;
+            st.main_ms = c;
+            st.final_ms = e;
+            st.total_ms = f;
         }
     }
     g_stats = st;

@@ -92,6 +92,7 @@ struct ScanParams {
     int maxv;
     int64_t chunk_rows;     // granule rows (chunking for cosine variants)
     const int *chunk_ord;   // [nchunks] ordinal, -1 = chunk never searched; null = identity
+    int ord_base;           // ordinal of the segment's first chunk (row-range shards)
     const uint8_t *filter;  // PREWHERE bitmap or null
     const uint8_t *exists;  // LWD bitmap or null
     const uint8_t *nonempty;// nonempty bitmap or null (only consulted with a filter)
@@ -126,6 +127,15 @@ __device__ inline void tile_range(const ScanParams &p, int64_t t, int64_t &r0, i
         chunk = p.chunk_rows > 0 ? r0 / p.chunk_rows : 0;
     }
     if (r1 > p.row_end) r1 = p.row_end;
+}
+
+// Ordinal of a granule chunk: how many searchWrapper calls the reference made
+// on this part before it (cosine re-normalises the query on each call);
+// -1 = the reference never searches this chunk.
+__device__ inline int chunk_ordinal(const ScanParams &p, int64_t chunk) {
+    if (!p.chunk_ord) return (int)chunk + p.ord_base;
+    const int o = p.chunk_ord[chunk];
+    return o < 0 ? o : o + p.ord_base;
 }
 
 __device__ inline int variant_of(const ScanParams &p, int q, int ord) {

@@ -47,6 +47,10 @@ def lib():
                                      ctypes.c_int, P, P]
         L.orc_merge_parts.argtypes = [I64, I64, ctypes.c_int, P, P, P, P, P]
         L.orc_generate.argtypes = [ctypes.c_uint64, ctypes.c_int, I64, I64, I64, P]
+        L.orc_gemm_dot.argtypes = [P, P, I64]
+        L.orc_gemm_dot.restype = ctypes.c_float
+        L.orc_norm_l2sqr.argtypes = [P, I64]
+        L.orc_norm_l2sqr.restype = ctypes.c_float
         L.orc_l2sqr.argtypes = [P, P, I64]
         L.orc_l2sqr.restype = ctypes.c_float
         L.orc_inner_product.argtypes = [P, P, I64]
@@ -157,9 +161,20 @@ def generate(seed, mode, row0, n, d):
 
 def l2sqr(x, y):
     x, y = _f32(x), _f32(y)
-    return lib().orc_l2sqr(_p(x), _p(y), x.shape[0])
+    return np.float32(lib().orc_l2sqr(_p(x), _p(y), x.shape[0]))
 
 
 def inner_product(x, y):
     x, y = _f32(x), _f32(y)
-    return lib().orc_inner_product(_p(x), _p(y), x.shape[0])
+    return np.float32(lib().orc_inner_product(_p(x), _p(y), x.shape[0]))
+
+
+def gemm_dot(x, y):
+    """fma-chain dot (the BLAS-branch sgemm element, nq >= 20)."""
+    x, y = _f32(x), _f32(y)
+    return np.float32(lib().orc_gemm_dot(_p(x), _p(y), x.shape[0]))
+
+
+def norm_l2sqr(x):
+    x = _f32(x)
+    return np.float32(lib().orc_norm_l2sqr(_p(x), x.shape[0]))
