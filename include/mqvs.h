@@ -164,12 +164,20 @@ typedef struct {
     int64_t main_rows;
     int32_t nq;
     int32_t k;
-    int32_t path;           /* 0 = VALU direct formula (nq < 20), 1 = MFMA */
-    int32_t rescans;        /* candidate-overflow re-scans */
+    int32_t path;           /* 0 = VALU direct formula (nq < 20), 1 = fp32 MFMA,
+                               2 = bf16 MFMA pre-filter + exact fp32 re-rank */
+    int32_t rescans;        /* candidate-overflow re-scans / fallbacks */
+    int32_t segments;       /* main-scan segments (threshold refinements + 1) */
+    int32_t reserved;
 } mqvs_search_stats;
 int mqvs_last_search_stats(mqvs_search_stats *out);
 /* Enable per-search HIP-event timing (off by default: one extra event pair). */
 int mqvs_set_timing(int enabled);
+/* Batch (nq >= 20) scan: 0 = bf16 MFMA pre-filter with a rigorous error bound
+ * and exact fp32 re-rank of the survivors (default; falls back to 1 when the
+ * bound admits too many rows), 1 = fp32 MFMA over every row.  Both return the
+ * same bits. */
+int mqvs_set_batch_mode(int mode);
 
 #ifdef __cplusplus
 }

@@ -28,7 +28,7 @@ SYMBOLS = [
     "mqvs_thread_release", "mqvs_segment_create", "mqvs_segment_create_device",
     "mqvs_segment_generate", "mqvs_segment_free", "mqvs_segment_info", "mqvs_segment_rows",
     "mqvs_search", "mqvs_knn_raw", "mqvs_rerank", "mqvs_merge_shards", "mqvs_generate_device",
-    "mqvs_last_search_stats", "mqvs_set_timing",
+    "mqvs_last_search_stats", "mqvs_set_timing", "mqvs_set_batch_mode",
 ]
 
 
@@ -38,7 +38,8 @@ class SearchStats(ctypes.Structure):
                 ("total_ms", ctypes.c_double), ("rows_scanned", ctypes.c_int64),
                 ("probe_rows", ctypes.c_int64), ("main_rows", ctypes.c_int64),
                 ("nq", ctypes.c_int32), ("k", ctypes.c_int32),
-                ("path", ctypes.c_int32), ("rescans", ctypes.c_int32)]
+                ("path", ctypes.c_int32), ("rescans", ctypes.c_int32),
+                ("segments", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 def _share_hip_runtime_with_torch():
@@ -81,6 +82,7 @@ def _load():
         "mqvs_generate_device": ([U64, I32, I64, I64, I32, P, P], ctypes.c_int),
         "mqvs_last_search_stats": ([P], ctypes.c_int),
         "mqvs_set_timing": ([ctypes.c_int], ctypes.c_int),
+        "mqvs_set_batch_mode": ([ctypes.c_int], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

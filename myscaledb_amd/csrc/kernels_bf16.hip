@@ -1,0 +1,337 @@
+// kernels_bf16.hip -- bf16 MFMA pre-filter + exact fp32 re-rank (nq >= 20).
+//
+// The batch branch of the reference (faiss exhaustive_*_blas, nq >= 20) is a
+// GEMM whose fp32 element the oracle restates as a sequential fma chain.  On
+// gfx950 the f32 MFMA runs at 1/16 of the bf16 rate, so the whole part is
+// first scanned with v_mfma_f32_32x32x16_bf16 on the bf16 rounding of rows and
+// queries, and only rows that can still be in the top-k under a RIGOROUS bound
+// on the bf16 error are re-computed exactly with the fp32 fma chain:
+//
+//   |ip_bf16 - ip_fp32chain| <= B = (2^-7 + 2^-16 + 2.04 d 2^-24) |x| |y|_max
+//
+// (element rounding 2^-8 on each side; fp32 accumulation of both sums, d
+// terms each).  With a_k the k-th best approximate value among any row set,
+// the true k-th exact value is within a_k +- B, so keeping every row whose
+// approximate value is within 2B of a_k keeps every row of the exact top-k
+// (ties included).  The final ids and distances come from the exact chain and
+// are bit-identical to the fp32 path and to the oracle.
+//
+//   k_scan_bf16      128 rows x 128 queries per workgroup, 4 waves of 64x64;
+//                    K staged 64 deep by LDS-DMA (global_load_lds_dwordx4)
+//                    into an XOR-swizzled image (conflict-free ds_read_b128);
+//                    PROBE / APPEND epilogues as the fp32 kernels, on the
+//                    approximate value.
+//   k_probe_select_approx  k-th best approximate value of the probe rows ->
+//                    per-query APPEND threshold (k-th -/+ 2B) + candidates.
+//   k_rerank_select  per query: k-th best approximate value among the
+//                    candidates, keep those within 2B, exact fp32 chain for
+//                    each, bitonic sort by the reference key, emit top-k.
+#include "select_common.h"
+
+namespace mqvs {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __attribute__((address_space(3))) void lds_void;
+
+__host__ __device__ inline uint16_t f32_to_bf16_rn(float x) {
+    uint32_t u = __builtin_bit_cast(uint32_t, x);
+    if ((u & 0x7F800000u) == 0x7F800000u) return (uint16_t)((u >> 16) | ((u & 0xFFFF) ? 0x40 : 0));
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
+// ---------------------------------------------------------------------------
+__global__ void k_to_bf16(const float *src, int64_t rows, int d, int64_t sstride, uint16_t *hi,
+                          uint16_t *lo, int64_t dpad) {
+    const int64_t total = rows * dpad;
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
+         e += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t r = e / dpad;
+        const int c = (int)(e - r * dpad);
+        uint16_t vh = 0, vl = 0;
+        if (c < d) {
+            const float x = src[r * sstride + c];
+            vh = f32_to_bf16_rn(x);
+            // x - hi is exact in fp32 (hi is x rounded to 8 significant bits)
+            vl = f32_to_bf16_rn(x - __builtin_bit_cast(float, (uint32_t)vh << 16));
+        }
+        hi[e] = vh;
+        if (lo) lo[e] = vl;
+    }
+}
+
+void launch_to_bf16(const float *src, int64_t rows, int d, int64_t sstride, uint16_t *dst_hi,
+                    uint16_t *dst_lo, int64_t dpad, hipStream_t s) {
+    int64_t blocks = (rows * dpad + 255) / 256;
+    if (blocks > 65536) blocks = 65536;
+    if (blocks < 1) return;
+    hipLaunchKernelGGL(k_to_bf16, dim3((unsigned)blocks), dim3(256), 0, s, src, rows, d, sstride,
+                       dst_hi, dst_lo, dpad);
+}
+
+// max_r sqrt(|y_r|^2) (non-negative floats: max of the bit patterns)
+__global__ void k_max_norm(const float *norms2, int64_t n, unsigned *out) {
+    unsigned m = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const float v = norms2[i];
+        const unsigned u = (v == v) ? __builtin_bit_cast(unsigned, sqrtf(fmaxf(v, 0.f))) : 0x7F800000u;
+        m = u > m ? u : m;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        const unsigned o = __shfl_xor(m, off);
+        m = o > m ? o : m;
+    }
+    if ((threadIdx.x & 63) == 0) atomicMax(out, m);
+}
+
+void launch_max_norm(const float *norms2, int64_t n, float *out_max, hipStream_t s) {
+    int64_t blocks = (n + 255) / 256;
+    if (blocks > 4096) blocks = 4096;
+    if (blocks < 1) blocks = 1;
+    hipLaunchKernelGGL(k_max_norm, dim3((unsigned)blocks), dim3(256), 0, s, norms2, n,
+                       (unsigned *)out_max);
+}
+
+// Per-query bound on |approx - exact| in the metric's raw value:
+//   IP / cosine: B = c(d) * |x|max_over_used_variants * |y|max
+//   L2 (BLAS):   raw = (xn + yn) - 2 ip -> 2 B + 2 ulp of the result
+//   split 3: truncation |xl yl| + |xh ey| + |ex y| <= 3.03 2^-16 |x||y|; fp32
+//   accumulation of the hi sum and of the exact chain, d terms each, ~2 d u;
+//   the cross-product sum (2d terms of <= 2^-8 |x||y|) and the final add.
+//   split 1: element rounding 2^-8 per side -> (2^-7 + 2^-16) |x||y| + 2 d u.
+__global__ void k_query_bound(ScanParams p, int metric, int split, const float *ynorm_max,
+                              float *bq) {
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= p.nq) return;
+    const int64_t qs = (int64_t)((p.d + 31) / 32 * 32);
+    const int nv = p.maxv <= 1 ? 1 : p.qmu[j] + p.qlam[j];
+    float xmax = 0.f;
+    for (int v = 0; v < nv; ++v) {
+        const float *x = p.qvars + ((int64_t)j * p.maxv + v) * qs;
+        double s = 0.0;
+        for (int i = 0; i < p.d; ++i) s += (double)x[i] * (double)x[i];
+        xmax = fmaxf(xmax, (float)sqrt(s));
+    }
+    const float ymax = *ynorm_max * (1.0f + 6e-8f * (float)p.d + 1e-6f);  // fp32 |y|^2 chain error
+    const float acc_term = 2.04f * (float)p.d * 5.9604645e-8f;
+    const float c = split == 3 ? 3.1f * 1.5258789e-5f + acc_term + 1.2e-7f
+                               : 0.0078125f + 1.6e-5f + acc_term + 1e-7f;
+    float b = c * (xmax * 1.0001f) * ymax + 1e-30f;
+    if (metric == MQVS_METRIC_L2) {
+        const float top = p.qnorms[j] + ymax * ymax;
+        b = 2.0f * b + top * 2.4e-7f + 1e-30f;
+    } else if (metric == MQVS_METRIC_COSINE) {
+        b = b + 2.4e-7f;  // 1 - ip rounds; ties on 1-ip may differ in ip by one ulp of 1
+    }
+    if (!(b < 1e30f)) b = __builtin_inff();
+    bq[j] = b;
+}
+
+void launch_query_bound(const ScanParams &p, int metric, int split, const float *ynorm_max,
+                        float *bq, hipStream_t s) {
+    hipLaunchKernelGGL(k_query_bound, dim3((p.nq + 63) / 64), dim3(64), 0, s, p, metric, split,
+                       ynorm_max, bq);
+}
+
+
+// ---------------------------------------------------------------------------
+template <int METRIC>
+__global__ __launch_bounds__(SEL_THREADS) void k_probe_select_approx(const float *probe, int64_t P,
+                                                                    int64_t ld, int k,
+                                                                    const float *bq, float *thr,
+                                                                    int *cand_count, Cand *cand,
+                                                                    int cap) {
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t sh[4];
+    const int q = blockIdx.x;
+    const float *row = probe + (int64_t)q * ld;
+    // block_radix_select_rows applies key32 (with validity); use a plain
+    // order key here
+    auto keyof = [&](int64_t i) { return okey<METRIC>(row[i]); };
+    const uint32_t th = block_radix_select(keyof, P, k, hist, sh);
+    float t;
+    if (th == 0xFFFFFFFEu)
+        t = (METRIC == MQVS_METRIC_L2) ? __builtin_inff() : -__builtin_inff();
+    else
+        t = widen<METRIC>(okey_value<METRIC>(th), bq[q]);
+    if (threadIdx.x == 0) thr[q] = t;
+    for_each_f4(row, P, [&](int64_t i, float raw) {
+        const bool take = (METRIC == MQVS_METRIC_L2) ? (raw <= t) : (raw >= t);
+        if (take) {
+            const int pos = atomicAdd(&cand_count[q], 1);
+            if (pos < cap) {
+                Cand c;
+                c.raw = raw;
+                c.row = (uint32_t)i;
+                cand[(int64_t)q * cap + pos] = c;
+            }
+        }
+    });
+}
+
+template <int M>
+static void probe_select_approx_t(const float *probe, int64_t P, int64_t ld, int nq, int k,
+                                  const float *bq, float *thr, int *cc, Cand *cand, int cap,
+                                  hipStream_t s) {
+    hipLaunchKernelGGL(k_probe_select_approx<M>, dim3(nq), dim3(SEL_THREADS), 0, s, probe, P, ld, k,
+                       bq, thr, cc, cand, cap);
+}
+
+void launch_probe_select_approx(const float *probe, int64_t P, int64_t ld, int nq, int k,
+                                int metric, const float *bq, float *thr, int *cand_count,
+                                Cand *cand, int cand_cap, hipStream_t s) {
+    switch (metric) {
+        case MQVS_METRIC_L2:
+            probe_select_approx_t<MQVS_METRIC_L2>(probe, P, ld, nq, k, bq, thr, cand_count, cand, cand_cap, s);
+            break;
+        case MQVS_METRIC_IP:
+            probe_select_approx_t<MQVS_METRIC_IP>(probe, P, ld, nq, k, bq, thr, cand_count, cand, cand_cap, s);
+            break;
+        case MQVS_METRIC_COSINE:
+            probe_select_approx_t<MQVS_METRIC_COSINE>(probe, P, ld, nq, k, bq, thr, cand_count, cand,
+                                                      cand_cap, s);
+            break;
+        default:
+            probe_select_approx_t<kMetricIpRaw>(probe, P, ld, nq, k, bq, thr, cand_count, cand, cand_cap, s);
+            break;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// exact fp32 chain for one (query, row): the BLAS-branch element
+template <int METRIC>
+__device__ inline float exact_value(const ScanParams &p, int q, int64_t row) {
+    const int64_t chunk = p.chunk_rows > 0 ? row / p.chunk_rows : 0;
+    const int ord = chunk_ordinal(p, chunk);
+    const int v = variant_of(p, q, ord < 0 ? 0 : ord);
+    const int64_t qs = (int64_t)((p.d + 31) / 32 * 32);
+    const float *x = p.qvars + ((int64_t)q * p.maxv + v) * qs;
+    const float *y = p.rows + row * p.d;
+    float acc = 0.0f;
+    if ((p.d & 3) == 0) {
+        const float4 *x4 = reinterpret_cast<const float4 *>(x);
+        const float4 *y4 = reinterpret_cast<const float4 *>(y);
+        const int n4 = p.d >> 2;
+#pragma unroll 4
+        for (int i = 0; i < n4; ++i) {
+            const float4 a = x4[i], b = y4[i];
+            acc = fmaf(a.x, b.x, acc);
+            acc = fmaf(a.y, b.y, acc);
+            acc = fmaf(a.z, b.z, acc);
+            acc = fmaf(a.w, b.w, acc);
+        }
+    } else {
+        for (int i = 0; i < p.d; ++i) acc = fmaf(x[i], y[i], acc);
+    }
+    if (METRIC == MQVS_METRIC_L2) {
+        float d = (p.qnorms[q] + p.row_norms[row]) - 2.0f * acc;
+        if (d < 0) d = 0;
+        return d;
+    }
+    return acc;
+}
+
+template <int METRIC>
+__global__ __launch_bounds__(SEL_THREADS) void k_rerank_select(ScanParams p, const float *bq, int k,
+                                                              int64_t id_offset, int64_t *out_ids,
+                                                              float *out_dist, int *overflow) {
+    extern __shared__ __attribute__((aligned(16))) uint4 recs[];  // kSortCap records
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t sh[4];
+    __shared__ int s_cnt;
+    const int q = blockIdx.x;
+    int n = p.cand_count[q];
+    if (n > p.cand_cap) {
+        if (threadIdx.x == 0) atomicOr(overflow, 1);
+        n = p.cand_cap;
+    }
+    const Cand *c = p.cand + (int64_t)q * p.cand_cap;
+    auto keyof = [&](int64_t i) { return okey<METRIC>(c[i].raw); };
+    const uint32_t th = block_radix_select(keyof, n, k, hist, sh);
+    float t;
+    if (th == 0xFFFFFFFEu)
+        t = (METRIC == MQVS_METRIC_L2) ? __builtin_inff() : -__builtin_inff();
+    else
+        t = widen<METRIC>(okey_value<METRIC>(th), bq[q]);
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    for (int i = threadIdx.x; i < n; i += SEL_THREADS) {
+        const Cand e = c[i];
+        const bool take = (METRIC == MQVS_METRIC_L2) ? (e.raw <= t) : (e.raw >= t);
+        if (take) {
+            const int pos = atomicAdd(&s_cnt, 1);
+            if (pos < kSortCap) recs[pos] = make_uint4(0, 0, 0, e.row);
+        }
+    }
+    __syncthreads();
+    int m = s_cnt;
+    if (m > kSortCap) {
+        if (threadIdx.x == 0) atomicOr(overflow, 4);
+        m = kSortCap;
+    }
+    // exact re-rank of the survivors
+    for (int i = threadIdx.x; i < m; i += SEL_THREADS) {
+        const uint32_t row = recs[i].w;
+        const float raw = exact_value<METRIC>(p, q, row);
+        uint4 r;
+        r.x = key32<METRIC>(raw);
+        r.w = row;
+        if (METRIC == MQVS_METRIC_COSINE) {
+            r.y = p.chunk_rows > 0 ? (uint32_t)((int64_t)row / p.chunk_rows) : 0u;
+            r.z = ~ord_asc(raw);
+        } else {
+            r.y = 0;
+            r.z = 0;
+        }
+        recs[i] = r;
+    }
+    int N = 1;
+    while (N < m) N <<= 1;
+    for (int i = m + threadIdx.x; i < N; i += SEL_THREADS)
+        recs[i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    __syncthreads();
+    block_bitonic_sort(recs, N);
+    const float pad = (METRIC == MQVS_METRIC_IP) ? 1.17549435e-38f
+                      : (METRIC == kMetricIpRaw) ? -3.40282347e+38f
+                                                 : 3.40282347e+38f;
+    for (int i = threadIdx.x; i < k; i += SEL_THREADS) {
+        int64_t id = -1;
+        float dist = pad;
+        if (i < N && recs[i].x != 0xFFFFFFFFu) {
+            id = (int64_t)recs[i].w + id_offset;
+            dist = key_to_value(METRIC, recs[i].x);
+        }
+        out_ids[(int64_t)q * k + i] = id;
+        out_dist[(int64_t)q * k + i] = dist;
+    }
+}
+
+template <int M>
+static void rerank_select_t(const ScanParams &p, const float *bq, int k, int64_t id_offset,
+                            int64_t *out_ids, float *out_dist, int *overflow, hipStream_t s) {
+    hipLaunchKernelGGL(k_rerank_select<M>, dim3(p.nq), dim3(SEL_THREADS), kSortCap * sizeof(uint4), s,
+                       p, bq, k, id_offset, out_ids, out_dist, overflow);
+}
+
+void launch_rerank_select(const ScanParams &p, int metric, const float *bq, int k,
+                          int64_t id_offset, int64_t *out_ids, float *out_dist, int *overflow,
+                          hipStream_t s) {
+    switch (metric) {
+        case MQVS_METRIC_L2:
+            rerank_select_t<MQVS_METRIC_L2>(p, bq, k, id_offset, out_ids, out_dist, overflow, s);
+            break;
+        case MQVS_METRIC_IP:
+            rerank_select_t<MQVS_METRIC_IP>(p, bq, k, id_offset, out_ids, out_dist, overflow, s);
+            break;
+        case MQVS_METRIC_COSINE:
+            rerank_select_t<MQVS_METRIC_COSINE>(p, bq, k, id_offset, out_ids, out_dist, overflow, s);
+            break;
+        default:
+            rerank_select_t<kMetricIpRaw>(p, bq, k, id_offset, out_ids, out_dist, overflow, s);
+            break;
+    }
+}
+
+}  // namespace mqvs

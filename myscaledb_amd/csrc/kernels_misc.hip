@@ -92,60 +92,84 @@ void launch_normalize_rows(float *rows, int64_t n, int d, hipStream_t s) {
 // dataset shared across chunks, MergeTreeVSManager.cpp:1279-1292,1473-1486),
 // so chunk ordinal c uses normalize^(c+1)(q).  Variants are generated until a
 // repeat: variants [0, mu) are the transient, [mu, mu+lam) the cycle.
-__global__ void k_query_prep(const float *q, int nq, int d, int metric, int blas, float *qvars,
+__global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d, int metric, int blas, float *qvars,
                              int maxv, float *qnorms, int *qmu, int *qlam, int *status) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= nq) return;
+    // one wave per query; lane l owns elements l, l+64, ... (same lane writes
+    // and later re-reads them, so the variant comparison needs no fence)
+    extern __shared__ __attribute__((aligned(16))) float qbuf[];
+    const int j = blockIdx.x;
+    const int lane = threadIdx.x;
     const int64_t qs = (int64_t)((d + 31) / 32 * 32);
     const float *src = q + (int64_t)j * d;
     float *v0 = qvars + (int64_t)j * maxv * qs;
-    if (metric != MQVS_METRIC_COSINE) {
-        float sum = 0.0f;
-        for (int i = 0; i < d; ++i) {
-            v0[i] = src[i];
-            sum = sum + src[i] * src[i];
+    for (int i = lane; i < d; i += 64) qbuf[i] = src[i];
+    __syncthreads();
+    // sequential fp32 sum of squares (product rounded, then added), lane 0
+    auto seqsum = [&]() -> float {
+        if (lane == 0) {
+            float s = 0.0f;
+#pragma unroll 8
+            for (int i = 0; i < d; ++i) s = s + qbuf[i] * qbuf[i];
+            qbuf[qs] = s;
         }
-        if (qnorms) qnorms[j] = blas ? sum : 0.0f;
-        qmu[j] = 0;
-        qlam[j] = 1;
+        __syncthreads();
+        const float r = qbuf[qs];
+        __syncthreads();
+        return r;
+    };
+    if (metric != MQVS_METRIC_COSINE) {
+        for (int i = lane; i < d; i += 64) v0[i] = qbuf[i];
+        const float sum = blas ? seqsum() : 0.0f;
+        if (lane == 0) {
+            if (qnorms) qnorms[j] = sum;
+            qmu[j] = 0;
+            qlam[j] = 1;
+        }
         return;
     }
     const float eps = 1.1920929e-07f;
-    const float *prev = src;
     for (int v = 0; v < maxv; ++v) {
         float *cur = v0 + (int64_t)v * qs;
-        float sum = 0.0f;
-        for (int i = 0; i < d; ++i) sum = sum + prev[i] * prev[i];
+        const float sum = seqsum();
         if (sum < eps) {
-            for (int i = 0; i < d; ++i) cur[i] = prev[i];
+            for (int i = lane; i < d; i += 64) cur[i] = qbuf[i];
         } else {
             const float s = sqrtf(sum);
-            for (int i = 0; i < d; ++i) cur[i] = prev[i] / s;
+            for (int i = lane; i < d; i += 64) {
+                const float x = qbuf[i] / s;
+                cur[i] = x;
+                qbuf[i] = x;
+            }
         }
+        __syncthreads();
         for (int u = 0; u < v; ++u) {
             const float *o = v0 + (int64_t)u * qs;
             bool eq = true;
-            for (int i = 0; i < d && eq; ++i)
-                eq = __builtin_bit_cast(uint32_t, o[i]) == __builtin_bit_cast(uint32_t, cur[i]);
-            if (eq) {
-                qmu[j] = u;
-                qlam[j] = v - u;
-                if (qnorms) qnorms[j] = 0.0f;
+            for (int i = lane; i < d; i += 64)
+                eq = eq && __builtin_bit_cast(uint32_t, o[i]) == __builtin_bit_cast(uint32_t, qbuf[i]);
+            if (__all(eq)) {
+                if (lane == 0) {
+                    qmu[j] = u;
+                    qlam[j] = v - u;
+                    if (qnorms) qnorms[j] = 0.0f;
+                }
                 return;
             }
         }
-        prev = cur;
     }
-    atomicOr(status, 1);  // no repeat within maxv normalisations
-    qmu[j] = 0;
-    qlam[j] = 1;
+    if (lane == 0) {
+        atomicOr(status, 1);  // no repeat within maxv normalisations
+        qmu[j] = 0;
+        qlam[j] = 1;
+    }
 }
 
 void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, float *qvars,
                        float *qnorms, int *qmu, int *qlam, int *status, hipStream_t s) {
     const int maxv = metric == MQVS_METRIC_COSINE ? kMaxVariants : 1;
-    hipLaunchKernelGGL(k_query_prep, dim3((nq + 63) / 64), dim3(64), 0, s, q, nq, d, metric,
-                       blas ? 1 : 0, qvars, maxv, qnorms, qmu, qlam, status);
+    const size_t lds = (size_t)((d + 31) / 32 * 32 + 4) * sizeof(float);
+    hipLaunchKernelGGL(k_query_prep, dim3(nq), dim3(64), lds, s, q, nq, d, metric, blas ? 1 : 0,
+                       qvars, maxv, qnorms, qmu, qlam, status);
 }
 
 // Counter-based synthetic generator; bit-identical to oracle/mqvs_oracle.c

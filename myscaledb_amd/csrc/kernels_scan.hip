@@ -32,6 +32,35 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 
 static __device__ inline float nan_f() { return __builtin_nanf(""); }
 
+// Wave-aggregated append: every lane of the wave calls this for the same
+// query j (VALU kernel); one atomic per wave instead of one per row.
+template <int METRIC, bool PROBE>
+__device__ inline void emit_wave(const ScanParams &p, int j, int64_t row, bool have, bool valid,
+                                 float raw) {
+    if (PROBE) {
+        if (have) p.probe[(int64_t)j * p.probe_ld + (row - p.row_begin)] = valid ? raw : __builtin_nanf("");
+        return;
+    }
+    const uint32_t key = key32<METRIC>(raw);
+    const bool take = have && valid && key != 0xFFFFFFFFu && key <= p.tau[j];
+    const unsigned long long m = __ballot(take);
+    if (m == 0) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((long long)m) - 1;
+    int base = 0;
+    if (lane == leader) base = atomicAdd(&p.cand_count[j], __popcll(m));
+    base = __shfl(base, leader);
+    if (take) {
+        const int pos = base + __popcll(m & ((1ull << lane) - 1ull));
+        if (pos < p.cand_cap) {
+            Cand c;
+            c.raw = raw;
+            c.row = (uint32_t)row;
+            p.cand[(int64_t)j * p.cand_cap + pos] = c;
+        }
+    }
+}
+
 template <int METRIC, bool PROBE>
 __device__ inline void emit(const ScanParams &p, int j, int64_t row, bool valid, float raw) {
     if (PROBE) {
@@ -69,6 +98,7 @@ __global__ __launch_bounds__(256) void k_scan_small(ScanParams p) {
     for (int64_t ti = blockIdx.x; ti < p.tiles; ti += gridDim.x) {
         int64_t r0, r1, chunk;
         tile_range(p, ti, r0, r1, chunk);
+        if (r0 >= r1) continue;  // tile past the end of a partial last granule (block-uniform)
         const int ord = chunk_ordinal(p, chunk);
         const int64_t row = r0 + t;
         const bool have = row < r1;
@@ -148,11 +178,11 @@ __global__ __launch_bounds__(256) void k_scan_small(ScanParams p) {
             if (s + 1 < nst) store((s + 1) & 1);
             __syncthreads();
         }
-        if (have) {
-            const bool valid = row_valid(p, row);
+        {
+            const bool valid = have && row_valid(p, row);
 #pragma unroll
             for (int j = 0; j < NQ; ++j)
-                if (j < p.nq) emit<METRIC, PROBE>(p, j, row, valid, acc[j]);
+                if (j < p.nq) emit_wave<METRIC, PROBE>(p, j, row, have, valid, acc[j]);
         }
     }
 }
@@ -220,6 +250,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_mfma(ScanParams p) {
 
     int64_t r0, r1, chunk;
     tile_range(p, ti, r0, r1, chunk);
+    if (r0 >= r1) return;  // tile past the end of a partial last granule
     const int ord = chunk_ordinal(p, chunk);
     const int t = threadIdx.x;
     const int lane = t & 63, w = t >> 6;

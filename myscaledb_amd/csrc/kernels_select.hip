@@ -12,85 +12,12 @@
 //   k_final_select  bitonic sort of the candidates in LDS by the full key
 //                   (L2/IP: key, row; cosine: 1-ip, chunk, ip desc, row) and
 //                   emit the first k in the reference's output layout.
-#include "mqvs_internal.h"
+
+#include "select_common.h"
 
 namespace mqvs {
 
-constexpr int SEL_THREADS = 256;
 
-// Histogram update with run-length aggregation: a thread keeps a running
-// (bucket, count) pair and only flushes to LDS when the bucket changes, which
-// removes the LDS-atomic pile-up on the few buckets that the high digits of
-// clustered float keys fall into.
-struct RunHist {
-    uint32_t cur = 0xFFFFFFFFu, cnt = 0;
-    __device__ void add(uint32_t *hist, uint32_t b) {
-        if (b == cur) {
-            ++cnt;
-        } else {
-            if (cnt) atomicAdd(&hist[cur], cnt);
-            cur = b;
-            cnt = 1;
-        }
-    }
-    __device__ void flush(uint32_t *hist) {
-        if (cnt) atomicAdd(&hist[cur], cnt);
-        cnt = 0;
-        cur = 0xFFFFFFFFu;
-    }
-};
-
-// k-th smallest valid key (1-based rank k) among `count` values produced by
-// load(i); 0xFFFFFFFE when fewer than k values are valid.  Block-wide.
-template <typename KeyFn>
-__device__ uint32_t block_radix_select(KeyFn keyof, int64_t count, int k, uint32_t *hist,
-                                       uint32_t *sh) {
-    const int t = threadIdx.x;
-    uint32_t prefix = 0, mask = 0, kk = (uint32_t)k;
-    for (int pass = 0; pass < 4; ++pass) {
-        const int shift = 24 - 8 * pass;
-        for (int i = t; i < 256; i += SEL_THREADS) hist[i] = 0;
-        __syncthreads();
-        RunHist rh;
-        for (int64_t i = t; i < count; i += SEL_THREADS) {
-            const uint32_t key = keyof(i);
-            if (key == 0xFFFFFFFFu) continue;
-            if ((key & mask) != prefix) continue;
-            rh.add(hist, (key >> shift) & 255u);
-        }
-        rh.flush(hist);
-        __syncthreads();
-        if (t == 0) {
-            uint32_t total = 0;
-            for (int b = 0; b < 256; ++b) total += hist[b];
-            uint32_t done = 0, cum = 0, bsel = 0;
-            if (pass == 0 && total < kk) {
-                done = 1;  // fewer than k valid: every valid value qualifies
-            } else {
-                for (int b = 0; b < 256; ++b) {
-                    if (cum + hist[b] >= kk) {
-                        bsel = (uint32_t)b;
-                        break;
-                    }
-                    cum += hist[b];
-                }
-            }
-            sh[0] = done;
-            sh[1] = bsel;
-            sh[2] = cum;
-        }
-        __syncthreads();
-        if (sh[0]) {
-            __syncthreads();
-            return 0xFFFFFFFEu;
-        }
-        prefix |= sh[1] << shift;
-        mask |= 255u << shift;
-        kk -= sh[2];
-        __syncthreads();
-    }
-    return prefix;
-}
 
 template <int METRIC>
 __global__ __launch_bounds__(SEL_THREADS) void k_probe_select(const float *probe, int64_t P,
@@ -101,11 +28,9 @@ __global__ __launch_bounds__(SEL_THREADS) void k_probe_select(const float *probe
     __shared__ uint32_t sh[4];
     const int q = blockIdx.x;
     const float *row = probe + (int64_t)q * ld;
-    auto keyof = [&](int64_t i) { return key32<METRIC>(row[i]); };
-    const uint32_t th = block_radix_select(keyof, P, k, hist, sh);
+    const uint32_t th = block_radix_select_rows<METRIC>(row, P, k, hist, sh);
     if (threadIdx.x == 0) tau[q] = th;
-    for (int64_t i = threadIdx.x; i < P; i += SEL_THREADS) {
-        const float raw = row[i];
+    for_each_f4(row, P, [&](int64_t i, float raw) {
         const uint32_t key = key32<METRIC>(raw);
         if (key != 0xFFFFFFFFu && key <= th) {
             const int pos = atomicAdd(&cand_count[q], 1);
@@ -116,7 +41,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_probe_select(const float *probe
                 cand[(int64_t)q * cap + pos] = c;
             }
         }
-    }
+    });
 }
 
 // Tighten tau for queries whose candidate list overflowed: the k-th key among
@@ -134,40 +59,6 @@ __global__ __launch_bounds__(SEL_THREADS) void k_cand_tau(const Cand *cand, cons
     if (threadIdx.x == 0 && th < tau[q]) tau[q] = th;
 }
 
-// ---------------------------------------------------------------------------
-// Bitonic sort of up to kSortCap 16-byte records in LDS, lexicographic on
-// (x, y, z, w) ascending.
-__device__ inline bool rec_less(const uint4 &a, const uint4 &b) {
-    if (a.x != b.x) return a.x < b.x;
-    if (a.y != b.y) return a.y < b.y;
-    if (a.z != b.z) return a.z < b.z;
-    return a.w < b.w;
-}
-
-__device__ void block_bitonic_sort(uint4 *recs, int N) {
-    for (int size = 2; size <= N; size <<= 1) {
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-            for (int i = threadIdx.x; i < (N >> 1); i += SEL_THREADS) {
-                const int lo = 2 * stride * (i / stride) + (i % stride);
-                const int hi = lo + stride;
-                const bool up = (lo & size) == 0;
-                uint4 a = recs[lo], b = recs[hi];
-                if (rec_less(b, a) == up) {
-                    recs[lo] = b;
-                    recs[hi] = a;
-                }
-            }
-            __syncthreads();
-        }
-    }
-}
-
-__device__ inline float key_to_value(int metric, uint32_t k1) {
-    // inverse of ord_asc / ~ord_asc
-    uint32_t u = (metric == MQVS_METRIC_IP || metric == kMetricIpRaw) ? ~k1 : k1;
-    u = (u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u;
-    return __builtin_bit_cast(float, u);
-}
 
 template <int METRIC>
 __global__ __launch_bounds__(SEL_THREADS) void k_final_select(const Cand *cand,
@@ -175,35 +66,61 @@ __global__ __launch_bounds__(SEL_THREADS) void k_final_select(const Cand *cand,
                                                              int k, int64_t chunk_rows,
                                                              int64_t id_offset, int64_t *out_ids,
                                                              float *out_dist, int *overflow) {
-    extern __shared__ __attribute__((aligned(16))) uint4 recs[];
+    extern __shared__ __attribute__((aligned(16))) uint4 recs[];  // kSortCap records
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t sh[4];
+    __shared__ int s_cnt;
     const int q = blockIdx.x;
     int n = cand_count[q];
     if (n > cap) {
         if (threadIdx.x == 0) atomicOr(overflow, 1);
         n = cap;
     }
-    int N = 1;
-    while (N < n) N <<= 1;
     const Cand *c = cand + (int64_t)q * cap;
-    for (int i = threadIdx.x; i < N; i += SEL_THREADS) {
-        uint4 r = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-        if (i < n) {
+    auto make_rec = [&](const Cand &e) {
+        uint4 r;
+        r.x = key32<METRIC>(e.raw);
+        r.w = e.row;
+        if (METRIC == MQVS_METRIC_COSINE) {
+            // ties on 1-ip: earlier granule chunk first (merge keeps `final`
+            // on equality), then ip descending within a chunk (faiss IP
+            // order), then row (MergeTreeVSManager.cpp:1653-1679)
+            r.y = chunk_rows > 0 ? (uint32_t)((int64_t)e.row / chunk_rows) : 0u;
+            r.z = ~ord_asc(e.raw);
+        } else {
+            r.y = 0;
+            r.z = 0;
+        }
+        return r;
+    };
+    int m = n;
+    if (n <= kSortCap) {
+        for (int i = threadIdx.x; i < n; i += SEL_THREADS) recs[i] = make_rec(c[i]);
+    } else {
+        // long list: k-th primary key first, then sort only key <= it (k + ties)
+        auto keyof = [&](int64_t i) { return key32<METRIC>(c[i].raw); };
+        const uint32_t th = block_radix_select(keyof, n, k, hist, sh);
+        if (threadIdx.x == 0) s_cnt = 0;
+        __syncthreads();
+        for (int i = threadIdx.x; i < n; i += SEL_THREADS) {
             const Cand e = c[i];
-            r.x = key32<METRIC>(e.raw);
-            r.w = e.row;
-            if (METRIC == MQVS_METRIC_COSINE) {
-                // ties on 1-ip: earlier granule chunk first (merge keeps
-                // `final` on equality), then ip descending within a chunk
-                // (faiss IP order), then row (MergeTreeVSManager.cpp:1653-1679)
-                r.y = chunk_rows > 0 ? (uint32_t)((int64_t)e.row / chunk_rows) : 0u;
-                r.z = ~ord_asc(e.raw);
-            } else {
-                r.y = 0;
-                r.z = 0;
+            const uint32_t key = key32<METRIC>(e.raw);
+            if (key != 0xFFFFFFFFu && key <= th) {
+                const int pos = atomicAdd(&s_cnt, 1);
+                if (pos < kSortCap) recs[pos] = make_rec(e);
             }
         }
-        recs[i] = r;
+        __syncthreads();
+        m = s_cnt;
+        if (m > kSortCap) {  // more than kSortCap rows tie at the k-th key
+            if (threadIdx.x == 0) atomicOr(overflow, 2);
+            m = kSortCap;
+        }
     }
+    int N = 1;
+    while (N < m) N <<= 1;
+    for (int i = m + threadIdx.x; i < N; i += SEL_THREADS)
+        recs[i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
     __syncthreads();
     block_bitonic_sort(recs, N);
     const float pad = (METRIC == MQVS_METRIC_IP) ? 1.17549435e-38f
@@ -312,7 +229,7 @@ template <int M>
 static void final_select_t(const Cand *cand, const int *cc, int cap, int nq, int k,
                            int64_t chunk_rows, int64_t id_offset, int64_t *out_ids,
                            float *out_dist, int *overflow, hipStream_t s) {
-    hipLaunchKernelGGL(k_final_select<M>, dim3(nq), dim3(SEL_THREADS), sort_lds(cap), s, cand, cc,
+    hipLaunchKernelGGL(k_final_select<M>, dim3(nq), dim3(SEL_THREADS), sort_lds(kSortCap), s, cand, cc,
                        cap, k, chunk_rows, id_offset, out_ids, out_dist, overflow);
 }
 
@@ -336,6 +253,86 @@ void launch_merge_shards(int nshards, int nq, int k, int metric, const int64_t *
     if (nq <= 0) return;
     MQVS_DISPATCH_METRIC(metric, merge_shards_t,
                          (nshards, nq, k, in_ids, in_dist, out_ids, out_dist, s));
+}
+
+// ---------------------------------------------------------------------------
+// Between scan segments: tighten the per-query threshold from the candidates
+// collected so far and compact the list into the other buffer.
+//   exact (APPROX = false): tau = min(tau, k-th key32 of the candidates)
+//   approx (bf16):          thr = tighter(thr, widen(k-th approximate value))
+// Every row of the exact top-k seen so far passes the new threshold (same
+// argument as the probe threshold), so nothing the final select needs is lost.
+template <int METRIC, bool APPROX>
+__global__ __launch_bounds__(SEL_THREADS) void k_refine(const Cand *cin, const int *cnt_in, int cap,
+                                                       int k, const float *bq, uint32_t *tau,
+                                                       float *thr, Cand *cout, int *cnt_out) {
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t sh[4];
+    __shared__ int s_cnt;
+    const int q = blockIdx.x;
+    int n = cnt_in[q];
+    if (n > cap) n = cap;  // overflowed lists keep their overflow: count stays > cap
+    const Cand *c = cin + (int64_t)q * cap;
+    uint32_t tk = 0;
+    float tf = 0.f;
+    if (APPROX) {
+        auto keyof = [&](int64_t i) { return okey<METRIC>(c[i].raw); };
+        const uint32_t th = block_radix_select(keyof, n, k, hist, sh);
+        tf = thr[q];
+        if (th != 0xFFFFFFFEu) {
+            const float w = widen<METRIC>(okey_value<METRIC>(th), bq[q]);
+            tf = (METRIC == MQVS_METRIC_L2) ? fminf(tf, w) : fmaxf(tf, w);
+        }
+    } else {
+        auto keyof = [&](int64_t i) { return key32<METRIC>(c[i].raw); };
+        const uint32_t th = block_radix_select(keyof, n, k, hist, sh);
+        tk = tau[q];
+        if (th < tk) tk = th;
+    }
+    if (threadIdx.x == 0) s_cnt = 0;
+    __syncthreads();
+    Cand *o = cout + (int64_t)q * cap;
+    for (int i = threadIdx.x; i < n; i += SEL_THREADS) {
+        const Cand e = c[i];
+        bool take;
+        if (APPROX) {
+            take = (METRIC == MQVS_METRIC_L2) ? (e.raw <= tf) : (e.raw >= tf);
+        } else {
+            const uint32_t key = key32<METRIC>(e.raw);
+            take = key != 0xFFFFFFFFu && key <= tk;
+        }
+        if (take) o[atomicAdd(&s_cnt, 1)] = e;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        // an overflowed input stays flagged as overflowed (its lost rows are unknown)
+        cnt_out[q] = cnt_in[q] > cap ? cnt_in[q] : s_cnt;
+        if (APPROX) thr[q] = tf;
+        else tau[q] = tk;
+    }
+}
+
+template <int M, bool A>
+static void refine_t(const Cand *cin, const int *cnt_in, int cap, int nq, int k, const float *bq,
+                     uint32_t *tau, float *thr, Cand *cout, int *cnt_out, hipStream_t s) {
+    hipLaunchKernelGGL((k_refine<M, A>), dim3(nq), dim3(SEL_THREADS), 0, s, cin, cnt_in, cap, k, bq, tau,
+                       thr, cout, cnt_out);
+}
+
+void launch_refine(const Cand *cin, const int *cnt_in, int cap, int nq, int k, int metric,
+                   bool approx, const float *bq, uint32_t *tau, float *thr, Cand *cout, int *cnt_out,
+                   hipStream_t s) {
+    if (nq <= 0) return;
+#define MQVS_REFINE(M)                                                                      \
+    (approx ? refine_t<M, true>(cin, cnt_in, cap, nq, k, bq, tau, thr, cout, cnt_out, s)   \
+            : refine_t<M, false>(cin, cnt_in, cap, nq, k, bq, tau, thr, cout, cnt_out, s))
+    switch (metric) {
+        case MQVS_METRIC_L2: MQVS_REFINE(MQVS_METRIC_L2); break;
+        case MQVS_METRIC_IP: MQVS_REFINE(MQVS_METRIC_IP); break;
+        case MQVS_METRIC_COSINE: MQVS_REFINE(MQVS_METRIC_COSINE); break;
+        default: MQVS_REFINE(kMetricIpRaw); break;
+    }
+#undef MQVS_REFINE
 }
 
 }  // namespace mqvs

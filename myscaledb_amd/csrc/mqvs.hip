@@ -28,7 +28,12 @@ struct mqvs_segment {
     int64_t granule = 0;
     int64_t row_offset = 0;
     float *rows = nullptr;
-    float *norms = nullptr;          // |y|^2 (L2/IP segments)
+    float *norms = nullptr;          // |y|^2 per row (fvec_norm_L2sqr order)
+    uint16_t *rows_hi = nullptr;     // bf16 rounding of the rows, [n][dpad]
+    uint16_t *rows_lo = nullptr;     // bf16 rounding of (row - hi), [n][dpad]
+    float *ynorm_max = nullptr;      // device scalar: max_r |y_r|
+    int64_t dpad = 0;
+    bool approx_ok = false;          // bf16 pre-filter usable for this segment
     uint8_t *nonempty_bits = nullptr;// null when every array is non-empty
     int *chunk_ord = nullptr;        // no-filter chunk ordinals (null = identity)
     size_t bytes = 0;
@@ -67,7 +72,7 @@ struct Workspace {
     hipStream_t stream = nullptr;
     hipEvent_t ev[6] = {};
     DevBuf queries, qvars, qnorms, qmu, qlam, status, filter, exists, ord, probe, tau, count, cand,
-        overflow, out_ids, out_dist, misc;
+        overflow, out_ids, out_dist, misc, qhi, bq, thr, cand2, count2;
     int *host_flags = nullptr;  // pinned
     void init() {
         if (stream) return;
@@ -77,7 +82,8 @@ struct Workspace {
     }
     void release() {
         DevBuf *all[] = {&queries, &qvars, &qnorms, &qmu,  &qlam,   &status,  &filter,   &exists, &ord,
-                         &probe,   &tau,   &count,  &cand, &overflow, &out_ids, &out_dist, &misc};
+                         &probe,   &tau,   &count,  &cand, &overflow, &out_ids, &out_dist, &misc,
+                         &qhi, &bq, &thr, &cand2, &count2};
         for (auto *b : all) b->release();
         if (host_flags) (void)hipHostFree(host_flags);
         host_flags = nullptr;
@@ -143,15 +149,35 @@ static void prepare_segment(mqvs_segment *s, const uint8_t *dev_nonempty_bytes,
         launch_chunk_ordinals(nullptr, s->nonempty_bits, nullptr, s->n, s->granule, 0,
                               s->chunk_ord, st);
     }
-    if (s->metric == MQVS_METRIC_COSINE) {
-        launch_normalize_rows(s->rows, s->n, s->d, st);
+    if (s->metric == MQVS_METRIC_COSINE) launch_normalize_rows(s->rows, s->n, s->d, st);
+    // |y|^2 per row: the BLAS-branch L2 norms, and (all metrics) the bound of
+    // the bf16 pre-filter
+    MQVS_HIP(hipMalloc((void **)&s->norms, sizeof(float) * std::max<int64_t>(s->n, 1)));
+    s->bytes += sizeof(float) * s->n;
+    launch_row_norms(s->rows, s->n, s->d, s->norms, st);
+    // bf16 plane of the rows for the nq >= 20 pre-filter (rows padded to kBfK)
+    s->dpad = (s->d + kBfK - 1) / kBfK * kBfK;
+    MQVS_HIP(hipMalloc((void **)&s->ynorm_max, 16));
+    MQVS_HIP(hipMemsetAsync(s->ynorm_max, 0, 16, st));
+    launch_max_norm(s->norms, s->n, s->ynorm_max, st);
+    const size_t hb = (size_t)std::max<int64_t>(s->n, 1) * s->dpad * sizeof(uint16_t);
+    if (hipMalloc((void **)&s->rows_hi, hb) == hipSuccess &&
+        hipMalloc((void **)&s->rows_lo, hb) == hipSuccess) {
+        s->bytes += 2 * hb;
+        launch_to_bf16(s->rows, s->n, s->d, s->d, s->rows_hi, s->rows_lo, s->dpad, st);
     } else {
-        MQVS_HIP(hipMalloc((void **)&s->norms, sizeof(float) * std::max<int64_t>(s->n, 1)));
-        s->bytes += sizeof(float) * s->n;
-        launch_row_norms(s->rows, s->n, s->d, s->norms, st);
+        (void)hipGetLastError();  // no room: exact fp32 batch path only
+        if (s->rows_hi) (void)hipFree(s->rows_hi);
+        s->rows_hi = nullptr;
+        s->rows_lo = nullptr;
     }
     MQVS_HIP(hipGetLastError());
+    float ymax = 0.f;
+    MQVS_HIP(hipMemcpyAsync(&ymax, s->ynorm_max, sizeof(float), hipMemcpyDeviceToHost, st));
     MQVS_HIP(hipStreamSynchronize(st));
+    // the bound needs finite, moderate norms (FLT_MAX-filled empty arrays of
+    // L2/IP parts overflow): otherwise the exact fp32 path serves nq >= 20
+    s->approx_ok = s->rows_hi != nullptr && ymax == ymax && ymax < 1e18f;
 }
 
 static void check_seg_args(int64_t n, int32_t d, int32_t metric, int64_t granule,
@@ -193,6 +219,9 @@ static void free_segment(mqvs_segment *s) {
     if (s->rows) (void)hipFree(s->rows);
     if (s->norms) (void)hipFree(s->norms);
     if (s->nonempty_bits) (void)hipFree(s->nonempty_bits);
+    if (s->rows_hi) (void)hipFree(s->rows_hi);
+    if (s->rows_lo) (void)hipFree(s->rows_lo);
+    if (s->ynorm_max) (void)hipFree(s->ynorm_max);
     if (s->chunk_ord) (void)hipFree(s->chunk_ord);
     if (cur >= 0) (void)hipSetDevice(cur);
     delete s;
@@ -224,15 +253,19 @@ static Range make_range(int64_t b, int64_t e, int64_t tile_rows, int64_t chunk_r
     return r;
 }
 
-static void run_scan(ScanParams p, const Range &r, bool mfma, int metric, bool probe, hipStream_t st) {
+enum ScanKind { kScanSmall = 0, kScanMfma32 = 1, kScanBf16 = 2 };
+
+static void run_scan(ScanParams p, const Range &r, int kind, int metric, bool probe, hipStream_t st) {
     if (r.tiles <= 0) return;
     p.row_begin = r.begin;
     p.row_end = r.end;
     p.tiles = r.tiles;
     p.tiles_per_chunk = r.tiles_per_chunk;
-    p.tile_rows = mfma ? kMfmaRows : kSmallRows;
-    if (mfma)
+    p.tile_rows = kind == kScanSmall ? kSmallRows : kMfmaRows;
+    if (kind == kScanMfma32)
         launch_scan_mfma(p, metric, probe, st);
+    else if (kind == kScanBf16)
+        launch_scan_bf16(p, metric, probe, kBfSplit, st);
     else
         launch_scan_small(p, metric, probe, st);
     MQVS_HIP(hipGetLastError());
@@ -241,9 +274,12 @@ static void run_scan(ScanParams p, const Range &r, bool mfma, int metric, bool p
 static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 
 // metric: public metric, or kMetricIpRaw for the faiss-contract entry point
+static int g_batch_mode = 0;  // 0: bf16 pre-filter + exact re-rank when possible, 1: fp32 MFMA
+
 static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, int metric,
                         const uint8_t *filter, const uint8_t *exists, int64_t *out_ids,
-                        float *out_dist, uint32_t flags, hipStream_t user_stream) {
+                        float *out_dist, uint32_t flags, hipStream_t user_stream,
+                        bool force_exact = false) {
     if (!seg) fail(MQVS_ERR_BAD_ARGUMENTS, "null segment");
     if (nq < 0 || k < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "nq and k must be non-negative");
     if (nq > 0 && k > 0 && (!queries || !out_ids || !out_dist))
@@ -296,6 +332,9 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
 
     // ---- query prep
     const bool mfma = nq >= kBlasThreshold;
+    const int kind = !mfma ? kScanSmall
+                     : (seg->approx_ok && !force_exact && g_batch_mode == 0) ? kScanBf16
+                                                                              : kScanMfma32;
     const int maxv = cos ? kMaxVariants : 1;
     const int64_t qstride = round_up(d, 32);
     float *qvars = (float *)ws.qvars.get(sizeof(float) * (size_t)nq * maxv * qstride);
@@ -325,10 +364,15 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     const bool aligned = cos || chunk_ord != nullptr;
     const int64_t tile_rows = mfma ? kMfmaRows : kSmallRows;
 
-    // ---- probe size: expected candidates ~ k*n/P; aim at cap/3
+    // ---- candidate capacity per query (a fixed budget spread over the
+    // batch) and probe size: expected candidates ~ k*n/P; aim at cap/3
+    int cap = (int)std::min<int64_t>(kCandMax, kCandBudget / std::max(nq, 1));
+    cap = std::max(cap, kSortCap) / 256 * 256;
+    // (more candidates = more appends from the scan; 16k keeps them cheap)
+    const int64_t target_cands = std::min<int64_t>(cap / 3, 16384);
     int64_t P = n;
     if (n > 32768) {
-        P = (int64_t)((3.0 * k * (double)n) / kSortCap) + 1;
+        P = (int64_t)(((double)k * (double)n) / target_cands) + 1;
         P = std::max<int64_t>(P, 8 * (int64_t)k);
         P = round_up(P, aligned ? seg->granule : tile_rows);
         if (P > n) P = n;
@@ -354,7 +398,6 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     p.exists = dexists;
     p.nonempty = seg->nonempty_bits;
     p.num_qblocks = (nq + kMfmaQ - 1) / kMfmaQ;
-    const int cap = kSortCap;
     uint32_t *tau = (uint32_t *)ws.tau.get(sizeof(uint32_t) * nq);
     int *count = (int *)ws.count.get(sizeof(int) * nq);
     Cand *cand = (Cand *)ws.cand.get(sizeof(Cand) * (size_t)nq * cap);
@@ -367,24 +410,75 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     p.probe = probe;
     p.probe_ld = P;
 
+    float *bq = nullptr;
+    if (kind == kScanBf16) {
+        // bf16 rounding of the query variants + per-query error bound
+        const size_t qe = (size_t)nq * maxv * seg->dpad;
+        uint16_t *qhi = (uint16_t *)ws.qhi.get(2 * sizeof(uint16_t) * qe);
+        launch_to_bf16(qvars, (int64_t)nq * maxv, d, qstride, qhi, qhi + qe, seg->dpad, s);
+        bq = (float *)ws.bq.get(sizeof(float) * nq);
+        p.rows_hi = seg->rows_hi;
+        p.rows_lo = seg->rows_lo;
+        p.q_hi = qhi;
+        p.q_lo = qhi + qe;
+        p.dpad = seg->dpad;
+        p.thr = (const float *)ws.thr.get(sizeof(float) * nq);
+        launch_query_bound(p, metric, kBfSplit, seg->ynorm_max, bq, s);
+        MQVS_HIP(hipGetLastError());
+    }
+
     const Range pr = make_range(0, P, tile_rows, seg->granule, aligned);
     const Range mr = make_range(P, n, tile_rows, seg->granule, aligned);
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[5], s));
-    run_scan(p, pr, mfma, metric, true, s);
+    run_scan(p, pr, kind, metric, true, s);
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[1], s));
     MQVS_HIP(hipMemsetAsync(count, 0, sizeof(int) * nq, s));
-    launch_probe_select(probe, P, P, nq, k, metric, tau, count, cand, cap, 0, s);
+    if (kind == kScanBf16)
+        launch_probe_select_approx(probe, P, P, nq, k, metric, bq, (float *)p.thr, count, cand, cap, s);
+    else
+        launch_probe_select(probe, P, P, nq, k, metric, tau, count, cand, cap, 0, s);
     MQVS_HIP(hipGetLastError());
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[2], s));
-    run_scan(p, mr, mfma, metric, false, s);
+    // main scan in geometrically growing segments; between segments the
+    // threshold tightens from the candidates so far and the lists compact
+    // into the other buffer (keeps appends and list lengths small when the
+    // probe's threshold is loose, e.g. clustered data)
+    {
+        const int64_t align = aligned ? seg->granule : tile_rows;
+        Cand *alt = (Cand *)ws.cand2.get(sizeof(Cand) * (size_t)nq * cap);
+        int *calt = (int *)ws.count2.get(sizeof(int) * nq);
+        int64_t b = P, seg_rows = std::max<int64_t>(2 * P, align);
+        int segs = 0;
+        while (b < n) {
+            const int64_t e = std::min(n, round_up(b + seg_rows, align));
+            run_scan(p, make_range(b, e, tile_rows, seg->granule, aligned), kind, metric, false, s);
+            b = e;
+            seg_rows *= 2;
+            ++segs;
+            if (b < n) {
+                launch_refine(cand, count, cap, nq, k, metric, kind == kScanBf16, bq, tau,
+                              (float *)p.thr, alt, calt, s);
+                MQVS_HIP(hipGetLastError());
+                std::swap(cand, alt);
+                std::swap(count, calt);
+                p.cand = cand;
+                p.cand_count = count;
+            }
+        }
+        st.segments = segs;
+        (void)mr;
+    }
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[3], s));
     MQVS_HIP(hipMemsetAsync(overflow, 0, sizeof(int) * 4, s));
-    launch_final_select(cand, count, cap, nq, k, metric, seg->granule, seg->row_offset, dids, ddist,
-                        overflow, s);
+    if (kind == kScanBf16)
+        launch_rerank_select(p, metric, bq, k, seg->row_offset, dids, ddist, overflow, s);
+    else
+        launch_final_select(cand, count, cap, nq, k, metric, seg->granule, seg->row_offset, dids, ddist,
+                            overflow, s);
     MQVS_HIP(hipGetLastError());
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[4], s));
 
-    st.path = mfma ? 1 : 0;
+    st.path = kind;
     st.probe_rows = P;
     st.main_rows = n - P;
     st.rows_scanned = n;
@@ -397,6 +491,13 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         MQVS_HIP(hipMemcpyAsync(ws.host_flags + 1, status, sizeof(int), hipMemcpyDeviceToHost, s));
         MQVS_HIP(hipStreamSynchronize(s));
         if (ws.host_flags[1]) fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not reach a cycle");
+        if (kind == kScanBf16 && ws.host_flags[0]) {
+            // the bf16 bound left too many candidates: exact fp32 path
+            search_impl(seg, queries, nq, k, metric, filter, exists, out_ids, out_dist, flags,
+                        user_stream, true);
+            g_stats.rescans += 1;
+            return;
+        }
         int rescans = 0;
         while (ws.host_flags[0]) {
             if (++rescans > 3)
@@ -404,7 +505,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
                                            " rows tie at the k-th distance");
             launch_cand_tau(cand, count, cap, nq, k, metric, tau, nullptr, s);
             MQVS_HIP(hipMemsetAsync(count, 0, sizeof(int) * nq, s));
-            run_scan(p, make_range(0, n, tile_rows, seg->granule, aligned), mfma, metric, false, s);
+            run_scan(p, make_range(0, n, tile_rows, seg->granule, aligned), kind, metric, false, s);
             MQVS_HIP(hipMemsetAsync(overflow, 0, sizeof(int) * 4, s));
             launch_final_select(cand, count, cap, nq, k, metric, seg->granule, seg->row_offset, dids,
                                 ddist, overflow, s);
@@ -671,6 +772,12 @@ int mqvs_rerank(mqvs_segment_t, const float *, int32_t, const int64_t *, int32_t
 int mqvs_last_search_stats(mqvs_search_stats *out) {
     if (!out) return MQVS_ERR_BAD_ARGUMENTS;
     *out = g_stats;
+    return MQVS_OK;
+}
+
+int mqvs_set_batch_mode(int mode) {
+    if (mode != 0 && mode != 1) return MQVS_ERR_BAD_ARGUMENTS;
+    g_batch_mode = mode;
     return MQVS_OK;
 }
 

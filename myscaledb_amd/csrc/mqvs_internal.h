@@ -15,6 +15,8 @@ namespace mqvs {
 constexpr int kBlasThreshold = 20;   // faiss distance_compute_blas_threshold
 constexpr int kMaxVariants = 16;     // cosine query re-normalisation variants kept
 constexpr int kSortCap = 4096;       // candidates sorted in LDS per query
+constexpr int64_t kCandBudget = 1 << 25;  // candidate slots per search (x 8 B)
+constexpr int64_t kCandMax = 1 << 20;     // candidate slots per query
 constexpr int kSmallRows = 256;      // rows per tile, VALU scan
 constexpr int kMfmaRows = 128;       // rows per tile, MFMA scan
 constexpr int kMfmaQ = 128;          // queries per tile, MFMA scan
@@ -109,6 +111,13 @@ struct ScanParams {
     Cand *cand;             // [nq][cand_cap]
     int cand_cap;
     int num_qblocks;        // MFMA: query blocks
+    // bf16 pre-filter path (nq >= 20): hi bf16 planes, row stride dpad
+    const uint16_t *rows_hi;  // [n][dpad]
+    const uint16_t *rows_lo;  // [n][dpad] bf16(x - hi) (split 3)
+    const uint16_t *q_hi;     // [nq][maxv][dpad]
+    const uint16_t *q_lo;     // [nq][maxv][dpad] (split 3)
+    int64_t dpad;
+    const float *thr;         // [nq] APPEND threshold on the approximate raw value
 };
 
 // Tile -> [r0, r1) and chunk index.
@@ -179,6 +188,26 @@ void launch_chunk_ordinals(const uint8_t *filter, const uint8_t *nonempty, const
                            hipStream_t s);
 void launch_rerank(const ScanParams &p, const int64_t *cand_ids, int ncand, int metric,
                    bool blas, hipStream_t s);
+
+// bf16 pre-filter path (kernels_bf16.hip)
+constexpr int kBfK = 64;    // bf16 planes padded to a multiple of this
+constexpr int kBfSplit = 3; // hi*hi + hi*lo + lo*hi (see kernels_bf16_scan.hip)
+// dst_hi = bf16_rn(x); dst_lo (optional) = bf16_rn(x - hi)
+void launch_to_bf16(const float *src, int64_t rows, int d, int64_t src_stride, uint16_t *dst_hi,
+                    uint16_t *dst_lo, int64_t dpad, hipStream_t s);
+void launch_max_norm(const float *norms2, int64_t n, float *out_max, hipStream_t s);
+void launch_query_bound(const ScanParams &p, int metric, int split, const float *ynorm_max,
+                        float *bq, hipStream_t s);
+void launch_scan_bf16(const ScanParams &p, int metric, bool probe, int split, hipStream_t s);
+void launch_probe_select_approx(const float *probe, int64_t P, int64_t ld, int nq, int k,
+                                int metric, const float *bq, float *thr, int *cand_count,
+                                Cand *cand, int cand_cap, hipStream_t s);
+void launch_refine(const Cand *cin, const int *cnt_in, int cap, int nq, int k, int metric,
+                   bool approx, const float *bq, uint32_t *tau, float *thr, Cand *cout, int *cnt_out,
+                   hipStream_t s);
+void launch_rerank_select(const ScanParams &p, int metric, const float *bq, int k,
+                          int64_t id_offset, int64_t *out_ids, float *out_dist, int *overflow,
+                          hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // Error plumbing

@@ -1,0 +1,224 @@
+// select_common.h -- block-wide radix select, float-row visitor and LDS bitonic
+// sort shared by the selection kernels (kernels_select.hip, kernels_bf16.hip).
+#pragma once
+#include "mqvs_internal.h"
+
+namespace mqvs {
+
+constexpr int SEL_THREADS = 256;
+
+// Histogram update with run-length aggregation: a thread keeps a running
+// (bucket, count) pair and only flushes to LDS when the bucket changes, which
+// removes the LDS-atomic pile-up on the few buckets that the high digits of
+// clustered float keys fall into.
+struct RunHist {
+    uint32_t cur = 0xFFFFFFFFu, cnt = 0;
+    __device__ void add(uint32_t *hist, uint32_t b) {
+        if (b == cur) {
+            ++cnt;
+        } else {
+            if (cnt) atomicAdd(&hist[cur], cnt);
+            cur = b;
+            cnt = 1;
+        }
+    }
+    __device__ void flush(uint32_t *hist) {
+        if (cnt) atomicAdd(&hist[cur], cnt);
+        cnt = 0;
+        cur = 0xFFFFFFFFu;
+    }
+};
+
+// k-th smallest valid key (1-based rank k) among `count` values produced by
+// load(i); 0xFFFFFFFE when fewer than k values are valid.  Block-wide.
+template <typename KeyFn>
+__device__ inline uint32_t block_radix_select(KeyFn keyof, int64_t count, int k, uint32_t *hist,
+                                       uint32_t *sh) {
+    const int t = threadIdx.x;
+    uint32_t prefix = 0, mask = 0, kk = (uint32_t)k;
+    for (int pass = 0; pass < 4; ++pass) {
+        const int shift = 24 - 8 * pass;
+        for (int i = t; i < 256; i += SEL_THREADS) hist[i] = 0;
+        __syncthreads();
+        RunHist rh;
+        for (int64_t i = t; i < count; i += SEL_THREADS) {
+            const uint32_t key = keyof(i);
+            if (key == 0xFFFFFFFFu) continue;
+            if ((key & mask) != prefix) continue;
+            rh.add(hist, (key >> shift) & 255u);
+        }
+        rh.flush(hist);
+        __syncthreads();
+        if (t == 0) {
+            uint32_t total = 0;
+            for (int b = 0; b < 256; ++b) total += hist[b];
+            uint32_t done = 0, cum = 0, bsel = 0;
+            if (pass == 0 && total < kk) {
+                done = 1;  // fewer than k valid: every valid value qualifies
+            } else {
+                for (int b = 0; b < 256; ++b) {
+                    if (cum + hist[b] >= kk) {
+                        bsel = (uint32_t)b;
+                        break;
+                    }
+                    cum += hist[b];
+                }
+            }
+            sh[0] = done;
+            sh[1] = bsel;
+            sh[2] = cum;
+        }
+        __syncthreads();
+        if (sh[0]) {
+            __syncthreads();
+            return 0xFFFFFFFEu;
+        }
+        prefix |= sh[1] << shift;
+        mask |= 255u << shift;
+        kk -= sh[2];
+        __syncthreads();
+    }
+    return prefix;
+}
+
+// Visit every element of a float row: float4 loads, 4 in flight per thread
+// (the probe rows are megabytes; a scalar loop leaves HBM idle).
+template <typename F>
+__device__ inline void for_each_f4(const float *row, int64_t P, F &&f) {
+    const int t = threadIdx.x;
+    const bool al = ((uintptr_t)row & 15) == 0;
+    int64_t head = 0;
+    if (al) {
+        const int64_t n4 = P / 4;
+        const float4 *r4 = reinterpret_cast<const float4 *>(row);
+        int64_t i = t;
+        for (; i + 3 * SEL_THREADS < n4; i += 4 * SEL_THREADS) {
+            const float4 a = r4[i], b = r4[i + SEL_THREADS], c = r4[i + 2 * SEL_THREADS],
+                         e = r4[i + 3 * SEL_THREADS];
+            f(4 * i, a.x); f(4 * i + 1, a.y); f(4 * i + 2, a.z); f(4 * i + 3, a.w);
+            const int64_t ib = i + SEL_THREADS, ic = i + 2 * SEL_THREADS, ie = i + 3 * SEL_THREADS;
+            f(4 * ib, b.x); f(4 * ib + 1, b.y); f(4 * ib + 2, b.z); f(4 * ib + 3, b.w);
+            f(4 * ic, c.x); f(4 * ic + 1, c.y); f(4 * ic + 2, c.z); f(4 * ic + 3, c.w);
+            f(4 * ie, e.x); f(4 * ie + 1, e.y); f(4 * ie + 2, e.z); f(4 * ie + 3, e.w);
+        }
+        for (; i < n4; i += SEL_THREADS) {
+            const float4 a = r4[i];
+            f(4 * i, a.x); f(4 * i + 1, a.y); f(4 * i + 2, a.z); f(4 * i + 3, a.w);
+        }
+        head = n4 * 4;
+    }
+    for (int64_t i = head + t; i < P; i += SEL_THREADS) f(i, row[i]);
+}
+
+template <int METRIC>
+__device__ inline uint32_t block_radix_select_rows(const float *row, int64_t P, int k, uint32_t *hist,
+                                            uint32_t *sh) {
+    const int t = threadIdx.x;
+    uint32_t prefix = 0, mask = 0, kk = (uint32_t)k;
+    for (int pass = 0; pass < 4; ++pass) {
+        const int shift = 24 - 8 * pass;
+        for (int i = t; i < 256; i += SEL_THREADS) hist[i] = 0;
+        __syncthreads();
+        RunHist rh;
+        for_each_f4(row, P, [&](int64_t, float raw) {
+            const uint32_t key = key32<METRIC>(raw);
+            if (key != 0xFFFFFFFFu && (key & mask) == prefix) rh.add(hist, (key >> shift) & 255u);
+        });
+        rh.flush(hist);
+        __syncthreads();
+        if (t == 0) {
+            uint32_t total = 0;
+            for (int b = 0; b < 256; ++b) total += hist[b];
+            uint32_t done = 0, cum = 0, bsel = 0;
+            if (pass == 0 && total < kk) {
+                done = 1;
+            } else {
+                for (int b = 0; b < 256; ++b) {
+                    if (cum + hist[b] >= kk) {
+                        bsel = (uint32_t)b;
+                        break;
+                    }
+                    cum += hist[b];
+                }
+            }
+            sh[0] = done;
+            sh[1] = bsel;
+            sh[2] = cum;
+        }
+        __syncthreads();
+        if (sh[0]) {
+            __syncthreads();
+            return 0xFFFFFFFEu;
+        }
+        prefix |= sh[1] << shift;
+        mask |= 255u << shift;
+        kk -= sh[2];
+        __syncthreads();
+    }
+    return prefix;
+}
+
+// ---------------------------------------------------------------------------
+// Bitonic sort of up to kSortCap 16-byte records in LDS, lexicographic on
+// (x, y, z, w) ascending.
+__device__ inline bool rec_less(const uint4 &a, const uint4 &b) {
+    if (a.x != b.x) return a.x < b.x;
+    if (a.y != b.y) return a.y < b.y;
+    if (a.z != b.z) return a.z < b.z;
+    return a.w < b.w;
+}
+
+__device__ inline void block_bitonic_sort(uint4 *recs, int N) {
+    for (int size = 2; size <= N; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = threadIdx.x; i < (N >> 1); i += SEL_THREADS) {
+                const int lo = 2 * stride * (i / stride) + (i % stride);
+                const int hi = lo + stride;
+                const bool up = (lo & size) == 0;
+                uint4 a = recs[lo], b = recs[hi];
+                if (rec_less(b, a) == up) {
+                    recs[lo] = b;
+                    recs[hi] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+}
+
+__device__ inline float key_to_value(int metric, uint32_t k1) {
+    // inverse of ord_asc / ~ord_asc
+    uint32_t u = (metric == MQVS_METRIC_IP || metric == kMetricIpRaw) ? ~k1 : k1;
+    u = (u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u;
+    return __builtin_bit_cast(float, u);
+}
+
+// Approximate ordering key: smaller = better, NaN last; no validity cut (the
+// exact value decides validity after the re-rank).
+template <int METRIC>
+__device__ inline uint32_t okey(float v) {
+    if (v != v) return 0xFFFFFFFFu;
+    const uint32_t o = ord_asc(v);
+    return (METRIC == MQVS_METRIC_L2) ? o : ~o;
+}
+
+template <int METRIC>
+__device__ inline float okey_value(uint32_t k) {
+    uint32_t u = (METRIC == MQVS_METRIC_L2) ? k : ~k;
+    u = (u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u;
+    return __builtin_bit_cast(float, u);
+}
+
+// threshold on the approximate value that keeps every row of the exact top-k
+template <int METRIC>
+__device__ inline float widen(float kth, float b) {
+    if (METRIC == MQVS_METRIC_L2) {
+        const float t = kth + 2.0f * b;
+        return t + fabsf(t) * 2.4e-7f + 1e-30f;
+    }
+    const float t = kth - 2.0f * b;
+    return t - fabsf(t) * 2.4e-7f - 1e-30f;
+}
+
+
+}  // namespace mqvs

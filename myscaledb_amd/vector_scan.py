@@ -229,3 +229,9 @@ def generate_device(seed, mode, row0, n, d, out_tensor, stream=None):
 
 def set_timing(enabled: bool):
     check(lib.mqvs_set_timing(1 if enabled else 0))
+
+
+def set_batch_mode(mode: int):
+    """nq >= 20: 0 = bf16 MFMA pre-filter + exact fp32 re-rank (default),
+    1 = fp32 MFMA over every row.  Both return identical bits."""
+    check(lib.mqvs_set_batch_mode(int(mode)))

@@ -100,11 +100,37 @@ PARITY = [
     ("l2_k_gt_n",       50,    8,   4,   100, "L2", 1, 16,  None, None, 0.0),
     ("l2_big_probe",    100000, 32, 2,   100, "L2", 1, 8192, None, None, 0.0),
     ("cos_big_probe",   80000, 32, 24,  100, "Cosine", 1, 8192, None, None, 0.0),
+    # long candidate lists: two-stage final select (radix k-th, then LDS sort)
+    ("l2_k1000_twostage", 200000, 16, 2, 1000, "L2", 1, 8192, None, None, 0.0),
+    ("cos_k512_twostage", 120000, 32, 20, 512, "Cosine", 1, 8192, None, None, 0.0),
+    ("ip_exact_ties_k700", 150000, 8, 3, 700, "IP", 0, 4096, None, None, 0.0),
+    # granule-aligned tiling with a short last granule (tiles past the end)
+    ("cos_partial_last_granule", 8292, 64, 24, 50, "Cosine", 1, 8192, None, None, 0.0),
+    ("cos_partial_last_granule_nq3", 8292, 64, 3, 50, "Cosine", 1, 8192, None, None, 0.0),
 ]
+
+
+BATCH = [c for c in PARITY if c[3] >= 20]
 
 
 @pytest.mark.parametrize("cfg", PARITY, ids=[c[0] for c in PARITY])
 def test_gpu_vs_oracle(mq, cfg):
+    run_parity(mq, cfg)
+
+
+@pytest.mark.parametrize("cfg", BATCH, ids=[c[0] for c in BATCH])
+def test_gpu_vs_oracle_fp32_batch_mode(mq, cfg):
+    """nq >= 20 through the fp32-MFMA-everywhere mode (the default is the bf16
+    pre-filter + exact re-rank): same bits."""
+    from myscaledb_amd.vector_scan import set_batch_mode
+    set_batch_mode(1)
+    try:
+        run_parity(mq, cfg)
+    finally:
+        set_batch_mode(0)
+
+
+def run_parity(mq, cfg):
     name, n, d, nq, k, metric, mode, gran, filt, lwd, empty = cfg
     seed = zlib.crc32(name.encode())
     rows, nonempty = make_part(0x5EED0001 ^ seed, n, d, mode, empty)
