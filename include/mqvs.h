@@ -156,8 +156,9 @@ int mqvs_generate_device(uint64_t seed, int32_t mode, int64_t row0, int64_t n, i
 typedef struct {
     double probe_ms;        /* probe scan kernel */
     double probe_select_ms; /* radix select over the probe */
-    double main_ms;         /* main scan kernel (rows [probe_rows, n)) */
-    double final_ms;        /* final select kernel */
+    double main_ms;         /* main scan kernels (rows [probe_rows, n), all segments) */
+    double refine_ms;       /* threshold refinements between main-scan segments */
+    double final_ms;        /* final select (or exact re-rank + select) kernel */
     double total_ms;        /* first to last event of the search */
     int64_t rows_scanned;
     int64_t probe_rows;

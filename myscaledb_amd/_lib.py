@@ -34,7 +34,8 @@ SYMBOLS = [
 
 class SearchStats(ctypes.Structure):
     _fields_ = [("probe_ms", ctypes.c_double), ("probe_select_ms", ctypes.c_double),
-                ("main_ms", ctypes.c_double), ("final_ms", ctypes.c_double),
+                ("main_ms", ctypes.c_double), ("refine_ms", ctypes.c_double),
+                ("final_ms", ctypes.c_double),
                 ("total_ms", ctypes.c_double), ("rows_scanned", ctypes.c_int64),
                 ("probe_rows", ctypes.c_int64), ("main_rows", ctypes.c_int64),
                 ("nq", ctypes.c_int32), ("k", ctypes.c_int32),

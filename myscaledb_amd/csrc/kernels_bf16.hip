@@ -97,25 +97,28 @@ void launch_max_norm(const float *norms2, int64_t n, float *out_max, hipStream_t
 // Per-query bound on |approx - exact| in the metric's raw value:
 //   IP / cosine: B = c(d) * |x|max_over_used_variants * |y|max
 //   L2 (BLAS):   raw = (xn + yn) - 2 ip -> 2 B + 2 ulp of the result
-//   split 3: truncation |xl yl| + |xh ey| + |ex y| <= 3.03 2^-16 |x||y|; fp32
-//   accumulation of the hi sum and of the exact chain, d terms each, ~2 d u;
-//   the cross-product sum (2d terms of <= 2^-8 |x||y|) and the final add.
+//   split 3: truncation |xl yl| + |xh ey| + |ex y| <= 3.03 2^-16 |x||y|; the
+//   three products are exact in fp32 and summed into ONE accumulator: 3d terms
+//   with sum |t| <= 1.008 |x||y| -> 3.03 d u, plus d u for the exact chain.
 //   split 1: element rounding 2^-8 per side -> (2^-7 + 2^-16) |x||y| + 2 d u.
 __global__ void k_query_bound(ScanParams p, int metric, int split, const float *ynorm_max,
                               float *bq) {
-    const int j = blockIdx.x * blockDim.x + threadIdx.x;
-    if (j >= p.nq) return;
+    // one wave per query; |x| in fp64 (an upper bound after the 1.0001 slack)
+    const int j = blockIdx.x;
+    const int lane = threadIdx.x;
     const int64_t qs = (int64_t)((p.d + 31) / 32 * 32);
     const int nv = p.maxv <= 1 ? 1 : p.qmu[j] + p.qlam[j];
     float xmax = 0.f;
     for (int v = 0; v < nv; ++v) {
         const float *x = p.qvars + ((int64_t)j * p.maxv + v) * qs;
         double s = 0.0;
-        for (int i = 0; i < p.d; ++i) s += (double)x[i] * (double)x[i];
+        for (int i = lane; i < p.d; i += 64) s += (double)x[i] * (double)x[i];
+        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
         xmax = fmaxf(xmax, (float)sqrt(s));
     }
+    if (lane != 0) return;
     const float ymax = *ynorm_max * (1.0f + 6e-8f * (float)p.d + 1e-6f);  // fp32 |y|^2 chain error
-    const float acc_term = 2.04f * (float)p.d * 5.9604645e-8f;
+    const float acc_term = (split == 3 ? 4.1f : 2.04f) * (float)p.d * 5.9604645e-8f;
     const float c = split == 3 ? 3.1f * 1.5258789e-5f + acc_term + 1.2e-7f
                                : 0.0078125f + 1.6e-5f + acc_term + 1e-7f;
     float b = c * (xmax * 1.0001f) * ymax + 1e-30f;
@@ -131,8 +134,7 @@ __global__ void k_query_bound(ScanParams p, int metric, int split, const float *
 
 void launch_query_bound(const ScanParams &p, int metric, int split, const float *ynorm_max,
                         float *bq, hipStream_t s) {
-    hipLaunchKernelGGL(k_query_bound, dim3((p.nq + 63) / 64), dim3(64), 0, s, p, metric, split,
-                       ynorm_max, bq);
+    hipLaunchKernelGGL(k_query_bound, dim3(p.nq), dim3(64), 0, s, p, metric, split, ynorm_max, bq);
 }
 
 

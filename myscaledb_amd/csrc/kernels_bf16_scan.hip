@@ -1,32 +1,56 @@
 // kernels_bf16_scan.hip -- split-precision bf16 MFMA scan (the nq >= 20
 // pre-filter of kernels_bf16.hip).
 //
-// SPLIT = 3: x = xh + xl (two bf16 roundings), x.y ~ xh.yh + (xh.yl + xl.yh),
-// the hi product and the two cross products in SEPARATE fp32 accumulators,
-// 3 v_mfma_f32_32x32x16_bf16 per 32x32x16 block-step (3/16 of the f32 MFMA
-// cost).  Error vs the fp32 chain (kernels_bf16.hip, k_query_bound):
-//   (3.1 2^-16 + 2.02 d 2^-24 + small) |x| |y|
-// SPLIT = 1: hi planes only, bound (2^-7 + ...) |x| |y|.
+// SPLIT = 3: x = xh + xl (two bf16 roundings) and
+//     x.y ~ xh.yh + xh.yl + xl.yh
+// accumulated in one fp32 accumulator: 3 bf16 MFMAs per block-step, 3/16 of
+// the f32 MFMA cost.  Error vs the exact fp32 chain (bound in
+// kernels_bf16.hip, k_query_bound):
+//     (3.1 2^-16 + 4.1 d 2^-24 + 1.2e-7) |x| |y|
+// SPLIT = 1: hi planes only, bound (2^-7 + 2^-16 + 2.1 d 2^-24) |x| |y|.
 //
-// Tile: 128 rows x 128 queries per workgroup, 4 waves of 64 x 64 (2 x 2
-// blocks of 32 x 32); K staged 32 bf16 deep (64 B per row per plane) by
-// LDS-DMA into double-buffered planes {Y hi, Y lo, Q hi, Q lo} of 8 KiB each
-// (64 KiB per workgroup, 2 workgroups per CU).  Chunk c (16 B) of image row r
-// sits at slot c ^ ((r >> 2) & 3): one ds_read_b128 lane group (16 rows,
-// distinct r mod 16) hits 16 distinct 16-B bank groups.
+// Workgroup tile: 256 rows x QT queries, 4 x WQ waves, each wave 64 rows x
+// (32 QB) queries:
+//     nq <= 64 : 256 x  64  (8 waves, QB 1)   LDS 2 x 40 KiB
+//     nq <= 128: 256 x 128  (8 waves, QB 2)   LDS 2 x 48 KiB
+//     else     : 256 x 256  (8 waves, QB 4)   LDS 2 x 64 KiB
+// K is staged 32 bf16 (64 B per row per plane) deep; one stage is the
+// contiguous image [Y hi | Y lo | Q hi | Q lo] filled by LDS-DMA
+// (global_load_lds_dwordx4, 1 KiB = 16 image rows per instruction), double
+// buffered.  The large tile gives each 64 KiB stage ~3k cycles of MFMA work,
+// enough for a one-stage prefetch to cover the load latency.
+//
+// Schedule variants (VAR bits, chosen per shape in launch_split):
+//   1  s_setprio(1) around the stage's MFMA work, so the waves of a SIMD
+//      keep the matrix pipe fed while another wave issues loads
+//   2  the next stage's LDS-DMA issue split in two halves placed between the
+//      MFMA groups (instead of one burst after the barrier, where every wave
+//      of the workgroup issues at once and the matrix pipe idles)
+//   4  v_mfma_f32_16x16x32_bf16 (4 x 2QB blocks of 16 x 16 per wave) instead
+//      of v_mfma_f32_32x32x16_bf16 (2 x QB blocks of 32 x 32)
+// Chunk c (16 B) of image row r sits at slot c ^ f(r): f(r) = (r >> 2) & 3 for
+// the 32x32 fragment reads, 2 ((r >> 2) & 1) for the 16x16 reads; either way
+// every ds_read_b128 lane group hits 16 distinct 16-B bank slots.
+#include <cstdio>
+#include <cstdlib>
+
 #include "mqvs_internal.h"
 
 namespace mqvs {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
 typedef __attribute__((address_space(3))) void lds_void;
 
-constexpr int BS_K = 32;                       // bf16 per row per stage
-constexpr int BS_ROWB = BS_K * 2;              // 64 B: 4 chunks of 16 B
-constexpr int BS_PLANE = kMfmaRows * BS_ROWB;  // 8 KiB (rows == queries == 128)
+constexpr int BS_K = 32;          // bf16 per row per stage
+constexpr int BS_ROWB = BS_K * 2; // 64 B: 4 chunks of 16 B
+constexpr int BS_RT = kBfRows;    // rows per workgroup tile (all shapes)
 
-__device__ inline int swz4(int r, int c) { return c ^ ((r >> 2) & 3); }
+template <bool M16>
+__device__ inline int swz(int r, int c) {
+    return M16 ? (c ^ (((r >> 2) & 1) << 1)) : (c ^ ((r >> 2) & 3));
+}
 
 template <int METRIC, bool PROBE>
 __device__ inline void emit_approx(const ScanParams &p, int j, int64_t row, bool valid, float raw) {
@@ -48,9 +72,69 @@ __device__ inline void emit_approx(const ScanParams &p, int j, int64_t row, bool
     }
 }
 
-template <int METRIC, bool PROBE, int SPLIT>
-__global__ __launch_bounds__(256, 2) void k_scan_bf16(ScanParams p) {
-    __shared__ __attribute__((aligned(16))) unsigned char lds[2][4][BS_PLANE];
+template <int METRIC, bool PROBE>
+__device__ inline void emit_ip(const ScanParams &p, int j, int64_t row, float ip) {
+    float raw = ip;
+    if (METRIC == MQVS_METRIC_L2) {
+        raw = (p.qnorms[j] + p.row_norms[row]) - 2.0f * ip;
+        if (raw < 0) raw = 0;
+    }
+    emit_approx<METRIC, PROBE>(p, j, row, row_valid(p, row), raw);
+}
+
+// Epilogue for NV accumulator values of query j (rows row_of(0..NV-1)).
+// APPEND: candidates are rare, so the fast path only compares every value
+// with the query's threshold (no row bounds, no bitmaps, no branches); the
+// values of a wave with any lane over it take the exact per-row path.
+template <int METRIC, bool PROBE, int NV, class RowFn, class ValFn>
+__device__ inline void emit_vals(const ScanParams &p, int j, int64_t r1, RowFn row_of, ValFn val) {
+    if (PROBE) {
+#pragma unroll
+        for (int r = 0; r < NV; ++r) {
+            const int64_t row = row_of(r);
+            if (row < r1) emit_ip<METRIC, true>(p, j, row, val(r));
+        }
+        return;
+    }
+    const float t = p.thr[j];
+    const float qn = (METRIC == MQVS_METRIC_L2) ? p.qnorms[j] : 0.f;
+    bool any = false;
+#pragma unroll
+    for (int r = 0; r < NV; ++r) {
+        float raw = val(r);
+        if (METRIC == MQVS_METRIC_L2) {
+            const int64_t row = min(row_of(r), r1 - 1);
+            raw = (qn + p.row_norms[row]) - 2.0f * raw;
+            if (raw < 0) raw = 0;
+            any |= raw <= t;
+        } else {
+            any |= raw >= t;
+        }
+    }
+    if (any) {
+#pragma unroll
+        for (int r = 0; r < NV; ++r) {
+            const int64_t row = row_of(r);
+            if (row < r1) emit_ip<METRIC, false>(p, j, row, val(r));
+        }
+    }
+}
+
+template <int METRIC, bool PROBE, int SPLIT, int WQ, int QB, int VAR>
+__global__ __launch_bounds__(256 * WQ) void k_scan_bf16(ScanParams p) {
+    constexpr bool PRIO = VAR & 1, SPLIT_ISSUE = VAR & 2, M16 = VAR & 4;
+    constexpr int WR = 4;                   // row waves
+    constexpr int NW = WR * WQ;             // waves per workgroup
+    constexpr int QT = 32 * QB * WQ;        // queries per workgroup
+    constexpr int PL = (SPLIT == 3) ? 2 : 1;// planes per operand
+    constexpr int GY = BS_RT / 16;          // 1-KiB groups per Y plane
+    constexpr int GQ = QT / 16;             // 1-KiB groups per Q plane
+    constexpr int G = PL * (GY + GQ);       // groups per stage
+    constexpr int GPW = G / NW;             // groups per wave
+    static_assert(G % NW == 0, "stage groups must split evenly over the waves");
+    constexpr int STAGE = G * 1024;         // bytes per stage
+    __shared__ __attribute__((aligned(16))) unsigned char lds[2][STAGE];
+
     const int64_t L = p.tiles * p.num_qblocks;
     const int64_t cpx = (L + 7) / 8;
     const int64_t b = blockIdx.x;
@@ -64,131 +148,434 @@ __global__ __launch_bounds__(256, 2) void k_scan_bf16(ScanParams p) {
     const int ord = chunk_ordinal(p, chunk);
     const int t = threadIdx.x;
     const int lane = t & 63, w = t >> 6;
-    const int wr = w >> 1, wq = w & 1;
-    const int h = lane >> 5, l32 = lane & 31;
-    const int q0 = qb * kMfmaQ;
+    const int wr = w % WR, wq = w / WR;
+    const int q0 = qb * QT;
 
     if (ord < 0) {
         if (PROBE) {
-            for (int i = t; i < kMfmaRows * kMfmaQ; i += 256) {
-                const int64_t row = r0 + (i % kMfmaRows);
-                const int j = q0 + i / kMfmaRows;
+            for (int i = t; i < BS_RT * QT; i += 64 * NW) {
+                const int64_t row = r0 + (i % BS_RT);
+                const int j = q0 + i / BS_RT;
                 if (row < r1 && j < p.nq) emit_approx<METRIC, true>(p, j, row, false, 0.f);
             }
         }
         return;
     }
 
-    // LDS-DMA sources: wave w fills image rows [(w*2+i)*16, +16) of a plane
-    // with one 1-KiB instruction per i; lane -> (row lane/4, slot lane%4)
-    const uint16_t *src[4][2];
+    // LDS-DMA sources: group g = wave w + i*NW (i < GPW) fills 16 image rows
+    // of one plane; lane -> (row lane/4, slot lane%4) holds chunk swz(row, slot)
+    const uint16_t *src[GPW];
 #pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        const int r = (w * 2 + i) * 16 + (lane >> 2);
-        const int c = swz4(r, lane & 3);
-        int64_t gr = r0 + r;
-        if (gr >= r1) gr = r0;  // padding rows: any valid row, results discarded
-        src[0][i] = p.rows_hi + gr * p.dpad + c * 8;
-        src[1][i] = (SPLIT == 3) ? p.rows_lo + gr * p.dpad + c * 8 : nullptr;
-        int j = q0 + r;
-        if (j >= p.nq) j = 0;
-        const int64_t qo = ((int64_t)j * p.maxv + variant_of(p, j, ord)) * p.dpad + c * 8;
-        src[2][i] = p.q_hi + qo;
-        src[3][i] = (SPLIT == 3) ? p.q_lo + qo : nullptr;
+    for (int i = 0; i < GPW; ++i) {
+        const int g = w + i * NW;
+        int pl, rbase;  // plane 0..3 = Yh, Yl, Qh, Ql
+        if (g < PL * GY) {
+            pl = g / GY;
+            rbase = (g % GY) * 16;
+        } else {
+            pl = 2 + (g - PL * GY) / GQ;
+            rbase = ((g - PL * GY) % GQ) * 16;
+        }
+        const int r = rbase + (lane >> 2);
+        const int c = swz<M16>(r, lane & 3);
+        if (pl < 2) {
+            int64_t gr = r0 + r;
+            if (gr >= r1) gr = r0;  // padding rows: any valid row, results discarded
+            src[i] = (pl == 0 ? p.rows_hi : p.rows_lo) + gr * p.dpad + c * 8;
+        } else {
+            int j = q0 + r;
+            if (j >= p.nq) j = 0;
+            const int64_t qo = ((int64_t)j * p.maxv + variant_of(p, j, ord)) * p.dpad + c * 8;
+            src[i] = (pl == 2 ? p.q_hi : p.q_lo) + qo;
+        }
     }
-    auto issue = [&](int s, int bf) {
+    auto issue = [&](int s, int bf, int i0, int i1) {
         const int64_t k0 = (int64_t)s * BS_K;
 #pragma unroll
-        for (int pl = 0; pl < 4; ++pl) {
-            if (SPLIT == 1 && (pl & 1)) continue;
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-                __builtin_amdgcn_global_load_lds((const void *)(src[pl][i] + k0),
-                                                 (lds_void *)&lds[bf][pl][(w * 2 + i) * 16 * BS_ROWB],
-                                                 16, 0, 0);
-        }
+        for (int i = 0; i < GPW; ++i)
+            if (i >= i0 && i < i1)
+                __builtin_amdgcn_global_load_lds((const void *)(src[i] + k0),
+                                                 (lds_void *)&lds[bf][(w + i * NW) * 1024], 16, 0, 0);
+    };
+    // split issue: half `part` of the next stage's pieces, pinned in place
+    auto issue_part = [&](bool more, int s, int part) {
+        if (!SPLIT_ISSUE || !more) return;
+        __builtin_amdgcn_sched_barrier(0);
+        issue(s + 1, (s + 1) & 1, part * (GPW / 2), part == 0 ? GPW / 2 : GPW);
+        __builtin_amdgcn_sched_barrier(0);
     };
 
-    f32x16 acc[2][2], cor[2][2];
+    // plane byte offsets inside a stage
+    constexpr int OFF_YH = 0;
+    constexpr int OFF_YL = GY * 1024;
+    constexpr int OFF_QH = PL * GY * 1024;
+    constexpr int OFF_QL = OFF_QH + GQ * 1024;
+    auto frag = [&](const unsigned char *st, int off, int r, int c) {
+        return *reinterpret_cast<const bf16x8 *>(st + off + r * BS_ROWB + swz<M16>(r, c) * 16);
+    };
+    auto mma32 = [](bf16x8 a, bf16x8 b, f32x16 c) {
+        return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+    };
+    auto mma16 = [](bf16x8 a, bf16x8 b, f32x4 c) {
+        return __builtin_amdgcn_mfma_f32_16x16x32_bf16(a, b, c, 0, 0, 0);
+    };
+
+    const int nst = (int)(p.dpad / BS_K);
+    issue(0, 0, 0, GPW);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+
+    if constexpr (!M16) {
+        const int h = lane >> 5, l32 = lane & 31;
+        f32x16 acc[2][QB];
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < QB; ++j) acc[i][j] = f32x16{0};
+        const int ra0 = wr * 64 + l32;
+        const int rq0 = wq * 32 * QB + l32;
+        for (int s = 0; s < nst; ++s) {
+            const bool more = s + 1 < nst;
+            if (!SPLIT_ISSUE && more) issue(s + 1, (s + 1) & 1, 0, GPW);
+            const unsigned char *st = lds[s & 1];
+            if (PRIO) __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int kk = 0; kk < BS_K / 16; ++kk) {
+                const int c = 2 * kk + h;
+                bf16x8 ah[2], al[2], bh[QB], bl[QB];
+#pragma unroll
+                for (int i = 0; i < 2; ++i) {
+                    ah[i] = frag(st, OFF_YH, ra0 + 32 * i, c);
+                    if (SPLIT == 3) al[i] = frag(st, OFF_YL, ra0 + 32 * i, c);
+                }
+#pragma unroll
+                for (int j = 0; j < QB; ++j) {
+                    bh[j] = frag(st, OFF_QH, rq0 + 32 * j, c);
+                    if (SPLIT == 3) bl[j] = frag(st, OFF_QL, rq0 + 32 * j, c);
+                }
+                issue_part(more, s, kk);
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int j = 0; j < QB; ++j) {
+                        acc[i][j] = mma32(ah[i], bh[j], acc[i][j]);
+                        if (SPLIT == 3) {
+                            acc[i][j] = mma32(ah[i], bl[j], acc[i][j]);
+                            acc[i][j] = mma32(al[i], bh[j], acc[i][j]);
+                        }
+                    }
+            }
+            if (PRIO) __builtin_amdgcn_s_setprio(0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+#pragma unroll
+        for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+            for (int jb = 0; jb < QB; ++jb) {
+                const int j = q0 + rq0 + jb * 32;
+                if (j >= p.nq) continue;
+                const int64_t rbase = r0 + wr * 64 + rb * 32 + 4 * h;
+                emit_vals<METRIC, PROBE, 16>(
+                    p, j, r1, [&](int r) { return rbase + (r & 3) + 8 * (r >> 2); },
+                    [&](int r) { return acc[rb][jb][r]; });
+            }
+    } else {
+        // 16x16x32: lane -> row (lane & 15) of a 16-row block, chunk lane >> 4
+        constexpr int QB16 = 2 * QB;  // 16-query blocks per wave
+        const int l16 = lane & 15, c = lane >> 4;
+        f32x4 acc[4][QB16];
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int j = 0; j < QB16; ++j) acc[i][j] = f32x4{0};
+        const int ra0 = wr * 64 + l16;
+        const int rq0 = wq * 32 * QB + l16;
+        for (int s = 0; s < nst; ++s) {
+            const bool more = s + 1 < nst;
+            if (!SPLIT_ISSUE && more) issue(s + 1, (s + 1) & 1, 0, GPW);
+            const unsigned char *st = lds[s & 1];
+            if (PRIO) __builtin_amdgcn_s_setprio(1);
+            bf16x8 ah[4], al[4];
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                ah[i] = frag(st, OFF_YH, ra0 + 16 * i, c);
+                if (SPLIT == 3) al[i] = frag(st, OFF_YL, ra0 + 16 * i, c);
+            }
+#pragma unroll
+            for (int hf = 0; hf < 2; ++hf) {
+                bf16x8 bh[QB], bl[QB];
+#pragma unroll
+                for (int jj = 0; jj < QB; ++jj) {
+                    bh[jj] = frag(st, OFF_QH, rq0 + 16 * (hf * QB + jj), c);
+                    if (SPLIT == 3) bl[jj] = frag(st, OFF_QL, rq0 + 16 * (hf * QB + jj), c);
+                }
+                issue_part(more, s, hf);
+#pragma unroll
+                for (int i = 0; i < 4; ++i)
+#pragma unroll
+                    for (int jj = 0; jj < QB; ++jj) {
+                        f32x4 &a = acc[i][hf * QB + jj];
+                        a = mma16(ah[i], bh[jj], a);
+                        if (SPLIT == 3) {
+                            a = mma16(ah[i], bl[jj], a);
+                            a = mma16(al[i], bh[jj], a);
+                        }
+                    }
+            }
+            if (PRIO) __builtin_amdgcn_s_setprio(0);
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+            __syncthreads();
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int jb = 0; jb < QB16; ++jb) {
+                const int j = q0 + rq0 + jb * 16;
+                if (j >= p.nq) continue;
+                const int64_t rbase = r0 + wr * 64 + i * 16 + 4 * c;
+                emit_vals<METRIC, PROBE, 4>(
+                    p, j, r1, [&](int r) { return rbase + r; }, [&](int r) { return acc[i][jb][r]; });
+            }
+    }
+}
+
+// Deep-pipelined form (VAR bit 8): K staged 16 deep (32 B per row per plane,
+// one v_mfma_f32_32x32x16_bf16 k-step per stage) in a ring of 4 stage buffers
+// with 3 stages in flight: the wave waits with a counted vmcnt for its pieces
+// of stage s only, then a raw s_barrier (no vmcnt(0) drain) publishes the
+// stage.  Chunk c of image row r (32-B rows) sits at slot c ^ ((r >> 3) & 1):
+// the 16 rows of a ds_read_b128 lane group land on 16 distinct bank slots.
+template <int METRIC, bool PROBE, int SPLIT, int WQ, int QB, int VAR>
+__global__ __launch_bounds__(256 * WQ) void k_scan_bf16_deep(ScanParams p) {
+    constexpr bool PRIO = VAR & 1;
+    constexpr int WR = 4, NW = WR * WQ, QT = 32 * QB * WQ;
+    constexpr int PL = (SPLIT == 3) ? 2 : 1;
+    constexpr int KD = 16, ROWB = 32, NBUF = 4;
+    constexpr int GY = BS_RT / 32;          // 1-KiB pieces (32 rows) per Y plane
+    constexpr int GQ = QT / 32;
+    constexpr int G = PL * (GY + GQ);
+    constexpr int GPW = G / NW;
+    static_assert(G % NW == 0, "stage pieces must split evenly over the waves");
+    constexpr int STAGE = G * 1024;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[NBUF][STAGE];
+
+    const int64_t L = p.tiles * p.num_qblocks;
+    const int64_t cpx = (L + 7) / 8;
+    const int64_t b = blockIdx.x;
+    const int64_t l = (b % 8) * cpx + b / 8;
+    if (l >= L) return;
+    const int64_t ti = l / p.num_qblocks;
+    const int qb = (int)(l % p.num_qblocks);
+    int64_t r0, r1, chunk;
+    tile_range(p, ti, r0, r1, chunk);
+    if (r0 >= r1) return;
+    const int ord = chunk_ordinal(p, chunk);
+    const int t = threadIdx.x;
+    const int lane = t & 63, w = t >> 6;
+    const int wr = w % WR, wq = w / WR;
+    const int q0 = qb * QT;
+    if (ord < 0) {
+        if (PROBE) {
+            for (int i = t; i < BS_RT * QT; i += 64 * NW) {
+                const int64_t row = r0 + (i % BS_RT);
+                const int j = q0 + i / BS_RT;
+                if (row < r1 && j < p.nq) emit_approx<METRIC, true>(p, j, row, false, 0.f);
+            }
+        }
+        return;
+    }
+
+    const uint16_t *src[GPW];
+#pragma unroll
+    for (int i = 0; i < GPW; ++i) {
+        const int g = w + i * NW;
+        int pl, rbase;
+        if (g < PL * GY) {
+            pl = g / GY;
+            rbase = (g % GY) * 32;
+        } else {
+            pl = 2 + (g - PL * GY) / GQ;
+            rbase = ((g - PL * GY) % GQ) * 32;
+        }
+        const int r = rbase + (lane >> 1);
+        const int c = (lane & 1) ^ ((r >> 3) & 1);
+        if (pl < 2) {
+            int64_t gr = r0 + r;
+            if (gr >= r1) gr = r0;
+            src[i] = (pl == 0 ? p.rows_hi : p.rows_lo) + gr * p.dpad + c * 8;
+        } else {
+            int j = q0 + r;
+            if (j >= p.nq) j = 0;
+            const int64_t qo = ((int64_t)j * p.maxv + variant_of(p, j, ord)) * p.dpad + c * 8;
+            src[i] = (pl == 2 ? p.q_hi : p.q_lo) + qo;
+        }
+    }
+    auto issue = [&](int s) {
+        const int64_t k0 = (int64_t)s * KD;
+        unsigned char *dst = lds[s % NBUF];
+#pragma unroll
+        for (int i = 0; i < GPW; ++i)
+            __builtin_amdgcn_global_load_lds((const void *)(src[i] + k0),
+                                             (lds_void *)&dst[(w + i * NW) * 1024], 16, 0, 0);
+    };
+    constexpr int OFF_YH = 0;
+    constexpr int OFF_YL = GY * 1024;
+    constexpr int OFF_QH = PL * GY * 1024;
+    constexpr int OFF_QL = OFF_QH + GQ * 1024;
+    const int h = lane >> 5, l32 = lane & 31;
+    auto frag = [&](const unsigned char *st, int off, int r) {
+        return *reinterpret_cast<const bf16x8 *>(st + off + r * ROWB + ((h ^ ((r >> 3) & 1)) * 16));
+    };
+
+    f32x16 acc[2][QB];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < 2; ++j) {
-            acc[i][j] = f32x16{0};
-            cor[i][j] = f32x16{0};
+        for (int j = 0; j < QB; ++j) acc[i][j] = f32x16{0};
+    const int ra0 = wr * 64 + l32;
+    const int rq0 = wq * 32 * QB + l32;
+    const int nst = (int)(p.dpad / KD);
+
+    // fragments of one stage (registers); two sets alternate so the reads of
+    // stage s+1 overlap the MFMAs of stage s
+    struct Frags {
+        bf16x8 ah[2], al[2], bh[QB], bl[QB];
+    };
+    auto read = [&](Frags &f, int s) {
+        const unsigned char *st = lds[s % NBUF];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) {
+            f.ah[i] = frag(st, OFF_YH, ra0 + 32 * i);
+            if (SPLIT == 3) f.al[i] = frag(st, OFF_YL, ra0 + 32 * i);
         }
-    const int nst = (int)(p.dpad / BS_K);
-    int ra[2], rq[2];
-    ra[0] = wr * 64 + l32;
-    ra[1] = ra[0] + 32;
-    rq[0] = wq * 64 + l32;
-    rq[1] = rq[0] + 32;
-    issue(0, 0);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    for (int s = 0; s < nst; ++s) {
-        if (s + 1 < nst) issue(s + 1, (s + 1) & 1);
-        const int bf = s & 1;
 #pragma unroll
-        for (int kk = 0; kk < BS_K / 16; ++kk) {
-            const int c = 2 * kk + h;
-            bf16x8 ah[2], al[2], bh[2], bl[2];
+        for (int j = 0; j < QB; ++j) {
+            f.bh[j] = frag(st, OFF_QH, rq0 + 32 * j);
+            if (SPLIT == 3) f.bl[j] = frag(st, OFF_QL, rq0 + 32 * j);
+        }
+    };
+    auto compute = [&](const Frags &f) {
+        if (PRIO) __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-            for (int i = 0; i < 2; ++i) {
-                ah[i] = *reinterpret_cast<const bf16x8 *>(&lds[bf][0][ra[i] * BS_ROWB + swz4(ra[i], c) * 16]);
-                bh[i] = *reinterpret_cast<const bf16x8 *>(&lds[bf][2][rq[i] * BS_ROWB + swz4(rq[i], c) * 16]);
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int j = 0; j < QB; ++j) {
+                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.ah[i], f.bh[j], acc[i][j], 0, 0, 0);
                 if (SPLIT == 3) {
-                    al[i] = *reinterpret_cast<const bf16x8 *>(&lds[bf][1][ra[i] * BS_ROWB + swz4(ra[i], c) * 16]);
-                    bl[i] = *reinterpret_cast<const bf16x8 *>(&lds[bf][3][rq[i] * BS_ROWB + swz4(rq[i], c) * 16]);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.ah[i], f.bl[j], acc[i][j], 0, 0, 0);
+                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.al[i], f.bh[j], acc[i][j], 0, 0, 0);
                 }
             }
-#pragma unroll
-            for (int i = 0; i < 2; ++i)
-#pragma unroll
-                for (int j = 0; j < 2; ++j) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[j], acc[i][j], 0, 0, 0);
-                    if (SPLIT == 3) {
-                        cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bl[j], cor[i][j], 0, 0, 0);
-                        cor[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(al[i], bh[j], cor[i][j], 0, 0, 0);
-                    }
-                }
-        }
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __syncthreads();
-    }
+        if (PRIO) __builtin_amdgcn_s_setprio(0);
+    };
+    // publish stage s: this wave's pieces of s have landed (only pieces of
+    // later stages stay in flight: `later` of them, 0..2), then the barrier
+    auto publish = [&](int later) {
+        if (later >= 2)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GPW) : "memory");
+        else if (later == 1)
+            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory");
+        else
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __builtin_amdgcn_s_barrier();
+    };
+    // one step: publish stage s+1, refill the ring (stage s+3 goes into the
+    // buffer of stage s-1, which every wave finished before this barrier),
+    // read stage s+1's fragments into `nx` while stage s (in `cu`) computes
+    // The reads are unconditional (the step after the last stage reads a
+    // stale buffer into registers nobody uses), so hipcc's lgkmcnt bookkeeping
+    // stays exact across the barrier; nst = dpad / 16 is even (dpad % 64 == 0).
+    auto step = [&](int s, Frags &cu, Frags &nx) {
+        publish(s + 2 < nst ? 1 : 0);
+        if (s + 3 < nst) issue(s + 3);
+        read(nx, s + 1);
+        compute(cu);
+    };
 
+    for (int s = 0; s < NBUF - 1 && s < nst; ++s) issue(s);
+    publish(min(nst - 1, 2));
+    Frags fa, fb;
+    read(fa, 0);
+    for (int s = 0; s < nst; s += 2) {
+        step(s, fa, fb);
+        step(s + 1, fb, fa);
+    }
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
 #pragma unroll
-        for (int qb2 = 0; qb2 < 2; ++qb2) {
-            const int j = q0 + wq * 64 + qb2 * 32 + l32;
+        for (int jb = 0; jb < QB; ++jb) {
+            const int j = q0 + rq0 + jb * 32;
             if (j >= p.nq) continue;
-            const float qn = (METRIC == MQVS_METRIC_L2) ? p.qnorms[j] : 0.f;
-#pragma unroll
-            for (int r = 0; r < 16; ++r) {
-                const int il = wr * 64 + rb * 32 + (r & 3) + 8 * (r >> 2) + 4 * h;
-                const int64_t row = r0 + il;
-                if (row >= r1) continue;
-                const float ip = (SPLIT == 3) ? acc[rb][qb2][r] + cor[rb][qb2][r] : acc[rb][qb2][r];
-                float raw = ip;
-                if (METRIC == MQVS_METRIC_L2) {
-                    raw = (qn + p.row_norms[row]) - 2.0f * ip;
-                    if (raw < 0) raw = 0;
-                }
-                emit_approx<METRIC, PROBE>(p, j, row, row_valid(p, row), raw);
-            }
+            const int64_t rbase = r0 + wr * 64 + rb * 32 + 4 * h;
+            emit_vals<METRIC, PROBE, 16>(
+                p, j, r1, [&](int r) { return rbase + (r & 3) + 8 * (r >> 2); },
+                [&](int r) { return acc[rb][jb][r]; });
         }
+}
+
+template <int METRIC, bool PROBE, int SPLIT, int WQ, int QB, int VAR>
+static void launch_shape(ScanParams p, hipStream_t s) {
+    constexpr int QT = 32 * QB * WQ;
+    p.num_qblocks = (p.nq + QT - 1) / QT;
+    const int64_t L = p.tiles * p.num_qblocks;
+    if (L < 1) return;
+    const int64_t grid = (L + 7) / 8 * 8;
+    if constexpr ((VAR & 8) != 0)
+        hipLaunchKernelGGL((k_scan_bf16_deep<METRIC, PROBE, SPLIT, WQ, QB, VAR>), dim3((unsigned)grid),
+                           dim3(256 * WQ), 0, s, p);
+    else
+        hipLaunchKernelGGL((k_scan_bf16<METRIC, PROBE, SPLIT, WQ, QB, VAR>), dim3((unsigned)grid),
+                           dim3(256 * WQ), 0, s, p);
+}
+
+// Tuning override (tools/tune_bf16.py, cosine APPEND split-3 launches only):
+// MQVS_BF16_TUNE="WQ,QB,VAR" picks the workgroup shape and schedule variant.
+static bool tune_override(int &wq, int &qb, int &var) {
+    const char *e = std::getenv("MQVS_BF16_TUNE");
+    if (!e || !*e) return false;
+    return std::sscanf(e, "%d,%d,%d", &wq, &qb, &var) == 3;
+}
+
+template <int METRIC, bool PROBE, int SPLIT>
+static bool launch_tuned(const ScanParams &p, hipStream_t s) {
+    int wq, qb, var;
+    if (!tune_override(wq, qb, var)) return false;
+    const int key = wq * 100 + qb * 10 + var;
+    switch (key) {
+#define MQVS_TUNE_CASE(WQ_, QB_, V_) \
+    case WQ_ * 100 + QB_ * 10 + V_: launch_shape<METRIC, PROBE, SPLIT, WQ_, QB_, V_>(p, s); return true;
+        MQVS_TUNE_CASE(1, 2, 0) MQVS_TUNE_CASE(1, 2, 4) MQVS_TUNE_CASE(1, 2, 7)
+        MQVS_TUNE_CASE(2, 1, 0) MQVS_TUNE_CASE(2, 1, 4) MQVS_TUNE_CASE(2, 1, 7)
+        MQVS_TUNE_CASE(1, 4, 0) MQVS_TUNE_CASE(1, 4, 4) MQVS_TUNE_CASE(1, 4, 7)
+        MQVS_TUNE_CASE(2, 2, 0) MQVS_TUNE_CASE(2, 2, 4) MQVS_TUNE_CASE(2, 2, 7)
+        MQVS_TUNE_CASE(2, 4, 0) MQVS_TUNE_CASE(2, 4, 4) MQVS_TUNE_CASE(2, 4, 7)
+        MQVS_TUNE_CASE(2, 4, 8)
+#undef MQVS_TUNE_CASE
+        default: return false;
+    }
+}
+
+template <int METRIC, bool PROBE, int SPLIT>
+static void launch_split(const ScanParams &p, hipStream_t s) {
+    if constexpr (METRIC == MQVS_METRIC_COSINE && !PROBE && SPLIT == 3)
+        if (launch_tuned<METRIC, PROBE, SPLIT>(p, s)) return;
+    // shapes and variants measured with tools/tune_bf16.py (10M x 768 cosine):
+    // nq 64: 6.15 ms (HBM ~5 TB/s), nq 128: 7.6 ms, nq 1000: 36.1 ms (1.27 PF/s)
+    if (p.nq <= 64)  // (split 1 has 20 pieces per stage: 4 waves)
+        launch_shape<METRIC, PROBE, SPLIT, SPLIT == 3 ? 2 : 1, SPLIT == 3 ? 1 : 2, 7>(p, s);
+    else if (p.nq <= 128)
+        launch_shape<METRIC, PROBE, SPLIT, 2, 2, 7>(p, s);
+    else
+        launch_shape<METRIC, PROBE, SPLIT, 2, 4, 7>(p, s);
 }
 
 template <int METRIC, bool PROBE>
 static void launch_bf16_t(const ScanParams &p, int split, hipStream_t s) {
-    const int64_t L = p.tiles * p.num_qblocks;
-    if (L < 1) return;
-    const int64_t grid = (L + 7) / 8 * 8;
     if (split == 3)
-        hipLaunchKernelGGL((k_scan_bf16<METRIC, PROBE, 3>), dim3((unsigned)grid), dim3(256), 0, s, p);
+        launch_split<METRIC, PROBE, 3>(p, s);
     else
-        hipLaunchKernelGGL((k_scan_bf16<METRIC, PROBE, 1>), dim3((unsigned)grid), dim3(256), 0, s, p);
+        launch_split<METRIC, PROBE, 1>(p, s);
 }
 
 void launch_scan_bf16(const ScanParams &p, int metric, bool probe, int split, hipStream_t s) {

@@ -71,6 +71,8 @@ struct DevBuf {
 struct Workspace {
     hipStream_t stream = nullptr;
     hipEvent_t ev[6] = {};
+    static constexpr int kSegEv = 64;
+    hipEvent_t seg_ev[kSegEv] = {};  // per main-scan segment: start, end
     DevBuf queries, qvars, qnorms, qmu, qlam, status, filter, exists, ord, probe, tau, count, cand,
         overflow, out_ids, out_dist, misc, qhi, bq, thr, cand2, count2;
     int *host_flags = nullptr;  // pinned
@@ -78,6 +80,7 @@ struct Workspace {
         if (stream) return;
         MQVS_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         for (auto &e : ev) MQVS_HIP(hipEventCreate(&e));
+        for (auto &e : seg_ev) MQVS_HIP(hipEventCreate(&e));
         MQVS_HIP(hipHostMalloc((void **)&host_flags, 64 * sizeof(int), hipHostMallocDefault));
     }
     void release() {
@@ -88,6 +91,8 @@ struct Workspace {
         if (host_flags) (void)hipHostFree(host_flags);
         host_flags = nullptr;
         for (auto &e : ev)
+            if (e) (void)hipEventDestroy(e);
+        for (auto &e : seg_ev)
             if (e) (void)hipEventDestroy(e);
         if (stream) (void)hipStreamDestroy(stream);
         stream = nullptr;
@@ -261,7 +266,7 @@ static void run_scan(ScanParams p, const Range &r, int kind, int metric, bool pr
     p.row_end = r.end;
     p.tiles = r.tiles;
     p.tiles_per_chunk = r.tiles_per_chunk;
-    p.tile_rows = kind == kScanSmall ? kSmallRows : kMfmaRows;
+    p.tile_rows = kind == kScanSmall ? kSmallRows : kind == kScanBf16 ? kBfRows : kMfmaRows;
     if (kind == kScanMfma32)
         launch_scan_mfma(p, metric, probe, st);
     else if (kind == kScanBf16)
@@ -362,7 +367,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         chunk_ord = seg->chunk_ord;
     }
     const bool aligned = cos || chunk_ord != nullptr;
-    const int64_t tile_rows = mfma ? kMfmaRows : kSmallRows;
+    const int64_t tile_rows = !mfma ? kSmallRows : kind == kScanBf16 ? kBfRows : kMfmaRows;
 
     // ---- candidate capacity per query (a fixed budget spread over the
     // batch) and probe size: expected candidates ~ k*n/P; aim at cap/3
@@ -451,7 +456,10 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         int segs = 0;
         while (b < n) {
             const int64_t e = std::min(n, round_up(b + seg_rows, align));
+            const bool tev = timing && 2 * segs + 1 < Workspace::kSegEv;
+            if (tev) MQVS_HIP(hipEventRecord(ws.seg_ev[2 * segs], s));
             run_scan(p, make_range(b, e, tile_rows, seg->granule, aligned), kind, metric, false, s);
+            if (tev) MQVS_HIP(hipEventRecord(ws.seg_ev[2 * segs + 1], s));
             b = e;
             seg_rows *= 2;
             ++segs;
@@ -528,7 +536,16 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
             MQVS_HIP(hipEventElapsedTime(&f, ws.ev[0], ws.ev[4]));
             st.probe_ms = a;
             st.probe_select_ms = b;
-            st.main_ms = c;
+            // main_ms: the scan kernels only; refine_ms: the refinements between
+            float scan = 0.f;
+            const int ns = std::min(st.segments, Workspace::kSegEv / 2);
+            for (int i = 0; i < ns; ++i) {
+                float x = 0.f;
+                MQVS_HIP(hipEventElapsedTime(&x, ws.seg_ev[2 * i], ws.seg_ev[2 * i + 1]));
+                scan += x;
+            }
+            st.main_ms = ns > 0 ? scan : c;
+            st.refine_ms = ns > 0 ? c - scan : 0.0;
             st.final_ms = e;
             st.total_ms = f;
         }

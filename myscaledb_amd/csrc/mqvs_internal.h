@@ -20,6 +20,7 @@ constexpr int64_t kCandMax = 1 << 20;     // candidate slots per query
 constexpr int kSmallRows = 256;      // rows per tile, VALU scan
 constexpr int kMfmaRows = 128;       // rows per tile, MFMA scan
 constexpr int kMfmaQ = 128;          // queries per tile, MFMA scan
+constexpr int kBfRows = 256;         // rows per tile, bf16 MFMA scan (kernels_bf16_scan.hip)
 // Internal metric id: raw faiss inner product (knn_inner_product: every
 // ip > -FLT_MAX enters the heap), used by mqvs_knn_raw only.  The operator
 // path (mqvs_search) applies searchWrapper's FLT_MIN cut instead.

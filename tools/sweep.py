@@ -47,7 +47,9 @@ def main():
                 "metric": metric, "nq": nq, "wall_ms": round(min(walls), 3),
                 "qps": round(nq / (min(walls) / 1e3), 1),
                 "probe_ms": round(st["probe_ms"], 3), "probe_select_ms": round(st["probe_select_ms"], 3),
-                "main_ms": round(st["main_ms"], 3), "final_ms": round(st["final_ms"], 3),
+                "main_ms": round(st["main_ms"], 3), "refine_ms": round(st["refine_ms"], 3),
+                "final_ms": round(st["final_ms"], 3),
+                "main_bf16x3_TFLOPs": round(3 * tfs, 1),
                 "total_ms": round(st["total_ms"], 3), "probe_rows": st["probe_rows"],
                 "main_GBps": round(gbs, 1), "main_hbm_frac": round(gbs / 8000.0, 3),
                 "main_TFLOPs": round(tfs, 2), "main_fp32_frac": round(tfs / 157.3, 3),

@@ -1,0 +1,67 @@
+#!/usr/bin/env python3
+"""A/B workgroup shapes / schedule variants of the bf16 scan in ONE process
+(interleaved rounds), on the bench workload (10M x 768 cosine, nq=1000 by
+default).  A config is "WQ,QB,VAR" (kernels_bf16_scan.hip, MQVS_BF16_TUNE).
+Every config must return the same bits as the first.  Prints one JSON line
+per config: min / median main-scan ms and the bf16x3 TFLOP/s."""
+import argparse
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--n", type=int, default=10_000_000)
+    ap.add_argument("--d", type=int, default=768)
+    ap.add_argument("--nq", type=int, default=1000)
+    ap.add_argument("--k", type=int, default=100)
+    ap.add_argument("--configs", default="2,4,0;2,4,4;2,4,7")
+    ap.add_argument("--rounds", type=int, default=5)
+    args = ap.parse_args()
+    import torch
+    import myscaledb_amd as mq
+    from myscaledb_amd import _lib
+    from myscaledb_amd.vector_scan import generate_device, set_timing
+    mq.init(0)
+    seg = mq.VectorScanSegment.generate(0x5EED0001, 2, args.n, args.d, "Cosine", 8192)
+    q = torch.empty((args.nq, args.d), dtype=torch.float32, device="cuda")
+    generate_device(0x5EED0002, 2, 0, args.nq, args.d, q)
+    variants = args.configs.split(";")
+    ref = None
+    times = {v: [] for v in variants}
+    rescans = {v: 0 for v in variants}
+    set_timing(True)
+    for rnd in range(args.rounds + 1):
+        for v in variants:
+            os.environ["MQVS_BF16_TUNE"] = v
+            ids, dist = seg.search(q, args.k)
+            st = _lib.last_search_stats()
+            rescans[v] += st["rescans"]
+            if ref is None:
+                ref = (ids.clone(), dist.clone())
+            elif not (torch.equal(ids, ref[0]) and torch.equal(dist, ref[1])):
+                print(json.dumps({"config": v, "error": "results differ from config %s" % variants[0]}),
+                      flush=True)
+                return 1
+            if rnd > 0:
+                times[v].append(st["main_ms"])
+        print(f"round {rnd} done", file=sys.stderr, flush=True)
+    set_timing(False)
+    flop = 3 * 2.0 * args.nq * (args.n - st["probe_rows"]) * args.d
+    for v in variants:
+        t = times[v]
+        print(json.dumps({"config": v, "nq": args.nq, "main_ms_min": round(min(t), 3),
+                          "main_ms_med": round(statistics.median(t), 3),
+                          "bf16x3_TFLOPs_med": round(flop / (statistics.median(t) * 1e-3) / 1e12, 1),
+                          "rescans": rescans[v]}), flush=True)
+    seg.free()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
