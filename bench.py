@@ -12,7 +12,6 @@ Prints ONE JSON line on rank 0 (see the driver contract in the task README).
 """
 import argparse
 import json
-import math
 import os
 import time
 
@@ -171,9 +170,8 @@ def main():
 
     mq.init(local)
     n, d, nq, k, g = args.n, args.d, args.nq, args.k, args.granule
-    nchunks = math.ceil(n / g)
-    c0, c1 = nchunks * rank // world, nchunks * (rank + 1) // world
-    r0, r1 = c0 * g, min(c1 * g, n)
+    from myscaledb_amd.sharded import shard_rows
+    r0, r1 = shard_rows(n, g, rank, world)
     seg = mq.VectorScanSegment.generate(SEED_BASE, args.mode, r1 - r0, d, args.metric, g, row_offset=r0)
     q = torch.empty((nq, d), dtype=torch.float32, device="cuda")
     generate_device(SEED_QUERY, args.mode, 0, nq, d, q)

@@ -129,18 +129,27 @@ int mqvs_search(mqvs_segment_t seg, const float *queries, int32_t nq, int32_t k,
 int mqvs_knn_raw(const float *x, const float *y, int64_t d, int64_t k, int64_t nx, int64_t ny,
                  int32_t metric, int64_t *result_id, float *distance);
 
-/* Exact re-rank of candidate ids (computeTopDistanceSubset contract): for
- * each query, distances to its ncand candidates (segment-local row ids, -1 =
- * none) with the brute-force formula for nq, then top-k as mqvs_search. */
+/* Exact re-rank of candidate rows (computeTopDistanceSubset contract,
+ * VIWithDataPart.cpp:838-856): cand is nq*ncand segment-local row ids (-1 or
+ * out-of-range = none; distinct rows per query), ncand <= 4096.  Each
+ * candidate gets the distance mqvs_search computes for the same batch size
+ * (nq < 20 sequential formula, else BLAS form; cosine with the row's chunk
+ * query variant); rows cleared in row_exists (LSB-first, n bits, or NULL)
+ * are skipped.  Output: top-k as mqvs_search (same order key and padding). */
 int mqvs_rerank(mqvs_segment_t seg, const float *queries, int32_t nq, const int64_t *cand,
-                int32_t ncand, int32_t k, int32_t metric, int64_t *out_ids, float *out_dist,
-                uint32_t flags, mqvs_stream_t stream);
+                int32_t ncand, int32_t k, int32_t metric, const uint8_t *row_exists,
+                int64_t *out_ids, float *out_dist, uint32_t flags, mqvs_stream_t stream);
 
-/* Merge per-shard top-k lists (row-range shards of one part, shard s holding
- * lower ids than shard s+1): in_ids/in_dist [nshards][nq][k] as returned by
- * mqvs_search on each shard; out nq*k.  Order: distance (desc for IP), then
- * shard, then position in the shard's list -- the reference's insertion-order
- * multimap merge. */
+/* Merge per-list top-k results: in_ids/in_dist [nshards][nq][k] as returned
+ * by mqvs_search; out nq*k (nshards * k <= 4096).
+ * Default (row-range shards of ONE part, shard s holding lower ids than shard
+ * s+1): order distance (desc for IP), then shard, then position -- the result
+ * equals the unsharded part's search.
+ * MQVS_F_PART_MERGE (lists = different data parts): the reference's cross-part
+ * merge MergeTreeBaseSearchManager::getTotalTopSearchResultImpl
+ * (MergeTreeBaseSearchManager.cpp:207-297), an insertion-ordered multimap read
+ * backwards for IP -- equal IP scores come out last-inserted first. */
+#define MQVS_F_PART_MERGE 0x4u
 int mqvs_merge_shards(int32_t nshards, int32_t nq, int32_t k, int32_t metric,
                       const int64_t *in_ids, const float *in_dist, int64_t *out_ids,
                       float *out_dist, uint32_t flags, mqvs_stream_t stream);

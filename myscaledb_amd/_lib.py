@@ -21,6 +21,7 @@ ERR_NOT_IMPLEMENTED, ERR_LOGICAL, ERR_ILLEGAL_COLUMN, ERR_BAD_ARGUMENTS, ERR_MEM
     ERR_DEVICE = 1, 2, 3, 4, 5, 6
 F_DEVICE_PTRS = 0x1
 F_ASYNC = 0x2
+F_PART_MERGE = 0x4
 
 # Exported C symbols: every one of these is declared in include/mqvs.h.
 SYMBOLS = [
@@ -78,7 +79,7 @@ def _load():
         "mqvs_segment_rows": ([P, P], ctypes.c_int),
         "mqvs_search": ([P, P, I32, I32, I32, P, P, P, P, U32, P], ctypes.c_int),
         "mqvs_knn_raw": ([P, P, I64, I64, I64, I64, I32, P, P], ctypes.c_int),
-        "mqvs_rerank": ([P, P, I32, P, I32, I32, I32, P, P, U32, P], ctypes.c_int),
+        "mqvs_rerank": ([P, P, I32, P, I32, I32, I32, P, P, P, U32, P], ctypes.c_int),
         "mqvs_merge_shards": ([I32, I32, I32, I32, P, P, P, P, U32, P], ctypes.c_int),
         "mqvs_generate_device": ([U64, I32, I64, I64, I32, P, P], ctypes.c_int),
         "mqvs_last_search_stats": ([P], ctypes.c_int),

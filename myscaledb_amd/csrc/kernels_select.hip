@@ -138,12 +138,16 @@ __global__ __launch_bounds__(SEL_THREADS) void k_final_select(const Cand *cand,
     }
 }
 
-// Merge of per-shard result lists: key (distance, shard, position).
+// Merge of per-list results: key (distance, list, position).  rev_ties (IP
+// cross-PART merge, MergeTreeBaseSearchManager.cpp:207-297): the reference
+// walks its insertion-ordered multimap backwards for DESC, so equal scores
+// come out last-inserted first -> key (distance, ~list, ~position).
 template <int METRIC>
 __global__ __launch_bounds__(SEL_THREADS) void k_merge_shards(int nshards, int nq, int k,
                                                              const int64_t *in_ids,
                                                              const float *in_dist,
-                                                             int64_t *out_ids, float *out_dist) {
+                                                             int64_t *out_ids, float *out_dist,
+                                                             int rev_ties) {
     extern __shared__ __attribute__((aligned(16))) uint4 recs[];
     const int q = blockIdx.x;
     const int n = nshards * k;
@@ -157,8 +161,8 @@ __global__ __launch_bounds__(SEL_THREADS) void k_merge_shards(int nshards, int n
             if (in_ids[off] >= 0) {
                 const float v = in_dist[off];
                 r.x = (METRIC == MQVS_METRIC_IP || METRIC == kMetricIpRaw) ? ~ord_asc(v) : ord_asc(v);
-                r.y = (uint32_t)s;
-                r.z = (uint32_t)pos;
+                r.y = rev_ties ? ~(uint32_t)s : (uint32_t)s;
+                r.z = rev_ties ? ~(uint32_t)pos : (uint32_t)pos;
                 r.w = (uint32_t)i;
             }
         }
@@ -243,16 +247,18 @@ void launch_final_select(const Cand *cand, const int *cand_count, int cand_cap, 
 
 template <int M>
 static void merge_shards_t(int nshards, int nq, int k, const int64_t *in_ids, const float *in_dist,
-                           int64_t *out_ids, float *out_dist, hipStream_t s) {
+                           int64_t *out_ids, float *out_dist, int rev_ties, hipStream_t s) {
     hipLaunchKernelGGL(k_merge_shards<M>, dim3(nq), dim3(SEL_THREADS), sort_lds(nshards * k), s,
-                       nshards, nq, k, in_ids, in_dist, out_ids, out_dist);
+                       nshards, nq, k, in_ids, in_dist, out_ids, out_dist, rev_ties);
 }
 
 void launch_merge_shards(int nshards, int nq, int k, int metric, const int64_t *in_ids,
-                         const float *in_dist, int64_t *out_ids, float *out_dist, hipStream_t s) {
+                         const float *in_dist, int64_t *out_ids, float *out_dist, bool part_merge,
+                         hipStream_t s) {
     if (nq <= 0) return;
+    const int rev = part_merge && (metric == MQVS_METRIC_IP || metric == kMetricIpRaw);
     MQVS_DISPATCH_METRIC(metric, merge_shards_t,
-                         (nshards, nq, k, in_ids, in_dist, out_ids, out_dist, s));
+                         (nshards, nq, k, in_ids, in_dist, out_ids, out_dist, rev, s));
 }
 
 // ---------------------------------------------------------------------------

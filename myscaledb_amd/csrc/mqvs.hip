@@ -553,6 +553,98 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     g_stats = st;
 }
 
+// Exact re-rank of caller-given candidate rows (computeTopDistanceSubset
+// contract, VIWithDataPart.cpp:838-856): the distance formula and cosine
+// query variant mqvs_search uses for the same batch size, then top-k by the
+// reference key.  Rows < 0, >= n or deleted (row_exists) are skipped; the
+// candidate list of a query is expected to hold distinct rows.
+static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const int64_t *cand,
+                        int ncand, int k, int metric, const uint8_t *exists, int64_t *out_ids,
+                        float *out_dist, uint32_t flags, hipStream_t user_stream) {
+    if (!seg) fail(MQVS_ERR_BAD_ARGUMENTS, "null segment");
+    if (nq < 0 || k < 0 || ncand < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "nq, k and ncand must be non-negative");
+    const bool cos = metric == MQVS_METRIC_COSINE;
+    if (metric != MQVS_METRIC_L2 && metric != MQVS_METRIC_IP && !cos)
+        fail(MQVS_ERR_NOT_IMPLEMENTED, "Metric not implemented in brute force search for Float32 Vector");
+    if (cos != (seg->metric == MQVS_METRIC_COSINE))
+        fail(MQVS_ERR_LOGICAL, "segment was prepared for a different metric");
+    if (k > kSortCap || ncand > kSortCap)
+        fail(MQVS_ERR_BAD_ARGUMENTS, "k and ncand must not exceed " + std::to_string(kSortCap));
+    if (nq > 0 && k > 0 && (!queries || !out_ids || !out_dist || (ncand > 0 && !cand)))
+        fail(MQVS_ERR_BAD_ARGUMENTS, "null query, candidate or output pointer");
+    g_stats = mqvs_search_stats{};
+    if (nq == 0 || k == 0) return;
+
+    DeviceGuard guard(seg->device);
+    Workspace &ws = workspace(seg->device);
+    hipStream_t s = user_stream ? (hipStream_t)user_stream : ws.stream;
+    const bool dev = flags & MQVS_F_DEVICE_PTRS;
+    const int d = seg->d;
+    const float *dq = queries;
+    const int64_t *dc = cand;
+    const uint8_t *dexists = exists;
+    int64_t *dids = out_ids;
+    float *ddist = out_dist;
+    if (!dev) {
+        float *q = (float *)ws.queries.get(sizeof(float) * (size_t)nq * d);
+        MQVS_HIP(hipMemcpyAsync(q, queries, sizeof(float) * (size_t)nq * d, hipMemcpyHostToDevice, s));
+        dq = q;
+        int64_t *c = (int64_t *)ws.misc.get(sizeof(int64_t) * std::max<size_t>((size_t)nq * ncand, 1));
+        if (ncand > 0)
+            MQVS_HIP(hipMemcpyAsync(c, cand, sizeof(int64_t) * (size_t)nq * ncand, hipMemcpyHostToDevice, s));
+        dc = c;
+        if (exists) {
+            const int64_t bm = (seg->n + 7) / 8;
+            auto *f = (uint8_t *)ws.exists.get(bm);
+            MQVS_HIP(hipMemcpyAsync(f, exists, bm, hipMemcpyHostToDevice, s));
+            dexists = f;
+        }
+        dids = (int64_t *)ws.out_ids.get(sizeof(int64_t) * (size_t)nq * k);
+        ddist = (float *)ws.out_dist.get(sizeof(float) * (size_t)nq * k);
+    }
+    const bool blas = nq >= kBlasThreshold;
+    const int maxv = cos ? kMaxVariants : 1;
+    const int64_t qstride = round_up(d, 32);
+    float *qvars = (float *)ws.qvars.get(sizeof(float) * (size_t)nq * maxv * qstride);
+    MQVS_HIP(hipMemsetAsync(qvars, 0, sizeof(float) * (size_t)nq * maxv * qstride, s));
+    float *qnorms = (float *)ws.qnorms.get(sizeof(float) * nq);
+    int *qmu = (int *)ws.qmu.get(sizeof(int) * nq);
+    int *qlam = (int *)ws.qlam.get(sizeof(int) * nq);
+    int *status = (int *)ws.status.get(sizeof(int) * 4);
+    MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
+    launch_query_prep(dq, nq, d, cos ? MQVS_METRIC_COSINE : MQVS_METRIC_L2, blas && metric == MQVS_METRIC_L2,
+                      qvars, qnorms, qmu, qlam, status, s);
+    MQVS_HIP(hipGetLastError());
+
+    ScanParams p{};
+    p.rows = seg->rows;
+    p.row_norms = seg->norms;
+    p.n = seg->n;
+    p.d = d;
+    p.nq = nq;
+    p.qvars = qvars;
+    p.qnorms = qnorms;
+    p.qmu = qmu;
+    p.qlam = qlam;
+    p.maxv = maxv;
+    p.chunk_rows = seg->granule;
+    p.chunk_ord = seg->chunk_ord;
+    p.ord_base = (int)(seg->row_offset / seg->granule);
+    p.exists = dexists;
+    p.nonempty = seg->nonempty_bits;
+    launch_rerank_ids(p, metric, dc, ncand, k, seg->row_offset, dids, ddist, s);
+    MQVS_HIP(hipGetLastError());
+    if (dev && (flags & MQVS_F_ASYNC)) return;
+    MQVS_HIP(hipMemcpyAsync(ws.host_flags, status, sizeof(int), hipMemcpyDeviceToHost, s));
+    MQVS_HIP(hipStreamSynchronize(s));
+    if (ws.host_flags[0]) fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not reach a cycle");
+    if (!dev) {
+        MQVS_HIP(hipMemcpyAsync(out_ids, dids, sizeof(int64_t) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
+        MQVS_HIP(hipMemcpyAsync(out_dist, ddist, sizeof(float) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
+        MQVS_HIP(hipStreamSynchronize(s));
+    }
+}
+
 }  // namespace mqvs
 
 using namespace mqvs;
@@ -756,7 +848,7 @@ int mqvs_merge_shards(int32_t nshards, int32_t nq, int32_t k, int32_t metric, co
             di = bi;
             dd = bd;
         }
-        launch_merge_shards(nshards, nq, k, metric, di, dd, oi, od, s);
+        launch_merge_shards(nshards, nq, k, metric, di, dd, oi, od, (flags & MQVS_F_PART_MERGE) != 0, s);
         MQVS_HIP(hipGetLastError());
         if (!devp) {
             MQVS_HIP(hipMemcpyAsync(out_ids, oi, nout * 8, hipMemcpyDeviceToHost, s));
@@ -780,10 +872,13 @@ int mqvs_generate_device(uint64_t seed, int32_t mode, int64_t row0, int64_t n, i
     });
 }
 
-int mqvs_rerank(mqvs_segment_t, const float *, int32_t, const int64_t *, int32_t, int32_t, int32_t,
-                int64_t *, float *, uint32_t, mqvs_stream_t) {
-    set_error("mqvs_rerank: not implemented in this build");
-    return MQVS_ERR_NOT_IMPLEMENTED;
+int mqvs_rerank(mqvs_segment_t seg, const float *queries, int32_t nq, const int64_t *cand,
+                int32_t ncand, int32_t k, int32_t metric, const uint8_t *row_exists, int64_t *out_ids,
+                float *out_dist, uint32_t flags, mqvs_stream_t stream) {
+    return guarded([&] {
+        rerank_impl(seg, queries, nq, cand, ncand, k, metric, row_exists, out_ids, out_dist, flags,
+                    (hipStream_t)stream);
+    });
 }
 
 int mqvs_last_search_stats(mqvs_search_stats *out) {

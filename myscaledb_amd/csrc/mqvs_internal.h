@@ -166,6 +166,8 @@ __device__ inline bool row_valid(const ScanParams &p, int64_t r) {
 // ---------------------------------------------------------------------------
 // Launchers (kernels_*.hip)
 void launch_scan_small(const ScanParams &p, int metric, bool probe, hipStream_t s);
+void launch_rerank_ids(const ScanParams &p, int metric, const int64_t *cand, int ncand, int k,
+                       int64_t id_offset, int64_t *out_ids, float *out_dist, hipStream_t s);
 void launch_scan_mfma(const ScanParams &p, int metric, bool probe, hipStream_t s);
 void launch_probe_select(const float *probe, int64_t P, int64_t ld, int nq, int k, int metric,
                          uint32_t *tau, int *cand_count, Cand *cand, int cand_cap,
@@ -176,7 +178,8 @@ void launch_final_select(const Cand *cand, const int *cand_count, int cand_cap, 
                          int metric, int64_t chunk_rows, int64_t id_offset, int64_t *out_ids,
                          float *out_dist, int *overflow, hipStream_t s);
 void launch_merge_shards(int nshards, int nq, int k, int metric, const int64_t *in_ids,
-                         const float *in_dist, int64_t *out_ids, float *out_dist, hipStream_t s);
+                         const float *in_dist, int64_t *out_ids, float *out_dist, bool part_merge,
+                         hipStream_t s);
 void launch_normalize_rows(float *rows, int64_t n, int d, hipStream_t s);
 void launch_row_norms(const float *rows, int64_t n, int d, float *norms, hipStream_t s);
 void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, float *qvars,
@@ -187,8 +190,6 @@ void launch_pack_nonempty(const uint8_t *bytes, int64_t n, uint8_t *bits, hipStr
 void launch_chunk_ordinals(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists,
                            int64_t n, int64_t chunk_rows, int require_filter, int *ord,
                            hipStream_t s);
-void launch_rerank(const ScanParams &p, const int64_t *cand_ids, int ncand, int metric,
-                   bool blas, hipStream_t s);
 
 // bf16 pre-filter path (kernels_bf16.hip)
 constexpr int kBfK = 64;    // bf16 planes padded to a multiple of this

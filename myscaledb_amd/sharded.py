@@ -1,0 +1,114 @@
+"""Row-range sharding of one data part over GPUs.
+
+One process per GPU (`torch.distributed`, backend "nccl" = RCCL over xGMI).
+Rank g owns the granule-aligned row range `shard_rows(n, granule, g, G)` of
+the part as its own resident segment (row_offset = range start, so ids are
+part-global and the cosine chunk ordinals continue across shards).  A search
+is a local top-k on every rank, ONE all-gather of the per-shard (ids, dist)
+lists (nq*k*12 bytes per rank), and a merge by distance, then shard (= row
+order), then position (mqvs_merge_shards).  The result equals the single-GPU
+search of the whole part -- a shard is not a data part, so the reference's
+cross-part multimap order (MergeTreeBaseSearchManager.cpp:207-297, which
+reverses exact IP ties between parts) is the wrong rule here; it is
+available as merge_shards(..., part_merge=True) for genuinely different parts.
+
+The local search and the merge are injectable so the decomposition can be
+exercised with the gloo backend on CPU (tests/test_sharded.py); the defaults
+are the HIP path (VectorScanSegment.search, mqvs_merge_shards).
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+
+
+def shard_rows(n: int, granule: int, rank: int, world: int) -> tuple[int, int]:
+    """[r0, r1) of rank's shard: whole granules, as even as possible."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError("bad rank / world size")
+    nchunks = math.ceil(n / granule) if n > 0 else 0
+    c0, c1 = nchunks * rank // world, nchunks * (rank + 1) // world
+    return min(c0 * granule, n), min(c1 * granule, n)
+
+
+def slice_bitmap(bits, n: int, r0: int, r1: int):
+    """Rows [r0, r1) of an LSB-first n-bit bitmap, re-packed from bit 0."""
+    if bits is None:
+        return None
+    b = np.asarray(bits, dtype=np.uint8)
+    if r0 % 8 == 0:
+        out = b[r0 // 8:(r1 + 7) // 8].copy()
+        tail = (r1 - r0) % 8
+        if tail and out.size:
+            out[-1] &= np.uint8((1 << tail) - 1)
+        return out
+    flat = np.unpackbits(b, bitorder="little")[:n]
+    return np.packbits(flat[r0:r1], bitorder="little")
+
+
+class ShardedScan:
+    """A part sharded over the ranks of a process group.
+
+    local_search(queries, k, filter_bits, row_exists_bits) -> (ids[nq,k], dist[nq,k])
+        ids part-global (the shard's row_offset applied), -1 padded
+    merge(ids[S,nq,k], dist[S,nq,k]) -> (ids[nq,k], dist[nq,k])
+    """
+
+    def __init__(self, n: int, granule: int, metric, local_search=None, merge=None,
+                 segment=None, group=None):
+        import torch.distributed as dist
+        self.dist = dist
+        self.group = group
+        self.world = dist.get_world_size(group) if dist.is_initialized() else 1
+        self.rank = dist.get_rank(group) if dist.is_initialized() else 0
+        self.n, self.granule, self.metric = n, granule, metric
+        self.r0, self.r1 = shard_rows(n, granule, self.rank, self.world)
+        self.segment = segment
+        if local_search is None:
+            if segment is None:
+                raise ValueError("need a segment or a local_search function")
+            local_search = self._segment_search
+        if merge is None:
+            from .vector_scan import merge_shards
+            merge = lambda i, d: merge_shards(i, d, metric)  # noqa: E731
+        self.local_search = local_search
+        self.merge = merge
+
+    @classmethod
+    def generate(cls, seed, mode, n, d, metric, granule, group=None):
+        """Each rank generates its own shard in HBM (counter-based generator)."""
+        import torch.distributed as dist
+        from .vector_scan import VectorScanSegment
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        r0, r1 = shard_rows(n, granule, rank, world)
+        seg = VectorScanSegment.generate(seed, mode, r1 - r0, d, metric, granule, row_offset=r0)
+        return cls(n, granule, metric, segment=seg, group=group)
+
+    def _segment_search(self, queries, k, filter_bits, row_exists_bits):
+        return self.segment.search(queries, k, self.metric, filter_bits, row_exists_bits)
+
+    def search(self, queries, k, filter_bits=None, row_exists_bits=None):
+        """Sharded top-k over the whole part; every rank returns the merged
+        result.  Bitmaps are the PART's (n bits); each rank uses its slice."""
+        import torch
+        f = slice_bitmap(filter_bits, self.n, self.r0, self.r1)
+        e = slice_bitmap(row_exists_bits, self.n, self.r0, self.r1)
+        ids, dist = self.local_search(queries, k, f, e)
+        if self.world == 1:
+            return self.merge(ids[None], dist[None]) if self.r1 - self.r0 < self.n else (ids, dist)
+        on_device = torch.is_tensor(ids) and ids.is_cuda
+        ti = ids if torch.is_tensor(ids) else torch.from_numpy(np.ascontiguousarray(ids))
+        td = dist if torch.is_tensor(dist) else torch.from_numpy(np.ascontiguousarray(dist))
+        gi = [torch.empty_like(ti) for _ in range(self.world)]
+        gd = [torch.empty_like(td) for _ in range(self.world)]
+        # ids and distances travel together: one gather of a 12-byte record
+        # would need a packed dtype; two small gathers (nq*k*8 + nq*k*4 bytes)
+        # are latency-bound either way
+        self.dist.all_gather(gi, ti, group=self.group)
+        self.dist.all_gather(gd, td, group=self.group)
+        si, sd = torch.stack(gi), torch.stack(gd)
+        if not on_device:
+            si, sd = si.numpy(), sd.numpy()
+        return self.merge(si, sd)

@@ -23,7 +23,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import F_ASYNC, F_DEVICE_PTRS, METRICS, check, lib
+from ._lib import F_ASYNC, F_DEVICE_PTRS, F_PART_MERGE, METRICS, check, lib
 
 FLT_MAX = np.float32(3.4028235e38)
 FLT_MIN = np.float32(1.1754944e-38)
@@ -153,6 +153,22 @@ class VectorScanSegment:
                               _ptr(_host_u8(row_exists)), _ptr(ids), _ptr(dist), 0, None))
         return ids, dist
 
+    def rerank(self, queries, candidates, k, metric=None, row_exists=None):
+        """mqvs_rerank (computeTopDistanceSubset contract, VIWithDataPart.cpp:838-856):
+        candidates[nq, ncand] segment-local rows (-1 = none) -> exact top-k
+        (ids, dist) with mqvs_search's formula, order key and padding."""
+        m = self.metric if metric is None else metric_id(metric)
+        q = _host_f32(queries)
+        if q.ndim == 1:
+            q = q[None, :]
+        nq = q.shape[0]
+        c = np.ascontiguousarray(np.asarray(candidates, dtype=np.int64).reshape(nq, -1))
+        ids = np.empty((nq, k), np.int64)
+        dist = np.empty((nq, k), np.float32)
+        check(lib.mqvs_rerank(self._h, _ptr(q), nq, _ptr(c), c.shape[1], k, m,
+                              _ptr(_host_u8(row_exists)), _ptr(ids), _ptr(dist), 0, None))
+        return ids, dist
+
     def free(self):
         if self._h:
             check(lib.mqvs_segment_free(self._h))
@@ -197,9 +213,14 @@ def vector_scan_without_index(segment: VectorScanSegment, query_vector, k, metri
     return label, distance
 
 
-def merge_shards(ids, dist, metric, out=None, async_=False, stream=None):
-    """Merge per-shard results [nshards, nq, k] -> [nq, k] (mqvs_merge_shards)."""
+def merge_shards(ids, dist, metric, out=None, async_=False, stream=None, part_merge=False):
+    """Merge per-shard results [nshards, nq, k] -> [nq, k] (mqvs_merge_shards).
+    part_merge=True: lists are different data parts, merged with the
+    reference's cross-part multimap order (MergeTreeBaseSearchManager.cpp:207-297;
+    exact IP ties come out last-inserted first); default: row-range shards of
+    one part (result == the unsharded part)."""
     m = metric_id(metric)
+    pm = F_PART_MERGE if part_merge else 0
     nshards, nq, k = ids.shape
     if _is_torch(ids):
         import torch
@@ -208,7 +229,7 @@ def merge_shards(ids, dist, metric, out=None, async_=False, stream=None):
             od = torch.empty((nq, k), dtype=torch.float32, device=ids.device)
         else:
             oi, od = out
-        flags = F_DEVICE_PTRS | (F_ASYNC if async_ else 0)
+        flags = F_DEVICE_PTRS | (F_ASYNC if async_ else 0) | pm
         check(lib.mqvs_merge_shards(nshards, nq, k, m, _ptr(ids.contiguous()), _ptr(dist.contiguous()),
                                     _ptr(oi), _ptr(od), flags,
                                     ctypes.c_void_p(stream) if stream else None))
@@ -217,7 +238,7 @@ def merge_shards(ids, dist, metric, out=None, async_=False, stream=None):
     dist = _host_f32(dist)
     oi = np.empty((nq, k), np.int64)
     od = np.empty((nq, k), np.float32)
-    check(lib.mqvs_merge_shards(nshards, nq, k, m, _ptr(ids), _ptr(dist), _ptr(oi), _ptr(od), 0,
+    check(lib.mqvs_merge_shards(nshards, nq, k, m, _ptr(ids), _ptr(dist), _ptr(oi), _ptr(od), pm,
                                 None))
     return oi, od
 

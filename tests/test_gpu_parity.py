@@ -237,3 +237,92 @@ def test_errors(mq):
     with pytest.raises(MqvsError):
         seg.search(np.zeros((1, 5), np.float32), 3)
     seg.free()
+
+
+@pytest.mark.parametrize("metric,nq,mode", [("L2", 3, 1), ("IP", 5, 1), ("Cosine", 4, 1),
+                                            ("L2", 25, 2), ("IP", 21, 0), ("Cosine", 30, 2)])
+def test_rerank_all_rows_equals_search(mq, metric, nq, mode):
+    """mqvs_rerank over every row of the segment reproduces mqvs_search bit
+    for bit (same formula branch, cosine variant per chunk, order key, padding),
+    with and without a lightweight-delete mask."""
+    n, d, k, gran = 3000, 48, 40, 512
+    rows = O.generate(31, mode, 0, n, d)
+    q = O.generate(32, mode, 0, nq, d)
+    seg = mq.VectorScanSegment.from_rows(rows, metric=metric, granule=gran)
+    try:
+        cand = np.tile(np.arange(n, dtype=np.int64), (nq, 1))
+        ids_s, dist_s = seg.search(q, k)
+        ids_r, dist_r = seg.rerank(q, cand, k)
+        assert_bitwise(ids_r, dist_r, ids_s, dist_s, f"rerank all {metric} nq={nq}")
+        rng = np.random.default_rng(3)
+        rex = np.packbits(rng.random(n) > 0.3, bitorder="little")
+        ids_s, dist_s = seg.search(q, k, row_exists=rex)
+        ids_r, dist_r = seg.rerank(q, cand, k, row_exists=rex)
+        assert_bitwise(ids_r, dist_r, ids_s, dist_s, f"rerank lwd {metric} nq={nq}")
+    finally:
+        seg.free()
+
+
+def test_rerank_subset_matches_oracle_knn(mq):
+    """Per-query candidate subsets (with -1 and out-of-range entries) against
+    the oracle's faiss knn over exactly those rows (nq < 20: direct formula)."""
+    n, d, nq, k, ncand = 5000, 40, 6, 16, 700
+    rows = O.generate(41, 1, 0, n, d)
+    q = O.generate(42, 1, 0, nq, d)
+    rng = np.random.default_rng(5)
+    cand = np.stack([rng.choice(n, ncand, replace=False) for _ in range(nq)]).astype(np.int64)
+    cand[:, :5] = -1
+    cand[:, 5:8] = n + 10
+    seg = mq.VectorScanSegment.from_rows(rows, metric="L2", granule=1024)
+    try:
+        ids_r, dist_r = seg.rerank(q, cand, k)
+    finally:
+        seg.free()
+    ids_o = np.empty((nq, k), np.int64)
+    dist_o = np.empty((nq, k), np.float32)
+    for i in range(nq):
+        valid = np.sort(cand[i][(cand[i] >= 0) & (cand[i] < n)])
+        io, do = O.knn(q[i:i + 1], rows[valid], k, O.L2)
+        ids_o[i] = np.where(io[0] >= 0, valid[np.maximum(io[0], 0)], -1)
+        dist_o[i] = do[0]
+    assert_bitwise(ids_r, dist_r, ids_o, dist_o, "rerank subset")
+
+
+def test_rerank_errors(mq):
+    from myscaledb_amd._lib import MqvsError
+    seg = mq.VectorScanSegment.from_rows(np.ones((10, 4), np.float32), metric="L2", granule=8)
+    try:
+        with pytest.raises(MqvsError) as e:
+            seg.rerank(np.ones((1, 4), np.float32), np.zeros((1, 5000), np.int64), 3)
+        assert e.value.name == "BAD_ARGUMENTS"
+        with pytest.raises(MqvsError) as e:
+            seg.rerank(np.ones((1, 4), np.float32), np.zeros((1, 5), np.int64), 3, "Cosine")
+        assert e.value.name == "LOGICAL_ERROR"
+        ids, dist = seg.rerank(np.ones((2, 4), np.float32), np.full((2, 3), -1, np.int64), 4)
+        assert (ids == -1).all() and (dist == FLT_MAX).all()
+    finally:
+        seg.free()
+
+
+@pytest.mark.parametrize("metric", ["IP", "L2"])
+def test_merge_parts_mode_matches_oracle(mq, metric):
+    """MQVS_F_PART_MERGE = getTotalTopSearchResultImpl (MergeTreeBaseSearchManager.cpp:207-297):
+    three data parts of small-integer rows (many exact ties), per-part lists
+    merged with the insertion-ordered multimap (IP read backwards)."""
+    nq, k, d = 9, 25, 8
+    parts = [O.generate(80 + p, 0, 0, 700, d) for p in range(3)]
+    q = O.generate(90, 0, 0, nq, d)
+    ids, dists = [], []
+    for rows in parts:
+        seg = mq.VectorScanSegment.from_rows(rows, metric=metric, granule=256)
+        i, dd = seg.search(q, k)
+        seg.free()
+        ids.append(i)
+        dists.append(dd)
+    ids, dists = np.stack(ids), np.stack(dists)
+    mi, md = mq.merge_shards(ids, dists, metric, part_merge=True)
+    m = O.IP if metric == "IP" else O.L2
+    for j in range(nq):
+        _, lab, dd = O.merge_parts(ids[:, j, :], dists[:, j, :], m)
+        assert np.array_equal(mi[j], lab), (metric, j, mi[j][:10], lab[:10])
+        assert np.array_equal(md[j].view(np.uint32), dd.view(np.uint32)), (metric, j)
