@@ -196,6 +196,18 @@ public:
         return out;
     }
 
+    /// As above, after the reference's dimension check (generateVectorDataset,
+    /// MergeTreeVSManager.cpp:135-182 throws on a mismatch).
+    ScanColumns scan(const float * queries, int32_t nq, int32_t query_dim, int32_t k, bool is_batch,
+                     const uint8_t * filter, const uint8_t * row_exists) const
+    {
+        if (query_dim != dim)
+            throw DB::Exception(DB::ErrorCodes::LOGICAL_ERROR, "{}",
+                                "The dimension of searched vector (" + std::to_string(query_dim)
+                                    + ") doesn't match the dimension of the vector column (" + std::to_string(dim) + ")");
+        return scan(queries, nq, k, is_batch, filter, row_exists);
+    }
+
     /// computeTopDistanceSubset: exact distances to nq*ncand candidate rows.
     void rerank(const float * queries, int32_t nq, const int64_t * cand, int32_t ncand, int32_t k,
                 const uint8_t * row_exists, int64_t * ids, float * dist) const
@@ -209,12 +221,22 @@ private:
     int metric;
 };
 
-/// Merge per-shard results [nshards][nq][k] (shard s holds lower row ids than
-/// s+1) into nq*k: the reference's cross-part multimap order.
+/// Merge per-shard results [nshards][nq][k] of row-range shards of ONE part
+/// (shard s holds lower row ids than s+1) into nq*k == the unsharded search.
 inline void mergeShardResults(int32_t nshards, int32_t nq, int32_t k, int mqvs_metric, const int64_t * in_ids,
                               const float * in_dist, int64_t * out_ids, float * out_dist)
 {
     check(mqvs_merge_shards(nshards, nq, k, mqvs_metric, in_ids, in_dist, out_ids, out_dist, 0, nullptr));
+}
+
+/// Cross-part top-k (getTotalTopSearchResultImpl, MergeTreeBaseSearchManager.cpp:207-297):
+/// per-part lists [nparts][nq][k] merged with the insertion-ordered multimap
+/// (read backwards for IP).
+inline void mergePartResults(int32_t nparts, int32_t nq, int32_t k, int mqvs_metric, const int64_t * in_ids,
+                             const float * in_dist, int64_t * out_ids, float * out_dist)
+{
+    check(mqvs_merge_shards(nparts, nq, k, mqvs_metric, in_ids, in_dist, out_ids, out_dist, MQVS_F_PART_MERGE,
+                            nullptr));
 }
 
 }
