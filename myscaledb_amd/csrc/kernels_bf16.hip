@@ -101,8 +101,14 @@ void launch_max_norm(const float *norms2, int64_t n, float *out_max, hipStream_t
 //   three products are exact in fp32 and summed into ONE accumulator: 3d terms
 //   with sum |t| <= 1.008 |x||y| -> 3.03 d u, plus d u for the exact chain.
 //   split 1: element rounding 2^-8 per side -> (2^-7 + 2^-16) |x||y| + 2 d u.
-__global__ void k_query_bound(ScanParams p, int metric, int split, const float *ynorm_max,
-                              float *bq) {
+//   direct (nq < 20: the exact value is faiss's sequential product-then-add
+//   formula, not the BLAS form): IP/cosine as above ((d+1) u |x||y| for the
+//   sequential sum is inside the constants); L2 compares the BLAS-form
+//   approximation with fl(sum (y-x)^2), so add the norms' rounding (d u each)
+//   and the direct sum's own error ((d+3) u (|x|+|y|)^2 <= 2 (d+3) u top):
+//   2 B + (3 d + 12) u top.
+__global__ void k_query_bound(ScanParams p, int metric, int split, int direct,
+                              const float *ynorm_max, float *bq) {
     // one wave per query; |x| in fp64 (an upper bound after the 1.0001 slack)
     const int j = blockIdx.x;
     const int lane = threadIdx.x;
@@ -123,8 +129,9 @@ __global__ void k_query_bound(ScanParams p, int metric, int split, const float *
                                : 0.0078125f + 1.6e-5f + acc_term + 1e-7f;
     float b = c * (xmax * 1.0001f) * ymax + 1e-30f;
     if (metric == MQVS_METRIC_L2) {
-        const float top = p.qnorms[j] + ymax * ymax;
-        b = 2.0f * b + top * 2.4e-7f + 1e-30f;
+        const float top = p.qnorms[j] * 1.0001f + ymax * ymax;
+        const float rel = direct ? (3.0f * (float)p.d + 12.0f) * 5.9604645e-8f : 2.4e-7f;
+        b = 2.0f * b + top * rel + 1e-30f;
     } else if (metric == MQVS_METRIC_COSINE) {
         b = b + 2.4e-7f;  // 1 - ip rounds; ties on 1-ip may differ in ip by one ulp of 1
     }
@@ -134,7 +141,8 @@ __global__ void k_query_bound(ScanParams p, int metric, int split, const float *
 
 void launch_query_bound(const ScanParams &p, int metric, int split, const float *ynorm_max,
                         float *bq, hipStream_t s) {
-    hipLaunchKernelGGL(k_query_bound, dim3(p.nq), dim3(64), 0, s, p, metric, split, ynorm_max, bq);
+    const int direct = p.nq < kBlasThreshold;
+    hipLaunchKernelGGL(k_query_bound, dim3(p.nq), dim3(64), 0, s, p, metric, split, direct, ynorm_max, bq);
 }
 
 
@@ -202,8 +210,10 @@ void launch_probe_select_approx(const float *probe, int64_t P, int64_t ld, int n
 }
 
 // ---------------------------------------------------------------------------
-// exact fp32 chain for one (query, row): the BLAS-branch element
-template <int METRIC>
+// exact value for one (query, row): the BLAS-branch element (fma chain), or
+// for nq < 20 (DIRECT) faiss's sequential product-then-add fvec formula in
+// kernels_scan.hip k_scan_small's order
+template <int METRIC, bool DIRECT>
 __device__ inline float exact_value(const ScanParams &p, int q, int64_t row) {
     const int64_t chunk = p.chunk_rows > 0 ? row / p.chunk_rows : 0;
     const int ord = chunk_ordinal(p, chunk);
@@ -212,6 +222,17 @@ __device__ inline float exact_value(const ScanParams &p, int q, int64_t row) {
     const float *x = p.qvars + ((int64_t)q * p.maxv + v) * qs;
     const float *y = p.rows + row * p.d;
     float acc = 0.0f;
+    if (DIRECT) {
+        for (int i = 0; i < p.d; ++i) {
+            if (METRIC == MQVS_METRIC_L2) {
+                const float e = y[i] - x[i];
+                acc = acc + e * e;
+            } else {
+                acc = acc + y[i] * x[i];
+            }
+        }
+        return acc;
+    }
     if ((p.d & 3) == 0) {
         const float4 *x4 = reinterpret_cast<const float4 *>(x);
         const float4 *y4 = reinterpret_cast<const float4 *>(y);
@@ -235,7 +256,7 @@ __device__ inline float exact_value(const ScanParams &p, int q, int64_t row) {
     return acc;
 }
 
-template <int METRIC>
+template <int METRIC, bool DIRECT>
 __global__ __launch_bounds__(SEL_THREADS) void k_rerank_select(ScanParams p, const float *bq, int k,
                                                               int64_t id_offset, int64_t *out_ids,
                                                               float *out_dist, int *overflow) {
@@ -276,7 +297,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_select(ScanParams p, con
     // exact re-rank of the survivors
     for (int i = threadIdx.x; i < m; i += SEL_THREADS) {
         const uint32_t row = recs[i].w;
-        const float raw = exact_value<METRIC>(p, q, row);
+        const float raw = exact_value<METRIC, DIRECT>(p, q, row);
         uint4 r;
         r.x = key32<METRIC>(raw);
         r.w = row;
@@ -313,8 +334,12 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_select(ScanParams p, con
 template <int M>
 static void rerank_select_t(const ScanParams &p, const float *bq, int k, int64_t id_offset,
                             int64_t *out_ids, float *out_dist, int *overflow, hipStream_t s) {
-    hipLaunchKernelGGL(k_rerank_select<M>, dim3(p.nq), dim3(SEL_THREADS), kSortCap * sizeof(uint4), s,
-                       p, bq, k, id_offset, out_ids, out_dist, overflow);
+    if (p.nq < kBlasThreshold)
+        hipLaunchKernelGGL((k_rerank_select<M, true>), dim3(p.nq), dim3(SEL_THREADS), kSortCap * sizeof(uint4),
+                           s, p, bq, k, id_offset, out_ids, out_dist, overflow);
+    else
+        hipLaunchKernelGGL((k_rerank_select<M, false>), dim3(p.nq), dim3(SEL_THREADS), kSortCap * sizeof(uint4),
+                           s, p, bq, k, id_offset, out_ids, out_dist, overflow);
 }
 
 void launch_rerank_select(const ScanParams &p, int metric, const float *bq, int k,

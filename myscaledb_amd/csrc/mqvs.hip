@@ -336,10 +336,12 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     }
 
     // ---- query prep
+    // faiss's formula branch is set by nq (kBlasThreshold); the bf16
+    // pre-filter serves both branches from kBf16MinNq queries up (its exact
+    // re-rank uses the branch's formula), the exact kernels the rest
     const bool mfma = nq >= kBlasThreshold;
-    const int kind = !mfma ? kScanSmall
-                     : (seg->approx_ok && !force_exact && g_batch_mode == 0) ? kScanBf16
-                                                                              : kScanMfma32;
+    const bool bf16 = seg->approx_ok && !force_exact && g_batch_mode == 0 && nq >= kBf16MinNq;
+    const int kind = bf16 ? kScanBf16 : !mfma ? kScanSmall : kScanMfma32;
     const int maxv = cos ? kMaxVariants : 1;
     const int64_t qstride = round_up(d, 32);
     float *qvars = (float *)ws.qvars.get(sizeof(float) * (size_t)nq * maxv * qstride);
@@ -349,7 +351,8 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     int *qlam = (int *)ws.qlam.get(sizeof(int) * nq);
     int *status = (int *)ws.status.get(sizeof(int) * 4);
     MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
-    launch_query_prep(dq, nq, d, cos ? MQVS_METRIC_COSINE : MQVS_METRIC_L2, mfma && metric == MQVS_METRIC_L2,
+    launch_query_prep(dq, nq, d, cos ? MQVS_METRIC_COSINE : MQVS_METRIC_L2,
+                      (mfma || bf16) && metric == MQVS_METRIC_L2,
                       qvars, qnorms, qmu, qlam, status, s);
     MQVS_HIP(hipGetLastError());
 
@@ -367,7 +370,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         chunk_ord = seg->chunk_ord;
     }
     const bool aligned = cos || chunk_ord != nullptr;
-    const int64_t tile_rows = !mfma ? kSmallRows : kind == kScanBf16 ? kBfRows : kMfmaRows;
+    const int64_t tile_rows = kind == kScanBf16 ? kBfRows : !mfma ? kSmallRows : kMfmaRows;
 
     // ---- candidate capacity per query (a fixed budget spread over the
     // batch) and probe size: expected candidates ~ k*n/P; aim at cap/3

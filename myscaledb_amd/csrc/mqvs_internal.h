@@ -21,6 +21,7 @@ constexpr int kSmallRows = 256;      // rows per tile, VALU scan
 constexpr int kMfmaRows = 128;       // rows per tile, MFMA scan
 constexpr int kMfmaQ = 128;          // queries per tile, MFMA scan
 constexpr int kBfRows = 256;         // rows per tile, bf16 MFMA scan (kernels_bf16_scan.hip)
+constexpr int kBf16MinNq = 8;        // bf16 pre-filter from this batch size up (tools/sweep.py)
 // Internal metric id: raw faiss inner product (knn_inner_product: every
 // ip > -FLT_MAX enters the heap), used by mqvs_knn_raw only.  The operator
 // path (mqvs_search) applies searchWrapper's FLT_MIN cut instead.

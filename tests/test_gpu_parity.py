@@ -107,10 +107,21 @@ PARITY = [
     # granule-aligned tiling with a short last granule (tiles past the end)
     ("cos_partial_last_granule", 8292, 64, 24, 50, "Cosine", 1, 8192, None, None, 0.0),
     ("cos_partial_last_granule_nq3", 8292, 64, 3, 50, "Cosine", 1, 8192, None, None, 0.0),
+    # nq 8..19: bf16 pre-filter + re-rank with faiss's sequential (direct) formula
+    ("l2_nq8_gauss",    9000,  96,  8,   50, "L2", 1, 1024, None, None, 0.0),
+    ("l2_nq12_mix",     9000,  256, 12,  100, "L2", 2, 2048, None, None, 0.0),
+    ("ip_nq10_gauss",   7000,  64,  10,  40, "IP", 1, 512, None, None, 0.0),
+    ("ip_nq17_exact",   5000,  40,  17,  64, "IP", 0, 256, None, None, 0.0),
+    ("cos_nq9_mix",     8000,  768, 9,   100, "Cosine", 2, 1024, None, None, 0.0),
+    ("cos_nq16_gauss",  8000,  128, 16,  100, "Cosine", 1, 512, None, None, 0.0),
+    ("l2_filter_lwd_nq14", 8000, 64, 14, 60, "L2", 1, 256, 0.1, 0.2, 0.0),
+    ("cos_empty_filter_nq11", 5000, 32, 11, 30, "Cosine", 1, 128, 0.3, None, 0.2),
+    ("cos_big_probe_nq15", 90000, 32, 15, 100, "Cosine", 1, 8192, None, None, 0.0),
+    ("l2_partial_granule_nq18", 8292, 64, 18, 50, "L2", 1, 8192, None, None, 0.0),
 ]
 
 
-BATCH = [c for c in PARITY if c[3] >= 20]
+BATCH = [c for c in PARITY if c[3] >= 8]
 
 
 @pytest.mark.parametrize("cfg", PARITY, ids=[c[0] for c in PARITY])
@@ -120,8 +131,8 @@ def test_gpu_vs_oracle(mq, cfg):
 
 @pytest.mark.parametrize("cfg", BATCH, ids=[c[0] for c in BATCH])
 def test_gpu_vs_oracle_fp32_batch_mode(mq, cfg):
-    """nq >= 20 through the fp32-MFMA-everywhere mode (the default is the bf16
-    pre-filter + exact re-rank): same bits."""
+    """nq >= 8 through the exact-kernels-only mode (VALU below 20, fp32 MFMA
+    from 20; the default is the bf16 pre-filter + exact re-rank): same bits."""
     from myscaledb_amd.vector_scan import set_batch_mode
     set_batch_mode(1)
     try:
@@ -326,3 +337,23 @@ def test_merge_parts_mode_matches_oracle(mq, metric):
         _, lab, dd = O.merge_parts(ids[:, j, :], dists[:, j, :], m)
         assert np.array_equal(mi[j], lab), (metric, j, mi[j][:10], lab[:10])
         assert np.array_equal(md[j].view(np.uint32), dd.view(np.uint32)), (metric, j)
+
+
+def test_path_selection(mq):
+    """nq < 8: VALU direct formula (path 0); nq >= 8: bf16 pre-filter (path 2);
+    batch mode 1: exact kernels only (VALU below 20, fp32 MFMA from 20)."""
+    from myscaledb_amd import _lib
+    from myscaledb_amd.vector_scan import set_batch_mode
+    rows = O.generate(3, 1, 0, 4000, 64)
+    seg = mq.VectorScanSegment.from_rows(rows, metric="L2", granule=512)
+    try:
+        for nq, want in ((7, 0), (8, 2), (19, 2), (20, 2)):
+            seg.search(O.generate(4, 1, 0, nq, 64), 10)
+            assert _lib.last_search_stats()["path"] == want, nq
+        set_batch_mode(1)
+        for nq, want in ((8, 0), (19, 0), (20, 1)):
+            seg.search(O.generate(4, 1, 0, nq, 64), 10)
+            assert _lib.last_search_stats()["path"] == want, nq
+    finally:
+        set_batch_mode(0)
+        seg.free()
