@@ -340,180 +340,6 @@ __global__ __launch_bounds__(256 * WQ) void k_scan_bf16(ScanParams p) {
     }
 }
 
-// Deep-pipelined form (VAR bit 8): K staged 16 deep (32 B per row per plane,
-// one v_mfma_f32_32x32x16_bf16 k-step per stage) in a ring of 4 stage buffers
-// with 3 stages in flight: the wave waits with a counted vmcnt for its pieces
-// of stage s only, then a raw s_barrier (no vmcnt(0) drain) publishes the
-// stage.  Chunk c of image row r (32-B rows) sits at slot c ^ ((r >> 3) & 1):
-// the 16 rows of a ds_read_b128 lane group land on 16 distinct bank slots.
-template <int METRIC, bool PROBE, int SPLIT, int WQ, int QB, int VAR>
-__global__ __launch_bounds__(256 * WQ) void k_scan_bf16_deep(ScanParams p) {
-    constexpr bool PRIO = VAR & 1;
-    constexpr int WR = 4, NW = WR * WQ, QT = 32 * QB * WQ;
-    constexpr int PL = (SPLIT == 3) ? 2 : 1;
-    constexpr int KD = 16, ROWB = 32, NBUF = 4;
-    constexpr int GY = BS_RT / 32;          // 1-KiB pieces (32 rows) per Y plane
-    constexpr int GQ = QT / 32;
-    constexpr int G = PL * (GY + GQ);
-    constexpr int GPW = G / NW;
-    static_assert(G % NW == 0, "stage pieces must split evenly over the waves");
-    constexpr int STAGE = G * 1024;
-    __shared__ __attribute__((aligned(16))) unsigned char lds[NBUF][STAGE];
-
-    const int64_t L = p.tiles * p.num_qblocks;
-    const int64_t cpx = (L + 7) / 8;
-    const int64_t b = blockIdx.x;
-    const int64_t l = (b % 8) * cpx + b / 8;
-    if (l >= L) return;
-    const int64_t ti = l / p.num_qblocks;
-    const int qb = (int)(l % p.num_qblocks);
-    int64_t r0, r1, chunk;
-    tile_range(p, ti, r0, r1, chunk);
-    if (r0 >= r1) return;
-    const int ord = chunk_ordinal(p, chunk);
-    const int t = threadIdx.x;
-    const int lane = t & 63, w = t >> 6;
-    const int wr = w % WR, wq = w / WR;
-    const int q0 = qb * QT;
-    if (ord < 0) {
-        if (PROBE) {
-            for (int i = t; i < BS_RT * QT; i += 64 * NW) {
-                const int64_t row = r0 + (i % BS_RT);
-                const int j = q0 + i / BS_RT;
-                if (row < r1 && j < p.nq) emit_approx<METRIC, true>(p, j, row, false, 0.f);
-            }
-        }
-        return;
-    }
-
-    const uint16_t *src[GPW];
-#pragma unroll
-    for (int i = 0; i < GPW; ++i) {
-        const int g = w + i * NW;
-        int pl, rbase;
-        if (g < PL * GY) {
-            pl = g / GY;
-            rbase = (g % GY) * 32;
-        } else {
-            pl = 2 + (g - PL * GY) / GQ;
-            rbase = ((g - PL * GY) % GQ) * 32;
-        }
-        const int r = rbase + (lane >> 1);
-        const int c = (lane & 1) ^ ((r >> 3) & 1);
-        if (pl < 2) {
-            int64_t gr = r0 + r;
-            if (gr >= r1) gr = r0;
-            src[i] = (pl == 0 ? p.rows_hi : p.rows_lo) + gr * p.dpad + c * 8;
-        } else {
-            int j = q0 + r;
-            if (j >= p.nq) j = 0;
-            const int64_t qo = ((int64_t)j * p.maxv + variant_of(p, j, ord)) * p.dpad + c * 8;
-            src[i] = (pl == 2 ? p.q_hi : p.q_lo) + qo;
-        }
-    }
-    auto issue = [&](int s) {
-        const int64_t k0 = (int64_t)s * KD;
-        unsigned char *dst = lds[s % NBUF];
-#pragma unroll
-        for (int i = 0; i < GPW; ++i)
-            __builtin_amdgcn_global_load_lds((const void *)(src[i] + k0),
-                                             (lds_void *)&dst[(w + i * NW) * 1024], 16, 0, 0);
-    };
-    constexpr int OFF_YH = 0;
-    constexpr int OFF_YL = GY * 1024;
-    constexpr int OFF_QH = PL * GY * 1024;
-    constexpr int OFF_QL = OFF_QH + GQ * 1024;
-    const int h = lane >> 5, l32 = lane & 31;
-    auto frag = [&](const unsigned char *st, int off, int r) {
-        return *reinterpret_cast<const bf16x8 *>(st + off + r * ROWB + ((h ^ ((r >> 3) & 1)) * 16));
-    };
-
-    f32x16 acc[2][QB];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < QB; ++j) acc[i][j] = f32x16{0};
-    const int ra0 = wr * 64 + l32;
-    const int rq0 = wq * 32 * QB + l32;
-    const int nst = (int)(p.dpad / KD);
-
-    // fragments of one stage (registers); two sets alternate so the reads of
-    // stage s+1 overlap the MFMAs of stage s
-    struct Frags {
-        bf16x8 ah[2], al[2], bh[QB], bl[QB];
-    };
-    auto read = [&](Frags &f, int s) {
-        const unsigned char *st = lds[s % NBUF];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) {
-            f.ah[i] = frag(st, OFF_YH, ra0 + 32 * i);
-            if (SPLIT == 3) f.al[i] = frag(st, OFF_YL, ra0 + 32 * i);
-        }
-#pragma unroll
-        for (int j = 0; j < QB; ++j) {
-            f.bh[j] = frag(st, OFF_QH, rq0 + 32 * j);
-            if (SPLIT == 3) f.bl[j] = frag(st, OFF_QL, rq0 + 32 * j);
-        }
-    };
-    auto compute = [&](const Frags &f) {
-        if (PRIO) __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int j = 0; j < QB; ++j) {
-                acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.ah[i], f.bh[j], acc[i][j], 0, 0, 0);
-                if (SPLIT == 3) {
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.ah[i], f.bl[j], acc[i][j], 0, 0, 0);
-                    acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(f.al[i], f.bh[j], acc[i][j], 0, 0, 0);
-                }
-            }
-        if (PRIO) __builtin_amdgcn_s_setprio(0);
-    };
-    // publish stage s: this wave's pieces of s have landed (only pieces of
-    // later stages stay in flight: `later` of them, 0..2), then the barrier
-    auto publish = [&](int later) {
-        if (later >= 2)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * GPW) : "memory");
-        else if (later == 1)
-            asm volatile("s_waitcnt vmcnt(%0)" ::"n"(GPW) : "memory");
-        else
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __builtin_amdgcn_s_barrier();
-    };
-    // one step: publish stage s+1, refill the ring (stage s+3 goes into the
-    // buffer of stage s-1, which every wave finished before this barrier),
-    // read stage s+1's fragments into `nx` while stage s (in `cu`) computes
-    // The reads are unconditional (the step after the last stage reads a
-    // stale buffer into registers nobody uses), so hipcc's lgkmcnt bookkeeping
-    // stays exact across the barrier; nst = dpad / 16 is even (dpad % 64 == 0).
-    auto step = [&](int s, Frags &cu, Frags &nx) {
-        publish(s + 2 < nst ? 1 : 0);
-        if (s + 3 < nst) issue(s + 3);
-        read(nx, s + 1);
-        compute(cu);
-    };
-
-    for (int s = 0; s < NBUF - 1 && s < nst; ++s) issue(s);
-    publish(min(nst - 1, 2));
-    Frags fa, fb;
-    read(fa, 0);
-    for (int s = 0; s < nst; s += 2) {
-        step(s, fa, fb);
-        step(s + 1, fb, fa);
-    }
-#pragma unroll
-    for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-        for (int jb = 0; jb < QB; ++jb) {
-            const int j = q0 + rq0 + jb * 32;
-            if (j >= p.nq) continue;
-            const int64_t rbase = r0 + wr * 64 + rb * 32 + 4 * h;
-            emit_vals<METRIC, PROBE, 16>(
-                p, j, r1, [&](int r) { return rbase + (r & 3) + 8 * (r >> 2); },
-                [&](int r) { return acc[rb][jb][r]; });
-        }
-}
-
 template <int METRIC, bool PROBE, int SPLIT, int WQ, int QB, int VAR>
 static void launch_shape(ScanParams p, hipStream_t s) {
     constexpr int QT = 32 * QB * WQ;
@@ -521,12 +347,8 @@ static void launch_shape(ScanParams p, hipStream_t s) {
     const int64_t L = p.tiles * p.num_qblocks;
     if (L < 1) return;
     const int64_t grid = (L + 7) / 8 * 8;
-    if constexpr ((VAR & 8) != 0)
-        hipLaunchKernelGGL((k_scan_bf16_deep<METRIC, PROBE, SPLIT, WQ, QB, VAR>), dim3((unsigned)grid),
-                           dim3(256 * WQ), 0, s, p);
-    else
-        hipLaunchKernelGGL((k_scan_bf16<METRIC, PROBE, SPLIT, WQ, QB, VAR>), dim3((unsigned)grid),
-                           dim3(256 * WQ), 0, s, p);
+    hipLaunchKernelGGL((k_scan_bf16<METRIC, PROBE, SPLIT, WQ, QB, VAR>), dim3((unsigned)grid),
+                       dim3(256 * WQ), 0, s, p);
 }
 
 // Tuning override (tools/tune_bf16.py, cosine APPEND split-3 launches only):
@@ -541,16 +363,15 @@ template <int METRIC, bool PROBE, int SPLIT>
 static bool launch_tuned(const ScanParams &p, hipStream_t s) {
     int wq, qb, var;
     if (!tune_override(wq, qb, var)) return false;
-    const int key = wq * 100 + qb * 10 + var;
+    const int key = (wq * 10 + qb) * 100 + var;
     switch (key) {
 #define MQVS_TUNE_CASE(WQ_, QB_, V_) \
-    case WQ_ * 100 + QB_ * 10 + V_: launch_shape<METRIC, PROBE, SPLIT, WQ_, QB_, V_>(p, s); return true;
+    case (WQ_ * 10 + QB_) * 100 + V_: launch_shape<METRIC, PROBE, SPLIT, WQ_, QB_, V_>(p, s); return true;
         MQVS_TUNE_CASE(1, 2, 0) MQVS_TUNE_CASE(1, 2, 4) MQVS_TUNE_CASE(1, 2, 7)
         MQVS_TUNE_CASE(2, 1, 0) MQVS_TUNE_CASE(2, 1, 4) MQVS_TUNE_CASE(2, 1, 7)
         MQVS_TUNE_CASE(1, 4, 0) MQVS_TUNE_CASE(1, 4, 4) MQVS_TUNE_CASE(1, 4, 7)
         MQVS_TUNE_CASE(2, 2, 0) MQVS_TUNE_CASE(2, 2, 4) MQVS_TUNE_CASE(2, 2, 7)
         MQVS_TUNE_CASE(2, 4, 0) MQVS_TUNE_CASE(2, 4, 4) MQVS_TUNE_CASE(2, 4, 7)
-        MQVS_TUNE_CASE(2, 4, 8)
 #undef MQVS_TUNE_CASE
         default: return false;
     }
