@@ -122,6 +122,18 @@ int mqvs_search(mqvs_segment_t seg, const float *queries, int32_t nq, int32_t k,
                 int32_t metric, const uint8_t *filter, const uint8_t *row_exists,
                 int64_t *out_ids, float *out_dist, uint32_t flags, mqvs_stream_t stream);
 
+/* mqvs_search for a row-range shard of a part, with the cosine chunk-ordinal
+ * base given: the number of granule chunks BEFORE the shard's first row that
+ * the reference searches for this query (MergeTreeVSManager.cpp:960-1536:
+ * a chunk is searched iff it holds a non-empty row that, with a PREWHERE
+ * filter, also passes the filter and is not deleted).  The query is
+ * re-normalised once per searched chunk, so this base picks the variant.
+ * chunk_ord_base < 0: row_offset / granule_rows (every earlier chunk
+ * searched).  Only cosine results depend on it. */
+int mqvs_search_ex(mqvs_segment_t seg, const float *queries, int32_t nq, int32_t k, int32_t metric,
+                   const uint8_t *filter, const uint8_t *row_exists, int64_t chunk_ord_base,
+                   int64_t *out_ids, float *out_dist, uint32_t flags, mqvs_stream_t stream);
+
 /* tryBruteForceSearch contract (BruteForceSearch.h:62-111): x nx*d queries,
  * y ny*d base (host pointers), one pass with no granule chunking, metric L2 or
  * IP only (anything else -> MQVS_ERR_NOT_IMPLEMENTED); result_id / distance

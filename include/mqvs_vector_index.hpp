@@ -175,6 +175,15 @@ public:
         check(mqvs_search(seg.get(), queries, nq, k, metric, filter, row_exists, ids, dist, 0, nullptr));
     }
 
+    /// Raw top-k of a row-range shard of a larger part: chunk_ord_base = chunks
+    /// before the shard that the reference searches (cosine query variant).
+    void searchShard(const float * queries, int32_t nq, int32_t k, const uint8_t * filter,
+                     const uint8_t * row_exists, int64_t chunk_ord_base, int64_t * ids, float * dist) const
+    {
+        check(mqvs_search_ex(seg.get(), queries, nq, k, metric, filter, row_exists, chunk_ord_base, ids, dist, 0,
+                             nullptr));
+    }
+
     /// The operator's output for this part, -1 ids dropped; vector_id filled
     /// for batch searches (is_batch) as in MergeTreeVSManager.cpp:1502-1517.
     ScanColumns scan(const float * queries, int32_t nq, int32_t k, bool is_batch,

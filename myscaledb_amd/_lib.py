@@ -28,7 +28,7 @@ SYMBOLS = [
     "mqvs_abi_version", "mqvs_init", "mqvs_device_count", "mqvs_last_error",
     "mqvs_thread_release", "mqvs_segment_create", "mqvs_segment_create_device",
     "mqvs_segment_generate", "mqvs_segment_free", "mqvs_segment_info", "mqvs_segment_rows",
-    "mqvs_search", "mqvs_knn_raw", "mqvs_rerank", "mqvs_merge_shards", "mqvs_generate_device",
+    "mqvs_search", "mqvs_search_ex", "mqvs_knn_raw", "mqvs_rerank", "mqvs_merge_shards", "mqvs_generate_device",
     "mqvs_last_search_stats", "mqvs_set_timing", "mqvs_set_batch_mode",
 ]
 
@@ -78,6 +78,7 @@ def _load():
         "mqvs_segment_info": ([P, P, P, P, P, P, P], ctypes.c_int),
         "mqvs_segment_rows": ([P, P], ctypes.c_int),
         "mqvs_search": ([P, P, I32, I32, I32, P, P, P, P, U32, P], ctypes.c_int),
+        "mqvs_search_ex": ([P, P, I32, I32, I32, P, P, I64, P, P, U32, P], ctypes.c_int),
         "mqvs_knn_raw": ([P, P, I64, I64, I64, I64, I32, P, P], ctypes.c_int),
         "mqvs_rerank": ([P, P, I32, P, I32, I32, I32, P, P, P, U32, P], ctypes.c_int),
         "mqvs_merge_shards": ([I32, I32, I32, I32, P, P, P, P, U32, P], ctypes.c_int),

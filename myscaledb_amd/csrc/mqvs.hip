@@ -284,7 +284,7 @@ static int g_batch_mode = 0;  // 0: bf16 pre-filter + exact re-rank when possibl
 static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, int metric,
                         const uint8_t *filter, const uint8_t *exists, int64_t *out_ids,
                         float *out_dist, uint32_t flags, hipStream_t user_stream,
-                        bool force_exact = false) {
+                        bool force_exact = false, int64_t ord_base = -1) {
     if (!seg) fail(MQVS_ERR_BAD_ARGUMENTS, "null segment");
     if (nq < 0 || k < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "nq and k must be non-negative");
     if (nq > 0 && k > 0 && (!queries || !out_ids || !out_dist))
@@ -401,7 +401,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     p.chunk_ord = chunk_ord;
     // a row-range shard of a part continues the part's chunk ordinals (all
     // earlier chunks assumed searched; see DESIGN.md, cosine + shards)
-    p.ord_base = (int)(seg->row_offset / seg->granule);
+    p.ord_base = (int)(ord_base >= 0 ? ord_base : seg->row_offset / seg->granule);
     p.filter = dfilter;
     p.exists = dexists;
     p.nonempty = seg->nonempty_bits;
@@ -505,7 +505,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         if (kind == kScanBf16 && ws.host_flags[0]) {
             // the bf16 bound left too many candidates: exact fp32 path
             search_impl(seg, queries, nq, k, metric, filter, exists, out_ids, out_dist, flags,
-                        user_stream, true);
+                        user_stream, true, ord_base);
             g_stats.rescans += 1;
             return;
         }
@@ -789,6 +789,16 @@ int mqvs_search(mqvs_segment_t seg, const float *queries, int32_t nq, int32_t k,
     return guarded([&] {
         search_impl(seg, queries, nq, k, metric, filter, row_exists, out_ids, out_dist, flags,
                     (hipStream_t)stream);
+    });
+}
+
+int mqvs_search_ex(mqvs_segment_t seg, const float *queries, int32_t nq, int32_t k, int32_t metric,
+                   const uint8_t *filter, const uint8_t *row_exists, int64_t chunk_ord_base,
+                   int64_t *out_ids, float *out_dist, uint32_t flags, mqvs_stream_t stream) {
+    return guarded([&] {
+        if (chunk_ord_base > INT32_MAX) fail(MQVS_ERR_BAD_ARGUMENTS, "chunk_ord_base out of range");
+        search_impl(seg, queries, nq, k, metric, filter, row_exists, out_ids, out_dist, flags,
+                    (hipStream_t)stream, false, chunk_ord_base);
     });
 }
 

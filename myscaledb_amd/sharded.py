@@ -47,22 +47,46 @@ def slice_bitmap(bits, n: int, r0: int, r1: int):
     return np.packbits(flat[r0:r1], bitorder="little")
 
 
+def chunk_ordinal_base(r0: int, granule: int, n: int, nonempty=None, filter_bits=None,
+                       row_exists_bits=None) -> int:
+    """How many granule chunks before row r0 the reference searches (and so
+    re-normalises a cosine query for): a chunk is searched iff it holds a
+    non-empty row that, under a PREWHERE filter, also passes it and is not
+    deleted (MergeTreeVSManager.cpp:960-1536; the device twin is
+    kernels_misc.hip k_chunk_active)."""
+    nch = r0 // granule
+    if nch == 0:
+        return 0
+    if nonempty is None and filter_bits is None:
+        return nch
+    m = r0  # rows of the chunks before the shard
+    ok = np.ones(m, bool) if nonempty is None else np.asarray(nonempty, bool)[:m].copy()
+    if filter_bits is not None:
+        ok &= np.unpackbits(np.asarray(filter_bits, np.uint8), bitorder="little")[:m].astype(bool)
+        if row_exists_bits is not None:
+            ok &= np.unpackbits(np.asarray(row_exists_bits, np.uint8), bitorder="little")[:m].astype(bool)
+    return int(ok.reshape(nch, granule).any(axis=1).sum())
+
+
 class ShardedScan:
     """A part sharded over the ranks of a process group.
 
-    local_search(queries, k, filter_bits, row_exists_bits) -> (ids[nq,k], dist[nq,k])
-        ids part-global (the shard's row_offset applied), -1 padded
+    local_search(queries, k, filter_bits, row_exists_bits, ord_base) -> (ids[nq,k], dist[nq,k])
+        ids part-global (the shard's row_offset applied), -1 padded;
+        ord_base = chunk_ordinal_base of the shard (cosine query variant)
     merge(ids[S,nq,k], dist[S,nq,k]) -> (ids[nq,k], dist[nq,k])
+    nonempty: the PART's per-row non-empty flags (n bytes) or None.
     """
 
     def __init__(self, n: int, granule: int, metric, local_search=None, merge=None,
-                 segment=None, group=None):
+                 segment=None, group=None, nonempty=None):
         import torch.distributed as dist
         self.dist = dist
         self.group = group
         self.world = dist.get_world_size(group) if dist.is_initialized() else 1
         self.rank = dist.get_rank(group) if dist.is_initialized() else 0
         self.n, self.granule, self.metric = n, granule, metric
+        self.nonempty = nonempty
         self.r0, self.r1 = shard_rows(n, granule, self.rank, self.world)
         self.segment = segment
         if local_search is None:
@@ -86,8 +110,9 @@ class ShardedScan:
         seg = VectorScanSegment.generate(seed, mode, r1 - r0, d, metric, granule, row_offset=r0)
         return cls(n, granule, metric, segment=seg, group=group)
 
-    def _segment_search(self, queries, k, filter_bits, row_exists_bits):
-        return self.segment.search(queries, k, self.metric, filter_bits, row_exists_bits)
+    def _segment_search(self, queries, k, filter_bits, row_exists_bits, ord_base):
+        return self.segment.search(queries, k, self.metric, filter_bits, row_exists_bits,
+                                   ord_base=ord_base)
 
     def search(self, queries, k, filter_bits=None, row_exists_bits=None):
         """Sharded top-k over the whole part; every rank returns the merged
@@ -95,7 +120,9 @@ class ShardedScan:
         import torch
         f = slice_bitmap(filter_bits, self.n, self.r0, self.r1)
         e = slice_bitmap(row_exists_bits, self.n, self.r0, self.r1)
-        ids, dist = self.local_search(queries, k, f, e)
+        base = chunk_ordinal_base(self.r0, self.granule, self.n, self.nonempty, filter_bits,
+                                  row_exists_bits)
+        ids, dist = self.local_search(queries, k, f, e, base)
         if self.world == 1:
             return self.merge(ids[None], dist[None]) if self.r1 - self.r0 < self.n else (ids, dist)
         on_device = torch.is_tensor(ids) and ids.is_cuda

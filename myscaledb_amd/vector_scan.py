@@ -123,9 +123,16 @@ class VectorScanSegment:
         return p.value
 
     def search(self, queries, k, metric=None, filter_bitmap=None, row_exists=None, out=None,
-               async_=False, stream=None):
-        """Raw mqvs_search: (ids[nq,k] int64, dist[nq,k] float32), -1 padded."""
+               async_=False, stream=None, ord_base=None):
+        """Raw mqvs_search: (ids[nq,k] int64, dist[nq,k] float32), -1 padded.
+        ord_base: cosine chunk-ordinal base of a row-range shard
+        (mqvs_search_ex; None = every earlier chunk searched)."""
         m = self.metric if metric is None else metric_id(metric)
+        base = -1 if ord_base is None else int(ord_base)
+
+        def call(qp, nq, fp, ep, ip, dp, flags, st):
+            check(lib.mqvs_search_ex(self._h, qp, nq, k, m, fp, ep, base, ip, dp, flags, st))
+
         if _is_torch(queries):
             import torch
             assert queries.is_cuda and queries.is_contiguous() and queries.dtype == torch.float32
@@ -136,9 +143,8 @@ class VectorScanSegment:
             else:
                 ids, dist = out
             flags = F_DEVICE_PTRS | (F_ASYNC if async_ else 0)
-            check(lib.mqvs_search(self._h, _ptr(queries), nq, k, m, _ptr(filter_bitmap),
-                                  _ptr(row_exists), _ptr(ids), _ptr(dist), flags,
-                                  ctypes.c_void_p(stream) if stream else None))
+            call(_ptr(queries), nq, _ptr(filter_bitmap), _ptr(row_exists), _ptr(ids), _ptr(dist), flags,
+                 ctypes.c_void_p(stream) if stream else None)
             return ids, dist
         q = _host_f32(queries)
         if q.ndim == 1:
@@ -149,8 +155,8 @@ class VectorScanSegment:
                                  f"query dimension {q.shape[1]} != column dimension {self.d}")
         ids = np.empty((nq, k), np.int64)
         dist = np.empty((nq, k), np.float32)
-        check(lib.mqvs_search(self._h, _ptr(q), nq, k, m, _ptr(_host_u8(filter_bitmap)),
-                              _ptr(_host_u8(row_exists)), _ptr(ids), _ptr(dist), 0, None))
+        call(_ptr(q), nq, _ptr(_host_u8(filter_bitmap)), _ptr(_host_u8(row_exists)), _ptr(ids),
+             _ptr(dist), 0, None)
         return ids, dist
 
     def rerank(self, queries, candidates, k, metric=None, row_exists=None):

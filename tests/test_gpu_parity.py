@@ -357,3 +357,35 @@ def test_path_selection(mq):
     finally:
         set_batch_mode(0)
         seg.free()
+
+
+@pytest.mark.parametrize("nq", [3, 12, 40])
+def test_cosine_shards_with_skipped_chunks(mq, nq):
+    """Row-range shards of a cosine part whose earlier chunks the reference
+    never searches (fully filtered out / all empty): mqvs_search_ex with the
+    chunk-ordinal base from sharded.chunk_ordinal_base + merge == one part."""
+    from myscaledb_amd.sharded import chunk_ordinal_base, shard_rows, slice_bitmap
+    n, d, k, gran, world = 12000, 48, 30, 3000, 3
+    rows = O.generate(61, 2, 0, n, d)
+    q = O.generate(62, 2, 0, nq, d)
+    rng = np.random.default_rng(4)
+    keep = rng.random(n) > 0.3
+    keep[0:gran] = False                     # chunk 0: filtered out entirely
+    ne = (rng.random(n) > 0.1).astype(np.uint8)
+    ne[gran:2 * gran] = 0                    # chunk 1: all arrays empty
+    rows[ne == 0] = FLT_MAX
+    flt = np.packbits(keep, bitorder="little")
+    for f in (flt, None):
+        ids_o, dist_o = O.vector_scan(rows, q, k, O.COSINE, gran, nonempty=ne, filter_bits=f, fast=True)
+        got_i, got_d = [], []
+        for r in range(world):
+            r0, r1 = shard_rows(n, gran, r, world)
+            seg = mq.VectorScanSegment.from_rows(rows[r0:r1], metric="Cosine", granule=gran,
+                                                 nonempty=ne[r0:r1], row_offset=r0)
+            base = chunk_ordinal_base(r0, gran, n, ne, f)
+            i, dd = seg.search(q, k, filter_bitmap=slice_bitmap(f, n, r0, r1), ord_base=base)
+            seg.free()
+            got_i.append(i)
+            got_d.append(dd)
+        mi, md = mq.merge_shards(np.stack(got_i), np.stack(got_d), "Cosine")
+        assert_bitwise(mi, md, ids_o, dist_o, f"cosine shards nq={nq} filter={f is not None}")
