@@ -190,7 +190,8 @@ typedef struct {
                                2 = bf16 MFMA pre-filter + exact fp32 re-rank */
     int32_t rescans;        /* candidate-overflow re-scans / fallbacks */
     int32_t segments;       /* main-scan segments (threshold refinements + 1) */
-    int32_t reserved;
+    int32_t gather;         /* 1: selective PREWHERE, the scan walked the gather list
+                               of selected rows (rows_scanned = list entries) */
 } mqvs_search_stats;
 int mqvs_last_search_stats(mqvs_search_stats *out);
 /* Enable per-search HIP-event timing (off by default: one extra event pair). */
@@ -200,6 +201,10 @@ int mqvs_set_timing(int enabled);
  * bound admits too many rows), 1 = fp32 MFMA over every row.  Both return the
  * same bits. */
 int mqvs_set_batch_mode(int mode);
+/* Selective PREWHERE scans: 0 = always scan every row and mask, 1 = scan only
+ * the selected rows (a device-built gather list) when at most half the part
+ * passes the filter (default), 2 = always gather.  All return the same bits. */
+int mqvs_set_gather_mode(int mode);
 
 #ifdef __cplusplus
 }

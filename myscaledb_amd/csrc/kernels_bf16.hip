@@ -152,7 +152,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_probe_select_approx(const float
                                                                     int64_t ld, int k,
                                                                     const float *bq, float *thr,
                                                                     int *cand_count, Cand *cand,
-                                                                    int cap) {
+                                                                    int cap, const int32_t *row_list) {
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh[4];
     const int q = blockIdx.x;
@@ -174,7 +174,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_probe_select_approx(const float
             if (pos < cap) {
                 Cand c;
                 c.raw = raw;
-                c.row = (uint32_t)i;
+                c.row = row_list ? (uint32_t)row_list[i] : (uint32_t)i;  // column = scan position
                 cand[(int64_t)q * cap + pos] = c;
             }
         }
@@ -184,29 +184,22 @@ __global__ __launch_bounds__(SEL_THREADS) void k_probe_select_approx(const float
 template <int M>
 static void probe_select_approx_t(const float *probe, int64_t P, int64_t ld, int nq, int k,
                                   const float *bq, float *thr, int *cc, Cand *cand, int cap,
-                                  hipStream_t s) {
+                                  const int32_t *row_list, hipStream_t s) {
     hipLaunchKernelGGL(k_probe_select_approx<M>, dim3(nq), dim3(SEL_THREADS), 0, s, probe, P, ld, k,
-                       bq, thr, cc, cand, cap);
+                       bq, thr, cc, cand, cap, row_list);
 }
 
 void launch_probe_select_approx(const float *probe, int64_t P, int64_t ld, int nq, int k,
                                 int metric, const float *bq, float *thr, int *cand_count,
-                                Cand *cand, int cand_cap, hipStream_t s) {
+                                Cand *cand, int cand_cap, const int32_t *row_list, hipStream_t s) {
+#define MQVS_PSA(M) probe_select_approx_t<M>(probe, P, ld, nq, k, bq, thr, cand_count, cand, cand_cap, row_list, s)
     switch (metric) {
-        case MQVS_METRIC_L2:
-            probe_select_approx_t<MQVS_METRIC_L2>(probe, P, ld, nq, k, bq, thr, cand_count, cand, cand_cap, s);
-            break;
-        case MQVS_METRIC_IP:
-            probe_select_approx_t<MQVS_METRIC_IP>(probe, P, ld, nq, k, bq, thr, cand_count, cand, cand_cap, s);
-            break;
-        case MQVS_METRIC_COSINE:
-            probe_select_approx_t<MQVS_METRIC_COSINE>(probe, P, ld, nq, k, bq, thr, cand_count, cand,
-                                                      cand_cap, s);
-            break;
-        default:
-            probe_select_approx_t<kMetricIpRaw>(probe, P, ld, nq, k, bq, thr, cand_count, cand, cand_cap, s);
-            break;
+        case MQVS_METRIC_L2: MQVS_PSA(MQVS_METRIC_L2); break;
+        case MQVS_METRIC_IP: MQVS_PSA(MQVS_METRIC_IP); break;
+        case MQVS_METRIC_COSINE: MQVS_PSA(MQVS_METRIC_COSINE); break;
+        default: MQVS_PSA(kMetricIpRaw); break;
     }
+#undef MQVS_PSA
 }
 
 // ---------------------------------------------------------------------------

@@ -53,9 +53,10 @@ __device__ inline int swz(int r, int c) {
 }
 
 template <int METRIC, bool PROBE>
-__device__ inline void emit_approx(const ScanParams &p, int j, int64_t row, bool valid, float raw) {
+__device__ inline void emit_approx(const ScanParams &p, int j, int64_t pos, int64_t row, bool valid,
+                                   float raw) {
     if (PROBE) {
-        p.probe[(int64_t)j * p.probe_ld + (row - p.row_begin)] = valid ? raw : __builtin_nanf("");
+        p.probe[(int64_t)j * p.probe_ld + (pos - p.row_begin)] = valid ? raw : __builtin_nanf("");
         return;
     }
     if (!valid) return;
@@ -72,27 +73,32 @@ __device__ inline void emit_approx(const ScanParams &p, int j, int64_t row, bool
     }
 }
 
+// pos: scan position (probe column); row: its row, -1 = gather padding
 template <int METRIC, bool PROBE>
-__device__ inline void emit_ip(const ScanParams &p, int j, int64_t row, float ip) {
+__device__ inline void emit_ip(const ScanParams &p, int j, int64_t pos, int64_t row, float ip) {
+    if (row < 0) {
+        if (PROBE) emit_approx<METRIC, true>(p, j, pos, row, false, 0.f);
+        return;
+    }
     float raw = ip;
     if (METRIC == MQVS_METRIC_L2) {
         raw = (p.qnorms[j] + p.row_norms[row]) - 2.0f * ip;
         if (raw < 0) raw = 0;
     }
-    emit_approx<METRIC, PROBE>(p, j, row, row_valid(p, row), raw);
+    emit_approx<METRIC, PROBE>(p, j, pos, row, row_valid(p, row), raw);
 }
 
-// Epilogue for NV accumulator values of query j (rows row_of(0..NV-1)).
+// Epilogue for NV accumulator values of query j (scan positions pos_of(0..NV-1)).
 // APPEND: candidates are rare, so the fast path only compares every value
 // with the query's threshold (no row bounds, no bitmaps, no branches); the
 // values of a wave with any lane over it take the exact per-row path.
 template <int METRIC, bool PROBE, int NV, class RowFn, class ValFn>
-__device__ inline void emit_vals(const ScanParams &p, int j, int64_t r1, RowFn row_of, ValFn val) {
+__device__ inline void emit_vals(const ScanParams &p, int j, int64_t r1, RowFn pos_of, ValFn val) {
     if (PROBE) {
 #pragma unroll
         for (int r = 0; r < NV; ++r) {
-            const int64_t row = row_of(r);
-            if (row < r1) emit_ip<METRIC, true>(p, j, row, val(r));
+            const int64_t pos = pos_of(r);
+            if (pos < r1) emit_ip<METRIC, true>(p, j, pos, row_at(p, pos), val(r));
         }
         return;
     }
@@ -103,7 +109,7 @@ __device__ inline void emit_vals(const ScanParams &p, int j, int64_t r1, RowFn r
     for (int r = 0; r < NV; ++r) {
         float raw = val(r);
         if (METRIC == MQVS_METRIC_L2) {
-            const int64_t row = min(row_of(r), r1 - 1);
+            const int64_t row = max(row_at(p, min(pos_of(r), r1 - 1)), (int64_t)0);
             raw = (qn + p.row_norms[row]) - 2.0f * raw;
             if (raw < 0) raw = 0;
             any |= raw <= t;
@@ -114,8 +120,8 @@ __device__ inline void emit_vals(const ScanParams &p, int j, int64_t r1, RowFn r
     if (any) {
 #pragma unroll
         for (int r = 0; r < NV; ++r) {
-            const int64_t row = row_of(r);
-            if (row < r1) emit_ip<METRIC, false>(p, j, row, val(r));
+            const int64_t pos = pos_of(r);
+            if (pos < r1) emit_ip<METRIC, false>(p, j, pos, row_at(p, pos), val(r));
         }
     }
 }
@@ -156,7 +162,7 @@ __global__ __launch_bounds__(256 * WQ) void k_scan_bf16(ScanParams p) {
             for (int i = t; i < BS_RT * QT; i += 64 * NW) {
                 const int64_t row = r0 + (i % BS_RT);
                 const int j = q0 + i / BS_RT;
-                if (row < r1 && j < p.nq) emit_approx<METRIC, true>(p, j, row, false, 0.f);
+                if (row < r1 && j < p.nq) emit_approx<METRIC, true>(p, j, row, -1, false, 0.f);
             }
         }
         return;
@@ -179,8 +185,9 @@ __global__ __launch_bounds__(256 * WQ) void k_scan_bf16(ScanParams p) {
         const int r = rbase + (lane >> 2);
         const int c = swz<M16>(r, lane & 3);
         if (pl < 2) {
-            int64_t gr = r0 + r;
-            if (gr >= r1) gr = r0;  // padding rows: any valid row, results discarded
+            const int64_t gp = r0 + r;
+            int64_t gr = gp < r1 ? row_at(p, gp) : -1;
+            if (gr < 0) gr = row_at(p, r0);  // padding: any real row, results discarded
             src[i] = (pl == 0 ? p.rows_hi : p.rows_lo) + gr * p.dpad + c * 8;
         } else {
             int j = q0 + r;

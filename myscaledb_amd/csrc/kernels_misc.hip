@@ -300,6 +300,108 @@ __global__ __launch_bounds__(256) void k_exclusive_ord(int *flag_ord, int64_t nc
     }
 }
 
+// ---------------------------------------------------------------------------
+// Gather list of a selective PREWHERE scan: the rows that pass the filter,
+// are non-empty and not deleted, chunk by chunk in row order, each chunk's
+// run padded with -1 to a multiple of `tile` entries.
+__device__ inline bool row_selected(const uint8_t *filter, const uint8_t *nonempty,
+                                    const uint8_t *exists, int64_t r) {
+    return bit_test(filter, r) && (!nonempty || bit_test(nonempty, r)) && (!exists || bit_test(exists, r));
+}
+
+__global__ __launch_bounds__(256) void k_chunk_count(const uint8_t *filter, const uint8_t *nonempty,
+                                                      const uint8_t *exists, int64_t n, int64_t chunk_rows,
+                                                      int *count) {
+    const int64_t c = blockIdx.x;
+    const int64_t r0 = c * chunk_rows;
+    const int64_t r1 = r0 + chunk_rows < n ? r0 + chunk_rows : n;
+    int total = 0;
+    for (int64_t base = r0; base < r1; base += 256) {
+        const int64_t r = base + threadIdx.x;
+        total += __syncthreads_count(r < r1 && row_selected(filter, nonempty, exists, r));
+    }
+    if (threadIdx.x == 0) count[c] = total;
+}
+
+// offsets[c] = sum of padded counts before c; totals[0] = padded list
+// length, totals[1] = selected rows
+__global__ __launch_bounds__(256) void k_pad_scan(const int *count, int64_t nchunks, int tile,
+                                                   int64_t *offsets, int64_t *totals) {
+    __shared__ int64_t sums[256];
+    __shared__ int64_t carry, selected;
+    if (threadIdx.x == 0) carry = selected = 0;
+    __syncthreads();
+    for (int64_t base = 0; base < nchunks; base += 256) {
+        const int64_t c = base + threadIdx.x;
+        const int cnt = c < nchunks ? count[c] : 0;
+        const int64_t padded = (int64_t)(cnt + tile - 1) / tile * tile;
+        sums[threadIdx.x] = padded;
+        __syncthreads();
+        for (int off = 1; off < 256; off <<= 1) {
+            const int64_t v = threadIdx.x >= off ? sums[threadIdx.x - off] : 0;
+            __syncthreads();
+            sums[threadIdx.x] += v;
+            __syncthreads();
+        }
+        if (c < nchunks) offsets[c] = carry + sums[threadIdx.x] - padded;
+        if (cnt) atomicAdd((unsigned long long *)&selected, (unsigned long long)cnt);
+        __syncthreads();
+        if (threadIdx.x == 255) carry += sums[255];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        totals[0] = carry;
+        totals[1] = selected;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_compact_rows(const uint8_t *filter, const uint8_t *nonempty,
+                                                       const uint8_t *exists, int64_t n, int64_t chunk_rows,
+                                                       const int *count, const int64_t *offsets, int tile,
+                                                       int32_t *list) {
+    __shared__ int wsum[4];
+    const int64_t c = blockIdx.x;
+    const int64_t r0 = c * chunk_rows;
+    const int64_t r1 = r0 + chunk_rows < n ? r0 + chunk_rows : n;
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    int32_t *out = list + offsets[c];
+    int run = 0;
+    for (int64_t base = r0; base < r1; base += 256) {
+        const int64_t r = base + threadIdx.x;
+        const bool ok = r < r1 && row_selected(filter, nonempty, exists, r);
+        const unsigned long long m = __ballot(ok);
+        if (lane == 0) wsum[w] = __popcll(m);
+        __syncthreads();
+        int before = run;
+        for (int i = 0; i < w; ++i) before += wsum[i];
+        if (ok) out[before + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)r;
+        run += wsum[0] + wsum[1] + wsum[2] + wsum[3];
+        __syncthreads();
+    }
+    const int cnt = count[c];
+    const int padded = (cnt + tile - 1) / tile * tile;
+    for (int i = cnt + threadIdx.x; i < padded; i += 256) out[i] = -1;
+}
+
+void launch_gather_count(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists, int64_t n,
+                         int64_t chunk_rows, int tile, int *count, int64_t *offsets, int64_t *totals,
+                         hipStream_t s) {
+    const int64_t nchunks = (n + chunk_rows - 1) / chunk_rows;
+    if (nchunks < 1) return;
+    hipLaunchKernelGGL(k_chunk_count, dim3((unsigned)nchunks), dim3(256), 0, s, filter, nonempty, exists, n,
+                       chunk_rows, count);
+    hipLaunchKernelGGL(k_pad_scan, dim3(1), dim3(256), 0, s, count, nchunks, tile, offsets, totals);
+}
+
+void launch_gather_list(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists, int64_t n,
+                        int64_t chunk_rows, int tile, const int *count, const int64_t *offsets, int32_t *list,
+                        hipStream_t s) {
+    const int64_t nchunks = (n + chunk_rows - 1) / chunk_rows;
+    if (nchunks < 1) return;
+    hipLaunchKernelGGL(k_compact_rows, dim3((unsigned)nchunks), dim3(256), 0, s, filter, nonempty, exists, n,
+                       chunk_rows, count, offsets, tile, list);
+}
+
 void launch_chunk_ordinals(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists,
                            int64_t n, int64_t chunk_rows, int require_filter, int *ord,
                            hipStream_t s) {

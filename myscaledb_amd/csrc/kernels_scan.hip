@@ -34,11 +34,14 @@ static __device__ inline float nan_f() { return __builtin_nanf(""); }
 
 // Wave-aggregated append: every lane of the wave calls this for the same
 // query j (VALU kernel); one atomic per wave instead of one per row.
+// pos: scan position (probe column); row: the row (-1 = gather padding);
+// inrange: pos inside the scanned range; have: inrange and a real row.
 template <int METRIC, bool PROBE>
-__device__ inline void emit_wave(const ScanParams &p, int j, int64_t row, bool have, bool valid,
-                                 float raw) {
+__device__ inline void emit_wave(const ScanParams &p, int j, int64_t pos, int64_t row, bool inrange,
+                                 bool have, bool valid, float raw) {
     if (PROBE) {
-        if (have) p.probe[(int64_t)j * p.probe_ld + (row - p.row_begin)] = valid ? raw : __builtin_nanf("");
+        if (inrange)
+            p.probe[(int64_t)j * p.probe_ld + (pos - p.row_begin)] = (have && valid) ? raw : __builtin_nanf("");
         return;
     }
     const uint32_t key = key32<METRIC>(raw);
@@ -62,9 +65,9 @@ __device__ inline void emit_wave(const ScanParams &p, int j, int64_t row, bool h
 }
 
 template <int METRIC, bool PROBE>
-__device__ inline void emit(const ScanParams &p, int j, int64_t row, bool valid, float raw) {
+__device__ inline void emit(const ScanParams &p, int j, int64_t pos, int64_t row, bool valid, float raw) {
     if (PROBE) {
-        p.probe[(int64_t)j * p.probe_ld + (row - p.row_begin)] = valid ? raw : nan_f();
+        p.probe[(int64_t)j * p.probe_ld + (pos - p.row_begin)] = valid ? raw : nan_f();
     } else if (valid) {
         const uint32_t key = key32<METRIC>(raw);
         if (key != 0xFFFFFFFFu && key <= p.tau[j]) {
@@ -100,11 +103,13 @@ __global__ __launch_bounds__(256) void k_scan_small(ScanParams p) {
         tile_range(p, ti, r0, r1, chunk);
         if (r0 >= r1) continue;  // tile past the end of a partial last granule (block-uniform)
         const int ord = chunk_ordinal(p, chunk);
-        const int64_t row = r0 + t;
-        const bool have = row < r1;
+        const int64_t pos = r0 + t;
+        const bool inrange = pos < r1;
+        const int64_t row = inrange ? row_at(p, pos) : -1;
+        const bool have = row >= 0;
         if (ord < 0) {  // chunk never searched by the reference (all arrays empty)
-            if (PROBE && have)
-                for (int j = 0; j < p.nq; ++j) emit<METRIC, true>(p, j, row, false, 0.f);
+            if (PROBE && inrange)
+                for (int j = 0; j < p.nq; ++j) emit<METRIC, true>(p, j, pos, row, false, 0.f);
             continue;
         }
         const float *qsrc = qload
@@ -121,9 +126,10 @@ __global__ __launch_bounds__(256) void k_scan_small(ScanParams p) {
             for (int i = 0; i < 8; ++i) {
                 const int f = t + 256 * i;
                 const int lr = f >> 3, c = (f & 7) * 4;
-                const int64_t gr = r0 + lr;
+                const int64_t gp = r0 + lr;
+                const int64_t gr = gp < r1 ? row_at(p, gp) : -1;
                 float4 v = make_float4(0.f, 0.f, 0.f, 0.f);
-                if (gr < r1) {
+                if (gr >= 0) {
                     const float *src = p.rows + gr * d + k0 + c;
                     if (VEC4) {
                         if (k0 + c < d) v = *reinterpret_cast<const float4 *>(src);
@@ -182,7 +188,7 @@ __global__ __launch_bounds__(256) void k_scan_small(ScanParams p) {
             const bool valid = have && row_valid(p, row);
 #pragma unroll
             for (int j = 0; j < NQ; ++j)
-                if (j < p.nq) emit_wave<METRIC, PROBE>(p, j, row, have, valid, acc[j]);
+                if (j < p.nq) emit_wave<METRIC, PROBE>(p, j, pos, row, inrange, have, valid, acc[j]);
         }
     }
 }
@@ -265,7 +271,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_mfma(ScanParams p) {
             for (int i = t; i < kMfmaRows * kMfmaQ; i += 256) {
                 const int64_t row = r0 + (i % kMfmaRows);
                 const int j = q0 + i / kMfmaRows;
-                if (row < r1 && j < p.nq) emit<METRIC, true>(p, j, row, false, 0.f);
+                if (row < r1 && j < p.nq) emit<METRIC, true>(p, j, row, row, false, 0.f);
             }
         }
         return;
@@ -361,7 +367,7 @@ __global__ __launch_bounds__(256, 2) void k_scan_mfma(ScanParams p) {
                 raw = (qn + p.row_norms[row]) - 2.0f * acc[r];
                 if (raw < 0) raw = 0;
             }
-            emit<METRIC, PROBE>(p, j, row, row_valid(p, row), raw);
+            emit<METRIC, PROBE>(p, j, row, row, row_valid(p, row), raw);
         }
     };
     epi(acc00, 0, 0);

@@ -23,7 +23,8 @@ template <int METRIC>
 __global__ __launch_bounds__(SEL_THREADS) void k_probe_select(const float *probe, int64_t P,
                                                              int64_t ld, int k, uint32_t *tau,
                                                              int *cand_count, Cand *cand,
-                                                             int cap, int64_t row_base) {
+                                                             int cap, int64_t row_base,
+                                                             const int32_t *row_list) {
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh[4];
     const int q = blockIdx.x;
@@ -37,7 +38,8 @@ __global__ __launch_bounds__(SEL_THREADS) void k_probe_select(const float *probe
             if (pos < cap) {
                 Cand c;
                 c.raw = raw;
-                c.row = (uint32_t)(row_base + i);
+                // probe column = scan position; gather mode maps it to the row
+                c.row = row_list ? (uint32_t)row_list[row_base + i] : (uint32_t)(row_base + i);
                 cand[(int64_t)q * cap + pos] = c;
             }
         }
@@ -198,17 +200,17 @@ __global__ __launch_bounds__(SEL_THREADS) void k_merge_shards(int nshards, int n
 template <int M>
 static void probe_select_t(const float *probe, int64_t P, int64_t ld, int nq, int k,
                            uint32_t *tau, int *cc, Cand *cand, int cap, int64_t row_base,
-                           hipStream_t s) {
+                           const int32_t *row_list, hipStream_t s) {
     hipLaunchKernelGGL(k_probe_select<M>, dim3(nq), dim3(SEL_THREADS), 0, s, probe, P, ld, k, tau,
-                       cc, cand, cap, row_base);
+                       cc, cand, cap, row_base, row_list);
 }
 
 void launch_probe_select(const float *probe, int64_t P, int64_t ld, int nq, int k, int metric,
                          uint32_t *tau, int *cand_count, Cand *cand, int cand_cap,
-                         int64_t row_base, hipStream_t s) {
+                         int64_t row_base, const int32_t *row_list, hipStream_t s) {
     if (nq <= 0) return;
     MQVS_DISPATCH_METRIC(metric, probe_select_t,
-                         (probe, P, ld, nq, k, tau, cand_count, cand, cand_cap, row_base, s));
+                         (probe, P, ld, nq, k, tau, cand_count, cand, cand_cap, row_base, row_list, s));
 }
 
 template <int M>

@@ -74,7 +74,7 @@ struct Workspace {
     static constexpr int kSegEv = 64;
     hipEvent_t seg_ev[kSegEv] = {};  // per main-scan segment: start, end
     DevBuf queries, qvars, qnorms, qmu, qlam, status, filter, exists, ord, probe, tau, count, cand,
-        overflow, out_ids, out_dist, misc, qhi, bq, thr, cand2, count2;
+        overflow, out_ids, out_dist, misc, qhi, bq, thr, cand2, count2, gcount, goff, glist;
     int *host_flags = nullptr;  // pinned
     void init() {
         if (stream) return;
@@ -86,7 +86,7 @@ struct Workspace {
     void release() {
         DevBuf *all[] = {&queries, &qvars, &qnorms, &qmu,  &qlam,   &status,  &filter,   &exists, &ord,
                          &probe,   &tau,   &count,  &cand, &overflow, &out_ids, &out_dist, &misc,
-                         &qhi, &bq, &thr, &cand2, &count2};
+                         &qhi, &bq, &thr, &cand2, &count2, &gcount, &goff, &glist};
         for (auto *b : all) b->release();
         if (host_flags) (void)hipHostFree(host_flags);
         host_flags = nullptr;
@@ -280,6 +280,7 @@ static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 
 // metric: public metric, or kMetricIpRaw for the faiss-contract entry point
 static int g_batch_mode = 0;  // 0: bf16 pre-filter + exact re-rank when possible, 1: fp32 MFMA
+static int g_gather_mode = 1;  // selective PREWHERE: 0 never gather, 1 when <= 50% selected, 2 always
 
 static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, int metric,
                         const uint8_t *filter, const uint8_t *exists, int64_t *out_ids,
@@ -335,13 +336,51 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         ddist = (float *)ws.out_dist.get(sizeof(float) * (size_t)nq * k);
     }
 
-    // ---- query prep
+    // ---- selective PREWHERE: count the rows that pass (filter, non-empty,
+    // not deleted); a selective scan then walks a gather list of just those
+    // rows (per chunk in row order, padded to whole tiles) and reads
+    // selectivity x n rows instead of all of them
+    static_assert(kSmallRows == kBfRows, "gather-list padding is one tile of either kernel");
+    int64_t selected = -1, gpadded = 0;
+    int *gcount = nullptr;
+    int64_t *goff = nullptr;
+    if (dfilter && g_gather_mode != 0 && n > 0) {
+        const int64_t nch = (n + seg->granule - 1) / seg->granule;
+        gcount = (int *)ws.gcount.get(sizeof(int) * nch);
+        goff = (int64_t *)ws.goff.get(sizeof(int64_t) * (nch + 2));
+        launch_gather_count(dfilter, seg->nonempty_bits, dexists, n, seg->granule, kSmallRows, gcount, goff,
+                            goff + nch, s);
+        MQVS_HIP(hipGetLastError());
+        int64_t *htot = reinterpret_cast<int64_t *>(ws.host_flags + 8);
+        MQVS_HIP(hipMemcpyAsync(htot, goff + nch, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        MQVS_HIP(hipStreamSynchronize(s));
+        gpadded = htot[0];
+        selected = htot[1];
+    }
+
+    // ---- kernel choice
     // faiss's formula branch is set by nq (kBlasThreshold); the bf16
     // pre-filter serves both branches from kBf16MinNq queries up (its exact
-    // re-rank uses the branch's formula), the exact kernels the rest
+    // re-rank uses the branch's formula), the exact kernels the rest.  A
+    // gathered (selective) scan prefers the bf16 kernel at any nq: its LDS-DMA
+    // keeps whole tiles of scattered rows in flight and gathers efficiently up
+    // to ~60% selectivity, while the VALU kernel's 128-B row slices only pay
+    // below ~30% (tools/sweep.py --sels, profiles/r01)
     const bool mfma = nq >= kBlasThreshold;
-    const bool bf16 = seg->approx_ok && !force_exact && g_batch_mode == 0 && nq >= kBf16MinNq;
+    const bool bf16_ok = seg->approx_ok && !force_exact && g_batch_mode == 0;
+    bool bf16 = bf16_ok && nq >= kBf16MinNq;
+    bool gather = false;
+    if (selected >= 0) {
+        if (g_gather_mode == 2)
+            gather = bf16 || !mfma;
+        else if (bf16_ok && 10 * selected <= 6 * n)
+            gather = bf16 = true;
+        else if (!bf16 && !mfma && 10 * selected <= 3 * n)
+            gather = true;
+    }
     const int kind = bf16 ? kScanBf16 : !mfma ? kScanSmall : kScanMfma32;
+
+    // ---- query prep
     const int maxv = cos ? kMaxVariants : 1;
     const int64_t qstride = round_up(d, 32);
     float *qvars = (float *)ws.qvars.get(sizeof(float) * (size_t)nq * maxv * qstride);
@@ -369,7 +408,20 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     } else {
         chunk_ord = seg->chunk_ord;
     }
-    const bool aligned = cos || chunk_ord != nullptr;
+
+    // ---- gather list of the selected rows
+    const int32_t *row_list = nullptr;
+    int64_t scan_n = n;  // scan positions: rows, or gather-list entries
+    if (gather) {
+        int32_t *list = (int32_t *)ws.glist.get(sizeof(int32_t) * std::max<int64_t>(gpadded, 1));
+        launch_gather_list(dfilter, seg->nonempty_bits, dexists, n, seg->granule, kSmallRows, gcount, goff, list,
+                           s);
+        MQVS_HIP(hipGetLastError());
+        row_list = list;
+        scan_n = gpadded;
+        st.gather = 1;
+    }
+    const bool aligned = !row_list && (cos || chunk_ord != nullptr);
     const int64_t tile_rows = kind == kScanBf16 ? kBfRows : !mfma ? kSmallRows : kMfmaRows;
 
     // ---- candidate capacity per query (a fixed budget spread over the
@@ -378,12 +430,12 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     cap = std::max(cap, kSortCap) / 256 * 256;
     // (more candidates = more appends from the scan; 16k keeps them cheap)
     const int64_t target_cands = std::min<int64_t>(cap / 3, 16384);
-    int64_t P = n;
-    if (n > 32768) {
-        P = (int64_t)(((double)k * (double)n) / target_cands) + 1;
+    int64_t P = scan_n;
+    if (scan_n > 32768) {
+        P = (int64_t)(((double)k * (double)scan_n) / target_cands) + 1;
         P = std::max<int64_t>(P, 8 * (int64_t)k);
         P = round_up(P, aligned ? seg->granule : tile_rows);
-        if (P > n) P = n;
+        if (P > scan_n) P = scan_n;
     }
 
     ScanParams p{};
@@ -405,6 +457,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     p.filter = dfilter;
     p.exists = dexists;
     p.nonempty = seg->nonempty_bits;
+    p.row_list = row_list;
     p.num_qblocks = (nq + kMfmaQ - 1) / kMfmaQ;
     uint32_t *tau = (uint32_t *)ws.tau.get(sizeof(uint32_t) * nq);
     int *count = (int *)ws.count.get(sizeof(int) * nq);
@@ -436,15 +489,16 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     }
 
     const Range pr = make_range(0, P, tile_rows, seg->granule, aligned);
-    const Range mr = make_range(P, n, tile_rows, seg->granule, aligned);
+    const Range mr = make_range(P, scan_n, tile_rows, seg->granule, aligned);
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[5], s));
     run_scan(p, pr, kind, metric, true, s);
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[1], s));
     MQVS_HIP(hipMemsetAsync(count, 0, sizeof(int) * nq, s));
     if (kind == kScanBf16)
-        launch_probe_select_approx(probe, P, P, nq, k, metric, bq, (float *)p.thr, count, cand, cap, s);
+        launch_probe_select_approx(probe, P, P, nq, k, metric, bq, (float *)p.thr, count, cand, cap, row_list,
+                                   s);
     else
-        launch_probe_select(probe, P, P, nq, k, metric, tau, count, cand, cap, 0, s);
+        launch_probe_select(probe, P, P, nq, k, metric, tau, count, cand, cap, 0, row_list, s);
     MQVS_HIP(hipGetLastError());
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[2], s));
     // main scan in geometrically growing segments; between segments the
@@ -457,8 +511,8 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         int *calt = (int *)ws.count2.get(sizeof(int) * nq);
         int64_t b = P, seg_rows = std::max<int64_t>(2 * P, align);
         int segs = 0;
-        while (b < n) {
-            const int64_t e = std::min(n, round_up(b + seg_rows, align));
+        while (b < scan_n) {
+            const int64_t e = std::min(scan_n, round_up(b + seg_rows, align));
             const bool tev = timing && 2 * segs + 1 < Workspace::kSegEv;
             if (tev) MQVS_HIP(hipEventRecord(ws.seg_ev[2 * segs], s));
             run_scan(p, make_range(b, e, tile_rows, seg->granule, aligned), kind, metric, false, s);
@@ -466,7 +520,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
             b = e;
             seg_rows *= 2;
             ++segs;
-            if (b < n) {
+            if (b < scan_n) {
                 launch_refine(cand, count, cap, nq, k, metric, kind == kScanBf16, bq, tau,
                               (float *)p.thr, alt, calt, s);
                 MQVS_HIP(hipGetLastError());
@@ -491,8 +545,8 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
 
     st.path = kind;
     st.probe_rows = P;
-    st.main_rows = n - P;
-    st.rows_scanned = n;
+    st.main_rows = scan_n - P;
+    st.rows_scanned = scan_n;
     st.nq = nq;
     st.k = k;
 
@@ -516,7 +570,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
                                            " rows tie at the k-th distance");
             launch_cand_tau(cand, count, cap, nq, k, metric, tau, nullptr, s);
             MQVS_HIP(hipMemsetAsync(count, 0, sizeof(int) * nq, s));
-            run_scan(p, make_range(0, n, tile_rows, seg->granule, aligned), kind, metric, false, s);
+            run_scan(p, make_range(0, scan_n, tile_rows, seg->granule, aligned), kind, metric, false, s);
             MQVS_HIP(hipMemsetAsync(overflow, 0, sizeof(int) * 4, s));
             launch_final_select(cand, count, cap, nq, k, metric, seg->granule, seg->row_offset, dids,
                                 ddist, overflow, s);
@@ -903,6 +957,12 @@ int mqvs_last_search_stats(mqvs_search_stats *out) {
 int mqvs_set_batch_mode(int mode) {
     if (mode != 0 && mode != 1) return MQVS_ERR_BAD_ARGUMENTS;
     g_batch_mode = mode;
+    return MQVS_OK;
+}
+
+int mqvs_set_gather_mode(int mode) {
+    if (mode < 0 || mode > 2) return MQVS_ERR_BAD_ARGUMENTS;
+    g_gather_mode = mode;
     return MQVS_OK;
 }
 

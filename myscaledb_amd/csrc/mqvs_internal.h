@@ -120,11 +120,30 @@ struct ScanParams {
     const uint16_t *q_lo;     // [nq][maxv][dpad] (split 3)
     int64_t dpad;
     const float *thr;         // [nq] APPEND threshold on the approximate raw value
+    // gather mode (selective PREWHERE): the scan walks positions of this list
+    // of selected rows instead of rows; each chunk's rows are padded with -1 to
+    // whole 256-entry tiles, so a tile never spans two chunks.  Probe columns
+    // are list positions; candidates store rows.
+    const int32_t *row_list;  // null = contiguous rows
 };
 
-// Tile -> [r0, r1) and chunk index.
+// Row at scan position pos (-1 = padding entry of the gather list).
+__device__ inline int64_t row_at(const ScanParams &p, int64_t pos) {
+    return p.row_list ? (int64_t)p.row_list[pos] : pos;
+}
+
+// Tile -> [r0, r1) and chunk index ([r0, r1) are scan positions: rows, or
+// gather-list positions).
 __device__ inline void tile_range(const ScanParams &p, int64_t t, int64_t &r0, int64_t &r1,
                                   int64_t &chunk) {
+    if (p.row_list) {
+        // the first entry of a tile is a real row (padding only ends a chunk)
+        r0 = p.row_begin + t * p.tile_rows;
+        r1 = r0 + p.tile_rows;
+        if (r1 > p.row_end) r1 = p.row_end;
+        chunk = r0 < r1 ? (int64_t)p.row_list[r0] / p.chunk_rows : 0;
+        return;
+    }
     if (p.tiles_per_chunk > 0) {
         const int64_t c0 = p.row_begin / p.chunk_rows;  // row_begin is chunk-aligned
         chunk = c0 + t / p.tiles_per_chunk;
@@ -167,12 +186,18 @@ __device__ inline bool row_valid(const ScanParams &p, int64_t r) {
 // ---------------------------------------------------------------------------
 // Launchers (kernels_*.hip)
 void launch_scan_small(const ScanParams &p, int metric, bool probe, hipStream_t s);
+void launch_gather_count(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists, int64_t n,
+                         int64_t chunk_rows, int tile, int *count, int64_t *offsets, int64_t *totals,
+                         hipStream_t s);
+void launch_gather_list(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists, int64_t n,
+                        int64_t chunk_rows, int tile, const int *count, const int64_t *offsets, int32_t *list,
+                        hipStream_t s);
 void launch_rerank_ids(const ScanParams &p, int metric, const int64_t *cand, int ncand, int k,
                        int64_t id_offset, int64_t *out_ids, float *out_dist, hipStream_t s);
 void launch_scan_mfma(const ScanParams &p, int metric, bool probe, hipStream_t s);
 void launch_probe_select(const float *probe, int64_t P, int64_t ld, int nq, int k, int metric,
                          uint32_t *tau, int *cand_count, Cand *cand, int cand_cap,
-                         int64_t row_base, hipStream_t s);
+                         int64_t row_base, const int32_t *row_list, hipStream_t s);
 void launch_cand_tau(const Cand *cand, const int *cand_count, int cand_cap, int nq, int k,
                      int metric, uint32_t *tau, const int *overflow_q, hipStream_t s);
 void launch_final_select(const Cand *cand, const int *cand_count, int cand_cap, int nq, int k,
@@ -204,7 +229,7 @@ void launch_query_bound(const ScanParams &p, int metric, int split, const float 
 void launch_scan_bf16(const ScanParams &p, int metric, bool probe, int split, hipStream_t s);
 void launch_probe_select_approx(const float *probe, int64_t P, int64_t ld, int nq, int k,
                                 int metric, const float *bq, float *thr, int *cand_count,
-                                Cand *cand, int cand_cap, hipStream_t s);
+                                Cand *cand, int cand_cap, const int32_t *row_list, hipStream_t s);
 void launch_refine(const Cand *cin, const int *cnt_in, int cap, int nq, int k, int metric,
                    bool approx, const float *bq, uint32_t *tau, float *thr, Cand *cout, int *cnt_out,
                    hipStream_t s);

@@ -258,6 +258,12 @@ def set_timing(enabled: bool):
     check(lib.mqvs_set_timing(1 if enabled else 0))
 
 
+def set_gather_mode(mode: int):
+    """Selective PREWHERE: 0 scan all rows + mask, 1 gather the selected rows
+    when <= 50% pass (default), 2 always gather (mqvs_set_gather_mode)."""
+    check(lib.mqvs_set_gather_mode(int(mode)))
+
+
 def set_batch_mode(mode: int):
     """nq >= 20: 0 = bf16 MFMA pre-filter + exact fp32 re-rank (default),
     1 = fp32 MFMA over every row.  Both return identical bits."""

@@ -123,6 +123,32 @@ PARITY = [
 
 BATCH = [c for c in PARITY if c[3] >= 8]
 
+# selective PREWHERE: gather list (default when <= 50% pass) vs masked full scan
+FILTERED = [c for c in PARITY if c[8] is not None] + [
+    ("l2_filter_none_nq2", 6000, 32, 2, 20, "L2", 1, 512, 0.0, None, 0.0),
+    ("cos_filter_all_nq9", 6000, 32, 9, 20, "Cosine", 1, 512, 1.0, None, 0.0),
+    ("cos_filter_sparse_nq3", 50000, 64, 3, 50, "Cosine", 2, 2048, 0.003, 0.2, 0.1),
+    ("ip_filter_sparse_nq30", 50000, 64, 30, 50, "IP", 1, 1000, 0.01, None, 0.0),
+    ("l2_filter_mid_nq12", 40000, 96, 12, 100, "L2", 2, 4096, 0.08, 0.1, 0.05),
+]
+
+
+@pytest.mark.parametrize("gmode", [0, 2])
+@pytest.mark.parametrize("cfg", FILTERED, ids=[c[0] for c in FILTERED])
+def test_gpu_vs_oracle_gather_modes(mq, cfg, gmode):
+    """Selective PREWHERE through the gather list (mode 2: always) and the
+    masked full scan (mode 0: never): same bits as the oracle either way."""
+    from myscaledb_amd import _lib
+    from myscaledb_amd.vector_scan import set_gather_mode
+    set_gather_mode(gmode)
+    try:
+        run_parity(mq, cfg)
+        st = _lib.last_search_stats()
+        # (the exact fp32 MFMA path, path 1, always scans every row)
+        assert st["gather"] == (1 if gmode == 2 and st["path"] != 1 else 0), st
+    finally:
+        set_gather_mode(1)
+
 
 @pytest.mark.parametrize("cfg", PARITY, ids=[c[0] for c in PARITY])
 def test_gpu_vs_oracle(mq, cfg):
