@@ -216,14 +216,29 @@ __device__ inline float exact_value(const ScanParams &p, int q, int64_t row) {
     const float *y = p.rows + row * p.d;
     float acc = 0.0f;
     if (DIRECT) {
-        for (int i = 0; i < p.d; ++i) {
+        // element order 0..d-1, product then add (16-B loads when aligned)
+        auto step = [&](float a, float b) {
             if (METRIC == MQVS_METRIC_L2) {
-                const float e = y[i] - x[i];
+                const float e = a - b;
                 acc = acc + e * e;
             } else {
-                acc = acc + y[i] * x[i];
+                acc = acc + a * b;
             }
+        };
+        int i = 0;
+        if ((p.d & 3) == 0) {
+            const float4 *x4 = reinterpret_cast<const float4 *>(x);
+            const float4 *y4 = reinterpret_cast<const float4 *>(y);
+            for (; i < (p.d >> 2); ++i) {
+                const float4 a = y4[i], b = x4[i];
+                step(a.x, b.x);
+                step(a.y, b.y);
+                step(a.z, b.z);
+                step(a.w, b.w);
+            }
+            return acc;
         }
+        for (; i < p.d; ++i) step(y[i], x[i]);
         return acc;
     }
     if ((p.d & 3) == 0) {

@@ -24,13 +24,26 @@ __device__ inline float cand_value(const ScanParams &p, int q, int64_t row) {
     float acc = 0.0f;
     if (DIRECT) {
         // kernels_scan.hip k_scan_small order: sequential, product then add
-        for (int i = 0; i < p.d; ++i) {
+        auto step = [&](float a, float b) {
             if (METRIC == MQVS_METRIC_L2) {
-                const float e = y[i] - x[i];
+                const float e = a - b;
                 acc = acc + e * e;
             } else {
-                acc = acc + y[i] * x[i];
+                acc = acc + a * b;
             }
+        };
+        if ((p.d & 3) == 0) {
+            const float4 *x4 = reinterpret_cast<const float4 *>(x);
+            const float4 *y4 = reinterpret_cast<const float4 *>(y);
+            for (int i = 0; i < (p.d >> 2); ++i) {
+                const float4 a = y4[i], b = x4[i];
+                step(a.x, b.x);
+                step(a.y, b.y);
+                step(a.z, b.z);
+                step(a.w, b.w);
+            }
+        } else {
+            for (int i = 0; i < p.d; ++i) step(y[i], x[i]);
         }
         return acc;
     }
