@@ -433,6 +433,9 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     int64_t P = scan_n;
     if (scan_n > 32768) {
         P = (int64_t)(((double)k * (double)scan_n) / target_cands) + 1;
+        // (a shorter probe is cheaper but its looser threshold sends more
+        // waves of the first segments down the append path: measured net
+        // loss at nq = 1000 with a 64 MB cap on the probe matrix)
         P = std::max<int64_t>(P, 8 * (int64_t)k);
         P = round_up(P, aligned ? seg->granule : tile_rows);
         if (P > scan_n) P = scan_n;
