@@ -128,7 +128,8 @@ __device__ inline void emit_vals(const ScanParams &p, int j, int64_t r1, RowFn p
 
 template <int METRIC, bool PROBE, int SPLIT, int WQ, int QB, int VAR>
 __global__ __launch_bounds__(256 * WQ) void k_scan_bf16(ScanParams p) {
-    constexpr bool PRIO = VAR & 1, SPLIT_ISSUE = VAR & 2, M16 = VAR & 4;
+    constexpr bool PRIO = VAR & 1, SPLIT_ISSUE = VAR & 2, M16 = VAR & 4, STAMPS = VAR & 64,
+                   YEARLY = (VAR & 128) && M16;
     constexpr int WR = 4;                   // row waves
     constexpr int NW = WR * WQ;             // waves per workgroup
     constexpr int QT = 32 * QB * WQ;        // queries per workgroup
@@ -139,6 +140,8 @@ __global__ __launch_bounds__(256 * WQ) void k_scan_bf16(ScanParams p) {
     constexpr int GPW = G / NW;             // groups per wave
     static_assert(G % NW == 0, "stage groups must split evenly over the waves");
     constexpr int STAGE = G * 1024;         // bytes per stage
+    constexpr int YPW = (PL * GY) / NW;     // Y-plane groups per wave: src[0, YPW)
+    static_assert((PL * GY) % NW == 0, "Y groups must split evenly over the waves");
     __shared__ __attribute__((aligned(16))) unsigned char lds[2][STAGE];
 
     const int64_t L = p.tiles * p.num_qblocks;
@@ -228,9 +231,11 @@ __global__ __launch_bounds__(256 * WQ) void k_scan_bf16(ScanParams p) {
     };
 
     const int nst = (int)(p.dpad / BS_K);
-    issue(0, 0, 0, GPW);
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+    if constexpr (!YEARLY) {
+        issue(0, 0, 0, GPW);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __syncthreads();
+    }
 
     if constexpr (!M16) {
         const int h = lane >> 5, l32 = lane & 31;
@@ -298,7 +303,89 @@ __global__ __launch_bounds__(256 * WQ) void k_scan_bf16(ScanParams p) {
             for (int j = 0; j < QB16; ++j) acc[i][j] = f32x4{0};
         const int ra0 = wr * 64 + l16;
         const int rq0 = wq * 32 * QB + l16;
-        for (int s = 0; s < nst; ++s) {
+        // diagnostic build only (VAR bit 64): per-wave s_memtime stamps
+        uint64_t sum_read = 0, sum_mfma = 0, sum_sync = 0, tp = 0;
+        auto stamp = [&]() -> uint64_t {
+            uint64_t tt = 0;
+            if constexpr (STAMPS) {
+                __builtin_amdgcn_sched_barrier(0);
+                asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(tt)::"memory");
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            return tt;
+        };
+        if constexpr (STAMPS) tp = stamp();
+        if constexpr (YEARLY) {
+            // Y-early ring (VAR bit 128): a stage's Y planes are consumed as
+            // soon as every wave has its row fragments, so the Y part of stage
+            // s+2 is issued into the current buffer right after a mid-stage
+            // barrier (~1.9 stages of lead for the HBM-streamed rows); the Q
+            // part of stage s+1 goes out at the top of stage s.  Issue order
+            // per wave: Y(s+1) < Q(s+1) < Y(s+2), so the wait for stage s+1
+            // is vmcnt(YPW).  Barriers are raw (no vmcnt(0) drain) and written
+            // as one asm statement with a memory clobber, so no LDS access
+            // moves across them.
+            issue(0, 0, 0, GPW);
+            if (nst > 1) {
+                issue(1, 1, 0, YPW);
+                asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(YPW) : "memory");
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+            }
+            for (int s = 0; s < nst; ++s) {
+                const unsigned char *st = lds[s & 1];
+                if (s + 1 < nst) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    issue(s + 1, (s + 1) & 1, YPW, GPW);  // Q(s+1): its buffer part is free
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+                if (PRIO) __builtin_amdgcn_s_setprio(1);
+                bf16x8 ah[4], al[4], bh[QB], bl[QB];
+#pragma unroll
+                for (int i = 0; i < 4; ++i) {
+                    ah[i] = frag(st, OFF_YH, ra0 + 16 * i, c);
+                    if (SPLIT == 3) al[i] = frag(st, OFF_YL, ra0 + 16 * i, c);
+                }
+#pragma unroll
+                for (int jj = 0; jj < QB; ++jj) {
+                    bh[jj] = frag(st, OFF_QH, rq0 + 16 * jj, c);
+                    if (SPLIT == 3) bl[jj] = frag(st, OFF_QL, rq0 + 16 * jj, c);
+                }
+                asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");  // Y(s) consumed
+                if (s + 2 < nst) {
+                    __builtin_amdgcn_sched_barrier(0);
+                    issue(s + 2, s & 1, 0, YPW);
+                    __builtin_amdgcn_sched_barrier(0);
+                }
+#pragma unroll
+                for (int hf = 0; hf < 2; ++hf) {
+                    if (hf == 1) {
+#pragma unroll
+                        for (int jj = 0; jj < QB; ++jj) {
+                            bh[jj] = frag(st, OFF_QH, rq0 + 16 * (QB + jj), c);
+                            if (SPLIT == 3) bl[jj] = frag(st, OFF_QL, rq0 + 16 * (QB + jj), c);
+                        }
+                    }
+#pragma unroll
+                    for (int i = 0; i < 4; ++i)
+#pragma unroll
+                        for (int jj = 0; jj < QB; ++jj) {
+                            f32x4 &a = acc[i][hf * QB + jj];
+                            a = mma16(ah[i], bh[jj], a);
+                            if (SPLIT == 3) {
+                                a = mma16(ah[i], bl[jj], a);
+                                a = mma16(al[i], bh[jj], a);
+                            }
+                        }
+                }
+                if (PRIO) __builtin_amdgcn_s_setprio(0);
+                if (s + 2 < nst)
+                    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(YPW) : "memory");
+                else if (s + 1 < nst)
+                    asm volatile("s_waitcnt vmcnt(0)\n\ts_barrier" ::: "memory");
+            }
+        }
+        for (int s = 0; s < (YEARLY ? 0 : nst); ++s) {
             const bool more = s + 1 < nst;
             if (!SPLIT_ISSUE && more) issue(s + 1, (s + 1) & 1, 0, GPW);
             const unsigned char *st = lds[s & 1];
@@ -317,6 +404,13 @@ __global__ __launch_bounds__(256 * WQ) void k_scan_bf16(ScanParams p) {
                     bh[jj] = frag(st, OFF_QH, rq0 + 16 * (hf * QB + jj), c);
                     if (SPLIT == 3) bl[jj] = frag(st, OFF_QL, rq0 + 16 * (hf * QB + jj), c);
                 }
+                if constexpr (STAMPS) {
+                    if (hf == 0) {
+                        const uint64_t t1 = stamp();
+                        sum_read += t1 - tp;
+                        tp = t1;
+                    }
+                }
                 issue_part(more, s, hf);
 #pragma unroll
                 for (int i = 0; i < 4; ++i)
@@ -331,8 +425,27 @@ __global__ __launch_bounds__(256 * WQ) void k_scan_bf16(ScanParams p) {
                     }
             }
             if (PRIO) __builtin_amdgcn_s_setprio(0);
+            if constexpr (STAMPS) {
+                const uint64_t t2 = stamp();
+                sum_mfma += t2 - tp;
+                tp = t2;
+            }
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
             __syncthreads();
+            if constexpr (STAMPS) {
+                const uint64_t t3 = stamp();
+                sum_sync += t3 - tp;
+                tp = t3;
+            }
+        }
+        if constexpr (STAMPS) {
+            if (lane == 0 && p.dbg) {
+                atomicAdd(&p.dbg[0], (unsigned long long)sum_read);
+                atomicAdd(&p.dbg[1], (unsigned long long)sum_mfma);
+                atomicAdd(&p.dbg[2], (unsigned long long)sum_sync);
+                atomicAdd(&p.dbg[3], 1ull);
+                atomicAdd(&p.dbg[4], (unsigned long long)nst);
+            }
         }
 #pragma unroll
         for (int i = 0; i < 4; ++i)
@@ -354,6 +467,22 @@ static void launch_shape(ScanParams p, hipStream_t s) {
     const int64_t L = p.tiles * p.num_qblocks;
     if (L < 1) return;
     const int64_t grid = (L + 7) / 8 * 8;
+    if constexpr ((VAR & 64) != 0) {
+        // diagnostic build: per-wave stage-segment cycle sums, printed per launch
+        static unsigned long long *dbg = nullptr;
+        if (!dbg) (void)hipMalloc((void **)&dbg, 8 * sizeof(unsigned long long));
+        (void)hipMemsetAsync(dbg, 0, 8 * sizeof(unsigned long long), s);
+        p.dbg = dbg;
+        hipLaunchKernelGGL((k_scan_bf16<METRIC, PROBE, SPLIT, WQ, QB, VAR>), dim3((unsigned)grid),
+                           dim3(256 * WQ), 0, s, p);
+        unsigned long long h[8] = {0};
+        (void)hipMemcpyAsync(h, dbg, sizeof(h), hipMemcpyDeviceToHost, s);
+        (void)hipStreamSynchronize(s);
+        const double stages = h[4] ? (double)h[4] : 1.0;
+        std::fprintf(stderr, "stamps waves=%llu stages=%llu cycles/stage: read %.0f mfma %.0f sync %.0f\n", h[3],
+                     h[4], h[0] / stages, h[1] / stages, h[2] / stages);
+        return;
+    }
     hipLaunchKernelGGL((k_scan_bf16<METRIC, PROBE, SPLIT, WQ, QB, VAR>), dim3((unsigned)grid),
                        dim3(256 * WQ), 0, s, p);
 }
@@ -378,7 +507,8 @@ static bool launch_tuned(const ScanParams &p, hipStream_t s) {
         MQVS_TUNE_CASE(2, 1, 0) MQVS_TUNE_CASE(2, 1, 4) MQVS_TUNE_CASE(2, 1, 7)
         MQVS_TUNE_CASE(1, 4, 0) MQVS_TUNE_CASE(1, 4, 4) MQVS_TUNE_CASE(1, 4, 7)
         MQVS_TUNE_CASE(2, 2, 0) MQVS_TUNE_CASE(2, 2, 4) MQVS_TUNE_CASE(2, 2, 7)
-        MQVS_TUNE_CASE(2, 4, 0) MQVS_TUNE_CASE(2, 4, 4) MQVS_TUNE_CASE(2, 4, 7)
+        MQVS_TUNE_CASE(2, 4, 0) MQVS_TUNE_CASE(2, 4, 4) MQVS_TUNE_CASE(2, 4, 7) MQVS_TUNE_CASE(2, 4, 71)
+        MQVS_TUNE_CASE(2, 4, 132) MQVS_TUNE_CASE(2, 4, 133) MQVS_TUNE_CASE(2, 2, 133) MQVS_TUNE_CASE(2, 1, 133)
 #undef MQVS_TUNE_CASE
         default: return false;
     }
@@ -388,12 +518,15 @@ template <int METRIC, bool PROBE, int SPLIT>
 static void launch_split(const ScanParams &p, hipStream_t s) {
     if constexpr (METRIC == MQVS_METRIC_COSINE && !PROBE && SPLIT == 3)
         if (launch_tuned<METRIC, PROBE, SPLIT>(p, s)) return;
-    // shapes and variants measured with tools/tune_bf16.py (10M x 768 cosine):
-    // nq 64: 6.15 ms (HBM ~5 TB/s), nq 128: 7.6 ms, nq 1000: 36.1 ms (1.27 PF/s)
+    // shapes and variants measured with tools/tune_bf16.py (10M x 768 cosine,
+    // profiles/r01/tune_bf16_*.jsonl): nq 64: 5.86 ms (Y-early ring, HBM
+    // ~5.2 TB/s), nq 128: 7.33 ms (Y-early), nq 1000: 36.1 ms (1.27 PF/s; the
+    // Y-early ring's extra barrier costs 5% on this MFMA-bound shape)
+    constexpr int kSmallVar = SPLIT == 3 ? 133 : 7;
     if (p.nq <= 64)  // (split 1 has 20 pieces per stage: 4 waves)
-        launch_shape<METRIC, PROBE, SPLIT, SPLIT == 3 ? 2 : 1, SPLIT == 3 ? 1 : 2, 7>(p, s);
+        launch_shape<METRIC, PROBE, SPLIT, SPLIT == 3 ? 2 : 1, SPLIT == 3 ? 1 : 2, kSmallVar>(p, s);
     else if (p.nq <= 128)
-        launch_shape<METRIC, PROBE, SPLIT, 2, 2, 7>(p, s);
+        launch_shape<METRIC, PROBE, SPLIT, 2, 2, kSmallVar>(p, s);
     else
         launch_shape<METRIC, PROBE, SPLIT, 2, 4, 7>(p, s);
 }

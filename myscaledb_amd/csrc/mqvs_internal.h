@@ -125,6 +125,7 @@ struct ScanParams {
     // whole 256-entry tiles, so a tile never spans two chunks.  Probe columns
     // are list positions; candidates store rows.
     const int32_t *row_list;  // null = contiguous rows
+    unsigned long long *dbg;  // diagnostic builds only (stage timing stamps)
 };
 
 // Row at scan position pos (-1 = padding entry of the gather list).
