@@ -28,6 +28,13 @@
 //      of the workgroup issues at once and the matrix pipe idles)
 //   4  v_mfma_f32_16x16x32_bf16 (4 x 2QB blocks of 16 x 16 per wave) instead
 //      of v_mfma_f32_32x32x16_bf16 (2 x QB blocks of 32 x 32)
+//   128 Y-early ring (16x16x32 only): the Y part of stage s+2 is issued right
+//      after a mid-stage barrier (default for the nq <= 128 shapes)
+// Diagnostic builds, reachable only through MQVS_BF16_TUNE: 64 s_memtime
+// stage stamps; 256 / 512 drop the per-stage load wait / all per-stage sync
+// (WRONG results, timing only -- they showed the 256 x 256 shape is bound by
+// its MFMA + ds_read + LDS-DMA issue stream, not by load latency: no change
+// without the wait, +3.5% without any barrier).
 // Chunk c (16 B) of image row r sits at slot c ^ f(r): f(r) = (r >> 2) & 3 for
 // the 32x32 fragment reads, 2 ((r >> 2) & 1) for the 16x16 reads; either way
 // every ds_read_b128 lane group hits 16 distinct 16-B bank slots.
@@ -430,8 +437,14 @@ __global__ __launch_bounds__(256 * WQ) void k_scan_bf16(ScanParams p) {
                 sum_mfma += t2 - tp;
                 tp = t2;
             }
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            __syncthreads();
+            if constexpr ((VAR & 512) != 0) {
+                // diagnostic only (wrong results): no per-stage sync at all
+            } else if constexpr ((VAR & 256) != 0) {
+                asm volatile("s_barrier" ::: "memory");  // diagnostic only: barrier without the load wait
+            } else {
+                asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                __syncthreads();
+            }
             if constexpr (STAMPS) {
                 const uint64_t t3 = stamp();
                 sum_sync += t3 - tp;
@@ -499,16 +512,17 @@ template <int METRIC, bool PROBE, int SPLIT>
 static bool launch_tuned(const ScanParams &p, hipStream_t s) {
     int wq, qb, var;
     if (!tune_override(wq, qb, var)) return false;
-    const int key = (wq * 10 + qb) * 100 + var;
+    const int key = (wq * 10 + qb) * 1000 + var;
     switch (key) {
 #define MQVS_TUNE_CASE(WQ_, QB_, V_) \
-    case (WQ_ * 10 + QB_) * 100 + V_: launch_shape<METRIC, PROBE, SPLIT, WQ_, QB_, V_>(p, s); return true;
+    case (WQ_ * 10 + QB_) * 1000 + V_:launch_shape<METRIC, PROBE, SPLIT, WQ_, QB_, V_>(p, s); return true;
         MQVS_TUNE_CASE(1, 2, 0) MQVS_TUNE_CASE(1, 2, 4) MQVS_TUNE_CASE(1, 2, 7)
         MQVS_TUNE_CASE(2, 1, 0) MQVS_TUNE_CASE(2, 1, 4) MQVS_TUNE_CASE(2, 1, 7)
         MQVS_TUNE_CASE(1, 4, 0) MQVS_TUNE_CASE(1, 4, 4) MQVS_TUNE_CASE(1, 4, 7)
         MQVS_TUNE_CASE(2, 2, 0) MQVS_TUNE_CASE(2, 2, 4) MQVS_TUNE_CASE(2, 2, 7)
         MQVS_TUNE_CASE(2, 4, 0) MQVS_TUNE_CASE(2, 4, 4) MQVS_TUNE_CASE(2, 4, 7) MQVS_TUNE_CASE(2, 4, 71)
         MQVS_TUNE_CASE(2, 4, 132) MQVS_TUNE_CASE(2, 4, 133) MQVS_TUNE_CASE(2, 2, 133) MQVS_TUNE_CASE(2, 1, 133)
+        MQVS_TUNE_CASE(2, 4, 263) MQVS_TUNE_CASE(2, 4, 519)
 #undef MQVS_TUNE_CASE
         default: return false;
     }

@@ -22,6 +22,8 @@ def main():
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--configs", default="2,4,0;2,4,4;2,4,7")
     ap.add_argument("--rounds", type=int, default=5)
+    ap.add_argument("--no-check", action="store_true",
+                    help="timing-only diagnostic variants (wrong results by design)")
     args = ap.parse_args()
     import torch
     import myscaledb_amd as mq
@@ -44,7 +46,7 @@ def main():
             rescans[v] += st["rescans"]
             if ref is None:
                 ref = (ids.clone(), dist.clone())
-            elif not (torch.equal(ids, ref[0]) and torch.equal(dist, ref[1])):
+            elif not args.no_check and not (torch.equal(ids, ref[0]) and torch.equal(dist, ref[1])):
                 print(json.dumps({"config": v, "error": "results differ from config %s" % variants[0]}),
                       flush=True)
                 return 1
