@@ -202,9 +202,16 @@ int mqvs_set_timing(int enabled);
  * same bits. */
 int mqvs_set_batch_mode(int mode);
 /* Selective PREWHERE scans: 0 = always scan every row and mask, 1 = scan only
- * the selected rows (a device-built gather list) when at most half the part
- * passes the filter (default), 2 = always gather.  All return the same bits. */
+ * the selected rows (a device-built gather list) when few enough pass the
+ * filter (default: <= 60% when the bf16 pre-filter serves the batch, <= 30%
+ * for the exact small-batch kernel), 2 = always gather.  All return the same
+ * bits. */
 int mqvs_set_gather_mode(int mode);
+/* Pre-filter planes built by segments created AFTER the call: 6 = bf16 hi
+ * plane + block-scaled fp6 cross plane, cross terms on the MX MFMA (default;
+ * 3.5 B per element), 3 = bf16 hi + lo planes, three bf16 MFMAs (4 B per
+ * element).  Both bound their error rigorously and return the same bits. */
+int mqvs_set_prefilter(int split);
 
 #ifdef __cplusplus
 }

@@ -29,7 +29,7 @@ SYMBOLS = [
     "mqvs_thread_release", "mqvs_segment_create", "mqvs_segment_create_device",
     "mqvs_segment_generate", "mqvs_segment_free", "mqvs_segment_info", "mqvs_segment_rows",
     "mqvs_search", "mqvs_search_ex", "mqvs_knn_raw", "mqvs_rerank", "mqvs_merge_shards", "mqvs_generate_device",
-    "mqvs_last_search_stats", "mqvs_set_timing", "mqvs_set_batch_mode", "mqvs_set_gather_mode",
+    "mqvs_last_search_stats", "mqvs_set_timing", "mqvs_set_batch_mode", "mqvs_set_gather_mode", "mqvs_set_prefilter",
 ]
 
 
@@ -87,6 +87,7 @@ def _load():
         "mqvs_set_timing": ([ctypes.c_int], ctypes.c_int),
         "mqvs_set_batch_mode": ([ctypes.c_int], ctypes.c_int),
         "mqvs_set_gather_mode": ([ctypes.c_int], ctypes.c_int),
+        "mqvs_set_prefilter": ([ctypes.c_int], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -34,13 +34,6 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) void lds_void;
 
-__host__ __device__ inline uint16_t f32_to_bf16_rn(float x) {
-    uint32_t u = __builtin_bit_cast(uint32_t, x);
-    if ((u & 0x7F800000u) == 0x7F800000u) return (uint16_t)((u >> 16) | ((u & 0xFFFF) ? 0x40 : 0));
-    u += 0x7FFFu + ((u >> 16) & 1u);
-    return (uint16_t)(u >> 16);
-}
-
 // ---------------------------------------------------------------------------
 __global__ void k_to_bf16(const float *src, int64_t rows, int d, int64_t sstride, uint16_t *hi,
                           uint16_t *lo, int64_t dpad) {
@@ -107,15 +100,20 @@ void launch_max_norm(const float *norms2, int64_t n, float *out_max, hipStream_t
 //   approximation with fl(sum (y-x)^2), so add the norms' rounding (d u each)
 //   and the direct sum's own error ((d+3) u (|x|+|y|)^2 <= 2 (d+3) u top):
 //   2 B + (3 d + 12) u top.
+//   split 6 (kernels_mx.hip): from the query variant's norm record q and the
+//   segment's maxima Y (|h| |r| |h6| |h-h6| |r6| |r-r6| |x|):
+//     truncation  q3 Y1 + q2 Y5 + q5 Y0 + q4 Y3 + q1 Y1
+//     accumulation 3.03 d u (q0 Y0 + q2 Y4 + q4 Y2) + 1.01 d u |x||y| (exact chain)
+//     MX internal 2^-10 (q2 Y4 + q4 Y2) (an allowance far above fp32 rounding)
 __global__ void k_query_bound(ScanParams p, int metric, int split, int direct,
-                              const float *ynorm_max, float *bq) {
+                              const float *ynorm_max, const float *qrec, const float *yrec, float *bq) {
     // one wave per query; |x| in fp64 (an upper bound after the 1.0001 slack)
     const int j = blockIdx.x;
     const int lane = threadIdx.x;
     const int64_t qs = (int64_t)((p.d + 31) / 32 * 32);
     const int nv = p.maxv <= 1 ? 1 : p.qmu[j] + p.qlam[j];
     float xmax = 0.f;
-    for (int v = 0; v < nv; ++v) {
+    for (int v = 0; v < (split == kMxSplit ? 0 : nv); ++v) {
         const float *x = p.qvars + ((int64_t)j * p.maxv + v) * qs;
         double s = 0.0;
         for (int i = lane; i < p.d; i += 64) s += (double)x[i] * (double)x[i];
@@ -124,10 +122,28 @@ __global__ void k_query_bound(ScanParams p, int metric, int split, int direct,
     }
     if (lane != 0) return;
     const float ymax = *ynorm_max * (1.0f + 6e-8f * (float)p.d + 1e-6f);  // fp32 |y|^2 chain error
-    const float acc_term = (split == 3 ? 4.1f : 2.04f) * (float)p.d * 5.9604645e-8f;
-    const float c = split == 3 ? 3.1f * 1.5258789e-5f + acc_term + 1.2e-7f
-                               : 0.0078125f + 1.6e-5f + acc_term + 1e-7f;
-    float b = c * (xmax * 1.0001f) * ymax + 1e-30f;
+    const float du = (float)p.d * 5.9604645e-8f;
+    float b;
+    if (split == kMxSplit) {
+        const float *Y = yrec;
+        b = 0.f;
+        for (int v = 0; v < nv; ++v) {
+            const float *q = qrec + ((int64_t)j * p.maxv + v) * kMxRec;
+            xmax = fmaxf(xmax, q[6]);
+            const float trunc = q[3] * Y[1] + q[2] * Y[5] + q[5] * Y[0] + q[4] * Y[3] + q[1] * Y[1];
+            const float mx = q[2] * Y[4] + q[4] * Y[2];
+            const float terms = q[0] * Y[0] + mx;
+            const float bv = trunc + 9.765625e-4f * mx + 3.03f * du * terms + 1.01f * du * q[6] * ymax +
+                             1.2e-7f * q[6] * ymax;
+            b = fmaxf(b, bv * 1.0001f);
+        }
+        b += 1e-30f;
+    } else {
+        const float acc_term = (split == 3 ? 4.1f : 2.04f) * du;
+        const float c = split == 3 ? 3.1f * 1.5258789e-5f + acc_term + 1.2e-7f
+                                   : 0.0078125f + 1.6e-5f + acc_term + 1e-7f;
+        b = c * (xmax * 1.0001f) * ymax + 1e-30f;
+    }
     if (metric == MQVS_METRIC_L2) {
         const float top = p.qnorms[j] * 1.0001f + ymax * ymax;
         const float rel = direct ? (3.0f * (float)p.d + 12.0f) * 5.9604645e-8f : 2.4e-7f;
@@ -140,9 +156,10 @@ __global__ void k_query_bound(ScanParams p, int metric, int split, int direct,
 }
 
 void launch_query_bound(const ScanParams &p, int metric, int split, const float *ynorm_max,
-                        float *bq, hipStream_t s) {
+                        const float *qrec, const float *yrec, float *bq, hipStream_t s) {
     const int direct = p.nq < kBlasThreshold;
-    hipLaunchKernelGGL(k_query_bound, dim3(p.nq), dim3(64), 0, s, p, metric, split, direct, ynorm_max, bq);
+    hipLaunchKernelGGL(k_query_bound, dim3(p.nq), dim3(64), 0, s, p, metric, split, direct, ynorm_max, qrec, yrec,
+                       bq);
 }
 
 

@@ -128,16 +128,19 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
         return;
     }
     const float eps = 1.1920929e-07f;
-    for (int v = 0; v < maxv; ++v) {
-        float *cur = v0 + (int64_t)v * qs;
+    // variants 0..maxv-1 are stored; normalisation maxv is only compared, so a
+    // fixed point reached at the last stored variant is still detected
+    for (int v = 0; v <= maxv; ++v) {
+        float *cur = v < maxv ? v0 + (int64_t)v * qs : nullptr;
         const float sum = seqsum();
         if (sum < eps) {
-            for (int i = lane; i < d; i += 64) cur[i] = qbuf[i];
+            if (cur)
+                for (int i = lane; i < d; i += 64) cur[i] = qbuf[i];
         } else {
             const float s = sqrtf(sum);
             for (int i = lane; i < d; i += 64) {
                 const float x = qbuf[i] / s;
-                cur[i] = x;
+                if (cur) cur[i] = x;
                 qbuf[i] = x;
             }
         }
@@ -158,9 +161,13 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
         }
     }
     if (lane == 0) {
-        atomicOr(status, 1);  // no repeat within maxv normalisations
-        qmu[j] = 0;
+        // no repeat within maxv + 1 normalisations: variants 0..maxv-1 are
+        // exact, later chunk ordinals are not (the host fails the search if
+        // the part has that many searched chunks)
+        atomicOr(status, 1);
+        qmu[j] = maxv - 1;
         qlam[j] = 1;
+        if (qnorms) qnorms[j] = 0.0f;
     }
 }
 

@@ -30,8 +30,11 @@ struct mqvs_segment {
     float *rows = nullptr;
     float *norms = nullptr;          // |y|^2 per row (fvec_norm_L2sqr order)
     uint16_t *rows_hi = nullptr;     // bf16 rounding of the rows, [n][dpad]
-    uint16_t *rows_lo = nullptr;     // bf16 rounding of (row - hi), [n][dpad]
-    float *ynorm_max = nullptr;      // device scalar: max_r |y_r|
+    uint16_t *rows_lo = nullptr;     // bf16 rounding of (row - hi), [n][dpad] (split 3)
+    uint8_t *rows_x6 = nullptr;      // fp6 cross plane [n][dpad/32][48 B] (split 6)
+    uint8_t *rows_sc = nullptr;      // E8M0 scales [n][2] (split 6)
+    float *ynorm_max = nullptr;      // device scalar: max_r |y_r|; split 6: + [kMxRec] norm maxima at +16 B
+    int split = 0;                   // pre-filter planes built: 3, 6, 0 = none
     int64_t dpad = 0;
     bool approx_ok = false;          // bf16 pre-filter usable for this segment
     uint8_t *nonempty_bits = nullptr;// null when every array is non-empty
@@ -44,6 +47,7 @@ namespace mqvs {
 static thread_local std::string g_error;
 static thread_local mqvs_search_stats g_stats{};
 static int g_timing = 0;
+static int g_prefilter = 6;  // planes built by new segments (mqvs_set_prefilter)
 
 void set_error(const std::string &msg) { g_error = msg; }
 
@@ -162,19 +166,39 @@ static void prepare_segment(mqvs_segment *s, const uint8_t *dev_nonempty_bytes,
     launch_row_norms(s->rows, s->n, s->d, s->norms, st);
     // bf16 plane of the rows for the nq >= 20 pre-filter (rows padded to kBfK)
     s->dpad = (s->d + kBfK - 1) / kBfK * kBfK;
-    MQVS_HIP(hipMalloc((void **)&s->ynorm_max, 16));
-    MQVS_HIP(hipMemsetAsync(s->ynorm_max, 0, 16, st));
+    MQVS_HIP(hipMalloc((void **)&s->ynorm_max, 16 + sizeof(float) * kMxRec));
+    MQVS_HIP(hipMemsetAsync(s->ynorm_max, 0, 16 + sizeof(float) * kMxRec, st));
     launch_max_norm(s->norms, s->n, s->ynorm_max, st);
-    const size_t hb = (size_t)std::max<int64_t>(s->n, 1) * s->dpad * sizeof(uint16_t);
-    if (hipMalloc((void **)&s->rows_hi, hb) == hipSuccess &&
-        hipMalloc((void **)&s->rows_lo, hb) == hipSuccess) {
-        s->bytes += 2 * hb;
-        launch_to_bf16(s->rows, s->n, s->d, s->d, s->rows_hi, s->rows_lo, s->dpad, st);
+    const int64_t nr = std::max<int64_t>(s->n, 1);
+    const int64_t nr16 = (nr + 15) / 16 * 16;  // MX planes are blocked by 16 rows
+    const size_t hb = (size_t)(g_prefilter == kMxSplit ? nr16 : nr) * s->dpad * sizeof(uint16_t);
+    const size_t xb = (size_t)nr16 * (s->dpad / 32) * 48;
+    bool ok = hipMalloc((void **)&s->rows_hi, hb) == hipSuccess;
+    if (g_prefilter == kMxSplit) {
+        ok = ok && hipMalloc((void **)&s->rows_x6, xb) == hipSuccess &&
+             hipMalloc((void **)&s->rows_sc, (size_t)nr * 2) == hipSuccess;
+    } else {
+        ok = ok && hipMalloc((void **)&s->rows_lo, hb) == hipSuccess;
+    }
+    if (ok) {
+        if (g_prefilter == kMxSplit) {
+            s->bytes += hb + xb + (size_t)nr * 2;
+            launch_to_mx(s->rows, s->n, s->d, s->d, s->dpad, 1, nr16, true, s->rows_hi, s->rows_x6, s->rows_sc,
+                         nullptr, s->ynorm_max + 4, st);
+            s->split = kMxSplit;
+        } else {
+            s->bytes += 2 * hb;
+            launch_to_bf16(s->rows, s->n, s->d, s->d, s->rows_hi, s->rows_lo, s->dpad, st);
+            s->split = kBfSplit;
+        }
     } else {
         (void)hipGetLastError();  // no room: exact fp32 batch path only
-        if (s->rows_hi) (void)hipFree(s->rows_hi);
+        for (void *q : {(void *)s->rows_hi, (void *)s->rows_lo, (void *)s->rows_x6, (void *)s->rows_sc})
+            if (q) (void)hipFree(q);
         s->rows_hi = nullptr;
         s->rows_lo = nullptr;
+        s->rows_x6 = nullptr;
+        s->rows_sc = nullptr;
     }
     MQVS_HIP(hipGetLastError());
     float ymax = 0.f;
@@ -226,6 +250,8 @@ static void free_segment(mqvs_segment *s) {
     if (s->nonempty_bits) (void)hipFree(s->nonempty_bits);
     if (s->rows_hi) (void)hipFree(s->rows_hi);
     if (s->rows_lo) (void)hipFree(s->rows_lo);
+    if (s->rows_x6) (void)hipFree(s->rows_x6);
+    if (s->rows_sc) (void)hipFree(s->rows_sc);
     if (s->ynorm_max) (void)hipFree(s->ynorm_max);
     if (s->chunk_ord) (void)hipFree(s->chunk_ord);
     if (cur >= 0) (void)hipSetDevice(cur);
@@ -269,6 +295,8 @@ static void run_scan(ScanParams p, const Range &r, int kind, int metric, bool pr
     p.tile_rows = kind == kScanSmall ? kSmallRows : kind == kScanBf16 ? kBfRows : kMfmaRows;
     if (kind == kScanMfma32)
         launch_scan_mfma(p, metric, probe, st);
+    else if (kind == kScanBf16 && p.rows_x6)
+        launch_scan_mx(p, metric, probe, st);
     else if (kind == kScanBf16)
         launch_scan_bf16(p, metric, probe, kBfSplit, st);
     else
@@ -476,18 +504,42 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
 
     float *bq = nullptr;
     if (kind == kScanBf16) {
-        // bf16 rounding of the query variants + per-query error bound
-        const size_t qe = (size_t)nq * maxv * seg->dpad;
-        uint16_t *qhi = (uint16_t *)ws.qhi.get(2 * sizeof(uint16_t) * qe);
-        launch_to_bf16(qvars, (int64_t)nq * maxv, d, qstride, qhi, qhi + qe, seg->dpad, s);
+        // split planes of the query variants + per-query error bound
+        const int64_t nvec = (int64_t)nq * maxv;
+        const size_t qe = (size_t)nvec * seg->dpad;
         bq = (float *)ws.bq.get(sizeof(float) * nq);
         p.rows_hi = seg->rows_hi;
-        p.rows_lo = seg->rows_lo;
-        p.q_hi = qhi;
-        p.q_lo = qhi + qe;
         p.dpad = seg->dpad;
         p.thr = (const float *)ws.thr.get(sizeof(float) * nq);
-        launch_query_bound(p, metric, kBfSplit, seg->ynorm_max, bq, s);
+        if (seg->split == kMxSplit) {
+            // [hi: maxv x vpad x dpad x 2 B][fp6: maxv x vpad x dpad/32 x 48 B]
+            // [scales: nvec x 2][records: nvec x kMxRec floats]
+            const int64_t vpad = round_up(nq, 16);
+            const int64_t pvec = (int64_t)maxv * vpad;
+            const size_t o_x6 = (size_t)round_up(pvec * seg->dpad * 2, 256);
+            const size_t o_sc = (size_t)round_up((int64_t)(o_x6 + (size_t)pvec * (seg->dpad / 32) * 48), 256);
+            const size_t o_rec = (size_t)round_up((int64_t)(o_sc + (size_t)nvec * 2), 256);
+            auto *base = (unsigned char *)ws.qhi.get(o_rec + sizeof(float) * kMxRec * (size_t)nvec);
+            auto *qhi = (uint16_t *)base;
+            auto *qx6 = base + o_x6;
+            auto *qsc = base + o_sc;
+            auto *qrec = (float *)(base + o_rec);
+            launch_to_mx(qvars, nvec, d, qstride, seg->dpad, maxv, vpad, false, qhi, qx6, qsc, qrec, nullptr, s);
+            p.q_vpad = vpad;
+            p.q_hi = qhi;
+            p.rows_x6 = seg->rows_x6;
+            p.rows_sc = seg->rows_sc;
+            p.q_x6 = qx6;
+            p.q_sc = qsc;
+            launch_query_bound(p, metric, kMxSplit, seg->ynorm_max, qrec, seg->ynorm_max + 4, bq, s);
+        } else {
+            uint16_t *qhi = (uint16_t *)ws.qhi.get(2 * sizeof(uint16_t) * qe);
+            launch_to_bf16(qvars, nvec, d, qstride, qhi, qhi + qe, seg->dpad, s);
+            p.rows_lo = seg->rows_lo;
+            p.q_hi = qhi;
+            p.q_lo = qhi + qe;
+            launch_query_bound(p, metric, kBfSplit, seg->ynorm_max, nullptr, nullptr, bq, s);
+        }
         MQVS_HIP(hipGetLastError());
     }
 
@@ -558,7 +610,11 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         MQVS_HIP(hipMemcpyAsync(ws.host_flags, overflow, sizeof(int), hipMemcpyDeviceToHost, s));
         MQVS_HIP(hipMemcpyAsync(ws.host_flags + 1, status, sizeof(int), hipMemcpyDeviceToHost, s));
         MQVS_HIP(hipStreamSynchronize(s));
-        if (ws.host_flags[1]) fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not reach a cycle");
+        // a query whose re-normalisation does not repeat within kMaxVariants
+        // steps is exact only on the part's first kMaxVariants chunk ordinals
+        if (ws.host_flags[1] && p.ord_base + (n + seg->granule - 1) / seg->granule > kMaxVariants)
+            fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not repeat within " +
+                                       std::to_string(kMaxVariants) + " steps on a part of more chunks");
         if (kind == kScanBf16 && ws.host_flags[0]) {
             // the bf16 bound left too many candidates: exact fp32 path
             search_impl(seg, queries, nq, k, metric, filter, exists, out_ids, out_dist, flags,
@@ -697,7 +753,9 @@ static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const i
     if (dev && (flags & MQVS_F_ASYNC)) return;
     MQVS_HIP(hipMemcpyAsync(ws.host_flags, status, sizeof(int), hipMemcpyDeviceToHost, s));
     MQVS_HIP(hipStreamSynchronize(s));
-    if (ws.host_flags[0]) fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not reach a cycle");
+    if (ws.host_flags[0] && p.ord_base + (seg->n + seg->granule - 1) / seg->granule > kMaxVariants)
+        fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not repeat within " + std::to_string(kMaxVariants) +
+                                   " steps on a part of more chunks");
     if (!dev) {
         MQVS_HIP(hipMemcpyAsync(out_ids, dids, sizeof(int64_t) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
         MQVS_HIP(hipMemcpyAsync(out_dist, ddist, sizeof(float) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
@@ -960,6 +1018,12 @@ int mqvs_last_search_stats(mqvs_search_stats *out) {
 int mqvs_set_batch_mode(int mode) {
     if (mode != 0 && mode != 1) return MQVS_ERR_BAD_ARGUMENTS;
     g_batch_mode = mode;
+    return MQVS_OK;
+}
+
+int mqvs_set_prefilter(int split) {
+    if (split != kBfSplit && split != kMxSplit) return MQVS_ERR_BAD_ARGUMENTS;
+    g_prefilter = split;
     return MQVS_OK;
 }
 

@@ -13,7 +13,7 @@ namespace mqvs {
 // ---------------------------------------------------------------------------
 // Tunables
 constexpr int kBlasThreshold = 20;   // faiss distance_compute_blas_threshold
-constexpr int kMaxVariants = 16;     // cosine query re-normalisation variants kept
+constexpr int kMaxVariants = 32;     // cosine query re-normalisation variants kept
 constexpr int kSortCap = 4096;       // candidates sorted in LDS per query
 constexpr int64_t kCandBudget = 1 << 25;  // candidate slots per search (x 8 B)
 constexpr int64_t kCandMax = 1 << 20;     // candidate slots per query
@@ -77,6 +77,14 @@ __host__ __device__ inline uint32_t key32_rt(int metric, float raw) {
                                           : key32<kMetricIpRaw>(raw);
 }
 
+// bf16 bits of x, round to nearest even (NaN stays NaN)
+__host__ __device__ inline uint16_t f32_to_bf16_rn(float x) {
+    uint32_t u = __builtin_bit_cast(uint32_t, x);
+    if ((u & 0x7F800000u) == 0x7F800000u) return (uint16_t)((u >> 16) | ((u & 0xFFFF) ? 0x40 : 0));
+    u += 0x7FFFu + ((u >> 16) & 1u);
+    return (uint16_t)(u >> 16);
+}
+
 __device__ inline bool bit_test(const uint8_t *bm, int64_t i) {
     return (bm[i >> 3] >> (i & 7)) & 1;
 }
@@ -119,6 +127,15 @@ struct ScanParams {
     const uint16_t *q_hi;     // [nq][maxv][dpad]
     const uint16_t *q_lo;     // [nq][maxv][dpad] (split 3)
     int64_t dpad;
+    // MX pre-filter (kernels_mx.hip): fp6 cross planes, [vec][dpad/32][48 B]
+    // (two 32-element e2m3 halves per 32 columns, layout in kernels_mx.hip),
+    // E8M0 scale per vector and half [vec][2]
+    const uint8_t *rows_x6;   // halves (bf16 residual, hi)
+    const uint8_t *rows_sc;
+    const uint8_t *q_x6;      // halves (hi, bf16 residual), plane vector v q_vpad + j
+    const uint8_t *q_sc;      // [nq][maxv][2]
+    int64_t q_vpad;           // nq rounded up to 16 (MX query planes)
+    int xcd_mode;             // MX scan workgroup -> XCD grouping (kernels_mx.hip)
     const float *thr;         // [nq] APPEND threshold on the approximate raw value
     // gather mode (selective PREWHERE): the scan walks positions of this list
     // of selected rows instead of rows; each chunk's rows are padded with -1 to
@@ -221,13 +238,26 @@ void launch_chunk_ordinals(const uint8_t *filter, const uint8_t *nonempty, const
 // bf16 pre-filter path (kernels_bf16.hip)
 constexpr int kBfK = 64;    // bf16 planes padded to a multiple of this
 constexpr int kBfSplit = 3; // hi*hi + hi*lo + lo*hi (see kernels_bf16_scan.hip)
+constexpr int kMxSplit = 6; // bf16 hi*hi + fp6-MX (hi*res + res*hi) (kernels_mx.hip)
+constexpr int kMxRec = 8;   // floats per vector in the MX norm records (kernels_mx.hip)
 // dst_hi = bf16_rn(x); dst_lo (optional) = bf16_rn(x - hi)
 void launch_to_bf16(const float *src, int64_t rows, int d, int64_t src_stride, uint16_t *dst_hi,
                     uint16_t *dst_lo, int64_t dpad, hipStream_t s);
 void launch_max_norm(const float *norms2, int64_t n, float *out_max, hipStream_t s);
+// split 6: qrec [nq][maxv][kMxRec] query-variant norms, yrec [kMxRec] segment maxima
 void launch_query_bound(const ScanParams &p, int metric, int split, const float *ynorm_max,
-                        float *bq, hipStream_t s);
+                        const float *qrec, const float *yrec, float *bq, hipStream_t s);
 void launch_scan_bf16(const ScanParams &p, int metric, bool probe, int split, hipStream_t s);
+// MX pre-filter (kernels_mx.hip).  to_mx: bf16 hi plane [rows][dpad], fp6
+// cross plane, scales, and per-vector norm records (rec, optional) / their
+// maxima over the vectors (maxrec, optional, atomic); res_first: rows
+// (residual half first) vs queries (hi half first)
+// planes are row-blocked (16 vectors x 32 columns contiguous, kernels_mx.hip);
+// source vector v goes to plane vector (v % vgroup) vpad + v / vgroup
+void launch_to_mx(const float *src, int64_t rows, int d, int64_t src_stride, int64_t dpad, int64_t vgroup,
+                  int64_t vpad, bool res_first, uint16_t *hi, uint8_t *x6, uint8_t *sc, float *rec, float *maxrec,
+                  hipStream_t s);
+void launch_scan_mx(const ScanParams &p, int metric, bool probe, hipStream_t s);
 void launch_probe_select_approx(const float *probe, int64_t P, int64_t ld, int nq, int k,
                                 int metric, const float *bq, float *thr, int *cand_count,
                                 Cand *cand, int cand_cap, const int32_t *row_list, hipStream_t s);

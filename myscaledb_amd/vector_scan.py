@@ -260,8 +260,16 @@ def set_timing(enabled: bool):
 
 def set_gather_mode(mode: int):
     """Selective PREWHERE: 0 scan all rows + mask, 1 gather the selected rows
-    when <= 50% pass (default), 2 always gather (mqvs_set_gather_mode)."""
+    when few pass (default: <= 60% on the bf16 pre-filter, <= 30% on the exact
+    small-batch kernel), 2 always gather (mqvs_set_gather_mode)."""
     check(lib.mqvs_set_gather_mode(int(mode)))
+
+
+def set_prefilter(split: int):
+    """Pre-filter planes of segments created after the call: 6 = bf16 hi +
+    block-scaled fp6 cross plane (default), 3 = bf16 hi + lo planes
+    (mqvs_set_prefilter).  Both return the same bits."""
+    check(lib.mqvs_set_prefilter(int(split)))
 
 
 def set_batch_mode(mode: int):

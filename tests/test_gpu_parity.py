@@ -167,6 +167,55 @@ def test_gpu_vs_oracle_fp32_batch_mode(mq, cfg):
         set_batch_mode(0)
 
 
+@pytest.mark.parametrize("cfg", BATCH, ids=[c[0] for c in BATCH])
+def test_gpu_vs_oracle_split3_prefilter(mq, cfg):
+    """nq >= 8 through the split-3 pre-filter (bf16 hi + lo planes, three bf16
+    MFMAs; the default is split 6, bf16 + fp6-MX cross terms): same bits."""
+    from myscaledb_amd.vector_scan import set_prefilter
+    set_prefilter(3)
+    try:
+        run_parity(mq, cfg)
+    finally:
+        set_prefilter(6)
+
+
+def _wide_range_part(seed, n, d, nq, near):
+    """Rows whose elements span ~8 decades inside one vector (the per-vector
+    fp6 scales leave the small elements almost nothing), plus `near` rows that
+    are tiny perturbations of one row (many approximate values inside the
+    bound's window)."""
+    rng = np.random.default_rng(seed)
+    mag = 10.0 ** rng.uniform(-4, 4, size=(n, d))
+    rows = (rng.standard_normal((n, d)) * mag).astype(np.float32)
+    base = rows[0].copy()
+    for i in range(1, near + 1):
+        rows[i] = base * (1 + 1e-6 * rng.standard_normal(d)).astype(np.float32)
+    q = (rng.standard_normal((nq, d)) * 10.0 ** rng.uniform(-4, 4, size=(nq, d))).astype(np.float32)
+    q[: nq // 2] = base * (1 + 1e-3 * rng.standard_normal(d)).astype(np.float32)
+    return rows, q
+
+
+@pytest.mark.parametrize("split", [6, 3])
+@pytest.mark.parametrize("metric", ["L2", "IP", "Cosine"])
+@pytest.mark.parametrize("nq", [12, 40])
+def test_prefilter_wide_dynamic_range(mq, split, metric, nq):
+    """The pre-filter bound holds on adversarial magnitudes: bit-identical to
+    the oracle (the bound is computed from measured quantisation norms, so
+    poorly represented data only widens the candidate window)."""
+    from myscaledb_amd.vector_scan import set_prefilter
+    rows, q = _wide_range_part(1000 + nq, 6000, 96, nq, near=300)
+    m = O.METRICS[metric]
+    ids_o, dist_o = O.vector_scan(rows, q, 50, m, 1024, fast=True)
+    set_prefilter(split)
+    try:
+        seg = mq.VectorScanSegment.from_rows(rows, metric=metric, granule=1024)
+        ids_g, dist_g = seg.search(q, 50, metric)
+        seg.free()
+    finally:
+        set_prefilter(6)
+    assert_bitwise(ids_g, dist_g, ids_o, dist_o, f"wide split={split} {metric} nq={nq}")
+
+
 def run_parity(mq, cfg):
     name, n, d, nq, k, metric, mode, gran, filt, lwd, empty = cfg
     seed = zlib.crc32(name.encode())
@@ -383,6 +432,45 @@ def test_path_selection(mq):
     finally:
         set_batch_mode(0)
         seg.free()
+
+
+@pytest.mark.parametrize("nq", [1, 9, 24])
+def test_cosine_slow_normalisation_cycle(mq, nq):
+    """A query whose repeated fp32 re-normalisation first repeats at step 16
+    (mu 15, lam 1: generator mode 2, seed 12, d 256, query 259) on a part of
+    24 chunks, so chunk ordinals 15 and up use the late variants."""
+    q = O.generate(12, 2, 0, 300, 256)
+    queries = np.concatenate([q[259:260], q[:nq - 1]])
+    rows = O.generate(77, 2, 0, 24 * 128, 256)
+    ids_o, dist_o = O.vector_scan(rows, queries, 20, O.COSINE, 128, fast=True)
+    seg = mq.VectorScanSegment.from_rows(rows, metric="Cosine", granule=128)
+    try:
+        ids_g, dist_g = seg.search(queries, 20, "Cosine")
+    finally:
+        seg.free()
+    assert_bitwise(ids_g, dist_g, ids_o, dist_o, f"slow cycle nq={nq}")
+
+
+@pytest.mark.parametrize("split", [6, 3])
+def test_prefilter_no_exact_fallback(mq, split):
+    """Both pre-filters keep the survivors within the re-rank's capacity on
+    ordinary data (no silent fallback to the exact fp32 path: rescans 0)."""
+    from myscaledb_amd import _lib
+    from myscaledb_amd.vector_scan import set_prefilter
+    set_prefilter(split)
+    try:
+        for metric, mode in (("L2", 1), ("IP", 1), ("Cosine", 1)):
+            rows = O.generate(11, mode, 0, 30000, 256)
+            seg = mq.VectorScanSegment.from_rows(rows, metric=metric, granule=8192)
+            try:
+                for nq in (8, 64, 300):
+                    seg.search(O.generate(12, mode, 0, nq, 256), 100)
+                    st = _lib.last_search_stats()
+                    assert st["path"] == 2 and st["rescans"] == 0, (metric, nq, st)
+            finally:
+                seg.free()
+    finally:
+        set_prefilter(6)
 
 
 @pytest.mark.parametrize("nq", [3, 12, 40])

@@ -1,9 +1,12 @@
 #!/usr/bin/env python3
-"""A/B workgroup shapes / schedule variants of the bf16 scan in ONE process
-(interleaved rounds), on the bench workload (10M x 768 cosine, nq=1000 by
-default).  A config is "WQ,QB,VAR" (kernels_bf16_scan.hip, MQVS_BF16_TUNE).
-Every config must return the same bits as the first.  Prints one JSON line
-per config: min / median main-scan ms and the bf16x3 TFLOP/s."""
+"""A/B workgroup shapes / schedule variants of the pre-filter scans in ONE
+process (interleaved rounds), on the bench workload (10M x 768 cosine,
+nq=1000 by default).  A config is "WQ,QB,VAR" or "bf:WQ,QB,VAR" for the split-3
+bf16 scan (kernels_bf16_scan.hip, MQVS_BF16_TUNE) and "mx:WQ,QB,VAR" for the
+split-6 MX scan (kernels_mx.hip, MQVS_MX_TUNE); "mx:default" / "bf:default"
+take the library's own choice; a suffix "@xG" sets MQVS_MX_XCD=G.  Every config must return the same bits as the
+first.  Prints one JSON line per config: min / median main-scan ms and the
+split-3-equivalent TFLOP/s (3 x 2 nq n d per scan, whatever the split)."""
 import argparse
 import json
 import os
@@ -30,18 +33,33 @@ def main():
     from myscaledb_amd import _lib
     from myscaledb_amd.vector_scan import generate_device, set_timing
     mq.init(0)
-    seg = mq.VectorScanSegment.generate(0x5EED0001, 2, args.n, args.d, "Cosine", 8192)
+    from myscaledb_amd.vector_scan import set_prefilter
+    variants = args.configs.split(";")
+    segs = {}
+    for kind, split in (("bf", 3), ("mx", 6)):
+        if any(v.startswith(kind + ":") or (kind == "bf" and ":" not in v) for v in variants):
+            set_prefilter(split)
+            segs[kind] = mq.VectorScanSegment.generate(0x5EED0001, 2, args.n, args.d, "Cosine", 8192)
+    set_prefilter(6)
     q = torch.empty((args.nq, args.d), dtype=torch.float32, device="cuda")
     generate_device(0x5EED0002, 2, 0, args.nq, args.d, q)
-    variants = args.configs.split(";")
     ref = None
     times = {v: [] for v in variants}
     rescans = {v: 0 for v in variants}
     set_timing(True)
     for rnd in range(args.rounds + 1):
         for v in variants:
-            os.environ["MQVS_BF16_TUNE"] = v
-            ids, dist = seg.search(q, args.k)
+            kind, cfg = v.split(":") if ":" in v else ("bf", v)
+            env = "MQVS_MX_TUNE" if kind == "mx" else "MQVS_BF16_TUNE"
+            os.environ.pop("MQVS_MX_TUNE", None)
+            os.environ.pop("MQVS_BF16_TUNE", None)
+            os.environ.pop("MQVS_MX_XCD", None)
+            if "@x" in cfg:  # "@xG": MX workgroup -> XCD grouping G (kernels_mx.hip)
+                cfg, g = cfg.split("@x")
+                os.environ["MQVS_MX_XCD"] = g
+            if cfg != "default":
+                os.environ[env] = cfg
+            ids, dist = segs[kind].search(q, args.k)
             st = _lib.last_search_stats()
             rescans[v] += st["rescans"]
             if ref is None:
@@ -61,7 +79,8 @@ def main():
                           "main_ms_med": round(statistics.median(t), 3),
                           "bf16x3_TFLOPs_med": round(flop / (statistics.median(t) * 1e-3) / 1e12, 1),
                           "rescans": rescans[v]}), flush=True)
-    seg.free()
+    for sg in segs.values():
+        sg.free()
     return 0
 
 
