@@ -216,7 +216,33 @@ def main():
     main_ms = float(np.mean([s["main_ms"] for s in stats]))
     st = stats[-1]
     main_rows = st["main_rows"]
-    if nq >= 20 and st["path"] == 2:
+    if nq >= 20 and st["path"] == 2 and st.get("prefilter") == 6:
+        # MX pre-filter (kernels_mx.hip): per 32x32 block and 32 columns, two
+        # v_mfma_f32_32x32x16_bf16 (hi*hi) + one v_mfma_scale_f32_32x32x64_f8f6f4
+        # (fp6 cross terms), which issues in the cycles of one bf16 32x32x16
+        # (tools/mx_probe.hip): executed matrix work = 1.5 x the bf16 flops of
+        # one fp32 product, priced against the dense bf16 peak
+        alg = 2.0 * nq * main_rows * d
+        flop = 1.5 * alg
+        achieved = flop / (main_ms * 1e-3) / 1e12
+        plane_bytes = 3.5 * main_rows * seg_dpad(d)  # bf16 hi + fp6 cross planes, once per query block
+        qb = -(-nq // 256)
+        stream = (3.5 * main_rows * seg_dpad(d) * qb + 3.5 * nq * seg_dpad(d) * -(-main_rows // 256))
+        roof = {"bound": "mfma", "kernel": "k_scan_mx<metric,APPEND,WQ=2,QB=4,VAR=3> "
+                                           "(bf16 32x32x16 + fp6-MX 32x32x64; all main-scan segments of a search)",
+                "achieved": round(achieved, 2), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / BF16_MFMA_PEAK_TFLOPS, 4), "traffic": None,
+                "flop_definition": "bf16-cycle-equivalent MFMA flops = 2*nq*rows*d (hi*hi) + "
+                                   "2*nq*rows*2d / 4 (fp6 MX cross terms at 4x the bf16 rate)",
+                "algorithmic_fp32_tflops": round(alg / (main_ms * 1e-3) / 1e12, 2),
+                "algorithmic_vs_fp32_mfma_peak": round(alg / (main_ms * 1e-3) / 1e12 / FP32_MFMA_PEAK_TFLOPS, 3),
+                "hbm_frac_algorithmic": round(plane_bytes / (main_ms * 1e-3) / 1e9 / HBM_PEAK_GBS, 4),
+                "l2_to_lds_tb_s": round(stream / (main_ms * 1e-3) / 1e12, 2),
+                "note": ("co-bound by the L2->LDS stream (Y x query blocks + Q x row tiles) and the MFMA + "
+                         "LDS-read issue: DESIGN.md, MX pre-filter measurements"),
+                "per_search": {"rows": main_rows, "flop": flop, "algorithmic_bytes": plane_bytes,
+                               "l2_to_lds_bytes": stream, "ms": round(main_ms, 3), "launches": st["segments"]}}
+    elif nq >= 20 and st["path"] == 2:
         # bf16x3 split pre-filter: 3 bf16 MFMA products per fp32 MAC
         alg = 2.0 * nq * main_rows * d
         flop = 3.0 * alg
@@ -253,7 +279,8 @@ def main():
         with open(pmc_path) as f:
             pmc = json.load(f)
         for name, kinfo in pmc.get("kernels", {}).items():
-            if "false, 3, 2, 4, 7" in name and "hbm_bytes_per_search" in kinfo:
+            want = "k_scan_mx<" if st.get("prefilter") == 6 else "k_scan_bf16<"
+            if want in name and "false" in name and "hbm_bytes_per_search" in kinfo:
                 roof["traffic"] = round(kinfo["hbm_bytes_per_search"])
                 roof["traffic_unit"] = "HBM bytes per search (all main-scan launches)"
                 roof["traffic_source"] = os.path.relpath(pmc_path, ROOT)
@@ -281,7 +308,10 @@ def main():
             "scaling": "strong",
             "vs_baseline": None,
             "dtype": "f32",
-            "compute": ("bf16x3 split MFMA pre-filter (rigorous error bound) + exact f32 fma-chain "
+            "compute": ("bf16 + fp6-MX split MFMA pre-filter (rigorous error bound) + exact f32 fma-chain "
+                        "re-rank; results bit-identical to the f32 path" if st["path"] == 2 and
+                        st.get("prefilter") == 6 else
+                        "bf16x3 split MFMA pre-filter (rigorous error bound) + exact f32 fma-chain "
                         "re-rank; results bit-identical to the f32 path" if st["path"] == 2 else
                         "f32 MFMA fma chain" if st["path"] == 1 else "f32 VALU, product then add"),
             "data": "synthetic (counter-based gaussian mixture, generated in HBM)",

@@ -192,6 +192,8 @@ typedef struct {
     int32_t segments;       /* main-scan segments (threshold refinements + 1) */
     int32_t gather;         /* 1: selective PREWHERE, the scan walked the gather list
                                of selected rows (rows_scanned = list entries) */
+    int32_t prefilter;      /* path 2: pre-filter split (6 = bf16 + fp6 MX, 3 = bf16 x3) */
+    int32_t reserved;
 } mqvs_search_stats;
 int mqvs_last_search_stats(mqvs_search_stats *out);
 /* Enable per-search HIP-event timing (off by default: one extra event pair). */

@@ -41,7 +41,8 @@ class SearchStats(ctypes.Structure):
                 ("probe_rows", ctypes.c_int64), ("main_rows", ctypes.c_int64),
                 ("nq", ctypes.c_int32), ("k", ctypes.c_int32),
                 ("path", ctypes.c_int32), ("rescans", ctypes.c_int32),
-                ("segments", ctypes.c_int32), ("gather", ctypes.c_int32)]
+                ("segments", ctypes.c_int32), ("gather", ctypes.c_int32),
+                ("prefilter", ctypes.c_int32), ("reserved", ctypes.c_int32)]
 
 
 def _share_hip_runtime_with_torch():

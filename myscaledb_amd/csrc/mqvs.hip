@@ -599,6 +599,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[4], s));
 
     st.path = kind;
+    st.prefilter = kind == kScanBf16 ? seg->split : 0;
     st.probe_rows = P;
     st.main_rows = scan_n - P;
     st.rows_scanned = scan_n;

@@ -29,7 +29,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root", help="directory holding pmc1/ pmc2/ pmc3/ (gpurun_out)")
     ap.add_argument("--searches", type=int, required=True)
-    ap.add_argument("--kernel", default="k_scan_bf16")
+    ap.add_argument("--kernel", default="k_scan_(?:bf16|mx)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
