@@ -170,6 +170,78 @@ int mqvs_merge_shards(int32_t nshards, int32_t nq, int32_t k, int32_t metric,
 int mqvs_generate_device(uint64_t seed, int32_t mode, int64_t row0, int64_t n, int32_t d,
                          float *dev_out, mqvs_stream_t stream);
 
+/* ---- index path: MSTG-type vector index over a resident segment ----------
+ * The reference's index seam for one data part and vector column:
+ *   mqvs_index_build   Search::createVectorIndex<IStream, OStream, DenseBitmap,
+ *                      FloatVector>(name, IndexType::MSTG, metric, dim, total_vec,
+ *                      params, ...) + VectorIndex::build(...)
+ *                      (src/VectorIndex/Common/VIWithDataPart.cpp:416-447,
+ *                      VIWithDataPart.h:295-339)
+ *   mqvs_index_search  VectorIndex::search(queries, k, params, first_stage_only,
+ *                      filter) as VIWithColumnInPart::search calls it
+ *                      (VIWithDataPart.cpp:858-957, the call at :926)
+ *   computeTopDistanceSubset (stage 2 of a two-stage search,
+ *                      VIWithDataPart.cpp:838-856) is mqvs_rerank on the
+ *                      index's segment.
+ * The MSTG library is absent from the reference snapshot; this
+ * is a GPU-native index with its parameter surface: a k-means partition of the
+ * part into lists stored as one bf16 plane in list order, an MFMA scan of the
+ * lists each query probes, and an exact fp32 re-rank of the best num_reorder
+ * candidates (distances bit-identical to mqvs_search / mqvs_rerank for the
+ * same rows).
+ * The segment must outlive the index.  index_type: "MSTG" (also accepted:
+ * "IVFFLAT").  params: comma-separated key=value (Search::Parameters):
+ *   metric_type  L2 | IP | Cosine (must match the segment's metric family;
+ *                default: the segment's metric)
+ *   alpha        default search alpha (MSTG's accuracy knob, [1, 4], default 3)
+ *   nlist        lists (default about n / 1000)
+ *   kmeans_iters k-means iterations (default 8)
+ *   sample       k-means training rows (default min(n, 64 * nlist))
+ * Unknown keys fail with MQVS_ERR_BAD_ARGUMENTS. */
+typedef struct mqvs_index *mqvs_index_t;
+int mqvs_index_build(mqvs_segment_t seg, const char *index_type, const char *params, mqvs_index_t *out);
+int mqvs_index_free(mqvs_index_t idx);
+typedef struct {
+    int64_t nlist;        /* lists */
+    int64_t npos;         /* positions of the list-ordered plane (with padding) */
+    int64_t max_list;     /* longest list */
+    int64_t rows_indexed; /* rows in some list (empty arrays are not indexed) */
+    int32_t metric;
+    int32_t dim;
+    size_t hbm_bytes;     /* index-owned HBM (the segment's rows not counted) */
+    double build_ms;
+} mqvs_index_info_t;
+int mqvs_index_info(mqvs_index_t idx, mqvs_index_info_t *out);
+/* Search params (comma-separated key=value, may be NULL or ""):
+ *   alpha        [1, 4]: probes nprobe(alpha) lists (more = higher recall)
+ *   nprobe       lists probed per query (overrides alpha; <= min(nlist, 4096))
+ *   num_reorder  candidates re-ranked exactly (default max(2k, 64), <= 4096)
+ * filter / row_exists: LSB-first bitmaps over the segment's rows, or NULL.
+ * Output as mqvs_search (k per query, reference order, -1 padding).  With
+ * MQVS_F_FIRST_STAGE the call returns the first stage only: the k best rows
+ * by the approximate bf16 distance (approximate distances), to be re-ranked
+ * by mqvs_rerank (the reference's two-stage search). */
+#define MQVS_F_FIRST_STAGE 0x8u
+int mqvs_index_search(mqvs_index_t idx, const float *queries, int32_t nq, int32_t k, const char *params,
+                      const uint8_t *filter, const uint8_t *row_exists, int64_t *out_ids, float *out_dist,
+                      uint32_t flags, mqvs_stream_t stream);
+/* Stats of the calling thread's last mqvs_index_search (times only with
+ * mqvs_set_timing(1)). */
+typedef struct {
+    double coarse_ms;     /* nearest lists per query (FLAT search over the centroids) */
+    double plan_ms;       /* grouping (query, list) pairs into work items */
+    double scan_ms;       /* bf16 MFMA scan of the probed lists */
+    double select_ms;     /* num_reorder best approximate values per query */
+    double rerank_ms;     /* exact fp32 re-rank + top-k */
+    double total_ms;
+    int64_t values;       /* approximate values computed (query x probed position) */
+    int64_t items;        /* scan work items (list x 16-query group) */
+    int64_t plane_bytes;  /* bf16 plane bytes streamed by the scan */
+    int64_t pairs;        /* (query, list) pairs */
+    int32_t nq, k, nprobe, num_reorder;
+} mqvs_index_search_stats;
+int mqvs_index_last_stats(mqvs_index_search_stats *out);
+
 /* ---- observability -------------------------------------------------------
  * Stats of the calling thread's last mqvs_search: per-launch kernel times
  * (ms, HIP events on the search stream; only with mqvs_set_timing(1)), rows

@@ -14,6 +14,7 @@ from .vector_scan import (  # noqa: F401
     try_brute_force_search,
     vector_scan_without_index,
 )
+from .vector_index import VectorIndex  # noqa: F401
 
 __all__ = ["VectorScanSegment", "init", "merge_shards", "pack_bitmap",
-           "try_brute_force_search", "vector_scan_without_index"]
+           "try_brute_force_search", "vector_scan_without_index", "VectorIndex"]

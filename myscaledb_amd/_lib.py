@@ -22,6 +22,7 @@ ERR_NOT_IMPLEMENTED, ERR_LOGICAL, ERR_ILLEGAL_COLUMN, ERR_BAD_ARGUMENTS, ERR_MEM
 F_DEVICE_PTRS = 0x1
 F_ASYNC = 0x2
 F_PART_MERGE = 0x4
+F_FIRST_STAGE = 0x8
 
 # Exported C symbols: every one of these is declared in include/mqvs.h.
 SYMBOLS = [
@@ -30,6 +31,7 @@ SYMBOLS = [
     "mqvs_segment_generate", "mqvs_segment_free", "mqvs_segment_info", "mqvs_segment_rows",
     "mqvs_search", "mqvs_search_ex", "mqvs_knn_raw", "mqvs_rerank", "mqvs_merge_shards", "mqvs_generate_device",
     "mqvs_last_search_stats", "mqvs_set_timing", "mqvs_set_batch_mode", "mqvs_set_gather_mode", "mqvs_set_prefilter",
+    "mqvs_index_build", "mqvs_index_free", "mqvs_index_info", "mqvs_index_search", "mqvs_index_last_stats",
 ]
 
 
@@ -43,6 +45,22 @@ class SearchStats(ctypes.Structure):
                 ("path", ctypes.c_int32), ("rescans", ctypes.c_int32),
                 ("segments", ctypes.c_int32), ("gather", ctypes.c_int32),
                 ("prefilter", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+
+
+class IndexInfo(ctypes.Structure):
+    _fields_ = [("nlist", ctypes.c_int64), ("npos", ctypes.c_int64), ("max_list", ctypes.c_int64),
+                ("rows_indexed", ctypes.c_int64), ("metric", ctypes.c_int32), ("dim", ctypes.c_int32),
+                ("hbm_bytes", ctypes.c_size_t), ("build_ms", ctypes.c_double)]
+
+
+class IndexSearchStats(ctypes.Structure):
+    _fields_ = [("coarse_ms", ctypes.c_double), ("plan_ms", ctypes.c_double),
+                ("scan_ms", ctypes.c_double), ("select_ms", ctypes.c_double),
+                ("rerank_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
+                ("values", ctypes.c_int64), ("items", ctypes.c_int64),
+                ("plane_bytes", ctypes.c_int64), ("pairs", ctypes.c_int64),
+                ("nq", ctypes.c_int32), ("k", ctypes.c_int32),
+                ("nprobe", ctypes.c_int32), ("num_reorder", ctypes.c_int32)]
 
 
 def _share_hip_runtime_with_torch():
@@ -89,6 +107,11 @@ def _load():
         "mqvs_set_batch_mode": ([ctypes.c_int], ctypes.c_int),
         "mqvs_set_gather_mode": ([ctypes.c_int], ctypes.c_int),
         "mqvs_set_prefilter": ([ctypes.c_int], ctypes.c_int),
+        "mqvs_index_build": ([P, ctypes.c_char_p, ctypes.c_char_p, P], ctypes.c_int),
+        "mqvs_index_free": ([P], ctypes.c_int),
+        "mqvs_index_info": ([P, P], ctypes.c_int),
+        "mqvs_index_search": ([P, P, I32, I32, ctypes.c_char_p, P, P, P, P, U32, P], ctypes.c_int),
+        "mqvs_index_last_stats": ([P], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)
@@ -135,3 +158,9 @@ def last_search_stats():
     st = SearchStats()
     check(lib.mqvs_last_search_stats(ctypes.byref(st)))
     return {f: getattr(st, f) for f, _ in SearchStats._fields_}
+
+
+def last_index_stats():
+    st = IndexSearchStats()
+    check(lib.mqvs_index_last_stats(ctypes.byref(st)))
+    return {f: getattr(st, f) for f, _ in IndexSearchStats._fields_}

@@ -1,0 +1,629 @@
+// index.hip -- the index path of libmqvs: an MSTG-type vector index over a
+// resident segment (mqvs_index_*; C-ABI in include/mqvs.h).
+//
+// Reference seam (src/VectorIndex/Common/VIWithDataPart.cpp):
+//   createIndex -> Search::createVectorIndex<..., FloatVector>(...)   :416-447
+//   VIWithColumnInPart::search -> VectorIndex::search(queries, k, params,
+//       first_stage_only, filter ∩ delete bitmap)                    :858-957
+//   computeTopDistanceSubset (two-stage search, stage 2)              :838-856
+// The MSTG library itself is absent from the snapshot, so the
+// structure below is this library's own design for HBM and MFMA:
+//
+// Build (all on the GPU except two counting sorts on the host):
+//   k-means over a row sample: assignment = FLAT top-1 search of the sample
+//   rows against a centroid segment (the MFMA pre-filter path of mqvs_search),
+//   deterministic ordered means (k_centroid_mean); cosine centroids are
+//   re-normalised (spherical k-means).  Every row is then assigned to its
+//   nearest centroid, rows are grouped by list (stable: row order within a
+//   list), and the lists are written back to back as a bf16 plane.
+// Search:
+//   coarse   FLAT search of the queries against the centroid segment, k =
+//            nprobe (L2 for L2 parts, raw inner product for IP and cosine)
+//   plan     (query, list) pairs grouped by list into 16-query work items
+//   scan     bf16 MFMA over each probed list (kernels_ivf.hip)
+//   select   num_reorder best approximate values per query
+//   re-rank  exact fp32 distances of those rows (k_rerank_ids: the formula
+//            and cosine query variant of mqvs_search / mqvs_rerank), top-k by
+//            the reference order key
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <cstring>
+#include <map>
+#include <string>
+#include <vector>
+
+#include "mqvs_internal.h"
+
+struct mqvs_index {
+    mqvs_segment *seg = nullptr;   // borrowed: the caller keeps the segment alive
+    int metric = 0;                // search metric (L2, IP or Cosine)
+    int coarse_metric = 0;         // L2 or kMetricIpRaw
+    int64_t nlist = 0;
+    int64_t npos = 0;
+    int64_t max_list = 0;
+    int64_t rows_indexed = 0;
+    int64_t dpad = 0;
+    float alpha = 3.0f;            // default search alpha
+    mqvs_segment *cent = nullptr;  // centroid segment (coarse quantizer)
+    uint16_t *plane = nullptr;     // [npos][dpad] bf16 rows in list order
+    int32_t *perm = nullptr;       // [npos] row of each position, -1 = padding
+    float *pnorm = nullptr;        // [npos] |y|^2
+    int64_t *list_off = nullptr;   // [nlist+1]
+    size_t bytes = 0;
+    double build_ms = 0.0;
+};
+
+namespace mqvs {
+
+static thread_local mqvs_index_search_stats g_istats{};
+
+struct IndexWorkspace {
+    hipEvent_t ev[6] = {};
+    DevBuf queries, qc, qvars, qnorms, qmu, qlam, status, qhi, probes, pdist, filter, exists, lcount, lfill, lstart,
+        lq, items, grp, nitems, qbase, qstart, cand, rows, out_ids, out_dist, stats, ord;
+    void init() {
+        if (ev[0]) return;
+        for (auto &e : ev) MQVS_HIP(hipEventCreate(&e));
+    }
+};
+
+static thread_local std::map<int, IndexWorkspace> *g_iws = nullptr;
+
+static IndexWorkspace &index_workspace(int device) {
+    if (!g_iws) g_iws = new std::map<int, IndexWorkspace>();  // leaked at exit on purpose
+    IndexWorkspace &w = (*g_iws)[device];
+    w.init();
+    return w;
+}
+
+static int64_t rup(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+// ---- Search::Parameters: "k=v,k=v" ----------------------------------------
+static std::map<std::string, std::string> parse_params(const char *s) {
+    std::map<std::string, std::string> out;
+    if (!s) return out;
+    std::string str(s);
+    size_t i = 0;
+    while (i < str.size()) {
+        size_t j = str.find(',', i);
+        if (j == std::string::npos) j = str.size();
+        std::string kv = str.substr(i, j - i);
+        i = j + 1;
+        auto trim = [](std::string x) {
+            const auto b = x.find_first_not_of(" \t'\"");
+            const auto e = x.find_last_not_of(" \t'\"");
+            return b == std::string::npos ? std::string() : x.substr(b, e - b + 1);
+        };
+        kv = trim(kv);
+        if (kv.empty()) continue;
+        const size_t eq = kv.find('=');
+        if (eq == std::string::npos) fail(MQVS_ERR_BAD_ARGUMENTS, "index parameter `" + kv + "` is not key=value");
+        std::string key = trim(kv.substr(0, eq)), val = trim(kv.substr(eq + 1));
+        for (auto &ch : key) ch = (char)std::tolower((unsigned char)ch);
+        out[key] = val;
+    }
+    return out;
+}
+
+static double num_param(const std::map<std::string, std::string> &m, const std::string &key, double dflt,
+                        double lo, double hi) {
+    auto it = m.find(key);
+    if (it == m.end()) return dflt;
+    char *end = nullptr;
+    const double v = std::strtod(it->second.c_str(), &end);
+    if (!end || *end != '\0' || it->second.empty() || !(v >= lo && v <= hi))
+        fail(MQVS_ERR_BAD_ARGUMENTS, "index parameter `" + key + "` = `" + it->second + "` out of range [" +
+                                         std::to_string(lo) + ", " + std::to_string(hi) + "]");
+    return v;
+}
+
+static void check_keys(const std::map<std::string, std::string> &m, const std::vector<std::string> &valid,
+                       const char *what) {
+    for (auto &kv : m) {
+        if (std::find(valid.begin(), valid.end(), kv.first) == valid.end()) {
+            std::string list;
+            for (auto &v : valid) list += (list.empty() ? "" : ",") + v;
+            fail(MQVS_ERR_BAD_ARGUMENTS, std::string("MSTG doesn't support ") + what + " parameter: `" + kv.first +
+                                             "`, valid parameters is [" + list + "].");
+        }
+    }
+}
+
+// nprobe for a search alpha: nprobe(3) = base, doubling per unit of alpha
+static int nprobe_of(const mqvs_index *ix, double alpha) {
+    const double base = std::max<double>(4.0, std::ceil((double)ix->nlist / 256.0));
+    const double np = std::ceil(base * std::pow(2.0, alpha - 3.0));
+    return (int)std::max<double>(1.0, std::min<double>(np, (double)std::min<int64_t>(ix->nlist, kSortCap)));
+}
+
+// ---- build ------------------------------------------------------------------
+
+// nearest centroid of `m` rows (device, row-major d) -> assign[m] (int64, -1 = none)
+static void assign_rows(mqvs_index *ix, mqvs_segment *cseg, const float *rows, int64_t m, int64_t *assign,
+                        float *scratch_dist, hipStream_t s) {
+    constexpr int64_t kBatch = 8192;
+    for (int64_t b = 0; b < m; b += kBatch) {
+        const int nb = (int)std::min(kBatch, m - b);
+        search_internal(cseg, rows + b * ix->seg->d, nb, 1, ix->coarse_metric, nullptr, nullptr, assign + b,
+                        scratch_dist, MQVS_F_DEVICE_PTRS, s);
+    }
+}
+
+// stable counting sort of assign[m] (list ids, -1 dropped): order (indices
+// into the assigned set, ascending within a list) and offsets [L+1]
+static void group_by_list(const std::vector<int64_t> &assign, int64_t L, int64_t pad, std::vector<int32_t> &order,
+                          std::vector<int64_t> &off, const std::vector<uint8_t> *keep) {
+    std::vector<int64_t> cnt(L + 1, 0);
+    for (size_t i = 0; i < assign.size(); ++i) {
+        const int64_t a = assign[i];
+        if (a >= 0 && a < L && (!keep || (*keep)[i])) ++cnt[a];
+    }
+    off.assign(L + 1, 0);
+    for (int64_t l = 0; l < L; ++l) off[l + 1] = off[l] + rup(cnt[l], pad);
+    order.assign(off[L], -1);
+    std::vector<int64_t> cur(off.begin(), off.end() - 1);
+    for (size_t i = 0; i < assign.size(); ++i) {
+        const int64_t a = assign[i];
+        if (a >= 0 && a < L && (!keep || (*keep)[i])) order[cur[a]++] = (int32_t)i;
+    }
+}
+
+static void free_index(mqvs_index *ix) {
+    if (!ix) return;
+    int cur = -1;
+    (void)hipGetDevice(&cur);
+    if (ix->seg) (void)hipSetDevice(ix->seg->device);
+    if (ix->cent) segment_release(ix->cent);
+    for (void *q : {(void *)ix->plane, (void *)ix->perm, (void *)ix->pnorm, (void *)ix->list_off})
+        if (q) (void)hipFree(q);
+    if (cur >= 0) (void)hipSetDevice(cur);
+    delete ix;
+}
+
+template <typename T>
+static T *dalloc(mqvs_index *ix, size_t count) {
+    T *p = nullptr;
+    const size_t bytes = sizeof(T) * std::max<size_t>(count, 1);
+    if (hipMalloc((void **)&p, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        fail(MQVS_ERR_MEMORY_LIMIT, "HBM allocation of " + std::to_string(bytes) + " bytes failed");
+    }
+    ix->bytes += bytes;
+    return p;
+}
+
+struct TmpBuf {
+    void *p = nullptr;
+    explicit TmpBuf(size_t bytes) {
+        if (hipMalloc(&p, std::max<size_t>(bytes, 16)) != hipSuccess) {
+            (void)hipGetLastError();
+            fail(MQVS_ERR_MEMORY_LIMIT, "HBM allocation of " + std::to_string(bytes) + " bytes failed");
+        }
+    }
+    ~TmpBuf() {
+        if (p) (void)hipFree(p);
+    }
+    template <typename T>
+    T *as() const {
+        return (T *)p;
+    }
+};
+
+static mqvs_index *build_impl(mqvs_segment *seg, const char *index_type, const char *params) {
+    if (!seg) fail(MQVS_ERR_BAD_ARGUMENTS, "null segment");
+    std::string type = index_type ? index_type : "MSTG";
+    for (auto &ch : type) ch = (char)std::toupper((unsigned char)ch);
+    if (type != "MSTG" && type != "IVFFLAT")
+        fail(MQVS_ERR_NOT_IMPLEMENTED, "index type `" + type + "` is not implemented (MSTG, IVFFLAT)");
+    const auto pm = parse_params(params);
+    check_keys(pm, {"alpha", "metric_type", "nlist", "kmeans_iters", "sample"}, "index");
+    int metric = seg->metric;
+    if (pm.count("metric_type")) {
+        std::string mt = pm.at("metric_type");
+        for (auto &ch : mt) ch = (char)std::toupper((unsigned char)ch);
+        if (mt == "L2")
+            metric = MQVS_METRIC_L2;
+        else if (mt == "IP")
+            metric = MQVS_METRIC_IP;
+        else if (mt == "COSINE")
+            metric = MQVS_METRIC_COSINE;
+        else
+            fail(MQVS_ERR_NOT_IMPLEMENTED, "metric_type `" + pm.at("metric_type") + "` is not supported for Float32 vectors");
+        if ((metric == MQVS_METRIC_COSINE) != (seg->metric == MQVS_METRIC_COSINE))
+            fail(MQVS_ERR_LOGICAL, "segment was prepared for a different metric (cosine segments are normalised in HBM)");
+    }
+    const int64_t n = seg->n;
+    const int d = seg->d;
+    const int64_t dflt_nlist = std::max<int64_t>(1, std::min<int64_t>(65536, (n + 500) / 1000));
+    const int64_t L = (int64_t)num_param(pm, "nlist", (double)dflt_nlist, 1, 1 << 20);
+    if (n > 0 && L > n) fail(MQVS_ERR_BAD_ARGUMENTS, "nlist must not exceed the number of rows");
+    const int iters = (int)num_param(pm, "kmeans_iters", 8, 0, 1000);
+    const int64_t S = std::max<int64_t>(std::min<int64_t>(n, (int64_t)num_param(pm, "sample",
+                                                                                 (double)std::min<int64_t>(n, 64 * L),
+                                                                                 1, 1e12)),
+                                        std::min<int64_t>(n, L));
+
+    DeviceGuard guard(seg->device);
+    hipStream_t s = thread_stream(seg->device);
+    hipEvent_t e0, e1;
+    MQVS_HIP(hipEventCreate(&e0));
+    MQVS_HIP(hipEventCreate(&e1));
+    MQVS_HIP(hipEventRecord(e0, s));
+
+    auto *ix = new mqvs_index();
+    try {
+        ix->seg = seg;
+        ix->metric = metric;
+        ix->coarse_metric = metric == MQVS_METRIC_L2 ? MQVS_METRIC_L2 : kMetricIpRaw;
+        ix->nlist = std::max<int64_t>(L, 1);
+        ix->alpha = (float)num_param(pm, "alpha", 3.0, 1.0, 4.0);
+        ix->dpad = rup(d, kBfK);
+        const int cseg_metric = metric == MQVS_METRIC_L2 ? MQVS_METRIC_L2 : MQVS_METRIC_IP;
+
+        // rows that can be indexed: non-empty arrays
+        std::vector<uint8_t> keep;
+        if (seg->nonempty_bits && n > 0) {
+            std::vector<uint8_t> bits((n + 7) / 8);
+            MQVS_HIP(hipMemcpyAsync(bits.data(), seg->nonempty_bits, bits.size(), hipMemcpyDeviceToHost, s));
+            MQVS_HIP(hipStreamSynchronize(s));
+            keep.resize(n);
+            for (int64_t i = 0; i < n; ++i) keep[i] = (bits[i >> 3] >> (i & 7)) & 1;
+        }
+
+        // ---- k-means on a strided sample of the rows
+        std::vector<int64_t> sidx;
+        for (int64_t i = 0; i < S; ++i) {
+            const int64_t r = (int64_t)((__int128)i * n / S);
+            if (keep.empty() || keep[r]) sidx.push_back(r);
+        }
+        const int64_t Sm = (int64_t)sidx.size();
+        const int64_t Lc = ix->nlist;
+        TmpBuf dsidx(sizeof(int64_t) * std::max<int64_t>(Sm, 1));
+        TmpBuf samp(sizeof(float) * std::max<int64_t>(Sm, 1) * d);
+        TmpBuf cent(sizeof(float) * Lc * d);
+        MQVS_HIP(hipMemsetAsync(cent.p, 0, sizeof(float) * Lc * d, s));
+        if (Sm > 0) {
+            MQVS_HIP(hipMemcpyAsync(dsidx.p, sidx.data(), sizeof(int64_t) * Sm, hipMemcpyHostToDevice, s));
+            launch_gather_rows(seg->rows, d, d, dsidx.as<int64_t>(), Sm, samp.as<float>(), s);
+            // initial centroids: evenly spaced sample rows
+            std::vector<int64_t> init;
+            for (int64_t c = 0; c < std::min(Lc, Sm); ++c) init.push_back((int64_t)((__int128)c * Sm / std::min(Lc, Sm)));
+            TmpBuf dinit(sizeof(int64_t) * init.size());
+            MQVS_HIP(hipMemcpyAsync(dinit.p, init.data(), sizeof(int64_t) * init.size(), hipMemcpyHostToDevice, s));
+            launch_gather_rows(samp.as<float>(), d, d, dinit.as<int64_t>(), (int64_t)init.size(), cent.as<float>(), s);
+            MQVS_HIP(hipGetLastError());
+            MQVS_HIP(hipStreamSynchronize(s));
+        }
+        TmpBuf assign(sizeof(int64_t) * std::max<int64_t>(std::max(Sm, n), 1));
+        TmpBuf adist(sizeof(float) * 8192);
+        std::vector<int64_t> ha;
+        std::vector<int32_t> order;
+        std::vector<int64_t> off;
+        for (int it = 0; it < iters && Sm > 0 && Lc > 1; ++it) {
+            mqvs_segment *cs = segment_from_device(cent.as<float>(), Lc, d, cseg_metric, s);
+            try {
+                assign_rows(ix, cs, samp.as<float>(), Sm, assign.as<int64_t>(), adist.as<float>(), s);
+            } catch (...) {
+                segment_release(cs);
+                throw;
+            }
+            segment_release(cs);
+            ha.resize(Sm);
+            MQVS_HIP(hipMemcpyAsync(ha.data(), assign.p, sizeof(int64_t) * Sm, hipMemcpyDeviceToHost, s));
+            MQVS_HIP(hipStreamSynchronize(s));
+            group_by_list(ha, Lc, 1, order, off, nullptr);
+            TmpBuf dord(sizeof(int32_t) * std::max<size_t>(order.size(), 1));
+            TmpBuf doff(sizeof(int64_t) * off.size());
+            if (!order.empty())
+                MQVS_HIP(hipMemcpyAsync(dord.p, order.data(), sizeof(int32_t) * order.size(), hipMemcpyHostToDevice, s));
+            MQVS_HIP(hipMemcpyAsync(doff.p, off.data(), sizeof(int64_t) * off.size(), hipMemcpyHostToDevice, s));
+            launch_centroid_mean(samp.as<float>(), d, dord.as<int32_t>(), doff.as<int64_t>(), (int)Lc, cent.as<float>(), s);
+            if (metric == MQVS_METRIC_COSINE) launch_normalize_rows(cent.as<float>(), Lc, d, s);
+            MQVS_HIP(hipGetLastError());
+            MQVS_HIP(hipStreamSynchronize(s));
+        }
+        ix->cent = segment_from_device(cent.as<float>(), Lc, d, cseg_metric, s);
+
+        // ---- every row to its nearest centroid; lists in row order
+        ha.assign(n, 0);
+        if (Lc > 1 && n > 0) {
+            assign_rows(ix, ix->cent, seg->rows, n, assign.as<int64_t>(), adist.as<float>(), s);
+            MQVS_HIP(hipMemcpyAsync(ha.data(), assign.p, sizeof(int64_t) * n, hipMemcpyDeviceToHost, s));
+            MQVS_HIP(hipStreamSynchronize(s));
+        }
+        group_by_list(ha, Lc, kIvfPad, order, off, keep.empty() ? nullptr : &keep);
+        ix->npos = off[Lc];
+        ix->rows_indexed = 0;
+        for (int64_t l = 0; l < Lc; ++l) {
+            int64_t len = 0;
+            for (int64_t pos = off[l]; pos < off[l + 1]; ++pos) len += order[pos] >= 0;
+            ix->rows_indexed += len;
+            ix->max_list = std::max(ix->max_list, off[l + 1] - off[l]);
+        }
+        ix->perm = dalloc<int32_t>(ix, ix->npos);
+        ix->list_off = dalloc<int64_t>(ix, Lc + 1);
+        ix->plane = dalloc<uint16_t>(ix, (size_t)ix->npos * ix->dpad);
+        ix->pnorm = dalloc<float>(ix, ix->npos);
+        if (ix->npos > 0)
+            MQVS_HIP(hipMemcpyAsync(ix->perm, order.data(), sizeof(int32_t) * ix->npos, hipMemcpyHostToDevice, s));
+        MQVS_HIP(hipMemcpyAsync(ix->list_off, off.data(), sizeof(int64_t) * (Lc + 1), hipMemcpyHostToDevice, s));
+        launch_ivf_pack(seg->rows, seg->norms, d, ix->perm, ix->npos, ix->dpad, ix->plane, ix->pnorm, s);
+        MQVS_HIP(hipGetLastError());
+        MQVS_HIP(hipEventRecord(e1, s));
+        MQVS_HIP(hipStreamSynchronize(s));
+        float ms = 0.f;
+        MQVS_HIP(hipEventElapsedTime(&ms, e0, e1));
+        ix->build_ms = ms;
+        ix->bytes += ix->cent->bytes;
+    } catch (...) {
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        free_index(ix);
+        throw;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return ix;
+}
+
+// ---- search -----------------------------------------------------------------
+
+static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int k, const char *params,
+                              const uint8_t *filter, const uint8_t *exists, int64_t *out_ids, float *out_dist,
+                              uint32_t flags, hipStream_t user_stream) {
+    if (!ix) fail(MQVS_ERR_BAD_ARGUMENTS, "null index");
+    if (nq < 0 || k < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "nq and k must be non-negative");
+    if (nq > 0 && k > 0 && (!queries || !out_ids || !out_dist))
+        fail(MQVS_ERR_BAD_ARGUMENTS, "null query or output pointer");
+    if (k > kSortCap) fail(MQVS_ERR_BAD_ARGUMENTS, "k above " + std::to_string(kSortCap) + " not supported");
+    const auto pm = parse_params(params);
+    check_keys(pm, {"alpha", "nprobe", "num_reorder"}, "search");
+    const bool first_stage = flags & MQVS_F_FIRST_STAGE;
+    const double alpha = num_param(pm, "alpha", ix->alpha, 1.0, 4.0);
+    const int nprobe = pm.count("nprobe")
+                           ? (int)num_param(pm, "nprobe", 1, 1, (double)std::min<int64_t>(ix->nlist, kSortCap))
+                           : nprobe_of(ix, alpha);
+    const int R = first_stage ? k
+                              : (int)num_param(pm, "num_reorder", (double)std::min(kSortCap, std::max(2 * k, 64)),
+                                               (double)std::max(k, 1), (double)kSortCap);
+    mqvs_index_search_stats st{};
+    st.nq = nq;
+    st.k = k;
+    st.nprobe = nprobe;
+    st.num_reorder = R;
+    g_istats = st;
+    if (nq == 0 || k == 0) return;
+
+    mqvs_segment *seg = ix->seg;
+    DeviceGuard guard(seg->device);
+    IndexWorkspace &ws = index_workspace(seg->device);
+    hipStream_t s = user_stream ? user_stream : thread_stream(seg->device);
+    const bool dev = flags & MQVS_F_DEVICE_PTRS;
+    const int d = seg->d;
+    const bool cos = ix->metric == MQVS_METRIC_COSINE;
+    MQVS_HIP(hipEventRecord(ws.ev[0], s));
+
+    const float *dq = queries;
+    const uint8_t *dfilter = filter, *dexists = exists;
+    const int64_t bm = (seg->n + 7) / 8;
+    if (!dev) {
+        float *q = (float *)ws.queries.get(sizeof(float) * (size_t)nq * d);
+        MQVS_HIP(hipMemcpyAsync(q, queries, sizeof(float) * (size_t)nq * d, hipMemcpyHostToDevice, s));
+        dq = q;
+        if (filter) {
+            auto *f = (uint8_t *)ws.filter.get(bm);
+            MQVS_HIP(hipMemcpyAsync(f, filter, bm, hipMemcpyHostToDevice, s));
+            dfilter = f;
+        }
+        if (exists) {
+            auto *f = (uint8_t *)ws.exists.get(bm);
+            MQVS_HIP(hipMemcpyAsync(f, exists, bm, hipMemcpyHostToDevice, s));
+            dexists = f;
+        }
+    }
+    int64_t *dids = out_ids;
+    float *ddist = out_dist;
+    if (!dev) {
+        dids = (int64_t *)ws.out_ids.get(sizeof(int64_t) * (size_t)nq * k);
+        ddist = (float *)ws.out_dist.get(sizeof(float) * (size_t)nq * k);
+    }
+
+    // ---- query prep: cosine re-normalisation variants (the re-rank uses the
+    // row's chunk variant, as mqvs_search does), |q|^2
+    const int maxv = cos ? kMaxVariants : 1;
+    const int64_t qstride = rup(d, 32);
+    float *qvars = (float *)ws.qvars.get(sizeof(float) * (size_t)nq * maxv * qstride);
+    MQVS_HIP(hipMemsetAsync(qvars, 0, sizeof(float) * (size_t)nq * maxv * qstride, s));
+    float *qnorms = (float *)ws.qnorms.get(sizeof(float) * nq);
+    int *qmu = (int *)ws.qmu.get(sizeof(int) * nq);
+    int *qlam = (int *)ws.qlam.get(sizeof(int) * nq);
+    int *status = (int *)ws.status.get(sizeof(int) * 4);
+    MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
+    launch_query_prep(dq, nq, d, cos ? MQVS_METRIC_COSINE : MQVS_METRIC_L2, ix->metric == MQVS_METRIC_L2, qvars,
+                      qnorms, qmu, qlam, status, s);
+    MQVS_HIP(hipGetLastError());
+    // first variant of every query, contiguous (the coarse search's queries)
+    const float *qc = dq;
+    if (cos) {
+        float *b = (float *)ws.qc.get(sizeof(float) * (size_t)nq * d);
+        launch_gather_rows(qvars, (int64_t)maxv * qstride, d, nullptr, nq, b, s);
+        MQVS_HIP(hipGetLastError());
+        qc = b;
+    }
+    uint16_t *qhi = (uint16_t *)ws.qhi.get(sizeof(uint16_t) * (size_t)nq * ix->dpad);
+    launch_to_bf16(qvars, nq, d, (int64_t)maxv * qstride, qhi, nullptr, ix->dpad, s);
+    MQVS_HIP(hipGetLastError());
+
+    // ---- coarse: nprobe nearest lists per query
+    int64_t *probes = (int64_t *)ws.probes.get(sizeof(int64_t) * (size_t)nq * nprobe);
+    float *pdist = (float *)ws.pdist.get(sizeof(float) * (size_t)nq * nprobe);
+    search_internal(ix->cent, qc, nq, nprobe, ix->coarse_metric, nullptr, nullptr, probes, pdist, MQVS_F_DEVICE_PTRS,
+                    s);
+    MQVS_HIP(hipEventRecord(ws.ev[1], s));
+
+    // ---- plan
+    const int64_t E = (int64_t)nq * nprobe;
+    IvfParams p{};
+    p.plane = ix->plane;
+    p.perm = ix->perm;
+    p.pnorm = ix->pnorm;
+    p.list_off = ix->list_off;
+    p.nlist = (int)ix->nlist;
+    p.dpad = ix->dpad;
+    p.nq = nq;
+    p.nprobe = nprobe;
+    p.probes = probes;
+    p.q_hi = qhi;
+    p.qnorm = qnorms;
+    p.filter = dfilter;
+    p.exists = dexists;
+    p.lcount = (int *)ws.lcount.get(sizeof(int) * ix->nlist);
+    p.lfill = (int *)ws.lfill.get(sizeof(int) * ix->nlist);
+    p.lstart = (int64_t *)ws.lstart.get(sizeof(int64_t) * ix->nlist);
+    p.lq = (int *)ws.lq.get(sizeof(int) * E);
+    p.item_list = (int *)ws.items.get(sizeof(int) * E);
+    p.item_grp = (int *)ws.grp.get(sizeof(int) * E);
+    p.nitems = (int *)ws.nitems.get(sizeof(int) * 4);
+    p.qbase = (int64_t *)ws.qbase.get(sizeof(int64_t) * E);
+    p.qstart = (int64_t *)ws.qstart.get(sizeof(int64_t) * (nq + 1));
+    // a query's region is at most min(nprobe * longest list, every position)
+    const int64_t cap = (int64_t)nq * std::min<int64_t>((int64_t)nprobe * ix->max_list, ix->npos);
+    p.cand = (Cand *)ws.cand.get(sizeof(Cand) * (size_t)std::max<int64_t>(cap, 1));
+    int64_t *dstats = (int64_t *)ws.stats.get(sizeof(int64_t) * 8);
+    p.stats = dstats;
+    launch_ivf_plan(p, s);
+    MQVS_HIP(hipGetLastError());
+    MQVS_HIP(hipEventRecord(ws.ev[2], s));
+
+    // ---- scan
+    launch_ivf_scan(p, ix->metric, 2048, s);
+    MQVS_HIP(hipGetLastError());
+    MQVS_HIP(hipEventRecord(ws.ev[3], s));
+
+    // ---- select
+    if (first_stage) {
+        launch_ivf_select(p.cand, p.qstart, nq, R, ix->metric, dids, seg->row_offset, ddist, s);
+        MQVS_HIP(hipGetLastError());
+        MQVS_HIP(hipEventRecord(ws.ev[4], s));
+        MQVS_HIP(hipEventRecord(ws.ev[5], s));
+    } else {
+        int64_t *crow = (int64_t *)ws.rows.get(sizeof(int64_t) * (size_t)nq * R);
+        launch_ivf_select(p.cand, p.qstart, nq, R, ix->metric, crow, 0, nullptr, s);
+        MQVS_HIP(hipGetLastError());
+        MQVS_HIP(hipEventRecord(ws.ev[4], s));
+        // ---- exact re-rank
+        ScanParams rp{};
+        rp.rows = seg->rows;
+        rp.row_norms = seg->norms;
+        rp.n = seg->n;
+        rp.d = d;
+        rp.nq = nq;
+        rp.qvars = qvars;
+        rp.qnorms = qnorms;
+        rp.qmu = qmu;
+        rp.qlam = qlam;
+        rp.maxv = maxv;
+        rp.chunk_rows = seg->granule;
+        rp.chunk_ord = seg->chunk_ord;
+        if (cos && dfilter) {
+            // chunk ordinals as mqvs_search computes them under a PREWHERE
+            // filter (chunks without a selected row are never searched), so
+            // the re-rank picks the same cosine query variant per row
+            const int64_t nch = (seg->n + seg->granule - 1) / seg->granule;
+            int *o = (int *)ws.ord.get(sizeof(int) * std::max<int64_t>(nch, 1));
+            launch_chunk_ordinals(dfilter, seg->nonempty_bits, dexists, seg->n, seg->granule, 1, o, s);
+            MQVS_HIP(hipGetLastError());
+            rp.chunk_ord = o;
+        }
+        rp.ord_base = (int)(seg->row_offset / seg->granule);
+        rp.exists = dexists;
+        rp.filter = nullptr;  // the scan applied the filter; candidates pass it
+        rp.nonempty = seg->nonempty_bits;
+        launch_rerank_ids(rp, ix->metric, crow, R, k, seg->row_offset, dids, ddist, s);
+        MQVS_HIP(hipGetLastError());
+        MQVS_HIP(hipEventRecord(ws.ev[5], s));
+    }
+
+    const bool async = dev && (flags & MQVS_F_ASYNC);
+    if (async) return;
+    int64_t hs[4] = {0, 0, 0, 0};
+    MQVS_HIP(hipMemcpyAsync(hs, dstats, sizeof(hs), hipMemcpyDeviceToHost, s));
+    int hstatus = 0;
+    MQVS_HIP(hipMemcpyAsync(&hstatus, status, sizeof(int), hipMemcpyDeviceToHost, s));
+    MQVS_HIP(hipStreamSynchronize(s));
+    if (hstatus && !first_stage &&
+        (int64_t)(seg->row_offset / seg->granule) + (seg->n + seg->granule - 1) / seg->granule > kMaxVariants)
+        fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not repeat within " + std::to_string(kMaxVariants) +
+                                   " steps on a part of more chunks");
+    if (!dev) {
+        MQVS_HIP(hipMemcpyAsync(out_ids, dids, sizeof(int64_t) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
+        MQVS_HIP(hipMemcpyAsync(out_dist, ddist, sizeof(float) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
+        MQVS_HIP(hipStreamSynchronize(s));
+    }
+    st.values = hs[0];
+    st.items = hs[1];
+    st.plane_bytes = hs[2];
+    st.pairs = hs[3];
+    float t[5] = {0, 0, 0, 0, 0}, tot = 0;
+    for (int i = 0; i < 5; ++i) MQVS_HIP(hipEventElapsedTime(&t[i], ws.ev[i], ws.ev[i + 1]));
+    MQVS_HIP(hipEventElapsedTime(&tot, ws.ev[0], ws.ev[5]));
+    st.coarse_ms = t[0];
+    st.plan_ms = t[1];
+    st.scan_ms = t[2];
+    st.select_ms = t[3];
+    st.rerank_ms = t[4];
+    st.total_ms = tot;
+    g_istats = st;
+}
+
+}  // namespace mqvs
+
+using namespace mqvs;
+
+extern "C" {
+
+int mqvs_index_build(mqvs_segment_t seg, const char *index_type, const char *params, mqvs_index_t *out) {
+    return guarded([&] {
+        if (!out) fail(MQVS_ERR_BAD_ARGUMENTS, "null output handle");
+        *out = nullptr;
+        *out = build_impl(seg, index_type, params);
+    });
+}
+
+int mqvs_index_free(mqvs_index_t idx) {
+    return guarded([&] { free_index(idx); });
+}
+
+int mqvs_index_info(mqvs_index_t idx, mqvs_index_info_t *out) {
+    return guarded([&] {
+        if (!idx || !out) fail(MQVS_ERR_BAD_ARGUMENTS, "null argument");
+        out->nlist = idx->nlist;
+        out->npos = idx->npos;
+        out->max_list = idx->max_list;
+        out->rows_indexed = idx->rows_indexed;
+        out->metric = idx->metric;
+        out->dim = idx->seg->d;
+        out->hbm_bytes = idx->bytes;
+        out->build_ms = idx->build_ms;
+    });
+}
+
+int mqvs_index_search(mqvs_index_t idx, const float *queries, int32_t nq, int32_t k, const char *params,
+                      const uint8_t *filter, const uint8_t *row_exists, int64_t *out_ids, float *out_dist,
+                      uint32_t flags, mqvs_stream_t stream) {
+    return guarded([&] {
+        search_index_impl(idx, queries, nq, k, params, filter, row_exists, out_ids, out_dist, flags,
+                          (hipStream_t)stream);
+    });
+}
+
+int mqvs_index_last_stats(mqvs_index_search_stats *out) {
+    if (!out) return MQVS_ERR_BAD_ARGUMENTS;
+    *out = g_istats;
+    return MQVS_OK;
+}
+
+}  // extern "C"

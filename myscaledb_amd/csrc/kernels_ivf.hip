@@ -1,0 +1,409 @@
+// kernels_ivf.hip -- kernels of the index path (mqvs_index_*, index.hip):
+// the MSTG-type index (the reference's Search::VectorIndex behind
+// VIWithColumnInPart::search, VIWithDataPart.cpp:858-957) laid out for HBM.
+//
+// Layout.  The part's rows are partitioned into `nlist` lists by a k-means
+// coarse quantizer.  The lists are stored back to back as one bf16 plane in
+// list order ([npos][dpad], each list padded to a multiple of 16 positions),
+// with perm[pos] = segment row (-1 = padding) and pnorm[pos] = |y|^2.
+//
+// Search (one batch of nq queries, each probing nprobe lists):
+//   k_ivf_plan    one workgroup: group the nq*nprobe (query, probe) pairs by
+//                 list, cut each list's queries into 16-query work items, and
+//                 give every pair its region of the candidate buffer
+//   k_ivf_scan    per work item: stream the list's bf16 rows from HBM straight
+//                 into MFMA A fragments (v_mfma_f32_16x16x32_bf16), the 16
+//                 queries as B from LDS; approximate values to the regions
+//   k_ivf_select  per query: radix-select the num_reorder best approximate
+//                 values, ordered compaction, bitonic sort in LDS
+// then the exact fp32 re-rank (k_rerank_ids, kernels_rerank.hip).
+#include "mqvs_internal.h"
+#include "select_common.h"
+
+namespace mqvs {
+
+typedef __bf16 ivf_bf16x8 __attribute__((ext_vector_type(8)));
+typedef float ivf_f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int kPlanThreads = 1024;
+
+// Exclusive scan of `n` int64 values produced by val(i) into out(i, prefix);
+// returns the total.  One workgroup of kPlanThreads; each thread owns a
+// contiguous run, run sums are scanned in LDS.
+template <class Val, class Out>
+__device__ int64_t block_exclusive_scan(int64_t n, Val val, Out out, int64_t *sh) {
+    const int t = threadIdx.x;
+    const int64_t per = (n + kPlanThreads - 1) / kPlanThreads;
+    const int64_t b = t * per, e = min(n, b + per);
+    int64_t s = 0;
+    for (int64_t i = b; i < e; ++i) s += val(i);
+    sh[t] = s;
+    __syncthreads();
+    if (t == 0) {
+        int64_t acc = 0;
+        for (int i = 0; i < kPlanThreads; ++i) {
+            const int64_t v = sh[i];
+            sh[i] = acc;
+            acc += v;
+        }
+        sh[kPlanThreads] = acc;
+    }
+    __syncthreads();
+    int64_t run = sh[t];
+    for (int64_t i = b; i < e; ++i) {
+        const int64_t v = val(i);
+        out(i, run);
+        run += v;
+    }
+    const int64_t total = sh[kPlanThreads];
+    __syncthreads();
+    return total;
+}
+
+__global__ __launch_bounds__(kPlanThreads) void k_ivf_plan(IvfParams p) {
+    __shared__ int64_t sh[kPlanThreads + 1];
+    const int t = threadIdx.x;
+    const int L = p.nlist;
+    const int64_t E = (int64_t)p.nq * p.nprobe;
+    for (int i = t; i < L; i += kPlanThreads) {
+        p.lcount[i] = 0;
+        p.lfill[i] = 0;
+    }
+    __syncthreads();
+    for (int64_t e = t; e < E; e += kPlanThreads) {
+        const int64_t l = p.probes[e];
+        if (l >= 0 && l < L) atomicAdd(&p.lcount[l], 1);
+    }
+    __syncthreads();
+    // list -> start of its pairs in lq
+    block_exclusive_scan(
+        L, [&](int64_t i) { return (int64_t)p.lcount[i]; },
+        [&](int64_t i, int64_t v) { p.lstart[i] = v; }, sh);
+    // list -> its work items (16 queries each)
+    const int64_t items = block_exclusive_scan(
+        L, [&](int64_t i) { return (int64_t)((p.lcount[i] + kIvfQG - 1) / kIvfQG); },
+        [&](int64_t i, int64_t v) {
+            const int g = (p.lcount[i] + kIvfQG - 1) / kIvfQG;
+            for (int j = 0; j < g; ++j) {
+                p.item_list[v + j] = (int)i;
+                p.item_grp[v + j] = j;
+            }
+        },
+        sh);
+    // pairs grouped by list (order inside a list is free: every pair owns
+    // its output region, so results do not depend on it)
+    for (int64_t e = t; e < E; e += kPlanThreads) {
+        const int64_t l = p.probes[e];
+        if (l >= 0 && l < L) {
+            const int slot = atomicAdd(&p.lfill[l], 1);
+            p.lq[p.lstart[l] + slot] = (int)e;
+        }
+    }
+    // per query: regions of its probes, back to back in probe order
+    for (int q = t; q < p.nq; q += kPlanThreads) {
+        int64_t tot = 0;
+        for (int r = 0; r < p.nprobe; ++r) {
+            const int64_t e = (int64_t)q * p.nprobe + r;
+            const int64_t l = p.probes[e];
+            p.qbase[e] = tot;
+            if (l >= 0 && l < L) tot += p.list_off[l + 1] - p.list_off[l];
+        }
+        p.qstart[q] = tot;  // region length for now
+    }
+    __syncthreads();
+    const int64_t total = block_exclusive_scan(
+        p.nq, [&](int64_t i) { return p.qstart[i]; }, [&](int64_t i, int64_t v) { p.qstart[i] = v; }, sh);
+    for (int64_t e = t; e < E; e += kPlanThreads) p.qbase[e] += p.qstart[e / p.nprobe];
+    // bf16 bytes the scan streams (every work item reads its list once)
+    int64_t bytes = 0;
+    for (int i = t; i < L; i += kPlanThreads)
+        bytes += (int64_t)((p.lcount[i] + kIvfQG - 1) / kIvfQG) * (p.list_off[i + 1] - p.list_off[i]);
+    sh[t] = bytes;
+    __syncthreads();
+    if (t == 0) {
+        int64_t b = 0;
+        for (int i = 0; i < kPlanThreads; ++i) b += sh[i];
+        p.qstart[p.nq] = total;
+        *p.nitems = (int)items;
+        p.stats[0] = total;                   // approximate values written
+        p.stats[1] = items;                   // work items
+        p.stats[2] = b * p.dpad * 2;          // plane bytes streamed
+        p.stats[3] = E;                       // (query, probe) pairs
+    }
+}
+
+template <int METRIC>
+__global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char qtile[];  // 16 x (2 dpad + 16) B
+    __shared__ int s_ent[kIvfQG];
+    __shared__ int64_t s_base[kIvfQG];
+    __shared__ float s_qn[kIvfQG];
+    const int64_t qstr = 2 * p.dpad + 16;  // +16 B: the 16 query rows hit distinct bank groups
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+    const int l16 = lane & 15, c = lane >> 4;
+    const int nitems = *p.nitems;
+    const int cpr = (int)(p.dpad / 8);  // 16-B chunks per query row
+    for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
+        const int l = p.item_list[it], g = p.item_grp[it];
+        const int cnt = min(kIvfQG, p.lcount[l] - g * kIvfQG);
+        __syncthreads();  // the previous item's readers are done with qtile
+        if (threadIdx.x < kIvfQG) {
+            const int j = threadIdx.x;
+            const int e = j < cnt ? p.lq[p.lstart[l] + (int64_t)g * kIvfQG + j] : -1;
+            s_ent[j] = e;
+            s_base[j] = e >= 0 ? p.qbase[e] : 0;
+            s_qn[j] = (e >= 0 && METRIC == MQVS_METRIC_L2) ? p.qnorm[e / p.nprobe] : 0.f;
+        }
+        __syncthreads();
+        for (int i = threadIdx.x; i < kIvfQG * cpr; i += 256) {
+            const int j = i / cpr, cc = i - j * cpr;
+            const int e = s_ent[j];
+            uint4 v = make_uint4(0, 0, 0, 0);
+            if (e >= 0) v = reinterpret_cast<const uint4 *>(p.q_hi + (int64_t)(e / p.nprobe) * p.dpad)[cc];
+            *reinterpret_cast<uint4 *>(qtile + j * qstr + cc * 16) = v;
+        }
+        __syncthreads();
+        const int64_t pos0 = p.list_off[l];
+        const int nb = (int)((p.list_off[l + 1] - pos0) / 16);
+        const unsigned char *qp = qtile + l16 * qstr + c * 32;
+        const int e = s_ent[l16];
+        for (int b = w; b < nb; b += 4) {
+            // lane (l16, c) reads 32 contiguous bytes of row l16 per 64-column
+            // window; both MFMA k-steps of the window use the same column
+            // assignment for A (rows) and B (queries)
+            const uint16_t *rp = p.plane + (pos0 + (int64_t)b * 16 + l16) * p.dpad + c * 16;
+            ivf_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+            ivf_bf16x8 a0 = *reinterpret_cast<const ivf_bf16x8 *>(rp);
+            ivf_bf16x8 a1 = *reinterpret_cast<const ivf_bf16x8 *>(rp + 8);
+            for (int64_t kw = 0; kw < p.dpad; kw += 64) {
+                ivf_bf16x8 n0 = a0, n1 = a1;
+                if (kw + 64 < p.dpad) {
+                    n0 = *reinterpret_cast<const ivf_bf16x8 *>(rp + kw + 64);
+                    n1 = *reinterpret_cast<const ivf_bf16x8 *>(rp + kw + 72);
+                }
+                const ivf_bf16x8 b0 = *reinterpret_cast<const ivf_bf16x8 *>(qp + 2 * kw);
+                const ivf_bf16x8 b1 = *reinterpret_cast<const ivf_bf16x8 *>(qp + 2 * kw + 16);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc, 0, 0, 0);
+                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc, 0, 0, 0);
+                a0 = n0;
+                a1 = n1;
+            }
+            // C: lane (l16, c) holds rows 4c..4c+3 of the block for query slot l16
+            if (e >= 0) {
+                const int64_t lp = (int64_t)b * 16 + 4 * c;
+                Cand out[4];
+#pragma unroll
+                for (int r = 0; r < 4; ++r) {
+                    const int64_t gpos = pos0 + lp + r;
+                    const int32_t row = p.perm[gpos];
+                    bool valid = row >= 0;
+                    if (valid && p.filter) valid = bit_test(p.filter, row);
+                    if (valid && p.exists) valid = bit_test(p.exists, row);
+                    float raw = acc[r];
+                    if (METRIC == MQVS_METRIC_L2) raw = (s_qn[l16] + p.pnorm[gpos]) - 2.0f * raw;
+                    out[r].raw = valid ? raw : __builtin_nanf("");
+                    out[r].row = valid ? (uint32_t)row : 0xFFFFFFFFu;
+                }
+                uint4 *dst = reinterpret_cast<uint4 *>(p.cand + s_base[l16] + lp);
+                dst[0] = *reinterpret_cast<const uint4 *>(&out[0]);
+                dst[1] = *reinterpret_cast<const uint4 *>(&out[2]);
+            }
+        }
+    }
+}
+
+// Per query: the R best approximate values (ties at the R-th key by position,
+// so the selection is deterministic), sorted by (key, row).  Writes the rows
+// (for the exact re-rank) and, for first-stage-only searches, ids + the
+// approximate distance.
+template <int METRIC>
+__global__ __launch_bounds__(SEL_THREADS) void k_ivf_select(const Cand *cand, const int64_t *qstart, int R,
+                                                           int64_t *out_rows, int64_t id_offset,
+                                                           float *out_approx) {
+    extern __shared__ __attribute__((aligned(16))) uint4 recs[];  // pow2 >= R records
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t sh[4];
+    __shared__ int s_wave[SEL_THREADS / 64];
+    __shared__ int s_m;
+    const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const Cand *c = cand + qstart[q];
+    const int64_t T = qstart[q + 1] - qstart[q];
+    auto keyof = [&](int64_t i) {
+        const Cand e = c[i];
+        return e.row == 0xFFFFFFFFu ? 0xFFFFFFFFu : okey<METRIC>(e.raw);
+    };
+    const uint32_t th = block_radix_select(keyof, T, R, hist, sh);
+    if (t == 0) s_m = 0;
+    __syncthreads();
+    for (int pass = 0; pass < 2; ++pass) {
+        if (th == 0xFFFFFFFEu && pass == 1) break;  // fewer than R valid: pass 0 took all
+        for (int64_t base = 0; base < T; base += SEL_THREADS) {
+            const int m0 = s_m;
+            if (m0 >= R) break;
+            const int64_t i = base + t;
+            bool flag = false;
+            Cand e{0.f, 0xFFFFFFFFu};
+            uint32_t key = 0xFFFFFFFFu;
+            if (i < T) {
+                e = c[i];
+                key = e.row == 0xFFFFFFFFu ? 0xFFFFFFFFu : okey<METRIC>(e.raw);
+                if (th == 0xFFFFFFFEu)
+                    flag = key != 0xFFFFFFFFu;
+                else
+                    flag = pass == 0 ? key < th : key == th;
+            }
+            const uint64_t bal = __ballot(flag);
+            if (lane == 0) s_wave[wv] = __popcll(bal);
+            __syncthreads();
+            int off = m0;
+            for (int x = 0; x < wv; ++x) off += s_wave[x];
+            off += __popcll(bal & ((1ull << lane) - 1ull));
+            if (flag && off < R) recs[off] = make_uint4(key, e.row, __builtin_bit_cast(uint32_t, e.raw), 0u);
+            __syncthreads();
+            if (t == 0) {
+                int tot = 0;
+                for (int x = 0; x < SEL_THREADS / 64; ++x) tot += s_wave[x];
+                s_m = min(R, m0 + tot);
+            }
+            __syncthreads();
+        }
+    }
+    const int m = s_m;
+    int N = 1;
+    while (N < m) N <<= 1;
+    for (int i = m + t; i < N; i += SEL_THREADS)
+        recs[i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    __syncthreads();
+    block_bitonic_sort(recs, N);
+    for (int i = t; i < R; i += SEL_THREADS) {
+        const bool ok = i < m;
+        const uint4 r = ok ? recs[i] : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        if (out_approx) {
+            out_rows[(int64_t)q * R + i] = ok ? (int64_t)r.y + id_offset : -1;
+            const float raw = __builtin_bit_cast(float, r.z);
+            float dist = (METRIC == MQVS_METRIC_COSINE) ? cos_dist(raw) : raw;
+            if (!ok) dist = (METRIC == MQVS_METRIC_IP) ? 1.17549435e-38f : 3.40282347e+38f;
+            out_approx[(int64_t)q * R + i] = dist;
+        } else {
+            out_rows[(int64_t)q * R + i] = ok ? (int64_t)r.y : -1;
+        }
+    }
+}
+
+// ---- build kernels ---------------------------------------------------------
+
+// plane[pos] = bf16(rows[perm[pos]]) (zero for padding and columns >= d),
+// pnorm[pos] = |y|^2
+__global__ __launch_bounds__(256) void k_ivf_pack(const float *rows, const float *norms, int d,
+                                                  const int32_t *perm, int64_t npos, int64_t dpad,
+                                                  uint16_t *plane, float *pnorm) {
+    const int64_t c8 = dpad / 8;
+    const int64_t total = npos * c8;
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int64_t pos = i / c8, cc = i - pos * c8;
+        const int32_t row = perm[pos];
+        uint16_t v[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int64_t col = cc * 8 + j;
+            const float x = (row >= 0 && col < d) ? rows[(int64_t)row * d + col] : 0.f;
+            v[j] = f32_to_bf16_rn(x);
+        }
+        uint4 o;
+        o.x = v[0] | ((uint32_t)v[1] << 16);
+        o.y = v[2] | ((uint32_t)v[3] << 16);
+        o.z = v[4] | ((uint32_t)v[5] << 16);
+        o.w = v[6] | ((uint32_t)v[7] << 16);
+        reinterpret_cast<uint4 *>(plane + pos * dpad)[cc] = o;
+        if (cc == 0) pnorm[pos] = row >= 0 ? norms[row] : 0.f;
+    }
+}
+
+// dst[i] = src[idx[i]] (rows of d floats, source row stride src_ld; idx null = identity)
+__global__ __launch_bounds__(256) void k_gather_rows(const float *src, int64_t src_ld, int d, const int64_t *idx,
+                                                     int64_t m, float *dst) {
+    const int64_t total = m * d;
+    for (int64_t i = blockIdx.x * 256ll + threadIdx.x; i < total; i += (int64_t)gridDim.x * 256) {
+        const int64_t r = i / d, col = i - r * d;
+        dst[i] = src[(idx ? idx[r] : r) * src_ld + col];
+    }
+}
+
+// k-means update: centroid c = mean of its members (rows order[off[c]..off[c+1]),
+// summed in that order, so the result is deterministic); empty clusters keep
+// their centroid.
+__global__ __launch_bounds__(256) void k_centroid_mean(const float *rows, int d, const int32_t *order,
+                                                       const int64_t *off, float *cent) {
+    const int c = blockIdx.x;
+    const int64_t b = off[c], e = off[c + 1];
+    if (e <= b) return;
+    const float inv = 1.0f / (float)(e - b);
+    for (int j = threadIdx.x; j < d; j += 256) {
+        float s = 0.f;
+        for (int64_t i = b; i < e; ++i) s += rows[(int64_t)order[i] * d + j];
+        cent[(int64_t)c * d + j] = s * inv;
+    }
+}
+
+// ---- launchers -------------------------------------------------------------
+
+void launch_ivf_plan(const IvfParams &p, hipStream_t s) {
+    hipLaunchKernelGGL(k_ivf_plan, dim3(1), dim3(kPlanThreads), 0, s, p);
+}
+
+void launch_ivf_scan(const IvfParams &p, int metric, int grid, hipStream_t s) {
+    const size_t lds = (size_t)kIvfQG * (2 * p.dpad + 16);
+    switch (metric) {
+        case MQVS_METRIC_L2:
+            hipLaunchKernelGGL(k_ivf_scan<MQVS_METRIC_L2>, dim3(grid), dim3(256), lds, s, p);
+            break;
+        case MQVS_METRIC_IP:
+            hipLaunchKernelGGL(k_ivf_scan<MQVS_METRIC_IP>, dim3(grid), dim3(256), lds, s, p);
+            break;
+        default:
+            hipLaunchKernelGGL(k_ivf_scan<MQVS_METRIC_COSINE>, dim3(grid), dim3(256), lds, s, p);
+            break;
+    }
+}
+
+void launch_ivf_select(const Cand *cand, const int64_t *qstart, int nq, int R, int metric, int64_t *out_rows,
+                       int64_t id_offset, float *out_approx, hipStream_t s) {
+    int N = 1;
+    while (N < R) N <<= 1;
+    const size_t lds = sizeof(uint4) * N;
+    switch (metric) {
+        case MQVS_METRIC_L2:
+            hipLaunchKernelGGL(k_ivf_select<MQVS_METRIC_L2>, dim3(nq), dim3(SEL_THREADS), lds, s, cand, qstart, R,
+                               out_rows, id_offset, out_approx);
+            break;
+        case MQVS_METRIC_IP:
+            hipLaunchKernelGGL(k_ivf_select<MQVS_METRIC_IP>, dim3(nq), dim3(SEL_THREADS), lds, s, cand, qstart, R,
+                               out_rows, id_offset, out_approx);
+            break;
+        default:
+            hipLaunchKernelGGL(k_ivf_select<MQVS_METRIC_COSINE>, dim3(nq), dim3(SEL_THREADS), lds, s, cand, qstart,
+                               R, out_rows, id_offset, out_approx);
+            break;
+    }
+}
+
+void launch_ivf_pack(const float *rows, const float *norms, int d, const int32_t *perm, int64_t npos, int64_t dpad,
+                     uint16_t *plane, float *pnorm, hipStream_t s) {
+    const int64_t total = npos * (dpad / 8);
+    const int grid = (int)std::min<int64_t>((total + 255) / 256, 65536);
+    if (grid > 0) hipLaunchKernelGGL(k_ivf_pack, dim3(grid), dim3(256), 0, s, rows, norms, d, perm, npos, dpad, plane, pnorm);
+}
+
+void launch_gather_rows(const float *src, int64_t src_ld, int d, const int64_t *idx, int64_t m, float *dst,
+                        hipStream_t s) {
+    const int64_t total = m * d;
+    const int grid = (int)std::min<int64_t>((total + 255) / 256, 65536);
+    if (grid > 0) hipLaunchKernelGGL(k_gather_rows, dim3(grid), dim3(256), 0, s, src, src_ld, d, idx, m, dst);
+}
+
+void launch_centroid_mean(const float *rows, int d, const int32_t *order, const int64_t *off, int nlist, float *cent,
+                          hipStream_t s) {
+    if (nlist > 0) hipLaunchKernelGGL(k_centroid_mean, dim3(nlist), dim3(256), 0, s, rows, d, order, off, cent);
+}
+
+}  // namespace mqvs

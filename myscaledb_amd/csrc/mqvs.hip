@@ -20,27 +20,6 @@
 
 #include "mqvs_internal.h"
 
-struct mqvs_segment {
-    int device = 0;
-    int64_t n = 0;
-    int d = 0;
-    int metric = 0;
-    int64_t granule = 0;
-    int64_t row_offset = 0;
-    float *rows = nullptr;
-    float *norms = nullptr;          // |y|^2 per row (fvec_norm_L2sqr order)
-    uint16_t *rows_hi = nullptr;     // bf16 rounding of the rows, [n][dpad]
-    uint16_t *rows_lo = nullptr;     // bf16 rounding of (row - hi), [n][dpad] (split 3)
-    uint8_t *rows_x6 = nullptr;      // fp6 cross plane [n][dpad/32][48 B] (split 6)
-    uint8_t *rows_sc = nullptr;      // E8M0 scales [n][2] (split 6)
-    float *ynorm_max = nullptr;      // device scalar: max_r |y_r|; split 6: + [kMxRec] norm maxima at +16 B
-    int split = 0;                   // pre-filter planes built: 3, 6, 0 = none
-    int64_t dpad = 0;
-    bool approx_ok = false;          // bf16 pre-filter usable for this segment
-    uint8_t *nonempty_bits = nullptr;// null when every array is non-empty
-    int *chunk_ord = nullptr;        // no-filter chunk ordinals (null = identity)
-    size_t bytes = 0;
-};
 
 namespace mqvs {
 
@@ -51,26 +30,6 @@ static int g_prefilter = 6;  // planes built by new segments (mqvs_set_prefilter
 
 void set_error(const std::string &msg) { g_error = msg; }
 
-struct DevBuf {
-    void *p = nullptr;
-    size_t cap = 0;
-    void *get(size_t bytes) {
-        if (bytes == 0) bytes = 16;
-        if (bytes > cap) {
-            if (p) (void)hipFree(p);
-            p = nullptr;
-            cap = 0;
-            MQVS_HIP(hipMalloc(&p, bytes));
-            cap = bytes;
-        }
-        return p;
-    }
-    void release() {
-        if (p) (void)hipFree(p);
-        p = nullptr;
-        cap = 0;
-    }
-};
 
 struct Workspace {
     hipStream_t stream = nullptr;
@@ -112,36 +71,6 @@ static Workspace &workspace(int device) {
     return w;
 }
 
-struct DeviceGuard {
-    int prev = -1;
-    explicit DeviceGuard(int dev) {
-        MQVS_HIP(hipGetDevice(&prev));
-        if (prev != dev) MQVS_HIP(hipSetDevice(dev));
-    }
-    ~DeviceGuard() {
-        int cur = -1;
-        if (hipGetDevice(&cur) == hipSuccess && prev >= 0 && cur != prev) (void)hipSetDevice(prev);
-    }
-};
-
-template <typename F>
-static int guarded(F &&f) {
-    try {
-        f();
-        return MQVS_OK;
-    } catch (const Error &e) {
-        set_error(e.msg);
-        return e.code;
-    } catch (const std::bad_alloc &) {
-        set_error("host allocation failed");
-        return MQVS_ERR_MEMORY_LIMIT;
-    } catch (...) {
-        set_error("unknown error");
-        return MQVS_ERR_DEVICE;
-    }
-}
-
-[[noreturn]] static void fail(int code, const std::string &msg) { throw Error{code, msg}; }
 
 // ---------------------------------------------------------------------------
 // segments
@@ -763,6 +692,32 @@ static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const i
         MQVS_HIP(hipStreamSynchronize(s));
     }
 }
+
+// ---------------------------------------------------------------------------
+// services for the index path (index.hip)
+
+hipStream_t thread_stream(int device) { return workspace(device).stream; }
+
+void search_internal(mqvs_segment *seg, const float *queries, int nq, int k, int metric,
+                     const uint8_t *filter, const uint8_t *exists, int64_t *out_ids, float *out_dist,
+                     uint32_t flags, hipStream_t stream) {
+    search_impl(seg, queries, nq, k, metric, filter, exists, out_ids, out_dist, flags, stream);
+}
+
+mqvs_segment *segment_from_device(const float *dev_rows, int64_t n, int d, int metric, hipStream_t st) {
+    mqvs_segment *s = new_segment(n, d, metric, std::max<int64_t>(n, 1), 0);
+    try {
+        if (n > 0)
+            MQVS_HIP(hipMemcpyAsync(s->rows, dev_rows, sizeof(float) * (size_t)n * d, hipMemcpyDeviceToDevice, st));
+        prepare_segment(s, nullptr, st);
+    } catch (...) {
+        free_segment(s);
+        throw;
+    }
+    return s;
+}
+
+void segment_release(mqvs_segment *s) { free_segment(s); }
 
 }  // namespace mqvs
 

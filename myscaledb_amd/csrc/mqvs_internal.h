@@ -5,8 +5,32 @@
 #include <stdint.h>
 
 #include <string>
+#include <stdexcept>
+#include <algorithm>
 
 #include "../../include/mqvs.h"
+
+struct mqvs_segment {
+    int device = 0;
+    int64_t n = 0;
+    int d = 0;
+    int metric = 0;
+    int64_t granule = 0;
+    int64_t row_offset = 0;
+    float *rows = nullptr;
+    float *norms = nullptr;          // |y|^2 per row (fvec_norm_L2sqr order)
+    uint16_t *rows_hi = nullptr;     // bf16 rounding of the rows, [n][dpad]
+    uint16_t *rows_lo = nullptr;     // bf16 rounding of (row - hi), [n][dpad] (split 3)
+    uint8_t *rows_x6 = nullptr;      // fp6 cross plane [n][dpad/32][48 B] (split 6)
+    uint8_t *rows_sc = nullptr;      // E8M0 scales [n][2] (split 6)
+    float *ynorm_max = nullptr;      // device scalar: max_r |y_r|; split 6: + [kMxRec] norm maxima at +16 B
+    int split = 0;                   // pre-filter planes built: 3, 6, 0 = none
+    int64_t dpad = 0;
+    bool approx_ok = false;          // bf16 pre-filter usable for this segment
+    uint8_t *nonempty_bits = nullptr;// null when every array is non-empty
+    int *chunk_ord = nullptr;        // no-filter chunk ordinals (null = identity)
+    size_t bytes = 0;
+};
 
 namespace mqvs {
 
@@ -269,6 +293,48 @@ void launch_rerank_select(const ScanParams &p, int metric, const float *bq, int 
                           hipStream_t s);
 
 // ---------------------------------------------------------------------------
+// Index path (kernels_ivf.hip, index.hip)
+constexpr int kIvfQG = 16;   // queries per scan work item (one MFMA B block)
+constexpr int kIvfPad = 16;  // list lengths padded to this many positions
+
+struct IvfParams {
+    const uint16_t *plane;    // [npos][dpad] bf16 rows in list order
+    const int32_t *perm;      // [npos] segment row of each position, -1 = padding
+    const float *pnorm;       // [npos] |y|^2 per position
+    const int64_t *list_off;  // [nlist+1] list start positions (multiples of kIvfPad)
+    int nlist;
+    int64_t dpad;
+    int nq, nprobe;
+    const int64_t *probes;    // [nq][nprobe] list ids (-1 = none)
+    const uint16_t *q_hi;     // [nq][dpad] bf16 query (cosine: normalised)
+    const float *qnorm;       // [nq] |q|^2 (L2)
+    const uint8_t *filter;    // PREWHERE bitmap (rows) or null
+    const uint8_t *exists;    // LWD bitmap (rows) or null
+    int *lcount;              // [nlist] queries probing each list
+    int *lfill;               // [nlist] scatter cursors
+    int64_t *lstart;          // [nlist] first pair of each list in lq
+    int *lq;                  // [nq*nprobe] pairs (q*nprobe + probe) grouped by list
+    int *item_list;           // [nq*nprobe] work item -> list
+    int *item_grp;            // work item -> 16-query group within the list
+    int *nitems;              // number of work items
+    int64_t *qbase;           // [nq*nprobe] start of each pair's region in cand
+    int64_t *qstart;          // [nq+1] start of each query's region
+    Cand *cand;               // approximate values, one per (pair, list position)
+    int64_t *stats;           // [4] values written, items, plane bytes, pairs
+};
+
+void launch_ivf_plan(const IvfParams &p, hipStream_t s);
+void launch_ivf_scan(const IvfParams &p, int metric, int grid, hipStream_t s);
+void launch_ivf_select(const Cand *cand, const int64_t *qstart, int nq, int R, int metric, int64_t *out_rows,
+                       int64_t id_offset, float *out_approx, hipStream_t s);
+void launch_ivf_pack(const float *rows, const float *norms, int d, const int32_t *perm, int64_t npos, int64_t dpad,
+                     uint16_t *plane, float *pnorm, hipStream_t s);
+void launch_gather_rows(const float *src, int64_t src_ld, int d, const int64_t *idx, int64_t m, float *dst,
+                        hipStream_t s);
+void launch_centroid_mean(const float *rows, int d, const int32_t *order, const int64_t *off, int nlist, float *cent,
+                          hipStream_t s);
+
+// ---------------------------------------------------------------------------
 // Error plumbing
 void set_error(const std::string &msg);
 
@@ -276,8 +342,6 @@ struct Error {
     int code;
     std::string msg;
 };
-
-}  // namespace mqvs
 
 #define MQVS_HIP(call)                                                                 \
     do {                                                                               \
@@ -287,3 +351,72 @@ struct Error {
                                                           : MQVS_ERR_DEVICE,             \
                                 std::string(#call) + ": " + hipGetErrorString(e_)};    \
     } while (0)
+
+// ---------------------------------------------------------------------------
+// Host-side plumbing shared by mqvs.hip (segments, FLAT search) and
+// index.hip (the index path)
+
+struct DevBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    void *get(size_t bytes) {
+        if (bytes == 0) bytes = 16;
+        if (bytes > cap) {
+            if (p) (void)hipFree(p);
+            p = nullptr;
+            cap = 0;
+            MQVS_HIP(hipMalloc(&p, bytes));
+            cap = bytes;
+        }
+        return p;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+struct DeviceGuard {
+    int prev = -1;
+    explicit DeviceGuard(int dev) {
+        MQVS_HIP(hipGetDevice(&prev));
+        if (prev != dev) MQVS_HIP(hipSetDevice(dev));
+    }
+    ~DeviceGuard() {
+        int cur = -1;
+        if (hipGetDevice(&cur) == hipSuccess && prev >= 0 && cur != prev) (void)hipSetDevice(prev);
+    }
+};
+
+template <typename F>
+static int guarded(F &&f) {
+    try {
+        f();
+        return MQVS_OK;
+    } catch (const Error &e) {
+        set_error(e.msg);
+        return e.code;
+    } catch (const std::bad_alloc &) {
+        set_error("host allocation failed");
+        return MQVS_ERR_MEMORY_LIMIT;
+    } catch (...) {
+        set_error("unknown error");
+        return MQVS_ERR_DEVICE;
+    }
+}
+
+[[noreturn]] inline void fail(int code, const std::string &msg) { throw Error{code, msg}; }
+
+// mqvs.hip services used by the index path
+hipStream_t thread_stream(int device);
+// FLAT search of a segment (MergeTreeVSManager::vectorScanWithoutIndex);
+// metric may be kMetricIpRaw (faiss knn_inner_product contract)
+void search_internal(mqvs_segment *seg, const float *queries, int nq, int k, int metric,
+                     const uint8_t *filter, const uint8_t *exists, int64_t *out_ids, float *out_dist,
+                     uint32_t flags, hipStream_t stream);
+// segment from rows already on the current device (copied); granule = n
+mqvs_segment *segment_from_device(const float *dev_rows, int64_t n, int d, int metric, hipStream_t st);
+void segment_release(mqvs_segment *s);
+
+}  // namespace mqvs

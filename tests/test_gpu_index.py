@@ -1,0 +1,200 @@
+"""Index path (mqvs_index_*, through the C-ABI) on the GPU.
+
+The MSTG library is absent from the reference snapshot, so the index is pinned
+three ways ("Index-path and MSTG goldens"):
+
+* the reference's own MSTG known-answer tests (00028, 00029; fixtures in
+  tests/golden/index_kats.json): ids exact, distances within the tolerance
+  the survey states (2 ulp relative; 2.4e-7 absolute for cosine, one ulp of
+  the inner product near 1), since the absent library's reduction order is
+  unknown;
+* exhaustive probing (nprobe = nlist) equals the FLAT search bit for bit --
+  ids, distances, order, padding -- because the re-rank computes the exact
+  distance mqvs_search computes for the same rows;
+* recall@10 against the FLAT ground truth at the default search parameters.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+from oracle import oracle as O
+
+pytestmark = pytest.mark.gpu
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+KATS = json.load(open(os.path.join(HERE, "golden", "index_kats.json")))["cases"]
+
+
+@pytest.fixture(scope="module")
+def mq():
+    import myscaledb_amd as m
+    m.init(0)
+    return m
+
+
+def kat_table(c):
+    n, d = c["n"], c["d"]
+    if c["table"] == "mstg768":
+        nn = np.arange(n, dtype=np.float64)[:, None]
+        x = np.arange(d, dtype=np.float64)[None, :]
+        sign = np.where(np.arange(d) % 2 == 0, -1.0, 1.0)[None, :]
+        return ((0.00001 * (nn * 768 + x + 1)) * sign).astype(np.float32)
+    nn = np.arange(n)[:, None]
+    return (nn + np.array([0, 7, 6, 5, 4, 3, 2, 1])[None, :]).astype(np.float32)
+
+
+def bitmap_without(n, ids):
+    m = np.ones(n, np.uint8)
+    m[list(ids)] = 0
+    return np.packbits(m, bitorder="little")
+
+
+@pytest.mark.parametrize("case", KATS, ids=[c["name"] for c in KATS])
+def test_index_kat(mq, case):
+    rows = kat_table(case)
+    q = np.array(case["query"], np.float64).astype(np.float32)[None, :]
+    seg = mq.VectorScanSegment.from_rows(rows, metric=case["metric"], granule=case["granularity"])
+    idx = mq.VectorIndex.build(seg, "MSTG", f"metric_type={case['metric']}")
+    try:
+        flt = bitmap_without(case["n"], case["where_not"]) if case["where_not"] else None
+        ex = bitmap_without(case["n"], case["deleted"]) if case["deleted"] else None
+        ids, dist = idx.search(q, case["k"], case["params"], filter_bitmap=flt, row_exists=ex)
+    finally:
+        idx.free()
+        seg.free()
+    exp_ids = [e[0] for e in case["expect"]]
+    exp_d = np.array([np.float32(e[1]) for e in case["expect"]], np.float32)
+    assert list(ids[0]) == exp_ids
+    if case["metric"] == "Cosine":
+        assert np.all(np.abs(dist[0] - exp_d) <= 2.4e-7), (dist[0], exp_d)
+    else:
+        ulp = np.abs(dist[0].view(np.int32).astype(np.int64) - exp_d.view(np.int32).astype(np.int64))
+        assert np.all(ulp <= 2), (dist[0], exp_d, ulp)
+
+
+EXHAUSTIVE = [
+    # name,           n,     d,   nq, k,   metric,  mode, gran, nlist, filter, lwd
+    ("l2_nq1",        6000,  64,  1,  10,  "L2",     2, 1024, 8,  None, None),
+    ("l2_nq32",       9000,  128, 32, 50,  "L2",     2, 2048, 16, None, None),
+    ("ip_nq5",        7000,  96,  5,  20,  "IP",     1, 1024, 8,  None, None),
+    ("ip_nq40",       7000,  96,  40, 100, "IP",     2, 1024, 12, None, None),
+    ("cos_nq3",       8000,  128, 3,  30,  "Cosine", 2, 512,  10, None, None),
+    ("cos_nq64_768",  6000,  768, 64, 100, "Cosine", 2, 1024, 16, None, None),
+    ("l2_filter",     8000,  64,  24, 40,  "L2",     2, 1024, 8,  0.3,  None),
+    ("cos_filter_lwd", 8000, 64,  7,  40,  "Cosine", 2, 512,  8,  0.5,  0.2),
+    ("ip_lwd",        8000,  48,  21, 30,  "IP",     1, 1024, 8,  None, 0.3),
+    ("l2_d3_small",   300,   3,   20, 100, "L2",     0, 64,   4,  None, None),
+]
+
+
+@pytest.mark.parametrize("cfg", EXHAUSTIVE, ids=[c[0] for c in EXHAUSTIVE])
+def test_index_exhaustive_equals_flat(mq, cfg):
+    name, n, d, nq, k, metric, mode, gran, nlist, fsel, lwd = cfg
+    rows = O.generate(0x5EED0001, mode, 0, n, d)
+    q = O.generate(0x5EED0002, mode, 0, nq, d)
+    rng = np.random.default_rng(n + nq)
+    flt = np.packbits((rng.random(n) < fsel).astype(np.uint8), bitorder="little") if fsel else None
+    ex = np.packbits((rng.random(n) >= lwd).astype(np.uint8), bitorder="little") if lwd else None
+    seg = mq.VectorScanSegment.from_rows(rows, metric=metric, granule=gran)
+    idx = mq.VectorIndex.build(seg, "MSTG", {"nlist": nlist})
+    try:
+        info = idx.info()
+        assert info["nlist"] == nlist and info["rows_indexed"] == n
+        ids_i, dist_i = idx.search(q, k, {"nprobe": nlist, "num_reorder": 4096}, filter_bitmap=flt, row_exists=ex)
+        ids_f, dist_f = seg.search(q, k, filter_bitmap=flt, row_exists=ex)
+        st = mq.vector_index.last_index_stats()
+    finally:
+        idx.free()
+        seg.free()
+    assert st["nprobe"] == nlist and st["num_reorder"] == 4096
+    assert np.array_equal(ids_i, ids_f), name
+    assert np.array_equal(dist_i.view(np.uint32), dist_f.view(np.uint32)), name
+
+
+@pytest.mark.parametrize("metric", ["L2", "IP", "Cosine"])
+def test_index_recall_default_params(mq, metric):
+    """Gaussian-mixture part, default nlist / alpha: recall@10 >= 0.95 against
+    the FLAT search, and every returned distance is the exact one.  Queries
+    are held-out draws of the same mixture (generator rows past the part)."""
+    n, d, nq, k = 60000, 128, 200, 100
+    seg = mq.VectorScanSegment.generate(0x5EED0001, 2, n, d, metric=metric)
+    q = O.generate(0x5EED0001, 2, n, nq, d)
+    idx = mq.VectorIndex.build(seg, "MSTG")
+    try:
+        ids_i, dist_i = idx.search(q, k)
+        ids_f, _ = seg.search(q, k)
+        # returned rows carry their exact distances (mqvs_rerank of the same ids)
+        ids_r, dist_r = seg.rerank(q, ids_i, k)
+    finally:
+        idx.free()
+        seg.free()
+    hit = [len(set(ids_i[i, :10]) & set(ids_f[i, :10])) for i in range(nq)]
+    recall = np.mean(hit) / 10
+    assert recall >= 0.95, recall
+    assert np.array_equal(ids_r, ids_i)
+    assert np.array_equal(dist_r.view(np.uint32), dist_i.view(np.uint32))
+
+
+def test_index_two_stage(mq):
+    """first_stage_only + compute_top_distance_subset == one-call search."""
+    n, d, nq, k, R = 20000, 64, 30, 20, 200
+    seg = mq.VectorScanSegment.generate(0x5EED0001, 2, n, d, metric="Cosine", granule=2048)
+    q = O.generate(0x5EED0002, 2, 0, nq, d)
+    idx = mq.VectorIndex.build(seg, "MSTG", "nlist=20")
+    try:
+        c_ids, c_dist = idx.search(q, R, "nprobe=4", first_stage_only=True)
+        ids2, dist2 = idx.compute_top_distance_subset(q, c_ids, k)
+        ids1, dist1 = idx.search(q, k, f"nprobe=4,num_reorder={R}")
+    finally:
+        idx.free()
+        seg.free()
+    # stage 1 is sorted by the approximate distance, ascending for cosine
+    valid = c_ids >= 0
+    assert valid[:, :k].all()
+    assert np.all(np.diff(np.where(valid, c_dist, np.inf), axis=1) >= 0)
+    assert np.array_equal(ids1, ids2)
+    assert np.array_equal(dist1.view(np.uint32), dist2.view(np.uint32))
+
+
+def test_index_params_errors(mq):
+    from myscaledb_amd import _lib
+    seg = mq.VectorScanSegment.generate(1, 1, 2000, 16, metric="L2")
+    try:
+        with pytest.raises(_lib.MqvsError, match="MSTG doesn't support index parameter: `disk_mode`"):
+            mq.VectorIndex.build(seg, "MSTG", "disk_mode=1")
+        with pytest.raises(_lib.MqvsError, match="LOGICAL_ERROR"):
+            mq.VectorIndex.build(seg, "MSTG", "metric_type=Cosine")
+        with pytest.raises(_lib.NotImplementedMetric):
+            mq.VectorIndex.build(seg, "HNSWSQ")
+        idx = mq.VectorIndex.build(seg, "MSTG", "nlist=4")
+        q = np.ones((2, 16), np.float32)
+        with pytest.raises(_lib.MqvsError, match="search parameter: `ef_s`"):
+            idx.search(q, 5, "ef_s=100")
+        with pytest.raises(_lib.MqvsError, match="alpha"):
+            idx.search(q, 5, "alpha=9")
+        with pytest.raises(_lib.MqvsError, match="dimension"):
+            idx.search(np.ones((2, 8), np.float32), 5)
+        ids, dist = idx.search(q, 5, "alpha=1")
+        assert ids.shape == (2, 5) and (ids >= 0).all()
+        idx.free()
+    finally:
+        seg.free()
+
+
+def test_index_torch_device_pointers(mq):
+    import torch
+    n, d, nq, k = 30000, 96, 100, 10
+    seg = mq.VectorScanSegment.generate(0x5EED0001, 2, n, d, metric="L2")
+    idx = mq.VectorIndex.build(seg, "MSTG")
+    try:
+        qh = O.generate(0x5EED0002, 2, 0, nq, d)
+        qd = torch.from_numpy(qh).cuda()
+        ids_d, dist_d = idx.search(qd, k)
+        ids_h, dist_h = idx.search(qh, k)
+    finally:
+        idx.free()
+        seg.free()
+    assert np.array_equal(ids_d.cpu().numpy(), ids_h)
+    assert np.array_equal(dist_d.cpu().numpy().view(np.uint32), dist_h.view(np.uint32))
