@@ -47,11 +47,18 @@ struct mqvs_index {
     int64_t rows_indexed = 0;
     int64_t dpad = 0;
     float alpha = 3.0f;            // default search alpha
-    mqvs_segment *cent = nullptr;  // centroid segment (coarse quantizer)
+    mqvs_segment *cent = nullptr;  // centroid segment (k-means assignment during the build)
     uint16_t *plane = nullptr;     // [npos][dpad] bf16 rows in list order
     int32_t *perm = nullptr;       // [npos] row of each position, -1 = padding
     float *pnorm = nullptr;        // [npos] |y|^2
     int64_t *list_off = nullptr;   // [nlist+1]
+    // coarse quantizer in the same list layout: the centroids in chunks of
+    // kCoarseChunk (every query probes every chunk), bf16 plane + |c|^2
+    int64_t cnl = 0, cnpos = 0, cmax = 0;
+    uint16_t *cplane = nullptr;
+    int32_t *cperm = nullptr;
+    float *cpnorm = nullptr;
+    int64_t *clist_off = nullptr;
     size_t bytes = 0;
     double build_ms = 0.0;
 };
@@ -59,11 +66,18 @@ struct mqvs_index {
 namespace mqvs {
 
 static thread_local mqvs_index_search_stats g_istats{};
+constexpr int64_t kCoarseChunk = 256;  // centroids per coarse "list"
+
+// plan / scan / select buffers of one list pass
+struct ListBufs {
+    DevBuf lcount, lfill, lstart, lq, items, grp, nitems, qbase, qstart, cand, stats;
+};
 
 struct IndexWorkspace {
     hipEvent_t ev[6] = {};
-    DevBuf queries, qc, qvars, qnorms, qmu, qlam, status, qhi, probes, pdist, filter, exists, lcount, lfill, lstart,
-        lq, items, grp, nitems, qbase, qstart, cand, rows, out_ids, out_dist, stats, ord;
+    DevBuf queries, qvars, qnorms, qmu, qlam, status, qhi, probes, cprobes, filter, exists, rows, out_ids, out_dist,
+        ord;
+    ListBufs coarse, fine;
     void init() {
         if (ev[0]) return;
         for (auto &e : ev) MQVS_HIP(hipEventCreate(&e));
@@ -177,7 +191,8 @@ static void free_index(mqvs_index *ix) {
     (void)hipGetDevice(&cur);
     if (ix->seg) (void)hipSetDevice(ix->seg->device);
     if (ix->cent) segment_release(ix->cent);
-    for (void *q : {(void *)ix->plane, (void *)ix->perm, (void *)ix->pnorm, (void *)ix->list_off})
+    for (void *q : {(void *)ix->plane, (void *)ix->perm, (void *)ix->pnorm, (void *)ix->list_off, (void *)ix->cplane,
+                    (void *)ix->cperm, (void *)ix->cpnorm, (void *)ix->clist_off})
         if (q) (void)hipFree(q);
     if (cur >= 0) (void)hipSetDevice(cur);
     delete ix;
@@ -352,6 +367,29 @@ static mqvs_index *build_impl(mqvs_segment *seg, const char *index_type, const c
         MQVS_HIP(hipMemcpyAsync(ix->list_off, off.data(), sizeof(int64_t) * (Lc + 1), hipMemcpyHostToDevice, s));
         launch_ivf_pack(seg->rows, seg->norms, d, ix->perm, ix->npos, ix->dpad, ix->plane, ix->pnorm, s);
         MQVS_HIP(hipGetLastError());
+        // ---- coarse quantizer as lists of kCoarseChunk centroids
+        {
+            ix->cnl = (Lc + kCoarseChunk - 1) / kCoarseChunk;
+            std::vector<int64_t> coff(ix->cnl + 1, 0);
+            std::vector<int32_t> cperm;
+            for (int64_t j = 0; j < ix->cnl; ++j) {
+                const int64_t b = j * kCoarseChunk, e = std::min(Lc, b + kCoarseChunk);
+                for (int64_t c = b; c < e; ++c) cperm.push_back((int32_t)c);
+                while ((int64_t)cperm.size() % kIvfPad) cperm.push_back(-1);
+                coff[j + 1] = (int64_t)cperm.size();
+                ix->cmax = std::max(ix->cmax, coff[j + 1] - coff[j]);
+            }
+            ix->cnpos = (int64_t)cperm.size();
+            ix->cperm = dalloc<int32_t>(ix, ix->cnpos);
+            ix->clist_off = dalloc<int64_t>(ix, ix->cnl + 1);
+            ix->cplane = dalloc<uint16_t>(ix, (size_t)ix->cnpos * ix->dpad);
+            ix->cpnorm = dalloc<float>(ix, ix->cnpos);
+            MQVS_HIP(hipMemcpyAsync(ix->cperm, cperm.data(), sizeof(int32_t) * ix->cnpos, hipMemcpyHostToDevice, s));
+            MQVS_HIP(hipMemcpyAsync(ix->clist_off, coff.data(), sizeof(int64_t) * (ix->cnl + 1), hipMemcpyHostToDevice, s));
+            launch_ivf_pack(ix->cent->rows, ix->cent->norms, d, ix->cperm, ix->cnpos, ix->dpad, ix->cplane, ix->cpnorm, s);
+            MQVS_HIP(hipGetLastError());
+            MQVS_HIP(hipStreamSynchronize(s));  // cperm / coff are host temporaries
+        }
         MQVS_HIP(hipEventRecord(e1, s));
         MQVS_HIP(hipStreamSynchronize(s));
         float ms = 0.f;
@@ -370,6 +408,56 @@ static mqvs_index *build_impl(mqvs_segment *seg, const char *index_type, const c
 }
 
 // ---- search -----------------------------------------------------------------
+
+// One list pass: plan + bf16 MFMA scan + select of nq queries over a list
+// layout (the index's lists, or the coarse quantizer's centroid chunks).
+// probes[nq][nprobe] are list ids; out: the R best rows per query by the
+// approximate distance (+ id_offset; with out_approx, ids and approximate
+// distances for a first-stage result).  ev (optional): events 2..4 after
+// plan, scan and select.
+static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, const float *pnorm,
+                      const int64_t *list_off, int64_t nlist, int64_t npos, int64_t max_list, int64_t dpad, int metric,
+                      const uint16_t *qhi, const float *qnorm, int nq, const int64_t *probes, int nprobe,
+                      const uint8_t *filter, const uint8_t *exists, int R, int64_t *out_rows, int64_t id_offset,
+                      float *out_approx, hipEvent_t *ev, hipStream_t s) {
+    const int64_t E = (int64_t)nq * nprobe;
+    IvfParams p{};
+    p.plane = plane;
+    p.perm = perm;
+    p.pnorm = pnorm;
+    p.list_off = list_off;
+    p.nlist = (int)nlist;
+    p.dpad = dpad;
+    p.nq = nq;
+    p.nprobe = nprobe;
+    p.probes = probes;
+    p.q_hi = qhi;
+    p.qnorm = qnorm;
+    p.filter = filter;
+    p.exists = exists;
+    p.lcount = (int *)b.lcount.get(sizeof(int) * nlist);
+    p.lfill = (int *)b.lfill.get(sizeof(int) * nlist);
+    p.lstart = (int64_t *)b.lstart.get(sizeof(int64_t) * nlist);
+    p.lq = (int *)b.lq.get(sizeof(int) * E);
+    p.item_list = (int *)b.items.get(sizeof(int) * E);
+    p.item_grp = (int *)b.grp.get(sizeof(int) * E);
+    p.nitems = (int *)b.nitems.get(sizeof(int) * 4);
+    p.qbase = (int64_t *)b.qbase.get(sizeof(int64_t) * E);
+    p.qstart = (int64_t *)b.qstart.get(sizeof(int64_t) * (nq + 1));
+    // a query's region is at most min(nprobe * longest list, every position)
+    const int64_t cap = (int64_t)nq * std::min<int64_t>((int64_t)nprobe * max_list, npos);
+    p.cand = (Cand *)b.cand.get(sizeof(Cand) * (size_t)std::max<int64_t>(cap, 1));
+    p.stats = (int64_t *)b.stats.get(sizeof(int64_t) * 8);
+    launch_ivf_plan(p, s);
+    MQVS_HIP(hipGetLastError());
+    if (ev) MQVS_HIP(hipEventRecord(ev[2], s));
+    launch_ivf_scan(p, metric, 2048, s);
+    MQVS_HIP(hipGetLastError());
+    if (ev) MQVS_HIP(hipEventRecord(ev[3], s));
+    launch_ivf_select(p.cand, p.qstart, nq, R, metric, out_rows, id_offset, out_approx, s);
+    MQVS_HIP(hipGetLastError());
+    if (ev) MQVS_HIP(hipEventRecord(ev[4], s));
+}
 
 static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int k, const char *params,
                               const uint8_t *filter, const uint8_t *exists, int64_t *out_ids, float *out_dist,
@@ -445,75 +533,32 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     launch_query_prep(dq, nq, d, cos ? MQVS_METRIC_COSINE : MQVS_METRIC_L2, ix->metric == MQVS_METRIC_L2, qvars,
                       qnorms, qmu, qlam, status, s);
     MQVS_HIP(hipGetLastError());
-    // first variant of every query, contiguous (the coarse search's queries)
-    const float *qc = dq;
-    if (cos) {
-        float *b = (float *)ws.qc.get(sizeof(float) * (size_t)nq * d);
-        launch_gather_rows(qvars, (int64_t)maxv * qstride, d, nullptr, nq, b, s);
-        MQVS_HIP(hipGetLastError());
-        qc = b;
-    }
     uint16_t *qhi = (uint16_t *)ws.qhi.get(sizeof(uint16_t) * (size_t)nq * ix->dpad);
     launch_to_bf16(qvars, nq, d, (int64_t)maxv * qstride, qhi, nullptr, ix->dpad, s);
     MQVS_HIP(hipGetLastError());
 
-    // ---- coarse: nprobe nearest lists per query
+    // ---- coarse: the nprobe nearest centroids, by the same list pass over
+    // the centroid chunks (every query probes every chunk)
+    int64_t *cprobes = (int64_t *)ws.cprobes.get(sizeof(int64_t) * (size_t)nq * ix->cnl);
+    launch_iota_probes(cprobes, nq, (int)ix->cnl, s);
+    MQVS_HIP(hipGetLastError());
     int64_t *probes = (int64_t *)ws.probes.get(sizeof(int64_t) * (size_t)nq * nprobe);
-    float *pdist = (float *)ws.pdist.get(sizeof(float) * (size_t)nq * nprobe);
-    search_internal(ix->cent, qc, nq, nprobe, ix->coarse_metric, nullptr, nullptr, probes, pdist, MQVS_F_DEVICE_PTRS,
-                    s);
+    list_pass(ws.coarse, ix->cplane, ix->cperm, ix->cpnorm, ix->clist_off, ix->cnl, ix->cnpos, ix->cmax, ix->dpad,
+              ix->metric, qhi, qnorms, nq, cprobes, (int)ix->cnl, nullptr, nullptr, nprobe, probes, 0, nullptr,
+              nullptr, s);
     MQVS_HIP(hipEventRecord(ws.ev[1], s));
 
-    // ---- plan
-    const int64_t E = (int64_t)nq * nprobe;
-    IvfParams p{};
-    p.plane = ix->plane;
-    p.perm = ix->perm;
-    p.pnorm = ix->pnorm;
-    p.list_off = ix->list_off;
-    p.nlist = (int)ix->nlist;
-    p.dpad = ix->dpad;
-    p.nq = nq;
-    p.nprobe = nprobe;
-    p.probes = probes;
-    p.q_hi = qhi;
-    p.qnorm = qnorms;
-    p.filter = dfilter;
-    p.exists = dexists;
-    p.lcount = (int *)ws.lcount.get(sizeof(int) * ix->nlist);
-    p.lfill = (int *)ws.lfill.get(sizeof(int) * ix->nlist);
-    p.lstart = (int64_t *)ws.lstart.get(sizeof(int64_t) * ix->nlist);
-    p.lq = (int *)ws.lq.get(sizeof(int) * E);
-    p.item_list = (int *)ws.items.get(sizeof(int) * E);
-    p.item_grp = (int *)ws.grp.get(sizeof(int) * E);
-    p.nitems = (int *)ws.nitems.get(sizeof(int) * 4);
-    p.qbase = (int64_t *)ws.qbase.get(sizeof(int64_t) * E);
-    p.qstart = (int64_t *)ws.qstart.get(sizeof(int64_t) * (nq + 1));
-    // a query's region is at most min(nprobe * longest list, every position)
-    const int64_t cap = (int64_t)nq * std::min<int64_t>((int64_t)nprobe * ix->max_list, ix->npos);
-    p.cand = (Cand *)ws.cand.get(sizeof(Cand) * (size_t)std::max<int64_t>(cap, 1));
-    int64_t *dstats = (int64_t *)ws.stats.get(sizeof(int64_t) * 8);
-    p.stats = dstats;
-    launch_ivf_plan(p, s);
-    MQVS_HIP(hipGetLastError());
-    MQVS_HIP(hipEventRecord(ws.ev[2], s));
-
-    // ---- scan
-    launch_ivf_scan(p, ix->metric, 2048, s);
-    MQVS_HIP(hipGetLastError());
-    MQVS_HIP(hipEventRecord(ws.ev[3], s));
-
-    // ---- select
+    // ---- fine: the probed lists
+    int64_t *dstats = nullptr;
     if (first_stage) {
-        launch_ivf_select(p.cand, p.qstart, nq, R, ix->metric, dids, seg->row_offset, ddist, s);
-        MQVS_HIP(hipGetLastError());
-        MQVS_HIP(hipEventRecord(ws.ev[4], s));
+        list_pass(ws.fine, ix->plane, ix->perm, ix->pnorm, ix->list_off, ix->nlist, ix->npos, ix->max_list, ix->dpad,
+                  ix->metric, qhi, qnorms, nq, probes, nprobe, dfilter, dexists, R, dids, seg->row_offset, ddist,
+                  ws.ev, s);
         MQVS_HIP(hipEventRecord(ws.ev[5], s));
     } else {
         int64_t *crow = (int64_t *)ws.rows.get(sizeof(int64_t) * (size_t)nq * R);
-        launch_ivf_select(p.cand, p.qstart, nq, R, ix->metric, crow, 0, nullptr, s);
-        MQVS_HIP(hipGetLastError());
-        MQVS_HIP(hipEventRecord(ws.ev[4], s));
+        list_pass(ws.fine, ix->plane, ix->perm, ix->pnorm, ix->list_off, ix->nlist, ix->npos, ix->max_list, ix->dpad,
+                  ix->metric, qhi, qnorms, nq, probes, nprobe, dfilter, dexists, R, crow, 0, nullptr, ws.ev, s);
         // ---- exact re-rank
         ScanParams rp{};
         rp.rows = seg->rows;
@@ -546,6 +591,7 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
         MQVS_HIP(hipGetLastError());
         MQVS_HIP(hipEventRecord(ws.ev[5], s));
     }
+    dstats = (int64_t *)ws.fine.stats.get(sizeof(int64_t) * 8);
 
     const bool async = dev && (flags & MQVS_F_ASYNC);
     if (async) return;

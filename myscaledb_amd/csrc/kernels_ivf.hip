@@ -8,15 +8,17 @@
 // with perm[pos] = segment row (-1 = padding) and pnorm[pos] = |y|^2.
 //
 // Search (one batch of nq queries, each probing nprobe lists):
-//   k_ivf_plan    one workgroup: group the nq*nprobe (query, probe) pairs by
-//                 list, cut each list's queries into 16-query work items, and
-//                 give every pair its region of the candidate buffer
+//   k_plan_*      group the nq*nprobe (query, probe) pairs by list, cut each
+//                 list's queries into 16-query work items, and give every
+//                 pair its region of the candidate buffer
 //   k_ivf_scan    per work item: stream the list's bf16 rows from HBM straight
 //                 into MFMA A fragments (v_mfma_f32_16x16x32_bf16), the 16
 //                 queries as B from LDS; approximate values to the regions
 //   k_ivf_select  per query: radix-select the num_reorder best approximate
 //                 values, ordered compaction, bitonic sort in LDS
 // then the exact fp32 re-rank (k_rerank_ids, kernels_rerank.hip).
+#include <cstdlib>
+
 #include "mqvs_internal.h"
 #include "select_common.h"
 
@@ -26,6 +28,7 @@ typedef __bf16 ivf_bf16x8 __attribute__((ext_vector_type(8)));
 typedef float ivf_f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kPlanThreads = 1024;
+constexpr int kIvfWin = 4;  // 64-column windows loaded per group in the scan
 
 // Exclusive scan of `n` int64 values produced by val(i) into out(i, prefix);
 // returns the total.  One workgroup of kPlanThreads; each thread owns a
@@ -60,26 +63,25 @@ __device__ int64_t block_exclusive_scan(int64_t n, Val val, Out out, int64_t *sh
     return total;
 }
 
-__global__ __launch_bounds__(kPlanThreads) void k_ivf_plan(IvfParams p) {
-    __shared__ int64_t sh[kPlanThreads + 1];
-    const int t = threadIdx.x;
-    const int L = p.nlist;
+// Plan, in four launches (the pairs are spread over the grid; only the two
+// prefix sums run in a single workgroup):
+//   count    lcount[l] = pairs probing list l
+//   lists    exclusive scans over the lists: lstart (pairs), work items
+//   scatter  pairs grouped by list; per query, probe offsets inside its region
+//   queries  exclusive scan of the query regions (qstart)
+__global__ __launch_bounds__(256) void k_plan_count(IvfParams p) {
     const int64_t E = (int64_t)p.nq * p.nprobe;
-    for (int i = t; i < L; i += kPlanThreads) {
-        p.lcount[i] = 0;
-        p.lfill[i] = 0;
-    }
-    __syncthreads();
-    for (int64_t e = t; e < E; e += kPlanThreads) {
+    for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < E; e += (int64_t)gridDim.x * 256) {
         const int64_t l = p.probes[e];
-        if (l >= 0 && l < L) atomicAdd(&p.lcount[l], 1);
+        if (l >= 0 && l < p.nlist) atomicAdd(&p.lcount[l], 1);
     }
-    __syncthreads();
-    // list -> start of its pairs in lq
+}
+
+__global__ __launch_bounds__(kPlanThreads) void k_plan_lists(IvfParams p) {
+    __shared__ int64_t sh[kPlanThreads + 1];
+    const int L = p.nlist;
     block_exclusive_scan(
-        L, [&](int64_t i) { return (int64_t)p.lcount[i]; },
-        [&](int64_t i, int64_t v) { p.lstart[i] = v; }, sh);
-    // list -> its work items (16 queries each)
+        L, [&](int64_t i) { return (int64_t)p.lcount[i]; }, [&](int64_t i, int64_t v) { p.lstart[i] = v; }, sh);
     const int64_t items = block_exclusive_scan(
         L, [&](int64_t i) { return (int64_t)((p.lcount[i] + kIvfQG - 1) / kIvfQG); },
         [&](int64_t i, int64_t v) {
@@ -90,49 +92,62 @@ __global__ __launch_bounds__(kPlanThreads) void k_ivf_plan(IvfParams p) {
             }
         },
         sh);
+    // bf16 bytes the scan streams (every work item reads its list once)
+    const int64_t rows = block_exclusive_scan(
+        L,
+        [&](int64_t i) {
+            return (int64_t)((p.lcount[i] + kIvfQG - 1) / kIvfQG) * (p.list_off[i + 1] - p.list_off[i]);
+        },
+        [&](int64_t, int64_t) {}, sh);
+    if (threadIdx.x == 0) {
+        *p.nitems = (int)items;
+        p.stats[1] = items;
+        p.stats[2] = rows * p.dpad * 2;
+        p.stats[3] = (int64_t)p.nq * p.nprobe;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_plan_scatter(IvfParams p) {
+    const int64_t E = (int64_t)p.nq * p.nprobe;
+    const int64_t gt = blockIdx.x * 256ll + threadIdx.x, gs = (int64_t)gridDim.x * 256;
     // pairs grouped by list (order inside a list is free: every pair owns
     // its output region, so results do not depend on it)
-    for (int64_t e = t; e < E; e += kPlanThreads) {
+    for (int64_t e = gt; e < E; e += gs) {
         const int64_t l = p.probes[e];
-        if (l >= 0 && l < L) {
+        if (l >= 0 && l < p.nlist) {
             const int slot = atomicAdd(&p.lfill[l], 1);
             p.lq[p.lstart[l] + slot] = (int)e;
         }
     }
-    // per query: regions of its probes, back to back in probe order
-    for (int q = t; q < p.nq; q += kPlanThreads) {
+    // per query: its probes' regions back to back in probe order (offsets
+    // relative to the query's region; qstart added by the scan)
+    for (int64_t q = gt; q < p.nq; q += gs) {
         int64_t tot = 0;
         for (int r = 0; r < p.nprobe; ++r) {
-            const int64_t e = (int64_t)q * p.nprobe + r;
+            const int64_t e = q * p.nprobe + r;
             const int64_t l = p.probes[e];
             p.qbase[e] = tot;
-            if (l >= 0 && l < L) tot += p.list_off[l + 1] - p.list_off[l];
+            if (l >= 0 && l < p.nlist) tot += p.list_off[l + 1] - p.list_off[l];
         }
-        p.qstart[q] = tot;  // region length for now
-    }
-    __syncthreads();
-    const int64_t total = block_exclusive_scan(
-        p.nq, [&](int64_t i) { return p.qstart[i]; }, [&](int64_t i, int64_t v) { p.qstart[i] = v; }, sh);
-    for (int64_t e = t; e < E; e += kPlanThreads) p.qbase[e] += p.qstart[e / p.nprobe];
-    // bf16 bytes the scan streams (every work item reads its list once)
-    int64_t bytes = 0;
-    for (int i = t; i < L; i += kPlanThreads)
-        bytes += (int64_t)((p.lcount[i] + kIvfQG - 1) / kIvfQG) * (p.list_off[i + 1] - p.list_off[i]);
-    sh[t] = bytes;
-    __syncthreads();
-    if (t == 0) {
-        int64_t b = 0;
-        for (int i = 0; i < kPlanThreads; ++i) b += sh[i];
-        p.qstart[p.nq] = total;
-        *p.nitems = (int)items;
-        p.stats[0] = total;                   // approximate values written
-        p.stats[1] = items;                   // work items
-        p.stats[2] = b * p.dpad * 2;          // plane bytes streamed
-        p.stats[3] = E;                       // (query, probe) pairs
+        p.qstart[q] = tot;
     }
 }
 
-template <int METRIC>
+__global__ __launch_bounds__(kPlanThreads) void k_plan_queries(IvfParams p) {
+    __shared__ int64_t sh[kPlanThreads + 1];
+    const int64_t total = block_exclusive_scan(
+        p.nq, [&](int64_t i) { return p.qstart[i]; }, [&](int64_t i, int64_t v) { p.qstart[i] = v; }, sh);
+    if (threadIdx.x == 0) {
+        p.qstart[p.nq] = total;
+        p.stats[0] = total;  // approximate values written
+    }
+}
+
+// MAP 0: lane (l16, c) reads bytes [32c, 32c + 32) of each 128-B window
+//        (k-step 1 = its first 16 B, k-step 2 = the next 16 B);
+// MAP 1: k-step 1 reads bytes [16c, 16c + 16), k-step 2 [64 + 16c, ...) --
+//        each load instruction covers one contiguous 64-B half-window per row.
+template <int METRIC, int MAP>
 __global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
     extern __shared__ __attribute__((aligned(16))) unsigned char qtile[];  // 16 x (2 dpad + 16) B
     __shared__ int s_ent[kIvfQG];
@@ -151,7 +166,7 @@ __global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
             const int j = threadIdx.x;
             const int e = j < cnt ? p.lq[p.lstart[l] + (int64_t)g * kIvfQG + j] : -1;
             s_ent[j] = e;
-            s_base[j] = e >= 0 ? p.qbase[e] : 0;
+            s_base[j] = e >= 0 ? p.qstart[e / p.nprobe] + p.qbase[e] : 0;
             s_qn[j] = (e >= 0 && METRIC == MQVS_METRIC_L2) ? p.qnorm[e / p.nprobe] : 0.f;
         }
         __syncthreads();
@@ -165,28 +180,44 @@ __global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
         __syncthreads();
         const int64_t pos0 = p.list_off[l];
         const int nb = (int)((p.list_off[l + 1] - pos0) / 16);
-        const unsigned char *qp = qtile + l16 * qstr + c * 32;
+        const unsigned char *qp = qtile + l16 * qstr + (MAP == 0 ? c * 32 : c * 16);
+        constexpr int kOff2 = MAP == 0 ? 8 : 32;  // element offset of k-step 2 within the window
         const int e = s_ent[l16];
+        const int ngrp = (int)((p.dpad / 64 + kIvfWin - 1) / kIvfWin);
         for (int b = w; b < nb; b += 4) {
             // lane (l16, c) reads 32 contiguous bytes of row l16 per 64-column
             // window; both MFMA k-steps of the window use the same column
             // assignment for A (rows) and B (queries)
-            const uint16_t *rp = p.plane + (pos0 + (int64_t)b * 16 + l16) * p.dpad + c * 16;
+            const uint16_t *rp = p.plane + (pos0 + (int64_t)b * 16 + l16) * p.dpad + (MAP == 0 ? c * 16 : c * 8);
             ivf_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-            ivf_bf16x8 a0 = *reinterpret_cast<const ivf_bf16x8 *>(rp);
-            ivf_bf16x8 a1 = *reinterpret_cast<const ivf_bf16x8 *>(rp + 8);
-            for (int64_t kw = 0; kw < p.dpad; kw += 64) {
-                ivf_bf16x8 n0 = a0, n1 = a1;
-                if (kw + 64 < p.dpad) {
-                    n0 = *reinterpret_cast<const ivf_bf16x8 *>(rp + kw + 64);
-                    n1 = *reinterpret_cast<const ivf_bf16x8 *>(rp + kw + 72);
+            // kIvfWin windows (kIvfWin * 128 B per row) in flight per lane,
+            // the next group prefetched while this one feeds the MFMAs
+            ivf_bf16x8 cur[2 * kIvfWin], nxt[2 * kIvfWin];
+            auto load = [&](int grp, ivf_bf16x8 *dst) {
+#pragma unroll
+                for (int u = 0; u < kIvfWin; ++u) {
+                    const int64_t kw = ((int64_t)grp * kIvfWin + u) * 64;
+                    if (kw < p.dpad) {
+                        dst[2 * u] = *reinterpret_cast<const ivf_bf16x8 *>(rp + kw);
+                        dst[2 * u + 1] = *reinterpret_cast<const ivf_bf16x8 *>(rp + kw + kOff2);
+                    }
                 }
-                const ivf_bf16x8 b0 = *reinterpret_cast<const ivf_bf16x8 *>(qp + 2 * kw);
-                const ivf_bf16x8 b1 = *reinterpret_cast<const ivf_bf16x8 *>(qp + 2 * kw + 16);
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a0, b0, acc, 0, 0, 0);
-                acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a1, b1, acc, 0, 0, 0);
-                a0 = n0;
-                a1 = n1;
+            };
+            load(0, cur);
+            for (int grp = 0; grp < ngrp; ++grp) {
+                if (grp + 1 < ngrp) load(grp + 1, nxt);
+#pragma unroll
+                for (int u = 0; u < kIvfWin; ++u) {
+                    const int64_t kw = ((int64_t)grp * kIvfWin + u) * 64;
+                    if (kw < p.dpad) {
+                        const ivf_bf16x8 b0 = *reinterpret_cast<const ivf_bf16x8 *>(qp + 2 * kw);
+                        const ivf_bf16x8 b1 = *reinterpret_cast<const ivf_bf16x8 *>(qp + 2 * kw + 2 * kOff2);
+                        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[2 * u], b0, acc, 0, 0, 0);
+                        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[2 * u + 1], b1, acc, 0, 0, 0);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < 2 * kIvfWin; ++u) cur[u] = nxt[u];
             }
             // C: lane (l16, c) holds rows 4c..4c+3 of the block for query slot l16
             if (e >= 0) {
@@ -345,25 +376,60 @@ __global__ __launch_bounds__(256) void k_centroid_mean(const float *rows, int d,
     }
 }
 
+// probes[q][j] = j: every query probes every list (the coarse quantizer's
+// centroid chunks)
+__global__ __launch_bounds__(256) void k_iota_probes(int64_t *probes, int64_t E, int np) {
+    for (int64_t e = blockIdx.x * 256ll + threadIdx.x; e < E; e += (int64_t)gridDim.x * 256) probes[e] = e % np;
+}
+
 // ---- launchers -------------------------------------------------------------
 
+void launch_iota_probes(int64_t *probes, int nq, int np, hipStream_t s) {
+    const int64_t E = (int64_t)nq * np;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((E + 255) / 256, 1024));
+    hipLaunchKernelGGL(k_iota_probes, dim3(grid), dim3(256), 0, s, probes, E, np);
+}
+
 void launch_ivf_plan(const IvfParams &p, hipStream_t s) {
-    hipLaunchKernelGGL(k_ivf_plan, dim3(1), dim3(kPlanThreads), 0, s, p);
+    MQVS_HIP(hipMemsetAsync(p.lcount, 0, sizeof(int) * p.nlist, s));
+    MQVS_HIP(hipMemsetAsync(p.lfill, 0, sizeof(int) * p.nlist, s));
+    const int64_t E = (int64_t)p.nq * p.nprobe;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((std::max(E, (int64_t)p.nq) + 255) / 256, 2048));
+    hipLaunchKernelGGL(k_plan_count, dim3(grid), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(k_plan_lists, dim3(1), dim3(kPlanThreads), 0, s, p);
+    hipLaunchKernelGGL(k_plan_scatter, dim3(grid), dim3(256), 0, s, p);
+    hipLaunchKernelGGL(k_plan_queries, dim3(1), dim3(kPlanThreads), 0, s, p);
+}
+
+static int ivf_scan_map() {
+    static const int m = [] {
+        const char *e = std::getenv("MQVS_IVF_SCAN_MAP");  // tuning knob (tools/index_sweep.py)
+        return e && e[0] == '0' ? 0 : 1;
+    }();
+    return m;
+}
+
+template <int MAP>
+static void ivf_scan_t(const IvfParams &p, int metric, int grid, size_t lds, hipStream_t s) {
+    switch (metric) {
+        case MQVS_METRIC_L2:
+            hipLaunchKernelGGL((k_ivf_scan<MQVS_METRIC_L2, MAP>), dim3(grid), dim3(256), lds, s, p);
+            break;
+        case MQVS_METRIC_IP:
+            hipLaunchKernelGGL((k_ivf_scan<MQVS_METRIC_IP, MAP>), dim3(grid), dim3(256), lds, s, p);
+            break;
+        default:
+            hipLaunchKernelGGL((k_ivf_scan<MQVS_METRIC_COSINE, MAP>), dim3(grid), dim3(256), lds, s, p);
+            break;
+    }
 }
 
 void launch_ivf_scan(const IvfParams &p, int metric, int grid, hipStream_t s) {
     const size_t lds = (size_t)kIvfQG * (2 * p.dpad + 16);
-    switch (metric) {
-        case MQVS_METRIC_L2:
-            hipLaunchKernelGGL(k_ivf_scan<MQVS_METRIC_L2>, dim3(grid), dim3(256), lds, s, p);
-            break;
-        case MQVS_METRIC_IP:
-            hipLaunchKernelGGL(k_ivf_scan<MQVS_METRIC_IP>, dim3(grid), dim3(256), lds, s, p);
-            break;
-        default:
-            hipLaunchKernelGGL(k_ivf_scan<MQVS_METRIC_COSINE>, dim3(grid), dim3(256), lds, s, p);
-            break;
-    }
+    if (ivf_scan_map() == 0)
+        ivf_scan_t<0>(p, metric, grid, lds, s);
+    else
+        ivf_scan_t<1>(p, metric, grid, lds, s);
 }
 
 void launch_ivf_select(const Cand *cand, const int64_t *qstart, int nq, int R, int metric, int64_t *out_rows,

@@ -86,16 +86,126 @@ void launch_normalize_rows(float *rows, int64_t n, int d, hipStream_t s) {
     hipLaunchKernelGGL(k_normalize_rows, dim3((unsigned)blocks), dim3(256), 0, s, rows, n, d);
 }
 
-// Query preparation, one lane per query.  L2/IP: variant 0 = the query,
+// Query preparation, one wave per query.  L2/IP: variant 0 = the query,
 // qnorm = |q|^2 (BLAS branch).  Cosine: the reference normalises the SAME
 // query object once per searched granule chunk (VIWithDataPart.h:358 on the
 // dataset shared across chunks, MergeTreeVSManager.cpp:1279-1292,1473-1486),
 // so chunk ordinal c uses normalize^(c+1)(q).  Variants are generated until a
 // repeat: variants [0, mu) are the transient, [mu, mu+lam) the cycle.
+//
+// The sums are sequential fp32 (product rounded, then added: the order of
+// VectorDataset::normalize / fvec_norm_L2sqr), a 768-long dependent chain per
+// normalisation.  Lane l holds elements l + 64 j in registers (J slots); the
+// chain walks them with v_readlane into the wave-uniform accumulator, so it
+// costs one readlane + one add per element instead of an LDS round trip.
+// J = 0: generic d (elements in LDS, lane 0 walks them).
+// sum_{i<d} x_i^2, sequential fp32 (x_i held by lane i % 64, slot i / 64)
+template <int J>
+__device__ __forceinline__ float seq_sq_sum(const float (&x)[J], int d) {
+    float acc = 0.0f;
+#pragma unroll
+    for (int u = 0; u < J; ++u) {
+        const int sq = __builtin_bit_cast(int, x[u] * x[u]);
+        if (64 * u + 64 <= d) {
+#pragma unroll
+            for (int l = 0; l < 64; ++l) acc = acc + __builtin_bit_cast(float, __builtin_amdgcn_readlane(sq, l));
+        } else {
+#pragma unroll
+            for (int l = 0; l < 64; ++l)
+                if (64 * u + l < d) acc = acc + __builtin_bit_cast(float, __builtin_amdgcn_readlane(sq, l));
+        }
+    }
+    return acc;
+}
+
+// J > 0: d <= 64 J, the query in registers
+template <int J>
 __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d, int metric, int blas, float *qvars,
-                             int maxv, float *qnorms, int *qmu, int *qlam, int *status) {
-    // one wave per query; lane l owns elements l, l+64, ... (same lane writes
-    // and later re-reads them, so the variant comparison needs no fence)
+                                                   int maxv, float *qnorms, int *qmu, int *qlam, int *status) {
+    const int j = blockIdx.x;
+    const int lane = threadIdx.x;
+    const int64_t qs = (int64_t)((d + 31) / 32 * 32);
+    const float *src = q + (int64_t)j * d;
+    float *v0 = qvars + (int64_t)j * maxv * qs;
+    float x[J];
+#pragma unroll
+    for (int u = 0; u < J; ++u) {
+        const int i = lane + 64 * u;
+        x[u] = i < d ? src[i] : 0.0f;
+    }
+    if (metric != MQVS_METRIC_COSINE) {
+#pragma unroll
+        for (int u = 0; u < J; ++u)
+            if (lane + 64 * u < d) v0[lane + 64 * u] = x[u];
+        const float sum = blas ? seq_sq_sum<J>(x, d) : 0.0f;
+        if (lane == 0) {
+            if (qnorms) qnorms[j] = sum;
+            qmu[j] = 0;
+            qlam[j] = 1;
+        }
+        return;
+    }
+    const float eps = 1.1920929e-07f;
+    // variants 0..maxv-1 are stored; normalisation maxv is only compared, so a
+    // fixed point reached at the last stored variant is still detected.  A
+    // repeat is found by a 64-bit signature of each variant (wave-reduced in
+    // registers); only a signature match is confirmed element by element.
+    __shared__ uint64_t sig[kMaxVariants + 1];
+    for (int v = 0; v <= maxv; ++v) {
+        const float sum = seq_sq_sum<J>(x, d);
+        if (!(sum < eps)) {
+            const float sr = sqrtf(sum);
+#pragma unroll
+            for (int u = 0; u < J; ++u) x[u] = x[u] / sr;
+        }
+        if (v < maxv) {
+            float *cur = v0 + (int64_t)v * qs;
+#pragma unroll
+            for (int u = 0; u < J; ++u)
+                if (lane + 64 * u < d) cur[lane + 64 * u] = x[u];
+        }
+        uint64_t h = 0;
+#pragma unroll
+        for (int u = 0; u < J; ++u) {
+            const uint64_t b = __builtin_bit_cast(uint32_t, x[u]);
+            h += (b + 0x9E3779B97F4A7C15ull * (uint64_t)(u + 1)) * (b | 1ull) ^ (b << 29);
+        }
+        for (int off = 32; off > 0; off >>= 1) h += __shfl_xor(h, off);
+        if (v < maxv && lane == 0) sig[v] = h;
+        __syncthreads();
+        for (int u = 0; u < v; ++u) {
+            if (sig[u] != h) continue;
+            const float *o = v0 + (int64_t)u * qs;
+            bool eq = true;
+#pragma unroll
+            for (int w = 0; w < J; ++w)
+                if (lane + 64 * w < d)
+                    eq = eq && __builtin_bit_cast(uint32_t, o[lane + 64 * w]) == __builtin_bit_cast(uint32_t, x[w]);
+            if (__all(eq)) {
+                if (lane == 0) {
+                    qmu[j] = u;
+                    qlam[j] = v - u;
+                    if (qnorms) qnorms[j] = 0.0f;
+                }
+                return;
+            }
+        }
+    }
+    if (lane == 0) {
+        // no repeat within maxv + 1 normalisations: variants 0..maxv-1 are
+        // exact, later chunk ordinals are not (the host fails the search if
+        // the part has that many searched chunks)
+        atomicOr(status, 1);
+        qmu[j] = maxv - 1;
+        qlam[j] = 1;
+        if (qnorms) qnorms[j] = 0.0f;
+    }
+}
+
+// generic d: elements in LDS, lane 0 walks the sequential sums
+__global__ __launch_bounds__(64) void k_query_prep_lds(const float *q, int nq, int d, int metric, int blas,
+                                                       float *qvars, int maxv, float *qnorms, int *qmu, int *qlam,
+                                                       int *status) {
     extern __shared__ __attribute__((aligned(16))) float qbuf[];
     const int j = blockIdx.x;
     const int lane = threadIdx.x;
@@ -104,7 +214,6 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
     float *v0 = qvars + (int64_t)j * maxv * qs;
     for (int i = lane; i < d; i += 64) qbuf[i] = src[i];
     __syncthreads();
-    // sequential fp32 sum of squares (product rounded, then added), lane 0
     auto seqsum = [&]() -> float {
         if (lane == 0) {
             float s = 0.0f;
@@ -128,8 +237,6 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
         return;
     }
     const float eps = 1.1920929e-07f;
-    // variants 0..maxv-1 are stored; normalisation maxv is only compared, so a
-    // fixed point reached at the last stored variant is still detected
     for (int v = 0; v <= maxv; ++v) {
         float *cur = v < maxv ? v0 + (int64_t)v * qs : nullptr;
         const float sum = seqsum();
@@ -161,9 +268,6 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
         }
     }
     if (lane == 0) {
-        // no repeat within maxv + 1 normalisations: variants 0..maxv-1 are
-        // exact, later chunk ordinals are not (the host fails the search if
-        // the part has that many searched chunks)
         atomicOr(status, 1);
         qmu[j] = maxv - 1;
         qlam[j] = 1;
@@ -175,8 +279,25 @@ void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, flo
                        float *qnorms, int *qmu, int *qlam, int *status, hipStream_t s) {
     const int maxv = metric == MQVS_METRIC_COSINE ? kMaxVariants : 1;
     const size_t lds = (size_t)((d + 31) / 32 * 32 + 4) * sizeof(float);
-    hipLaunchKernelGGL(k_query_prep, dim3(nq), dim3(64), lds, s, q, nq, d, metric, blas ? 1 : 0,
-                       qvars, maxv, qnorms, qmu, qlam, status);
+#define MQVS_QP(J)                                                                                             \
+    hipLaunchKernelGGL(k_query_prep<J>, dim3(nq), dim3(64), 0, s, q, nq, d, metric, blas ? 1 : 0, qvars, maxv,   \
+                       qnorms, qmu, qlam, status)
+    if (d <= 128)
+        MQVS_QP(2);
+    else if (d <= 256)
+        MQVS_QP(4);
+    else if (d <= 512)
+        MQVS_QP(8);
+    else if (d <= 768)
+        MQVS_QP(12);
+    else if (d <= 1024)
+        MQVS_QP(16);
+    else if (d <= 1536)
+        MQVS_QP(24);
+    else
+        hipLaunchKernelGGL(k_query_prep_lds, dim3(nq), dim3(64), lds, s, q, nq, d, metric, blas ? 1 : 0, qvars, maxv,
+                           qnorms, qmu, qlam, status);
+#undef MQVS_QP
 }
 
 // Counter-based synthetic generator; bit-identical to oracle/mqvs_oracle.c

@@ -56,31 +56,27 @@ __device__ inline float cand_value(const ScanParams &p, int q, int64_t row) {
     return acc;
 }
 
-template <int METRIC, bool DIRECT>
-__global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids(ScanParams p, const int64_t *cand, int ncand,
-                                                           int k, int64_t id_offset, int64_t *out_ids,
-                                                           float *out_dist) {
-    extern __shared__ __attribute__((aligned(16))) uint4 recs[];  // kSortCap records
-    const int q = blockIdx.x;
-    const int64_t *c = cand + (int64_t)q * ncand;
-    for (int i = threadIdx.x; i < ncand; i += SEL_THREADS) {
-        const int64_t row = c[i];
-        uint4 r = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-        if (row >= 0 && row < p.n && row_valid(p, row)) {
-            const float raw = cand_value<METRIC, DIRECT>(p, q, row);
-            r.x = key32<METRIC>(raw);
-            r.w = (uint32_t)row;
-            if (METRIC == MQVS_METRIC_COSINE) {
-                r.y = p.chunk_rows > 0 ? (uint32_t)(row / p.chunk_rows) : 0u;
-                r.z = ~ord_asc(raw);
-            } else {
-                r.y = 0;
-                r.z = 0;
-            }
-            if (r.x == 0xFFFFFFFFu) r = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-        }
-        recs[i] = r;
+// candidate record -> top-k outputs (shared by both re-rank kernels)
+template <int METRIC>
+__device__ inline uint4 rerank_rec(const ScanParams &p, int64_t row, float raw) {
+    uint4 r = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    if (row < 0) return r;
+    r.x = key32<METRIC>(raw);
+    r.w = (uint32_t)row;
+    if (METRIC == MQVS_METRIC_COSINE) {
+        r.y = p.chunk_rows > 0 ? (uint32_t)(row / p.chunk_rows) : 0u;
+        r.z = ~ord_asc(raw);
+    } else {
+        r.y = 0;
+        r.z = 0;
     }
+    if (r.x == 0xFFFFFFFFu) r = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    return r;
+}
+
+template <int METRIC>
+__device__ inline void rerank_emit(uint4 *recs, int ncand, int k, int q, int64_t id_offset, int64_t *out_ids,
+                                   float *out_dist) {
     int N = 1;
     while (N < ncand) N <<= 1;
     for (int i = ncand + threadIdx.x; i < N; i += SEL_THREADS)
@@ -100,11 +96,154 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids(ScanParams p, const 
     }
 }
 
+// Generic form (any d): one thread per candidate walks its row.
+template <int METRIC, bool DIRECT>
+__global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids(ScanParams p, const int64_t *cand, int ncand,
+                                                           int k, int64_t id_offset, int64_t *out_ids,
+                                                           float *out_dist) {
+    extern __shared__ __attribute__((aligned(16))) uint4 recs[];  // pow2 >= ncand records
+    const int q = blockIdx.x;
+    const int64_t *c = cand + (int64_t)q * ncand;
+    for (int i = threadIdx.x; i < ncand; i += SEL_THREADS) {
+        int64_t row = c[i];
+        if (!(row >= 0 && row < p.n && row_valid(p, row))) row = -1;
+        recs[i] = rerank_rec<METRIC>(p, row, row >= 0 ? cand_value<METRIC, DIRECT>(p, q, row) : 0.f);
+    }
+    rerank_emit<METRIC>(recs, ncand, k, q, id_offset, out_ids, out_dist);
+}
+
+// d % 4 == 0: the same per-candidate sequential chain (bit-identical), with
+// the rows streamed cooperatively: per 32-column tile a wave loads its 64
+// candidates' 128-B row slices with float4 loads (8 lanes per row, full
+// cache lines), prefetching the next tile into registers, and stages them
+// in LDS (row stride 33 floats: conflict-free column reads); each lane then
+// runs its chain from LDS.  Lanes of a wave run in lockstep, so the wave's
+// own LDS tile needs no barrier.
+constexpr int kRrStride = 33;
+
+template <int METRIC, bool DIRECT>
+__global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids_tiled(ScanParams p, const int64_t *cand, int ncand,
+                                                                 int k, int64_t id_offset, int64_t *out_ids,
+                                                                 float *out_dist, int nrec) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    uint4 *recs = reinterpret_cast<uint4 *>(smem);
+    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    float *tile = reinterpret_cast<float *>(smem + (size_t)nrec * sizeof(uint4)) + wv * 64 * kRrStride;
+    const int q = blockIdx.x;
+    const int64_t *c = cand + (int64_t)q * ncand;
+    const int d = p.d;
+    const int64_t qs = (int64_t)((d + 31) / 32 * 32);
+    const int ntiles = (d + 31) / 32;
+    for (int cb = 0; cb < ncand; cb += SEL_THREADS) {
+        const int i = cb + threadIdx.x;
+        int64_t row = -1;
+        if (i < ncand) {
+            row = c[i];
+            if (!(row >= 0 && row < p.n && row_valid(p, row))) row = -1;
+        }
+        const float *x = p.qvars;
+        if (row >= 0) {
+            const int64_t chunk = p.chunk_rows > 0 ? row / p.chunk_rows : 0;
+            const int ord = chunk_ordinal(p, chunk);
+            const int v = variant_of(p, q, ord < 0 ? 0 : ord);
+            x = p.qvars + ((int64_t)q * p.maxv + v) * qs;
+        }
+        float acc = 0.0f;
+        if (__ballot(row >= 0)) {
+            // rows this lane loads: slot j*8 + lane/8, float4 column lane%8
+            int64_t lrow[8];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) lrow[j] = __shfl(row, j * 8 + (lane >> 3));
+            float4 ry[8], rx[8];
+            auto load = [&](int t) {
+                const int col = t * 32 + (lane & 7) * 4;
+#pragma unroll
+                for (int j = 0; j < 8; ++j)
+                    ry[j] = (lrow[j] >= 0 && col < d)
+                                ? *reinterpret_cast<const float4 *>(p.rows + lrow[j] * d + col)
+                                : make_float4(0.f, 0.f, 0.f, 0.f);
+                // the lane's own query slice (variant of its row's chunk)
+#pragma unroll
+                for (int j = 0; j < 8; ++j) rx[j] = *reinterpret_cast<const float4 *>(x + t * 32 + 4 * j);
+            };
+            load(0);
+            for (int t = 0; t < ntiles; ++t) {
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    float *dst = tile + (j * 8 + (lane >> 3)) * kRrStride + (lane & 7) * 4;
+                    dst[0] = ry[j].x;
+                    dst[1] = ry[j].y;
+                    dst[2] = ry[j].z;
+                    dst[3] = ry[j].w;
+                }
+                float xt[32];
+#pragma unroll
+                for (int j = 0; j < 8; ++j) {
+                    xt[4 * j] = rx[j].x;
+                    xt[4 * j + 1] = rx[j].y;
+                    xt[4 * j + 2] = rx[j].z;
+                    xt[4 * j + 3] = rx[j].w;
+                }
+                if (t + 1 < ntiles) load(t + 1);
+                __builtin_amdgcn_wave_barrier();
+                const float *mine = tile + lane * kRrStride;
+                const int cols = min(32, d - t * 32);
+                if (cols == 32) {
+#pragma unroll
+                    for (int cc = 0; cc < 32; ++cc) {
+                        const float a = mine[cc], b = xt[cc];
+                        if (DIRECT) {
+                            if (METRIC == MQVS_METRIC_L2) {
+                                const float e = a - b;
+                                acc = acc + e * e;
+                            } else {
+                                acc = acc + a * b;
+                            }
+                        } else {
+                            acc = fmaf(b, a, acc);
+                        }
+                    }
+                } else {
+                    for (int cc = 0; cc < cols; ++cc) {
+                        const float a = mine[cc], b = x[t * 32 + cc];
+                        if (DIRECT) {
+                            if (METRIC == MQVS_METRIC_L2) {
+                                const float e = a - b;
+                                acc = acc + e * e;
+                            } else {
+                                acc = acc + a * b;
+                            }
+                        } else {
+                            acc = fmaf(b, a, acc);
+                        }
+                    }
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+        }
+        float raw = acc;
+        if (!DIRECT && METRIC == MQVS_METRIC_L2 && row >= 0) {
+            raw = (p.qnorms[q] + p.row_norms[row]) - 2.0f * acc;
+            if (raw < 0) raw = 0;
+        }
+        if (i < ncand) recs[i] = rerank_rec<METRIC>(p, row, raw);
+    }
+    rerank_emit<METRIC>(recs, ncand, k, q, id_offset, out_ids, out_dist);
+}
+
 template <int M, bool DIRECT>
 static void rerank_ids_t(const ScanParams &p, const int64_t *cand, int ncand, int k, int64_t id_offset,
                          int64_t *ids, float *dist, hipStream_t s) {
-    hipLaunchKernelGGL((k_rerank_ids<M, DIRECT>), dim3(p.nq), dim3(SEL_THREADS), kSortCap * sizeof(uint4), s,
-                       p, cand, ncand, k, id_offset, ids, dist);
+    int N = 1;
+    while (N < ncand) N <<= 1;
+    if ((p.d & 3) == 0) {
+        const size_t lds = N * sizeof(uint4) + (SEL_THREADS / 64) * 64 * kRrStride * sizeof(float);
+        hipLaunchKernelGGL((k_rerank_ids_tiled<M, DIRECT>), dim3(p.nq), dim3(SEL_THREADS), lds, s, p, cand, ncand, k,
+                           id_offset, ids, dist, N);
+    } else {
+        hipLaunchKernelGGL((k_rerank_ids<M, DIRECT>), dim3(p.nq), dim3(SEL_THREADS), N * sizeof(uint4), s, p, cand,
+                           ncand, k, id_offset, ids, dist);
+    }
 }
 
 void launch_rerank_ids(const ScanParams &p, int metric, const int64_t *cand, int ncand, int k,

@@ -324,6 +324,7 @@ struct IvfParams {
 };
 
 void launch_ivf_plan(const IvfParams &p, hipStream_t s);
+void launch_iota_probes(int64_t *probes, int nq, int np, hipStream_t s);
 void launch_ivf_scan(const IvfParams &p, int metric, int grid, hipStream_t s);
 void launch_ivf_select(const Cand *cand, const int64_t *qstart, int nq, int R, int metric, int64_t *out_rows,
                        int64_t id_offset, float *out_approx, hipStream_t s);
