@@ -70,7 +70,7 @@ constexpr int64_t kCoarseChunk = 256;  // centroids per coarse "list"
 
 // plan / scan / select buffers of one list pass
 struct ListBufs {
-    DevBuf lcount, lfill, lstart, lq, items, grp, nitems, qbase, qstart, cand, stats;
+    DevBuf lcount, lfill, lstart, lq, items, grp, chk, nitems, qbase, qstart, cand, stats;
 };
 
 struct IndexWorkspace {
@@ -419,7 +419,7 @@ static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, c
                       const int64_t *list_off, int64_t nlist, int64_t npos, int64_t max_list, int64_t dpad, int metric,
                       const uint16_t *qhi, const float *qnorm, int nq, const int64_t *probes, int nprobe,
                       const uint8_t *filter, const uint8_t *exists, int R, int64_t *out_rows, int64_t id_offset,
-                      float *out_approx, hipEvent_t *ev, hipStream_t s) {
+                      float *out_approx, hipEvent_t *ev, hipStream_t s, bool dense = false) {
     const int64_t E = (int64_t)nq * nprobe;
     IvfParams p{};
     p.plane = plane;
@@ -439,8 +439,14 @@ static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, c
     p.lfill = (int *)b.lfill.get(sizeof(int) * nlist);
     p.lstart = (int64_t *)b.lstart.get(sizeof(int64_t) * nlist);
     p.lq = (int *)b.lq.get(sizeof(int) * E);
-    p.item_list = (int *)b.items.get(sizeof(int) * E);
-    p.item_grp = (int *)b.grp.get(sizeof(int) * E);
+    // 32-query work items when lists are probed by many queries (each A
+    // fragment then feeds two MFMAs)
+    p.qg = (dense || E >= 24 * nlist) ? 32 : 16;
+    // work items = sum over probed lists of groups x 512-position slices
+    const int64_t max_items = (E / p.qg + std::min<int64_t>(E, nlist)) * (max_list / 512 + 1);
+    p.item_list = (int *)b.items.get(sizeof(int) * max_items);
+    p.item_grp = (int *)b.grp.get(sizeof(int) * max_items);
+    p.item_chk = (int *)b.chk.get(sizeof(int) * max_items);
     p.nitems = (int *)b.nitems.get(sizeof(int) * 4);
     p.qbase = (int64_t *)b.qbase.get(sizeof(int64_t) * E);
     p.qstart = (int64_t *)b.qstart.get(sizeof(int64_t) * (nq + 1));
@@ -448,13 +454,17 @@ static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, c
     const int64_t cap = (int64_t)nq * std::min<int64_t>((int64_t)nprobe * max_list, npos);
     p.cand = (Cand *)b.cand.get(sizeof(Cand) * (size_t)std::max<int64_t>(cap, 1));
     p.stats = (int64_t *)b.stats.get(sizeof(int64_t) * 8);
-    launch_ivf_plan(p, s);
+    if (dense)
+        launch_ivf_plan_dense(p, npos, s);
+    else
+        launch_ivf_plan(p, s);
     MQVS_HIP(hipGetLastError());
     if (ev) MQVS_HIP(hipEventRecord(ev[2], s));
-    launch_ivf_scan(p, metric, 2048, s);
+    launch_ivf_scan(p, metric, 1024, s);
     MQVS_HIP(hipGetLastError());
     if (ev) MQVS_HIP(hipEventRecord(ev[3], s));
-    launch_ivf_select(p.cand, p.qstart, nq, R, metric, out_rows, id_offset, out_approx, s);
+    const int64_t expect = dense ? npos : (int64_t)((double)nprobe * npos / std::max<int64_t>(nlist, 1) * 1.5);
+    launch_ivf_select(p.cand, p.qstart, nq, R, metric, out_rows, id_offset, out_approx, expect, s);
     MQVS_HIP(hipGetLastError());
     if (ev) MQVS_HIP(hipEventRecord(ev[4], s));
 }
@@ -539,13 +549,11 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
 
     // ---- coarse: the nprobe nearest centroids, by the same list pass over
     // the centroid chunks (every query probes every chunk)
-    int64_t *cprobes = (int64_t *)ws.cprobes.get(sizeof(int64_t) * (size_t)nq * ix->cnl);
-    launch_iota_probes(cprobes, nq, (int)ix->cnl, s);
-    MQVS_HIP(hipGetLastError());
+    const int64_t *cprobes = nullptr;  // dense plan: probe r of every query is chunk r
     int64_t *probes = (int64_t *)ws.probes.get(sizeof(int64_t) * (size_t)nq * nprobe);
     list_pass(ws.coarse, ix->cplane, ix->cperm, ix->cpnorm, ix->clist_off, ix->cnl, ix->cnpos, ix->cmax, ix->dpad,
               ix->metric, qhi, qnorms, nq, cprobes, (int)ix->cnl, nullptr, nullptr, nprobe, probes, 0, nullptr,
-              nullptr, s);
+              nullptr, s, true);
     MQVS_HIP(hipEventRecord(ws.ev[1], s));
 
     // ---- fine: the probed lists

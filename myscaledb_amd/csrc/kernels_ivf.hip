@@ -28,7 +28,8 @@ typedef __bf16 ivf_bf16x8 __attribute__((ext_vector_type(8)));
 typedef float ivf_f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kPlanThreads = 1024;
-constexpr int kIvfWin = 4;  // 64-column windows loaded per group in the scan
+constexpr int kIvfWin = 4;      // 64-column windows loaded per group in the scan
+constexpr int kIvfChunk = 512;  // list positions per scan work item (balances long and short lists)
 
 // Exclusive scan of `n` int64 values produced by val(i) into out(i, prefix);
 // returns the total.  One workgroup of kPlanThreads; each thread owns a
@@ -40,19 +41,26 @@ __device__ int64_t block_exclusive_scan(int64_t n, Val val, Out out, int64_t *sh
     const int64_t b = t * per, e = min(n, b + per);
     int64_t s = 0;
     for (int64_t i = b; i < e; ++i) s += val(i);
-    sh[t] = s;
+    // block prefix of the run sums: wave scans, then the 16 wave totals
+    const int lane = t & 63, wv = t >> 6;
+    int64_t inc = s;
+    for (int off = 1; off < 64; off <<= 1) {
+        const int64_t y = __shfl_up(inc, off);
+        if (lane >= off) inc += y;
+    }
+    if (lane == 63) sh[wv] = inc;
     __syncthreads();
     if (t == 0) {
         int64_t acc = 0;
-        for (int i = 0; i < kPlanThreads; ++i) {
-            const int64_t v = sh[i];
-            sh[i] = acc;
+        for (int w = 0; w < kPlanThreads / 64; ++w) {
+            const int64_t v = sh[w];
+            sh[w] = acc;
             acc += v;
         }
         sh[kPlanThreads] = acc;
     }
     __syncthreads();
-    int64_t run = sh[t];
+    int64_t run = sh[wv] + inc - s;
     for (int64_t i = b; i < e; ++i) {
         const int64_t v = val(i);
         out(i, run);
@@ -82,21 +90,30 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_lists(IvfParams p) {
     const int L = p.nlist;
     block_exclusive_scan(
         L, [&](int64_t i) { return (int64_t)p.lcount[i]; }, [&](int64_t i, int64_t v) { p.lstart[i] = v; }, sh);
+    // work items: (16/32-query group) x (kIvfChunk-position slice of the list)
     const int64_t items = block_exclusive_scan(
-        L, [&](int64_t i) { return (int64_t)((p.lcount[i] + kIvfQG - 1) / kIvfQG); },
+        L,
+        [&](int64_t i) {
+            return (int64_t)((p.lcount[i] + p.qg - 1) / p.qg) *
+                   ((p.list_off[i + 1] - p.list_off[i] + kIvfChunk - 1) / kIvfChunk);
+        },
         [&](int64_t i, int64_t v) {
-            const int g = (p.lcount[i] + kIvfQG - 1) / kIvfQG;
-            for (int j = 0; j < g; ++j) {
-                p.item_list[v + j] = (int)i;
-                p.item_grp[v + j] = j;
-            }
+            const int g = (p.lcount[i] + p.qg - 1) / p.qg;
+            const int nc = (int)((p.list_off[i + 1] - p.list_off[i] + kIvfChunk - 1) / kIvfChunk);
+            for (int j = 0; j < g; ++j)
+                for (int cc = 0; cc < nc; ++cc) {
+                    p.item_list[v] = (int)i;
+                    p.item_grp[v] = j;
+                    p.item_chk[v] = cc;
+                    ++v;
+                }
         },
         sh);
     // bf16 bytes the scan streams (every work item reads its list once)
     const int64_t rows = block_exclusive_scan(
         L,
         [&](int64_t i) {
-            return (int64_t)((p.lcount[i] + kIvfQG - 1) / kIvfQG) * (p.list_off[i + 1] - p.list_off[i]);
+            return (int64_t)((p.lcount[i] + p.qg - 1) / p.qg) * (p.list_off[i + 1] - p.list_off[i]);
         },
         [&](int64_t, int64_t) {}, sh);
     if (threadIdx.x == 0) {
@@ -143,34 +160,73 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_queries(IvfParams p) {
     }
 }
 
-// MAP 0: lane (l16, c) reads bytes [32c, 32c + 32) of each 128-B window
-//        (k-step 1 = its first 16 B, k-step 2 = the next 16 B);
-// MAP 1: k-step 1 reads bytes [16c, 16c + 16), k-step 2 [64 + 16c, ...) --
-//        each load instruction covers one contiguous 64-B half-window per row.
-template <int METRIC, int MAP>
+// Plan for the dense case (every query probes every list, probe r = list r:
+// the coarse quantizer's centroid chunks), in one grid kernel.
+__global__ __launch_bounds__(256) void k_plan_dense(IvfParams p, int64_t npos) {
+    const int L = p.nlist, G = (p.nq + p.qg - 1) / p.qg;
+    const int64_t E = (int64_t)p.nq * L;
+    const int64_t gt = blockIdx.x * 256ll + threadIdx.x, gs = (int64_t)gridDim.x * 256;
+    for (int64_t e = gt; e < E; e += gs) {
+        const int64_t q = e / L, l = e - q * L;
+        p.lq[l * p.nq + q] = (int)e;
+        p.qbase[e] = p.list_off[l];
+    }
+    // items (list, group, slice): lists here are centroid chunks of equal
+    // length, so every list has the same slices
+    const int NC = (int)((p.list_off[1] - p.list_off[0] + kIvfChunk - 1) / kIvfChunk);
+    for (int64_t i = gt; i < (int64_t)L * G * NC; i += gs) {
+        p.item_list[i] = (int)(i / ((int64_t)G * NC));
+        p.item_grp[i] = (int)((i / NC) % G);
+        p.item_chk[i] = (int)(i % NC);
+    }
+    for (int64_t l = gt; l < L; l += gs) {
+        p.lcount[l] = p.nq;
+        p.lstart[l] = l * p.nq;
+    }
+    for (int64_t q = gt; q <= p.nq; q += gs) p.qstart[q] = q * npos;
+    if (gt == 0) {
+        *p.nitems = L * G * NC;
+        p.stats[0] = (int64_t)p.nq * npos;
+        p.stats[1] = (int64_t)L * G * NC;
+        p.stats[2] = (int64_t)G * npos * p.dpad * 2;
+        p.stats[3] = E;
+    }
+}
+
+// Scan work item = one list x up to 16 QB queries (QB MFMA B blocks).  The
+// query tile sits in LDS (row stride 2 dpad + 16 B: the 16 rows of a B block
+// hit distinct bank groups).  Each wave takes 16-row blocks of the list; lane
+// (l16, c) streams row l16 straight from HBM into A fragments: per 64-column
+// window, k-step 1 = bytes [16c, 16c + 16), k-step 2 = [64 + 16c, ...), so
+// one load instruction covers a contiguous 64-B half-window of 16 rows.
+// kIvfWin windows are in flight per lane and the next group is prefetched
+// while the current one feeds the MFMAs; every A fragment serves QB MFMAs.
+template <int METRIC, int QB>
 __global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
-    extern __shared__ __attribute__((aligned(16))) unsigned char qtile[];  // 16 x (2 dpad + 16) B
-    __shared__ int s_ent[kIvfQG];
-    __shared__ int64_t s_base[kIvfQG];
-    __shared__ float s_qn[kIvfQG];
-    const int64_t qstr = 2 * p.dpad + 16;  // +16 B: the 16 query rows hit distinct bank groups
+    constexpr int QG = 16 * QB;
+    extern __shared__ __attribute__((aligned(16))) unsigned char qtile[];  // QG x (2 dpad + 16) B
+    __shared__ int s_ent[QG];
+    __shared__ int64_t s_base[QG];
+    __shared__ float s_qn[QG];
+    const int64_t qstr = 2 * p.dpad + 16;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int l16 = lane & 15, c = lane >> 4;
     const int nitems = *p.nitems;
     const int cpr = (int)(p.dpad / 8);  // 16-B chunks per query row
+    const int ngrp = (int)((p.dpad / 64 + kIvfWin - 1) / kIvfWin);
     for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
-        const int l = p.item_list[it], g = p.item_grp[it];
-        const int cnt = min(kIvfQG, p.lcount[l] - g * kIvfQG);
+        const int l = p.item_list[it], g = p.item_grp[it], chk = p.item_chk[it];
+        const int cnt = min(QG, p.lcount[l] - g * QG);
         __syncthreads();  // the previous item's readers are done with qtile
-        if (threadIdx.x < kIvfQG) {
+        if (threadIdx.x < QG) {
             const int j = threadIdx.x;
-            const int e = j < cnt ? p.lq[p.lstart[l] + (int64_t)g * kIvfQG + j] : -1;
+            const int e = j < cnt ? p.lq[p.lstart[l] + (int64_t)g * QG + j] : -1;
             s_ent[j] = e;
             s_base[j] = e >= 0 ? p.qstart[e / p.nprobe] + p.qbase[e] : 0;
             s_qn[j] = (e >= 0 && METRIC == MQVS_METRIC_L2) ? p.qnorm[e / p.nprobe] : 0.f;
         }
         __syncthreads();
-        for (int i = threadIdx.x; i < kIvfQG * cpr; i += 256) {
+        for (int i = threadIdx.x; i < QG * cpr; i += 256) {
             const int j = i / cpr, cc = i - j * cpr;
             const int e = s_ent[j];
             uint4 v = make_uint4(0, 0, 0, 0);
@@ -179,19 +235,16 @@ __global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
         }
         __syncthreads();
         const int64_t pos0 = p.list_off[l];
-        const int nb = (int)((p.list_off[l + 1] - pos0) / 16);
-        const unsigned char *qp = qtile + l16 * qstr + (MAP == 0 ? c * 32 : c * 16);
-        constexpr int kOff2 = MAP == 0 ? 8 : 32;  // element offset of k-step 2 within the window
-        const int e = s_ent[l16];
-        const int ngrp = (int)((p.dpad / 64 + kIvfWin - 1) / kIvfWin);
-        for (int b = w; b < nb; b += 4) {
-            // lane (l16, c) reads 32 contiguous bytes of row l16 per 64-column
-            // window; both MFMA k-steps of the window use the same column
-            // assignment for A (rows) and B (queries)
-            const uint16_t *rp = p.plane + (pos0 + (int64_t)b * 16 + l16) * p.dpad + (MAP == 0 ? c * 16 : c * 8);
-            ivf_f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-            // kIvfWin windows (kIvfWin * 128 B per row) in flight per lane,
-            // the next group prefetched while this one feeds the MFMAs
+        const int nb = (int)min<int64_t>((p.list_off[l + 1] - pos0) / 16, (int64_t)(chk + 1) * (kIvfChunk / 16));
+        const unsigned char *qp = qtile + l16 * qstr + c * 16;
+        int ent[QB];
+#pragma unroll
+        for (int j = 0; j < QB; ++j) ent[j] = s_ent[16 * j + l16];
+        for (int b = chk * (kIvfChunk / 16) + w; b < nb; b += 4) {
+            const uint16_t *rp = p.plane + (pos0 + (int64_t)b * 16 + l16) * p.dpad + c * 8;
+            ivf_f32x4 acc[QB];
+#pragma unroll
+            for (int j = 0; j < QB; ++j) acc[j] = ivf_f32x4{0.f, 0.f, 0.f, 0.f};
             ivf_bf16x8 cur[2 * kIvfWin], nxt[2 * kIvfWin];
             auto load = [&](int grp, ivf_bf16x8 *dst) {
 #pragma unroll
@@ -199,7 +252,7 @@ __global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
                     const int64_t kw = ((int64_t)grp * kIvfWin + u) * 64;
                     if (kw < p.dpad) {
                         dst[2 * u] = *reinterpret_cast<const ivf_bf16x8 *>(rp + kw);
-                        dst[2 * u + 1] = *reinterpret_cast<const ivf_bf16x8 *>(rp + kw + kOff2);
+                        dst[2 * u + 1] = *reinterpret_cast<const ivf_bf16x8 *>(rp + kw + 32);
                     }
                 }
             };
@@ -210,32 +263,44 @@ __global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
                 for (int u = 0; u < kIvfWin; ++u) {
                     const int64_t kw = ((int64_t)grp * kIvfWin + u) * 64;
                     if (kw < p.dpad) {
-                        const ivf_bf16x8 b0 = *reinterpret_cast<const ivf_bf16x8 *>(qp + 2 * kw);
-                        const ivf_bf16x8 b1 = *reinterpret_cast<const ivf_bf16x8 *>(qp + 2 * kw + 2 * kOff2);
-                        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[2 * u], b0, acc, 0, 0, 0);
-                        acc = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[2 * u + 1], b1, acc, 0, 0, 0);
+#pragma unroll
+                        for (int j = 0; j < QB; ++j) {
+                            const unsigned char *qj = qp + 16 * j * qstr + 2 * kw;
+                            const ivf_bf16x8 b0 = *reinterpret_cast<const ivf_bf16x8 *>(qj);
+                            const ivf_bf16x8 b1 = *reinterpret_cast<const ivf_bf16x8 *>(qj + 64);
+                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[2 * u], b0, acc[j], 0, 0, 0);
+                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[2 * u + 1], b1, acc[j], 0, 0, 0);
+                        }
                     }
                 }
 #pragma unroll
                 for (int u = 0; u < 2 * kIvfWin; ++u) cur[u] = nxt[u];
             }
-            // C: lane (l16, c) holds rows 4c..4c+3 of the block for query slot l16
-            if (e >= 0) {
-                const int64_t lp = (int64_t)b * 16 + 4 * c;
+            // C: lane (l16, c) holds rows 4c..4c+3 of the block for query slot 16 j + l16
+            const int64_t lp = (int64_t)b * 16 + 4 * c;
+            int32_t rows[4];
+            float pn[4];
+#pragma unroll
+            for (int r = 0; r < 4; ++r) {
+                const int64_t gpos = pos0 + lp + r;
+                int32_t row = p.perm[gpos];
+                if (row >= 0 && p.filter && !bit_test(p.filter, row)) row = -1;
+                if (row >= 0 && p.exists && !bit_test(p.exists, row)) row = -1;
+                rows[r] = row;
+                pn[r] = METRIC == MQVS_METRIC_L2 ? p.pnorm[gpos] : 0.f;
+            }
+#pragma unroll
+            for (int j = 0; j < QB; ++j) {
+                if (ent[j] < 0) continue;
                 Cand out[4];
 #pragma unroll
                 for (int r = 0; r < 4; ++r) {
-                    const int64_t gpos = pos0 + lp + r;
-                    const int32_t row = p.perm[gpos];
-                    bool valid = row >= 0;
-                    if (valid && p.filter) valid = bit_test(p.filter, row);
-                    if (valid && p.exists) valid = bit_test(p.exists, row);
-                    float raw = acc[r];
-                    if (METRIC == MQVS_METRIC_L2) raw = (s_qn[l16] + p.pnorm[gpos]) - 2.0f * raw;
-                    out[r].raw = valid ? raw : __builtin_nanf("");
-                    out[r].row = valid ? (uint32_t)row : 0xFFFFFFFFu;
+                    float raw = acc[j][r];
+                    if (METRIC == MQVS_METRIC_L2) raw = (s_qn[16 * j + l16] + pn[r]) - 2.0f * raw;
+                    out[r].raw = rows[r] >= 0 ? raw : __builtin_nanf("");
+                    out[r].row = rows[r] >= 0 ? (uint32_t)rows[r] : 0xFFFFFFFFu;
                 }
-                uint4 *dst = reinterpret_cast<uint4 *>(p.cand + s_base[l16] + lp);
+                uint4 *dst = reinterpret_cast<uint4 *>(p.cand + s_base[16 * j + l16] + lp);
                 dst[0] = *reinterpret_cast<const uint4 *>(&out[0]);
                 dst[1] = *reinterpret_cast<const uint4 *>(&out[2]);
             }
@@ -246,24 +311,46 @@ __global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
 // Per query: the R best approximate values (ties at the R-th key by position,
 // so the selection is deterministic), sorted by (key, row).  Writes the rows
 // (for the exact re-rank) and, for first-stage-only searches, ids + the
-// approximate distance.
+// approximate distance.  Regions up to `keycap` values keep their keys in
+// LDS for the four radix passes; longer ones stream them (4 in flight).
+
 template <int METRIC>
 __global__ __launch_bounds__(SEL_THREADS) void k_ivf_select(const Cand *cand, const int64_t *qstart, int R,
                                                            int64_t *out_rows, int64_t id_offset,
-                                                           float *out_approx) {
-    extern __shared__ __attribute__((aligned(16))) uint4 recs[];  // pow2 >= R records
+                                                           float *out_approx, int keycap) {
+    extern __shared__ __attribute__((aligned(16))) uint4 recs[];  // pow2 >= R records, then the key cache
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh[4];
     __shared__ int s_wave[SEL_THREADS / 64];
     __shared__ int s_m;
+    int N = 1;
+    while (N < R) N <<= 1;
+    uint32_t *kc = reinterpret_cast<uint32_t *>(recs + N);
     const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const Cand *c = cand + qstart[q];
     const int64_t T = qstart[q + 1] - qstart[q];
-    auto keyof = [&](int64_t i) {
+    auto gkey = [&](int64_t i) {
         const Cand e = c[i];
         return e.row == 0xFFFFFFFFu ? 0xFFFFFFFFu : okey<METRIC>(e.raw);
     };
-    const uint32_t th = block_radix_select(keyof, T, R, hist, sh);
+    const bool cached = T <= keycap;
+    uint32_t th;
+    if (cached) {
+        int64_t i = t;
+        for (; i + 3 * SEL_THREADS < T; i += 4 * SEL_THREADS) {
+            const uint32_t k0 = gkey(i), k1 = gkey(i + SEL_THREADS), k2 = gkey(i + 2 * SEL_THREADS),
+                           k3 = gkey(i + 3 * SEL_THREADS);
+            kc[i] = k0;
+            kc[i + SEL_THREADS] = k1;
+            kc[i + 2 * SEL_THREADS] = k2;
+            kc[i + 3 * SEL_THREADS] = k3;
+        }
+        for (; i < T; i += SEL_THREADS) kc[i] = gkey(i);
+        __syncthreads();
+        th = block_radix_select_mlp([&](int64_t j) { return kc[j]; }, T, R, hist, sh);
+    } else {
+        th = block_radix_select_mlp(gkey, T, R, hist, sh);
+    }
     if (t == 0) s_m = 0;
     __syncthreads();
     for (int pass = 0; pass < 2; ++pass) {
@@ -273,11 +360,9 @@ __global__ __launch_bounds__(SEL_THREADS) void k_ivf_select(const Cand *cand, co
             if (m0 >= R) break;
             const int64_t i = base + t;
             bool flag = false;
-            Cand e{0.f, 0xFFFFFFFFu};
             uint32_t key = 0xFFFFFFFFu;
             if (i < T) {
-                e = c[i];
-                key = e.row == 0xFFFFFFFFu ? 0xFFFFFFFFu : okey<METRIC>(e.raw);
+                key = cached ? kc[i] : gkey(i);
                 if (th == 0xFFFFFFFEu)
                     flag = key != 0xFFFFFFFFu;
                 else
@@ -289,7 +374,10 @@ __global__ __launch_bounds__(SEL_THREADS) void k_ivf_select(const Cand *cand, co
             int off = m0;
             for (int x = 0; x < wv; ++x) off += s_wave[x];
             off += __popcll(bal & ((1ull << lane) - 1ull));
-            if (flag && off < R) recs[off] = make_uint4(key, e.row, __builtin_bit_cast(uint32_t, e.raw), 0u);
+            if (flag && off < R) {
+                const Cand e = c[i];
+                recs[off] = make_uint4(key, e.row, __builtin_bit_cast(uint32_t, e.raw), 0u);
+            }
             __syncthreads();
             if (t == 0) {
                 int tot = 0;
@@ -300,12 +388,12 @@ __global__ __launch_bounds__(SEL_THREADS) void k_ivf_select(const Cand *cand, co
         }
     }
     const int m = s_m;
-    int N = 1;
-    while (N < m) N <<= 1;
-    for (int i = m + t; i < N; i += SEL_THREADS)
+    int Nm = 1;
+    while (Nm < m) Nm <<= 1;
+    for (int i = m + t; i < Nm; i += SEL_THREADS)
         recs[i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
     __syncthreads();
-    block_bitonic_sort(recs, N);
+    block_bitonic_sort(recs, Nm);
     for (int i = t; i < R; i += SEL_THREADS) {
         const bool ok = i < m;
         const uint4 r = ok ? recs[i] : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
@@ -384,6 +472,12 @@ __global__ __launch_bounds__(256) void k_iota_probes(int64_t *probes, int64_t E,
 
 // ---- launchers -------------------------------------------------------------
 
+void launch_ivf_plan_dense(const IvfParams &p, int64_t npos, hipStream_t s) {
+    const int64_t E = (int64_t)p.nq * p.nlist;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((E + 255) / 256, 2048));
+    hipLaunchKernelGGL(k_plan_dense, dim3(grid), dim3(256), 0, s, p, npos);
+}
+
 void launch_iota_probes(int64_t *probes, int nq, int np, hipStream_t s) {
     const int64_t E = (int64_t)nq * np;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((E + 255) / 256, 1024));
@@ -401,56 +495,46 @@ void launch_ivf_plan(const IvfParams &p, hipStream_t s) {
     hipLaunchKernelGGL(k_plan_queries, dim3(1), dim3(kPlanThreads), 0, s, p);
 }
 
-static int ivf_scan_map() {
-    static const int m = [] {
-        const char *e = std::getenv("MQVS_IVF_SCAN_MAP");  // tuning knob (tools/index_sweep.py)
-        return e && e[0] == '0' ? 0 : 1;
-    }();
-    return m;
-}
-
-template <int MAP>
-static void ivf_scan_t(const IvfParams &p, int metric, int grid, size_t lds, hipStream_t s) {
+template <int QB>
+static void ivf_scan_t(const IvfParams &p, int metric, int grid, hipStream_t s) {
+    const size_t lds = (size_t)16 * QB * (2 * p.dpad + 16);
     switch (metric) {
         case MQVS_METRIC_L2:
-            hipLaunchKernelGGL((k_ivf_scan<MQVS_METRIC_L2, MAP>), dim3(grid), dim3(256), lds, s, p);
+            hipLaunchKernelGGL((k_ivf_scan<MQVS_METRIC_L2, QB>), dim3(grid), dim3(256), lds, s, p);
             break;
         case MQVS_METRIC_IP:
-            hipLaunchKernelGGL((k_ivf_scan<MQVS_METRIC_IP, MAP>), dim3(grid), dim3(256), lds, s, p);
+            hipLaunchKernelGGL((k_ivf_scan<MQVS_METRIC_IP, QB>), dim3(grid), dim3(256), lds, s, p);
             break;
         default:
-            hipLaunchKernelGGL((k_ivf_scan<MQVS_METRIC_COSINE, MAP>), dim3(grid), dim3(256), lds, s, p);
+            hipLaunchKernelGGL((k_ivf_scan<MQVS_METRIC_COSINE, QB>), dim3(grid), dim3(256), lds, s, p);
             break;
     }
 }
 
 void launch_ivf_scan(const IvfParams &p, int metric, int grid, hipStream_t s) {
-    const size_t lds = (size_t)kIvfQG * (2 * p.dpad + 16);
-    if (ivf_scan_map() == 0)
-        ivf_scan_t<0>(p, metric, grid, lds, s);
+    if (p.qg == 32)
+        ivf_scan_t<2>(p, metric, grid, s);
     else
-        ivf_scan_t<1>(p, metric, grid, lds, s);
+        ivf_scan_t<1>(p, metric, grid, s);
 }
 
 void launch_ivf_select(const Cand *cand, const int64_t *qstart, int nq, int R, int metric, int64_t *out_rows,
-                       int64_t id_offset, float *out_approx, hipStream_t s) {
+                       int64_t id_offset, float *out_approx, int64_t expect_len, hipStream_t s) {
     int N = 1;
     while (N < R) N <<= 1;
-    const size_t lds = sizeof(uint4) * N;
+    // LDS key cache sized for the expected region length (<= 64 KiB)
+    int keycap = 1024;
+    while (keycap < expect_len && keycap < 16384) keycap <<= 1;
+    const size_t lds = sizeof(uint4) * N + sizeof(uint32_t) * keycap;
+#define MQVS_SEL(M)                                                                                              \
+    hipLaunchKernelGGL(k_ivf_select<M>, dim3(nq), dim3(SEL_THREADS), lds, s, cand, qstart, R, out_rows, id_offset, \
+                       out_approx, keycap)
     switch (metric) {
-        case MQVS_METRIC_L2:
-            hipLaunchKernelGGL(k_ivf_select<MQVS_METRIC_L2>, dim3(nq), dim3(SEL_THREADS), lds, s, cand, qstart, R,
-                               out_rows, id_offset, out_approx);
-            break;
-        case MQVS_METRIC_IP:
-            hipLaunchKernelGGL(k_ivf_select<MQVS_METRIC_IP>, dim3(nq), dim3(SEL_THREADS), lds, s, cand, qstart, R,
-                               out_rows, id_offset, out_approx);
-            break;
-        default:
-            hipLaunchKernelGGL(k_ivf_select<MQVS_METRIC_COSINE>, dim3(nq), dim3(SEL_THREADS), lds, s, cand, qstart,
-                               R, out_rows, id_offset, out_approx);
-            break;
+        case MQVS_METRIC_L2: MQVS_SEL(MQVS_METRIC_L2); break;
+        case MQVS_METRIC_IP: MQVS_SEL(MQVS_METRIC_IP); break;
+        default: MQVS_SEL(MQVS_METRIC_COSINE); break;
     }
+#undef MQVS_SEL
 }
 
 void launch_ivf_pack(const float *rows, const float *norms, int d, const int32_t *perm, int64_t npos, int64_t dpad,

@@ -99,20 +99,24 @@ void launch_normalize_rows(float *rows, int64_t n, int d, hipStream_t s) {
 // chain walks them with v_readlane into the wave-uniform accumulator, so it
 // costs one readlane + one add per element instead of an LDS round trip.
 // J = 0: generic d (elements in LDS, lane 0 walks them).
-// sum_{i<d} x_i^2, sequential fp32 (x_i held by lane i % 64, slot i / 64)
+// sum_{i<d} x_i^2, sequential fp32 (x_i held by lane i % 64, slot i / 64).
+// Padding elements (i >= d) hold 0 and add +0.0f, which leaves the
+// non-negative running sum bit-identical, so every slot walks all 64 lanes
+// without branches; readlanes go 16 at a time ahead of their adds.
 template <int J>
 __device__ __forceinline__ float seq_sq_sum(const float (&x)[J], int d) {
+    (void)d;
     float acc = 0.0f;
 #pragma unroll
     for (int u = 0; u < J; ++u) {
         const int sq = __builtin_bit_cast(int, x[u] * x[u]);
-        if (64 * u + 64 <= d) {
 #pragma unroll
-            for (int l = 0; l < 64; ++l) acc = acc + __builtin_bit_cast(float, __builtin_amdgcn_readlane(sq, l));
-        } else {
+        for (int l0 = 0; l0 < 64; l0 += 16) {
+            float t[16];
 #pragma unroll
-            for (int l = 0; l < 64; ++l)
-                if (64 * u + l < d) acc = acc + __builtin_bit_cast(float, __builtin_amdgcn_readlane(sq, l));
+            for (int l = 0; l < 16; ++l) t[l] = __builtin_bit_cast(float, __builtin_amdgcn_readlane(sq, l0 + l));
+#pragma unroll
+            for (int l = 0; l < 16; ++l) acc = acc + t[l];
         }
     }
     return acc;

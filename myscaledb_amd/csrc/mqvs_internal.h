@@ -294,7 +294,6 @@ void launch_rerank_select(const ScanParams &p, int metric, const float *bq, int 
 
 // ---------------------------------------------------------------------------
 // Index path (kernels_ivf.hip, index.hip)
-constexpr int kIvfQG = 16;   // queries per scan work item (one MFMA B block)
 constexpr int kIvfPad = 16;  // list lengths padded to this many positions
 
 struct IvfParams {
@@ -305,6 +304,7 @@ struct IvfParams {
     int nlist;
     int64_t dpad;
     int nq, nprobe;
+    int qg;                   // queries per scan work item: 16 or 32 (MFMA B blocks x 16)
     const int64_t *probes;    // [nq][nprobe] list ids (-1 = none)
     const uint16_t *q_hi;     // [nq][dpad] bf16 query (cosine: normalised)
     const float *qnorm;       // [nq] |q|^2 (L2)
@@ -315,7 +315,8 @@ struct IvfParams {
     int64_t *lstart;          // [nlist] first pair of each list in lq
     int *lq;                  // [nq*nprobe] pairs (q*nprobe + probe) grouped by list
     int *item_list;           // [nq*nprobe] work item -> list
-    int *item_grp;            // work item -> 16-query group within the list
+    int *item_grp;            // work item -> query group within the list
+    int *item_chk;            // work item -> slice of the list
     int *nitems;              // number of work items
     int64_t *qbase;           // [nq*nprobe] start of each pair's region in cand
     int64_t *qstart;          // [nq+1] start of each query's region
@@ -325,9 +326,11 @@ struct IvfParams {
 
 void launch_ivf_plan(const IvfParams &p, hipStream_t s);
 void launch_iota_probes(int64_t *probes, int nq, int np, hipStream_t s);
+void launch_ivf_plan_dense(const IvfParams &p, int64_t npos, hipStream_t s);
 void launch_ivf_scan(const IvfParams &p, int metric, int grid, hipStream_t s);
+// expect_len: typical per-query region length (sizes the LDS key cache)
 void launch_ivf_select(const Cand *cand, const int64_t *qstart, int nq, int R, int metric, int64_t *out_rows,
-                       int64_t id_offset, float *out_approx, hipStream_t s);
+                       int64_t id_offset, float *out_approx, int64_t expect_len, hipStream_t s);
 void launch_ivf_pack(const float *rows, const float *norms, int d, const int32_t *perm, int64_t npos, int64_t dpad,
                      uint16_t *plane, float *pnorm, hipStream_t s);
 void launch_gather_rows(const float *src, int64_t src_ld, int d, const int64_t *idx, int64_t m, float *dst,

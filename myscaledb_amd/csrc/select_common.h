@@ -81,6 +81,89 @@ __device__ inline uint32_t block_radix_select(KeyFn keyof, int64_t count, int k,
     return prefix;
 }
 
+// Bucket holding the kk-th smallest key (1-based) of a 256-bucket histogram,
+// found by wave 0 in parallel (4 buckets per lane + a lane prefix sum).
+// Writes sh[0] = done (total < kk on the first pass), sh[1] = bucket,
+// sh[2] = count below the bucket.  Caller syncs before and after.
+__device__ inline void hist_pick(const uint32_t *hist, uint32_t kk, bool first, uint32_t *sh) {
+    if (threadIdx.x >= 64) return;
+    const int lane = threadIdx.x;
+    const uint32_t h0 = hist[4 * lane], h1 = hist[4 * lane + 1], h2 = hist[4 * lane + 2], h3 = hist[4 * lane + 3];
+    const uint32_t mine = h0 + h1 + h2 + h3;
+    uint32_t inc = mine;
+    for (int off = 1; off < 64; off <<= 1) {
+        const uint32_t y = __shfl_up(inc, off);
+        if (lane >= off) inc += y;
+    }
+    const uint32_t total = __shfl(inc, 63);
+    const uint32_t before = inc - mine;
+    if (first && total < kk) {
+        if (lane == 0) {
+            sh[0] = 1;
+            sh[1] = 0;
+            sh[2] = 0;
+        }
+        return;
+    }
+    // the first lane whose inclusive count reaches kk holds the bucket
+    const uint64_t hit = __ballot(inc >= kk);
+    const int L = __ffsll((long long)hit) - 1;
+    if (lane == L) {
+        uint32_t cum = before, b = 4 * lane;
+        const uint32_t hs[4] = {h0, h1, h2, h3};
+        for (int j = 0; j < 4; ++j) {
+            if (cum + hs[j] >= kk) {
+                b = 4 * lane + j;
+                break;
+            }
+            cum += hs[j];
+        }
+        sh[0] = 0;
+        sh[1] = b;
+        sh[2] = cum;
+    }
+}
+
+// block_radix_select with the bucket search in parallel and 4 keys in
+// flight per thread (keyof(i) may read global memory).
+template <typename KeyFn>
+__device__ inline uint32_t block_radix_select_mlp(KeyFn keyof, int64_t count, int k, uint32_t *hist, uint32_t *sh) {
+    const int t = threadIdx.x;
+    uint32_t prefix = 0, mask = 0, kk = (uint32_t)k;
+    for (int pass = 0; pass < 4; ++pass) {
+        const int shift = 24 - 8 * pass;
+        for (int i = t; i < 256; i += SEL_THREADS) hist[i] = 0;
+        __syncthreads();
+        RunHist rh;
+        int64_t i = t;
+        for (; i + 3 * SEL_THREADS < count; i += 4 * SEL_THREADS) {
+            const uint32_t k0 = keyof(i), k1 = keyof(i + SEL_THREADS), k2 = keyof(i + 2 * SEL_THREADS),
+                           k3 = keyof(i + 3 * SEL_THREADS);
+            if (k0 != 0xFFFFFFFFu && (k0 & mask) == prefix) rh.add(hist, (k0 >> shift) & 255u);
+            if (k1 != 0xFFFFFFFFu && (k1 & mask) == prefix) rh.add(hist, (k1 >> shift) & 255u);
+            if (k2 != 0xFFFFFFFFu && (k2 & mask) == prefix) rh.add(hist, (k2 >> shift) & 255u);
+            if (k3 != 0xFFFFFFFFu && (k3 & mask) == prefix) rh.add(hist, (k3 >> shift) & 255u);
+        }
+        for (; i < count; i += SEL_THREADS) {
+            const uint32_t key = keyof(i);
+            if (key != 0xFFFFFFFFu && (key & mask) == prefix) rh.add(hist, (key >> shift) & 255u);
+        }
+        rh.flush(hist);
+        __syncthreads();
+        hist_pick(hist, kk, pass == 0, sh);
+        __syncthreads();
+        if (sh[0]) {
+            __syncthreads();
+            return 0xFFFFFFFEu;
+        }
+        prefix |= sh[1] << shift;
+        mask |= 255u << shift;
+        kk -= sh[2];
+        __syncthreads();
+    }
+    return prefix;
+}
+
 // Visit every element of a float row: float4 loads, 4 in flight per thread
 // (the probe rows are megabytes; a scalar loop leaves HBM idle).
 template <typename F>
