@@ -646,3 +646,232 @@ void orc_generate(uint64_t seed, int mode, int64_t row0, int64_t n, int64_t d,
         }
     }
 }
+
+/* ------------------------------------------------------------------------ */
+/* Binary vectors (FixedString(N) columns): tryBruteForceSearch<BinaryVector>
+ * (BruteForceSearch.h:94-110).  The two callees live in the absent faiss fork
+ * (contrib/search-index), so they are restated from upstream faiss
+ * (utils/hamming.cpp, hammings_knn_mc; unpinned version) and from the
+ * reference's own KAT 00038_mqvs_binary_vector_feature for jaccard_knn. */
+
+static inline int popc8(uint8_t v) { return __builtin_popcount((unsigned)v); }
+
+/* faiss::hammings_knn_mc with HCounterState: per query, counters[d] and up to
+ * k ids per distance in arrival order (j ascending).  update_counter:
+ *   dis <= thres:  dis < thres -> store, ++count_lt, and while count_lt == k
+ *                  lower thres (count_eq = counters[thres], count_lt -= it);
+ *                  dis == thres -> store only while count_eq < k.
+ * Output: distances b = 0 .. nBit-1 (b < nBit: a row whose every bit differs
+ * is never returned), k per query, padding -1 / INT32_MAX. */
+int orc_hamming_knn(const uint8_t *x, const uint8_t *y, int64_t nbytes, int64_t k,
+                    int64_t nx, int64_t ny, int64_t *ids, int32_t *dist) {
+    const int nbit = (int)(nbytes * 8);
+    int *counters = (int *)malloc(sizeof(int) * (nbit + 1));
+    int64_t *per = (int64_t *)malloc(sizeof(int64_t) * (size_t)(nbit + 1) * (size_t)(k > 0 ? k : 1));
+    for (int64_t i = 0; i < nx; i++) {
+        memset(counters, 0, sizeof(int) * (nbit + 1));
+        int thres = nbit + 1, count_lt = 0, count_eq = 0;
+        const uint8_t *xi = x + i * nbytes;
+        for (int64_t j = 0; j < ny; j++) {
+            const uint8_t *yj = y + j * nbytes;
+            int dis = 0;
+            for (int64_t b = 0; b < nbytes; b++) dis += popc8(xi[b] ^ yj[b]);
+            if (dis > thres) continue;
+            if (dis < thres) {
+                per[(int64_t)dis * k + counters[dis]++] = j;
+                ++count_lt;
+                while (count_lt == k && thres > 0) {
+                    --thres;
+                    count_eq = counters[thres];
+                    count_lt -= count_eq;
+                }
+            } else if (count_eq < k) {
+                per[(int64_t)dis * k + count_eq++] = j;
+                counters[dis] = count_eq;
+            }
+        }
+        int64_t nres = 0;
+        for (int b = 0; b < nbit && nres < k; b++)
+            for (int l = 0; l < counters[b] && nres < k; l++) {
+                ids[i * k + nres] = per[(int64_t)b * k + l];
+                dist[i * k + nres] = b;
+                nres++;
+            }
+        for (; nres < k; nres++) {
+            ids[i * k + nres] = -1;
+            dist[i * k + nres] = 2147483647;
+        }
+    }
+    free(counters);
+    free(per);
+    return 0;
+}
+
+/* Jaccard distance of two codes.  The reference's KAT 00038 pins the fp32
+ * form (den - num) / den (1 - num/den misses 0.2 and 0.22222222 by an ulp);
+ * num == 0 -> 1.0 (assumed; equal to the formula unless both codes are 0). */
+float orc_jaccard(const uint8_t *a, const uint8_t *b, int64_t nbytes) {
+    int num = 0, den = 0;
+    for (int64_t i = 0; i < nbytes; i++) {
+        num += popc8(a[i] & b[i]);
+        den += popc8(a[i] | b[i]);
+    }
+    if (num == 0) return 1.0f;
+    return (float)(den - num) / (float)den;
+}
+
+/* jaccard_knn (faiss fork, absent): a max-heap of k entries that a row enters
+ * only when strictly better than the current worst; output ordered by
+ * (distance, row).  Equivalently: the k smallest by (distance, row). */
+int orc_jaccard_knn(const uint8_t *x, const uint8_t *y, int64_t nbytes, int64_t k,
+                    int64_t nx, int64_t ny, int64_t *ids, float *dist) {
+    float *val = (float *)malloc(sizeof(float) * (size_t)(k > 0 ? k : 1));
+    int64_t *lab = (int64_t *)malloc(sizeof(int64_t) * (size_t)(k > 0 ? k : 1));
+    for (int64_t i = 0; i < nx; i++) {
+        for (int64_t j = 0; j < k; j++) {
+            val[j] = FLT_MAX;
+            lab[j] = -1;
+        }
+        heap_heapify(1, k, val, lab);
+        for (int64_t j = 0; j < ny; j++) {
+            const float dis = orc_jaccard(x + i * nbytes, y + j * nbytes, nbytes);
+            if (dis < val[0]) heap_replace_top(1, k, val, lab, dis, j);
+        }
+        heap_reorder(1, k, val, lab);
+        memcpy(dist + i * k, val, sizeof(float) * k);
+        memcpy(ids + i * k, lab, sizeof(int64_t) * k);
+    }
+    free(val);
+    free(lab);
+    return 0;
+}
+
+/* tryBruteForceSearch<BinaryVector>: d in bits.  Hamming writes int32 counts
+ * into the float buffer (the reference's reinterpret_cast<int32_t*>). */
+int orc_knn_binary(const uint8_t *x, const uint8_t *y, int64_t d, int64_t k, int64_t nx,
+                   int64_t ny, int metric, int64_t *ids, float *dist) {
+    if (metric == ORC_HAMMING) return orc_hamming_knn(x, y, d / 8, k, nx, ny, ids, (int32_t *)dist);
+    if (metric == ORC_JACCARD) return orc_jaccard_knn(x, y, d / 8, k, nx, ny, ids, dist);
+    return -1;
+}
+
+/* searchWrapper (MergeTreeVSManager.cpp:1538-1680) for binary chunks: per
+ * chunk k + deleted results, drop deleted rows, PREWHERE id remap, strict
+ * two-pointer merge (ascending).  Hamming's int32 counts are compared by the
+ * reference as the float bit patterns (positive denormals, same order as the
+ * integers; INT32_MAX padding is NaN and never enters); here they are
+ * converted to the float values the SQL prints (KAT 00038). */
+static void search_wrapper_binary(int prewhere, const uint8_t *query, int64_t nq,
+                                  const uint8_t *base, int64_t nbase, int64_t nbytes, int64_t k,
+                                  int64_t num_rows_read, int64_t *final_id, float *final_dist,
+                                  const int64_t *actual, int metric, const uint8_t *exists_chunk,
+                                  int64_t del) {
+    const int64_t kk = k + del;
+    int64_t *tid = (int64_t *)malloc(sizeof(int64_t) * kk * nq);
+    float *tdist = (float *)malloc(sizeof(float) * kk * nq);
+    int64_t *per_id = (int64_t *)malloc(sizeof(int64_t) * k * nq);
+    float *per_dist = (float *)malloc(sizeof(float) * k * nq);
+    for (int64_t i = 0; i < k * nq; i++) {
+        per_id[i] = -1;
+        per_dist[i] = FLT_MAX;
+    }
+    if (metric == ORC_HAMMING) {
+        int32_t *hd = (int32_t *)malloc(sizeof(int32_t) * kk * nq);
+        orc_hamming_knn(query, base, nbytes, kk, nq, nbase, tid, hd);
+        for (int64_t i = 0; i < kk * nq; i++) tdist[i] = tid[i] >= 0 ? (float)hd[i] : FLT_MAX;
+        free(hd);
+    } else {
+        orc_jaccard_knn(query, base, nbytes, kk, nq, nbase, tid, tdist);
+    }
+    for (int64_t q = 0; q < nq; q++) {
+        int64_t cur = 0;
+        for (int64_t t = 0; t < kk && cur < k; t++) {
+            const int64_t id = tid[q * kk + t];
+            if (id < 0) continue;
+            if (exists_chunk && !bit_test(exists_chunk, id)) continue;
+            per_id[q * k + cur] = prewhere ? actual[id] : id;
+            per_dist[q * k + cur] = tdist[q * kk + t];
+            cur++;
+        }
+    }
+    float *inter_d = (float *)malloc(sizeof(float) * k * nq);
+    int64_t *inter_i = (int64_t *)malloc(sizeof(int64_t) * k * nq);
+    for (int64_t q = 0; q < nq; q++) {
+        int64_t j = q * k, z = q * k;
+        for (int64_t i = 0; i < k; i++) {
+            if (final_dist[j] > per_dist[z]) {
+                inter_d[q * k + i] = per_dist[z];
+                inter_i[q * k + i] = per_id[z] + num_rows_read;
+                z++;
+            } else {
+                inter_d[q * k + i] = final_dist[j];
+                inter_i[q * k + i] = final_id[j];
+                j++;
+            }
+        }
+    }
+    memcpy(final_dist, inter_d, sizeof(float) * k * nq);
+    memcpy(final_id, inter_i, sizeof(int64_t) * k * nq);
+    free(inter_d);
+    free(inter_i);
+    free(tid);
+    free(tdist);
+    free(per_id);
+    free(per_dist);
+}
+
+/* vectorScanWithoutIndex<BinaryVector> (MergeTreeVSManager.cpp:1188-1273
+ * filtered gather of FixedString rows, :1395-1425 whole-chunk copy): codes
+ * n x nbytes; same chunking, filter and delete handling as the float path. */
+int orc_vector_scan_binary(const uint8_t *rows, int64_t n, int64_t nbytes,
+                           const int64_t *mark_rows, int64_t n_marks, const uint8_t *queries,
+                           int64_t nq, int64_t k, int metric, const uint8_t *filter,
+                           const uint8_t *row_exists, int64_t *out_ids, float *out_dist) {
+    if (metric != ORC_HAMMING && metric != ORC_JACCARD) return -1;
+    for (int64_t i = 0; i < k * nq; i++) {
+        out_dist[i] = FLT_MAX;
+        out_ids[i] = -1;
+    }
+    if (n == 0 || nq == 0 || k <= 0) return 0;
+    if (filter) {
+        int64_t parsed = 0;
+        uint8_t *chunk = NULL;
+        int64_t *actual = NULL;
+        for (int64_t m = 0; m < n_marks && parsed < n; m++) {
+            int64_t rows_m = mark_rows[m];
+            if (parsed + rows_m > n) rows_m = n - parsed;
+            chunk = (uint8_t *)realloc(chunk, (size_t)(rows_m > 0 ? rows_m : 1) * nbytes);
+            actual = (int64_t *)realloc(actual, sizeof(int64_t) * (rows_m > 0 ? rows_m : 1));
+            int64_t left = 0;
+            for (int64_t i = parsed; i < parsed + rows_m; i++)
+                if (bit_test(filter, i) && (!row_exists || bit_test(row_exists, i))) {
+                    memcpy(chunk + left * nbytes, rows + i * nbytes, nbytes);
+                    actual[left++] = i;
+                }
+            parsed += rows_m;
+            if (left == 0) continue;
+            search_wrapper_binary(1, queries, nq, chunk, left, nbytes, k, 0, out_ids, out_dist, actual,
+                                  metric, NULL, 0);
+        }
+        free(chunk);
+        free(actual);
+    } else {
+        const int64_t chunk_rows = n_marks > 0 && mark_rows[0] > 0 ? mark_rows[0] : n;
+        uint8_t *exists = (uint8_t *)malloc((size_t)(chunk_rows + 7) / 8);
+        for (int64_t r0 = 0; r0 < n; r0 += chunk_rows) {
+            const int64_t rows_c = (n - r0) < chunk_rows ? (n - r0) : chunk_rows;
+            int64_t del = 0;
+            memset(exists, 0xff, (size_t)(rows_c + 7) / 8);
+            if (row_exists)
+                for (int64_t r = 0; r < rows_c; r++)
+                    if (!bit_test(row_exists, r0 + r)) {
+                        exists[r >> 3] &= (uint8_t)~(1u << (r & 7));
+                        del++;
+                    }
+            search_wrapper_binary(0, queries, nq, rows + r0 * nbytes, rows_c, nbytes, k, r0, out_ids,
+                                  out_dist, NULL, metric, del ? exists : NULL, del);
+        }
+        free(exists);
+    }
+    return 0;
+}

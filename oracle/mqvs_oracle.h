@@ -31,7 +31,7 @@
 extern "C" {
 #endif
 
-enum { ORC_L2 = 0, ORC_IP = 1, ORC_COSINE = 2 };
+enum { ORC_L2 = 0, ORC_IP = 1, ORC_COSINE = 2, ORC_HAMMING = 4, ORC_JACCARD = 5 };
 
 /* faiss distance_compute_blas_threshold */
 #define ORC_BLAS_THRESHOLD 20
@@ -110,6 +110,29 @@ void orc_merge_parts(int64_t nparts, int64_t k, int metric,
  * mode 1 = approx N(0,1) (Irwin-Hall of 4), mode 2 = Gaussian mixture. */
 void orc_generate(uint64_t seed, int mode, int64_t row0, int64_t n, int64_t d,
                   float *out);
+
+/* ---- binary vectors (FixedString(N)), BruteForceSearch.h:94-110 ----------
+ * faiss::hammings_knn_mc restated (upstream faiss utils/hamming.cpp, version
+ * unpinned): k nearest by (distance, row), distances < d bits only, int32
+ * counts, padding -1 / INT32_MAX. */
+int orc_hamming_knn(const uint8_t *x, const uint8_t *y, int64_t nbytes, int64_t k,
+                    int64_t nx, int64_t ny, int64_t *ids, int32_t *dist);
+/* Jaccard distance, fp32 (den - num) / den, 1.0 when the codes share no bit
+ * (pinned by KAT 00038). */
+float orc_jaccard(const uint8_t *a, const uint8_t *b, int64_t nbytes);
+/* jaccard_knn (absent faiss fork): k smallest by (distance, row); -1/FLT_MAX pad. */
+int orc_jaccard_knn(const uint8_t *x, const uint8_t *y, int64_t nbytes, int64_t k,
+                    int64_t nx, int64_t ny, int64_t *ids, float *dist);
+/* tryBruteForceSearch<BinaryVector>: d in bits; Hamming distances are int32
+ * stored in the float buffer; other metrics -> -1 (NOT_IMPLEMENTED). */
+int orc_knn_binary(const uint8_t *x, const uint8_t *y, int64_t d, int64_t k, int64_t nx,
+                   int64_t ny, int metric, int64_t *ids, float *dist);
+/* vectorScanWithoutIndex<BinaryVector> over one part (codes n x nbytes);
+ * Hamming distances as float values, ascending; -1 / FLT_MAX padding. */
+int orc_vector_scan_binary(const uint8_t *rows, int64_t n, int64_t nbytes,
+                           const int64_t *mark_rows, int64_t n_marks, const uint8_t *queries,
+                           int64_t nq, int64_t k, int metric, const uint8_t *filter,
+                           const uint8_t *row_exists, int64_t *out_ids, float *out_dist);
 
 #ifdef __cplusplus
 }

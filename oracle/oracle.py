@@ -15,8 +15,8 @@ import numpy as np
 _HERE = os.path.dirname(os.path.abspath(__file__))
 _LIB_PATH = os.path.join(_HERE, "_build", "libmqvs_oracle.so")
 
-L2, IP, COSINE = 0, 1, 2
-METRICS = {"L2": L2, "IP": IP, "Cosine": COSINE, "COSINE": COSINE}
+L2, IP, COSINE, HAMMING, JACCARD = 0, 1, 2, 4, 5
+METRICS = {"L2": L2, "IP": IP, "Cosine": COSINE, "COSINE": COSINE, "Hamming": HAMMING, "Jaccard": JACCARD}
 
 _lib = None
 
@@ -46,6 +46,12 @@ def lib():
         L.orc_scan_parts.argtypes = [P, I64, I64, I64, P, I64, I64, ctypes.c_int, ctypes.c_int,
                                      ctypes.c_int, P, P]
         L.orc_merge_parts.argtypes = [I64, I64, ctypes.c_int, P, P, P, P, P]
+        L.orc_hamming_knn.argtypes = [P, P, I64, I64, I64, I64, P, P]
+        L.orc_jaccard_knn.argtypes = [P, P, I64, I64, I64, I64, P, P]
+        L.orc_jaccard.argtypes = [P, P, I64]
+        L.orc_jaccard.restype = ctypes.c_float
+        L.orc_knn_binary.argtypes = [P, P, I64, I64, I64, I64, ctypes.c_int, P, P]
+        L.orc_vector_scan_binary.argtypes = [P, I64, I64, P, I64, P, I64, I64, ctypes.c_int, P, P, P, P]
         L.orc_generate.argtypes = [ctypes.c_uint64, ctypes.c_int, I64, I64, I64, P]
         L.orc_gemm_dot.argtypes = [P, P, I64]
         L.orc_gemm_dot.restype = ctypes.c_float
@@ -127,6 +133,44 @@ def vector_scan(rows, queries, k, metric, mark_rows, nonempty=None, filter_bits=
     rc = fn(_p(rows), _p(ne), n, d, _p(mr), len(mr), _p(queries), nq, k, metric, _p(fb), _p(rb),
             _p(ids), _p(dist))
     if rc:
+        raise NotImplementedError
+    return ids, dist
+
+
+def _u8(a):
+    return np.ascontiguousarray(a, np.uint8)
+
+
+def knn_binary(x, y, k, metric):
+    """tryBruteForceSearch<BinaryVector> (BruteForceSearch.h:94-110) on code
+    arrays x (nx, N) and y (ny, N) uint8.  Hamming: int32 distances (the
+    reference's reinterpret of the float buffer); Jaccard: float32."""
+    x, y = _u8(x), _u8(y)
+    nx, nb = x.shape
+    ny = y.shape[0]
+    ids = np.empty((nx, k), np.int64)
+    dist = np.empty((nx, k), np.int32 if metric == HAMMING else np.float32)
+    if lib().orc_knn_binary(_p(x), _p(y), nb * 8, k, nx, ny, metric, _p(ids), _p(dist)):
+        raise NotImplementedError
+    return ids, dist
+
+
+def vector_scan_binary(codes, queries, k, metric, mark_rows, filter_bits=None, row_exists_bits=None):
+    """vectorScanWithoutIndex<BinaryVector> over one part: codes (n, N) uint8
+    (FixedString(N)); returns ids (nq, k) and float32 distances."""
+    codes, queries = _u8(codes), _u8(queries)
+    n, nb = codes.shape
+    nq = queries.shape[0]
+    if np.isscalar(mark_rows):
+        mr = np.full(max(1, -(-n // int(mark_rows))), int(mark_rows), np.int64)
+    else:
+        mr = np.ascontiguousarray(mark_rows, np.int64)
+    fb = None if filter_bits is None else _u8(filter_bits)
+    rb = None if row_exists_bits is None else _u8(row_exists_bits)
+    ids = np.empty((nq, k), np.int64)
+    dist = np.empty((nq, k), np.float32)
+    if lib().orc_vector_scan_binary(_p(codes), n, nb, _p(mr), len(mr), _p(queries), nq, k, metric, _p(fb),
+                                    _p(rb), _p(ids), _p(dist)):
         raise NotImplementedError
     return ids, dist
 

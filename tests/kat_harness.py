@@ -92,3 +92,50 @@ def check_case(case, search_fn):
         else:
             assert g[0] == e[0], f"{case['name']}: got {g}, expected {e}"
             assert g[1] == np.float32(e[1]), f"{case['name']}: got {g} ({g[1]!r}), expected {e}"
+
+
+# ---- binary vectors (KAT 00038, tests/golden/binary_kats.json) -------------
+
+def load_binary_cases():
+    with open(os.path.join(_HERE, "golden", "binary_kats.json")) as f:
+        return json.load(f)["cases"]
+
+
+def build_binary_table(table):
+    n = table["n"]
+    ids = np.arange(n, dtype=np.int64)
+    codes = np.repeat((ids % 256).astype(np.uint8)[:, None], 4, axis=1)  # char(n, n, n, n)
+    return ids, codes
+
+
+def run_binary_case(case, search_fn):
+    """search_fn(codes, granularity, queries_u8, k, metric_name, filter_bits,
+    row_exists_bits) -> (ids[nq,k], dist[nq,k] float32): one part's
+    vectorScanWithoutIndex<BinaryVector>; the SQL ORDER BY ... LIMIT is applied
+    here (one part)."""
+    ids, codes = build_binary_table(case["table"])
+    queries = np.array(case["queries"], np.uint8)
+    k = case["k"]
+    flt = bits(np.isin(ids, np.array(case["prewhere_ids"], np.int64))) if "prewhere_ids" in case else None
+    rex = bits(~np.isin(ids, np.array(case["deleted_ids"], np.int64))) if "deleted_ids" in case else None
+    out_ids, out_dist = search_fn(codes, case["table"]["granularity"], queries, k, case["metric"], flt, rex)
+    out_ids, out_dist = np.asarray(out_ids), np.asarray(out_dist)
+    res = []
+    for qi in range(len(queries)):
+        rq = [(int(ids[out_ids[qi, j]]), qi, np.float32(out_dist[qi, j])) for j in range(k) if out_ids[qi, j] >= 0]
+        rq.sort(key=lambda r: (r[2], r[0]))
+        res.extend(rq[:k])
+    if case.get("batch"):
+        return res
+    return [(r[0], r[2]) for r in res]
+
+
+def check_binary_case(case, search_fn):
+    got = run_binary_case(case, search_fn)
+    exp = case["expect"]
+    assert len(got) == len(exp), f"{case['name']}: {len(got)} rows, expected {len(exp)}"
+    for g, e in zip(got, exp):
+        if case.get("batch"):
+            assert (g[0], g[1]) == (e[0], e[1]) and g[2] == np.float32(e[2]), f"{case['name']}: got {g}, expected {e}"
+        else:
+            assert g[0] == e[0] and g[1] == np.float32(e[1]), f"{case['name']}: got {g} ({g[1]!r}), expected {e}"
