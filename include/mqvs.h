@@ -42,11 +42,14 @@ extern "C" {
 
 #define MQVS_ABI_VERSION 1
 
-/* Metric ids (VICommon.h VIMetric; float vectors only in this version). */
+/* Metric ids (VICommon.h VIMetric).  L2 / IP / Cosine: Float32 vectors;
+ * Hamming / Jaccard: binary vectors (FixedString(N) columns, mqvs_*_binary). */
 enum {
-    MQVS_METRIC_L2 = 0,     /* squared L2, ascending */
-    MQVS_METRIC_IP = 1,     /* inner product, descending */
-    MQVS_METRIC_COSINE = 2  /* 1 - <q/|q|, y/|y|>, ascending */
+    MQVS_METRIC_L2 = 0,      /* squared L2, ascending */
+    MQVS_METRIC_IP = 1,      /* inner product, descending */
+    MQVS_METRIC_COSINE = 2,  /* 1 - <q/|q|, y/|y|>, ascending */
+    MQVS_METRIC_HAMMING = 4, /* popcount(q ^ y), ascending (value 3 is internal) */
+    MQVS_METRIC_JACCARD = 5  /* (|q|y| - |q&y|) / |q|y| in fp32, ascending */
 };
 
 /* Status codes; each maps 1:1 onto the DB::ErrorCodes the reference throws. */
@@ -165,6 +168,33 @@ int mqvs_rerank(mqvs_segment_t seg, const float *queries, int32_t nq, const int6
 int mqvs_merge_shards(int32_t nshards, int32_t nq, int32_t k, int32_t metric,
                       const int64_t *in_ids, const float *in_dist, int64_t *out_ids,
                       float *out_dist, uint32_t flags, mqvs_stream_t stream);
+
+/* ---- binary vectors: FixedString(N) columns, Hamming / Jaccard ----------
+ * tryBruteForceSearch<BinaryVector> (BruteForceSearch.h:94-110) over
+ * vectorScanWithoutIndex<BinaryVector> (MergeTreeVSManager.cpp:1188-1273,
+ * 1395-1425).  Codes are n rows x dim_bits/8 bytes (the FixedString bytes).
+ *
+ * mqvs_segment_create_binary: register a part's binary column (host codes, or
+ * device codes with MQVS_F_DEVICE_PTRS in flags); metric is the column's
+ * default (Hamming or Jaccard; a search may use either).
+ * mqvs_search_binary: mqvs_search for binary segments -- queries nq x N bytes;
+ * output ascending by (distance, row), Hamming distances as float values
+ * (KAT 00038 prints 4, 8, ...), -1 / FLT_MAX padding.  Rows at Hamming
+ * distance == dim_bits are never returned (hammings_knn_mc emits b < nBit).
+ * mqvs_knn_binary_raw: the tryBruteForceSearch<BinaryVector> contract itself
+ * (host pointers, one pass): Hamming writes int32 counts into `distance`
+ * (reinterpret as int32_t*, padding -1 / INT32_MAX, faiss::hammings_knn_mc);
+ * Jaccard writes floats (padding -1 / FLT_MAX).  Float metrics ->
+ * MQVS_ERR_NOT_IMPLEMENTED ("Metric not implemented in brute force search
+ * for Binary Vector"), as BruteForceSearch.h:107. */
+int mqvs_segment_create_binary(const uint8_t *codes, int64_t n, int32_t dim_bits, int32_t metric,
+                               int64_t granule_rows, int64_t row_offset, uint32_t flags,
+                               mqvs_segment_t *out);
+int mqvs_search_binary(mqvs_segment_t seg, const uint8_t *queries, int32_t nq, int32_t k, int32_t metric,
+                       const uint8_t *filter, const uint8_t *row_exists, int64_t *out_ids, float *out_dist,
+                       uint32_t flags, mqvs_stream_t stream);
+int mqvs_knn_binary_raw(const uint8_t *x, const uint8_t *y, int64_t d, int64_t k, int64_t nx, int64_t ny,
+                        int32_t metric, int64_t *result_id, float *distance);
 
 /* Fill a device buffer with generator rows [row0, row0+n) (for queries). */
 int mqvs_generate_device(uint64_t seed, int32_t mode, int64_t row0, int64_t n, int32_t d,

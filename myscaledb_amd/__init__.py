@@ -7,14 +7,16 @@ operator surface (vector_scan) plus the multi-GPU row-range sharding
 """
 from . import _lib  # noqa: F401  (loads libmqvs.so, raises if absent)
 from .vector_scan import (  # noqa: F401
+    BinaryVectorScanSegment,
     VectorScanSegment,
     init,
     merge_shards,
     pack_bitmap,
     try_brute_force_search,
+    try_brute_force_search_binary,
     vector_scan_without_index,
 )
 from .vector_index import VectorIndex  # noqa: F401
 
-__all__ = ["VectorScanSegment", "init", "merge_shards", "pack_bitmap",
+__all__ = ["BinaryVectorScanSegment", "try_brute_force_search_binary", "VectorScanSegment", "init", "merge_shards", "pack_bitmap",
            "try_brute_force_search", "vector_scan_without_index", "VectorIndex"]

@@ -13,9 +13,11 @@ _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libmqvs.so")
 
 # include/mqvs.h
-METRIC_L2, METRIC_IP, METRIC_COSINE = 0, 1, 2
+METRIC_L2, METRIC_IP, METRIC_COSINE, METRIC_HAMMING, METRIC_JACCARD = 0, 1, 2, 4, 5
 METRICS = {"L2": METRIC_L2, "IP": METRIC_IP, "COSINE": METRIC_COSINE, "Cosine": METRIC_COSINE,
-           "cosine": METRIC_COSINE, "l2": METRIC_L2, "ip": METRIC_IP}
+           "cosine": METRIC_COSINE, "l2": METRIC_L2, "ip": METRIC_IP,
+           "Hamming": METRIC_HAMMING, "HAMMING": METRIC_HAMMING, "hamming": METRIC_HAMMING,
+           "Jaccard": METRIC_JACCARD, "JACCARD": METRIC_JACCARD, "jaccard": METRIC_JACCARD}
 OK = 0
 ERR_NOT_IMPLEMENTED, ERR_LOGICAL, ERR_ILLEGAL_COLUMN, ERR_BAD_ARGUMENTS, ERR_MEMORY_LIMIT, \
     ERR_DEVICE = 1, 2, 3, 4, 5, 6
@@ -32,6 +34,7 @@ SYMBOLS = [
     "mqvs_search", "mqvs_search_ex", "mqvs_knn_raw", "mqvs_rerank", "mqvs_merge_shards", "mqvs_generate_device",
     "mqvs_last_search_stats", "mqvs_set_timing", "mqvs_set_batch_mode", "mqvs_set_gather_mode", "mqvs_set_prefilter",
     "mqvs_index_build", "mqvs_index_free", "mqvs_index_info", "mqvs_index_search", "mqvs_index_last_stats",
+    "mqvs_segment_create_binary", "mqvs_search_binary", "mqvs_knn_binary_raw",
 ]
 
 
@@ -112,6 +115,9 @@ def _load():
         "mqvs_index_info": ([P, P], ctypes.c_int),
         "mqvs_index_search": ([P, P, I32, I32, ctypes.c_char_p, P, P, P, P, U32, P], ctypes.c_int),
         "mqvs_index_last_stats": ([P], ctypes.c_int),
+        "mqvs_segment_create_binary": ([P, I64, I32, I32, I64, I64, U32, P], ctypes.c_int),
+        "mqvs_search_binary": ([P, P, I32, I32, I32, P, P, P, P, U32, P], ctypes.c_int),
+        "mqvs_knn_binary_raw": ([P, P, I64, I64, I64, I64, I32, P, P], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

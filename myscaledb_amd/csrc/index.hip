@@ -229,6 +229,7 @@ struct TmpBuf {
 
 static mqvs_index *build_impl(mqvs_segment *seg, const char *index_type, const char *params) {
     if (!seg) fail(MQVS_ERR_BAD_ARGUMENTS, "null segment");
+    if (seg->binary) fail(MQVS_ERR_NOT_IMPLEMENTED, "vector index over binary vectors is not implemented");
     std::string type = index_type ? index_type : "MSTG";
     for (auto &ch : type) ch = (char)std::toupper((unsigned char)ch);
     if (type != "MSTG" && type != "IVFFLAT")

@@ -102,12 +102,45 @@ __global__ __launch_bounds__(SEL_THREADS) void k_final_select(const Cand *cand,
         // long list: k-th primary key first, then sort only key <= it (k + ties)
         auto keyof = [&](int64_t i) { return key32<METRIC>(c[i].raw); };
         const uint32_t th = block_radix_select(keyof, n, k, hist, sh);
+        // rows tying at the k-th key rank by row (L2 / IP / binary: the key
+        // then the row is the whole order), so when more than kSortCap rows
+        // reach the k-th key only the smallest rows of the tie are kept (the
+        // (k - #below)-th smallest tied row bounds them); cosine ties also
+        // rank by chunk and ip and keep the plain path
+        uint32_t rth = 0xFFFFFFFFu;
+        if (METRIC != MQVS_METRIC_COSINE && th != 0xFFFFFFFEu) {
+            if (threadIdx.x == 0) s_cnt = 0;
+            __syncthreads();
+            int below = 0, tie = 0;
+            for (int i = threadIdx.x; i < n; i += SEL_THREADS) {
+                const uint32_t key = keyof(i);
+                below += key < th;
+                tie += key == th;
+            }
+            atomicAdd(&s_cnt, below);
+            __syncthreads();
+            const int nbelow = s_cnt;
+            __syncthreads();
+            if (threadIdx.x == 0) s_cnt = 0;
+            __syncthreads();
+            atomicAdd(&s_cnt, tie);
+            __syncthreads();
+            const int ntie = s_cnt;
+            __syncthreads();
+            if (nbelow + ntie > kSortCap) {
+                auto rowof = [&](int64_t i) {
+                    const Cand e = c[i];
+                    return key32<METRIC>(e.raw) == th ? e.row : 0xFFFFFFFFu;
+                };
+                rth = block_radix_select(rowof, n, k - nbelow, hist, sh);
+            }
+        }
         if (threadIdx.x == 0) s_cnt = 0;
         __syncthreads();
         for (int i = threadIdx.x; i < n; i += SEL_THREADS) {
             const Cand e = c[i];
             const uint32_t key = key32<METRIC>(e.raw);
-            if (key != 0xFFFFFFFFu && key <= th) {
+            if (key != 0xFFFFFFFFu && (key < th || (key == th && e.row <= rth))) {
                 const int pos = atomicAdd(&s_cnt, 1);
                 if (pos < kSortCap) recs[pos] = make_rec(e);
             }

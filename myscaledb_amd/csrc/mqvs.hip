@@ -183,6 +183,7 @@ static void free_segment(mqvs_segment *s) {
     if (s->rows_sc) (void)hipFree(s->rows_sc);
     if (s->ynorm_max) (void)hipFree(s->ynorm_max);
     if (s->chunk_ord) (void)hipFree(s->chunk_ord);
+    if (s->codes) (void)hipFree(s->codes);
     if (cur >= 0) (void)hipSetDevice(cur);
     delete s;
 }
@@ -244,6 +245,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
                         float *out_dist, uint32_t flags, hipStream_t user_stream,
                         bool force_exact = false, int64_t ord_base = -1) {
     if (!seg) fail(MQVS_ERR_BAD_ARGUMENTS, "null segment");
+    if (seg->binary) fail(MQVS_ERR_LOGICAL, "binary (FixedString) segment: search it with mqvs_search_binary");
     if (nq < 0 || k < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "nq and k must be non-negative");
     if (nq > 0 && k > 0 && (!queries || !out_ids || !out_dist))
         fail(MQVS_ERR_BAD_ARGUMENTS, "null query or output pointer");
@@ -608,6 +610,7 @@ static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const i
                         int ncand, int k, int metric, const uint8_t *exists, int64_t *out_ids,
                         float *out_dist, uint32_t flags, hipStream_t user_stream) {
     if (!seg) fail(MQVS_ERR_BAD_ARGUMENTS, "null segment");
+    if (seg->binary) fail(MQVS_ERR_NOT_IMPLEMENTED, "computeTopDistanceSubset is for Float32 vectors");
     if (nq < 0 || k < 0 || ncand < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "nq, k and ncand must be non-negative");
     const bool cos = metric == MQVS_METRIC_COSINE;
     if (metric != MQVS_METRIC_L2 && metric != MQVS_METRIC_IP && !cos)
@@ -691,6 +694,230 @@ static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const i
         MQVS_HIP(hipMemcpyAsync(out_dist, ddist, sizeof(float) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
         MQVS_HIP(hipStreamSynchronize(s));
     }
+}
+
+
+// ---------------------------------------------------------------------------
+// binary vectors: vectorScanWithoutIndex<BinaryVector> for one part
+// (MergeTreeVSManager.cpp:1188-1273 filtered gather, :1395-1425 whole chunks)
+// on the same probe / threshold / append / select pipeline as the float VALU
+// path, with the popcount scan of kernels_binary.hip and the L2 ordering key
+// (both binary distances are ascending and finite).  No granule chunking is
+// needed: the reference's per-chunk strict merges keep the k best by
+// (distance, row) over the part, like the float L2 path.
+
+static mqvs_segment *new_binary_segment(int64_t n, int32_t dim_bits, int32_t metric, int64_t granule,
+                                        int64_t row_offset) {
+    if (n < 0 || n >= ((int64_t)1 << 32)) fail(MQVS_ERR_BAD_ARGUMENTS, "segment rows must be in [0, 2^32)");
+    if (dim_bits <= 0 || dim_bits % 8 != 0)
+        fail(MQVS_ERR_BAD_ARGUMENTS, "binary vector dimension must be a positive multiple of 8 bits");
+    if (metric != MQVS_METRIC_HAMMING && metric != MQVS_METRIC_JACCARD)
+        fail(MQVS_ERR_NOT_IMPLEMENTED, "Metric not implemented in brute force search for Binary Vector");
+    if (granule <= 0) fail(MQVS_ERR_BAD_ARGUMENTS, "granule_rows must be positive");
+    if (row_offset < 0 || row_offset % granule != 0)
+        fail(MQVS_ERR_BAD_ARGUMENTS, "row_offset must be a non-negative multiple of granule_rows");
+    auto *s = new mqvs_segment();
+    MQVS_HIP(hipGetDevice(&s->device));
+    s->binary = true;
+    s->n = n;
+    s->d = dim_bits;
+    s->metric = metric;
+    s->granule = granule;
+    s->row_offset = row_offset;
+    s->code_bytes = dim_bits / 8;
+    s->code_words = (int)round_up((s->code_bytes + 3) / 4, 4);
+    const size_t bytes = (size_t)std::max<int64_t>(n, 1) * s->code_words * 4;
+    if (hipMalloc((void **)&s->codes, bytes) != hipSuccess) {
+        (void)hipGetLastError();
+        delete s;
+        fail(MQVS_ERR_MEMORY_LIMIT, "HBM allocation of " + std::to_string(bytes) + " bytes failed");
+    }
+    s->bytes = bytes;
+    return s;
+}
+
+// rows of `nbytes` (host or device) -> zero-padded [n][words] on the device
+static void upload_codes(uint32_t *dst, int words, const uint8_t *src, int64_t nbytes, int64_t n, bool dev,
+                         hipStream_t s) {
+    if (n <= 0) return;
+    MQVS_HIP(hipMemsetAsync(dst, 0, (size_t)n * words * 4, s));
+    MQVS_HIP(hipMemcpy2DAsync(dst, (size_t)words * 4, src, (size_t)nbytes, (size_t)nbytes, (size_t)n,
+                              dev ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice, s));
+}
+
+static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq, int k, int metric,
+                               const uint8_t *filter, const uint8_t *exists, int64_t *out_ids, float *out_dist,
+                               uint32_t flags, hipStream_t user_stream) {
+    if (!seg) fail(MQVS_ERR_BAD_ARGUMENTS, "null segment");
+    if (!seg->binary) fail(MQVS_ERR_LOGICAL, "Float32 segment: search it with mqvs_search");
+    if (metric != MQVS_METRIC_HAMMING && metric != MQVS_METRIC_JACCARD)
+        fail(MQVS_ERR_NOT_IMPLEMENTED, "Metric not implemented in brute force search for Binary Vector");
+    if (nq < 0 || k < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "nq and k must be non-negative");
+    if (k > kSortCap) fail(MQVS_ERR_BAD_ARGUMENTS, "k above " + std::to_string(kSortCap) + " not supported");
+    if (nq > 0 && k > 0 && (!queries || !out_ids || !out_dist))
+        fail(MQVS_ERR_BAD_ARGUMENTS, "null query or output pointer");
+    mqvs_search_stats st{};
+    g_stats = st;
+    if (nq == 0 || k == 0) return;
+
+    DeviceGuard guard(seg->device);
+    Workspace &ws = workspace(seg->device);
+    hipStream_t s = user_stream ? (hipStream_t)user_stream : ws.stream;
+    const bool dev = flags & MQVS_F_DEVICE_PTRS;
+    const int64_t n = seg->n;
+    const int64_t bm_bytes = (n + 7) / 8;
+    const bool timing = g_timing != 0;
+    if (timing) MQVS_HIP(hipEventRecord(ws.ev[0], s));
+
+    uint32_t *qc = (uint32_t *)ws.queries.get((size_t)nq * seg->code_words * 4);
+    upload_codes(qc, seg->code_words, queries, seg->code_bytes, nq, dev, s);
+    const uint8_t *dfilter = filter, *dexists = exists;
+    if (!dev) {
+        if (filter) {
+            auto *f = (uint8_t *)ws.filter.get(bm_bytes);
+            MQVS_HIP(hipMemcpyAsync(f, filter, bm_bytes, hipMemcpyHostToDevice, s));
+            dfilter = f;
+        }
+        if (exists) {
+            auto *f = (uint8_t *)ws.exists.get(bm_bytes);
+            MQVS_HIP(hipMemcpyAsync(f, exists, bm_bytes, hipMemcpyHostToDevice, s));
+            dexists = f;
+        }
+    }
+    int64_t *dids = out_ids;
+    float *ddist = out_dist;
+    if (!dev) {
+        dids = (int64_t *)ws.out_ids.get(sizeof(int64_t) * (size_t)nq * k);
+        ddist = (float *)ws.out_dist.get(sizeof(float) * (size_t)nq * k);
+    }
+
+    // candidate capacity and probe size as the float path (mqvs.hip search_impl)
+    constexpr int64_t tile_rows = kSmallRows;
+    int cap = (int)std::min<int64_t>(kCandMax, kCandBudget / std::max(nq, 1));
+    cap = std::max(cap, kSortCap) / 256 * 256;
+    const int64_t target_cands = std::min<int64_t>(cap / 3, 16384);
+    int64_t P = n;
+    if (n > 32768) {
+        P = (int64_t)(((double)k * (double)n) / target_cands) + 1;
+        P = std::max<int64_t>(P, 8 * (int64_t)k);
+        P = round_up(P, tile_rows);
+        if (P > n) P = n;
+    }
+    ScanParams p{};
+    p.n = n;
+    p.nq = nq;
+    p.chunk_rows = seg->granule;
+    p.filter = dfilter;
+    p.exists = dexists;
+    p.codes = seg->codes;
+    p.qcodes = qc;
+    p.code_words = seg->code_words;
+    p.nbits = seg->d;
+    uint32_t *tau = (uint32_t *)ws.tau.get(sizeof(uint32_t) * nq);
+    int *count = (int *)ws.count.get(sizeof(int) * nq);
+    Cand *cand = (Cand *)ws.cand.get(sizeof(Cand) * (size_t)nq * cap);
+    int *overflow = (int *)ws.overflow.get(sizeof(int) * 4);
+    p.tau = tau;
+    p.cand_count = count;
+    p.cand = cand;
+    p.cand_cap = cap;
+    p.probe = (float *)ws.probe.get(sizeof(float) * (size_t)nq * std::max<int64_t>(P, 1));
+    p.probe_ld = P;
+    auto scan = [&](int64_t b, int64_t e, bool probe, bool strict) {
+        const Range r = make_range(b, e, tile_rows, seg->granule, false);
+        if (r.tiles <= 0) return;
+        p.row_begin = r.begin;
+        p.row_end = r.end;
+        p.tiles = r.tiles;
+        p.tiles_per_chunk = 0;
+        p.tile_rows = tile_rows;
+        p.tau_strict = strict ? 1 : 0;
+        launch_scan_binary(p, metric, probe, s);
+        MQVS_HIP(hipGetLastError());
+    };
+    constexpr int kOrder = MQVS_METRIC_L2;  // ascending finite values: ord_asc key, (key, row) ties
+    if (timing) MQVS_HIP(hipEventRecord(ws.ev[5], s));
+    scan(0, P, true, false);
+    if (timing) MQVS_HIP(hipEventRecord(ws.ev[1], s));
+    MQVS_HIP(hipMemsetAsync(count, 0, sizeof(int) * nq, s));
+    launch_probe_select(p.probe, P, P, nq, k, kOrder, tau, count, cand, cap, 0, nullptr, s);
+    MQVS_HIP(hipGetLastError());
+    if (timing) MQVS_HIP(hipEventRecord(ws.ev[2], s));
+    {
+        Cand *alt = (Cand *)ws.cand2.get(sizeof(Cand) * (size_t)nq * cap);
+        int *calt = (int *)ws.count2.get(sizeof(int) * nq);
+        int64_t b = P, seg_rows = std::max<int64_t>(2 * P, tile_rows);
+        int segs = 0;
+        while (b < n) {
+            const int64_t e = std::min(n, round_up(b + seg_rows, tile_rows));
+            scan(b, e, false, true);
+            b = e;
+            seg_rows *= 2;
+            ++segs;
+            if (b < n) {
+                launch_refine(cand, count, cap, nq, k, kOrder, false, nullptr, tau, nullptr, alt, calt, s);
+                MQVS_HIP(hipGetLastError());
+                std::swap(cand, alt);
+                std::swap(count, calt);
+                p.cand = cand;
+                p.cand_count = count;
+            }
+        }
+        st.segments = segs;
+    }
+    if (timing) MQVS_HIP(hipEventRecord(ws.ev[3], s));
+    MQVS_HIP(hipMemsetAsync(overflow, 0, sizeof(int) * 4, s));
+    launch_final_select(cand, count, cap, nq, k, kOrder, 0, seg->row_offset, dids, ddist, overflow, s);
+    MQVS_HIP(hipGetLastError());
+    if (timing) MQVS_HIP(hipEventRecord(ws.ev[4], s));
+    st.path = 3;  // binary popcount scan
+    st.probe_rows = P;
+    st.main_rows = n - P;
+    st.rows_scanned = n;
+    st.nq = nq;
+    st.k = k;
+    const bool async = dev && (flags & MQVS_F_ASYNC);
+    if (!async) {
+        MQVS_HIP(hipMemcpyAsync(ws.host_flags, overflow, sizeof(int), hipMemcpyDeviceToHost, s));
+        MQVS_HIP(hipStreamSynchronize(s));
+        int rescans = 0;
+        while (ws.host_flags[0]) {
+            // a list overflowed its capacity: tighten tau from what was kept and
+            // rescan the part inclusively (rare: > cap rows at or under the
+            // probe threshold)
+            if (++rescans > 3)
+                fail(MQVS_ERR_LOGICAL, "candidate overflow: more than " + std::to_string(cap) +
+                                           " rows tie at the k-th distance");
+            launch_cand_tau(cand, count, cap, nq, k, kOrder, tau, nullptr, s);
+            MQVS_HIP(hipMemsetAsync(count, 0, sizeof(int) * nq, s));
+            scan(0, n, false, false);
+            MQVS_HIP(hipMemsetAsync(overflow, 0, sizeof(int) * 4, s));
+            launch_final_select(cand, count, cap, nq, k, kOrder, 0, seg->row_offset, dids, ddist, overflow, s);
+            MQVS_HIP(hipGetLastError());
+            MQVS_HIP(hipMemcpyAsync(ws.host_flags, overflow, sizeof(int), hipMemcpyDeviceToHost, s));
+            MQVS_HIP(hipStreamSynchronize(s));
+        }
+        st.rescans = rescans;
+        if (!dev) {
+            MQVS_HIP(hipMemcpyAsync(out_ids, dids, sizeof(int64_t) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
+            MQVS_HIP(hipMemcpyAsync(out_dist, ddist, sizeof(float) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
+            MQVS_HIP(hipStreamSynchronize(s));
+        }
+        if (timing) {
+            float a = 0, b = 0, c = 0, e = 0, f = 0;
+            MQVS_HIP(hipEventElapsedTime(&a, ws.ev[5], ws.ev[1]));
+            MQVS_HIP(hipEventElapsedTime(&b, ws.ev[1], ws.ev[2]));
+            MQVS_HIP(hipEventElapsedTime(&c, ws.ev[2], ws.ev[3]));
+            MQVS_HIP(hipEventElapsedTime(&e, ws.ev[3], ws.ev[4]));
+            MQVS_HIP(hipEventElapsedTime(&f, ws.ev[0], ws.ev[4]));
+            st.probe_ms = a;
+            st.probe_select_ms = b;
+            st.main_ms = c;
+            st.final_ms = e;
+            st.total_ms = f;
+        }
+    }
+    g_stats = st;
 }
 
 // ---------------------------------------------------------------------------
@@ -850,6 +1077,7 @@ int mqvs_segment_info(mqvs_segment_t seg, int64_t *n, int32_t *d, int32_t *metri
 int mqvs_segment_rows(mqvs_segment_t seg, const float **dev_rows) {
     return guarded([&] {
         if (!seg || !dev_rows) fail(MQVS_ERR_BAD_ARGUMENTS, "null argument");
+        if (seg->binary) fail(MQVS_ERR_LOGICAL, "binary segment has no Float32 rows");
         *dev_rows = seg->rows;
     });
 }
@@ -904,6 +1132,79 @@ int mqvs_knn_raw(const float *x, const float *y, int64_t d, int64_t k, int64_t n
     });
 }
 
+int mqvs_segment_create_binary(const uint8_t *codes, int64_t n, int32_t dim_bits, int32_t metric,
+                               int64_t granule_rows, int64_t row_offset, uint32_t flags, mqvs_segment_t *out) {
+    return guarded([&] {
+        if (!out) fail(MQVS_ERR_BAD_ARGUMENTS, "null output handle");
+        *out = nullptr;
+        mqvs_segment *s = new_binary_segment(n, dim_bits, metric, granule_rows, row_offset);
+        try {
+            if (n > 0 && !codes) fail(MQVS_ERR_BAD_ARGUMENTS, "null codes");
+            Workspace &ws = workspace(s->device);
+            upload_codes(s->codes, s->code_words, codes, s->code_bytes, n, (flags & MQVS_F_DEVICE_PTRS) != 0,
+                         ws.stream);
+            MQVS_HIP(hipStreamSynchronize(ws.stream));
+        } catch (...) {
+            free_segment(s);
+            throw;
+        }
+        *out = s;
+    });
+}
+
+int mqvs_search_binary(mqvs_segment_t seg, const uint8_t *queries, int32_t nq, int32_t k, int32_t metric,
+                       const uint8_t *filter, const uint8_t *row_exists, int64_t *out_ids, float *out_dist,
+                       uint32_t flags, mqvs_stream_t stream) {
+    return guarded([&] {
+        search_binary_impl(seg, queries, nq, k, metric, filter, row_exists, out_ids, out_dist, flags,
+                           (hipStream_t)stream);
+    });
+}
+
+int mqvs_knn_binary_raw(const uint8_t *x, const uint8_t *y, int64_t d, int64_t k, int64_t nx, int64_t ny,
+                        int32_t metric, int64_t *result_id, float *distance) {
+    return guarded([&] {
+        if (metric != MQVS_METRIC_HAMMING && metric != MQVS_METRIC_JACCARD)
+            fail(MQVS_ERR_NOT_IMPLEMENTED, "Metric not implemented in brute force search for Binary Vector");
+        if (d <= 0 || d % 8 != 0 || d > INT32_MAX || k < 0 || k > INT32_MAX || nx < 0 || nx > INT32_MAX ||
+            ny < 0)
+            fail(MQVS_ERR_BAD_ARGUMENTS, "bad sizes");
+        if (nx == 0 || k == 0) return;
+        if (ny == 0) {
+            for (int64_t i = 0; i < nx * k; ++i) {
+                result_id[i] = -1;
+                if (metric == MQVS_METRIC_HAMMING)
+                    reinterpret_cast<int32_t *>(distance)[i] = INT32_MAX;
+                else
+                    distance[i] = 3.40282347e+38f;
+            }
+            return;
+        }
+        mqvs_segment *s = new_binary_segment(ny, (int32_t)d, metric, ny, 0);
+        try {
+            Workspace &ws = workspace(s->device);
+            upload_codes(s->codes, s->code_words, y, s->code_bytes, ny, false, ws.stream);
+            const size_t m = (size_t)nx * k;
+            auto *b = (char *)ws.misc.get(m * 12 + 16);
+            auto *di = (int64_t *)b;
+            auto *dd = (float *)(b + m * 8);
+            auto *qd = (uint8_t *)ws.glist.get((size_t)nx * (d / 8));
+            MQVS_HIP(hipMemcpyAsync(qd, x, (size_t)nx * (d / 8), hipMemcpyHostToDevice, ws.stream));
+            search_binary_impl(s, qd, (int)nx, (int)k, metric, nullptr, nullptr, di, dd, MQVS_F_DEVICE_PTRS,
+                               nullptr);
+            if (metric == MQVS_METRIC_HAMMING) launch_hamming_to_int(di, dd, (int64_t)m, ws.stream);
+            MQVS_HIP(hipGetLastError());
+            MQVS_HIP(hipMemcpyAsync(result_id, di, m * 8, hipMemcpyDeviceToHost, ws.stream));
+            MQVS_HIP(hipMemcpyAsync(distance, dd, m * 4, hipMemcpyDeviceToHost, ws.stream));
+            MQVS_HIP(hipStreamSynchronize(ws.stream));
+        } catch (...) {
+            free_segment(s);
+            throw;
+        }
+        free_segment(s);
+    });
+}
+
 int mqvs_merge_shards(int32_t nshards, int32_t nq, int32_t k, int32_t metric, const int64_t *in_ids,
                       const float *in_dist, int64_t *out_ids, float *out_dist, uint32_t flags,
                       mqvs_stream_t stream) {
@@ -932,7 +1233,9 @@ int mqvs_merge_shards(int32_t nshards, int32_t nq, int32_t k, int32_t metric, co
             di = bi;
             dd = bd;
         }
-        launch_merge_shards(nshards, nq, k, metric, di, dd, oi, od, (flags & MQVS_F_PART_MERGE) != 0, s);
+        // binary distances (Hamming, Jaccard) are ascending finite values: the L2 order
+        const int order = (metric == MQVS_METRIC_HAMMING || metric == MQVS_METRIC_JACCARD) ? MQVS_METRIC_L2 : metric;
+        launch_merge_shards(nshards, nq, k, order, di, dd, oi, od, (flags & MQVS_F_PART_MERGE) != 0, s);
         MQVS_HIP(hipGetLastError());
         if (!devp) {
             MQVS_HIP(hipMemcpyAsync(out_ids, oi, nout * 8, hipMemcpyDeviceToHost, s));

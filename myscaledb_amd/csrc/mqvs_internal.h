@@ -29,6 +29,11 @@ struct mqvs_segment {
     bool approx_ok = false;          // bf16 pre-filter usable for this segment
     uint8_t *nonempty_bits = nullptr;// null when every array is non-empty
     int *chunk_ord = nullptr;        // no-filter chunk ordinals (null = identity)
+    // binary segments (FixedString(N) codes; rows == nullptr)
+    bool binary = false;
+    uint32_t *codes = nullptr;       // [n][code_words], 16-B aligned rows, zero padded
+    int code_bytes = 0;              // N = d / 8
+    int code_words = 0;              // row stride in 32-bit words (multiple of 4)
     size_t bytes = 0;
 };
 
@@ -166,6 +171,12 @@ struct ScanParams {
     // whole 256-entry tiles, so a tile never spans two chunks.  Probe columns
     // are list positions; candidates store rows.
     const int32_t *row_list;  // null = contiguous rows
+    // binary scan (kernels_binary.hip)
+    const uint32_t *codes;    // [n][code_words]
+    const uint32_t *qcodes;   // [nq][code_words]
+    int code_words;
+    int nbits;                // d: Hamming distances == nbits are never returned
+    int tau_strict;           // APPEND takes key < tau (segments after the probe) instead of <=
     unsigned long long *dbg;  // diagnostic builds only (stage timing stamps)
 };
 
@@ -258,6 +269,10 @@ void launch_pack_nonempty(const uint8_t *bytes, int64_t n, uint8_t *bits, hipStr
 void launch_chunk_ordinals(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists,
                            int64_t n, int64_t chunk_rows, int require_filter, int *ord,
                            hipStream_t s);
+
+// binary vectors (kernels_binary.hip)
+void launch_scan_binary(const ScanParams &p, int metric, bool probe, hipStream_t s);
+void launch_hamming_to_int(const int64_t *ids, float *dist, int64_t m, hipStream_t s);
 
 // bf16 pre-filter path (kernels_bf16.hip)
 constexpr int kBfK = 64;    // bf16 planes padded to a multiple of this

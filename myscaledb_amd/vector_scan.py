@@ -7,6 +7,10 @@ Names and contracts follow the reference so the parity tests read like its own:
 * ``VectorScanSegment``       -- one data part's Array(Float32) column, registered
   once and resident in HBM (replaces the per-granule copy loop of
   MergeTreeVSManager.cpp:1366-1393).
+* ``BinaryVectorScanSegment`` / ``try_brute_force_search_binary`` -- the same for
+  FixedString(N) binary columns, Hamming / Jaccard
+  (tryBruteForceSearch<BinaryVector>, BruteForceSearch.h:94-110;
+  MergeTreeVSManager.cpp:1188-1273, 1395-1425).
 * ``vector_scan_without_index`` -- MergeTreeVSManager::vectorScanWithoutIndex<Float>
   (MergeTreeVSManager.cpp:960-1536) incl. searchWrapper (:1538-1680); returns
   the same result columns (label UInt32, [vector_id UInt32,] distance Float32)
@@ -198,6 +202,93 @@ def try_brute_force_search(x, y, d, k, nx, ny, metric):
     return ids, dist
 
 
+class BinaryVectorScanSegment:
+    """A data part's FixedString(N) binary vector column resident in HBM.
+
+    codes: (n, N) uint8 (numpy, or a torch CUDA uint8 tensor); dimension = 8N
+    bits.  metric: the column's binary_vector_search_metric_type (Hamming or
+    Jaccard); a search may pass the other one."""
+
+    def __init__(self, handle, n, nbytes, metric, granule, row_offset):
+        self._h = handle
+        self.n, self.nbytes, self.d = n, nbytes, 8 * nbytes
+        self.metric, self.granule, self.row_offset = metric, granule, row_offset
+
+    @classmethod
+    def from_codes(cls, codes, metric="Hamming", granule=DEFAULT_GRANULE, row_offset=0):
+        m = metric_id(metric)
+        h = ctypes.c_void_p()
+        if _is_torch(codes):
+            assert codes.is_cuda and codes.is_contiguous()
+            n, nb = codes.shape
+            check(lib.mqvs_segment_create_binary(_ptr(codes), n, 8 * nb, m, granule, row_offset, F_DEVICE_PTRS,
+                                                 ctypes.byref(h)))
+        else:
+            codes = _host_u8(codes)
+            n, nb = codes.shape
+            check(lib.mqvs_segment_create_binary(_ptr(codes), n, 8 * nb, m, granule, row_offset, 0,
+                                                 ctypes.byref(h)))
+        return cls(h, n, nb, m, granule, row_offset)
+
+    def search(self, queries, k, metric=None, filter_bitmap=None, row_exists=None, out=None, async_=False,
+               stream=None):
+        """mqvs_search_binary: (ids[nq,k] int64, dist[nq,k] float32), ascending,
+        -1 / FLT_MAX padded."""
+        m = self.metric if metric is None else metric_id(metric)
+        if _is_torch(queries):
+            import torch
+            assert queries.is_cuda and queries.is_contiguous() and queries.dtype == torch.uint8
+            nq = queries.shape[0]
+            if out is None:
+                ids = torch.empty((nq, k), dtype=torch.int64, device=queries.device)
+                dist = torch.empty((nq, k), dtype=torch.float32, device=queries.device)
+            else:
+                ids, dist = out
+            flags = F_DEVICE_PTRS | (F_ASYNC if async_ else 0)
+            check(lib.mqvs_search_binary(self._h, _ptr(queries), nq, k, m, _ptr(filter_bitmap), _ptr(row_exists),
+                                         _ptr(ids), _ptr(dist), flags, ctypes.c_void_p(stream) if stream else None))
+            return ids, dist
+        q = _host_u8(queries)
+        if q.ndim == 1:
+            q = q[None, :]
+        nq = q.shape[0]
+        if q.shape[1] != self.nbytes:
+            raise _lib.MqvsError(_lib.ERR_LOGICAL,
+                                 f"query length {q.shape[1]} bytes != column FixedString({self.nbytes})")
+        ids = np.empty((nq, k), np.int64)
+        dist = np.empty((nq, k), np.float32)
+        check(lib.mqvs_search_binary(self._h, _ptr(q), nq, k, m, _ptr(_host_u8(filter_bitmap)),
+                                     _ptr(_host_u8(row_exists)), _ptr(ids), _ptr(dist), 0, None))
+        return ids, dist
+
+    def free(self):
+        if self._h:
+            check(lib.mqvs_segment_free(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def try_brute_force_search_binary(x, y, d, k, nx, ny, metric):
+    """tryBruteForceSearch<BinaryVector> (BruteForceSearch.h:94-110): x, y
+    uint8 codes of d bits; returns (result_id[nx*k], distance[nx*k]) where the
+    distance buffer holds int32 counts for Hamming (faiss::hammings_knn_mc via
+    reinterpret_cast<int32_t*>) and float32 for Jaccard."""
+    m = metric_id(metric)
+    x = _host_u8(x).reshape(-1)
+    y = _host_u8(y).reshape(-1)
+    ids = np.empty(nx * k, np.int64)
+    dist = np.empty(nx * k, np.float32)
+    check(lib.mqvs_knn_binary_raw(_ptr(x), _ptr(y), d, k, nx, ny, m, _ptr(ids), _ptr(dist)))
+    if m == _lib.METRIC_HAMMING:
+        dist = dist.view(np.int32)
+    return ids, dist
+
+
 def vector_scan_without_index(segment: VectorScanSegment, query_vector, k, metric=None,
                               filter_bitmap=None, row_exists=None, is_batch=False):
     """MergeTreeVSManager::vectorScanWithoutIndex result columns.
@@ -205,7 +296,10 @@ def vector_scan_without_index(segment: VectorScanSegment, query_vector, k, metri
     Returns (label, distance) or, for batch, (label, vector_id, distance) with
     the reference's emission order: query-major, best first, -1 labels dropped.
     """
-    q = _host_f32(query_vector)
+    if isinstance(segment, BinaryVectorScanSegment):
+        q = _host_u8(query_vector)
+    else:
+        q = _host_f32(query_vector)
     if q.ndim == 1:
         q = q[None, :]
     ids, dist = segment.search(q, k, metric, filter_bitmap, row_exists)
