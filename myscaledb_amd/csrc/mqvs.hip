@@ -799,6 +799,10 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
     int64_t P = n;
     if (n > 32768) {
         P = (int64_t)(((double)k * (double)n) / target_cands) + 1;
+        // the refines between main segments keep appends near 2k per segment
+        // whatever the probe, so the probe stays short on big parts (its select
+        // is one workgroup per query)
+        P = std::min<int64_t>(P, std::max<int64_t>(nq <= 8 ? 16384 : 65536, 8 * (int64_t)k));
         P = std::max<int64_t>(P, 8 * (int64_t)k);
         P = round_up(P, tile_rows);
         if (P > n) P = n;
@@ -846,13 +850,15 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
     {
         Cand *alt = (Cand *)ws.cand2.get(sizeof(Cand) * (size_t)nq * cap);
         int *calt = (int *)ws.count2.get(sizeof(int) * nq);
+        // segments grow x4: each refine costs a launch, and appends per
+        // segment stay near (growth x k) with the threshold refined
         int64_t b = P, seg_rows = std::max<int64_t>(2 * P, tile_rows);
         int segs = 0;
         while (b < n) {
             const int64_t e = std::min(n, round_up(b + seg_rows, tile_rows));
             scan(b, e, false, true);
             b = e;
-            seg_rows *= 2;
+            seg_rows *= 4;
             ++segs;
             if (b < n) {
                 launch_refine(cand, count, cap, nq, k, kOrder, false, nullptr, tau, nullptr, alt, calt, s);

@@ -29,58 +29,6 @@ struct RunHist {
     }
 };
 
-// k-th smallest valid key (1-based rank k) among `count` values produced by
-// load(i); 0xFFFFFFFE when fewer than k values are valid.  Block-wide.
-template <typename KeyFn>
-__device__ inline uint32_t block_radix_select(KeyFn keyof, int64_t count, int k, uint32_t *hist,
-                                       uint32_t *sh) {
-    const int t = threadIdx.x;
-    uint32_t prefix = 0, mask = 0, kk = (uint32_t)k;
-    for (int pass = 0; pass < 4; ++pass) {
-        const int shift = 24 - 8 * pass;
-        for (int i = t; i < 256; i += SEL_THREADS) hist[i] = 0;
-        __syncthreads();
-        RunHist rh;
-        for (int64_t i = t; i < count; i += SEL_THREADS) {
-            const uint32_t key = keyof(i);
-            if (key == 0xFFFFFFFFu) continue;
-            if ((key & mask) != prefix) continue;
-            rh.add(hist, (key >> shift) & 255u);
-        }
-        rh.flush(hist);
-        __syncthreads();
-        if (t == 0) {
-            uint32_t total = 0;
-            for (int b = 0; b < 256; ++b) total += hist[b];
-            uint32_t done = 0, cum = 0, bsel = 0;
-            if (pass == 0 && total < kk) {
-                done = 1;  // fewer than k valid: every valid value qualifies
-            } else {
-                for (int b = 0; b < 256; ++b) {
-                    if (cum + hist[b] >= kk) {
-                        bsel = (uint32_t)b;
-                        break;
-                    }
-                    cum += hist[b];
-                }
-            }
-            sh[0] = done;
-            sh[1] = bsel;
-            sh[2] = cum;
-        }
-        __syncthreads();
-        if (sh[0]) {
-            __syncthreads();
-            return 0xFFFFFFFEu;
-        }
-        prefix |= sh[1] << shift;
-        mask |= 255u << shift;
-        kk -= sh[2];
-        __syncthreads();
-    }
-    return prefix;
-}
-
 // Bucket holding the kk-th smallest key (1-based) of a 256-bucket histogram,
 // found by wave 0 in parallel (4 buckets per lane + a lane prefix sum).
 // Writes sh[0] = done (total < kk on the first pass), sh[1] = bucket,
@@ -122,6 +70,40 @@ __device__ inline void hist_pick(const uint32_t *hist, uint32_t kk, bool first, 
         sh[1] = b;
         sh[2] = cum;
     }
+}
+
+// k-th smallest valid key (1-based rank k) among `count` values produced by
+// load(i); 0xFFFFFFFE when fewer than k values are valid.  Block-wide.
+template <typename KeyFn>
+__device__ inline uint32_t block_radix_select(KeyFn keyof, int64_t count, int k, uint32_t *hist,
+                                       uint32_t *sh) {
+    const int t = threadIdx.x;
+    uint32_t prefix = 0, mask = 0, kk = (uint32_t)k;
+    for (int pass = 0; pass < 4; ++pass) {
+        const int shift = 24 - 8 * pass;
+        for (int i = t; i < 256; i += SEL_THREADS) hist[i] = 0;
+        __syncthreads();
+        RunHist rh;
+        for (int64_t i = t; i < count; i += SEL_THREADS) {
+            const uint32_t key = keyof(i);
+            if (key == 0xFFFFFFFFu) continue;
+            if ((key & mask) != prefix) continue;
+            rh.add(hist, (key >> shift) & 255u);
+        }
+        rh.flush(hist);
+        __syncthreads();
+        hist_pick(hist, kk, pass == 0, sh);  // fewer than k valid on pass 0: sh[0] = done
+        __syncthreads();
+        if (sh[0]) {
+            __syncthreads();
+            return 0xFFFFFFFEu;
+        }
+        prefix |= sh[1] << shift;
+        mask |= 255u << shift;
+        kk -= sh[2];
+        __syncthreads();
+    }
+    return prefix;
 }
 
 // block_radix_select with the bucket search in parallel and 4 keys in
@@ -209,25 +191,7 @@ __device__ inline uint32_t block_radix_select_rows(const float *row, int64_t P, 
         });
         rh.flush(hist);
         __syncthreads();
-        if (t == 0) {
-            uint32_t total = 0;
-            for (int b = 0; b < 256; ++b) total += hist[b];
-            uint32_t done = 0, cum = 0, bsel = 0;
-            if (pass == 0 && total < kk) {
-                done = 1;
-            } else {
-                for (int b = 0; b < 256; ++b) {
-                    if (cum + hist[b] >= kk) {
-                        bsel = (uint32_t)b;
-                        break;
-                    }
-                    cum += hist[b];
-                }
-            }
-            sh[0] = done;
-            sh[1] = bsel;
-            sh[2] = cum;
-        }
+        hist_pick(hist, kk, pass == 0, sh);
         __syncthreads();
         if (sh[0]) {
             __syncthreads();

@@ -67,6 +67,9 @@ CASES = [
     (80000, 16, 2, 64, "Hamming", 8192, True, False, 0.5),
     (80000, 16, 1, 64, "Jaccard", 4096, False, True, 0.1),
     (3000, 8, 3, 200, "Hamming", 512, True, True, 0.5),
+    (30000, 128, 5, 30, "Jaccard", 8192, True, False, 0.5),     # 1024-bit codes, coalesced kernel
+    (40000, 128, 2, 40, "Hamming", 2048, False, True, 0.5),
+    (40000, 64, 12, 40, "Hamming", 8192, False, False, 0.5),    # nq > 8: row-per-lane kernel
 ]
 
 
