@@ -116,6 +116,10 @@ int toMqvsMetric(const MetricEnum & metric)
         return MQVS_METRIC_IP;
     if (metric == MetricEnum::Cosine)
         return MQVS_METRIC_COSINE;
+    if (metric == MetricEnum::Hamming)
+        return MQVS_METRIC_HAMMING;
+    if (metric == MetricEnum::Jaccard)
+        return MQVS_METRIC_JACCARD;
     return -1;
 }
 
@@ -138,6 +142,29 @@ void tryBruteForceSearch(
     int64_t * result_id, float * distance, const MetricEnum & metric_type)
 {
     tryBruteForceSearch(x, y, d, k, nx, ny, result_id, distance, toMqvsMetric(metric_type));
+}
+
+/// tryBruteForceSearch<BinaryVector> (BruteForceSearch.h:94-110): x nx*(d/8)
+/// query codes, y ny*(d/8) base codes (FixedString bytes), d in bits.
+/// Hamming fills `distance` with int32 counts as faiss::hammings_knn_mc does
+/// through reinterpret_cast<int32_t*>(distance); Jaccard with floats.
+inline void tryBruteForceSearchBinary(
+    const uint8_t * x, const uint8_t * y, size_t d, size_t k, size_t nx, size_t ny,
+    int64_t * result_id, float * distance, int mqvs_metric)
+{
+    if (mqvs_metric != MQVS_METRIC_HAMMING && mqvs_metric != MQVS_METRIC_JACCARD)
+        throw DB::Exception(DB::ErrorCodes::NOT_IMPLEMENTED, "{}",
+                            std::string("Metric not implemented in brute force search for Binary Vector"));
+    check(mqvs_knn_binary_raw(x, y, static_cast<int64_t>(d), static_cast<int64_t>(k), static_cast<int64_t>(nx),
+                              static_cast<int64_t>(ny), mqvs_metric, result_id, distance));
+}
+
+template <typename MetricEnum>
+void tryBruteForceSearchBinary(
+    const uint8_t * x, const uint8_t * y, size_t d, size_t k, size_t nx, size_t ny,
+    int64_t * result_id, float * distance, const MetricEnum & metric_type)
+{
+    tryBruteForceSearchBinary(x, y, d, k, nx, ny, result_id, distance, toMqvsMetric(metric_type));
 }
 
 /// Columns emitted by vectorScanWithoutIndex (MergeTreeVSManager.cpp:1502-1532).

@@ -16,7 +16,7 @@ namespace MI = VectorIndex::MI355X;
 
 // The metric enum the reference passes (Search::Metric, absent library):
 // only the member names matter to the shim.
-enum class Metric { L2, IP, Cosine, Hamming };
+enum class Metric { L2, IP, Cosine, Hamming, Jaccard };
 
 static float val(int i, int j) { return float((i * 31 + j * 17) % 23 - 11); }
 
@@ -45,6 +45,15 @@ static int errors() {
         return 1;
     } catch (const DB::Exception &e) {
         std::printf("hamming code=%d\n", e.code());
+        if (e.code() != DB::ErrorCodes::NOT_IMPLEMENTED) return 1;
+    }
+    // binary seam: float metrics are NOT_IMPLEMENTED (BruteForceSearch.h:107)
+    try {
+        const uint8_t bx[4] = {0}, by[8] = {0};
+        MI::tryBruteForceSearchBinary(bx, by, 32, 1, 1, 2, id, dist, Metric::L2);
+        return 1;
+    } catch (const DB::Exception &e) {
+        std::printf("binary l2 code=%d\n", e.code());
         if (e.code() != DB::ErrorCodes::NOT_IMPLEMENTED) return 1;
     }
     // direct C-ABI status mapping
