@@ -169,6 +169,23 @@ int mqvs_merge_shards(int32_t nshards, int32_t nq, int32_t k, int32_t metric,
                       const int64_t *in_ids, const float *in_dist, int64_t *out_ids,
                       float *out_dist, uint32_t flags, mqvs_stream_t stream);
 
+/* ---- column ingest: a part's Array(Float32) column from its compressed files
+ * Replaces the per-granule host read + copy of vectorScanWithoutIndex
+ * (MergeTreeVSManager.cpp:1348-1393): data_bin = the bytes of the nested
+ * Float32 stream (`<column>.bin`), sizes_bin = the array sizes stream
+ * (`<column>.size0.bin`, UInt64 per row), both as ClickHouse writes them
+ * (CompressedWriteBuffer blocks: 16-B checksum, method 0x82 LZ4 or 0x02 NONE,
+ * UInt32 compressed size, UInt32 decompressed size, payload; checksums are not
+ * verified).  Decoded on the GPU into the rows of :1381-1393 (FLT_MAX fill;
+ * empty arrays flagged empty; arrays longer than d truncated, shorter ones
+ * FLT_MAX-padded) and prepared as mqvs_segment_create.  flags:
+ * MQVS_F_DEVICE_PTRS when the streams are already in HBM.  Errors:
+ * MQVS_ERR_ILLEGAL_COLUMN (malformed blocks, sizes that do not match the data
+ * stream or n), MQVS_ERR_NOT_IMPLEMENTED (other codecs). */
+int mqvs_segment_create_from_column(const uint8_t *data_bin, int64_t data_bytes, const uint8_t *sizes_bin,
+                                    int64_t sizes_bytes, int64_t n, int32_t d, int32_t metric, int64_t granule_rows,
+                                    int64_t row_offset, uint32_t flags, mqvs_segment_t *out);
+
 /* ---- binary vectors: FixedString(N) columns, Hamming / Jaccard ----------
  * tryBruteForceSearch<BinaryVector> (BruteForceSearch.h:94-110) over
  * vectorScanWithoutIndex<BinaryVector> (MergeTreeVSManager.cpp:1188-1273,

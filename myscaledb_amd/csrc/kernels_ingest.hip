@@ -1,0 +1,311 @@
+// kernels_ingest.hip -- column ingest on the GPU: a
+// MergeTree Array(Float32) column, as the bytes of its compressed files, is
+// decoded in HBM into the rows matrix the scan reads.  It replaces the host
+// read + copy loop of MergeTreeVSManager.cpp:1348-1393 (per granule:
+// CompressedReadBuffer -> LZ4 -> ColumnArray -> vector_raw_data).
+//
+//   k_block_table   the chain of compressed blocks (CompressedReadBufferBase.cpp
+//                   :115-160; CompressionInfo.h: 16-B checksum, method byte,
+//                   UInt32 compressed size incl. the 9-B header, UInt32
+//                   decompressed size).  One thread walks the headers; a
+//                   1 MiB block costs one dependent 25-B read.
+//   k_decode_blocks one 64-lane workgroup per block.  LZ4 (LZ4_decompress_faster
+//                   .cpp:480-640 block format): every lane parses the token
+//                   stream in lock-step (uniform control flow), literal and
+//                   match bytes are copied 64 at a time.  Matches read from a
+//                   64 KiB LDS ring of the block's latest output (LZ4 offsets
+//                   are < 2^16), never from global memory, so no global
+//                   read-after-write ordering is needed; an overlapping match
+//                   (offset < length) is copied in steps of min(offset, 256).
+//   k_sizes_scan_*  array sizes (UInt64 per row) -> element offsets.
+//   k_array_rows    the copy loop of :1381-1393: FLT_MAX fill, first
+//                   min(size, d) elements of a non-empty array, nonempty flag.
+#include "mqvs_internal.h"
+
+namespace mqvs {
+
+constexpr int kRing = 65536;  // LZ4 window
+
+__global__ void k_block_table(const uint8_t *src, int64_t n, IngestBlock *tab, int64_t max_blocks,
+                              int64_t *out) {
+    if (blockIdx.x != 0 || threadIdx.x != 0) return;
+    int64_t pos = 0, nb = 0, total = 0, status = 0;
+    while (pos < n) {
+        if (n - pos < 25 || nb >= max_blocks) {
+            status = 1;
+            break;
+        }
+        const uint8_t *h = src + pos + 16;
+        const uint32_t method = h[0];
+        const uint32_t csize = (uint32_t)h[1] | ((uint32_t)h[2] << 8) | ((uint32_t)h[3] << 16) | ((uint32_t)h[4] << 24);
+        const uint32_t usize = (uint32_t)h[5] | ((uint32_t)h[6] << 8) | ((uint32_t)h[7] << 16) | ((uint32_t)h[8] << 24);
+        if ((method != 0x82 && method != 0x02) || csize < 9 || pos + 16 + (int64_t)csize > n ||
+            (method == 0x02 && csize - 9 != usize)) {
+            status = method != 0x82 && method != 0x02 ? 2 : 1;
+            break;
+        }
+        tab[nb].src = pos + 25;
+        tab[nb].dst = total;
+        tab[nb].csize = csize - 9;
+        tab[nb].usize = usize;
+        tab[nb].method = method;
+        ++nb;
+        total += usize;
+        pos += 16 + csize;
+    }
+    out[0] = nb;
+    out[1] = total;
+    out[2] = status;
+}
+
+// all lanes see the same values (uniform parse); bytes of the compressed input
+__device__ __forceinline__ uint32_t in_byte(const uint8_t *p, int64_t i) { return p[i]; }
+
+__global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, const IngestBlock *tab, int64_t nblocks,
+                                                      uint8_t *dst, int *status) {
+    __shared__ uint8_t ring[kRing];
+    const int lane = threadIdx.x;
+    for (int64_t bi = blockIdx.x; bi < nblocks; bi += gridDim.x) {
+        const IngestBlock blk = tab[bi];
+        const uint8_t *ip0 = src + blk.src;
+        uint8_t *out = dst + blk.dst;
+        const int64_t isz = blk.csize, osz = blk.usize;
+        if (blk.method == 0x02) {
+            for (int64_t i = lane; i < osz; i += 64) out[i] = ip0[i];
+            continue;
+        }
+        int64_t ip = 0, op = 0;
+        bool bad = false;
+        for (;;) {
+            if (ip >= isz) {
+                bad = true;
+                break;
+            }
+            const uint32_t token = in_byte(ip0, ip++);
+            int64_t len = token >> 4;
+            if (len == 15) {
+                uint32_t s;
+                do {
+                    if (ip >= isz) {
+                        bad = true;
+                        break;
+                    }
+                    s = in_byte(ip0, ip++);
+                    len += s;
+                } while (s == 255);
+                if (bad) break;
+            }
+            if (len > osz - op || len > isz - ip) {
+                bad = true;
+                break;
+            }
+            // literals: 256 bytes per step, 4 per lane in flight
+            for (int64_t b0 = 0; b0 < len; b0 += 256) {
+                uint8_t v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int64_t i = b0 + u * 64 + lane;
+                    v[u] = i < len ? ip0[ip + i] : 0;
+                }
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int64_t i = b0 + u * 64 + lane;
+                    if (i < len) {
+                        out[op + i] = v[u];
+                        ring[(op + i) & (kRing - 1)] = v[u];
+                    }
+                }
+            }
+            op += len;
+            ip += len;
+            if (op == osz) break;
+            if (isz - ip < 2) {
+                bad = true;
+                break;
+            }
+            const int64_t off = (int64_t)in_byte(ip0, ip) | ((int64_t)in_byte(ip0, ip + 1) << 8);
+            ip += 2;
+            if (off == 0 || off > op) {
+                bad = true;
+                break;
+            }
+            int64_t mlen = token & 15;
+            if (mlen == 15) {
+                uint32_t s;
+                do {
+                    if (ip >= isz) {
+                        bad = true;
+                        break;
+                    }
+                    s = in_byte(ip0, ip++);
+                    mlen += s;
+                } while (s == 255);
+                if (bad) break;
+            }
+            mlen += 4;
+            if (mlen > osz - op) {
+                bad = true;
+                break;
+            }
+            __syncthreads();  // literal bytes in the ring before the match reads them
+            // steps of at most min(off, 256) bytes: every byte a step reads was
+            // written by an earlier step
+            const int64_t step = off < 256 ? off : 256;
+            for (int64_t d0 = 0; d0 < mlen; d0 += step) {
+                const int64_t cnt = mlen - d0 < step ? mlen - d0 : step;
+                uint8_t v[4];
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int64_t i = u * 64 + lane;
+                    v[u] = i < cnt ? ring[(op + d0 + i - off) & (kRing - 1)] : 0;
+                }
+                __syncthreads();
+#pragma unroll
+                for (int u = 0; u < 4; ++u) {
+                    const int64_t i = u * 64 + lane;
+                    if (i < cnt) {
+                        out[op + d0 + i] = v[u];
+                        ring[(op + d0 + i) & (kRing - 1)] = v[u];
+                    }
+                }
+                __syncthreads();
+            }
+            op += mlen;
+        }
+        if (bad && lane == 0) atomicOr(status, 4);
+        __syncthreads();
+    }
+}
+
+// ---- array sizes -> element offsets (exclusive scan over n UInt64) ----------
+constexpr int kScanTile = 4096;  // sizes per workgroup (256 threads x 16)
+
+__global__ __launch_bounds__(256) void k_sizes_partial(const uint64_t *sizes, int64_t n, int d, int64_t *tile_sum,
+                                                       int64_t *stats) {
+    __shared__ int64_t red[256];
+    __shared__ int64_t cnt[256];
+    const int64_t base = (int64_t)blockIdx.x * kScanTile;
+    int64_t s = 0, notd = 0;
+    for (int i = threadIdx.x; i < kScanTile; i += 256) {
+        const int64_t r = base + i;
+        if (r < n) {
+            s += (int64_t)sizes[r];
+            notd += sizes[r] != (uint64_t)d;
+        }
+    }
+    red[threadIdx.x] = s;
+    cnt[threadIdx.x] = notd;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+        if (threadIdx.x < o) {
+            red[threadIdx.x] += red[threadIdx.x + o];
+            cnt[threadIdx.x] += cnt[threadIdx.x + o];
+        }
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) {
+        tile_sum[blockIdx.x] = red[0];
+        if (cnt[0]) atomicAdd((unsigned long long *)&stats[0], (unsigned long long)cnt[0]);
+    }
+}
+
+// exclusive prefix of the tile sums in place (one workgroup); total -> stats[1]
+__global__ __launch_bounds__(1024) void k_sizes_top(int64_t *tile_sum, int64_t ntiles, int64_t *stats) {
+    __shared__ int64_t part[1024];
+    const int t = threadIdx.x;
+    const int64_t per = (ntiles + 1023) / 1024;
+    const int64_t b = t * per, e = min(ntiles, b + per);
+    int64_t s = 0;
+    for (int64_t i = b; i < e; ++i) s += tile_sum[i];
+    part[t] = s;
+    __syncthreads();
+    if (t == 0) {
+        int64_t acc = 0;
+        for (int i = 0; i < 1024; ++i) {
+            const int64_t v = part[i];
+            part[i] = acc;
+            acc += v;
+        }
+        stats[1] = acc;
+    }
+    __syncthreads();
+    int64_t run = part[t];
+    for (int64_t i = b; i < e; ++i) {
+        const int64_t v = tile_sum[i];
+        tile_sum[i] = run;
+        run += v;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_sizes_final(const uint64_t *sizes, int64_t n, const int64_t *tile_base,
+                                                     int64_t *offsets) {
+    __shared__ int64_t wsum[4];
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int64_t base = (int64_t)blockIdx.x * kScanTile;
+    // thread t owns sizes [base + 16 t, base + 16 t + 16)
+    int64_t v[16], s = 0;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int64_t r = base + 16 * t + i;
+        v[i] = r < n ? (int64_t)sizes[r] : 0;
+        s += v[i];
+    }
+    int64_t inc = s;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+    }
+    if (lane == 63) wsum[w] = inc;
+    __syncthreads();
+    int64_t run = tile_base[blockIdx.x] + inc - s;
+    for (int x = 0; x < w; ++x) run += wsum[x];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+        const int64_t r = base + 16 * t + i;
+        if (r < n) offsets[r] = run;
+        run += v[i];
+    }
+}
+
+__global__ __launch_bounds__(256) void k_array_rows(const float *data, const int64_t *offsets, const uint64_t *sizes,
+                                                    int64_t n, int d, float *rows, uint8_t *nonempty) {
+    const float FLTMAX = 3.40282347e+38f;
+    for (int64_t r = blockIdx.x; r < n; r += gridDim.x) {
+        const int64_t sz = (int64_t)sizes[r], off = offsets[r];
+        for (int j = threadIdx.x; j < d; j += 256) rows[r * d + j] = j < sz ? data[off + j] : FLTMAX;
+        if (threadIdx.x == 0) nonempty[r] = sz > 0;
+    }
+}
+
+// ---- launchers ----------------------------------------------------------------
+
+void launch_block_table(const uint8_t *src, int64_t n, IngestBlock *tab, int64_t max_blocks, int64_t *out,
+                        hipStream_t s) {
+    hipLaunchKernelGGL(k_block_table, dim3(1), dim3(1), 0, s, src, n, tab, max_blocks, out);
+}
+
+void launch_decode_blocks(const uint8_t *src, const IngestBlock *tab, int64_t nblocks, uint8_t *dst, int *status,
+                          hipStream_t s) {
+    if (nblocks <= 0) return;
+    const int grid = (int)std::min<int64_t>(nblocks, 4096);
+    hipLaunchKernelGGL(k_decode_blocks, dim3(grid), dim3(64), 0, s, src, tab, nblocks, dst, status);
+}
+
+// offsets[n] (exclusive); stats[0] += rows whose size != d, stats[1] = total
+// elements (stats zeroed by the caller); scratch >= ceil(n / 4096) int64
+void launch_sizes_scan(const uint64_t *sizes, int64_t n, int d, int64_t *offsets, int64_t *scratch, int64_t *stats,
+                       hipStream_t s) {
+    const int64_t tiles = std::max<int64_t>(1, (n + kScanTile - 1) / kScanTile);
+    hipLaunchKernelGGL(k_sizes_partial, dim3((unsigned)tiles), dim3(256), 0, s, sizes, n, d, scratch, stats);
+    hipLaunchKernelGGL(k_sizes_top, dim3(1), dim3(1024), 0, s, scratch, tiles, stats);
+    hipLaunchKernelGGL(k_sizes_final, dim3((unsigned)tiles), dim3(256), 0, s, sizes, n, scratch, offsets);
+}
+
+void launch_array_rows(const float *data, const int64_t *offsets, const uint64_t *sizes, int64_t n, int d,
+                       float *rows, uint8_t *nonempty, hipStream_t s) {
+    if (n <= 0) return;
+    const int grid = (int)std::min<int64_t>(n, 65536);
+    hipLaunchKernelGGL(k_array_rows, dim3(grid), dim3(256), 0, s, data, offsets, sizes, n, d, rows, nonempty);
+}
+
+}  // namespace mqvs

@@ -926,6 +926,123 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
     g_stats = st;
 }
 
+
+// ---------------------------------------------------------------------------
+// column ingest: the compressed files of a part's Array(Float32) column,
+// decoded in HBM (kernels_ingest.hip) into the rows matrix + nonempty flags of
+// MergeTreeVSManager.cpp:1381-1393, then prepared like any segment.
+
+struct IngestTmp {
+    std::vector<void *> bufs;
+    void *alloc(size_t bytes) {
+        void *p = nullptr;
+        if (hipMalloc(&p, std::max<size_t>(bytes, 16)) != hipSuccess) {
+            (void)hipGetLastError();
+            fail(MQVS_ERR_MEMORY_LIMIT, "HBM allocation of " + std::to_string(bytes) + " bytes failed");
+        }
+        bufs.push_back(p);
+        return p;
+    }
+    ~IngestTmp() {
+        for (void *p : bufs) (void)hipFree(p);
+    }
+};
+
+// block table of one compressed stream; returns (blocks, decompressed bytes)
+static std::pair<int64_t, int64_t> stream_table(IngestTmp &tmp, const uint8_t *dsrc, int64_t n, IngestBlock **tab,
+                                                int64_t *hbuf, const char *what, hipStream_t s) {
+    const int64_t maxb = n / 25 + 1;
+    *tab = (IngestBlock *)tmp.alloc(sizeof(IngestBlock) * (size_t)maxb);
+    int64_t *dout = (int64_t *)tmp.alloc(4 * sizeof(int64_t));
+    launch_block_table(dsrc, n, *tab, maxb, dout, s);
+    MQVS_HIP(hipGetLastError());
+    MQVS_HIP(hipMemcpyAsync(hbuf, dout, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+    MQVS_HIP(hipStreamSynchronize(s));
+    if (hbuf[2] == 2)
+        fail(MQVS_ERR_NOT_IMPLEMENTED, std::string(what) + ": compression method other than LZ4 / NONE");
+    if (hbuf[2])
+        fail(MQVS_ERR_ILLEGAL_COLUMN, std::string(what) + ": malformed compressed block chain (CANNOT_DECOMPRESS)");
+    return {hbuf[0], hbuf[1]};
+}
+
+static mqvs_segment *ingest_column(const uint8_t *data_bin, int64_t data_bytes, const uint8_t *sizes_bin,
+                                   int64_t sizes_bytes, int64_t n, int32_t d, int32_t metric, int64_t granule,
+                                   int64_t row_offset, uint32_t flags) {
+    check_seg_args(n, d, metric, granule, row_offset);
+    if (data_bytes < 0 || sizes_bytes < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "negative stream size");
+    if ((data_bytes > 0 && !data_bin) || (sizes_bytes > 0 && !sizes_bin))
+        fail(MQVS_ERR_BAD_ARGUMENTS, "null column stream");
+    const bool dev = flags & MQVS_F_DEVICE_PTRS;
+    mqvs_segment *seg = new_segment(n, d, metric, granule, row_offset);
+    try {
+        Workspace &ws = workspace(seg->device);
+        hipStream_t s = ws.stream;
+        IngestTmp tmp;
+        const uint8_t *dd = data_bin, *ds = sizes_bin;
+        if (!dev) {
+            auto *a = (uint8_t *)tmp.alloc((size_t)data_bytes);
+            auto *b = (uint8_t *)tmp.alloc((size_t)sizes_bytes);
+            if (data_bytes) MQVS_HIP(hipMemcpyAsync(a, data_bin, (size_t)data_bytes, hipMemcpyHostToDevice, s));
+            if (sizes_bytes) MQVS_HIP(hipMemcpyAsync(b, sizes_bin, (size_t)sizes_bytes, hipMemcpyHostToDevice, s));
+            dd = a;
+            ds = b;
+        }
+        int64_t *h = reinterpret_cast<int64_t *>(ws.host_flags + 16);
+        IngestBlock *tab_s = nullptr, *tab_d = nullptr;
+        const auto sz = stream_table(tmp, ds, sizes_bytes, &tab_s, h, "array sizes stream", s);
+        if (sz.second != 8 * n)
+            fail(MQVS_ERR_ILLEGAL_COLUMN, "array sizes stream holds " + std::to_string(sz.second) + " bytes for " +
+                                              std::to_string(n) + " rows");
+        const auto dt = stream_table(tmp, dd, data_bytes, &tab_d, h, "vector data stream", s);
+        if (dt.second % 4) fail(MQVS_ERR_ILLEGAL_COLUMN, "vector data stream is not a whole number of Float32");
+        int *status = (int *)tmp.alloc(sizeof(int) * 4);
+        MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
+        auto *sizes = (uint64_t *)tmp.alloc(sizeof(uint64_t) * (size_t)std::max<int64_t>(n, 1));
+        launch_decode_blocks(ds, tab_s, sz.first, (uint8_t *)sizes, status, s);
+        // the common case (every array has d elements) decodes straight into the rows
+        const bool direct = dt.second == 4 * n * (int64_t)d;
+        float *data = direct ? seg->rows : (float *)tmp.alloc((size_t)dt.second);
+        launch_decode_blocks(dd, tab_d, dt.first, (uint8_t *)data, status, s);
+        MQVS_HIP(hipGetLastError());
+        const int64_t tiles = std::max<int64_t>(1, (n + 4095) / 4096);
+        auto *offs = (int64_t *)tmp.alloc(sizeof(int64_t) * (size_t)std::max<int64_t>(n, 1));
+        auto *scratch = (int64_t *)tmp.alloc(sizeof(int64_t) * (size_t)tiles);
+        auto *st = (int64_t *)tmp.alloc(sizeof(int64_t) * 4);
+        MQVS_HIP(hipMemsetAsync(st, 0, sizeof(int64_t) * 4, s));
+        if (n > 0) launch_sizes_scan(sizes, n, d, offs, scratch, st, s);
+        MQVS_HIP(hipGetLastError());
+        MQVS_HIP(hipMemcpyAsync(h, st, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        int *hstatus = reinterpret_cast<int *>(h + 2);
+        MQVS_HIP(hipMemcpyAsync(hstatus, status, sizeof(int), hipMemcpyDeviceToHost, s));
+        MQVS_HIP(hipStreamSynchronize(s));
+        if (*hstatus)
+            fail(MQVS_ERR_ILLEGAL_COLUMN, "malformed LZ4 block (CANNOT_DECOMPRESS)");
+        const int64_t notd = h[0], nelem = h[1];
+        if (nelem * 4 != dt.second)
+            fail(MQVS_ERR_ILLEGAL_COLUMN, "array sizes sum to " + std::to_string(nelem) + " elements, the data stream "
+                                              "holds " + std::to_string(dt.second / 4));
+        const uint8_t *nonempty = nullptr;
+        if (!(direct && notd == 0)) {
+            // ragged or empty arrays: the reference's copy loop
+            const float *srcdata = data;
+            if (direct) {
+                auto *copy = (float *)tmp.alloc((size_t)dt.second);
+                MQVS_HIP(hipMemcpyAsync(copy, data, (size_t)dt.second, hipMemcpyDeviceToDevice, s));
+                srcdata = copy;
+            }
+            auto *ne = (uint8_t *)tmp.alloc((size_t)std::max<int64_t>(n, 1));
+            launch_array_rows(srcdata, offs, sizes, n, d, seg->rows, ne, s);
+            MQVS_HIP(hipGetLastError());
+            nonempty = ne;
+        }
+        prepare_segment(seg, nonempty, s);  // synchronises the stream
+    } catch (...) {
+        free_segment(seg);
+        throw;
+    }
+    return seg;
+}
+
 // ---------------------------------------------------------------------------
 // services for the index path (index.hip)
 
@@ -1135,6 +1252,17 @@ int mqvs_knn_raw(const float *x, const float *y, int64_t d, int64_t k, int64_t n
             throw;
         }
         free_segment(s);
+    });
+}
+
+int mqvs_segment_create_from_column(const uint8_t *data_bin, int64_t data_bytes, const uint8_t *sizes_bin,
+                                    int64_t sizes_bytes, int64_t n, int32_t d, int32_t metric, int64_t granule_rows,
+                                    int64_t row_offset, uint32_t flags, mqvs_segment_t *out) {
+    return guarded([&] {
+        if (!out) fail(MQVS_ERR_BAD_ARGUMENTS, "null output handle");
+        *out = nullptr;
+        *out = ingest_column(data_bin, data_bytes, sizes_bin, sizes_bytes, n, d, metric, granule_rows, row_offset,
+                             flags);
     });
 }
 

@@ -270,6 +270,24 @@ void launch_chunk_ordinals(const uint8_t *filter, const uint8_t *nonempty, const
                            int64_t n, int64_t chunk_rows, int require_filter, int *ord,
                            hipStream_t s);
 
+// column ingest (kernels_ingest.hip): compressed MergeTree column files -> rows
+struct IngestBlock {
+    int64_t src;      // payload offset in the compressed stream
+    int64_t dst;      // offset in the decompressed stream
+    uint32_t csize;   // payload bytes
+    uint32_t usize;   // decompressed bytes
+    uint32_t method;  // 0x82 LZ4, 0x02 NONE
+    uint32_t pad;
+};
+void launch_block_table(const uint8_t *src, int64_t n, IngestBlock *tab, int64_t max_blocks, int64_t *out,
+                        hipStream_t s);
+void launch_decode_blocks(const uint8_t *src, const IngestBlock *tab, int64_t nblocks, uint8_t *dst, int *status,
+                          hipStream_t s);
+void launch_sizes_scan(const uint64_t *sizes, int64_t n, int d, int64_t *offsets, int64_t *scratch, int64_t *stats,
+                       hipStream_t s);
+void launch_array_rows(const float *data, const int64_t *offsets, const uint64_t *sizes, int64_t n, int d,
+                       float *rows, uint8_t *nonempty, hipStream_t s);
+
 // binary vectors (kernels_binary.hip)
 void launch_scan_binary(const ScanParams &p, int metric, bool probe, hipStream_t s);
 void launch_hamming_to_int(const int64_t *ids, float *dist, int64_t m, hipStream_t s);

@@ -105,6 +105,32 @@ class VectorScanSegment:
         return cls(h, n, d, m, granule, row_offset)
 
     @classmethod
+    def from_column(cls, data_bin, sizes_bin, n, d, metric="L2", granule=DEFAULT_GRANULE, row_offset=0):
+        """A part's Array(Float32) column from its compressed files, decoded on
+        the GPU (mqvs_segment_create_from_column): data_bin = `<col>.bin`
+        bytes, sizes_bin = `<col>.size0.bin` bytes (bytes / numpy uint8, or
+        torch uint8 CUDA tensors)."""
+        m = metric_id(metric)
+        h = ctypes.c_void_p()
+        if _is_torch(data_bin):
+            flags = F_DEVICE_PTRS
+            dp, dn = _ptr(data_bin), data_bin.numel()
+            sp, sn = _ptr(sizes_bin), sizes_bin.numel()
+            keep = None
+        else:
+            flags = 0
+            a = np.frombuffer(bytes(data_bin), np.uint8) if isinstance(data_bin, (bytes, bytearray)) \
+                else _host_u8(data_bin)
+            b = np.frombuffer(bytes(sizes_bin), np.uint8) if isinstance(sizes_bin, (bytes, bytearray)) \
+                else _host_u8(sizes_bin)
+            keep = (a, b)
+            dp, dn, sp, sn = _ptr(a), a.size, _ptr(b), b.size
+        check(lib.mqvs_segment_create_from_column(dp, dn, sp, sn, n, d, m, granule, row_offset, flags,
+                                                  ctypes.byref(h)))
+        del keep
+        return cls(h, n, d, m, granule, row_offset)
+
+    @classmethod
     def generate(cls, seed, mode, n, d, metric="L2", granule=DEFAULT_GRANULE, row_offset=0):
         """Synthetic part from the counter-based generator (mode 0 exact, 1 gauss, 2 mixture)."""
         m = metric_id(metric)

@@ -875,3 +875,196 @@ int orc_vector_scan_binary(const uint8_t *rows, int64_t n, int64_t nbytes,
     }
     return 0;
 }
+
+/* ------------------------------------------------------------------------ */
+/* Column ingest: a MergeTree Array(Float32) column as its
+ * compressed files -- the nested Float32 stream (`<col>.bin`) and the array
+ * sizes stream (`<col>.size0.bin`, UInt64 per row) -- decoded into the rows
+ * matrix of MergeTreeVSManager.cpp:1381-1393.
+ *
+ * Framing (CompressedReadBufferBase.cpp:115-160, CompressionInfo.h:22-49):
+ * per block 16-B CityHash128 checksum, then a 9-B header: method byte
+ * (0x82 LZ4, 0x02 NONE), UInt32 compressed size (header + payload), UInt32
+ * decompressed size; then the payload.  Checksums are not verified here.
+ *
+ * LZ4 block format as LZ4_decompress_faster.cpp:480-640 decodes it: token
+ * (literal length high nibble, match length - 4 low nibble, 15 = extended by
+ * 255-continued bytes), literals, 2-B little-endian offset, match copy (may
+ * overlap); the block ends when a literal run reaches the decompressed size. */
+
+static inline uint32_t rd32(const uint8_t *p) {
+    return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+/* Returns 0, or -1 on malformed input (ClickHouse: CANNOT_DECOMPRESS). */
+int orc_lz4_decompress(const uint8_t *src, int64_t src_size, uint8_t *dst, int64_t dst_size) {
+    const uint8_t *ip = src, *iend = src + src_size;
+    uint8_t *op = dst, *oend = dst + dst_size;
+    for (;;) {
+        if (ip >= iend) return -1;
+        const unsigned token = *ip++;
+        size_t length = token >> 4;
+        if (length == 15) {
+            unsigned s;
+            do {
+                if (ip >= iend) return -1;
+                s = *ip++;
+                length += s;
+            } while (s == 255);
+        }
+        if ((int64_t)length > oend - op || (int64_t)length > iend - ip) return -1;
+        memcpy(op, ip, length);
+        op += length;
+        ip += length;
+        if (op == oend) return 0;
+        if (iend - ip < 2) return -1;
+        const size_t offset = (size_t)ip[0] | ((size_t)ip[1] << 8);
+        ip += 2;
+        if (offset == 0 || (int64_t)offset > op - dst) return -1;
+        length = token & 15;
+        if (length == 15) {
+            unsigned s;
+            do {
+                if (ip >= iend) return -1;
+                s = *ip++;
+                length += s;
+            } while (s == 255);
+        }
+        length += 4;
+        if ((int64_t)length > oend - op) return -1;
+        const uint8_t *match = op - offset;
+        for (size_t i = 0; i < length; i++) op[i] = match[i]; /* byte order: overlap replicates */
+        op += length;
+    }
+}
+
+/* Test-data LZ4 compressor (greedy, 4-byte hash, 64 KiB window) producing the
+ * standard block format (last 5 bytes literal, no match starting in the last
+ * 12 bytes).  Returns the compressed size, or -1 if cap is too small. */
+int64_t orc_lz4_compress(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap) {
+    enum { HBITS = 16 };
+    int64_t *table = (int64_t *)malloc(sizeof(int64_t) << HBITS);
+    for (int64_t i = 0; i < ((int64_t)1 << HBITS); i++) table[i] = -1;
+    int64_t ip = 0, anchor = 0, o = 0;
+    const int64_t mflimit = n - 12;
+#define EMIT_LEN(v)                                       \
+    do {                                                  \
+        int64_t v_ = (v);                                 \
+        while (v_ >= 255) {                               \
+            if (o >= cap) goto fail;                      \
+            dst[o++] = 255;                               \
+            v_ -= 255;                                    \
+        }                                                 \
+        if (o >= cap) goto fail;                          \
+        dst[o++] = (uint8_t)v_;                           \
+    } while (0)
+    while (ip < mflimit) {
+        const uint32_t seq = rd32(src + ip);
+        const uint32_t h = (seq * 2654435761u) >> (32 - HBITS);
+        const int64_t ref = table[h];
+        table[h] = ip;
+        if (ref < 0 || ip - ref > 65535 || rd32(src + ref) != seq) {
+            ip++;
+            continue;
+        }
+        int64_t mlen = 4;
+        while (ip + mlen < n - 5 && src[ref + mlen] == src[ip + mlen]) mlen++;
+        const int64_t lit = ip - anchor;
+        if (o >= cap) goto fail;
+        const int64_t tok = o++;
+        dst[tok] = (uint8_t)(((lit >= 15 ? 15 : lit) << 4) | (mlen - 4 >= 15 ? 15 : mlen - 4));
+        if (lit >= 15) EMIT_LEN(lit - 15);
+        if (o + lit + 2 > cap) goto fail;
+        memcpy(dst + o, src + anchor, lit);
+        o += lit;
+        dst[o++] = (uint8_t)((ip - ref) & 255);
+        dst[o++] = (uint8_t)((ip - ref) >> 8);
+        if (mlen - 4 >= 15) EMIT_LEN(mlen - 4 - 15);
+        ip += mlen;
+        anchor = ip;
+    }
+    {
+        const int64_t lit = n - anchor;
+        if (o >= cap) goto fail;
+        dst[o++] = (uint8_t)((lit >= 15 ? 15 : lit) << 4);
+        if (lit >= 15) EMIT_LEN(lit - 15);
+        if (o + lit > cap) goto fail;
+        memcpy(dst + o, src + anchor, lit);
+        o += lit;
+    }
+#undef EMIT_LEN
+    free(table);
+    return o;
+fail:
+    free(table);
+    return -1;
+}
+
+/* CompressedWriteBuffer framing of `n` bytes in blocks of at most block_size
+ * (method 0x82 LZ4 or 0x02 NONE); checksum bytes are written as zero. */
+int64_t orc_compress_stream(const uint8_t *src, int64_t n, int64_t block_size, int method, uint8_t *dst,
+                            int64_t cap) {
+    int64_t o = 0;
+    for (int64_t b = 0; b < n; b += block_size) {
+        const int64_t len = (n - b) < block_size ? (n - b) : block_size;
+        if (o + 25 > cap) return -1;
+        memset(dst + o, 0, 16);
+        uint8_t *hdr = dst + o + 16;
+        int64_t payload;
+        if (method == 0x02) {
+            if (o + 25 + len > cap) return -1;
+            memcpy(hdr + 9, src + b, len);
+            payload = len;
+        } else {
+            payload = orc_lz4_compress(src + b, len, hdr + 9, cap - (o + 25));
+            if (payload < 0) return -1;
+        }
+        hdr[0] = (uint8_t)method;
+        const uint32_t csize = (uint32_t)(9 + payload), usize = (uint32_t)len;
+        memcpy(hdr + 1, &csize, 4);
+        memcpy(hdr + 5, &usize, 4);
+        o += 25 + payload;
+    }
+    return o;
+}
+
+/* CompressedReadBuffer over a whole stream: returns the decompressed size,
+ * or -1 (malformed framing / payload, or more than cap bytes). */
+int64_t orc_decompress_stream(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap) {
+    int64_t pos = 0, o = 0;
+    while (pos < n) {
+        if (n - pos < 25) return -1;
+        const uint8_t method = src[pos + 16];
+        const int64_t csize = rd32(src + pos + 17), usize = rd32(src + pos + 21);
+        if (csize < 9 || pos + 16 + csize > n || o + usize > cap) return -1;
+        const uint8_t *payload = src + pos + 25;
+        if (method == 0x82) {
+            if (orc_lz4_decompress(payload, csize - 9, dst + o, usize)) return -1;
+        } else if (method == 0x02) {
+            if (csize - 9 != usize) return -1;
+            memcpy(dst + o, payload, usize);
+        } else {
+            return -1;
+        }
+        o += usize;
+        pos += 16 + csize;
+    }
+    return o;
+}
+
+/* MergeTreeVSManager.cpp:1381-1393: rows pre-filled with FLT_MAX; a non-empty
+ * array copies its first min(size, d) elements (a shorter one keeps FLT_MAX
+ * in the rest); nonempty[r] = size > 0.  Returns -1 if the sizes need more
+ * elements than `nelem`. */
+int orc_array_rows(const float *data, int64_t nelem, const uint64_t *sizes, int64_t n, int64_t d, float *rows,
+                   uint8_t *nonempty) {
+    int64_t off = 0;
+    for (int64_t r = 0; r < n; r++) {
+        const int64_t sz = (int64_t)sizes[r];
+        if (off + sz > nelem) return -1;
+        for (int64_t j = 0; j < d; j++) rows[r * d + j] = (j < sz) ? data[off + j] : FLT_MAX;
+        nonempty[r] = sz > 0;
+        off += sz;
+    }
+    return off == nelem ? 0 : -1;
+}

@@ -134,6 +134,20 @@ int orc_vector_scan_binary(const uint8_t *rows, int64_t n, int64_t nbytes,
                            int64_t nq, int64_t k, int metric, const uint8_t *filter,
                            const uint8_t *row_exists, int64_t *out_ids, float *out_dist);
 
+/* ---- column ingest: MergeTree Array(Float32) files -> rows -------------
+ * LZ4 block format as src/Compression/LZ4_decompress_faster.cpp:480-640
+ * decodes it; 0 or -1 (CANNOT_DECOMPRESS). */
+int orc_lz4_decompress(const uint8_t *src, int64_t src_size, uint8_t *dst, int64_t dst_size);
+/* test-data compressor (standard LZ4 block format); size or -1 */
+int64_t orc_lz4_compress(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap);
+/* CompressedWriteBuffer / CompressedReadBuffer framing (zero checksums) */
+int64_t orc_compress_stream(const uint8_t *src, int64_t n, int64_t block_size, int method, uint8_t *dst,
+                            int64_t cap);
+int64_t orc_decompress_stream(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap);
+/* MergeTreeVSManager.cpp:1381-1393 copy loop: FLT_MAX fill, truncation at d */
+int orc_array_rows(const float *data, int64_t nelem, const uint64_t *sizes, int64_t n, int64_t d, float *rows,
+                   uint8_t *nonempty);
+
 #ifdef __cplusplus
 }
 #endif

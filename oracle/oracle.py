@@ -52,6 +52,14 @@ def lib():
         L.orc_jaccard.restype = ctypes.c_float
         L.orc_knn_binary.argtypes = [P, P, I64, I64, I64, I64, ctypes.c_int, P, P]
         L.orc_vector_scan_binary.argtypes = [P, I64, I64, P, I64, P, I64, I64, ctypes.c_int, P, P, P, P]
+        L.orc_lz4_decompress.argtypes = [P, I64, P, I64]
+        L.orc_lz4_compress.argtypes = [P, I64, P, I64]
+        L.orc_lz4_compress.restype = I64
+        L.orc_compress_stream.argtypes = [P, I64, I64, ctypes.c_int, P, I64]
+        L.orc_compress_stream.restype = I64
+        L.orc_decompress_stream.argtypes = [P, I64, P, I64]
+        L.orc_decompress_stream.restype = I64
+        L.orc_array_rows.argtypes = [P, I64, P, I64, I64, P, P]
         L.orc_generate.argtypes = [ctypes.c_uint64, ctypes.c_int, I64, I64, I64, P]
         L.orc_gemm_dot.argtypes = [P, P, I64]
         L.orc_gemm_dot.restype = ctypes.c_float
@@ -173,6 +181,38 @@ def vector_scan_binary(codes, queries, k, metric, mark_rows, filter_bits=None, r
                                     _p(rb), _p(ids), _p(dist)):
         raise NotImplementedError
     return ids, dist
+
+
+def compress_stream(data: bytes | np.ndarray, block_size=1 << 20, method=0x82) -> bytes:
+    """ClickHouse CompressedWriteBuffer framing + LZ4 (test data; zero checksums)."""
+    src = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else _u8(data.view(np.uint8))
+    cap = int(src.size + src.size // 200 + 64 * (src.size // block_size + 1) + 1024)
+    out = np.empty(cap, np.uint8)
+    n = lib().orc_compress_stream(_p(src), src.size, block_size, method, _p(out), cap)
+    if n < 0:
+        raise ValueError("compress_stream failed")
+    return out[:n].tobytes()
+
+
+def decompress_stream(blob: bytes, cap: int) -> bytes:
+    src = np.frombuffer(blob, np.uint8)
+    out = np.empty(max(cap, 1), np.uint8)
+    n = lib().orc_decompress_stream(_p(src), src.size, _p(out), cap)
+    if n < 0:
+        raise ValueError("CANNOT_DECOMPRESS")
+    return out[:n].tobytes()
+
+
+def array_rows(data_f32, sizes_u64, d):
+    """MergeTreeVSManager.cpp:1381-1393: (rows[n,d] float32, nonempty[n] uint8)."""
+    data = _f32(data_f32).reshape(-1)
+    sizes = np.ascontiguousarray(sizes_u64, np.uint64)
+    n = sizes.size
+    rows = np.empty((n, d), np.float32)
+    ne = np.empty(n, np.uint8)
+    if lib().orc_array_rows(_p(data), data.size, _p(sizes), n, d, _p(rows), _p(ne)):
+        raise ValueError("array sizes do not match the data stream")
+    return rows, ne
 
 
 def scan_parts(rows, queries, k, metric, granule, parts, threads):
