@@ -442,6 +442,8 @@ static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, c
     p.lq = (int *)b.lq.get(sizeof(int) * E);
     // 32-query work items when lists are probed by many queries (each A
     // fragment then feeds two MFMAs)
+    // (64-query items, QB = 4, measured slower on the dense coarse pass at
+    // d = 768: its 99 KiB LDS tile leaves one workgroup per CU)
     p.qg = (dense || E >= 24 * nlist) ? 32 : 16;
     // work items = sum over probed lists of groups x 512-position slices
     const int64_t max_items = (E / p.qg + std::min<int64_t>(E, nlist)) * (max_list / 512 + 1);

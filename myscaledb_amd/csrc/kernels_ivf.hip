@@ -85,6 +85,93 @@ __global__ __launch_bounds__(256) void k_plan_count(IvfParams p) {
     }
 }
 
+// nlist <= 16 x kPlanThreads: wave w owns lists [w S, (w + 1) S) (S a
+// multiple of 64) and walks them 64 at a time, lane l on list w S + 64 s + l,
+// so every load is coalesced; the (pair count, length) of its <= 16 steps stay
+// in registers.  The three prefix sums (pairs, work items, streamed rows) are
+// wave scans with a carry, then one combine over the 16 wave totals.
+__global__ __launch_bounds__(kPlanThreads) void k_plan_lists_reg(IvfParams p) {
+    constexpr int ST = 16;
+    constexpr int NWV = kPlanThreads / 64;
+    __shared__ int64_t sh[3][NWV];
+    const int L = p.nlist;
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int S = ((L + NWV - 1) / NWV + 63) / 64 * 64;
+    const int qs = p.qg == 64 ? 6 : p.qg == 32 ? 5 : 4;  // qg is 16, 32 or 64
+    int cnt[ST], len[ST];
+#pragma unroll
+    for (int u = 0; u < ST; ++u) {
+        const int i = wv * S + 64 * u + lane;
+        const bool in = 64 * u < S && i < L;
+        cnt[u] = in ? p.lcount[i] : 0;
+        len[u] = in ? (int)(p.list_off[i + 1] - p.list_off[i]) : 0;
+    }
+    auto items_of = [&](int u) { return (int64_t)((cnt[u] + p.qg - 1) >> qs) * ((len[u] + kIvfChunk - 1) / kIvfChunk); };
+    auto rows_of = [&](int u) { return (int64_t)((cnt[u] + p.qg - 1) >> qs) * len[u]; };
+    int64_t w0 = 0, w1 = 0, w2 = 0;
+#pragma unroll
+    for (int u = 0; u < ST; ++u) {
+        w0 += cnt[u];
+        w1 += items_of(u);
+        w2 += rows_of(u);
+    }
+    for (int o = 32; o > 0; o >>= 1) {
+        w0 += __shfl_xor(w0, o);
+        w1 += __shfl_xor(w1, o);
+        w2 += __shfl_xor(w2, o);
+    }
+    if (lane == 0) {
+        sh[0][wv] = w0;
+        sh[1][wv] = w1;
+        sh[2][wv] = w2;
+    }
+    __syncthreads();
+    int64_t c0 = 0, c1 = 0, t1 = 0, t2 = 0;
+    for (int w = 0; w < NWV; ++w) {
+        if (w < wv) {
+            c0 += sh[0][w];
+            c1 += sh[1][w];
+        }
+        t1 += sh[1][w];
+        t2 += sh[2][w];
+    }
+#pragma unroll
+    for (int u = 0; u < ST; ++u) {
+        if (64 * u >= S) break;  // wave-uniform
+        const int64_t v0 = cnt[u], v1 = items_of(u);
+        int64_t i0 = v0, i1 = v1;
+        for (int o = 1; o < 64; o <<= 1) {
+            const int64_t y0 = __shfl_up(i0, o), y1 = __shfl_up(i1, o);
+            if (lane >= o) {
+                i0 += y0;
+                i1 += y1;
+            }
+        }
+        const int i = wv * S + 64 * u + lane;
+        if (i < L) {
+            p.lstart[i] = c0 + i0 - v0;
+            int64_t r1 = c1 + i1 - v1;
+            const int g = (cnt[u] + p.qg - 1) >> qs;
+            const int nc = (len[u] + kIvfChunk - 1) / kIvfChunk;
+            for (int j = 0; j < g; ++j)
+                for (int cc = 0; cc < nc; ++cc) {
+                    p.item_list[r1] = i;
+                    p.item_grp[r1] = j;
+                    p.item_chk[r1] = cc;
+                    ++r1;
+                }
+        }
+        c0 += __shfl(i0, 63);
+        c1 += __shfl(i1, 63);
+    }
+    if (t == 0) {
+        *p.nitems = (int)t1;
+        p.stats[1] = t1;
+        p.stats[2] = t2 * p.dpad * 2;
+        p.stats[3] = (int64_t)p.nq * p.nprobe;
+    }
+}
+
 __global__ __launch_bounds__(kPlanThreads) void k_plan_lists(IvfParams p) {
     __shared__ int64_t sh[kPlanThreads + 1];
     const int L = p.nlist;
@@ -409,6 +496,64 @@ __global__ __launch_bounds__(SEL_THREADS) void k_ivf_select(const Cand *cand, co
     }
 }
 
+// Small R (the coarse quantizer: R = nprobe <= 16): one wave per query.  Each
+// lane keeps its RM best (key, row) in registers over a strided slice of the
+// region (8 loads in flight); the wave then pops the R smallest heads (64-bit
+// min over the lanes per pop).  Order = (key, row), like k_ivf_select for a
+// monotone perm.
+template <int METRIC, int RM>
+__global__ __launch_bounds__(256) void k_ivf_select_small(const Cand *cand, const int64_t *qstart, int nq, int R,
+                                                         int64_t *out_rows, int64_t id_offset, float *out_approx) {
+    constexpr int U = 8;
+    const int lane = threadIdx.x & 63;
+    const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (q >= nq) return;  // wave-uniform
+    const Cand *c = cand + qstart[q];
+    const int64_t T = qstart[q + 1] - qstart[q];
+    uint64_t best[RM];
+#pragma unroll
+    for (int i = 0; i < RM; ++i) best[i] = ~0ull;
+    auto insert = [&](uint64_t x) {
+        if (x >= best[RM - 1]) return;
+#pragma unroll
+        for (int j = 0; j < RM; ++j) {
+            const uint64_t lo = x < best[j] ? x : best[j];
+            const uint64_t hi = x < best[j] ? best[j] : x;
+            best[j] = lo;
+            x = hi;
+        }
+    };
+    for (int64_t i0 = lane; i0 < T; i0 += 64 * U) {
+        uint64_t v[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = i0 + 64 * u;
+            const Cand e = i < T ? c[i] : Cand{0.f, 0xFFFFFFFFu};
+            v[u] = e.row == 0xFFFFFFFFu ? ~0ull : ((uint64_t)okey<METRIC>(e.raw) << 32) | e.row;
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) insert(v[u]);
+    }
+    // the R smallest over the wave: pop the smallest head R times
+    int head = 0;
+    for (int i = 0; i < R; ++i) {
+        uint64_t mine = ~0ull;
+#pragma unroll
+        for (int j = 0; j < RM; ++j)
+            if (j == head) mine = best[j];
+        uint64_t m = mine;
+        for (int o = 32; o > 0; o >>= 1) {
+            const uint64_t y = __shfl_xor(m, o);
+            m = y < m ? y : m;
+        }
+        if (mine == m && m != ~0ull) ++head;  // (key, row) pairs are distinct
+        if (lane == 0) {
+            const bool ok = m != ~0ull && (uint32_t)(m >> 32) != 0xFFFFFFFFu;
+            out_rows[(int64_t)q * R + i] = ok ? (int64_t)(uint32_t)m + (out_approx ? id_offset : 0) : -1;
+        }
+    }
+}
+
 // ---- build kernels ---------------------------------------------------------
 
 // plane[pos] = bf16(rows[perm[pos]]) (zero for padding and columns >= d),
@@ -490,7 +635,10 @@ void launch_ivf_plan(const IvfParams &p, hipStream_t s) {
     const int64_t E = (int64_t)p.nq * p.nprobe;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((std::max(E, (int64_t)p.nq) + 255) / 256, 2048));
     hipLaunchKernelGGL(k_plan_count, dim3(grid), dim3(256), 0, s, p);
-    hipLaunchKernelGGL(k_plan_lists, dim3(1), dim3(kPlanThreads), 0, s, p);
+    if (p.nlist <= 16 * kPlanThreads)
+        hipLaunchKernelGGL(k_plan_lists_reg, dim3(1), dim3(kPlanThreads), 0, s, p);
+    else
+        hipLaunchKernelGGL(k_plan_lists, dim3(1), dim3(kPlanThreads), 0, s, p);
     hipLaunchKernelGGL(k_plan_scatter, dim3(grid), dim3(256), 0, s, p);
     hipLaunchKernelGGL(k_plan_queries, dim3(1), dim3(kPlanThreads), 0, s, p);
 }
@@ -498,6 +646,14 @@ void launch_ivf_plan(const IvfParams &p, hipStream_t s) {
 template <int QB>
 static void ivf_scan_t(const IvfParams &p, int metric, int grid, hipStream_t s) {
     const size_t lds = (size_t)16 * QB * (2 * p.dpad + 16);
+    if (lds > 65536) {  // 64-query tiles of wide rows: opt in to more than 64 KiB of LDS
+        MQVS_HIP(hipFuncSetAttribute((const void *)k_ivf_scan<MQVS_METRIC_L2, QB>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        MQVS_HIP(hipFuncSetAttribute((const void *)k_ivf_scan<MQVS_METRIC_IP, QB>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+        MQVS_HIP(hipFuncSetAttribute((const void *)k_ivf_scan<MQVS_METRIC_COSINE, QB>,
+                                     hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+    }
     switch (metric) {
         case MQVS_METRIC_L2:
             hipLaunchKernelGGL((k_ivf_scan<MQVS_METRIC_L2, QB>), dim3(grid), dim3(256), lds, s, p);
@@ -512,7 +668,9 @@ static void ivf_scan_t(const IvfParams &p, int metric, int grid, hipStream_t s) 
 }
 
 void launch_ivf_scan(const IvfParams &p, int metric, int grid, hipStream_t s) {
-    if (p.qg == 32)
+    if (p.qg == 64)
+        ivf_scan_t<4>(p, metric, grid, s);
+    else if (p.qg == 32)
         ivf_scan_t<2>(p, metric, grid, s);
     else
         ivf_scan_t<1>(p, metric, grid, s);
@@ -520,6 +678,25 @@ void launch_ivf_scan(const IvfParams &p, int metric, int grid, hipStream_t s) {
 
 void launch_ivf_select(const Cand *cand, const int64_t *qstart, int nq, int R, int metric, int64_t *out_rows,
                        int64_t id_offset, float *out_approx, int64_t expect_len, hipStream_t s) {
+    if (R <= 16 && !out_approx) {
+        const dim3 grid((unsigned)((nq + 3) / 4));
+#define MQVS_SMALL(M, RM_) \
+    hipLaunchKernelGGL((k_ivf_select_small<M, RM_>), grid, dim3(256), 0, s, cand, qstart, nq, R, out_rows, id_offset, \
+                       out_approx)
+#define MQVS_SMALL_M(M)              \
+    if (R <= 2) MQVS_SMALL(M, 2);      \
+    else if (R <= 4) MQVS_SMALL(M, 4); \
+    else if (R <= 8) MQVS_SMALL(M, 8); \
+    else MQVS_SMALL(M, 16);
+        switch (metric) {
+            case MQVS_METRIC_L2: MQVS_SMALL_M(MQVS_METRIC_L2); break;
+            case MQVS_METRIC_IP: MQVS_SMALL_M(MQVS_METRIC_IP); break;
+            default: MQVS_SMALL_M(MQVS_METRIC_COSINE); break;
+        }
+#undef MQVS_SMALL_M
+#undef MQVS_SMALL
+        return;
+    }
     int N = 1;
     while (N < R) N <<= 1;
     // LDS key cache sized for the expected region length (<= 64 KiB)
