@@ -15,6 +15,6 @@ cat gpurun_out/bench.json
     > "$GRAFT_REPO_ROOT/gpurun_out/prof_bench.json" 2> "$GRAFT_REPO_ROOT/gpurun_out/prof.err" )
 rc=$?; echo "rocprof rc=$rc"; [ $rc -ne 0 ] && exit 1
 [ "$1" = "--no-pmc" ] && exit 0
-bash tools/gpu_pmc.sh python bench.py --steps 2 --warmup 0 --no-cpu --no-verify || exit 1
+bash tools/gpu_pmc.sh python bench.py --steps 2 --warmup 0 --no-cpu --no-verify --no-index || exit 1
 python tools/pmc_traffic.py gpurun_out --searches 2 --out gpurun_out/pmc_traffic.json > /dev/null
 echo "pmc summary rc=$?"
