@@ -11,8 +11,9 @@
 //                   1 MiB block costs one dependent 25-B read.
 //   k_decode_blocks one 64-lane workgroup per block.  LZ4 (LZ4_decompress_faster
 //                   .cpp:480-640 block format): every lane parses the token
-//                   stream in lock-step (uniform control flow), literal and
-//                   match bytes are copied 64 at a time.  Matches read from a
+//                   stream in lock-step (uniform control flow); long literal
+//                   runs are copied as whole output dwords (copy_literals),
+//                   match bytes up to 256 per step.  Matches read from a
 //                   64 KiB LDS ring of the block's latest output (LZ4 offsets
 //                   are < 2^16), never from global memory, so no global
 //                   read-after-write ordering is needed; an overlapping match
@@ -61,19 +62,109 @@ __global__ void k_block_table(const uint8_t *src, int64_t n, IngestBlock *tab, i
 // all lanes see the same values (uniform parse); bytes of the compressed input
 __device__ __forceinline__ uint32_t in_byte(const uint8_t *p, int64_t i) { return p[i]; }
 
-__global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, const IngestBlock *tab, int64_t nblocks,
-                                                      uint8_t *dst, int *status) {
-    __shared__ uint8_t ring[kRing];
+// Literal run: output bytes [op, op + len) of the block <- s[0, len), also
+// into the LDS ring.  Long runs (incompressible floats are one run per block)
+// go by whole output dwords: two aligned source dwords per lane joined by
+// v_alignbyte, 8 per lane in flight (2 KiB per wave); the ragged head and tail
+// go byte by byte.  out must be 4-byte aligned for the dword path.
+__device__ __forceinline__ void copy_literals(const uint8_t *s, const uint8_t *s_end, uint8_t *out, int64_t op,
+                                              int64_t len, uint8_t *ring, int lane) {
+    auto byte_copy = [&](int64_t b, int64_t e) {
+        for (int64_t i = b + lane; i < e; i += 64) {
+            const uint8_t v = s[i];
+            out[op + i] = v;
+            ring[(op + i) & (kRing - 1)] = v;
+        }
+    };
+    if (len < 256 || ((uintptr_t)out & 3)) {
+        byte_copy(0, len);
+        return;
+    }
+    const int64_t head = (4 - (op & 3)) & 3;
+    byte_copy(0, head);
+    const int64_t p0 = op + head, nw = (len - head) >> 2;
+    const uintptr_t sa = (uintptr_t)(s + head);
+    const int sh = (int)(sa & 3);
+    const uint32_t *sw = reinterpret_cast<const uint32_t *>(sa & ~(uintptr_t)3);
+    uint32_t *ow = reinterpret_cast<uint32_t *>(out + p0);
+    uint32_t *rw = reinterpret_cast<uint32_t *>(ring);
+    const int64_t r0 = p0 >> 2;
+    constexpr int U = 8;
+    for (int64_t w0 = 0; w0 < nw; w0 += 64 * U) {
+        uint32_t lo[U], hi[U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t w = w0 + u * 64 + lane;
+            lo[u] = hi[u] = 0;
+            if (w < nw) {
+                lo[u] = sw[w];
+                if (sh) {
+                    const uint32_t *nx = sw + w + 1;
+                    if ((const uint8_t *)nx + 4 <= s_end) {
+                        hi[u] = *nx;
+                    } else {  // the stream ends inside this dword: only its leading bytes exist
+                        const uint8_t *b = (const uint8_t *)nx;
+                        for (int k = 0; k < 4 && b + k < s_end; ++k) hi[u] |= (uint32_t)b[k] << (8 * k);
+                    }
+                }
+            }
+        }
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t w = w0 + u * 64 + lane;
+            if (w < nw) {
+                const uint32_t v = sh ? __builtin_amdgcn_alignbyte(hi[u], lo[u], (uint32_t)sh) : lo[u];
+                ow[w] = v;
+                rw[(r0 + w) & (kRing / 4 - 1)] = v;
+            }
+        }
+    }
+    byte_copy(head + 4 * nw, len);
+}
+
+// Compressed-input window for the token parse: lane l holds the dword at
+// wa + 4 l (wa 4-byte aligned), so a parse byte costs one lane shuffle
+// instead of a dependent global load; the window moves (one coalesced load)
+// when the parse leaves it.  All lanes call it with the same address.
+struct InWindow {
+    const uint8_t *end;
+    uintptr_t wa = 0;
+    uint32_t w = 0;
+    bool valid = false;
+    __device__ void load(const uint8_t *x, int lane) {
+        wa = (uintptr_t)x & ~(uintptr_t)3;
+        const uint8_t *p = (const uint8_t *)wa + 4 * lane;
+        if (p + 4 <= end) {
+            w = *reinterpret_cast<const uint32_t *>(p);
+        } else {
+            w = 0;
+            for (int k = 0; k < 4 && p + k < end; ++k) w |= (uint32_t)p[k] << (8 * k);
+        }
+        valid = true;
+    }
+    __device__ uint32_t byte(const uint8_t *x, int lane) {
+        if (!valid || (uintptr_t)x < wa || (uintptr_t)x >= wa + 256) load(x, lane);
+        const uintptr_t o = (uintptr_t)x - wa;
+        return (__shfl(w, (int)(o >> 2)) >> (8 * (o & 3))) & 255u;
+    }
+};
+
+__global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_t src_bytes, const IngestBlock *tab,
+                                                      int64_t nblocks, uint8_t *dst, int *status) {
+    __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
+    const uint8_t *src_end = src + src_bytes;
     const int lane = threadIdx.x;
     for (int64_t bi = blockIdx.x; bi < nblocks; bi += gridDim.x) {
         const IngestBlock blk = tab[bi];
         const uint8_t *ip0 = src + blk.src;
         uint8_t *out = dst + blk.dst;
         const int64_t isz = blk.csize, osz = blk.usize;
-        if (blk.method == 0x02) {
-            for (int64_t i = lane; i < osz; i += 64) out[i] = ip0[i];
+        if (blk.method == 0x02) {  // stored block: one literal run (the ring copy is unused)
+            copy_literals(ip0, src_end, out, 0, osz, ring, lane);
             continue;
         }
+        InWindow win;
+        win.end = ip0 + isz;
         int64_t ip = 0, op = 0;
         bool bad = false;
         for (;;) {
@@ -81,7 +172,7 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, const 
                 bad = true;
                 break;
             }
-            const uint32_t token = in_byte(ip0, ip++);
+            const uint32_t token = win.byte(ip0 + ip++, lane);
             int64_t len = token >> 4;
             if (len == 15) {
                 uint32_t s;
@@ -90,7 +181,7 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, const 
                         bad = true;
                         break;
                     }
-                    s = in_byte(ip0, ip++);
+                    s = win.byte(ip0 + ip++, lane);
                     len += s;
                 } while (s == 255);
                 if (bad) break;
@@ -99,23 +190,7 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, const 
                 bad = true;
                 break;
             }
-            // literals: 256 bytes per step, 4 per lane in flight
-            for (int64_t b0 = 0; b0 < len; b0 += 256) {
-                uint8_t v[4];
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int64_t i = b0 + u * 64 + lane;
-                    v[u] = i < len ? ip0[ip + i] : 0;
-                }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int64_t i = b0 + u * 64 + lane;
-                    if (i < len) {
-                        out[op + i] = v[u];
-                        ring[(op + i) & (kRing - 1)] = v[u];
-                    }
-                }
-            }
+            copy_literals(ip0 + ip, src_end, out, op, len, ring, lane);
             op += len;
             ip += len;
             if (op == osz) break;
@@ -123,7 +198,7 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, const 
                 bad = true;
                 break;
             }
-            const int64_t off = (int64_t)in_byte(ip0, ip) | ((int64_t)in_byte(ip0, ip + 1) << 8);
+            const int64_t off = (int64_t)win.byte(ip0 + ip, lane) | ((int64_t)win.byte(ip0 + ip + 1, lane) << 8);
             ip += 2;
             if (off == 0 || off > op) {
                 bad = true;
@@ -137,7 +212,7 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, const 
                         bad = true;
                         break;
                     }
-                    s = in_byte(ip0, ip++);
+                    s = win.byte(ip0 + ip++, lane);
                     mlen += s;
                 } while (s == 255);
                 if (bad) break;
@@ -147,19 +222,25 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, const 
                 bad = true;
                 break;
             }
-            __syncthreads();  // literal bytes in the ring before the match reads them
-            // steps of at most min(off, 256) bytes: every byte a step reads was
-            // written by an earlier step
-            const int64_t step = off < 256 ? off : 256;
-            for (int64_t d0 = 0; d0 < mlen; d0 += step) {
-                const int64_t cnt = mlen - d0 < step ? mlen - d0 : step;
+            // Match, in chunks of up to 256 bytes: byte op + i equals byte
+            // op + i - m off for any m >= 1 (the copy replicates with period
+            // off), so chunk [d0, d0 + cnt) reads the latest off bytes before
+            // it, [op + d0 - off, op + d0), all final after the barrier.
+            // cnt <= 65536 - off keeps the chunk's ring writes off that window.
+            const int64_t chunk = off > 65280 ? 65536 - off : 256;
+            for (int64_t d0 = 0; d0 < mlen; d0 += chunk) {
+                __syncthreads();  // earlier literal / match bytes are in the ring
+                const int64_t cnt = mlen - d0 < chunk ? mlen - d0 : chunk;
                 uint8_t v[4];
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int64_t i = u * 64 + lane;
-                    v[u] = i < cnt ? ring[(op + d0 + i - off) & (kRing - 1)] : 0;
+                    v[u] = 0;
+                    if (i < cnt) {
+                        const int64_t m = i / off + 1;
+                        v[u] = ring[(op + d0 + i - m * off) & (kRing - 1)];
+                    }
                 }
-                __syncthreads();
 #pragma unroll
                 for (int u = 0; u < 4; ++u) {
                     const int64_t i = u * 64 + lane;
@@ -168,8 +249,8 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, const 
                         ring[(op + d0 + i) & (kRing - 1)] = v[u];
                     }
                 }
-                __syncthreads();
             }
+            __syncthreads();
             op += mlen;
         }
         if (bad && lane == 0) atomicOr(status, 4);
@@ -284,11 +365,11 @@ void launch_block_table(const uint8_t *src, int64_t n, IngestBlock *tab, int64_t
     hipLaunchKernelGGL(k_block_table, dim3(1), dim3(1), 0, s, src, n, tab, max_blocks, out);
 }
 
-void launch_decode_blocks(const uint8_t *src, const IngestBlock *tab, int64_t nblocks, uint8_t *dst, int *status,
-                          hipStream_t s) {
+void launch_decode_blocks(const uint8_t *src, int64_t src_bytes, const IngestBlock *tab, int64_t nblocks, uint8_t *dst,
+                          int *status, hipStream_t s) {
     if (nblocks <= 0) return;
     const int grid = (int)std::min<int64_t>(nblocks, 4096);
-    hipLaunchKernelGGL(k_decode_blocks, dim3(grid), dim3(64), 0, s, src, tab, nblocks, dst, status);
+    hipLaunchKernelGGL(k_decode_blocks, dim3(grid), dim3(64), 0, s, src, src_bytes, tab, nblocks, dst, status);
 }
 
 // offsets[n] (exclusive); stats[0] += rows whose size != d, stats[1] = total

@@ -998,11 +998,11 @@ static mqvs_segment *ingest_column(const uint8_t *data_bin, int64_t data_bytes, 
         int *status = (int *)tmp.alloc(sizeof(int) * 4);
         MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
         auto *sizes = (uint64_t *)tmp.alloc(sizeof(uint64_t) * (size_t)std::max<int64_t>(n, 1));
-        launch_decode_blocks(ds, tab_s, sz.first, (uint8_t *)sizes, status, s);
+        launch_decode_blocks(ds, sizes_bytes, tab_s, sz.first, (uint8_t *)sizes, status, s);
         // the common case (every array has d elements) decodes straight into the rows
         const bool direct = dt.second == 4 * n * (int64_t)d;
         float *data = direct ? seg->rows : (float *)tmp.alloc((size_t)dt.second);
-        launch_decode_blocks(dd, tab_d, dt.first, (uint8_t *)data, status, s);
+        launch_decode_blocks(dd, data_bytes, tab_d, dt.first, (uint8_t *)data, status, s);
         MQVS_HIP(hipGetLastError());
         const int64_t tiles = std::max<int64_t>(1, (n + 4095) / 4096);
         auto *offs = (int64_t *)tmp.alloc(sizeof(int64_t) * (size_t)std::max<int64_t>(n, 1));
