@@ -60,7 +60,8 @@ enum {
     MQVS_ERR_ILLEGAL_COLUMN = 3,    /* malformed column data */
     MQVS_ERR_BAD_ARGUMENTS = 4,     /* null pointers, k <= 0, ... */
     MQVS_ERR_MEMORY_LIMIT = 5,      /* HBM allocation failed (MEMORY_LIMIT_EXCEEDED) */
-    MQVS_ERR_DEVICE = 6             /* HIP runtime / kernel failure */
+    MQVS_ERR_DEVICE = 6,            /* HIP runtime / kernel failure */
+    MQVS_ERR_CHECKSUM = 7           /* compressed block checksum mismatch (CHECKSUM_DOESNT_MATCH) */
 };
 
 /* mqvs_search / mqvs_rerank flags */
@@ -175,13 +176,17 @@ int mqvs_merge_shards(int32_t nshards, int32_t nq, int32_t k, int32_t metric,
  * Float32 stream (`<column>.bin`), sizes_bin = the array sizes stream
  * (`<column>.size0.bin`, UInt64 per row), both as ClickHouse writes them
  * (CompressedWriteBuffer blocks: 16-B checksum, method 0x82 LZ4 or 0x02 NONE,
- * UInt32 compressed size, UInt32 decompressed size, payload; checksums are not
- * verified).  Decoded on the GPU into the rows of :1381-1393 (FLT_MAX fill;
+ * UInt32 compressed size, UInt32 decompressed size, payload).  Every block's
+ * checksum -- CityHash128 v1.0.2 of header + payload -- is verified on the GPU
+ * first (CompressedReadBufferBase.cpp:37-45, 192-196) unless flags has
+ * MQVS_F_NO_CHECKSUM (the reference's disable_checksum).  Decoded on the GPU into the rows of :1381-1393 (FLT_MAX fill;
  * empty arrays flagged empty; arrays longer than d truncated, shorter ones
  * FLT_MAX-padded) and prepared as mqvs_segment_create.  flags:
  * MQVS_F_DEVICE_PTRS when the streams are already in HBM.  Errors:
+ * MQVS_ERR_CHECKSUM (a block checksum does not match: CHECKSUM_DOESNT_MATCH),
  * MQVS_ERR_ILLEGAL_COLUMN (malformed blocks, sizes that do not match the data
  * stream or n), MQVS_ERR_NOT_IMPLEMENTED (other codecs). */
+#define MQVS_F_NO_CHECKSUM 0x10u
 int mqvs_segment_create_from_column(const uint8_t *data_bin, int64_t data_bytes, const uint8_t *sizes_bin,
                                     int64_t sizes_bytes, int64_t n, int32_t d, int32_t metric, int64_t granule_rows,
                                     int64_t row_offset, uint32_t flags, mqvs_segment_t *out);

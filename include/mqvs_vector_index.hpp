@@ -50,6 +50,7 @@ namespace DB
 namespace ErrorCodes
 {
     constexpr int BAD_ARGUMENTS = 36;
+    constexpr int CHECKSUM_DOESNT_MATCH = 40;
     constexpr int ILLEGAL_COLUMN = 44;
     constexpr int NOT_IMPLEMENTED = 48;
     constexpr int LOGICAL_ERROR = 49;
@@ -73,6 +74,7 @@ namespace DB
 namespace ErrorCodes
 {
     extern const int BAD_ARGUMENTS;
+    extern const int CHECKSUM_DOESNT_MATCH;
     extern const int ILLEGAL_COLUMN;
     extern const int NOT_IMPLEMENTED;
     extern const int LOGICAL_ERROR;
@@ -93,6 +95,7 @@ inline int dbErrorCode(int status)
         case MQVS_ERR_ILLEGAL_COLUMN: return DB::ErrorCodes::ILLEGAL_COLUMN;
         case MQVS_ERR_BAD_ARGUMENTS: return DB::ErrorCodes::BAD_ARGUMENTS;
         case MQVS_ERR_MEMORY_LIMIT: return DB::ErrorCodes::MEMORY_LIMIT_EXCEEDED;
+        case MQVS_ERR_CHECKSUM: return DB::ErrorCodes::CHECKSUM_DOESNT_MATCH;
         default: return DB::ErrorCodes::LOGICAL_ERROR;  /// LOGICAL / DEVICE
     }
 }

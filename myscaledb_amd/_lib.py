@@ -20,11 +20,12 @@ METRICS = {"L2": METRIC_L2, "IP": METRIC_IP, "COSINE": METRIC_COSINE, "Cosine": 
            "Jaccard": METRIC_JACCARD, "JACCARD": METRIC_JACCARD, "jaccard": METRIC_JACCARD}
 OK = 0
 ERR_NOT_IMPLEMENTED, ERR_LOGICAL, ERR_ILLEGAL_COLUMN, ERR_BAD_ARGUMENTS, ERR_MEMORY_LIMIT, \
-    ERR_DEVICE = 1, 2, 3, 4, 5, 6
+    ERR_DEVICE, ERR_CHECKSUM = 1, 2, 3, 4, 5, 6, 7
 F_DEVICE_PTRS = 0x1
 F_ASYNC = 0x2
 F_PART_MERGE = 0x4
 F_FIRST_STAGE = 0x8
+F_NO_CHECKSUM = 0x10
 
 # Exported C symbols: every one of these is declared in include/mqvs.h.
 SYMBOLS = [
@@ -133,10 +134,11 @@ lib = _load()
 
 # DB::ErrorCodes the reference throws for the same conditions
 CLICKHOUSE_CODE = {ERR_NOT_IMPLEMENTED: 48, ERR_LOGICAL: 49, ERR_ILLEGAL_COLUMN: 44,
-                   ERR_BAD_ARGUMENTS: 36, ERR_MEMORY_LIMIT: 241, ERR_DEVICE: 1001}
+                   ERR_BAD_ARGUMENTS: 36, ERR_MEMORY_LIMIT: 241, ERR_DEVICE: 1001, ERR_CHECKSUM: 40}
 CODE_NAME = {ERR_NOT_IMPLEMENTED: "NOT_IMPLEMENTED", ERR_LOGICAL: "LOGICAL_ERROR",
              ERR_ILLEGAL_COLUMN: "ILLEGAL_COLUMN", ERR_BAD_ARGUMENTS: "BAD_ARGUMENTS",
-             ERR_MEMORY_LIMIT: "MEMORY_LIMIT_EXCEEDED", ERR_DEVICE: "DEVICE_ERROR"}
+             ERR_MEMORY_LIMIT: "MEMORY_LIMIT_EXCEEDED", ERR_DEVICE: "DEVICE_ERROR",
+             ERR_CHECKSUM: "CHECKSUM_DOESNT_MATCH"}
 
 
 class MqvsError(RuntimeError):

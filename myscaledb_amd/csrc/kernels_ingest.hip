@@ -18,6 +18,8 @@
 //                   are < 2^16), never from global memory, so no global
 //                   read-after-write ordering is needed; an overlapping match
 //                   (offset < length) is copied in steps of min(offset, 256).
+//   k_block_checksum CityHash128 v1.0.2 of every block (one lane per block),
+//                   compared with the stored 16-B checksum.
 //   k_sizes_scan_*  array sizes (UInt64 per row) -> element offsets.
 //   k_array_rows    the copy loop of :1381-1393: FLT_MAX fill, first
 //                   min(size, d) elements of a non-empty array, nonempty flag.
@@ -258,6 +260,175 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
     }
 }
 
+// ---- block checksums: CityHash128 v1.0.2 ------------------------------------
+// CompressedReadBufferBase.cpp:37-45, 192-196 validates every block before
+// decompressing it: CityHash_v1_0_2::CityHash128 (contrib/cityhash102/src/
+// city.cc:256-358) over the 9-B header + payload, against the 16 bytes stored
+// before it.  CityHash is a sequential chain, so one lane hashes one block
+// (1 MiB blocks: ~3k lanes for a 3 GB column).  Blocks start at arbitrary byte
+// offsets: every 64-bit word is assembled from aligned dwords with
+// v_alignbyte (the shift is fixed per block), and the next 64-byte round's
+// dwords are loaded while the current round is mixed.
+namespace city {
+constexpr uint64_t K0 = 0xc3a5c85c97cb3127ULL, K1 = 0xb492b66fbe98f273ULL, K2 = 0x9ae16a3b2f90404fULL,
+                   K3 = 0xc949d7c7509e6557ULL;
+__device__ __forceinline__ uint64_t ror(uint64_t v, int s) { return s ? (v >> s) | (v << (64 - s)) : v; }
+__device__ __forceinline__ uint64_t mix47(uint64_t v) { return v ^ (v >> 47); }
+__device__ __forceinline__ uint64_t pair(uint64_t lo, uint64_t hi) {  // Hash128to64
+    constexpr uint64_t m = 0x9ddfea08eb382d69ULL;
+    const uint64_t a = mix47((lo ^ hi) * m);
+    return mix47((hi ^ a) * m) * m;
+}
+__device__ __forceinline__ uint32_t join(uint32_t lo, uint32_t hi, uint32_t sh) {
+    return __builtin_amdgcn_alignbyte(hi, lo, sh);
+}
+// unaligned little-endian loads; a dword is read only when it holds a needed byte
+__device__ __forceinline__ uint64_t ld64(const uint8_t *p) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    const uint32_t d0 = w[0], d1 = w[1], d2 = sh ? w[2] : 0u;
+    return (uint64_t)join(d0, d1, sh) | ((uint64_t)join(d1, d2, sh) << 32);
+}
+__device__ __forceinline__ uint64_t ld32(const uint8_t *p) {
+    const uintptr_t a = (uintptr_t)p;
+    const uint32_t *w = reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3);
+    const uint32_t sh = (uint32_t)(a & 3);
+    return join(w[0], sh ? w[1] : 0u, sh);
+}
+__device__ uint64_t short_hash(const uint8_t *s, uint64_t len) {  // HashLen0to16
+    if (len > 8) {
+        const uint64_t a = ld64(s), b = ld64(s + len - 8);
+        return pair(a, ror(b + len, (int)len)) ^ b;
+    }
+    if (len >= 4) return pair(len + (ld32(s) << 3), ld32(s + len - 4));
+    if (len > 0) {
+        const uint32_t y = (uint32_t)s[0] + ((uint32_t)s[len >> 1] << 8);
+        const uint32_t z = (uint32_t)len + ((uint32_t)s[len - 1] << 2);
+        return mix47(y * K2 ^ z * K3) * K2;
+    }
+    return K2;
+}
+// WeakHashLen32WithSeeds over words w0..w3
+__device__ __forceinline__ void weak32(uint64_t w0, uint64_t w1, uint64_t w2, uint64_t w3, uint64_t a, uint64_t b,
+                                       uint64_t &o1, uint64_t &o2) {
+    a += w0;
+    b = ror(b + a + w3, 21);
+    const uint64_t c = a;
+    a += w1 + w2;
+    b += ror(a, 44);
+    o1 = a + w3;
+    o2 = b + c;
+}
+__device__ void murmur(const uint8_t *s, uint64_t len, uint64_t a, uint64_t b, uint64_t h[2]) {  // CityMurmur
+    uint64_t c, d;
+    if (len <= 16) {
+        a = mix47(a * K1) * K1;
+        c = b * K1 + short_hash(s, len);
+        d = mix47(a + (len >= 8 ? ld64(s) : c));
+    } else {
+        c = pair(ld64(s + len - 8) + K1, a);
+        d = pair(b + len, c + ld64(s + len - 16));
+        a += d;
+        for (int64_t l = (int64_t)len - 16; l > 0; l -= 16, s += 16) {
+            a ^= mix47(ld64(s) * K1) * K1;
+            a *= K1;
+            b ^= a;
+            c ^= mix47(ld64(s + 8) * K1) * K1;
+            c *= K1;
+            d ^= c;
+        }
+    }
+    a = pair(a, c);
+    b = pair(d, b);
+    h[0] = a ^ b;
+    h[1] = pair(b, a);
+}
+// 64 bytes at an aligned dword base + sh as 17 raw dwords
+__device__ __forceinline__ void load_round(const uint32_t *w, uint32_t sh, uint32_t r[17]) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = w[i];
+    r[16] = sh ? w[16] : 0u;
+}
+__device__ void seeded(const uint8_t *s, uint64_t len, uint64_t x, uint64_t y, uint64_t h[2]) {  // CityHash128WithSeed
+    if (len < 128) {
+        murmur(s, len, x, y, h);
+        return;
+    }
+    uint64_t z = len * K1;
+    uint64_t v1 = ror(y ^ K1, 49) * K1 + ld64(s);
+    uint64_t v2 = ror(v1, 42) * K1 + ld64(s + 8);
+    uint64_t w1 = ror(y + z, 35) * K1 + x;
+    uint64_t w2 = ror(x + ld64(s + 88), 53) * K1;
+    const int64_t rounds = 2 * (int64_t)(len / 128);
+    const uintptr_t a0 = (uintptr_t)s;
+    const uint32_t sh = (uint32_t)(a0 & 3);
+    const uint32_t *base = reinterpret_cast<const uint32_t *>(a0 & ~(uintptr_t)3);
+    uint32_t cur[17];
+    load_round(base, sh, cur);
+    for (int64_t r = 0; r < rounds; ++r) {
+        uint32_t nxt[17];
+        load_round(base + 16 * (r + 1 < rounds ? r + 1 : r), sh, nxt);  // in flight during the mix
+        uint64_t q[8];
+#pragma unroll
+        for (int i = 0; i < 8; ++i)
+            q[i] = (uint64_t)join(cur[2 * i], cur[2 * i + 1], sh) | ((uint64_t)join(cur[2 * i + 1], cur[2 * i + 2], sh) << 32);
+        x = ror(x + y + v1 + q[2], 37) * K1;
+        y = ror(y + v2 + q[6], 42) * K1;
+        x ^= w2;
+        y ^= v1;
+        z = ror(z ^ w1, 33);
+        weak32(q[0], q[1], q[2], q[3], v2 * K1, x + w1, v1, v2);
+        weak32(q[4], q[5], q[6], q[7], z + w2, y, w1, w2);
+        const uint64_t t = z;
+        z = x;
+        x = t;
+#pragma unroll
+        for (int i = 0; i < 17; ++i) cur[i] = nxt[i];
+    }
+    s += 64 * rounds;
+    len -= 64 * (uint64_t)rounds;
+    y += ror(w1, 37) * K0 + z;
+    x += ror(v1 + z, 49) * K0;
+    for (uint64_t done = 0; done < len;) {
+        done += 32;
+        y = ror(y - x, 42) * K0 + v2;
+        w1 += ld64(s + len - done + 16);
+        x = ror(x, 49) * K0 + w1;
+        w1 += v1;
+        const uint8_t *p = s + len - done;
+        weak32(ld64(p), ld64(p + 8), ld64(p + 16), ld64(p + 24), v1, v2, v1, v2);
+    }
+    x = pair(x, v1);
+    y = pair(y, w1);
+    h[0] = pair(x + v2, w2) + y;
+    h[1] = pair(x + w2, y + v2);
+}
+__device__ void hash128(const uint8_t *s, uint64_t len, uint64_t h[2]) {  // CityHash128
+    if (len >= 16)
+        seeded(s + 16, len - 16, ld64(s) ^ K3, ld64(s + 8), h);
+    else if (len >= 8)
+        seeded(nullptr, 0, ld64(s) ^ (len * K0), ld64(s + len - 8) ^ K1, h);
+    else
+        seeded(s, len, K0, K1, h);
+}
+}  // namespace city
+
+__global__ __launch_bounds__(64) void k_block_checksum(const uint8_t *src, const IngestBlock *tab, int64_t nblocks,
+                                                       int flag, int *status, uint64_t *hash_out) {
+    const int64_t bi = (int64_t)blockIdx.x * 64 + threadIdx.x;
+    if (bi >= nblocks) return;
+    const IngestBlock b = tab[bi];
+    const uint8_t *hdr = src + b.src - 9;  // the hash covers header + payload
+    uint64_t h[2];
+    city::hash128(hdr, (uint64_t)b.csize + 9, h);
+    if (hash_out) {
+        hash_out[2 * bi] = h[0];
+        hash_out[2 * bi + 1] = h[1];
+    }
+    if (h[0] != city::ld64(hdr - 16) || h[1] != city::ld64(hdr - 8)) atomicOr(status, flag);
+}
+
 // ---- array sizes -> element offsets (exclusive scan over n UInt64) ----------
 constexpr int kScanTile = 4096;  // sizes per workgroup (256 threads x 16)
 
@@ -370,6 +541,13 @@ void launch_decode_blocks(const uint8_t *src, int64_t src_bytes, const IngestBlo
     if (nblocks <= 0) return;
     const int grid = (int)std::min<int64_t>(nblocks, 4096);
     hipLaunchKernelGGL(k_decode_blocks, dim3(grid), dim3(64), 0, s, src, src_bytes, tab, nblocks, dst, status);
+}
+
+void launch_block_checksum(const uint8_t *src, const IngestBlock *tab, int64_t nblocks, int flag, int *status,
+                           uint64_t *hash_out, hipStream_t s) {
+    if (nblocks <= 0) return;
+    hipLaunchKernelGGL(k_block_checksum, dim3((unsigned)((nblocks + 63) / 64)), dim3(64), 0, s, src, tab, nblocks, flag,
+                       status, hash_out);
 }
 
 // offsets[n] (exclusive); stats[0] += rows whose size != d, stats[1] = total

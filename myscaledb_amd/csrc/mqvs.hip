@@ -965,6 +965,8 @@ static std::pair<int64_t, int64_t> stream_table(IngestTmp &tmp, const uint8_t *d
     return {hbuf[0], hbuf[1]};
 }
 
+constexpr int kBadDataChecksum = 8, kBadSizesChecksum = 16;  // status bits (decode uses 4)
+
 static mqvs_segment *ingest_column(const uint8_t *data_bin, int64_t data_bytes, const uint8_t *sizes_bin,
                                    int64_t sizes_bytes, int64_t n, int32_t d, int32_t metric, int64_t granule,
                                    int64_t row_offset, uint32_t flags) {
@@ -997,6 +999,10 @@ static mqvs_segment *ingest_column(const uint8_t *data_bin, int64_t data_bytes, 
         if (dt.second % 4) fail(MQVS_ERR_ILLEGAL_COLUMN, "vector data stream is not a whole number of Float32");
         int *status = (int *)tmp.alloc(sizeof(int) * 4);
         MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
+        if (!(flags & MQVS_F_NO_CHECKSUM)) {  // CompressedReadBufferBase.cpp:192-196, before decompression
+            launch_block_checksum(ds, tab_s, sz.first, kBadSizesChecksum, status, nullptr, s);
+            launch_block_checksum(dd, tab_d, dt.first, kBadDataChecksum, status, nullptr, s);
+        }
         auto *sizes = (uint64_t *)tmp.alloc(sizeof(uint64_t) * (size_t)std::max<int64_t>(n, 1));
         launch_decode_blocks(ds, sizes_bytes, tab_s, sz.first, (uint8_t *)sizes, status, s);
         // the common case (every array has d elements) decodes straight into the rows
@@ -1015,6 +1021,10 @@ static mqvs_segment *ingest_column(const uint8_t *data_bin, int64_t data_bytes, 
         int *hstatus = reinterpret_cast<int *>(h + 2);
         MQVS_HIP(hipMemcpyAsync(hstatus, status, sizeof(int), hipMemcpyDeviceToHost, s));
         MQVS_HIP(hipStreamSynchronize(s));
+        if (*hstatus & (kBadSizesChecksum | kBadDataChecksum))
+            fail(MQVS_ERR_CHECKSUM, std::string("Checksum doesn't match: corrupted data (") +
+                                        (*hstatus & kBadSizesChecksum ? "array sizes stream" : "vector data stream") +
+                                        ", CityHash128 of a compressed block)");
         if (*hstatus)
             fail(MQVS_ERR_ILLEGAL_COLUMN, "malformed LZ4 block (CANNOT_DECOMPRESS)");
         const int64_t notd = h[0], nelem = h[1];

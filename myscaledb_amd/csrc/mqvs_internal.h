@@ -283,6 +283,10 @@ void launch_block_table(const uint8_t *src, int64_t n, IngestBlock *tab, int64_t
                         hipStream_t s);
 void launch_decode_blocks(const uint8_t *src, int64_t src_bytes, const IngestBlock *tab, int64_t nblocks, uint8_t *dst,
                           int *status, hipStream_t s);
+// CityHash128 of block i's header + payload != its stored checksum -> *status |= flag;
+// hash_out (optional) receives [nblocks][2] (low, high)
+void launch_block_checksum(const uint8_t *src, const IngestBlock *tab, int64_t nblocks, int flag, int *status,
+                           uint64_t *hash_out, hipStream_t s);
 void launch_sizes_scan(const uint64_t *sizes, int64_t n, int d, int64_t *offsets, int64_t *scratch, int64_t *stats,
                        hipStream_t s);
 void launch_array_rows(const float *data, const int64_t *offsets, const uint64_t *sizes, int64_t n, int d,

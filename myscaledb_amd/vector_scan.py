@@ -27,7 +27,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import F_ASYNC, F_DEVICE_PTRS, F_PART_MERGE, METRICS, check, lib
+from ._lib import F_ASYNC, F_DEVICE_PTRS, F_NO_CHECKSUM, F_PART_MERGE, METRICS, check, lib
 
 FLT_MAX = np.float32(3.4028235e38)
 FLT_MIN = np.float32(1.1754944e-38)
@@ -105,11 +105,13 @@ class VectorScanSegment:
         return cls(h, n, d, m, granule, row_offset)
 
     @classmethod
-    def from_column(cls, data_bin, sizes_bin, n, d, metric="L2", granule=DEFAULT_GRANULE, row_offset=0):
+    def from_column(cls, data_bin, sizes_bin, n, d, metric="L2", granule=DEFAULT_GRANULE, row_offset=0,
+                    verify_checksum=True):
         """A part's Array(Float32) column from its compressed files, decoded on
         the GPU (mqvs_segment_create_from_column): data_bin = `<col>.bin`
         bytes, sizes_bin = `<col>.size0.bin` bytes (bytes / numpy uint8, or
-        torch uint8 CUDA tensors)."""
+        torch uint8 CUDA tensors).  Block checksums are verified unless
+        verify_checksum=False (CompressedReadBufferBase's disable_checksum)."""
         m = metric_id(metric)
         h = ctypes.c_void_p()
         if _is_torch(data_bin):
@@ -125,6 +127,8 @@ class VectorScanSegment:
                 else _host_u8(sizes_bin)
             keep = (a, b)
             dp, dn, sp, sn = _ptr(a), a.size, _ptr(b), b.size
+        if not verify_checksum:
+            flags |= F_NO_CHECKSUM
         check(lib.mqvs_segment_create_from_column(dp, dn, sp, sn, n, d, m, granule, row_offset, flags,
                                                   ctypes.byref(h)))
         del keep

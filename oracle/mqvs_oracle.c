@@ -885,7 +885,7 @@ int orc_vector_scan_binary(const uint8_t *rows, int64_t n, int64_t nbytes,
  * Framing (CompressedReadBufferBase.cpp:115-160, CompressionInfo.h:22-49):
  * per block 16-B CityHash128 checksum, then a 9-B header: method byte
  * (0x82 LZ4, 0x02 NONE), UInt32 compressed size (header + payload), UInt32
- * decompressed size; then the payload.  Checksums are not verified here.
+ * decompressed size; then the payload.
  *
  * LZ4 block format as LZ4_decompress_faster.cpp:480-640 decodes it: token
  * (literal length high nibble, match length - 4 low nibble, 15 = extended by
@@ -894,6 +894,137 @@ int orc_vector_scan_binary(const uint8_t *rows, int64_t n, int64_t nbytes,
 
 static inline uint32_t rd32(const uint8_t *p) {
     return (uint32_t)p[0] | ((uint32_t)p[1] << 8) | ((uint32_t)p[2] << 16) | ((uint32_t)p[3] << 24);
+}
+
+/* Block checksum: CityHash128 v1.0.2 (the pre-1.0.3 variant ClickHouse keeps,
+ * contrib/cityhash102/src/city.cc:256-358, Hash128to64 city.h:91-100) over
+ * the 9-B header + payload, validated before decompression
+ * (CompressedReadBufferBase.cpp:37-45, 192-196; written by
+ * CompressedWriteBuffer.cpp:44).  Restated on 64-bit little-endian words;
+ * h[0] = low half (uint128.first), h[1] = high half; the stored 16 checksum
+ * bytes are h[0] then h[1], little-endian. */
+static const uint64_t CH_K0 = 0xc3a5c85c97cb3127ULL, CH_K1 = 0xb492b66fbe98f273ULL,
+                      CH_K2 = 0x9ae16a3b2f90404fULL, CH_K3 = 0xc949d7c7509e6557ULL;
+
+static inline uint64_t ch_ld64(const uint8_t *p) {
+    uint64_t v;
+    memcpy(&v, p, 8);
+    return v;
+}
+static inline uint64_t ch_ld32(const uint8_t *p) {
+    uint32_t v;
+    memcpy(&v, p, 4);
+    return v;
+}
+static inline uint64_t ch_ror(uint64_t v, int s) { return s ? (v >> s) | (v << (64 - s)) : v; }
+static inline uint64_t ch_mix47(uint64_t v) { return v ^ (v >> 47); }
+/* Hash128to64(uint128(lo, hi)) */
+static inline uint64_t ch_pair(uint64_t lo, uint64_t hi) {
+    const uint64_t m = 0x9ddfea08eb382d69ULL;
+    uint64_t a = ch_mix47((lo ^ hi) * m);
+    uint64_t b = ch_mix47((hi ^ a) * m);
+    return b * m;
+}
+static uint64_t ch_short(const uint8_t *s, uint64_t len) { /* HashLen0to16, city.cc:125-144 */
+    if (len > 8) {
+        const uint64_t a = ch_ld64(s), b = ch_ld64(s + len - 8);
+        return ch_pair(a, ch_ror(b + len, (int)len)) ^ b;
+    }
+    if (len >= 4) return ch_pair(len + (ch_ld32(s) << 3), ch_ld32(s + len - 4));
+    if (len > 0) {
+        const uint32_t y = (uint32_t)s[0] + ((uint32_t)s[len >> 1] << 8);
+        const uint32_t z = (uint32_t)len + ((uint32_t)s[len - 1] << 2);
+        return ch_mix47(y * CH_K2 ^ z * CH_K3) * CH_K2;
+    }
+    return CH_K2;
+}
+/* WeakHashLen32WithSeeds over s[0, 32) (city.cc:159-179) */
+static inline void ch_weak32(const uint8_t *s, uint64_t a, uint64_t b, uint64_t *o1, uint64_t *o2) {
+    const uint64_t w = ch_ld64(s), x = ch_ld64(s + 8), y = ch_ld64(s + 16), z = ch_ld64(s + 24);
+    a += w;
+    b = ch_ror(b + a + z, 21);
+    const uint64_t c = a;
+    a += x + y;
+    b += ch_ror(a, 44);
+    *o1 = a + z;
+    *o2 = b + c;
+}
+/* CityMurmur (city.cc:256-284): len < 128 */
+static void ch_murmur(const uint8_t *s, uint64_t len, uint64_t a, uint64_t b, uint64_t h[2]) {
+    uint64_t c, d;
+    if (len <= 16) {
+        a = ch_mix47(a * CH_K1) * CH_K1;
+        c = b * CH_K1 + ch_short(s, len);
+        d = ch_mix47(a + (len >= 8 ? ch_ld64(s) : c));
+    } else {
+        c = ch_pair(ch_ld64(s + len - 8) + CH_K1, a);
+        d = ch_pair(b + len, c + ch_ld64(s + len - 16));
+        a += d;
+        for (int64_t l = (int64_t)len - 16; l > 0; l -= 16, s += 16) {
+            a ^= ch_mix47(ch_ld64(s) * CH_K1) * CH_K1;
+            a *= CH_K1;
+            b ^= a;
+            c ^= ch_mix47(ch_ld64(s + 8) * CH_K1) * CH_K1;
+            c *= CH_K1;
+            d ^= c;
+        }
+    }
+    a = ch_pair(a, c);
+    b = ch_pair(d, b);
+    h[0] = a ^ b;
+    h[1] = ch_pair(b, a);
+}
+/* CityHash128WithSeed (city.cc:286-342), seed = (lo, hi) */
+static void ch_seeded(const uint8_t *s, uint64_t len, uint64_t lo, uint64_t hi, uint64_t h[2]) {
+    if (len < 128) {
+        ch_murmur(s, len, lo, hi, h);
+        return;
+    }
+    uint64_t x = lo, y = hi, z = len * CH_K1;
+    uint64_t v1 = ch_ror(y ^ CH_K1, 49) * CH_K1 + ch_ld64(s);
+    uint64_t v2 = ch_ror(v1, 42) * CH_K1 + ch_ld64(s + 8);
+    uint64_t w1 = ch_ror(y + z, 35) * CH_K1 + x;
+    uint64_t w2 = ch_ror(x + ch_ld64(s + 88), 53) * CH_K1;
+    do { /* two 64-byte rounds per 128 bytes */
+        for (int r = 0; r < 2; r++) {
+            x = ch_ror(x + y + v1 + ch_ld64(s + 16), 37) * CH_K1;
+            y = ch_ror(y + v2 + ch_ld64(s + 48), 42) * CH_K1;
+            x ^= w2;
+            y ^= v1;
+            z = ch_ror(z ^ w1, 33);
+            ch_weak32(s, v2 * CH_K1, x + w1, &v1, &v2);
+            ch_weak32(s + 32, z + w2, y, &w1, &w2);
+            const uint64_t t = z;
+            z = x;
+            x = t;
+            s += 64;
+        }
+        len -= 128;
+    } while (len >= 128);
+    y += ch_ror(w1, 37) * CH_K0 + z;
+    x += ch_ror(v1 + z, 49) * CH_K0;
+    for (uint64_t done = 0; done < len;) { /* up to four 32-byte tail pieces, from the end */
+        done += 32;
+        y = ch_ror(y - x, 42) * CH_K0 + v2;
+        w1 += ch_ld64(s + len - done + 16);
+        x = ch_ror(x, 49) * CH_K0 + w1;
+        w1 += v1;
+        ch_weak32(s + len - done, v1, v2, &v1, &v2);
+    }
+    x = ch_pair(x, v1);
+    y = ch_pair(y, w1);
+    h[0] = ch_pair(x + v2, w2) + y;
+    h[1] = ch_pair(x + w2, y + v2);
+}
+/* CityHash128 (city.cc:344-358) */
+void orc_cityhash128(const uint8_t *s, int64_t len, uint64_t h[2]) {
+    const uint64_t n = (uint64_t)len;
+    if (n >= 16)
+        ch_seeded(s + 16, n - 16, ch_ld64(s) ^ CH_K3, ch_ld64(s + 8), h);
+    else if (n >= 8)
+        ch_seeded(NULL, 0, ch_ld64(s) ^ (n * CH_K0), ch_ld64(s + n - 8) ^ CH_K1, h);
+    else
+        ch_seeded(s, n, CH_K0, CH_K1, h);
 }
 
 /* Returns 0, or -1 on malformed input (ClickHouse: CANNOT_DECOMPRESS). */
@@ -1001,7 +1132,7 @@ fail:
 }
 
 /* CompressedWriteBuffer framing of `n` bytes in blocks of at most block_size
- * (method 0x82 LZ4 or 0x02 NONE); checksum bytes are written as zero. */
+ * (method 0x82 LZ4 or 0x02 NONE), each with its CityHash128 checksum. */
 int64_t orc_compress_stream(const uint8_t *src, int64_t n, int64_t block_size, int method, uint8_t *dst,
                             int64_t cap) {
     int64_t o = 0;
@@ -1023,20 +1154,29 @@ int64_t orc_compress_stream(const uint8_t *src, int64_t n, int64_t block_size, i
         const uint32_t csize = (uint32_t)(9 + payload), usize = (uint32_t)len;
         memcpy(hdr + 1, &csize, 4);
         memcpy(hdr + 5, &usize, 4);
+        uint64_t h[2];
+        orc_cityhash128(hdr, csize, h);
+        memcpy(dst + o, h, 16);
         o += 25 + payload;
     }
     return o;
 }
 
 /* CompressedReadBuffer over a whole stream: returns the decompressed size,
- * or -1 (malformed framing / payload, or more than cap bytes). */
-int64_t orc_decompress_stream(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap) {
+ * -1 (malformed framing / payload, or more than cap bytes) or -2 (a block
+ * checksum does not match; checked first, when verify != 0). */
+int64_t orc_decompress_stream(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap, int verify) {
     int64_t pos = 0, o = 0;
     while (pos < n) {
         if (n - pos < 25) return -1;
         const uint8_t method = src[pos + 16];
         const int64_t csize = rd32(src + pos + 17), usize = rd32(src + pos + 21);
         if (csize < 9 || pos + 16 + csize > n || o + usize > cap) return -1;
+        if (verify) {
+            uint64_t h[2];
+            orc_cityhash128(src + pos + 16, csize, h);
+            if (memcmp(h, src + pos, 16)) return -2; /* CHECKSUM_DOESNT_MATCH */
+        }
         const uint8_t *payload = src + pos + 25;
         if (method == 0x82) {
             if (orc_lz4_decompress(payload, csize - 9, dst + o, usize)) return -1;

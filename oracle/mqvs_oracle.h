@@ -140,10 +140,12 @@ int orc_vector_scan_binary(const uint8_t *rows, int64_t n, int64_t nbytes,
 int orc_lz4_decompress(const uint8_t *src, int64_t src_size, uint8_t *dst, int64_t dst_size);
 /* test-data compressor (standard LZ4 block format); size or -1 */
 int64_t orc_lz4_compress(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap);
-/* CompressedWriteBuffer / CompressedReadBuffer framing (zero checksums) */
+/* CompressedWriteBuffer / CompressedReadBuffer framing (CityHash128 block checksums) */
 int64_t orc_compress_stream(const uint8_t *src, int64_t n, int64_t block_size, int method, uint8_t *dst,
                             int64_t cap);
-int64_t orc_decompress_stream(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap);
+int64_t orc_decompress_stream(const uint8_t *src, int64_t n, uint8_t *dst, int64_t cap, int verify);
+/* CityHash128 v1.0.2 (contrib/cityhash102/src/city.cc:344-358): h[0] low, h[1] high */
+void orc_cityhash128(const uint8_t *s, int64_t len, uint64_t h[2]);
 /* MergeTreeVSManager.cpp:1381-1393 copy loop: FLT_MAX fill, truncation at d */
 int orc_array_rows(const float *data, int64_t nelem, const uint64_t *sizes, int64_t n, int64_t d, float *rows,
                    uint8_t *nonempty);

@@ -57,7 +57,8 @@ def lib():
         L.orc_lz4_compress.restype = I64
         L.orc_compress_stream.argtypes = [P, I64, I64, ctypes.c_int, P, I64]
         L.orc_compress_stream.restype = I64
-        L.orc_decompress_stream.argtypes = [P, I64, P, I64]
+        L.orc_decompress_stream.argtypes = [P, I64, P, I64, ctypes.c_int]
+        L.orc_cityhash128.argtypes = [P, I64, P]
         L.orc_decompress_stream.restype = I64
         L.orc_array_rows.argtypes = [P, I64, P, I64, I64, P, P]
         L.orc_generate.argtypes = [ctypes.c_uint64, ctypes.c_int, I64, I64, I64, P]
@@ -184,7 +185,7 @@ def vector_scan_binary(codes, queries, k, metric, mark_rows, filter_bits=None, r
 
 
 def compress_stream(data: bytes | np.ndarray, block_size=1 << 20, method=0x82) -> bytes:
-    """ClickHouse CompressedWriteBuffer framing + LZ4 (test data; zero checksums)."""
+    """ClickHouse CompressedWriteBuffer framing + LZ4 (test data), CityHash128 block checksums."""
     src = np.frombuffer(bytes(data), np.uint8) if not isinstance(data, np.ndarray) else _u8(data.view(np.uint8))
     cap = int(src.size + src.size // 200 + 64 * (src.size // block_size + 1) + 1024)
     out = np.empty(cap, np.uint8)
@@ -194,13 +195,29 @@ def compress_stream(data: bytes | np.ndarray, block_size=1 << 20, method=0x82) -
     return out[:n].tobytes()
 
 
-def decompress_stream(blob: bytes, cap: int) -> bytes:
+def decompress_stream(blob: bytes, cap: int, verify: bool = True) -> bytes:
     src = np.frombuffer(blob, np.uint8)
     out = np.empty(max(cap, 1), np.uint8)
-    n = lib().orc_decompress_stream(_p(src), src.size, _p(out), cap)
+    n = lib().orc_decompress_stream(_p(src), src.size, _p(out), cap, int(verify))
+    if n == -2:
+        raise ValueError("CHECKSUM_DOESNT_MATCH")
     if n < 0:
         raise ValueError("CANNOT_DECOMPRESS")
     return out[:n].tobytes()
+
+
+def cityhash128(data) -> tuple:
+    """CityHash_v1_0_2::CityHash128 (oracle restatement): (low64, high64)."""
+    src = np.frombuffer(bytes(data), np.uint8)
+    h = np.zeros(2, np.uint64)
+    lib().orc_cityhash128(_p(src) if src.size else None, src.size, _p(h))
+    return int(h[0]), int(h[1])
+
+
+def checksum_bytes(data) -> bytes:
+    """The 16 checksum bytes ClickHouse stores before a compressed block."""
+    lo, hi = cityhash128(data)
+    return lo.to_bytes(8, "little") + hi.to_bytes(8, "little")
 
 
 def array_rows(data_f32, sizes_u64, d):

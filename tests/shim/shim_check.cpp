@@ -58,9 +58,9 @@ static int errors() {
     }
     // direct C-ABI status mapping
     const int st[] = {MQVS_ERR_NOT_IMPLEMENTED, MQVS_ERR_LOGICAL, MQVS_ERR_ILLEGAL_COLUMN,
-                      MQVS_ERR_BAD_ARGUMENTS, MQVS_ERR_MEMORY_LIMIT, MQVS_ERR_DEVICE};
-    const int want[] = {48, 49, 44, 36, 241, 49};
-    for (int i = 0; i < 6; ++i) {
+                      MQVS_ERR_BAD_ARGUMENTS, MQVS_ERR_MEMORY_LIMIT, MQVS_ERR_DEVICE, MQVS_ERR_CHECKSUM};
+    const int want[] = {48, 49, 44, 36, 241, 49, 40};
+    for (int i = 0; i < 7; ++i) {
         try {
             MI::check(st[i]);
             return 1;

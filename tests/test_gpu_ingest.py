@@ -115,7 +115,8 @@ def _hand_block(offset):
     """12 bytes = 3 floats: literal "abcd", a 4-byte match at `offset`, last
     literals "wxyz" (LZ4 block format)."""
     blk = bytes([0x40]) + b"abcd" + struct.pack("<H", offset) + bytes([0x40]) + b"wxyz"
-    return bytes(16) + struct.pack("<BII", 0x82, 9 + len(blk), 12) + blk
+    body = struct.pack("<BII", 0x82, 9 + len(blk), 12) + blk
+    return O.checksum_bytes(body) + body
 
 
 def test_gpu_ingest_hand_built_lz4(mq):
@@ -147,3 +148,54 @@ def test_gpu_ingest_errors(mq, what, status):
     with pytest.raises(_lib.MqvsError) as e:
         mq.VectorScanSegment.from_column(db, sb, nn, d, metric="L2")
     assert e.value.status == status, str(e.value)
+
+
+@pytest.mark.parametrize("stream,where", [("data", "payload"), ("data", "stored"), ("sizes", "payload")])
+def test_gpu_ingest_checksum_mismatch(mq, stream, where):
+    """CompressedReadBufferBase.cpp:192-196: a corrupted block fails with
+    CHECKSUM_DOESNT_MATCH (status 7, ClickHouse code 40) before decoding;
+    with verification disabled the (NONE-method) block decodes as stored."""
+    from myscaledb_amd import _lib
+    rng = np.random.default_rng(15)
+    n, d = 3000, 16
+    rows = rng.standard_normal((n, d)).astype(np.float32)
+    db, sb = column_files(rows, np.full(n, d, np.uint64), 1 << 14, 0x02)
+    b = bytearray(db if stream == "data" else sb)
+    b[25 + 1000 if where == "payload" else 5] ^= 0x04
+    db, sb = (bytes(b), sb) if stream == "data" else (db, bytes(b))
+    with pytest.raises(_lib.MqvsError) as e:
+        mq.VectorScanSegment.from_column(db, sb, n, d, metric="L2")
+    assert e.value.status == _lib.ERR_CHECKSUM, str(e.value)
+    assert _lib.CLICKHOUSE_CODE[e.value.status] == 40
+    if stream == "data":
+        seg = mq.VectorScanSegment.from_column(db, sb, n, d, metric="L2", verify_checksum=False)
+        try:
+            want = np.frombuffer(O.decompress_stream(db, rows.nbytes, verify=False), np.float32).reshape(n, d)
+            assert np.array_equal(device_rows(mq, seg).view(np.uint32), want.view(np.uint32))
+        finally:
+            seg.free()
+
+
+def test_gpu_checksum_every_block_length(mq):
+    """Blocks of 1..400 payload bytes (hashed lengths 10..409: every
+    CityMurmur / 128-byte-loop / tail branch) at every byte alignment, NONE and
+    LZ4 alternating: the GPU CityHash128 must accept all of them (one wrong
+    hash fails the ingest) and the rows must round-trip bit-exactly."""
+    rng = np.random.default_rng(16)
+    n, d = 700, 64
+    rows = np.round(rng.standard_normal((n, d)), 1).astype(np.float32)
+    raw = rows.tobytes()
+    parts, o, blen = [], 0, 1
+    while o < len(raw):
+        take = min(blen, len(raw) - o)
+        parts.append(O.compress_stream(raw[o:o + take], take, 0x02 if blen % 2 else 0x82))
+        o += take
+        blen = blen % 400 + 1
+    db = b"".join(parts)
+    sb = O.compress_stream(np.full(n, d, np.uint64).tobytes(), 1 << 20)
+    assert O.decompress_stream(db, len(raw)) == raw
+    seg = mq.VectorScanSegment.from_column(db, sb, n, d, metric="L2")
+    try:
+        assert np.array_equal(device_rows(mq, seg).view(np.uint32), rows.view(np.uint32))
+    finally:
+        seg.free()

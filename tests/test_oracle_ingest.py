@@ -7,6 +7,9 @@ MergeTreeVSManager.cpp:1381-1393 (copy loop).  No compressed fixture ships
 with the reference, so the decoder is pinned by hand-built blocks that follow
 the LZ4 block format and by compress -> decompress round trips.
 """
+import ctypes
+import json
+import os
 import struct
 
 import numpy as np
@@ -16,7 +19,57 @@ from oracle import oracle as O
 
 
 def frame(payload: bytes, usize: int, method=0x82) -> bytes:
-    return bytes(16) + struct.pack("<BII", method, 9 + len(payload), usize) + payload
+    body = struct.pack("<BII", method, 9 + len(payload), usize) + payload
+    return O.checksum_bytes(body) + body
+
+
+# Block checksum (CompressedReadBufferBase.cpp:37-45, CityHash128 v1.0.2):
+# pinned by golden vectors from the reference's own city.cc
+# (tests/golden/cityhash102.json, made by tests/golden/make_cityhash.py) and,
+# when oracle/_ref is built, against that build directly.
+GOLDEN = os.path.join(os.path.dirname(__file__), "golden", "cityhash102.json")
+REF_CITY = os.path.join(os.path.dirname(__file__), "..", "oracle", "_ref", "libcityref.so")
+
+
+def golden_data(n):
+    return ((np.arange(n, dtype=np.int64) * 131 + n * 7 + 3) & 255).astype(np.uint8).tobytes()
+
+
+def test_cityhash_golden_vectors():
+    """Oracle CityHash128 == the reference city.cc on every golden length
+    (0..199 covers every short / murmur / tail branch; up to 1 MiB + 9)."""
+    vec = json.load(open(GOLDEN))["vectors"]
+    assert len(vec) >= 200
+    for v in vec:
+        lo, hi = O.cityhash128(golden_data(v["len"]))
+        assert (f"{lo:016x}", f"{hi:016x}") == (v["lo"], v["hi"]), v["len"]
+
+
+@pytest.mark.skipif(not os.path.exists(REF_CITY), reason="oracle/_ref not built (make -C oracle ref)")
+def test_cityhash_vs_reference_build():
+    ref = ctypes.CDLL(REF_CITY)
+    ref.ref_cityhash128.argtypes = [ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p]
+    rng = np.random.default_rng(9)
+    for n in list(range(0, 300)) + [1023, 4096 + 9, 65536 + 37]:
+        a = rng.integers(0, 256, n, dtype=np.uint8)
+        h = np.zeros(2, np.uint64)
+        ref.ref_cityhash128(a.ctypes.data if n else None, n, h.ctypes.data)
+        assert O.cityhash128(a.tobytes()) == (int(h[0]), int(h[1])), n
+
+
+@pytest.mark.parametrize("where", ["payload", "header", "stored"])
+def test_checksum_mismatch_detected(where):
+    """A flipped bit anywhere in a block -> CHECKSUM_DOESNT_MATCH before any
+    decoding (CompressedReadBufferBase.cpp:192-196); verify=False decodes."""
+    data = np.arange(5000, dtype=np.float32).tobytes()
+    c = bytearray(O.compress_stream(data, 4096, 0x02))
+    pos = {"payload": 25 + 100, "header": 16 + 5, "stored": 3}[where]
+    c[pos] ^= 0x10
+    with pytest.raises(ValueError, match="CHECKSUM"):
+        O.decompress_stream(bytes(c), len(data))
+    if where != "header":  # sizes intact: decodes without verification
+        out = O.decompress_stream(bytes(c), len(data), verify=False)
+        assert len(out) == len(data) and (out == data) == (where == "stored")
 
 
 def test_lz4_hand_built_blocks():
