@@ -267,8 +267,8 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
 // before it.  CityHash is a sequential chain, so one lane hashes one block
 // (1 MiB blocks: ~3k lanes for a 3 GB column).  Blocks start at arbitrary byte
 // offsets: every 64-bit word is assembled from aligned dwords with
-// v_alignbyte (the shift is fixed per block), and the next 64-byte round's
-// dwords are loaded while the current round is mixed.
+// v_alignbyte (the shift is fixed per block), and the next three 64-byte
+// rounds' dwords are loaded while the current three are mixed.
 namespace city {
 constexpr uint64_t K0 = 0xc3a5c85c97cb3127ULL, K1 = 0xb492b66fbe98f273ULL, K2 = 0x9ae16a3b2f90404fULL,
                    K3 = 0xc949d7c7509e6557ULL;
@@ -364,27 +364,42 @@ __device__ void seeded(const uint8_t *s, uint64_t len, uint64_t x, uint64_t y, u
     const uintptr_t a0 = (uintptr_t)s;
     const uint32_t sh = (uint32_t)(a0 & 3);
     const uint32_t *base = reinterpret_cast<const uint32_t *>(a0 & ~(uintptr_t)3);
-    uint32_t cur[17];
-    load_round(base, sh, cur);
-    for (int64_t r = 0; r < rounds; ++r) {
-        uint32_t nxt[17];
-        load_round(base + 16 * (r + 1 < rounds ? r + 1 : r), sh, nxt);  // in flight during the mix
-        uint64_t q[8];
+    // kAhead rounds in flight while kAhead rounds are mixed (3 x 17 dword
+    // loads stay under the 63 outstanding vector loads a wave can count)
+    constexpr int kAhead = 3;
+    uint32_t cur[kAhead][17];
 #pragma unroll
-        for (int i = 0; i < 8; ++i)
-            q[i] = (uint64_t)join(cur[2 * i], cur[2 * i + 1], sh) | ((uint64_t)join(cur[2 * i + 1], cur[2 * i + 2], sh) << 32);
-        x = ror(x + y + v1 + q[2], 37) * K1;
-        y = ror(y + v2 + q[6], 42) * K1;
-        x ^= w2;
-        y ^= v1;
-        z = ror(z ^ w1, 33);
-        weak32(q[0], q[1], q[2], q[3], v2 * K1, x + w1, v1, v2);
-        weak32(q[4], q[5], q[6], q[7], z + w2, y, w1, w2);
-        const uint64_t t = z;
-        z = x;
-        x = t;
+    for (int j = 0; j < kAhead; ++j) load_round(base + 16 * (j < rounds ? j : rounds - 1), sh, cur[j]);
+    for (int64_t r = 0; r < rounds; r += kAhead) {
+        uint32_t nxt[kAhead][17];
 #pragma unroll
-        for (int i = 0; i < 17; ++i) cur[i] = nxt[i];
+        for (int j = 0; j < kAhead; ++j) {
+            const int64_t rr = r + kAhead + j;
+            load_round(base + 16 * (rr < rounds ? rr : rounds - 1), sh, nxt[j]);
+        }
+#pragma unroll
+        for (int j = 0; j < kAhead; ++j) {
+            if (r + j >= rounds) break;
+            uint64_t q[8];
+#pragma unroll
+            for (int i = 0; i < 8; ++i)
+                q[i] = (uint64_t)join(cur[j][2 * i], cur[j][2 * i + 1], sh) |
+                       ((uint64_t)join(cur[j][2 * i + 1], cur[j][2 * i + 2], sh) << 32);
+            x = ror(x + y + v1 + q[2], 37) * K1;
+            y = ror(y + v2 + q[6], 42) * K1;
+            x ^= w2;
+            y ^= v1;
+            z = ror(z ^ w1, 33);
+            weak32(q[0], q[1], q[2], q[3], v2 * K1, x + w1, v1, v2);
+            weak32(q[4], q[5], q[6], q[7], z + w2, y, w1, w2);
+            const uint64_t t = z;
+            z = x;
+            x = t;
+        }
+#pragma unroll
+        for (int j = 0; j < kAhead; ++j)
+#pragma unroll
+            for (int i = 0; i < 17; ++i) cur[j][i] = nxt[j][i];
     }
     s += 64 * rounds;
     len -= 64 * (uint64_t)rounds;
