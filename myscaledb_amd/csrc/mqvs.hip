@@ -943,8 +943,16 @@ struct IngestTmp {
         bufs.push_back(p);
         return p;
     }
+    // side stream for the block checksums (overlaps the decode; joined before
+    // the status is read)
+    hipStream_t side = nullptr;
+    hipEvent_t fork = nullptr, join = nullptr;
     ~IngestTmp() {
+        if (side) (void)hipStreamSynchronize(side);
         for (void *p : bufs) (void)hipFree(p);
+        if (fork) (void)hipEventDestroy(fork);
+        if (join) (void)hipEventDestroy(join);
+        if (side) (void)hipStreamDestroy(side);
     }
 };
 
@@ -999,9 +1007,17 @@ static mqvs_segment *ingest_column(const uint8_t *data_bin, int64_t data_bytes, 
         if (dt.second % 4) fail(MQVS_ERR_ILLEGAL_COLUMN, "vector data stream is not a whole number of Float32");
         int *status = (int *)tmp.alloc(sizeof(int) * 4);
         MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
-        if (!(flags & MQVS_F_NO_CHECKSUM)) {  // CompressedReadBufferBase.cpp:192-196, before decompression
-            launch_block_checksum(ds, tab_s, sz.first, kBadSizesChecksum, status, nullptr, s);
-            launch_block_checksum(dd, tab_d, dt.first, kBadDataChecksum, status, nullptr, s);
+        const bool verify = !(flags & MQVS_F_NO_CHECKSUM);
+        if (verify) {  // CompressedReadBufferBase.cpp:192-196; the verdict is read before any decoded byte is used
+            MQVS_HIP(hipStreamCreateWithFlags(&tmp.side, hipStreamNonBlocking));
+            MQVS_HIP(hipEventCreateWithFlags(&tmp.fork, hipEventDisableTiming));
+            MQVS_HIP(hipEventCreateWithFlags(&tmp.join, hipEventDisableTiming));
+            MQVS_HIP(hipEventRecord(tmp.fork, s));
+            MQVS_HIP(hipStreamWaitEvent(tmp.side, tmp.fork, 0));
+            launch_block_checksum(ds, tab_s, sz.first, kBadSizesChecksum, status, nullptr, tmp.side);
+            launch_block_checksum(dd, tab_d, dt.first, kBadDataChecksum, status, nullptr, tmp.side);
+            MQVS_HIP(hipGetLastError());
+            MQVS_HIP(hipEventRecord(tmp.join, tmp.side));
         }
         auto *sizes = (uint64_t *)tmp.alloc(sizeof(uint64_t) * (size_t)std::max<int64_t>(n, 1));
         launch_decode_blocks(ds, sizes_bytes, tab_s, sz.first, (uint8_t *)sizes, status, s);
@@ -1019,6 +1035,7 @@ static mqvs_segment *ingest_column(const uint8_t *data_bin, int64_t data_bytes, 
         MQVS_HIP(hipGetLastError());
         MQVS_HIP(hipMemcpyAsync(h, st, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
         int *hstatus = reinterpret_cast<int *>(h + 2);
+        if (verify) MQVS_HIP(hipStreamWaitEvent(s, tmp.join, 0));
         MQVS_HIP(hipMemcpyAsync(hstatus, status, sizeof(int), hipMemcpyDeviceToHost, s));
         MQVS_HIP(hipStreamSynchronize(s));
         if (*hstatus & (kBadSizesChecksum | kBadDataChecksum))
