@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define MQVS_ABI_VERSION 1
+#define MQVS_ABI_VERSION 2
 
 /* Metric ids (VICommon.h VIMetric).  L2 / IP / Cosine: Float32 vectors;
  * Hamming / Jaccard: binary vectors (FixedString(N) columns, mqvs_*_binary). */
@@ -316,8 +316,12 @@ typedef struct {
     int32_t segments;       /* main-scan segments (threshold refinements + 1) */
     int32_t gather;         /* 1: selective PREWHERE, the scan walked the gather list
                                of selected rows (rows_scanned = list entries) */
-    int32_t prefilter;      /* path 2: pre-filter split (6 = bf16 + fp6 MX, 3 = bf16 x3) */
+    int32_t prefilter;      /* path 2: pre-filter split (2 = bf16 hi, 6 = bf16 + fp6 MX,
+                               3 = bf16 x3) */
     int32_t reserved;
+    int64_t survivors_total;/* path 2: rows re-ranked exactly (sum over queries) */
+    int32_t survivors_max;  /* path 2: most rows re-ranked for one query */
+    int32_t candidates_max; /* path 2: longest candidate list before the final bound */
 } mqvs_search_stats;
 int mqvs_last_search_stats(mqvs_search_stats *out);
 /* Enable per-search HIP-event timing (off by default: one extra event pair). */

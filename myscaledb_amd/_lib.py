@@ -49,7 +49,9 @@ class SearchStats(ctypes.Structure):
                 ("nq", ctypes.c_int32), ("k", ctypes.c_int32),
                 ("path", ctypes.c_int32), ("rescans", ctypes.c_int32),
                 ("segments", ctypes.c_int32), ("gather", ctypes.c_int32),
-                ("prefilter", ctypes.c_int32), ("reserved", ctypes.c_int32)]
+                ("prefilter", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("survivors_total", ctypes.c_int64), ("survivors_max", ctypes.c_int32),
+                ("candidates_max", ctypes.c_int32)]
 
 
 class IndexInfo(ctypes.Structure):

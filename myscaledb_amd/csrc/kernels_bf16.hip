@@ -113,7 +113,7 @@ __global__ void k_query_bound(ScanParams p, int metric, int split, int direct,
     const int64_t qs = (int64_t)((p.d + 31) / 32 * 32);
     const int nv = p.maxv <= 1 ? 1 : p.qmu[j] + p.qlam[j];
     float xmax = 0.f;
-    for (int v = 0; v < (split == kMxSplit ? 0 : nv); ++v) {
+    for (int v = 0; v < (split == kMxSplit || split == kHiSplit ? 0 : nv); ++v) {
         const float *x = p.qvars + ((int64_t)j * p.maxv + v) * qs;
         double s = 0.0;
         for (int i = lane; i < p.d; i += 64) s += (double)x[i] * (double)x[i];
@@ -124,7 +124,23 @@ __global__ void k_query_bound(ScanParams p, int metric, int split, int direct,
     const float ymax = *ynorm_max * (1.0f + 6e-8f * (float)p.d + 1e-6f);  // fp32 |y|^2 chain error
     const float du = (float)p.d * 5.9604645e-8f;
     float b;
-    if (split == kMxSplit) {
+    if (split == kHiSplit) {
+        // x.y - xh.yh = xh.ry + rx.yh + rx.ry (records: q[0] |xh|, q[1] |rx|,
+        // q[6] |x|; Y the segment maxima); the MFMA sums d exact products, at
+        // most 2 u relative per addition (2.04 d u |xh||yh|, covers
+        // round-toward-zero; measured: tools/mfma_acc_probe.hip); the exact
+        // chain's own error 1.01 d u |x||y| + one ulp
+        const float *Y = yrec;
+        b = 0.f;
+        for (int v = 0; v < nv; ++v) {
+            const float *q = qrec + ((int64_t)j * p.maxv + v) * kMxRec;
+            xmax = fmaxf(xmax, q[6]);
+            const float trunc = q[0] * Y[1] + q[1] * Y[0] + q[1] * Y[1];
+            const float bv = trunc + 2.04f * du * q[0] * Y[0] + 1.01f * du * q[6] * ymax + 1.2e-7f * q[6] * ymax;
+            b = fmaxf(b, bv * 1.0001f);
+        }
+        b += 1e-30f;
+    } else if (split == kMxSplit) {
         const float *Y = yrec;
         b = 0.f;
         for (int v = 0; v < nv; ++v) {
@@ -315,6 +331,11 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_select(ScanParams p, con
     }
     __syncthreads();
     int m = s_cnt;
+    if (threadIdx.x == 0) {
+        atomicMax(overflow + 1, m);      // survivors of the bound (stats)
+        atomicAdd(overflow + 2, m);
+        atomicMax(overflow + 3, n);      // candidates before it
+    }
     if (m > kSortCap) {
         if (threadIdx.x == 0) atomicOr(overflow, 4);
         m = kSortCap;

@@ -1,0 +1,429 @@
+// kernels_hi.hip -- bf16-hi pre-filter (split 2, the default): ONE bf16 MFMA
+// per block-step on the bf16 roundings of rows and queries, a rigorous error
+// bound from norms measured at quantisation, and the exact fp32 re-rank of the
+// survivors (kernels_bf16.hip, k_rerank_select).
+//
+// Why one product is enough.  With h = bf16_rn(v) and r = v - h (exact),
+//     x.y - xh.yh = xh.ry + rx.yh + rx.ry
+// so |x.y - xh.yh| <= |xh||ry| + |rx||yh| + |rx||ry| (Cauchy-Schwarz), where
+// |r| / |v| is ~2^-9 for any vector (round-to-nearest to 8 significant bits).
+// The margin this leaves around the k-th value (~0.004 of |x||y|) admits a
+// few hundred extra rows per query on the Gaussian / mixture parts measured;
+// every one of them is re-ranked with the exact fp32 chain, so the output is
+// bit-identical to the fp32 path.  Against the bf16 + fp6-MX pre-filter
+// (kernels_mx.hip, split 6) this streams 2 B per element instead of 3.5 and
+// issues 2 MFMAs per 32-column stage and 32x32 block instead of 3 -- the MX
+// kernel was bound by exactly that L2 -> LDS stream.
+//
+// Planes are row-blocked as the MX hi plane (16 vectors x 32 columns = 1 KiB
+// contiguous): vector u, stage s at byte ((u >> 4) nst + s) 1024 + (u & 15) 64.
+//
+// Scan pipeline: a ring of NBUF LDS stages (stage = 32 columns of the 256-row
+// tile and of the QT-query tile, filled by global_load_lds_dwordx4 in 1 KiB
+// pieces), NBUF - 1 stages in flight.  Per stage: a counted vmcnt for this
+// wave's pieces of the stage being consumed (later stages stay in flight), ONE
+// raw s_barrier (every wave's pieces have landed; every wave is done with the
+// stage consumed before, whose buffer is re-issued right after the barrier),
+// then the MFMA work.  No __syncthreads() in the loop: its fence would drain
+// the in-flight LDS-DMA (cdna_hip_programming.md, "Pipelining across barriers").
+#include <cstdio>
+#include <cstdlib>
+
+#include "mqvs_internal.h"
+#include "scan_emit.h"
+
+namespace mqvs {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned int bf16x4x2 __attribute__((ext_vector_type(4)));  // 8 bf16 as 4 dwords (16-B loads)
+typedef __attribute__((address_space(3))) void lds_void;
+
+constexpr int HI_K = 32;  // columns per stage
+
+// sqrt(s) rounded up to float
+__device__ inline float hi_sqrt_up(double s) { return (float)(sqrt(s) * (1.0 + 1e-7)); }
+
+// ---------------------------------------------------------------------------
+// quantisation: source vector v -> plane vector u = (v % vgroup) vpad + v / vgroup
+// record (kMxRec floats, the MX record's slots): [0] |h|, [1] |r|, [6] |x|
+__global__ __launch_bounds__(256) void k_to_hi(const float *src, int64_t rows, int d, int64_t sstride, int64_t dpad,
+                                               int64_t vgroup, int64_t vpad, uint16_t *hi, float *rec,
+                                               float *maxrec) {
+    const int lane = threadIdx.x & 63;
+    const int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    if (v >= rows) return;  // whole wave
+    const float *x = src + v * sstride;
+    const int nb = (int)(dpad / HI_K);
+    const int64_t u = (v % vgroup) * vpad + v / vgroup;
+    uint16_t *hu = hi + (u >> 4) * nb * 512 + (u & 15) * 32;
+    double nx = 0, nh = 0, nr = 0;
+    for (int64_t i = lane; i < dpad; i += 64) {
+        const float xv = i < d ? x[i] : 0.f;
+        const uint16_t hb = f32_to_bf16_rn(xv);
+        const float hv = __builtin_bit_cast(float, (uint32_t)hb << 16);
+        const float rv = xv - hv;  // exact
+        hu[(i >> 5) * 512 + (i & 31)] = hb;
+        nx += (double)xv * xv;
+        nh += (double)hv * hv;
+        nr += (double)rv * rv;
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+        nx += __shfl_xor(nx, off);
+        nh += __shfl_xor(nh, off);
+        nr += __shfl_xor(nr, off);
+    }
+    if (lane == 0) {
+        float r[kMxRec] = {hi_sqrt_up(nh), hi_sqrt_up(nr), 0.f, 0.f, 0.f, 0.f, hi_sqrt_up(nx), 0.f};
+#pragma unroll
+        for (int t = 0; t < kMxRec; ++t) {
+            if (rec) rec[v * kMxRec + t] = r[t];
+            if (maxrec && (t < 2 || t == 6)) {
+                // non-negative floats order as their bit patterns; NaN -> +inf
+                const unsigned b = (r[t] == r[t]) ? __builtin_bit_cast(unsigned, r[t]) : 0x7F800000u;
+                atomicMax(reinterpret_cast<unsigned *>(maxrec) + t, b);
+            }
+        }
+    }
+}
+
+void launch_to_hi(const float *src, int64_t rows, int d, int64_t src_stride, int64_t dpad, int64_t vgroup,
+                  int64_t vpad, uint16_t *hi, float *rec, float *maxrec, hipStream_t s) {
+    if (rows <= 0) return;
+    const int64_t blocks = (rows + 3) / 4;
+    hipLaunchKernelGGL(k_to_hi, dim3((unsigned)blocks), dim3(256), 0, s, src, rows, d, src_stride, dpad, vgroup, vpad,
+                       hi, rec, maxrec);
+}
+
+// ---------------------------------------------------------------------------
+// scan
+
+__device__ inline int hswz(int r, int c) { return c ^ ((r >> 2) & 3); }
+
+// s_waitcnt vmcnt(N) + raw s_barrier, N a compile-time count
+template <int N>
+__device__ inline void wait_barrier() {
+    asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
+}
+
+template <int GPW, int NBUF>
+__device__ inline void wait_stage(int pending) {
+    // pending: stages issued after the one about to be consumed (0 .. NBUF-2)
+    static_assert(NBUF >= 2 && NBUF <= 4, "ring depth");
+    if (NBUF >= 4 && pending >= 2) {
+        wait_barrier<GPW * 2>();
+    } else if (NBUF >= 3 && pending >= 1) {
+        wait_barrier<GPW * 1>();
+    } else {
+        wait_barrier<0>();
+    }
+}
+
+// Workgroup tile 256 rows x QT queries (QT = 32 QB WQ), 4 x WQ waves of 64
+// rows x 32 QB queries, 32x32x16 bf16 MFMA blocks; workgroup -> (row tile,
+// query block) with the query blocks of a row tile on one XCD (its L2 serves
+// the tile's re-reads).
+template <int METRIC, bool PROBE, int WQ, int QB, int NBUF>
+__global__ __launch_bounds__(256 * WQ) void k_scan_hi(ScanParams p) {
+    constexpr int WR = 4;
+    constexpr int NW = WR * WQ;
+    constexpr int QT = 32 * QB * WQ;
+    constexpr int RT = kBfRows;     // 256
+    constexpr int GY = RT / 16;     // 1-KiB pieces of the Y image
+    constexpr int GQ = QT / 16;     // 1-KiB pieces of the Q image
+    constexpr int G = GY + GQ;
+    static_assert(G % NW == 0, "stage pieces must split evenly over the waves");
+    constexpr int GPW = G / NW;
+    constexpr int STAGE = G * 1024;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[NBUF * STAGE];
+
+    const int64_t L = p.tiles * p.num_qblocks;
+    const int64_t cpx = (L + 7) / 8;
+    const int64_t b = blockIdx.x;
+    const int64_t l = (b % 8) * cpx + b / 8;  // query blocks of a row tile on one XCD
+    if (l >= L) return;
+    const int64_t ti = l / p.num_qblocks;
+    const int qb = (int)(l % p.num_qblocks);
+    int64_t r0, r1, chunk;
+    tile_range(p, ti, r0, r1, chunk);
+    if (r0 >= r1) return;
+    const int ord = chunk_ordinal(p, chunk);
+    const int t = threadIdx.x;
+    const int lane = t & 63, w = t >> 6;
+    const int wr = w % WR, wq = w / WR;
+    const int q0 = qb * QT;
+
+    if (ord < 0) {
+        if (PROBE) {
+            for (int i = t; i < RT * QT; i += 64 * NW) {
+                const int64_t row = r0 + (i % RT);
+                const int j = q0 + i / RT;
+                if (row < r1 && j < p.nq) emit_approx<METRIC, true>(p, j, row, -1, false, 0.f);
+            }
+        }
+        return;
+    }
+
+    const int nb = (int)(p.dpad / HI_K);
+    // piece g = w + i NW fills 16 image rows; lane -> (image row lane / 4,
+    // slot lane % 4) holds chunk hswz(row, slot)
+    const unsigned char *src[GPW];
+#pragma unroll
+    for (int i = 0; i < GPW; ++i) {
+        const int g = w + i * NW;
+        const bool isy = g < GY;
+        const int r = (isy ? g : g - GY) * 16 + (lane >> 2);
+        const int c = hswz(r, lane & 3);
+        int64_t u;
+        const uint16_t *plane;
+        if (isy) {
+            const int64_t gp = r0 + r;
+            u = gp < r1 ? row_at(p, gp) : -1;
+            if (u < 0) u = row_at(p, r0);  // padding: any real row, results discarded
+            plane = p.rows_hi;
+        } else {
+            int j = q0 + r;
+            if (j >= p.nq) j = 0;
+            u = (int64_t)variant_of(p, j, ord) * p.q_vpad + j;
+            plane = p.q_hi;
+        }
+        src[i] = reinterpret_cast<const unsigned char *>(plane) + ((u >> 4) * nb * 1024 + (u & 15) * 64 + c * 16);
+    }
+    auto issue = [&](int s) {
+        unsigned char *dst = lds + (s % NBUF) * STAGE;
+#pragma unroll
+        for (int i = 0; i < GPW; ++i)
+            __builtin_amdgcn_global_load_lds((const void *)(src[i] + (int64_t)s * 1024),
+                                             (lds_void *)(dst + (w + i * NW) * 1024), 16, 0, 0);
+    };
+
+    constexpr int OFF_Q = GY * 1024;
+    const int h = lane >> 5, l32 = lane & 31;
+    auto frag = [&](const unsigned char *st, int r, int c) {
+        return *reinterpret_cast<const bf16x8 *>(st + r * 64 + hswz(r, c) * 16);
+    };
+    const int ra0 = wr * 64 + l32;
+    const int rq0 = wq * 32 * QB + l32;
+
+    f32x16 acc[2][QB];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int jb = 0; jb < QB; ++jb) acc[i][jb] = f32x16{0};
+
+    const int nst = (int)(p.dpad / HI_K);
+    // prologue: stages 0 .. NBUF-2 in flight
+#pragma unroll
+    for (int s = 0; s < NBUF - 1; ++s)
+        if (s < nst) issue(s);
+    for (int s = 0; s < nst; ++s) {
+        const int after = nst - 1 - s;  // stages after s
+        wait_stage<GPW, NBUF>(after < NBUF - 2 ? after : NBUF - 2);
+        // every wave is past its reads of stage s-1: its buffer takes stage s+NBUF-1
+        if (s + NBUF - 1 < nst) {
+            __builtin_amdgcn_sched_barrier(0);
+            issue(s + NBUF - 1);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        const unsigned char *st = lds + (s % NBUF) * STAGE;
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int kk = 0; kk < 2; ++kk) {
+            const int c = 2 * kk + h;
+            bf16x8 ah[2], bh[QB];
+#pragma unroll
+            for (int i = 0; i < 2; ++i) ah[i] = frag(st, ra0 + 32 * i, c);
+#pragma unroll
+            for (int jb = 0; jb < QB; ++jb) bh[jb] = frag(st + OFF_Q, rq0 + 32 * jb, c);
+#pragma unroll
+            for (int i = 0; i < 2; ++i)
+#pragma unroll
+                for (int jb = 0; jb < QB; ++jb)
+                    acc[i][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[jb], acc[i][jb], 0, 0, 0);
+        }
+        __builtin_amdgcn_s_setprio(0);
+        // (the next iteration's barrier orders these reads before the buffer
+        // is re-issued: the MFMAs consumed every fragment, so the reads retired)
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    }
+#pragma unroll
+    for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+        for (int jb = 0; jb < QB; ++jb) {
+            const int j = q0 + rq0 + jb * 32;
+            if (j >= p.nq) continue;
+            const int64_t rbase = r0 + wr * 64 + rb * 32 + 4 * h;
+            emit_vals<METRIC, PROBE, 16>(
+                p, j, r1, [&](int r) { return rbase + (r & 3) + 8 * (r >> 2); },
+                [&](int r) { return acc[rb][jb][r]; });
+        }
+}
+
+// Small batches (nq <= 32): HBM-bound, so no LDS staging at all.  The 256-row
+// tile is 16 row blocks of 16 rows; wave w takes blocks w, w+4, w+8, w+12.  A
+// row block's 32-column stage is ONE contiguous KiB of the row-blocked plane
+// and exactly the A operand of v_mfma_f32_16x16x32_bf16 (lane l: row l & 15,
+// columns 8 (l >> 4) .. +8), so each stage is one global_load_dwordx4 straight
+// into the fragment; a block's whole row (nst loads, 24 KiB at d = 768) is in
+// flight while the previous block feeds the MFMAs.  The query tile (NQB blocks
+// of 16 queries, every stage's B fragment: 4 VGPRs each) stays in registers.
+template <int METRIC, bool PROBE, int NQB, int NST>
+__global__ __launch_bounds__(256) void k_scan_hi_reg(ScanParams p) {
+    constexpr int RT = kBfRows;
+    const int64_t ti = blockIdx.x / p.num_qblocks;
+    const int qb = (int)(blockIdx.x % p.num_qblocks);
+    if (ti >= p.tiles) return;
+    int64_t r0, r1, chunk;
+    tile_range(p, ti, r0, r1, chunk);
+    if (r0 >= r1) return;
+    const int ord = chunk_ordinal(p, chunk);
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int l16 = lane & 15, c = lane >> 4;
+    const int q0 = qb * 16 * NQB;
+    if (ord < 0) {
+        if (PROBE) {
+            for (int i = t; i < RT * 16 * NQB; i += 256) {
+                const int64_t row = r0 + (i % RT);
+                const int j = q0 + i / RT;
+                if (row < r1 && j < p.nq) emit_approx<METRIC, true>(p, j, row, -1, false, 0.f);
+            }
+        }
+        return;
+    }
+    const int nb = (int)(p.dpad / HI_K);  // == NST (template: registers)
+    bf16x4x2 qf[NQB][NST];
+#pragma unroll
+    for (int jb = 0; jb < NQB; ++jb) {
+        int j = q0 + 16 * jb + l16;
+        if (j >= p.nq) j = 0;
+        const int64_t u = (int64_t)variant_of(p, j, ord) * p.q_vpad + j;
+        const unsigned char *qs = reinterpret_cast<const unsigned char *>(p.q_hi) + (u >> 4) * nb * 1024 +
+                                  (u & 15) * 64 + c * 16;
+#pragma unroll
+        for (int s = 0; s < NST; ++s) qf[jb][s] = *reinterpret_cast<const bf16x4x2 *>(qs + (int64_t)s * 1024);
+    }
+    auto rowsrc = [&](int rb) {
+        const int64_t gp = r0 + 16 * rb + l16;
+        int64_t u = gp < r1 ? row_at(p, gp) : -1;
+        if (u < 0) u = row_at(p, r0);  // padding: any real row, results discarded
+        return reinterpret_cast<const unsigned char *>(p.rows_hi) + (u >> 4) * nb * 1024 + (u & 15) * 64 + c * 16;
+    };
+    bf16x4x2 a[2][NST];
+    auto load = [&](int buf, int rb) {
+        const unsigned char *src = rowsrc(rb);
+#pragma unroll
+        for (int s = 0; s < NST; ++s) a[buf][s] = *reinterpret_cast<const bf16x4x2 *>(src + (int64_t)s * 1024);
+    };
+    load(0, w);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        const int rb = w + 4 * i;
+        if (i + 1 < 4) load((i + 1) & 1, rb + 4);
+        f32x4 acc[NQB];
+#pragma unroll
+        for (int jb = 0; jb < NQB; ++jb) acc[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int s = 0; s < NST; ++s)
+#pragma unroll
+            for (int jb = 0; jb < NQB; ++jb)
+                acc[jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a[i & 1][s]),
+                                                                 __builtin_bit_cast(bf16x8, qf[jb][s]), acc[jb],
+                                                                 0, 0, 0);
+        // C: lane (l16, c) holds rows 4c .. 4c+3 of the block for query l16
+#pragma unroll
+        for (int jb = 0; jb < NQB; ++jb) {
+            const int j = q0 + 16 * jb + l16;
+            if (j >= p.nq) continue;
+            const int64_t rbase = r0 + 16 * rb + 4 * c;
+            emit_vals<METRIC, PROBE, 4>(
+                p, j, r1, [&](int r) { return rbase + r; }, [&](int r) { return acc[jb][r]; });
+        }
+    }
+}
+
+template <int METRIC, bool PROBE, int NQB>
+static void launch_hi_reg(ScanParams p, hipStream_t s) {
+    p.num_qblocks = (p.nq + 16 * NQB - 1) / (16 * NQB);
+    const int64_t grid = p.tiles * p.num_qblocks;
+    if (grid < 1) return;
+    switch (p.dpad / HI_K) {
+#define MQVS_HI_REG(N_) \
+    case N_: hipLaunchKernelGGL((k_scan_hi_reg<METRIC, PROBE, NQB, N_>), dim3((unsigned)grid), dim3(256), 0, s, p); return;
+        MQVS_HI_REG(2) MQVS_HI_REG(4) MQVS_HI_REG(6) MQVS_HI_REG(8) MQVS_HI_REG(10) MQVS_HI_REG(12)
+        MQVS_HI_REG(14) MQVS_HI_REG(16) MQVS_HI_REG(18) MQVS_HI_REG(20) MQVS_HI_REG(22) MQVS_HI_REG(24)
+#undef MQVS_HI_REG
+        default: break;
+    }
+    fail(MQVS_ERR_DEVICE, "k_scan_hi_reg: no build for dpad " + std::to_string(p.dpad));
+}
+
+// dpad (d rounded to 64) of the register kernel's builds
+constexpr int kHiRegMaxDpad = 24 * HI_K;
+
+template <int METRIC, bool PROBE, int WQ, int QB, int NBUF>
+static void launch_hi_shape(ScanParams p, hipStream_t s) {
+    constexpr int QT = 32 * QB * WQ;
+    p.num_qblocks = (p.nq + QT - 1) / QT;
+    const int64_t L = p.tiles * p.num_qblocks;
+    if (L < 1) return;
+    const int64_t grid = (L + 7) / 8 * 8;
+    hipLaunchKernelGGL((k_scan_hi<METRIC, PROBE, WQ, QB, NBUF>), dim3((unsigned)grid), dim3(256 * WQ), 0, s, p);
+}
+
+// Tuning override (tools/tune_hi.py): MQVS_HI_TUNE="WQ,QB,NBUF"
+template <int METRIC, bool PROBE>
+static bool launch_hi_tuned(const ScanParams &p, hipStream_t s) {
+    const char *e = std::getenv("MQVS_HI_TUNE");
+    int wq, qb, nbuf;
+    if (!e || !*e || std::sscanf(e, "%d,%d,%d", &wq, &qb, &nbuf) != 3) return false;
+    switch ((wq * 10 + qb) * 10 + nbuf) {
+#define MQVS_HI_CASE(WQ_, QB_, NB_) \
+    case (WQ_ * 10 + QB_) * 10 + NB_: launch_hi_shape<METRIC, PROBE, WQ_, QB_, NB_>(p, s); return true;
+        MQVS_HI_CASE(2, 4, 2) MQVS_HI_CASE(2, 4, 3) MQVS_HI_CASE(2, 4, 4)
+        MQVS_HI_CASE(2, 2, 2) MQVS_HI_CASE(2, 2, 3) MQVS_HI_CASE(2, 2, 4)
+        MQVS_HI_CASE(1, 2, 2) MQVS_HI_CASE(1, 2, 3) MQVS_HI_CASE(1, 2, 4)
+#undef MQVS_HI_CASE
+        default: return false;
+    }
+}
+
+template <int METRIC, bool PROBE>
+static void launch_hi_t(const ScanParams &p, hipStream_t s) {
+    if constexpr (!PROBE)
+        if (launch_hi_tuned<METRIC, PROBE>(p, s)) return;
+    const char *reg = std::getenv("MQVS_HI_REG");  // A/B switch (tools/ab_split.py): 0 = LDS kernel only
+    const bool use_reg = !(reg && reg[0] == '0');
+    if (use_reg && p.nq <= 32 && p.dpad <= kHiRegMaxDpad) {
+        if (p.nq <= 16)
+            launch_hi_reg<METRIC, PROBE, 1>(p, s);
+        else
+            launch_hi_reg<METRIC, PROBE, 2>(p, s);
+        return;
+    }
+    if (p.nq <= 64)
+        launch_hi_shape<METRIC, PROBE, 1, 2, 3>(p, s);
+    else if (p.nq <= 128)
+        launch_hi_shape<METRIC, PROBE, 2, 2, 3>(p, s);
+    else
+        launch_hi_shape<METRIC, PROBE, 2, 4, 4>(p, s);
+}
+
+void launch_scan_hi(const ScanParams &p, int metric, bool probe, hipStream_t s) {
+    switch (metric) {
+        case MQVS_METRIC_L2:
+            probe ? launch_hi_t<MQVS_METRIC_L2, true>(p, s) : launch_hi_t<MQVS_METRIC_L2, false>(p, s);
+            break;
+        case MQVS_METRIC_IP:
+            probe ? launch_hi_t<MQVS_METRIC_IP, true>(p, s) : launch_hi_t<MQVS_METRIC_IP, false>(p, s);
+            break;
+        case MQVS_METRIC_COSINE:
+            probe ? launch_hi_t<MQVS_METRIC_COSINE, true>(p, s) : launch_hi_t<MQVS_METRIC_COSINE, false>(p, s);
+            break;
+        default:
+            probe ? launch_hi_t<kMetricIpRaw, true>(p, s) : launch_hi_t<kMetricIpRaw, false>(p, s);
+            break;
+    }
+}
+
+}  // namespace mqvs

@@ -26,7 +26,7 @@ namespace mqvs {
 static thread_local std::string g_error;
 static thread_local mqvs_search_stats g_stats{};
 static int g_timing = 0;
-static int g_prefilter = 6;  // planes built by new segments (mqvs_set_prefilter)
+static int g_prefilter = 2;  // planes built by new segments (mqvs_set_prefilter)
 
 void set_error(const std::string &msg) { g_error = msg; }
 
@@ -99,27 +99,31 @@ static void prepare_segment(mqvs_segment *s, const uint8_t *dev_nonempty_bytes,
     MQVS_HIP(hipMemsetAsync(s->ynorm_max, 0, 16 + sizeof(float) * kMxRec, st));
     launch_max_norm(s->norms, s->n, s->ynorm_max, st);
     const int64_t nr = std::max<int64_t>(s->n, 1);
-    const int64_t nr16 = (nr + 15) / 16 * 16;  // MX planes are blocked by 16 rows
-    const size_t hb = (size_t)(g_prefilter == kMxSplit ? nr16 : nr) * s->dpad * sizeof(uint16_t);
+    const int64_t nr16 = (nr + 15) / 16 * 16;  // row-blocked planes: blocks of 16 rows
+    const int split = g_prefilter;
+    const size_t hb = (size_t)(split == kBfSplit ? nr : nr16) * s->dpad * sizeof(uint16_t);
     const size_t xb = (size_t)nr16 * (s->dpad / 32) * 48;
     bool ok = hipMalloc((void **)&s->rows_hi, hb) == hipSuccess;
-    if (g_prefilter == kMxSplit) {
+    if (split == kMxSplit) {
         ok = ok && hipMalloc((void **)&s->rows_x6, xb) == hipSuccess &&
              hipMalloc((void **)&s->rows_sc, (size_t)nr * 2) == hipSuccess;
-    } else {
+    } else if (split == kBfSplit) {
         ok = ok && hipMalloc((void **)&s->rows_lo, hb) == hipSuccess;
     }
     if (ok) {
-        if (g_prefilter == kMxSplit) {
+        if (split == kHiSplit) {
+            s->bytes += hb;
+            launch_to_hi(s->rows, s->n, s->d, s->d, s->dpad, 1, nr16, s->rows_hi, nullptr, s->ynorm_max + 4, st);
+        } else if (split == kMxSplit) {
             s->bytes += hb + xb + (size_t)nr * 2;
             launch_to_mx(s->rows, s->n, s->d, s->d, s->dpad, 1, nr16, true, s->rows_hi, s->rows_x6, s->rows_sc,
                          nullptr, s->ynorm_max + 4, st);
-            s->split = kMxSplit;
         } else {
             s->bytes += 2 * hb;
             launch_to_bf16(s->rows, s->n, s->d, s->d, s->rows_hi, s->rows_lo, s->dpad, st);
-            s->split = kBfSplit;
         }
+        s->split = split;
+        s->plane_bytes = split == kHiSplit ? hb : split == kMxSplit ? hb + xb + (size_t)nr * 2 : 2 * hb;
     } else {
         (void)hipGetLastError();  // no room: exact fp32 batch path only
         for (void *q : {(void *)s->rows_hi, (void *)s->rows_lo, (void *)s->rows_x6, (void *)s->rows_sc})
@@ -225,7 +229,9 @@ static void run_scan(ScanParams p, const Range &r, int kind, int metric, bool pr
     p.tile_rows = kind == kScanSmall ? kSmallRows : kind == kScanBf16 ? kBfRows : kMfmaRows;
     if (kind == kScanMfma32)
         launch_scan_mfma(p, metric, probe, st);
-    else if (kind == kScanBf16 && p.rows_x6)
+    else if (kind == kScanBf16 && p.split == kHiSplit)
+        launch_scan_hi(p, metric, probe, st);
+    else if (kind == kScanBf16 && p.split == kMxSplit)
         launch_scan_mx(p, metric, probe, st);
     else if (kind == kScanBf16)
         launch_scan_bf16(p, metric, probe, kBfSplit, st);
@@ -327,7 +333,9 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     // below ~30% (tools/sweep.py --sels, profiles/r01)
     const bool mfma = nq >= kBlasThreshold;
     const bool bf16_ok = seg->approx_ok && !force_exact && g_batch_mode == 0;
-    bool bf16 = bf16_ok && nq >= kBf16MinNq;
+    // (split 2 streams half the bytes of the fp32 rows, so it serves every
+    // batch size; the older splits start at kBf16MinNq)
+    bool bf16 = bf16_ok && nq >= (seg->split == kHiSplit ? 1 : kBf16MinNq);
     bool gather = false;
     if (selected >= 0) {
         if (g_gather_mode == 2)
@@ -442,7 +450,20 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         p.rows_hi = seg->rows_hi;
         p.dpad = seg->dpad;
         p.thr = (const float *)ws.thr.get(sizeof(float) * nq);
-        if (seg->split == kMxSplit) {
+        p.split = seg->split;
+        if (seg->split == kHiSplit) {
+            // [hi: maxv x vpad x dpad x 2 B][records: nvec x kMxRec floats]
+            const int64_t vpad = round_up(nq, 16);
+            const int64_t pvec = (int64_t)maxv * vpad;
+            const size_t o_rec = (size_t)round_up(pvec * seg->dpad * 2, 256);
+            auto *base = (unsigned char *)ws.qhi.get(o_rec + sizeof(float) * kMxRec * (size_t)nvec);
+            auto *qhi = (uint16_t *)base;
+            auto *qrec = (float *)(base + o_rec);
+            launch_to_hi(qvars, nvec, d, qstride, seg->dpad, maxv, vpad, qhi, qrec, nullptr, s);
+            p.q_vpad = vpad;
+            p.q_hi = qhi;
+            launch_query_bound(p, metric, kHiSplit, seg->ynorm_max, qrec, seg->ynorm_max + 4, bq, s);
+        } else if (seg->split == kMxSplit) {
             // [hi: maxv x vpad x dpad x 2 B][fp6: maxv x vpad x dpad/32 x 48 B]
             // [scales: nvec x 2][records: nvec x kMxRec floats]
             const int64_t vpad = round_up(nq, 16);
@@ -541,7 +562,13 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     if (!async) {
         MQVS_HIP(hipMemcpyAsync(ws.host_flags, overflow, sizeof(int), hipMemcpyDeviceToHost, s));
         MQVS_HIP(hipMemcpyAsync(ws.host_flags + 1, status, sizeof(int), hipMemcpyDeviceToHost, s));
+        MQVS_HIP(hipMemcpyAsync(ws.host_flags + 4, overflow + 1, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
         MQVS_HIP(hipStreamSynchronize(s));
+        if (kind == kScanBf16) {
+            st.survivors_max = ws.host_flags[4];
+            st.survivors_total = (uint32_t)ws.host_flags[5];
+            st.candidates_max = ws.host_flags[6];
+        }
         // a query whose re-normalisation does not repeat within kMaxVariants
         // steps is exact only on the part's first kMaxVariants chunk ordinals
         if (ws.host_flags[1] && p.ord_base + (n + seg->granule - 1) / seg->granule > kMaxVariants)
@@ -1442,7 +1469,7 @@ int mqvs_set_batch_mode(int mode) {
 }
 
 int mqvs_set_prefilter(int split) {
-    if (split != kBfSplit && split != kMxSplit) return MQVS_ERR_BAD_ARGUMENTS;
+    if (split != kHiSplit && split != kBfSplit && split != kMxSplit) return MQVS_ERR_BAD_ARGUMENTS;
     g_prefilter = split;
     return MQVS_OK;
 }

@@ -23,10 +23,11 @@ struct mqvs_segment {
     uint16_t *rows_lo = nullptr;     // bf16 rounding of (row - hi), [n][dpad] (split 3)
     uint8_t *rows_x6 = nullptr;      // fp6 cross plane [n][dpad/32][48 B] (split 6)
     uint8_t *rows_sc = nullptr;      // E8M0 scales [n][2] (split 6)
-    float *ynorm_max = nullptr;      // device scalar: max_r |y_r|; split 6: + [kMxRec] norm maxima at +16 B
-    int split = 0;                   // pre-filter planes built: 3, 6, 0 = none
+    float *ynorm_max = nullptr;      // device scalar: max_r |y_r|; splits 2, 6: + [kMxRec] norm maxima at +16 B
+    int split = 0;                   // pre-filter planes built: 2, 3, 6, 0 = none
     int64_t dpad = 0;
     bool approx_ok = false;          // bf16 pre-filter usable for this segment
+    size_t plane_bytes = 0;          // HBM of the pre-filter planes (0: none built)
     uint8_t *nonempty_bits = nullptr;// null when every array is non-empty
     int *chunk_ord = nullptr;        // no-filter chunk ordinals (null = identity)
     // binary segments (FixedString(N) codes; rows == nullptr)
@@ -165,6 +166,7 @@ struct ScanParams {
     const uint8_t *q_sc;      // [nq][maxv][2]
     int64_t q_vpad;           // nq rounded up to 16 (MX query planes)
     int xcd_mode;             // MX scan workgroup -> XCD grouping (kernels_mx.hip)
+    int split;                // pre-filter planes of the scan: kHiSplit, kBfSplit, kMxSplit
     const float *thr;         // [nq] APPEND threshold on the approximate raw value
     // gather mode (selective PREWHERE): the scan walks positions of this list
     // of selected rows instead of rows; each chunk's rows are padded with -1 to
@@ -300,6 +302,7 @@ void launch_hamming_to_int(const int64_t *ids, float *dist, int64_t m, hipStream
 constexpr int kBfK = 64;    // bf16 planes padded to a multiple of this
 constexpr int kBfSplit = 3; // hi*hi + hi*lo + lo*hi (see kernels_bf16_scan.hip)
 constexpr int kMxSplit = 6; // bf16 hi*hi + fp6-MX (hi*res + res*hi) (kernels_mx.hip)
+constexpr int kHiSplit = 2; // bf16 hi*hi only, bound from measured residual norms (kernels_hi.hip)
 constexpr int kMxRec = 8;   // floats per vector in the MX norm records (kernels_mx.hip)
 // dst_hi = bf16_rn(x); dst_lo (optional) = bf16_rn(x - hi)
 void launch_to_bf16(const float *src, int64_t rows, int d, int64_t src_stride, uint16_t *dst_hi,
@@ -319,6 +322,11 @@ void launch_to_mx(const float *src, int64_t rows, int d, int64_t src_stride, int
                   int64_t vpad, bool res_first, uint16_t *hi, uint8_t *x6, uint8_t *sc, float *rec, float *maxrec,
                   hipStream_t s);
 void launch_scan_mx(const ScanParams &p, int metric, bool probe, hipStream_t s);
+// split 2 (kernels_hi.hip): row-blocked bf16 hi plane as the MX one + records
+// [|h|, |r|, -, -, -, -, |x|] per vector (rec) / maxima (maxrec, atomic)
+void launch_to_hi(const float *src, int64_t rows, int d, int64_t src_stride, int64_t dpad, int64_t vgroup,
+                  int64_t vpad, uint16_t *hi, float *rec, float *maxrec, hipStream_t s);
+void launch_scan_hi(const ScanParams &p, int metric, bool probe, hipStream_t s);
 void launch_probe_select_approx(const float *probe, int64_t P, int64_t ld, int nq, int k,
                                 int metric, const float *bq, float *thr, int *cand_count,
                                 Cand *cand, int cand_cap, const int32_t *row_list, hipStream_t s);
