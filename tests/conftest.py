@@ -11,3 +11,4 @@ if TESTS not in sys.path:
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through libmqvs.so)")
+    config.addinivalue_line("markers", "fullsize: a BASELINE.json configuration at its full size (GPU, ~10-60 s)")

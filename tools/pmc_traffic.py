@@ -29,7 +29,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("root", help="directory holding pmc1/ pmc2/ pmc3/ (gpurun_out)")
     ap.add_argument("--searches", type=int, required=True)
-    ap.add_argument("--kernel", default="k_scan_(?:bf16|mx)")
+    ap.add_argument("--nq", type=int, default=None, help="batch size of the profiled searches")
+    ap.add_argument("--kernel", default="k_scan_(?:bf16|mx|hi)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -49,7 +50,7 @@ def main():
             dur[(key, tag)][r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     out = {"source": "rocprofv3 --pmc (separate passes: SQ/GRBM, FETCH_SIZE, WRITE_SIZE+TCC)",
            "fetch_correction": "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950)",
-           "searches": args.searches, "kernels": {}}
+           "searches": args.searches, "nq": args.nq, "kernels": {}}
     for key, c in agg.items():
         k = {}
         launches = max(len(v) for v in disp[key].values())
