@@ -107,6 +107,29 @@ __device__ inline void wait_barrier() {
     asm volatile("s_waitcnt vmcnt(%0)\n\ts_barrier" ::"n"(N) : "memory");
 }
 
+// raw s_barrier, no memory-op or MFMA movement across it
+__device__ inline void raw_barrier() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// s_waitcnt vmcnt(pend * P), pend in [0, DMAX - 1] (a runtime count: the tail
+// of a loop issues fewer stages)
+template <int P, int DMAX>
+__device__ inline void wait_vm(int pend) {
+    __builtin_amdgcn_sched_barrier(0);
+    if (DMAX >= 4 && pend >= 3)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P * 3) : "memory");
+    else if (DMAX >= 3 && pend >= 2)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P * 2) : "memory");
+    else if (DMAX >= 2 && pend >= 1)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P * 1) : "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
 template <int GPW, int NBUF>
 __device__ inline void wait_stage(int pending) {
     // pending: stages issued after the one about to be consumed (0 .. NBUF-2)
@@ -124,7 +147,22 @@ __device__ inline void wait_stage(int pending) {
 // rows x 32 QB queries, 32x32x16 bf16 MFMA blocks; workgroup -> (row tile,
 // query block) with the query blocks of a row tile on one XCD (its L2 serves
 // the tile's re-reads).
-template <int METRIC, bool PROBE, int WQ, int QB, int NBUF>
+//
+// PP (ping-pong): the two waves of a SIMD (waves w and w + 4: the query halves
+// wq = 0 / 1) run one barrier apart, so that while one computes its 16 MFMAs of
+// a stage the other reads its fragments of the next stage from LDS and issues
+// its LDS-DMA pieces; the MFMA pipe then never waits for a wave's own reads /
+// DMA issue (the lock-step loop leaves it idle during both: 18 ms compute-only
+// against 6.6 ms of MFMA cycles at 10M x 768, nq 1000).  Every barrier is a
+// raw s_barrier; a stage is ready for reading after a barrier that every
+// issuing wave reached past a counted vmcnt covering its pieces; a buffer is
+// re-issued only after the barrier that follows the last MFMA phase reading
+// it.  Stages are issued D = NBUF - 2 ahead.
+// DIAG (diagnostic builds, wrong results): 1 = row pieces read from the first
+// 8 tiles only (an L2-resident row stream), 2 = query pieces from query
+// group 0 only, 4 = query pieces not issued, 8 = row pieces not issued (the
+// stage then holds stale bytes; the waits count only the issued pieces).
+template <int METRIC, bool PROBE, int WQ, int QB, int NBUF, int PP = 0, int DIAG = 0>
 __global__ __launch_bounds__(256 * WQ) void k_scan_hi(ScanParams p) {
     constexpr int WR = 4;
     constexpr int NW = WR * WQ;
@@ -181,21 +219,28 @@ __global__ __launch_bounds__(256 * WQ) void k_scan_hi(ScanParams p) {
             const int64_t gp = r0 + r;
             u = gp < r1 ? row_at(p, gp) : -1;
             if (u < 0) u = row_at(p, r0);  // padding: any real row, results discarded
+            if (DIAG & 1) u = (ti & 7) * RT + r;
             plane = p.rows_hi;
         } else {
             int j = q0 + r;
             if (j >= p.nq) j = 0;
+            if (DIAG & 2) j = r & 15;
             u = (int64_t)variant_of(p, j, ord) * p.q_vpad + j;
             plane = p.q_hi;
         }
         src[i] = reinterpret_cast<const unsigned char *>(plane) + ((u >> 4) * nb * 1024 + (u & 15) * 64 + c * 16);
     }
+    static_assert(GY % NW == 0, "row pieces: whole rounds of the waves");
+    constexpr int YPW = GY / NW;  // pieces i < YPW are row pieces, the rest query pieces
     auto issue = [&](int s) {
         unsigned char *dst = lds + (s % NBUF) * STAGE;
 #pragma unroll
-        for (int i = 0; i < GPW; ++i)
+        for (int i = 0; i < GPW; ++i) {
+            if ((DIAG & 8) && i < YPW) continue;
+            if ((DIAG & 4) && i >= YPW) continue;
             __builtin_amdgcn_global_load_lds((const void *)(src[i] + (int64_t)s * 1024),
                                              (lds_void *)(dst + (w + i * NW) * 1024), 16, 0, 0);
+        }
     };
 
     constexpr int OFF_Q = GY * 1024;
@@ -213,39 +258,88 @@ __global__ __launch_bounds__(256 * WQ) void k_scan_hi(ScanParams p) {
         for (int jb = 0; jb < QB; ++jb) acc[i][jb] = f32x16{0};
 
     const int nst = (int)(p.dpad / HI_K);
-    // prologue: stages 0 .. NBUF-2 in flight
+    constexpr int NPW = GPW - ((DIAG & 8) ? YPW : 0) - ((DIAG & 4) ? GPW - YPW : 0);  // pieces per wave, stage
+    if constexpr (PP) {
+        static_assert(WQ == 2 && NBUF >= 3, "ping-pong: two query halves, stages issued NBUF - 2 ahead");
+        constexpr int D = NBUF - 2;
+        const int grp = wq;  // waves w and w + 4 share a SIMD
+        auto stage_frags = [&](int s, bf16x8 (&ah)[2][2], bf16x8 (&bh)[2][QB]) {
+            const unsigned char *st = lds + (s % NBUF) * STAGE;
 #pragma unroll
-    for (int s = 0; s < NBUF - 1; ++s)
-        if (s < nst) issue(s);
-    for (int s = 0; s < nst; ++s) {
-        const int after = nst - 1 - s;  // stages after s
-        wait_stage<GPW, NBUF>(after < NBUF - 2 ? after : NBUF - 2);
-        // every wave is past its reads of stage s-1: its buffer takes stage s+NBUF-1
-        if (s + NBUF - 1 < nst) {
-            __builtin_amdgcn_sched_barrier(0);
-            issue(s + NBUF - 1);
-            __builtin_amdgcn_sched_barrier(0);
+            for (int kk = 0; kk < 2; ++kk) {
+                const int c = 2 * kk + h;
+#pragma unroll
+                for (int i = 0; i < 2; ++i) ah[kk][i] = frag(st, ra0 + 32 * i, c);
+#pragma unroll
+                for (int jb = 0; jb < QB; ++jb) bh[kk][jb] = frag(st + OFF_Q, rq0 + 32 * jb, c);
+            }
+        };
+        // prologue: stages 0 .. D-1 issued, stage 0 landed for everyone
+#pragma unroll
+        for (int s = 0; s < D; ++s)
+            if (s < nst) issue(s);
+        wait_vm<NPW, D>(nst - 1 < D - 1 ? nst - 1 : D - 1);
+        raw_barrier();
+        if (grp == 1) raw_barrier();
+        for (int s = 0; s < nst; ++s) {
+            bf16x8 ah[2][2], bh[2][QB];
+            // read phase (the partner wave computes meanwhile)
+            stage_frags(s, ah, bh);
+            if (s + D < nst) issue(s + D);
+            // pieces younger than stage s+1's, which the barrier after the
+            // partner's next read phase must find landed
+            const int pend = (nst - 2 - s) < D - 1 ? (nst - 2 - s) : D - 1;
+            if (grp == 1 && s + 1 < nst) wait_vm<NPW, D>(pend);
+            raw_barrier();
+            // MFMA phase (the partner reads meanwhile)
+            __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int jb = 0; jb < QB; ++jb)
+                        acc[i][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[kk][i], bh[kk][jb], acc[i][jb], 0, 0,
+                                                                             0);
+            __builtin_amdgcn_s_setprio(0);
+            if (grp == 0 && s + 1 < nst) wait_vm<NPW, D>(pend);
+            raw_barrier();
         }
-        const unsigned char *st = lds + (s % NBUF) * STAGE;
-        __builtin_amdgcn_s_setprio(1);
+        if (grp == 0) raw_barrier();
+    } else {
 #pragma unroll
-        for (int kk = 0; kk < 2; ++kk) {
-            const int c = 2 * kk + h;
-            bf16x8 ah[2], bh[QB];
+        for (int s = 0; s < NBUF - 1; ++s)
+            if (s < nst) issue(s);
+        for (int s = 0; s < nst; ++s) {
+            const int after = nst - 1 - s;  // stages after s
+            wait_stage<NPW, NBUF>(after < NBUF - 2 ? after : NBUF - 2);
+            // every wave is past its reads of stage s-1: its buffer takes stage s+NBUF-1
+            if (s + NBUF - 1 < nst) {
+                __builtin_amdgcn_sched_barrier(0);
+                issue(s + NBUF - 1);
+                __builtin_amdgcn_sched_barrier(0);
+            }
+            const unsigned char *st = lds + (s % NBUF) * STAGE;
+            __builtin_amdgcn_s_setprio(1);
 #pragma unroll
-            for (int i = 0; i < 2; ++i) ah[i] = frag(st, ra0 + 32 * i, c);
+            for (int kk = 0; kk < 2; ++kk) {
+                const int c = 2 * kk + h;
+                bf16x8 ah[2], bh[QB];
 #pragma unroll
-            for (int jb = 0; jb < QB; ++jb) bh[jb] = frag(st + OFF_Q, rq0 + 32 * jb, c);
+                for (int i = 0; i < 2; ++i) ah[i] = frag(st, ra0 + 32 * i, c);
 #pragma unroll
-            for (int i = 0; i < 2; ++i)
+                for (int jb = 0; jb < QB; ++jb) bh[jb] = frag(st + OFF_Q, rq0 + 32 * jb, c);
 #pragma unroll
-                for (int jb = 0; jb < QB; ++jb)
-                    acc[i][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[jb], acc[i][jb], 0, 0, 0);
+                for (int i = 0; i < 2; ++i)
+#pragma unroll
+                    for (int jb = 0; jb < QB; ++jb)
+                        acc[i][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[jb], acc[i][jb], 0, 0, 0);
+            }
+            __builtin_amdgcn_s_setprio(0);
+            // (the next iteration's barrier orders these reads before the buffer
+            // is re-issued: the MFMAs consumed every fragment, so the reads retired)
+            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         }
-        __builtin_amdgcn_s_setprio(0);
-        // (the next iteration's barrier orders these reads before the buffer
-        // is re-issued: the MFMAs consumed every fragment, so the reads retired)
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
 #pragma unroll
     for (int rb = 0; rb < 2; ++rb)
@@ -258,6 +352,322 @@ __global__ __launch_bounds__(256 * WQ) void k_scan_hi(ScanParams p) {
                 p, j, r1, [&](int r) { return rbase + (r & 3) + 8 * (r >> 2); },
                 [&](int r) { return acc[rb][jb][r]; });
         }
+}
+
+// ---------------------------------------------------------------------------
+// Persistent ping-pong scan (batch APPEND, Cosine / IP, contiguous rows).
+//
+// Measured on k_scan_hi (10M rows, nq 1000, d 256 .. 1536): main-scan time
+// = ~6 ms + ~5 ms per 256 dimensions, i.e. every workgroup pays ~10 us outside
+// its K loop (a cold prologue that waits for its first stages, the epilogue,
+// the launch), a third of the search at d = 768.  Here one workgroup per CU
+// walks a sequence of (row tile, query block) items, and the LDS-DMA stage
+// ring runs ACROSS items: the next item's first stages are in flight while
+// the current item's last stages and epilogue run.  The two waves of each
+// SIMD (query halves wq = 0 / 1) run one barrier apart (read phase of one
+// against MFMA phase of the other, see k_scan_hi's PP notes).
+//
+// Epilogue without global memory: values over the query's threshold go to an
+// LDS queue (ds atomics only), flushed to the candidate lists once at the end
+// of the launch -- a global atomic's returned slot would make the wave wait
+// for every LDS-DMA piece issued before it.  Thresholds and the cosine
+// variant cycle of the workgroup's queries are loaded once (a workgroup keeps
+// one query block).  A full queue falls back to the global append.
+//
+// Items: XCD x = blockIdx % 8 holds the tiles t = x (mod 8); its S slots split
+// into S / nqb groups of nqb query blocks, group g taking tiles
+// x + 8 (g + (S / nqb) i): the query blocks of a tile run together on one XCD
+// and share its rows through that L2.
+constexpr int kPpQueue = 1984;  // LDS candidate queue entries (16 B)
+
+struct PpEntry {
+    float raw;
+    uint32_t row;
+    int j;
+    int pad;
+};
+
+// LDS queue append by inline asm: a compiler-visible LDS access here would
+// get a wait for every LDS-DMA piece in flight (the waitcnt pass cannot tell
+// that the queue and the stage ring do not overlap)
+__device__ inline int lds_add_rtn(const void *addr, int v) {
+    int r;
+    const unsigned a = (unsigned)(size_t)(lds_void *)addr;
+    asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(a), "v"(v) : "memory");
+    return r;
+}
+__device__ inline void lds_store_b128(const void *addr, float x, uint32_t y, int z) {
+    const unsigned a = (unsigned)(size_t)(lds_void *)addr;
+    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+    const u32x4 v = {__builtin_bit_cast(unsigned, x), y, (unsigned)z, 0u};
+    asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
+}
+
+// DIAG (diagnostic builds, wrong results; MQVS_HI_PPDIAG): 1 = row pieces
+// from the first 8 tiles only (L2-resident rows), 4 = query pieces not
+// issued, 8 = row pieces not issued, 16 = a trivial epilogue (the MFMAs stay
+// live: one compare of an accumulator sum per item).
+template <int METRIC, int NBUF, int DIAG = 0>
+__global__ __launch_bounds__(512) void k_scan_hi_pp(ScanParams p, int slots) {
+    constexpr int WR = 4, WQ = 2, QB = 4, NW = 8;
+    constexpr int QT = 32 * QB * WQ;  // 256
+    constexpr int RT = kBfRows;       // 256
+    constexpr int GY = RT / 16, GQ = QT / 16, G = GY + GQ;
+    constexpr int GPW = G / NW;       // 4 pieces per wave and stage
+    constexpr int YPW = GY / NW;      // 2 of them row pieces
+    constexpr int STAGE = G * 1024;
+    constexpr int D = NBUF - 2;       // stages in flight ahead of the one read
+    static_assert(D >= 1 && GY % NW == 0, "shape");
+    constexpr int NPW = GPW - ((DIAG & 8) ? YPW : 0) - ((DIAG & 4) ? GPW - YPW : 0);  // pieces per wave, stage
+    // ONE __shared__ object: the stage ring, the candidate queue and its
+    // counter (an LDS access to a second object after an LDS-DMA makes the
+    // compiler wait for every DMA in flight, cdna_hip_programming.md)
+    __shared__ __attribute__((aligned(16))) unsigned char lds[NBUF * STAGE + kPpQueue * 16 + 16];
+    PpEntry *queue = reinterpret_cast<PpEntry *>(lds + NBUF * STAGE);
+    int &qcount = *reinterpret_cast<int *>(lds + NBUF * STAGE + kPpQueue * 16);
+
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wr = w % WR, wq = w / WR;
+    const int grp = wq;  // waves w and w + 4 share a SIMD
+    const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
+    const int nqb = p.num_qblocks;
+    const int ngroups = slots / nqb;
+    if (slot >= ngroups * nqb) return;  // whole workgroup, before any barrier
+    const int qb = slot % nqb, tg = slot / nqb;
+    const int q0 = qb * QT;
+    const int64_t tstride = 8 * (int64_t)ngroups;
+    const int nb = (int)(p.dpad / HI_K);
+    const int nst = nb;
+    if (t == 0) qcount = 0;
+
+    // per-lane constants: the two query rows of this wave's Q pieces (their
+    // variant cycle), the four query columns of its accumulators (thresholds)
+    int qj[2], qmu[2] = {0, 0}, qlam[2] = {1, 1};
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+        int j = q0 + (w + i * NW) * 16 + (lane >> 2);
+        if (j >= p.nq) j = 0;
+        qj[i] = j;
+        if (p.maxv > 1) {
+            qmu[i] = p.qmu[j];
+            qlam[i] = p.qlam[j];
+        }
+        asm volatile("" : "+v"(qmu[i]), "+v"(qlam[i]));  // (the loads' waits land here, before the ring)
+    }
+    const int h = lane >> 5, l32 = lane & 31;
+    const int ra0 = wr * 64 + l32;
+    const int rq0 = wq * 32 * QB + l32;
+    float thr[QB];
+#pragma unroll
+    for (int jb = 0; jb < QB; ++jb) {
+        const int j = q0 + rq0 + jb * 32;
+        thr[jb] = j < p.nq ? p.thr[j] : __builtin_inff();  // (never taken)
+        asm volatile("" : "+v"(thr[jb]));
+    }
+
+    // item cursor helpers (items are tiles of this slot's sequence)
+    auto item_range = [&](int64_t ti, int64_t &r0, int64_t &r1, int &ord) -> bool {
+        int64_t chunk;
+        tile_range(p, ti, r0, r1, chunk);
+        ord = (int)chunk + p.ord_base;  // (no chunk_ord table on this path)
+        return r0 < r1;
+    };
+    auto next_item = [&](int64_t ti, int64_t &r0, int64_t &r1, int &ord) -> int64_t {
+        for (; ti < p.tiles; ti += tstride)
+            if (item_range(ti, r0, r1, ord)) return ti;
+        return -1;
+    };
+
+    // issue cursor: item ti_i (rows [ir0, ir1), ordinal iord), next stage si
+    int64_t ir0 = 0, ir1 = 0;
+    int iord = 0;
+    int64_t ti_i = next_item(xcd + 8 * (int64_t)tg, ir0, ir1, iord);
+    if (ti_i < 0) return;  // no work (uniform)
+    const unsigned char *src[GPW];
+    auto set_src = [&]() {
+#pragma unroll
+        for (int i = 0; i < GPW; ++i) {
+            const int g = w + i * NW;
+            const int r = (i < YPW ? g : g - GY) * 16 + (lane >> 2);
+            const int c = hswz(r, lane & 3);
+            int64_t u;
+            const uint16_t *plane;
+            if (i < YPW) {
+                u = ir0 + r < ir1 ? ir0 + r : ir0;  // padding rows: any real row, discarded
+                if (DIAG & 1) u = ((ir0 / RT) & 7) * RT + r;
+                plane = p.rows_hi;
+            } else {
+                const int k = i - YPW;
+                const int var = p.maxv <= 1 ? 0 : (iord < qmu[k] ? iord : qmu[k] + (iord - qmu[k]) % qlam[k]);
+                u = (int64_t)var * p.q_vpad + qj[k];
+                plane = p.q_hi;
+            }
+            src[i] = reinterpret_cast<const unsigned char *>(plane) + ((u >> 4) * nb * 1024 + (u & 15) * 64 + c * 16);
+        }
+    };
+    set_src();
+    int si = 0;
+    int64_t issued = 0;  // stages issued so far (global stage counter)
+    auto issue_next = [&]() {
+        if (ti_i < 0) return;
+        unsigned char *dst = lds + (int)(issued % NBUF) * STAGE;
+#pragma unroll
+        for (int i = 0; i < GPW; ++i) {
+            if ((DIAG & 8) && i < YPW) continue;
+            if ((DIAG & 4) && i >= YPW) continue;
+            __builtin_amdgcn_global_load_lds((const void *)(src[i] + (int64_t)si * 1024),
+                                             (lds_void *)(dst + (w + i * NW) * 1024), 16, 0, 0);
+        }
+        ++issued;
+        if (++si == nst) {
+            si = 0;
+            ti_i = next_item(ti_i + tstride, ir0, ir1, iord);
+            if (ti_i >= 0) set_src();
+        }
+    };
+
+    // compute cursor: item rows [cr0, cr1), stage sc, global stage gc
+    int64_t cr0 = ir0, cr1 = ir1;
+    int64_t ti_c = ti_i;
+    int sc = 0;
+    int64_t gc = 0;
+
+    constexpr int OFF_Q = GY * 1024;
+    auto frag = [&](const unsigned char *st, int r, int c) {
+        return *reinterpret_cast<const bf16x8 *>(st + r * 64 + hswz(r, c) * 16);
+    };
+    f32x16 acc[2][QB];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int jb = 0; jb < QB; ++jb) acc[i][jb] = f32x16{0};
+
+    // prologue: D stages in flight, the first landed for everyone
+    for (int s = 0; s < D; ++s) issue_next();
+    {
+        const int64_t pend = issued - 1 < D - 1 ? issued - 1 : D - 1;
+        wait_vm<NPW, D>((int)pend);
+    }
+    __syncthreads();  // (qcount = 0 visible; no DMA wait hidden in it: all waited above)
+    if (grp == 1) raw_barrier();
+    while (true) {
+        // read phase (the partner wave computes meanwhile): the first half
+        // (16 columns) of the stage's fragments; the second half is read
+        // inside the MFMA phase, after the first half's MFMAs have issued
+        // (keeps the fragments at 24 VGPRs: acc takes 128)
+        const unsigned char *st = lds + (int)(gc % NBUF) * STAGE;
+        bf16x8 ah[2], bh[QB];
+#pragma unroll
+        for (int i = 0; i < 2; ++i) ah[i] = frag(st, ra0 + 32 * i, h);
+#pragma unroll
+        for (int jb = 0; jb < QB; ++jb) bh[jb] = frag(st + OFF_Q, rq0 + 32 * jb, h);
+        __builtin_amdgcn_sched_barrier(0);
+        issue_next();
+        const bool has_next = gc + 1 < issued;
+        // pieces issued after stage gc+1 may stay in flight
+        const int pend = has_next ? (int)(issued - gc - 2) : 0;
+        if (grp == 1 && has_next) wait_vm<NPW, D>(pend);
+        raw_barrier();
+        __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int jb = 0; jb < QB; ++jb)
+                acc[i][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[jb], acc[i][jb], 0, 0, 0);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < 2; ++i) ah[i] = frag(st, ra0 + 32 * i, 2 + h);
+#pragma unroll
+        for (int jb = 0; jb < QB; ++jb) bh[jb] = frag(st + OFF_Q, rq0 + 32 * jb, 2 + h);
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+            for (int jb = 0; jb < QB; ++jb)
+                acc[i][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[jb], acc[i][jb], 0, 0, 0);
+        __builtin_amdgcn_s_setprio(0);
+        if (++sc == nst) {
+            // item epilogue: values over the threshold -> LDS queue
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb)
+                if (!(DIAG & 16))
+#pragma unroll
+                for (int jb = 0; jb < QB; ++jb) {
+                    const int j = q0 + rq0 + jb * 32;
+                    const int64_t rbase = cr0 + wr * 64 + rb * 32 + 4 * h;
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) {
+                        const float raw = acc[rb][jb][r];
+                        const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
+                        if (raw >= thr[jb] && row < cr1 && j < p.nq) {
+                            const int pos = lds_add_rtn(&qcount, 1);
+                            if (pos < kPpQueue) {
+                                lds_store_b128(queue + pos, raw, (uint32_t)row, j);
+                            } else {
+                                emit_approx<METRIC, false>(p, j, row, row, row_valid(p, row), raw);
+                            }
+                        }
+                    }
+                }
+            if (DIAG & 16) {
+                float sum = 0.f;
+#pragma unroll
+                for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+                    for (int jb = 0; jb < QB; ++jb)
+#pragma unroll
+                        for (int r = 0; r < 16; ++r) sum += acc[rb][jb][r];
+                if (sum == -1.2345e-30f) lds_add_rtn(&qcount, 1);
+            }
+#pragma unroll
+            for (int rb = 0; rb < 2; ++rb)
+#pragma unroll
+                for (int jb = 0; jb < QB; ++jb) acc[rb][jb] = f32x16{0};
+            sc = 0;
+            int cord;
+            ti_c = next_item(ti_c + tstride, cr0, cr1, cord);
+        }
+        ++gc;
+        if (grp == 0 && has_next) wait_vm<NPW, D>(pend);
+        raw_barrier();
+        if (!has_next) break;
+    }
+    if (grp == 0) raw_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (asm queue stores retired)
+    __syncthreads();
+    const int nqueue = qcount < kPpQueue ? qcount : kPpQueue;
+    for (int e = t; e < nqueue; e += 512) {
+        const PpEntry en = queue[e];
+        emit_approx<METRIC, false>(p, en.j, en.row, en.row, row_valid(p, en.row), en.raw);
+    }
+}
+
+template <int METRIC>
+static bool launch_hi_pp(ScanParams p, hipStream_t s) {
+    constexpr int QT = 256;
+    p.num_qblocks = (p.nq + QT - 1) / QT;
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        MQVS_HIP(hipGetDevice(&dev));
+        MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    const int per_xcd = cus / 8;
+    if (p.num_qblocks > per_xcd || p.tiles < 1) return false;
+    const int slots = per_xcd / p.num_qblocks * p.num_qblocks;
+    const char *dg = std::getenv("MQVS_HI_PPDIAG");
+    const int diag = dg ? std::atoi(dg) : 0;
+#define MQVS_PP(DG_) \
+    hipLaunchKernelGGL((k_scan_hi_pp<METRIC, 4, DG_>), dim3((unsigned)(8 * per_xcd)), dim3(512), 0, s, p, slots)
+    switch (diag) {
+        case 16: MQVS_PP(16); break;
+        case 17: MQVS_PP(17); break;
+        case 20: MQVS_PP(20); break;
+        case 24: MQVS_PP(24); break;
+        case 28: MQVS_PP(28); break;
+        default: MQVS_PP(0); break;
+    }
+#undef MQVS_PP
+    return true;
 }
 
 // Small batches (nq <= 32): HBM-bound, so no LDS staging at all.  The 256-row
@@ -361,28 +771,33 @@ static void launch_hi_reg(ScanParams p, hipStream_t s) {
 // dpad (d rounded to 64) of the register kernel's builds
 constexpr int kHiRegMaxDpad = 24 * HI_K;
 
-template <int METRIC, bool PROBE, int WQ, int QB, int NBUF>
+template <int METRIC, bool PROBE, int WQ, int QB, int NBUF, int PP = 0, int DIAG = 0>
 static void launch_hi_shape(ScanParams p, hipStream_t s) {
     constexpr int QT = 32 * QB * WQ;
     p.num_qblocks = (p.nq + QT - 1) / QT;
     const int64_t L = p.tiles * p.num_qblocks;
     if (L < 1) return;
     const int64_t grid = (L + 7) / 8 * 8;
-    hipLaunchKernelGGL((k_scan_hi<METRIC, PROBE, WQ, QB, NBUF>), dim3((unsigned)grid), dim3(256 * WQ), 0, s, p);
+    hipLaunchKernelGGL((k_scan_hi<METRIC, PROBE, WQ, QB, NBUF, PP, DIAG>), dim3((unsigned)grid), dim3(256 * WQ), 0, s,
+                       p);
 }
 
-// Tuning override (tools/tune_hi.py): MQVS_HI_TUNE="WQ,QB,NBUF"
+// Tuning override (tools/ab_split.py --tunes): MQVS_HI_TUNE="WQ,QB,NBUF[,PP[,DIAG]]"
 template <int METRIC, bool PROBE>
 static bool launch_hi_tuned(const ScanParams &p, hipStream_t s) {
     const char *e = std::getenv("MQVS_HI_TUNE");
-    int wq, qb, nbuf;
-    if (!e || !*e || std::sscanf(e, "%d,%d,%d", &wq, &qb, &nbuf) != 3) return false;
-    switch ((wq * 10 + qb) * 10 + nbuf) {
-#define MQVS_HI_CASE(WQ_, QB_, NB_) \
-    case (WQ_ * 10 + QB_) * 10 + NB_: launch_hi_shape<METRIC, PROBE, WQ_, QB_, NB_>(p, s); return true;
-        MQVS_HI_CASE(2, 4, 2) MQVS_HI_CASE(2, 4, 3) MQVS_HI_CASE(2, 4, 4)
-        MQVS_HI_CASE(2, 2, 2) MQVS_HI_CASE(2, 2, 3) MQVS_HI_CASE(2, 2, 4)
-        MQVS_HI_CASE(1, 2, 2) MQVS_HI_CASE(1, 2, 3) MQVS_HI_CASE(1, 2, 4)
+    int wq, qb, nbuf, pp = 0, diag = 0;
+    if (!e || !*e || std::sscanf(e, "%d,%d,%d,%d,%d", &wq, &qb, &nbuf, &pp, &diag) < 3) return false;
+    switch ((((wq * 10 + qb) * 10 + nbuf) * 100 + pp) * 100 + diag) {
+#define MQVS_HI_CASE(WQ_, QB_, NB_, PP_, DG_)                                         \
+    case (((WQ_ * 10 + QB_) * 10 + NB_) * 100 + PP_) * 100 + DG_:                     \
+        launch_hi_shape<METRIC, PROBE, WQ_, QB_, NB_, PP_, DG_>(p, s);                \
+        return true;
+        MQVS_HI_CASE(2, 4, 3, 0, 0) MQVS_HI_CASE(2, 4, 4, 0, 0)
+        MQVS_HI_CASE(2, 4, 4, 0, 2) MQVS_HI_CASE(2, 4, 4, 0, 12)
+        MQVS_HI_CASE(2, 4, 4, 1, 0) MQVS_HI_CASE(2, 4, 3, 1, 0) MQVS_HI_CASE(2, 4, 4, 1, 12)
+        MQVS_HI_CASE(2, 2, 3, 0, 0) MQVS_HI_CASE(2, 2, 4, 1, 0) MQVS_HI_CASE(2, 2, 3, 1, 0)
+        MQVS_HI_CASE(1, 2, 3, 0, 0)
 #undef MQVS_HI_CASE
         default: return false;
     }
@@ -392,6 +807,12 @@ template <int METRIC, bool PROBE>
 static void launch_hi_t(const ScanParams &p, hipStream_t s) {
     if constexpr (!PROBE)
         if (launch_hi_tuned<METRIC, PROBE>(p, s)) return;
+    if constexpr (!PROBE && METRIC != MQVS_METRIC_L2) {
+        // persistent ping-pong kernel: batches served by the 256 x 256 shape,
+        // contiguous rows, identity chunk ordinals (A/B switch MQVS_HI_PP=0)
+        const char *pp = std::getenv("MQVS_HI_PP");
+        if (!(pp && pp[0] == '0') && p.nq > 128 && !p.row_list && !p.chunk_ord && launch_hi_pp<METRIC>(p, s)) return;
+    }
     const char *reg = std::getenv("MQVS_HI_REG");  // A/B switch (tools/ab_split.py): 0 = LDS kernel only
     const bool use_reg = !(reg && reg[0] == '0');
     if (use_reg && p.nq <= 32 && p.dpad <= kHiRegMaxDpad) {
