@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define MQVS_ABI_VERSION 2
+#define MQVS_ABI_VERSION 3
 
 /* Metric ids (VICommon.h VIMetric).  L2 / IP / Cosine: Float32 vectors;
  * Hamming / Jaccard: binary vectors (FixedString(N) columns, mqvs_*_binary). */
@@ -68,9 +68,20 @@ enum {
 #define MQVS_F_DEVICE_PTRS 0x1u /* queries, bitmaps, candidates and outputs are
                                    device pointers on the segment's GPU */
 #define MQVS_F_ASYNC 0x2u       /* with DEVICE_PTRS: do not synchronise the
-                                   stream before returning (results valid after
-                                   the stream drains); the candidate-overflow
-                                   fallback then reports MQVS_ERR_LOGICAL */
+                                   stream before returning.  The results are
+                                   valid once the stream drains AND
+                                   mqvs_async_check returns MQVS_OK: a search
+                                   that would have needed a host-driven
+                                   fallback (candidate overflow, cosine variant
+                                   check) is reported there as
+                                   MQVS_ERR_LOGICAL and must be repeated
+                                   without ASYNC */
+/* Per-call path selection (override the process-wide mqvs_set_* defaults for
+ * this call only; all paths return the same bits): */
+#define MQVS_F_EXACT 0x20u         /* exact fp32 scan of every row (no bf16 pre-filter) */
+#define MQVS_F_GATHER_NEVER 0x40u  /* PREWHERE: scan every row and mask */
+#define MQVS_F_GATHER_ALWAYS 0x80u /* PREWHERE: always walk a gather list of the selected rows */
+#define MQVS_F_TIMING 0x100u       /* per-launch HIP-event timing in mqvs_last_search_stats */
 
 typedef struct mqvs_segment *mqvs_segment_t;
 typedef void *mqvs_stream_t; /* a hipStream_t, or NULL for the caller thread's stream */
@@ -82,6 +93,12 @@ int mqvs_init(int device);
 int mqvs_device_count(int *count);
 /* Thread-local message of the last failing call on this thread. */
 const char *mqvs_last_error(void);
+/* Outcome of this thread's MQVS_F_ASYNC calls on the current device since the
+ * last check: synchronises `stream` (NULL: the thread's own stream), then
+ * returns MQVS_OK, or MQVS_ERR_LOGICAL when one of them needed a host-driven
+ * fallback (its results are then invalid: repeat it synchronously).  Clears
+ * the record.  Callers that used several streams synchronise them first. */
+int mqvs_async_check(mqvs_stream_t stream);
 /* Release this thread's stream/workspace (optional; freed at thread exit). */
 int mqvs_thread_release(void);
 
@@ -121,7 +138,10 @@ int mqvs_segment_rows(mqvs_segment_t seg, const float **dev_rows);
  * queries: nq*d fp32 (original, un-normalised).
  * filter: PREWHERE bitmap, LSB-first, n bits, or NULL (no PREWHERE).
  * row_exists: lightweight-delete mask, LSB-first, n bits (1 = live), or NULL.
- * out_ids: nq*k int64; out_dist: nq*k fp32 (caller-owned). */
+ * out_ids: nq*k int64; out_dist: nq*k fp32 (caller-owned).
+ * k: 1 .. 16384 (the reference's max_search_result_window is 10000,
+ * Settings.h:923); above 4096 the final sort runs through a device scratch
+ * and large batches are searched in query sub-batches. */
 int mqvs_search(mqvs_segment_t seg, const float *queries, int32_t nq, int32_t k,
                 int32_t metric, const uint8_t *filter, const uint8_t *row_exists,
                 int64_t *out_ids, float *out_dist, uint32_t flags, mqvs_stream_t stream);
@@ -157,7 +177,8 @@ int mqvs_rerank(mqvs_segment_t seg, const float *queries, int32_t nq, const int6
                 int64_t *out_ids, float *out_dist, uint32_t flags, mqvs_stream_t stream);
 
 /* Merge per-list top-k results: in_ids/in_dist [nshards][nq][k] as returned
- * by mqvs_search; out nq*k (nshards * k <= 4096).
+ * by mqvs_search; out nq*k (nshards * k <= 2^20; above 4096 the records are
+ * sorted through a device scratch of 32 B per record and query).
  * Default (row-range shards of ONE part, shard s holding lower ids than shard
  * s+1): order distance (desc for IP), then shard, then position -- the result
  * equals the unsharded part's search.
@@ -337,10 +358,12 @@ int mqvs_set_batch_mode(int mode);
  * for the exact small-batch kernel), 2 = always gather.  All return the same
  * bits. */
 int mqvs_set_gather_mode(int mode);
-/* Pre-filter planes built by segments created AFTER the call: 6 = bf16 hi
- * plane + block-scaled fp6 cross plane, cross terms on the MX MFMA (default;
- * 3.5 B per element), 3 = bf16 hi + lo planes, three bf16 MFMAs (4 B per
- * element).  Both bound their error rigorously and return the same bits. */
+/* Pre-filter planes built by segments created AFTER the call: 2 = bf16 hi
+ * plane only, one bf16 MFMA product bounded by measured residual norms
+ * (default; 2 B per element), 6 = bf16 hi plane + block-scaled fp6 cross
+ * plane, cross terms on the MX MFMA (3.5 B per element), 3 = bf16 hi + lo
+ * planes, three bf16 MFMAs (4 B per element).  All bound their error
+ * rigorously and return the same bits. */
 int mqvs_set_prefilter(int split);
 
 #ifdef __cplusplus

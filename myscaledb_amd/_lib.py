@@ -26,6 +26,10 @@ F_ASYNC = 0x2
 F_PART_MERGE = 0x4
 F_FIRST_STAGE = 0x8
 F_NO_CHECKSUM = 0x10
+F_EXACT = 0x20
+F_GATHER_NEVER = 0x40
+F_GATHER_ALWAYS = 0x80
+F_TIMING = 0x100
 
 # Exported C symbols: every one of these is declared in include/mqvs.h.
 SYMBOLS = [
@@ -36,7 +40,7 @@ SYMBOLS = [
     "mqvs_last_search_stats", "mqvs_set_timing", "mqvs_set_batch_mode", "mqvs_set_gather_mode", "mqvs_set_prefilter",
     "mqvs_index_build", "mqvs_index_free", "mqvs_index_info", "mqvs_index_search", "mqvs_index_last_stats",
     "mqvs_segment_create_binary", "mqvs_search_binary", "mqvs_knn_binary_raw",
-    "mqvs_segment_create_from_column",
+    "mqvs_segment_create_from_column", "mqvs_async_check",
 ]
 
 
@@ -123,6 +127,7 @@ def _load():
         "mqvs_search_binary": ([P, P, I32, I32, I32, P, P, P, P, U32, P], ctypes.c_int),
         "mqvs_knn_binary_raw": ([P, P, I64, I64, I64, I64, I32, P, P], ctypes.c_int),
         "mqvs_segment_create_from_column": ([P, I64, P, I64, I64, I32, I32, I64, I64, U32, P], ctypes.c_int),
+        "mqvs_async_check": ([P], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -605,7 +605,14 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     dstats = (int64_t *)ws.fine.stats.get(sizeof(int64_t) * 8);
 
     const bool async = dev && (flags & MQVS_F_ASYNC);
-    if (async) return;
+    if (async) {
+        const bool variants_matter =
+            !first_stage &&
+            (int64_t)(seg->row_offset / seg->granule) + (seg->n + seg->granule - 1) / seg->granule > kMaxVariants;
+        launch_async_flags(nullptr, status, variants_matter ? 1 : 0, async_sticky(seg->device, s), s);
+        MQVS_HIP(hipGetLastError());
+        return;
+    }
     int64_t hs[4] = {0, 0, 0, 0};
     MQVS_HIP(hipMemcpyAsync(hs, dstats, sizeof(hs), hipMemcpyDeviceToHost, s));
     int hstatus = 0;

@@ -297,15 +297,19 @@ __device__ inline float exact_value(const ScanParams &p, int q, int64_t row) {
     return acc;
 }
 
+// scratch (k > kSortCap): 2 kLargeCap records per query; more than kSortCap
+// survivors are then re-ranked and sorted in global memory (global_sort).
 template <int METRIC, bool DIRECT>
 __global__ __launch_bounds__(SEL_THREADS) void k_rerank_select(ScanParams p, const float *bq, int k,
                                                               int64_t id_offset, int64_t *out_ids,
-                                                              float *out_dist, int *overflow) {
+                                                              float *out_dist, int *overflow, uint4 *scratch) {
     extern __shared__ __attribute__((aligned(16))) uint4 recs[];  // kSortCap records
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh[4];
     __shared__ int s_cnt;
     const int q = blockIdx.x;
+    uint4 *g = scratch ? scratch + (int64_t)q * 2 * kLargeCap : nullptr;
+    const int lcap = g ? kLargeCap : kSortCap;
     int n = p.cand_count[q];
     if (n > p.cand_cap) {
         if (threadIdx.x == 0) atomicOr(overflow, 1);
@@ -327,6 +331,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_select(ScanParams p, con
         if (take) {
             const int pos = atomicAdd(&s_cnt, 1);
             if (pos < kSortCap) recs[pos] = make_uint4(0, 0, 0, e.row);
+            if (g && pos < kLargeCap) g[pos] = make_uint4(0, 0, 0, e.row);
         }
     }
     __syncthreads();
@@ -336,13 +341,14 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_select(ScanParams p, con
         atomicAdd(overflow + 2, m);
         atomicMax(overflow + 3, n);      // candidates before it
     }
-    if (m > kSortCap) {
+    if (m > lcap) {
         if (threadIdx.x == 0) atomicOr(overflow, 4);
-        m = kSortCap;
+        m = lcap;
     }
-    // exact re-rank of the survivors
+    // exact re-rank of the survivors (in LDS, or in the global scratch)
+    uint4 *rr = m > kSortCap ? g : recs;
     for (int i = threadIdx.x; i < m; i += SEL_THREADS) {
-        const uint32_t row = recs[i].w;
+        const uint32_t row = rr[i].w;
         const float raw = exact_value<METRIC, DIRECT>(p, q, row);
         uint4 r;
         r.x = key32<METRIC>(raw);
@@ -354,7 +360,25 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_select(ScanParams p, con
             r.y = 0;
             r.z = 0;
         }
-        recs[i] = r;
+        rr[i] = r;
+    }
+    const float pad = (METRIC == MQVS_METRIC_IP) ? 1.17549435e-38f
+                      : (METRIC == kMetricIpRaw) ? -3.40282347e+38f
+                                                 : 3.40282347e+38f;
+    if (m > kSortCap) {
+        __syncthreads();
+        const uint4 *sorted = global_sort(g, g + kLargeCap, m, recs);
+        for (int i = threadIdx.x; i < k; i += SEL_THREADS) {
+            int64_t id = -1;
+            float dist = pad;
+            if (i < m && sorted[i].x != 0xFFFFFFFFu) {
+                id = (int64_t)sorted[i].w + id_offset;
+                dist = key_to_value(METRIC, sorted[i].x);
+            }
+            out_ids[(int64_t)q * k + i] = id;
+            out_dist[(int64_t)q * k + i] = dist;
+        }
+        return;
     }
     int N = 1;
     while (N < m) N <<= 1;
@@ -362,9 +386,6 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_select(ScanParams p, con
         recs[i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
     __syncthreads();
     block_bitonic_sort(recs, N);
-    const float pad = (METRIC == MQVS_METRIC_IP) ? 1.17549435e-38f
-                      : (METRIC == kMetricIpRaw) ? -3.40282347e+38f
-                                                 : 3.40282347e+38f;
     for (int i = threadIdx.x; i < k; i += SEL_THREADS) {
         int64_t id = -1;
         float dist = pad;
@@ -379,30 +400,30 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_select(ScanParams p, con
 
 template <int M>
 static void rerank_select_t(const ScanParams &p, const float *bq, int k, int64_t id_offset,
-                            int64_t *out_ids, float *out_dist, int *overflow, hipStream_t s) {
+                            int64_t *out_ids, float *out_dist, int *overflow, uint4 *scratch, hipStream_t s) {
     if (p.nq < kBlasThreshold)
         hipLaunchKernelGGL((k_rerank_select<M, true>), dim3(p.nq), dim3(SEL_THREADS), kSortCap * sizeof(uint4),
-                           s, p, bq, k, id_offset, out_ids, out_dist, overflow);
+                           s, p, bq, k, id_offset, out_ids, out_dist, overflow, scratch);
     else
         hipLaunchKernelGGL((k_rerank_select<M, false>), dim3(p.nq), dim3(SEL_THREADS), kSortCap * sizeof(uint4),
-                           s, p, bq, k, id_offset, out_ids, out_dist, overflow);
+                           s, p, bq, k, id_offset, out_ids, out_dist, overflow, scratch);
 }
 
 void launch_rerank_select(const ScanParams &p, int metric, const float *bq, int k,
                           int64_t id_offset, int64_t *out_ids, float *out_dist, int *overflow,
-                          hipStream_t s) {
+                          uint4 *scratch, hipStream_t s) {
     switch (metric) {
         case MQVS_METRIC_L2:
-            rerank_select_t<MQVS_METRIC_L2>(p, bq, k, id_offset, out_ids, out_dist, overflow, s);
+            rerank_select_t<MQVS_METRIC_L2>(p, bq, k, id_offset, out_ids, out_dist, overflow, scratch, s);
             break;
         case MQVS_METRIC_IP:
-            rerank_select_t<MQVS_METRIC_IP>(p, bq, k, id_offset, out_ids, out_dist, overflow, s);
+            rerank_select_t<MQVS_METRIC_IP>(p, bq, k, id_offset, out_ids, out_dist, overflow, scratch, s);
             break;
         case MQVS_METRIC_COSINE:
-            rerank_select_t<MQVS_METRIC_COSINE>(p, bq, k, id_offset, out_ids, out_dist, overflow, s);
+            rerank_select_t<MQVS_METRIC_COSINE>(p, bq, k, id_offset, out_ids, out_dist, overflow, scratch, s);
             break;
         default:
-            rerank_select_t<kMetricIpRaw>(p, bq, k, id_offset, out_ids, out_dist, overflow, s);
+            rerank_select_t<kMetricIpRaw>(p, bq, k, id_offset, out_ids, out_dist, overflow, scratch, s);
             break;
     }
 }

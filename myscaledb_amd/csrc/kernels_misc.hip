@@ -544,4 +544,19 @@ void launch_chunk_ordinals(const uint8_t *filter, const uint8_t *nonempty, const
     hipLaunchKernelGGL(k_exclusive_ord, dim3(1), dim3(256), 0, s, ord, nchunks);
 }
 
+// ---------------------------------------------------------------------------
+// ASYNC outcome of a search, OR-ed into the thread's sticky word
+// (mqvs_async_check)
+__global__ void k_async_flags(const int *overflow, const int *status, int status_matters, int *sticky) {
+    if (threadIdx.x != 0) return;
+    int w = 0;
+    if (overflow && overflow[0]) w |= 1;
+    if (status && status_matters && status[0]) w |= 2;
+    if (w) atomicOr(sticky, w);
+}
+
+void launch_async_flags(const int *overflow, const int *status, int status_matters, int *sticky, hipStream_t s) {
+    hipLaunchKernelGGL(k_async_flags, dim3(1), dim3(64), 0, s, overflow, status, status_matters, sticky);
+}
+
 }  // namespace mqvs

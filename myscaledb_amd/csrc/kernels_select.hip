@@ -62,17 +62,22 @@ __global__ __launch_bounds__(SEL_THREADS) void k_cand_tau(const Cand *cand, cons
 }
 
 
+// scratch (k > kSortCap): 2 kLargeCap records per query in global memory;
+// the records to sort then may exceed the LDS sort (global_sort).
 template <int METRIC>
 __global__ __launch_bounds__(SEL_THREADS) void k_final_select(const Cand *cand,
                                                              const int *cand_count, int cap,
                                                              int k, int64_t chunk_rows,
                                                              int64_t id_offset, int64_t *out_ids,
-                                                             float *out_dist, int *overflow) {
+                                                             float *out_dist, int *overflow,
+                                                             uint4 *scratch) {
     extern __shared__ __attribute__((aligned(16))) uint4 recs[];  // kSortCap records
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh[4];
     __shared__ int s_cnt;
     const int q = blockIdx.x;
+    uint4 *g = scratch ? scratch + (int64_t)q * 2 * kLargeCap : nullptr;
+    const int lcap = g ? kLargeCap : kSortCap;  // records this call can sort
     int n = cand_count[q];
     if (n > cap) {
         if (threadIdx.x == 0) atomicOr(overflow, 1);
@@ -127,7 +132,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_final_select(const Cand *cand,
             __syncthreads();
             const int ntie = s_cnt;
             __syncthreads();
-            if (nbelow + ntie > kSortCap) {
+            if (nbelow + ntie > lcap) {
                 auto rowof = [&](int64_t i) {
                     const Cand e = c[i];
                     return key32<METRIC>(e.raw) == th ? e.row : 0xFFFFFFFFu;
@@ -142,15 +147,35 @@ __global__ __launch_bounds__(SEL_THREADS) void k_final_select(const Cand *cand,
             const uint32_t key = key32<METRIC>(e.raw);
             if (key != 0xFFFFFFFFu && (key < th || (key == th && e.row <= rth))) {
                 const int pos = atomicAdd(&s_cnt, 1);
-                if (pos < kSortCap) recs[pos] = make_rec(e);
+                const uint4 r = make_rec(e);
+                if (pos < kSortCap) recs[pos] = r;
+                if (g && pos < kLargeCap) g[pos] = r;
             }
         }
         __syncthreads();
         m = s_cnt;
-        if (m > kSortCap) {  // more than kSortCap rows tie at the k-th key
+        if (m > lcap) {  // more than lcap rows tie at the k-th key
             if (threadIdx.x == 0) atomicOr(overflow, 2);
-            m = kSortCap;
+            m = lcap;
         }
+    }
+    const float pad = (METRIC == MQVS_METRIC_IP) ? 1.17549435e-38f
+                      : (METRIC == kMetricIpRaw) ? -3.40282347e+38f
+                                                 : 3.40282347e+38f;
+    if (m > kSortCap) {
+        __syncthreads();
+        const uint4 *sorted = global_sort(g, g + kLargeCap, m, recs);
+        for (int i = threadIdx.x; i < k; i += SEL_THREADS) {
+            int64_t id = -1;
+            float dist = pad;
+            if (i < m) {
+                id = (int64_t)sorted[i].w + id_offset;
+                dist = key_to_value(METRIC, sorted[i].x);
+            }
+            out_ids[(int64_t)q * k + i] = id;
+            out_dist[(int64_t)q * k + i] = dist;
+        }
+        return;
     }
     int N = 1;
     while (N < m) N <<= 1;
@@ -158,9 +183,6 @@ __global__ __launch_bounds__(SEL_THREADS) void k_final_select(const Cand *cand,
         recs[i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
     __syncthreads();
     block_bitonic_sort(recs, N);
-    const float pad = (METRIC == MQVS_METRIC_IP) ? 1.17549435e-38f
-                      : (METRIC == kMetricIpRaw) ? -3.40282347e+38f
-                                                 : 3.40282347e+38f;
     for (int i = threadIdx.x; i < k; i += SEL_THREADS) {
         int64_t id = -1;
         float dist = pad;
@@ -177,40 +199,51 @@ __global__ __launch_bounds__(SEL_THREADS) void k_final_select(const Cand *cand,
 // cross-PART merge, MergeTreeBaseSearchManager.cpp:207-297): the reference
 // walks its insertion-ordered multimap backwards for DESC, so equal scores
 // come out last-inserted first -> key (distance, ~list, ~position).
+// scratch: 2 nshards k records per query when nshards k > kSortCap (the
+// records are sorted through global memory), else null.
 template <int METRIC>
 __global__ __launch_bounds__(SEL_THREADS) void k_merge_shards(int nshards, int nq, int k,
                                                              const int64_t *in_ids,
                                                              const float *in_dist,
                                                              int64_t *out_ids, float *out_dist,
-                                                             int rev_ties) {
+                                                             int rev_ties, uint4 *scratch) {
     extern __shared__ __attribute__((aligned(16))) uint4 recs[];
     const int q = blockIdx.x;
     const int n = nshards * k;
-    int N = 1;
-    while (N < n) N <<= 1;
-    for (int i = threadIdx.x; i < N; i += SEL_THREADS) {
+    auto record = [&](int i) {
         uint4 r = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-        if (i < n) {
-            const int s = i / k, pos = i % k;
-            const int64_t off = ((int64_t)s * nq + q) * k + pos;
-            if (in_ids[off] >= 0) {
-                const float v = in_dist[off];
-                r.x = (METRIC == MQVS_METRIC_IP || METRIC == kMetricIpRaw) ? ~ord_asc(v) : ord_asc(v);
-                r.y = rev_ties ? ~(uint32_t)s : (uint32_t)s;
-                r.z = rev_ties ? ~(uint32_t)pos : (uint32_t)pos;
-                r.w = (uint32_t)i;
-            }
+        const int s = i / k, pos = i % k;
+        const int64_t off = ((int64_t)s * nq + q) * k + pos;
+        if (in_ids[off] >= 0) {
+            const float v = in_dist[off];
+            r.x = (METRIC == MQVS_METRIC_IP || METRIC == kMetricIpRaw) ? ~ord_asc(v) : ord_asc(v);
+            r.y = rev_ties ? ~(uint32_t)s : (uint32_t)s;
+            r.z = rev_ties ? ~(uint32_t)pos : (uint32_t)pos;
         }
-        recs[i] = r;
+        r.w = (uint32_t)i;  // (unique: empty slots sort last, by position)
+        return r;
+    };
+    const uint4 *sorted = recs;
+    int N = 1;
+    if (n > kSortCap) {
+        uint4 *g = scratch + (int64_t)q * 2 * n;
+        for (int i = threadIdx.x; i < n; i += SEL_THREADS) g[i] = record(i);
+        __syncthreads();
+        sorted = global_sort(g, g + n, n, recs);
+        N = n;
+    } else {
+        while (N < n) N <<= 1;
+        for (int i = threadIdx.x; i < N; i += SEL_THREADS)
+            recs[i] = i < n ? record(i) : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        __syncthreads();
+        block_bitonic_sort(recs, N);
     }
-    __syncthreads();
-    block_bitonic_sort(recs, N);
     const float pad = (METRIC == MQVS_METRIC_IP) ? 1.17549435e-38f : 3.40282347e+38f;
     for (int i = threadIdx.x; i < k; i += SEL_THREADS) {
         int64_t id = -1;
         float dist = pad;
-        if (i < N && recs[i].x != 0xFFFFFFFFu) {
-            const int src = (int)recs[i].w;
+        if (i < N && sorted[i].x != 0xFFFFFFFFu) {
+            const int src = (int)sorted[i].w;
             const int s = src / k, pos = src % k;
             const int64_t off = ((int64_t)s * nq + q) * k + pos;
             id = in_ids[off];
@@ -267,33 +300,34 @@ static size_t sort_lds(int n) {
 template <int M>
 static void final_select_t(const Cand *cand, const int *cc, int cap, int nq, int k,
                            int64_t chunk_rows, int64_t id_offset, int64_t *out_ids,
-                           float *out_dist, int *overflow, hipStream_t s) {
+                           float *out_dist, int *overflow, uint4 *scratch, hipStream_t s) {
     hipLaunchKernelGGL(k_final_select<M>, dim3(nq), dim3(SEL_THREADS), sort_lds(kSortCap), s, cand, cc,
-                       cap, k, chunk_rows, id_offset, out_ids, out_dist, overflow);
+                       cap, k, chunk_rows, id_offset, out_ids, out_dist, overflow, scratch);
 }
 
 void launch_final_select(const Cand *cand, const int *cand_count, int cand_cap, int nq, int k,
                          int metric, int64_t chunk_rows, int64_t id_offset, int64_t *out_ids,
-                         float *out_dist, int *overflow, hipStream_t s) {
+                         float *out_dist, int *overflow, uint4 *scratch, hipStream_t s) {
     if (nq <= 0) return;
     MQVS_DISPATCH_METRIC(metric, final_select_t, (cand, cand_count, cand_cap, nq, k, chunk_rows,
-                                                  id_offset, out_ids, out_dist, overflow, s));
+                                                  id_offset, out_ids, out_dist, overflow, scratch, s));
 }
 
 template <int M>
 static void merge_shards_t(int nshards, int nq, int k, const int64_t *in_ids, const float *in_dist,
-                           int64_t *out_ids, float *out_dist, int rev_ties, hipStream_t s) {
-    hipLaunchKernelGGL(k_merge_shards<M>, dim3(nq), dim3(SEL_THREADS), sort_lds(nshards * k), s,
-                       nshards, nq, k, in_ids, in_dist, out_ids, out_dist, rev_ties);
+                           int64_t *out_ids, float *out_dist, int rev_ties, uint4 *scratch, hipStream_t s) {
+    hipLaunchKernelGGL(k_merge_shards<M>, dim3(nq), dim3(SEL_THREADS),
+                       sort_lds(nshards * k > kSortCap ? kSortCap : nshards * k), s, nshards, nq, k, in_ids, in_dist,
+                       out_ids, out_dist, rev_ties, scratch);
 }
 
 void launch_merge_shards(int nshards, int nq, int k, int metric, const int64_t *in_ids,
                          const float *in_dist, int64_t *out_ids, float *out_dist, bool part_merge,
-                         hipStream_t s) {
+                         uint4 *scratch, hipStream_t s) {
     if (nq <= 0) return;
     const int rev = part_merge && (metric == MQVS_METRIC_IP || metric == kMetricIpRaw);
     MQVS_DISPATCH_METRIC(metric, merge_shards_t,
-                         (nshards, nq, k, in_ids, in_dist, out_ids, out_dist, rev, s));
+                         (nshards, nq, k, in_ids, in_dist, out_ids, out_dist, rev, scratch, s));
 }
 
 // ---------------------------------------------------------------------------

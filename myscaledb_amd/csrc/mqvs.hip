@@ -12,6 +12,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <atomic>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -25,8 +26,11 @@ namespace mqvs {
 
 static thread_local std::string g_error;
 static thread_local mqvs_search_stats g_stats{};
-static int g_timing = 0;
-static int g_prefilter = 2;  // planes built by new segments (mqvs_set_prefilter)
+// Process-wide defaults of the per-call mode flags (mqvs_set_*): atomics, read
+// once at the entry of a call, so a setter racing with searches on other
+// threads never switches a search's path midway (per-call flags override them).
+static std::atomic<int> g_timing{0};
+static std::atomic<int> g_prefilter{2};  // planes built by new segments (mqvs_set_prefilter)
 
 void set_error(const std::string &msg) { g_error = msg; }
 
@@ -37,7 +41,7 @@ struct Workspace {
     static constexpr int kSegEv = 64;
     hipEvent_t seg_ev[kSegEv] = {};  // per main-scan segment: start, end
     DevBuf queries, qvars, qnorms, qmu, qlam, status, filter, exists, ord, probe, tau, count, cand,
-        overflow, out_ids, out_dist, misc, qhi, bq, thr, cand2, count2, gcount, goff, glist;
+        overflow, out_ids, out_dist, misc, qhi, bq, thr, cand2, count2, gcount, goff, glist, large, sticky;
     int *host_flags = nullptr;  // pinned
     void init() {
         if (stream) return;
@@ -49,7 +53,7 @@ struct Workspace {
     void release() {
         DevBuf *all[] = {&queries, &qvars, &qnorms, &qmu,  &qlam,   &status,  &filter,   &exists, &ord,
                          &probe,   &tau,   &count,  &cand, &overflow, &out_ids, &out_dist, &misc,
-                         &qhi, &bq, &thr, &cand2, &count2, &gcount, &goff, &glist};
+                         &qhi, &bq, &thr, &cand2, &count2, &gcount, &goff, &glist, &large, &sticky};
         for (auto *b : all) b->release();
         if (host_flags) (void)hipHostFree(host_flags);
         host_flags = nullptr;
@@ -100,7 +104,7 @@ static void prepare_segment(mqvs_segment *s, const uint8_t *dev_nonempty_bytes,
     launch_max_norm(s->norms, s->n, s->ynorm_max, st);
     const int64_t nr = std::max<int64_t>(s->n, 1);
     const int64_t nr16 = (nr + 15) / 16 * 16;  // row-blocked planes: blocks of 16 rows
-    const int split = g_prefilter;
+    const int split = g_prefilter.load(std::memory_order_relaxed);
     const size_t hb = (size_t)(split == kBfSplit ? nr : nr16) * s->dpad * sizeof(uint16_t);
     const size_t xb = (size_t)nr16 * (s->dpad / 32) * 48;
     bool ok = hipMalloc((void **)&s->rows_hi, hb) == hipSuccess;
@@ -243,8 +247,46 @@ static void run_scan(ScanParams p, const Range &r, int kind, int metric, bool pr
 static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 
 // metric: public metric, or kMetricIpRaw for the faiss-contract entry point
-static int g_batch_mode = 0;  // 0: bf16 pre-filter + exact re-rank when possible, 1: fp32 MFMA
-static int g_gather_mode = 1;  // selective PREWHERE: 0 never gather, 1 when <= 50% selected, 2 always
+static std::atomic<int> g_batch_mode{0};   // 0: bf16 pre-filter + exact re-rank when possible, 1: fp32 MFMA
+static std::atomic<int> g_gather_mode{1};  // selective PREWHERE: 0 never gather, 1 when <= 60% selected, 2 always
+
+static int call_batch_mode(uint32_t flags) {
+    return (flags & MQVS_F_EXACT) ? 1 : g_batch_mode.load(std::memory_order_relaxed);
+}
+static int call_gather_mode(uint32_t flags) {
+    if (flags & MQVS_F_GATHER_NEVER) return 0;
+    if (flags & MQVS_F_GATHER_ALWAYS) return 2;
+    return g_gather_mode.load(std::memory_order_relaxed);
+}
+static bool call_timing(uint32_t flags) {
+    return (flags & MQVS_F_TIMING) || g_timing.load(std::memory_order_relaxed) != 0;
+}
+
+// ASYNC searches cannot run the host-driven fallbacks (exact re-scan after a
+// pre-filter overflow, tightened re-scan, the cosine variant check): their
+// device flags are OR-ed into this thread's sticky word, which
+// mqvs_async_check reads and clears.
+static int *sticky_word(Workspace &ws, hipStream_t s) {
+    if (!ws.sticky.p) {
+        ws.sticky.get(16);
+        MQVS_HIP(hipMemsetAsync(ws.sticky.p, 0, 16, s));
+    }
+    return (int *)ws.sticky.p;
+}
+
+int *async_sticky(int device, hipStream_t s) { return sticky_word(workspace(device), s); }
+
+// Large k (above the LDS sort): the global-scratch sort of the final select,
+// and query sub-batches small enough that the candidate lists and the dense
+// probe matrix stay within a fixed HBM budget.
+static int large_k_cap(int k) { return (int)std::min<int64_t>(kCandMax, (int64_t)16 * k); }
+static int large_k_batch(int64_t n, int k) {
+    const int64_t cap = large_k_cap(k);
+    const int64_t probe = std::min<int64_t>(n, (int64_t)((double)k * (double)n / (double)(cap / 3)) + 1);
+    const int64_t by_cand = ((int64_t)1 << 27) / cap;                  // 1 GB per candidate buffer
+    const int64_t by_probe = ((int64_t)1 << 28) / std::max<int64_t>(probe, 1);  // 1 GB of probe values
+    return (int)std::max<int64_t>(1, std::min(by_cand, by_probe));
+}
 
 static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, int metric,
                         const uint8_t *filter, const uint8_t *exists, int64_t *out_ids,
@@ -261,10 +303,23 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     if (cos != (seg->metric == MQVS_METRIC_COSINE))
         fail(MQVS_ERR_LOGICAL, "segment was prepared for a different metric (cosine segments are "
                                "normalised in HBM and serve only cosine searches)");
-    if (k > kSortCap) fail(MQVS_ERR_BAD_ARGUMENTS, "k above " + std::to_string(kSortCap) + " not supported");
+    if (k > kMaxK) fail(MQVS_ERR_BAD_ARGUMENTS, "k above " + std::to_string(kMaxK) + " not supported");
     mqvs_search_stats st{};
     g_stats = st;
     if (nq == 0 || k == 0) return;
+    if (k > kSortCap) {
+        // large k: query sub-batches (queries are independent searches)
+        const int qb = large_k_batch(seg->n, k);
+        if (nq > qb) {
+            for (int q0 = 0; q0 < nq; q0 += qb) {
+                const int m = std::min(qb, nq - q0);
+                search_impl(seg, queries + (size_t)q0 * seg->d, m, k, metric, filter, exists,
+                            out_ids + (size_t)q0 * k, out_dist + (size_t)q0 * k, flags, user_stream, force_exact,
+                            ord_base);
+            }
+            return;
+        }
+    }
 
     DeviceGuard guard(seg->device);
     Workspace &ws = workspace(seg->device);
@@ -273,7 +328,9 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     const int64_t n = seg->n;
     const int d = seg->d;
     const int64_t bm_bytes = (n + 7) / 8;
-    const bool timing = g_timing != 0;
+    const bool timing = call_timing(flags);
+    const int batch_mode = call_batch_mode(flags);
+    const int gather_mode = call_gather_mode(flags);
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[0], s));
 
     // ---- inputs on device
@@ -309,7 +366,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     int64_t selected = -1, gpadded = 0;
     int *gcount = nullptr;
     int64_t *goff = nullptr;
-    if (dfilter && g_gather_mode != 0 && n > 0) {
+    if (dfilter && gather_mode != 0 && n > 0) {
         const int64_t nch = (n + seg->granule - 1) / seg->granule;
         gcount = (int *)ws.gcount.get(sizeof(int) * nch);
         goff = (int64_t *)ws.goff.get(sizeof(int64_t) * (nch + 2));
@@ -332,13 +389,13 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     // to ~60% selectivity, while the VALU kernel's 128-B row slices only pay
     // below ~30% (tools/sweep.py --sels, profiles/r01)
     const bool mfma = nq >= kBlasThreshold;
-    const bool bf16_ok = seg->approx_ok && !force_exact && g_batch_mode == 0;
+    const bool bf16_ok = seg->approx_ok && !force_exact && batch_mode == 0;
     // (split 2 streams half the bytes of the fp32 rows, so it serves every
     // batch size; the older splits start at kBf16MinNq)
     bool bf16 = bf16_ok && nq >= (seg->split == kHiSplit ? 1 : kBf16MinNq);
     bool gather = false;
     if (selected >= 0) {
-        if (g_gather_mode == 2)
+        if (gather_mode == 2)
             gather = bf16 || !mfma;
         else if (bf16_ok && 10 * selected <= 6 * n)
             gather = bf16 = true;
@@ -394,9 +451,10 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     // ---- candidate capacity per query (a fixed budget spread over the
     // batch) and probe size: expected candidates ~ k*n/P; aim at cap/3
     int cap = (int)std::min<int64_t>(kCandMax, kCandBudget / std::max(nq, 1));
-    cap = std::max(cap, kSortCap) / 256 * 256;
+    cap = std::max(cap, k > kSortCap ? large_k_cap(k) : kSortCap) / 256 * 256;
     // (more candidates = more appends from the scan; 16k keeps them cheap)
-    const int64_t target_cands = std::min<int64_t>(cap / 3, 16384);
+    const int64_t target_cands = std::min<int64_t>(cap / 3, std::max<int64_t>(16384, 2 * (int64_t)k));
+    uint4 *large = k > kSortCap ? (uint4 *)ws.large.get(sizeof(uint4) * 2 * kLargeCap * (size_t)nq) : nullptr;
     int64_t P = scan_n;
     if (scan_n > 32768) {
         P = (int64_t)(((double)k * (double)scan_n) / target_cands) + 1;
@@ -543,10 +601,10 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[3], s));
     MQVS_HIP(hipMemsetAsync(overflow, 0, sizeof(int) * 4, s));
     if (kind == kScanBf16)
-        launch_rerank_select(p, metric, bq, k, seg->row_offset, dids, ddist, overflow, s);
+        launch_rerank_select(p, metric, bq, k, seg->row_offset, dids, ddist, overflow, large, s);
     else
         launch_final_select(cand, count, cap, nq, k, metric, seg->granule, seg->row_offset, dids, ddist,
-                            overflow, s);
+                            overflow, large, s);
     MQVS_HIP(hipGetLastError());
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[4], s));
 
@@ -559,7 +617,12 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     st.k = k;
 
     const bool async = dev && (flags & MQVS_F_ASYNC);
-    if (!async) {
+    if (async) {
+        // no host fallback possible: leave the outcome for mqvs_async_check
+        const bool variants_matter = p.ord_base + (n + seg->granule - 1) / seg->granule > kMaxVariants;
+        launch_async_flags(overflow, status, variants_matter ? 1 : 0, sticky_word(ws, s), s);
+        MQVS_HIP(hipGetLastError());
+    } else {
         MQVS_HIP(hipMemcpyAsync(ws.host_flags, overflow, sizeof(int), hipMemcpyDeviceToHost, s));
         MQVS_HIP(hipMemcpyAsync(ws.host_flags + 1, status, sizeof(int), hipMemcpyDeviceToHost, s));
         MQVS_HIP(hipMemcpyAsync(ws.host_flags + 4, overflow + 1, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
@@ -591,7 +654,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
             run_scan(p, make_range(0, scan_n, tile_rows, seg->granule, aligned), kind, metric, false, s);
             MQVS_HIP(hipMemsetAsync(overflow, 0, sizeof(int) * 4, s));
             launch_final_select(cand, count, cap, nq, k, metric, seg->granule, seg->row_offset, dids,
-                                ddist, overflow, s);
+                                ddist, overflow, large, s);
             MQVS_HIP(hipGetLastError());
             MQVS_HIP(hipMemcpyAsync(ws.host_flags, overflow, sizeof(int), hipMemcpyDeviceToHost, s));
             MQVS_HIP(hipStreamSynchronize(s));
@@ -710,7 +773,12 @@ static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const i
     p.nonempty = seg->nonempty_bits;
     launch_rerank_ids(p, metric, dc, ncand, k, seg->row_offset, dids, ddist, s);
     MQVS_HIP(hipGetLastError());
-    if (dev && (flags & MQVS_F_ASYNC)) return;
+    if (dev && (flags & MQVS_F_ASYNC)) {
+        const bool variants_matter = p.ord_base + (seg->n + seg->granule - 1) / seg->granule > kMaxVariants;
+        launch_async_flags(nullptr, status, variants_matter ? 1 : 0, sticky_word(ws, s), s);
+        MQVS_HIP(hipGetLastError());
+        return;
+    }
     MQVS_HIP(hipMemcpyAsync(ws.host_flags, status, sizeof(int), hipMemcpyDeviceToHost, s));
     MQVS_HIP(hipStreamSynchronize(s));
     if (ws.host_flags[0] && p.ord_base + (seg->n + seg->granule - 1) / seg->granule > kMaxVariants)
@@ -780,12 +848,23 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
     if (metric != MQVS_METRIC_HAMMING && metric != MQVS_METRIC_JACCARD)
         fail(MQVS_ERR_NOT_IMPLEMENTED, "Metric not implemented in brute force search for Binary Vector");
     if (nq < 0 || k < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "nq and k must be non-negative");
-    if (k > kSortCap) fail(MQVS_ERR_BAD_ARGUMENTS, "k above " + std::to_string(kSortCap) + " not supported");
+    if (k > kMaxK) fail(MQVS_ERR_BAD_ARGUMENTS, "k above " + std::to_string(kMaxK) + " not supported");
     if (nq > 0 && k > 0 && (!queries || !out_ids || !out_dist))
         fail(MQVS_ERR_BAD_ARGUMENTS, "null query or output pointer");
     mqvs_search_stats st{};
     g_stats = st;
     if (nq == 0 || k == 0) return;
+    if (k > kSortCap) {
+        const int qb = large_k_batch(seg->n, k);
+        if (nq > qb) {
+            for (int q0 = 0; q0 < nq; q0 += qb) {
+                const int m = std::min(qb, nq - q0);
+                search_binary_impl(seg, queries + (size_t)q0 * seg->code_bytes, m, k, metric, filter, exists,
+                                   out_ids + (size_t)q0 * k, out_dist + (size_t)q0 * k, flags, user_stream);
+            }
+            return;
+        }
+    }
 
     DeviceGuard guard(seg->device);
     Workspace &ws = workspace(seg->device);
@@ -793,7 +872,7 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
     const bool dev = flags & MQVS_F_DEVICE_PTRS;
     const int64_t n = seg->n;
     const int64_t bm_bytes = (n + 7) / 8;
-    const bool timing = g_timing != 0;
+    const bool timing = call_timing(flags);
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[0], s));
 
     uint32_t *qc = (uint32_t *)ws.queries.get((size_t)nq * seg->code_words * 4);
@@ -821,8 +900,9 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
     // candidate capacity and probe size as the float path (mqvs.hip search_impl)
     constexpr int64_t tile_rows = kSmallRows;
     int cap = (int)std::min<int64_t>(kCandMax, kCandBudget / std::max(nq, 1));
-    cap = std::max(cap, kSortCap) / 256 * 256;
-    const int64_t target_cands = std::min<int64_t>(cap / 3, 16384);
+    cap = std::max(cap, k > kSortCap ? large_k_cap(k) : kSortCap) / 256 * 256;
+    const int64_t target_cands = std::min<int64_t>(cap / 3, std::max<int64_t>(16384, 2 * (int64_t)k));
+    uint4 *large = k > kSortCap ? (uint4 *)ws.large.get(sizeof(uint4) * 2 * kLargeCap * (size_t)nq) : nullptr;
     int64_t P = n;
     if (n > 32768) {
         P = (int64_t)(((double)k * (double)n) / target_cands) + 1;
@@ -900,7 +980,7 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
     }
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[3], s));
     MQVS_HIP(hipMemsetAsync(overflow, 0, sizeof(int) * 4, s));
-    launch_final_select(cand, count, cap, nq, k, kOrder, 0, seg->row_offset, dids, ddist, overflow, s);
+    launch_final_select(cand, count, cap, nq, k, kOrder, 0, seg->row_offset, dids, ddist, overflow, large, s);
     MQVS_HIP(hipGetLastError());
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[4], s));
     st.path = 3;  // binary popcount scan
@@ -910,7 +990,10 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
     st.nq = nq;
     st.k = k;
     const bool async = dev && (flags & MQVS_F_ASYNC);
-    if (!async) {
+    if (async) {
+        launch_async_flags(overflow, nullptr, 0, sticky_word(ws, s), s);
+        MQVS_HIP(hipGetLastError());
+    } else {
         MQVS_HIP(hipMemcpyAsync(ws.host_flags, overflow, sizeof(int), hipMemcpyDeviceToHost, s));
         MQVS_HIP(hipStreamSynchronize(s));
         int rescans = 0;
@@ -925,7 +1008,8 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
             MQVS_HIP(hipMemsetAsync(count, 0, sizeof(int) * nq, s));
             scan(0, n, false, false);
             MQVS_HIP(hipMemsetAsync(overflow, 0, sizeof(int) * 4, s));
-            launch_final_select(cand, count, cap, nq, k, kOrder, 0, seg->row_offset, dids, ddist, overflow, s);
+            launch_final_select(cand, count, cap, nq, k, kOrder, 0, seg->row_offset, dids, ddist, overflow, large,
+                                s);
             MQVS_HIP(hipGetLastError());
             MQVS_HIP(hipMemcpyAsync(ws.host_flags, overflow, sizeof(int), hipMemcpyDeviceToHost, s));
             MQVS_HIP(hipStreamSynchronize(s));
@@ -1398,7 +1482,7 @@ int mqvs_merge_shards(int32_t nshards, int32_t nq, int32_t k, int32_t metric, co
                       mqvs_stream_t stream) {
     return guarded([&] {
         if (nshards <= 0 || nq < 0 || k < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "bad sizes");
-        if ((int64_t)nshards * k > kSortCap) fail(MQVS_ERR_BAD_ARGUMENTS, "nshards * k above sort capacity");
+        if ((int64_t)nshards * k > ((int64_t)1 << 20)) fail(MQVS_ERR_BAD_ARGUMENTS, "nshards * k above 2^20");
         if (nq == 0 || k == 0) return;
         int dev = 0;
         MQVS_HIP(hipGetDevice(&dev));
@@ -1423,7 +1507,10 @@ int mqvs_merge_shards(int32_t nshards, int32_t nq, int32_t k, int32_t metric, co
         }
         // binary distances (Hamming, Jaccard) are ascending finite values: the L2 order
         const int order = (metric == MQVS_METRIC_HAMMING || metric == MQVS_METRIC_JACCARD) ? MQVS_METRIC_L2 : metric;
-        launch_merge_shards(nshards, nq, k, order, di, dd, oi, od, (flags & MQVS_F_PART_MERGE) != 0, s);
+        uint4 *scratch = (int64_t)nshards * k > kSortCap
+                             ? (uint4 *)ws.large.get(sizeof(uint4) * 2 * (size_t)nshards * k * nq)
+                             : nullptr;
+        launch_merge_shards(nshards, nq, k, order, di, dd, oi, od, (flags & MQVS_F_PART_MERGE) != 0, scratch, s);
         MQVS_HIP(hipGetLastError());
         if (!devp) {
             MQVS_HIP(hipMemcpyAsync(out_ids, oi, nout * 8, hipMemcpyDeviceToHost, s));
@@ -1464,25 +1551,45 @@ int mqvs_last_search_stats(mqvs_search_stats *out) {
 
 int mqvs_set_batch_mode(int mode) {
     if (mode != 0 && mode != 1) return MQVS_ERR_BAD_ARGUMENTS;
-    g_batch_mode = mode;
+    g_batch_mode.store(mode);
     return MQVS_OK;
 }
 
 int mqvs_set_prefilter(int split) {
     if (split != kHiSplit && split != kBfSplit && split != kMxSplit) return MQVS_ERR_BAD_ARGUMENTS;
-    g_prefilter = split;
+    g_prefilter.store(split);
     return MQVS_OK;
 }
 
 int mqvs_set_gather_mode(int mode) {
     if (mode < 0 || mode > 2) return MQVS_ERR_BAD_ARGUMENTS;
-    g_gather_mode = mode;
+    g_gather_mode.store(mode);
     return MQVS_OK;
 }
 
 int mqvs_set_timing(int enabled) {
-    g_timing = enabled;
+    g_timing.store(enabled ? 1 : 0);
     return MQVS_OK;
+}
+
+int mqvs_async_check(mqvs_stream_t stream) {
+    return guarded([&] {
+        int dev = 0;
+        MQVS_HIP(hipGetDevice(&dev));
+        Workspace &ws = workspace(dev);
+        hipStream_t s = stream ? (hipStream_t)stream : ws.stream;
+        MQVS_HIP(hipStreamSynchronize(s));
+        if (!ws.sticky.p) return;
+        int word = 0;
+        MQVS_HIP(hipMemcpy(&word, ws.sticky.p, sizeof(int), hipMemcpyDeviceToHost));
+        MQVS_HIP(hipMemset(ws.sticky.p, 0, 16));
+        if (word & 1)
+            fail(MQVS_ERR_LOGICAL, "an ASYNC search needed its candidate-overflow fallback (results invalid): "
+                                   "repeat it without MQVS_F_ASYNC");
+        if (word & 2)
+            fail(MQVS_ERR_LOGICAL, "an ASYNC cosine search's query normalisation did not repeat within " +
+                                       std::to_string(kMaxVariants) + " steps on a part of more chunks");
+    });
 }
 
 }  // extern "C"

@@ -45,6 +45,8 @@ namespace mqvs {
 constexpr int kBlasThreshold = 20;   // faiss distance_compute_blas_threshold
 constexpr int kMaxVariants = 32;     // cosine query re-normalisation variants kept
 constexpr int kSortCap = 4096;       // candidates sorted in LDS per query
+constexpr int kMaxK = 16384;         // largest k (max_search_result_window is 10000, Settings.h:923)
+constexpr int kLargeCap = 32768;     // records per query sorted through global scratch (k > kSortCap)
 constexpr int64_t kCandBudget = 1 << 25;  // candidate slots per search (x 8 B)
 constexpr int64_t kCandMax = 1 << 20;     // candidate slots per query
 constexpr int kSmallRows = 256;      // rows per tile, VALU scan
@@ -255,12 +257,21 @@ void launch_probe_select(const float *probe, int64_t P, int64_t ld, int nq, int 
                          int64_t row_base, const int32_t *row_list, hipStream_t s);
 void launch_cand_tau(const Cand *cand, const int *cand_count, int cand_cap, int nq, int k,
                      int metric, uint32_t *tau, const int *overflow_q, hipStream_t s);
+// ASYNC calls: OR a search's device flags into the calling thread's sticky
+// word (read and cleared by mqvs_async_check): bit 0 = candidate overflow
+// (overflow[0] != 0), bit 1 = cosine variant chain did not repeat (status[0]
+// != 0 and status_matters).  overflow / status may be null.
+void launch_async_flags(const int *overflow, const int *status, int status_matters, int *sticky, hipStream_t s);
+int *async_sticky(int device, hipStream_t s);
+
+// scratch: null, or 2 kLargeCap uint4 records per query (k > kSortCap)
 void launch_final_select(const Cand *cand, const int *cand_count, int cand_cap, int nq, int k,
                          int metric, int64_t chunk_rows, int64_t id_offset, int64_t *out_ids,
-                         float *out_dist, int *overflow, hipStream_t s);
+                         float *out_dist, int *overflow, uint4 *scratch, hipStream_t s);
+// scratch: 2 nshards k uint4 records per query when nshards k > kSortCap
 void launch_merge_shards(int nshards, int nq, int k, int metric, const int64_t *in_ids,
                          const float *in_dist, int64_t *out_ids, float *out_dist, bool part_merge,
-                         hipStream_t s);
+                         uint4 *scratch, hipStream_t s);
 void launch_normalize_rows(float *rows, int64_t n, int d, hipStream_t s);
 void launch_row_norms(const float *rows, int64_t n, int d, float *norms, hipStream_t s);
 void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, float *qvars,
@@ -335,7 +346,7 @@ void launch_refine(const Cand *cin, const int *cnt_in, int cap, int nq, int k, i
                    hipStream_t s);
 void launch_rerank_select(const ScanParams &p, int metric, const float *bq, int k,
                           int64_t id_offset, int64_t *out_ids, float *out_dist, int *overflow,
-                          hipStream_t s);
+                          uint4 *scratch, hipStream_t s);
 
 // ---------------------------------------------------------------------------
 // Index path (kernels_ivf.hip, index.hip)

@@ -233,6 +233,59 @@ __device__ inline void block_bitonic_sort(uint4 *recs, int N) {
     }
 }
 
+// ---------------------------------------------------------------------------
+// Large result sets (k above kSortCap, up to kMaxK; shard merges of more than
+// kSortCap records): the records live in a global scratch of the query; runs
+// of kSortCap are sorted in LDS by the bitonic network above, then merged in
+// passes of doubling width.  Every record's key is unique (it ends with the
+// row / list position), so a record's place in the merged run is its place
+// in its own run plus the count of smaller records in the partner run (a
+// binary search) -- no two records ever claim the same slot.
+__device__ inline int count_less(const uint4 *a, int n, const uint4 &e) {
+    int lo = 0, hi = n;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if (rec_less(a[mid], e))
+            lo = mid + 1;
+        else
+            hi = mid;
+    }
+    return lo;
+}
+
+// Sorts g[0, m) (tmp: m more records of scratch); recs: kSortCap records of
+// LDS.  Returns the buffer that holds the sorted records (g or tmp).
+__device__ inline uint4 *global_sort(uint4 *g, uint4 *tmp, int m, uint4 *recs) {
+    for (int r0 = 0; r0 < m; r0 += kSortCap) {
+        const int len = m - r0 < kSortCap ? m - r0 : kSortCap;
+        int N = 1;
+        while (N < len) N <<= 1;
+        for (int i = threadIdx.x; i < N; i += SEL_THREADS)
+            recs[i] = i < len ? g[r0 + i] : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        __syncthreads();
+        block_bitonic_sort(recs, N);
+        for (int i = threadIdx.x; i < len; i += SEL_THREADS) g[r0 + i] = recs[i];
+        __syncthreads();
+    }
+    uint4 *src = g, *dst = tmp;
+    for (int w = kSortCap; w < m; w *= 2) {
+        for (int i = threadIdx.x; i < m; i += SEL_THREADS) {
+            const int base = i / (2 * w) * (2 * w);
+            const int a1 = base + w < m ? base + w : m;
+            const int b1 = base + 2 * w < m ? base + 2 * w : m;
+            const uint4 e = src[i];
+            const int pos = i < a1 ? (i - base) + count_less(src + a1, b1 - a1, e)
+                                   : (i - a1) + count_less(src + base, a1 - base, e);
+            dst[base + pos] = e;
+        }
+        __syncthreads();
+        uint4 *t = src;
+        src = dst;
+        dst = t;
+    }
+    return src;
+}
+
 __device__ inline float key_to_value(int metric, uint32_t k1) {
     // inverse of ord_asc / ~ord_asc
     uint32_t u = (metric == MQVS_METRIC_IP || metric == kMetricIpRaw) ? ~k1 : k1;

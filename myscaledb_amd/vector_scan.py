@@ -27,7 +27,8 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import F_ASYNC, F_DEVICE_PTRS, F_NO_CHECKSUM, F_PART_MERGE, METRICS, check, lib
+from ._lib import (F_ASYNC, F_DEVICE_PTRS, F_EXACT, F_GATHER_ALWAYS, F_GATHER_NEVER, F_NO_CHECKSUM,
+                   F_PART_MERGE, F_TIMING, METRICS, check, lib)
 
 FLT_MAX = np.float32(3.4028235e38)
 FLT_MIN = np.float32(1.1754944e-38)
@@ -157,15 +158,22 @@ class VectorScanSegment:
         return p.value
 
     def search(self, queries, k, metric=None, filter_bitmap=None, row_exists=None, out=None,
-               async_=False, stream=None, ord_base=None):
+               async_=False, stream=None, ord_base=None, exact=False, gather=None, timing=False):
         """Raw mqvs_search: (ids[nq,k] int64, dist[nq,k] float32), -1 padded.
         ord_base: cosine chunk-ordinal base of a row-range shard
-        (mqvs_search_ex; None = every earlier chunk searched)."""
+        (mqvs_search_ex; None = every earlier chunk searched).
+        Per-call path flags (same bits on every path): exact=True scans every
+        row in fp32 (MQVS_F_EXACT); gather=False / True forces the masked /
+        gathered PREWHERE scan; timing=True fills the stats' kernel times.
+        async_=True (device tensors): returns before the stream drains; check
+        the outcome with async_check()."""
         m = self.metric if metric is None else metric_id(metric)
         base = -1 if ord_base is None else int(ord_base)
+        extra = (F_EXACT if exact else 0) | (F_TIMING if timing else 0) | \
+            (0 if gather is None else F_GATHER_ALWAYS if gather else F_GATHER_NEVER)
 
         def call(qp, nq, fp, ep, ip, dp, flags, st):
-            check(lib.mqvs_search_ex(self._h, qp, nq, k, m, fp, ep, base, ip, dp, flags, st))
+            check(lib.mqvs_search_ex(self._h, qp, nq, k, m, fp, ep, base, ip, dp, flags | extra, st))
 
         if _is_torch(queries):
             import torch
@@ -378,6 +386,13 @@ def generate_device(seed, mode, row0, n, d, out_tensor, stream=None):
                                    ctypes.c_void_p(stream) if stream else None))
 
 
+def async_check(stream=None):
+    """mqvs_async_check: raises MqvsError(LOGICAL_ERROR) when one of this
+    thread's async searches since the last check needed a host-driven
+    fallback (its results are invalid: repeat it without async_)."""
+    check(lib.mqvs_async_check(ctypes.c_void_p(stream) if stream else None))
+
+
 def set_timing(enabled: bool):
     check(lib.mqvs_set_timing(1 if enabled else 0))
 
@@ -390,9 +405,9 @@ def set_gather_mode(mode: int):
 
 
 def set_prefilter(split: int):
-    """Pre-filter planes of segments created after the call: 6 = bf16 hi +
-    block-scaled fp6 cross plane (default), 3 = bf16 hi + lo planes
-    (mqvs_set_prefilter).  Both return the same bits."""
+    """Pre-filter planes of segments created after the call: 2 = bf16 hi
+    plane only (default), 6 = bf16 hi + block-scaled fp6 cross plane, 3 = bf16
+    hi + lo planes (mqvs_set_prefilter).  All return the same bits."""
     check(lib.mqvs_set_prefilter(int(split)))
 
 

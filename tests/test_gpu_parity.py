@@ -176,7 +176,7 @@ def test_gpu_vs_oracle_split3_prefilter(mq, cfg):
     try:
         run_parity(mq, cfg)
     finally:
-        set_prefilter(6)
+        set_prefilter(2)
 
 
 def _wide_range_part(seed, n, d, nq, near):
@@ -212,7 +212,7 @@ def test_prefilter_wide_dynamic_range(mq, split, metric, nq):
         ids_g, dist_g = seg.search(q, 50, metric)
         seg.free()
     finally:
-        set_prefilter(6)
+        set_prefilter(2)
     assert_bitwise(ids_g, dist_g, ids_o, dist_o, f"wide split={split} {metric} nq={nq}")
 
 
@@ -415,15 +415,26 @@ def test_merge_parts_mode_matches_oracle(mq, metric):
 
 
 def test_path_selection(mq):
-    """nq < 8: VALU direct formula (path 0); nq >= 8: bf16 pre-filter (path 2);
-    batch mode 1: exact kernels only (VALU below 20, fp32 MFMA from 20)."""
+    """Default (bf16-hi planes, split 2): the bf16 pre-filter serves every
+    batch size (path 2; it streams half the bytes of the fp32 rows).  Split-6 /
+    split-3 segments: nq < 8 VALU direct formula (path 0), nq >= 8 path 2.
+    Batch mode 1: exact kernels only (VALU below 20, fp32 MFMA from 20)."""
     from myscaledb_amd import _lib
-    from myscaledb_amd.vector_scan import set_batch_mode
+    from myscaledb_amd.vector_scan import set_batch_mode, set_prefilter
     rows = O.generate(3, 1, 0, 4000, 64)
     seg = mq.VectorScanSegment.from_rows(rows, metric="L2", granule=512)
+    set_prefilter(6)
     try:
-        for nq, want in ((7, 0), (8, 2), (19, 2), (20, 2)):
+        seg6 = mq.VectorScanSegment.from_rows(rows, metric="L2", granule=512)
+    finally:
+        set_prefilter(2)
+    try:
+        for nq in (1, 7, 8, 20):
             seg.search(O.generate(4, 1, 0, nq, 64), 10)
+            st = _lib.last_search_stats()
+            assert st["path"] == 2 and st["prefilter"] == 2, nq
+        for nq, want in ((7, 0), (8, 2), (19, 2), (20, 2)):
+            seg6.search(O.generate(4, 1, 0, nq, 64), 10)
             assert _lib.last_search_stats()["path"] == want, nq
         set_batch_mode(1)
         for nq, want in ((8, 0), (19, 0), (20, 1)):
@@ -432,6 +443,7 @@ def test_path_selection(mq):
     finally:
         set_batch_mode(0)
         seg.free()
+        seg6.free()
 
 
 @pytest.mark.parametrize("nq", [1, 9, 24])
@@ -470,7 +482,7 @@ def test_prefilter_no_exact_fallback(mq, split):
             finally:
                 seg.free()
     finally:
-        set_prefilter(6)
+        set_prefilter(2)
 
 
 @pytest.mark.parametrize("nq", [3, 12, 40])

@@ -40,7 +40,7 @@ def main():
         if any(v.startswith(kind + ":") or (kind == "bf" and ":" not in v) for v in variants):
             set_prefilter(split)
             segs[kind] = mq.VectorScanSegment.generate(0x5EED0001, 2, args.n, args.d, "Cosine", 8192)
-    set_prefilter(6)
+    set_prefilter(2)
     q = torch.empty((args.nq, args.d), dtype=torch.float32, device="cuda")
     generate_device(0x5EED0002, 2, 0, args.nq, args.d, q)
     ref = None
