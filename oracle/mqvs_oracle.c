@@ -15,6 +15,7 @@
 #include <string.h>
 
 #ifdef _OPENMP
+#include <immintrin.h>
 #include <omp.h>
 #endif
 
@@ -238,6 +239,51 @@ static void seq_block_dist(const float *xi, const float *y, int64_t d,
     for (int64_t r = 0; r < rows; r++) out[r] = acc[r];
 }
 
+/* BLAS-branch register-blocked micro-kernel (CPU-baseline timing only;
+ * bench.py cpu_baseline): 6 rows x 64 queries of accumulators in 24 zmm
+ * registers, one k step = 4 query loads + 24 fused multiply-adds with the
+ * row element broadcast.  Each (query, row) accumulator is still ONE fp32
+ * fma chain over k in ascending order -- the exact arithmetic of orc_gemm_dot
+ * and of the scalar loop below -- so results stay bit-identical; only the
+ * blocking changes.  xt: queries in blocks of 64, each block transposed and
+ * contiguous ([nxp / 64][d][64]: the k loop streams one block sequentially). */
+#define MK_R 6
+#define MK_Q 64
+__attribute__((target("avx512f"))) static void blas_block_avx512(const float *xt, int64_t nxp, int64_t q0,
+                                                                 const float *const *yr, int64_t d,
+                                                                 float out[MK_R][MK_Q]) {
+    __m512 a[MK_R][4];
+    for (int r = 0; r < MK_R; r++)
+        for (int v = 0; v < 4; v++) a[r][v] = _mm512_setzero_ps();
+    (void)nxp;
+    const float *xb = xt + q0 * d;  /* block q0 / 64: [d][64] */
+    for (int64_t kk = 0; kk < d; kk++) {
+        const float *xk = xb + kk * MK_Q;
+        const __m512 x0 = _mm512_loadu_ps(xk), x1 = _mm512_loadu_ps(xk + 16), x2 = _mm512_loadu_ps(xk + 32),
+                     x3 = _mm512_loadu_ps(xk + 48);
+        for (int r = 0; r < MK_R; r++) {
+            const __m512 yv = _mm512_set1_ps(yr[r][kk]);
+            a[r][0] = _mm512_fmadd_ps(x0, yv, a[r][0]);
+            a[r][1] = _mm512_fmadd_ps(x1, yv, a[r][1]);
+            a[r][2] = _mm512_fmadd_ps(x2, yv, a[r][2]);
+            a[r][3] = _mm512_fmadd_ps(x3, yv, a[r][3]);
+        }
+    }
+    for (int r = 0; r < MK_R; r++)
+        for (int v = 0; v < 4; v++) _mm512_storeu_ps(out[r] + 16 * v, a[r][v]);
+}
+
+static int use_avx512(void) {
+    static int v = -1;
+    if (v < 0) {
+        const char *e = getenv("ORC_NO_AVX512");
+        v = (e && e[0] == '1') ? 0 : __builtin_cpu_supports("avx512f");
+    }
+    return v;
+}
+
+int orc_has_avx512(void) { return use_avx512(); }
+
 int orc_knn_fast(const float *x, const float *y, int64_t d, int64_t k,
                  int64_t nx, int64_t ny, int metric, int64_t *ids, float *dist) {
     if (metric != ORC_L2 && metric != ORC_IP) return -1;
@@ -247,19 +293,26 @@ int orc_knn_fast(const float *x, const float *y, int64_t d, int64_t k,
     for (int64_t i = 0; i < nx; i++) heap_heapify(is_max, k, dist + i * k, ids + i * k);
     float *buf = (float *)malloc(sizeof(float) * FB_ROWS * (nx > 0 ? nx : 1));
     float *x_norms = NULL, *xt = NULL;
+    const int mk = blas && use_avx512();
     if (blas) {
-        /* queries transposed [d][nx_pad] so a block of FB_Q queries is
-         * contiguous for each k */
-        const int64_t nxp = (nx + FB_Q - 1) / FB_Q * FB_Q;
+        /* queries transposed [d][nx_pad] so a block of FB_Q (MK_Q with the
+         * micro-kernel) queries is contiguous for each k */
+        const int64_t qa = mk ? MK_Q : FB_Q;
+        const int64_t nxp = (nx + qa - 1) / qa * qa;
         xt = (float *)calloc((size_t)d * nxp, sizeof(float));
-        for (int64_t i = 0; i < nx; i++)
-            for (int64_t kk = 0; kk < d; kk++) xt[kk * nxp + i] = x[i * d + kk];
+        if (mk) {
+            for (int64_t i = 0; i < nx; i++)
+                for (int64_t kk = 0; kk < d; kk++) xt[((i / MK_Q) * d + kk) * MK_Q + i % MK_Q] = x[i * d + kk];
+        } else {
+            for (int64_t i = 0; i < nx; i++)
+                for (int64_t kk = 0; kk < d; kk++) xt[kk * nxp + i] = x[i * d + kk];
+        }
         if (metric == ORC_L2) {
             x_norms = (float *)malloc(sizeof(float) * nx);
             for (int64_t i = 0; i < nx; i++) x_norms[i] = orc_norm_l2sqr(x + i * d, d);
         }
     }
-    const int64_t nxp = (nx + FB_Q - 1) / FB_Q * FB_Q;
+    const int64_t nxp = mk ? (nx + MK_Q - 1) / MK_Q * MK_Q : (nx + FB_Q - 1) / FB_Q * FB_Q;
     for (int64_t j0 = 0; j0 < ny; j0 += FB_ROWS) {
         const int64_t rows = (ny - j0) < FB_ROWS ? (ny - j0) : FB_ROWS;
         const float *yb = y + j0 * d;
@@ -270,6 +323,24 @@ int orc_knn_fast(const float *x, const float *y, int64_t d, int64_t k,
             float y_norms[FB_ROWS];
             if (metric == ORC_L2)
                 for (int64_t r = 0; r < rows; r++) y_norms[r] = orc_norm_l2sqr(yb + r * d, d);
+            if (mk) {
+                float out[MK_R][MK_Q];
+                for (int64_t q0 = 0; q0 < nx; q0 += MK_Q)
+                    for (int64_t r0 = 0; r0 < rows; r0 += MK_R) {
+                        const float *yr[MK_R];
+                        for (int r = 0; r < MK_R; r++) yr[r] = yb + (r0 + r < rows ? r0 + r : r0) * d;
+                        blas_block_avx512(xt, nxp, q0, yr, d, out);
+                        for (int r = 0; r < MK_R && r0 + r < rows; r++)
+                            for (int qq = 0; qq < MK_Q && q0 + qq < nx; qq++) {
+                                float dis = out[r][qq];
+                                if (metric == ORC_L2) {
+                                    dis = (x_norms[q0 + qq] + y_norms[r0 + r]) - 2.0f * out[r][qq];
+                                    if (dis < 0) dis = 0;
+                                }
+                                buf[(q0 + qq) * FB_ROWS + r0 + r] = dis;
+                            }
+                    }
+            } else
             for (int64_t q0 = 0; q0 < nx; q0 += FB_Q) {
                 for (int64_t r = 0; r < rows; r++) {
                     float acc[FB_Q];
@@ -560,6 +631,42 @@ void orc_merge_parts(int64_t nparts, int64_t k, int metric,
         out_dist[i] = s->score;
     }
     free(e);
+}
+
+/* ------------------------------------------------------------------------ */
+/* STREAM triad a = b + s c over doubles (McCalpin's kernel and byte count:
+ * 24 B per element), `threads` OpenMP threads, best of `reps`; returns GB/s.
+ * Host DRAM bandwidth beside the CPU-baseline timing. */
+double orc_stream_triad(int64_t n, int threads, int reps) {
+    double *a = (double *)malloc(sizeof(double) * n), *b = (double *)malloc(sizeof(double) * n),
+           *c = (double *)malloc(sizeof(double) * n);
+    if (!a || !b || !c) {
+        free(a);
+        free(b);
+        free(c);
+        return -1.0;
+    }
+#pragma omp parallel for num_threads(threads) schedule(static)
+    for (int64_t i = 0; i < n; i++) {
+        a[i] = 0.0;
+        b[i] = 1.0;
+        c[i] = 2.0;
+    }
+    double best = 0.0;
+    for (int r = 0; r < reps; r++) {
+        const double t0 = omp_get_wtime();
+#pragma omp parallel for num_threads(threads) schedule(static)
+        for (int64_t i = 0; i < n; i++) a[i] = b[i] + 3.0 * c[i];
+        const double t = omp_get_wtime() - t0;
+        const double gbs = 24.0 * (double)n / t / 1e9;
+        if (gbs > best) best = gbs;
+    }
+    volatile double sink = a[n / 2];
+    (void)sink;
+    free(a);
+    free(b);
+    free(c);
+    return best;
 }
 
 /* ------------------------------------------------------------------------ */

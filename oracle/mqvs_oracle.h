@@ -93,6 +93,10 @@ int orc_vector_scan_fast(const float *rows, const uint8_t *nonempty, int64_t n,
  * parts at a time (MergeTreeSelectWithHybridSearchProcessor.cpp:1212-1241),
  * then the cross-part top-k merge (MergeTreeBaseSearchManager.cpp:207-297).
  * Uniform granularity `granule` rows.  Returns 0. */
+/* CPU-baseline helpers: AVX-512 micro-kernel in use by orc_knn_fast (runtime
+ * CPU check; ORC_NO_AVX512=1 disables it), STREAM triad GB/s. */
+int orc_has_avx512(void);
+double orc_stream_triad(int64_t n, int threads, int reps);
 int orc_scan_parts(const float *rows, int64_t n, int64_t d, int64_t granule,
                    const float *queries, int64_t nq, int64_t k, int metric,
                    int parts, int threads, int64_t *out_ids, float *out_dist);

@@ -243,6 +243,18 @@ def scan_parts(rows, queries, k, metric, granule, parts, threads):
     return ids, dist
 
 
+def has_avx512() -> bool:
+    return bool(lib().orc_has_avx512())
+
+
+def stream_triad(n=1 << 26, threads=1, reps=5) -> float:
+    """STREAM triad GB/s (doubles, 24 B per element) on `threads` threads."""
+    f = lib().orc_stream_triad
+    f.restype = ctypes.c_double
+    f.argtypes = [ctypes.c_int64, ctypes.c_int, ctypes.c_int]
+    return float(f(n, threads, reps))
+
+
 def merge_parts(labels, dists, metric):
     labels = np.ascontiguousarray(labels, np.int64)
     dists = _f32(dists)

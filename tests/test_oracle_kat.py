@@ -54,3 +54,20 @@ def test_oracle_hamming_knn_contract():
     ids, dist = O.knn_binary(x, y, 6, O.JACCARD)
     assert ids.tolist() == [[0, 1, 2, 3, 4, -1]]  # num == 0 -> 1.0 for every row
     assert dist[0, :5].tolist() == [1.0] * 5
+
+
+def test_fast_blas_microkernel_bit_identical():
+    """The CPU baseline's register-blocked AVX-512 micro-kernel (orc_knn_fast,
+    BLAS branch, nq >= 20) returns the scalar orc_knn's bits: every element is
+    still one ascending fp32 fma chain."""
+    import numpy as np
+    from oracle import oracle as O
+    rng = np.random.default_rng(17)
+    for nx, ny, d in ((20, 700, 7), (33, 513, 64), (64, 300, 96), (130, 257, 768)):
+        x = rng.standard_normal((nx, d)).astype(np.float32)
+        y = rng.standard_normal((ny, d)).astype(np.float32)
+        for metric in (O.L2, O.IP):
+            a = O.knn(x, y, 17, metric)
+            b = O.knn(x, y, 17, metric, fast=True)
+            assert np.array_equal(a[0], b[0]) and np.array_equal(a[1].view(np.uint32), b[1].view(np.uint32)), \
+                (nx, ny, d, metric, O.has_avx512())
