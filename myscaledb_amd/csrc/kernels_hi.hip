@@ -588,22 +588,21 @@ __global__ __launch_bounds__(512) void k_scan_hi_pp(ScanParams p, int slots) {
         if (++sc == nst) {
             // item epilogue: values over the threshold -> LDS queue.  A
             // candidate is rare (a few per item and query block), so each
-            // query column is first tested with ONE compare of the max of its
-            // 32 values (v_max3 chains); only a column over its threshold
-            // walks its values (the per-value branches cost 4 ms at
-            // 10M x 768, nq 1000, as much as the LDS-DMA stream)
+            // block of 16 values of a query column is first tested with ONE
+            // compare of their max (v_max3 chains); only a block over the
+            // threshold walks its values (per-value branches everywhere cost
+            // 4 ms at 10M x 768, nq 1000, as much as the LDS-DMA stream; a
+            // ballot-compacted walk measured slower than this one)
             if (!(DIAG & 16)) {
 #pragma unroll
-                for (int jb = 0; jb < QB; ++jb) {
-                    float mx = acc[0][jb][0];
+                for (int jb = 0; jb < QB; ++jb)
 #pragma unroll
-                    for (int rb = 0; rb < 2; ++rb)
+                    for (int rb = 0; rb < 2; ++rb) {
+                        float mx = acc[rb][jb][0];
 #pragma unroll
-                        for (int r = 0; r < 16; ++r) mx = fmaxf(mx, acc[rb][jb][r]);
-                    if (mx >= thr[jb]) {
-                        const int j = q0 + rq0 + jb * 32;
-#pragma unroll
-                        for (int rb = 0; rb < 2; ++rb) {
+                        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[rb][jb][r]);
+                        if (mx >= thr[jb]) {
+                            const int j = q0 + rq0 + jb * 32;
                             const int64_t rbase = cr0 + wr * 64 + rb * 32 + 4 * h;
 #pragma unroll
                             for (int r = 0; r < 16; ++r) {
@@ -611,16 +610,14 @@ __global__ __launch_bounds__(512) void k_scan_hi_pp(ScanParams p, int slots) {
                                 const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
                                 if (raw >= thr[jb] && row < cr1 && j < p.nq) {
                                     const int pos = lds_add_rtn(&qcount, 1);
-                                    if (pos < kPpQueue) {
+                                    if (pos < kPpQueue)
                                         lds_store_b128(queue + pos, raw, (uint32_t)row, j);
-                                    } else {
+                                    else
                                         emit_approx<METRIC, false>(p, j, row, row, row_valid(p, row), raw);
-                                    }
                                 }
                             }
                         }
                     }
-                }
             }
             if (DIAG & 16) {
                 float sum = 0.f;
