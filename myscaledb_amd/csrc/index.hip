@@ -534,18 +534,31 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
 
     // ---- query prep: cosine re-normalisation variants (the re-rank uses the
     // row's chunk variant, as mqvs_search does), |q|^2
-    const int maxv = cos ? kMaxVariants : 1;
+    // (a part with more chunks than kMaxVariants whose chains did not repeat
+    // gets one variant per chunk ordinal, as in mqvs_search: one host sync)
+    const int64_t ords = seg->row_offset / seg->granule + (seg->n + seg->granule - 1) / seg->granule;
+    const bool may_sync = !(dev && (flags & MQVS_F_ASYNC)) && !first_stage;
+    int maxv = cos ? kMaxVariants : 1;
     const int64_t qstride = rup(d, 32);
-    float *qvars = (float *)ws.qvars.get(sizeof(float) * (size_t)nq * maxv * qstride);
-    MQVS_HIP(hipMemsetAsync(qvars, 0, sizeof(float) * (size_t)nq * maxv * qstride, s));
+    float *qvars = nullptr;
     float *qnorms = (float *)ws.qnorms.get(sizeof(float) * nq);
     int *qmu = (int *)ws.qmu.get(sizeof(int) * nq);
     int *qlam = (int *)ws.qlam.get(sizeof(int) * nq);
     int *status = (int *)ws.status.get(sizeof(int) * 4);
-    MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
-    launch_query_prep(dq, nq, d, cos ? MQVS_METRIC_COSINE : MQVS_METRIC_L2, ix->metric == MQVS_METRIC_L2, qvars,
-                      qnorms, qmu, qlam, status, s);
-    MQVS_HIP(hipGetLastError());
+    for (int pass = 0; pass < 2; ++pass) {
+        qvars = (float *)ws.qvars.get(sizeof(float) * (size_t)nq * maxv * qstride);
+        MQVS_HIP(hipMemsetAsync(qvars, 0, sizeof(float) * (size_t)nq * maxv * qstride, s));
+        MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
+        launch_query_prep(dq, nq, d, cos ? MQVS_METRIC_COSINE : MQVS_METRIC_L2, ix->metric == MQVS_METRIC_L2, qvars,
+                          maxv, qnorms, qmu, qlam, status, s);
+        MQVS_HIP(hipGetLastError());
+        if (pass > 0 || !cos || ords <= maxv || !may_sync) break;
+        int hs = 0;
+        MQVS_HIP(hipMemcpyAsync(&hs, status, sizeof(int), hipMemcpyDeviceToHost, s));
+        MQVS_HIP(hipStreamSynchronize(s));
+        if (!hs) break;
+        maxv = (int)std::min<int64_t>(ords, kMaxVariantsCap);
+    }
     uint16_t *qhi = (uint16_t *)ws.qhi.get(sizeof(uint16_t) * (size_t)nq * ix->dpad);
     launch_to_bf16(qvars, nq, d, (int64_t)maxv * qstride, qhi, nullptr, ix->dpad, s);
     MQVS_HIP(hipGetLastError());
@@ -606,9 +619,7 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
 
     const bool async = dev && (flags & MQVS_F_ASYNC);
     if (async) {
-        const bool variants_matter =
-            !first_stage &&
-            (int64_t)(seg->row_offset / seg->granule) + (seg->n + seg->granule - 1) / seg->granule > kMaxVariants;
+        const bool variants_matter = !first_stage && ords > maxv;
         launch_async_flags(nullptr, status, variants_matter ? 1 : 0, async_sticky(seg->device, s), s);
         MQVS_HIP(hipGetLastError());
         return;
@@ -618,9 +629,8 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     int hstatus = 0;
     MQVS_HIP(hipMemcpyAsync(&hstatus, status, sizeof(int), hipMemcpyDeviceToHost, s));
     MQVS_HIP(hipStreamSynchronize(s));
-    if (hstatus && !first_stage &&
-        (int64_t)(seg->row_offset / seg->granule) + (seg->n + seg->granule - 1) / seg->granule > kMaxVariants)
-        fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not repeat within " + std::to_string(kMaxVariants) +
+    if (hstatus && !first_stage && ords > maxv)
+        fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not repeat within " + std::to_string(maxv) +
                                    " steps on a part of more chunks");
     if (!dev) {
         MQVS_HIP(hipMemcpyAsync(out_ids, dids, sizeof(int64_t) * (size_t)nq * k, hipMemcpyDeviceToHost, s));

@@ -154,7 +154,7 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
     // fixed point reached at the last stored variant is still detected.  A
     // repeat is found by a 64-bit signature of each variant (wave-reduced in
     // registers); only a signature match is confirmed element by element.
-    __shared__ uint64_t sig[kMaxVariants + 1];
+    extern __shared__ uint64_t sig[];  // maxv + 1 signatures
     for (int v = 0; v <= maxv; ++v) {
         const float sum = seq_sq_sum<J>(x, d);
         if (!(sum < eps)) {
@@ -279,12 +279,13 @@ __global__ __launch_bounds__(64) void k_query_prep_lds(const float *q, int nq, i
     }
 }
 
-void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, float *qvars,
+void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, float *qvars, int maxv,
                        float *qnorms, int *qmu, int *qlam, int *status, hipStream_t s) {
-    const int maxv = metric == MQVS_METRIC_COSINE ? kMaxVariants : 1;
+    if (metric != MQVS_METRIC_COSINE) maxv = 1;
     const size_t lds = (size_t)((d + 31) / 32 * 32 + 4) * sizeof(float);
-#define MQVS_QP(J)                                                                                             \
-    hipLaunchKernelGGL(k_query_prep<J>, dim3(nq), dim3(64), 0, s, q, nq, d, metric, blas ? 1 : 0, qvars, maxv,   \
+    const size_t sig = (size_t)(maxv + 1) * sizeof(uint64_t);
+#define MQVS_QP(J)                                                                                               \
+    hipLaunchKernelGGL(k_query_prep<J>, dim3(nq), dim3(64), sig, s, q, nq, d, metric, blas ? 1 : 0, qvars, maxv, \
                        qnorms, qmu, qlam, status)
     if (d <= 128)
         MQVS_QP(2);

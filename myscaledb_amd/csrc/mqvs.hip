@@ -246,6 +246,42 @@ static void run_scan(ScanParams p, const Range &r, int kind, int metric, bool pr
 
 static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 
+// Query variants.  Cosine re-normalises the query once per searched chunk
+// (VIWithDataPart.h:358, the query object shared across chunks); the chain
+// x, x/|x|, ... is stored until it repeats (mu, lambda per query).  The
+// default table of kMaxVariants covers the chains of typical data (Gaussian
+// and mixture parts repeat within ~15 steps).  When a part has more chunk
+// ordinals than that and some chain did not repeat (small-integer vectors
+// wander for hundreds of steps), the table is rebuilt with one variant per
+// ordinal (up to kMaxVariantsCap) -- one host sync, only on such parts.
+// Returns maxv; ASYNC calls cannot sync and keep the default table (their
+// outcome goes to mqvs_async_check).
+static int prep_variants(Workspace &ws, const float *dq, int nq, int d, bool cos, bool l2norms, int64_t ords,
+                         bool may_sync, float *&qvars, float *&qnorms, int *&qmu, int *&qlam, int *&status,
+                         hipStream_t s) {
+    const int64_t qstride = round_up(d, 32);
+    qnorms = (float *)ws.qnorms.get(sizeof(float) * nq);
+    qmu = (int *)ws.qmu.get(sizeof(int) * nq);
+    qlam = (int *)ws.qlam.get(sizeof(int) * nq);
+    status = (int *)ws.status.get(sizeof(int) * 4);
+    int maxv = cos ? kMaxVariants : 1;
+    for (int pass = 0; pass < 2; ++pass) {
+        const size_t bytes = sizeof(float) * (size_t)nq * maxv * qstride;
+        qvars = (float *)ws.qvars.get(bytes);
+        MQVS_HIP(hipMemsetAsync(qvars, 0, bytes, s));
+        MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
+        launch_query_prep(dq, nq, d, cos ? MQVS_METRIC_COSINE : MQVS_METRIC_L2, l2norms, qvars, maxv, qnorms, qmu,
+                          qlam, status, s);
+        MQVS_HIP(hipGetLastError());
+        if (pass > 0 || !cos || ords <= maxv || !may_sync) break;
+        MQVS_HIP(hipMemcpyAsync(ws.host_flags + 12, status, sizeof(int), hipMemcpyDeviceToHost, s));
+        MQVS_HIP(hipStreamSynchronize(s));
+        if (!ws.host_flags[12]) break;
+        maxv = (int)std::min<int64_t>(ords, kMaxVariantsCap);
+    }
+    return maxv;
+}
+
 // metric: public metric, or kMetricIpRaw for the faiss-contract entry point
 static std::atomic<int> g_batch_mode{0};   // 0: bf16 pre-filter + exact re-rank when possible, 1: fp32 MFMA
 static std::atomic<int> g_gather_mode{1};  // selective PREWHERE: 0 never gather, 1 when <= 60% selected, 2 always
@@ -405,19 +441,13 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     const int kind = bf16 ? kScanBf16 : !mfma ? kScanSmall : kScanMfma32;
 
     // ---- query prep
-    const int maxv = cos ? kMaxVariants : 1;
+    const int64_t ords = (ord_base >= 0 ? ord_base : seg->row_offset / seg->granule) +
+                         (n + seg->granule - 1) / seg->granule;
     const int64_t qstride = round_up(d, 32);
-    float *qvars = (float *)ws.qvars.get(sizeof(float) * (size_t)nq * maxv * qstride);
-    MQVS_HIP(hipMemsetAsync(qvars, 0, sizeof(float) * (size_t)nq * maxv * qstride, s));
-    float *qnorms = (float *)ws.qnorms.get(sizeof(float) * nq);
-    int *qmu = (int *)ws.qmu.get(sizeof(int) * nq);
-    int *qlam = (int *)ws.qlam.get(sizeof(int) * nq);
-    int *status = (int *)ws.status.get(sizeof(int) * 4);
-    MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
-    launch_query_prep(dq, nq, d, cos ? MQVS_METRIC_COSINE : MQVS_METRIC_L2,
-                      (mfma || bf16) && metric == MQVS_METRIC_L2,
-                      qvars, qnorms, qmu, qlam, status, s);
-    MQVS_HIP(hipGetLastError());
+    float *qvars = nullptr, *qnorms = nullptr;
+    int *qmu = nullptr, *qlam = nullptr, *status = nullptr;
+    const int maxv = prep_variants(ws, dq, nq, d, cos, (mfma || bf16) && metric == MQVS_METRIC_L2, ords,
+                                   !(dev && (flags & MQVS_F_ASYNC)), qvars, qnorms, qmu, qlam, status, s);
 
     // ---- chunk ordinals
     const int *chunk_ord = nullptr;
@@ -619,7 +649,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     const bool async = dev && (flags & MQVS_F_ASYNC);
     if (async) {
         // no host fallback possible: leave the outcome for mqvs_async_check
-        const bool variants_matter = p.ord_base + (n + seg->granule - 1) / seg->granule > kMaxVariants;
+        const bool variants_matter = ords > maxv;
         launch_async_flags(overflow, status, variants_matter ? 1 : 0, sticky_word(ws, s), s);
         MQVS_HIP(hipGetLastError());
     } else {
@@ -632,11 +662,12 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
             st.survivors_total = (uint32_t)ws.host_flags[5];
             st.candidates_max = ws.host_flags[6];
         }
-        // a query whose re-normalisation does not repeat within kMaxVariants
-        // steps is exact only on the part's first kMaxVariants chunk ordinals
-        if (ws.host_flags[1] && p.ord_base + (n + seg->granule - 1) / seg->granule > kMaxVariants)
-            fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not repeat within " +
-                                       std::to_string(kMaxVariants) + " steps on a part of more chunks");
+        // a query whose re-normalisation does not repeat within maxv steps is
+        // exact only on the part's first maxv chunk ordinals (maxv covers
+        // every ordinal unless the part has more than kMaxVariantsCap chunks)
+        if (ws.host_flags[1] && ords > maxv)
+            fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not repeat within " + std::to_string(maxv) +
+                                       " steps on a part of more chunks");
         if (kind == kScanBf16 && ws.host_flags[0]) {
             // the bf16 bound left too many candidates: exact fp32 path
             search_impl(seg, queries, nq, k, metric, filter, exists, out_ids, out_dist, flags,
@@ -742,18 +773,11 @@ static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const i
         ddist = (float *)ws.out_dist.get(sizeof(float) * (size_t)nq * k);
     }
     const bool blas = nq >= kBlasThreshold;
-    const int maxv = cos ? kMaxVariants : 1;
-    const int64_t qstride = round_up(d, 32);
-    float *qvars = (float *)ws.qvars.get(sizeof(float) * (size_t)nq * maxv * qstride);
-    MQVS_HIP(hipMemsetAsync(qvars, 0, sizeof(float) * (size_t)nq * maxv * qstride, s));
-    float *qnorms = (float *)ws.qnorms.get(sizeof(float) * nq);
-    int *qmu = (int *)ws.qmu.get(sizeof(int) * nq);
-    int *qlam = (int *)ws.qlam.get(sizeof(int) * nq);
-    int *status = (int *)ws.status.get(sizeof(int) * 4);
-    MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
-    launch_query_prep(dq, nq, d, cos ? MQVS_METRIC_COSINE : MQVS_METRIC_L2, blas && metric == MQVS_METRIC_L2,
-                      qvars, qnorms, qmu, qlam, status, s);
-    MQVS_HIP(hipGetLastError());
+    const int64_t ords = seg->row_offset / seg->granule + (seg->n + seg->granule - 1) / seg->granule;
+    float *qvars = nullptr, *qnorms = nullptr;
+    int *qmu = nullptr, *qlam = nullptr, *status = nullptr;
+    const int maxv = prep_variants(ws, dq, nq, d, cos, blas && metric == MQVS_METRIC_L2, ords,
+                                   !(dev && (flags & MQVS_F_ASYNC)), qvars, qnorms, qmu, qlam, status, s);
 
     ScanParams p{};
     p.rows = seg->rows;
@@ -774,15 +798,14 @@ static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const i
     launch_rerank_ids(p, metric, dc, ncand, k, seg->row_offset, dids, ddist, s);
     MQVS_HIP(hipGetLastError());
     if (dev && (flags & MQVS_F_ASYNC)) {
-        const bool variants_matter = p.ord_base + (seg->n + seg->granule - 1) / seg->granule > kMaxVariants;
-        launch_async_flags(nullptr, status, variants_matter ? 1 : 0, sticky_word(ws, s), s);
+        launch_async_flags(nullptr, status, ords > maxv ? 1 : 0, sticky_word(ws, s), s);
         MQVS_HIP(hipGetLastError());
         return;
     }
     MQVS_HIP(hipMemcpyAsync(ws.host_flags, status, sizeof(int), hipMemcpyDeviceToHost, s));
     MQVS_HIP(hipStreamSynchronize(s));
-    if (ws.host_flags[0] && p.ord_base + (seg->n + seg->granule - 1) / seg->granule > kMaxVariants)
-        fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not repeat within " + std::to_string(kMaxVariants) +
+    if (ws.host_flags[0] && ords > maxv)
+        fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not repeat within " + std::to_string(maxv) +
                                    " steps on a part of more chunks");
     if (!dev) {
         MQVS_HIP(hipMemcpyAsync(out_ids, dids, sizeof(int64_t) * (size_t)nq * k, hipMemcpyDeviceToHost, s));

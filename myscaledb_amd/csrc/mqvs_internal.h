@@ -43,7 +43,8 @@ namespace mqvs {
 // ---------------------------------------------------------------------------
 // Tunables
 constexpr int kBlasThreshold = 20;   // faiss distance_compute_blas_threshold
-constexpr int kMaxVariants = 32;     // cosine query re-normalisation variants kept
+constexpr int kMaxVariants = 32;     // cosine query re-normalisation variants kept (default table)
+constexpr int kMaxVariantsCap = 16384;  // one variant per chunk ordinal when a chain does not repeat
 constexpr int kSortCap = 4096;       // candidates sorted in LDS per query
 constexpr int kMaxK = 16384;         // largest k (max_search_result_window is 10000, Settings.h:923)
 constexpr int kLargeCap = 32768;     // records per query sorted through global scratch (k > kSortCap)
@@ -274,7 +275,8 @@ void launch_merge_shards(int nshards, int nq, int k, int metric, const int64_t *
                          uint4 *scratch, hipStream_t s);
 void launch_normalize_rows(float *rows, int64_t n, int d, hipStream_t s);
 void launch_row_norms(const float *rows, int64_t n, int d, float *norms, hipStream_t s);
-void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, float *qvars,
+// maxv: variants stored per query (1 unless cosine)
+void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, float *qvars, int maxv,
                        float *qnorms, int *qmu, int *qlam, int *status, hipStream_t s);
 void launch_generate(uint64_t seed, int mode, int64_t row0, int64_t n, int d, float *out,
                      hipStream_t s);

@@ -240,3 +240,27 @@ def test_async_overflow_is_reported(mq):
         _eq(ia.cpu().numpy(), da.cpu().numpy(), isy.cpu().numpy(), dsy.cpu().numpy(), "async vs sync")
     finally:
         seg2.free()
+
+
+@pytest.mark.parametrize("nq", [5, 24])
+def test_cosine_long_normalisation_chains(mq, nq):
+    """Small-integer queries whose fp32 re-normalisation chain does not repeat
+    within the default 32 variants (a third of them at d = 768) on a part of
+    60 granule chunks: the variant table grows to one per chunk ordinal and
+    the result equals the oracle's per-chunk re-normalisation bit for bit."""
+    n, d, k, gran = 60 * 64, 768, 40, 64
+    rows = O.generate(0x5EED0001, 0, 0, n, d)
+    q = O.generate(0x5EED0002, 0, 0, nq, d)
+    io, do = O.vector_scan(rows, q, k, O.COSINE, gran, fast=True)
+    seg = mq.VectorScanSegment.from_rows(rows, metric="Cosine", granule=gran)
+    try:
+        ig, dg = seg.search(q, k)
+        _eq(ig, dg, io, do, f"cosine long chains nq {nq}")
+        ie, de = seg.search(q, k, exact=True)
+        _eq(ie, de, io, do, f"cosine long chains nq {nq} exact")
+        # computeTopDistanceSubset over every row == the search
+        cand = np.tile(np.arange(n, dtype=np.int64)[None, :], (nq, 1))
+        ri, rd = seg.rerank(q, cand, k)
+        _eq(ri, rd, io, do, f"cosine long chains nq {nq} rerank")
+    finally:
+        seg.free()
