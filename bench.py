@@ -72,14 +72,24 @@ def verify_sample(O, ids, dist, q_host, args, n_probe_rows=20000):
     checked = 0
     for qi in (0, args.nq // 2):
         q = q_host[qi:qi + 1].copy()
-        variants = []
+        # cosine: the query re-normalised once per chunk (VIWithDataPart.h:358),
+        # the chain followed to its repeat (mu, lambda) or to the last chunk
+        variants, mu, lam = [], None, None
         if metric == O.COSINE:
-            v = q.copy()
-            for _ in range(16):
+            v, seen = q.copy(), {}
+            for step in range(-(-args.n // args.granule)):
                 v = O.normalize(v)
-                if variants and np.array_equal(v.view(np.uint32), variants[-1].view(np.uint32)):
+                key = v.tobytes()
+                if key in seen:
+                    mu, lam = seen[key], step - seen[key]
                     break
+                seen[key] = step
                 variants.append(v)
+
+        def variant(chunk):
+            if mu is None or chunk < mu:
+                return variants[min(chunk, len(variants) - 1)]
+            return variants[mu + (chunk - mu) % lam]
 
         def dist_of(rows_idx):
             rows = np.concatenate([O.generate(SEED_BASE, args.mode, int(r), 1, args.d)
@@ -88,7 +98,7 @@ def verify_sample(O, ids, dist, q_host, args, n_probe_rows=20000):
             for r, y in zip(rows_idx, rows):
                 if metric == O.COSINE:
                     yn = O.normalize(y[None, :])[0]
-                    qv = variants[min(int(r) // args.granule, len(variants) - 1)][0]
+                    qv = variant(int(r) // args.granule)[0]
                     ip = O.gemm_dot(qv, yn) if blas else O.inner_product(qv, yn)
                     out.append((np.float32(1.0) - np.float32(ip), ip))
                 elif metric == O.IP:

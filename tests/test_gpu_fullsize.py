@@ -180,17 +180,20 @@ def test_config2_index_10M_recall(mq):
 
 
 def test_config3_one_shard_ip_12p5M_x1536(mq):
-    """configs[3], one of the 8 row-range shards (rows [37.5M, 50M) of the
-    100M x 1536 part): IP, nq 1 / 16 / 1000, default path == exact path."""
-    n, d, k = 12_500_000, 1536, 100
-    seg = mq.VectorScanSegment.generate(SEED_BASE, 1, n, d, "IP", 8192, row_offset=3 * n)
+    """configs[3], one of the 8 row-range shards of the 100M x 1536 part (rank
+    3's granule-aligned range, ~12.5M rows): IP, nq 1 / 16 / 1000, default
+    path == exact path."""
+    from myscaledb_amd.sharded import shard_rows
+    d, k = 1536, 100
+    r0, r1 = shard_rows(100_000_000, 8192, 3, 8)  # granule-aligned row range of rank 3
+    seg = mq.VectorScanSegment.generate(SEED_BASE, 1, r1 - r0, d, "IP", 8192, row_offset=r0)
     try:
         for nq in (1, 16, 1000):
             q = _dev_queries(SEED_QUERY, 1, 0, nq, d)
             got, st, exact = _search_both(seg, q, k)
             assert st["rescans"] == 0, st
             _assert_same(got, exact, f"IP 12.5M x 1536 nq {nq}")
-            assert got[0].min() >= 3 * n
+            assert got[0].min() >= r0 and got[0].max() < r1
     finally:
         seg.free()
 
