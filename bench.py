@@ -306,7 +306,10 @@ def roofline(st, main_ms, nq, d, args):
         else:
             qt = 256 if nq > 128 else 128
             stream = 2.0 * rows * dp * -(-nq // qt) + 2.0 * nq * dp * -(-rows // 256)
-            roof = {"bound": "mfma", "kernel": "k_scan_hi<metric,APPEND,WQ=2,QB=4,NBUF=4> (bf16 32x32x16)",
+            kern = ("k_scan_hi_pp<metric,NBUF=4> (persistent ping-pong, bf16 32x32x16)"
+                    if st["path"] == 2 and args.metric != "L2" else
+                    "k_scan_hi<metric,APPEND,WQ=2,QB=4,NBUF=4> (bf16 32x32x16)")
+            roof = {"bound": "mfma", "kernel": kern,
                     "achieved": round(flop / sec / 1e12, 2), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(flop / sec / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4), "traffic": None,
                     "flop_definition": "executed bf16 MFMA flops = 2 * nq * rows * dpad (hi * hi)",
@@ -353,7 +356,8 @@ def roofline(st, main_ms, nq, d, args):
         want = {2: "k_scan_hi", 6: "k_scan_mx<", 3: "k_scan_bf16<"}.get(pf, "?")
         if pmc.get("nq") in (None, nq):
             for name, kinfo in pmc.get("kernels", {}).items():
-                if want in name and "false" in name and "hbm_bytes_per_search" in kinfo:
+                append = "false" in name or "_pp<" in name  # (the persistent kernel is APPEND only)
+                if want in name and append and "hbm_bytes_per_search" in kinfo:
                     roof["traffic"] = round(kinfo["hbm_bytes_per_search"])
                     roof["traffic_unit"] = "HBM bytes per search (all main-scan launches)"
                     roof["traffic_source"] = os.path.relpath(pmc_path, ROOT)
