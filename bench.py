@@ -464,8 +464,22 @@ def main():
         f_ids = torch.empty((nq, k), dtype=torch.int64, device="cuda")
         f_dst = torch.empty((nq, k), dtype=torch.float32, device="cuda")
     torch.cuda.synchronize()
+    # N > 1: libmqvs's own exchange (mqvs_sharded_search: RCCL all-gather of
+    # the per-shard top-k + device merge); torch.distributed's all_gather +
+    # mqvs_merge_shards if that communicator cannot be set up
+    comm, exchange = None, None
+    if dist_on:
+        try:
+            from myscaledb_amd.sharded import RcclComm
+            comm = RcclComm.from_process_group()
+            exchange = "mqvs_sharded_search (libmqvs RCCL all-gather + device merge)"
+        except Exception as e:  # noqa: BLE001
+            comm, exchange = None, f"torch.distributed all_gather + mqvs_merge_shards ({type(e).__name__})"
 
     def step():
+        if comm is not None:
+            comm.sharded_search(seg, q, k, out=(f_ids, f_dst))
+            return
         seg.search(q, k, out=(ids, dst))  # returns after its stream drained
         if dist_on:
             tdist.all_gather_into_tensor(g_ids, ids)
@@ -551,7 +565,8 @@ def main():
             "config": {"workload": f"FLAT {args.metric} {n // 1_000_000}M x {d} Float32, batch {nq}, "
                                    f"top-{k} (BASELINE configs[1])",
                        "n": n, "d": d, "nq": nq, "k": k, "metric": args.metric, "generator_mode": args.mode,
-                       "granule_rows": g, "parallelism": f"row-range shards x{world}"},
+                       "granule_rows": g, "parallelism": f"row-range shards x{world}",
+                       "exchange": exchange},
             "mdist_per_s": round(nq * n / (ms / 1000.0) / 1e6, 1),
             "recall_at_10": exact["recall_at_10"] if exact else None,
             "exact_check": exact,
@@ -570,6 +585,8 @@ def main():
         if not args.no_index and world == 1:
             result["index"] = index_leg(mq, seg, args)
         print(json.dumps(result), flush=True)
+    if comm is not None:
+        comm.free()
     seg.free()
     if dist_on:
         tdist.barrier()

@@ -239,6 +239,39 @@ int mqvs_search_binary(mqvs_segment_t seg, const uint8_t *queries, int32_t nq, i
 int mqvs_knn_binary_raw(const uint8_t *x, const uint8_t *y, int64_t d, int64_t k, int64_t nx, int64_t ny,
                         int32_t metric, int64_t *result_id, float *distance);
 
+/* ---- multi-GPU: one part sharded by row range over the GPUs of a node ----
+ * One rank per GPU (process or thread); rank r holds the granule-aligned row
+ * range [r0, r1) of the part as a segment created with row_offset = r0 (ids
+ * stay part-global).  The communicator is an RCCL one over xGMI:
+ *   mqvs_comm_unique_id  on ONE rank; ship the 128 bytes to the others out of
+ *                        band (the Distributed engine's channel, MPI, a file)
+ *   mqvs_comm_init       on every rank, with its device current (mqvs_init);
+ *                        blocks until all nranks have joined
+ *   mqvs_sharded_search  on every rank, same queries / k / metric: the local
+ *                        top-k of the rank's shard, ONE all-gather of the
+ *                        per-rank (id, distance) lists (nq*k*12 B per rank),
+ *                        and the device merge by (distance, rank, position);
+ *                        every rank gets the merged result, bit-identical to
+ *                        mqvs_search over the whole part.  filter / row_exists
+ *                        are the shard's bitmaps (its n bits).  Cosine: the
+ *                        ranks also all-gather how many granule chunks of
+ *                        their range the reference searches, which fixes each
+ *                        shard's query re-normalisation count (chunk-ordinal
+ *                        base) exactly, filters and deletes included.
+ * Replaces the cross-part / cross-shard merges of the reference
+ * (MergeTreeBaseSearchManager.cpp:207-297 getTotalTopSearchResultImpl; the
+ * Distributed engine's per-shard LIMIT + initiator merge,
+ * StorageDistributed.cpp:1057-1060) for one part spread over GPUs.  A
+ * communicator serves one search at a time. */
+#define MQVS_COMM_ID_BYTES 128
+typedef struct mqvs_comm *mqvs_comm_t;
+int mqvs_comm_unique_id(uint8_t *id /* MQVS_COMM_ID_BYTES */);
+int mqvs_comm_init(int32_t nranks, int32_t rank, const uint8_t *id, mqvs_comm_t *out);
+int mqvs_comm_free(mqvs_comm_t comm);
+int mqvs_sharded_search(mqvs_comm_t comm, mqvs_segment_t shard, const float *queries, int32_t nq, int32_t k,
+                        int32_t metric, const uint8_t *filter, const uint8_t *row_exists, int64_t *out_ids,
+                        float *out_dist, uint32_t flags, mqvs_stream_t stream);
+
 /* Fill a device buffer with generator rows [row0, row0+n) (for queries). */
 int mqvs_generate_device(uint64_t seed, int32_t mode, int64_t row0, int64_t n, int32_t d,
                          float *dev_out, mqvs_stream_t stream);

@@ -41,6 +41,7 @@ SYMBOLS = [
     "mqvs_index_build", "mqvs_index_free", "mqvs_index_info", "mqvs_index_search", "mqvs_index_last_stats",
     "mqvs_segment_create_binary", "mqvs_search_binary", "mqvs_knn_binary_raw",
     "mqvs_segment_create_from_column", "mqvs_async_check",
+    "mqvs_comm_unique_id", "mqvs_comm_init", "mqvs_comm_free", "mqvs_sharded_search",
 ]
 
 
@@ -128,6 +129,10 @@ def _load():
         "mqvs_knn_binary_raw": ([P, P, I64, I64, I64, I64, I32, P, P], ctypes.c_int),
         "mqvs_segment_create_from_column": ([P, I64, P, I64, I64, I32, I32, I64, I64, U32, P], ctypes.c_int),
         "mqvs_async_check": ([P], ctypes.c_int),
+        "mqvs_comm_unique_id": ([P], ctypes.c_int),
+        "mqvs_comm_init": ([I32, I32, P, P], ctypes.c_int),
+        "mqvs_comm_free": ([P], ctypes.c_int),
+        "mqvs_sharded_search": ([P, P, P, I32, I32, I32, P, P, P, P, U32, P], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

@@ -560,4 +560,29 @@ void launch_async_flags(const int *overflow, const int *status, int status_matte
     hipLaunchKernelGGL(k_async_flags, dim3(1), dim3(64), 0, s, overflow, status, status_matters, sticky);
 }
 
+// ---------------------------------------------------------------------------
+// searched chunks of a row range (the cosine chunk-ordinal base of the next
+// shard): k_chunk_active flags, then one block sums them
+__global__ __launch_bounds__(256) void k_sum_flags(const int *flags, int64_t nchunks, int64_t *count) {
+    __shared__ int64_t part[256];
+    int64_t s = 0;
+    for (int64_t c = threadIdx.x; c < nchunks; c += 256) s += flags[c] ? 1 : 0;
+    part[threadIdx.x] = s;
+    __syncthreads();
+    for (int off = 128; off > 0; off >>= 1) {
+        if ((int)threadIdx.x < off) part[threadIdx.x] += part[threadIdx.x + off];
+        __syncthreads();
+    }
+    if (threadIdx.x == 0) *count = part[0];
+}
+
+void launch_count_active_chunks(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists, int64_t n,
+                                int64_t chunk_rows, int *flags_scratch, int64_t *count, hipStream_t s) {
+    const int64_t nchunks = (n + chunk_rows - 1) / chunk_rows;
+    if (nchunks > 0)
+        hipLaunchKernelGGL(k_chunk_active, dim3((unsigned)nchunks), dim3(256), 0, s, filter, nonempty, exists, n,
+                           chunk_rows, filter ? 1 : 0, flags_scratch);
+    hipLaunchKernelGGL(k_sum_flags, dim3(1), dim3(256), 0, s, flags_scratch, nchunks, count);
+}
+
 }  // namespace mqvs

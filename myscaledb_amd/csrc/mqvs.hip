@@ -722,6 +722,15 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     g_stats = st;
 }
 
+// the search for other translation units (sharded.hip): device pointers,
+// caller stream, explicit chunk-ordinal base
+void search_segment(mqvs_segment *seg, const float *queries, int nq, int k, int metric, const uint8_t *filter,
+                    const uint8_t *exists, int64_t *out_ids, float *out_dist, uint32_t flags, hipStream_t stream,
+                    int64_t ord_base) {
+    search_impl(seg, queries, nq, k, metric, filter, exists, out_ids, out_dist, flags | MQVS_F_DEVICE_PTRS, stream,
+                false, ord_base);
+}
+
 // Exact re-rank of caller-given candidate rows (computeTopDistanceSubset
 // contract, VIWithDataPart.cpp:838-856): the distance formula and cosine
 // query variant mqvs_search uses for the same batch size, then top-k by the

@@ -258,6 +258,15 @@ void launch_probe_select(const float *probe, int64_t P, int64_t ld, int nq, int 
                          int64_t row_base, const int32_t *row_list, hipStream_t s);
 void launch_cand_tau(const Cand *cand, const int *cand_count, int cand_cap, int nq, int k,
                      int metric, uint32_t *tau, const int *overflow_q, hipStream_t s);
+// mqvs_search with device pointers on `stream` (sharded.hip)
+void search_segment(mqvs_segment *seg, const float *queries, int nq, int k, int metric, const uint8_t *filter,
+                    const uint8_t *exists, int64_t *out_ids, float *out_dist, uint32_t flags, hipStream_t stream,
+                    int64_t ord_base);
+// number of granule chunks of [0, n) the reference searches (a non-empty row
+// that, under a PREWHERE filter, passes it and is not deleted) -> *count
+void launch_count_active_chunks(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists, int64_t n,
+                                int64_t chunk_rows, int *flags_scratch, int64_t *count, hipStream_t s);
+
 // ASYNC calls: OR a search's device flags into the calling thread's sticky
 // word (read and cleared by mqvs_async_check): bit 0 = candidate overflow
 // (overflow[0] != 0), bit 1 = cosine variant chain did not repeat (status[0]

@@ -139,3 +139,85 @@ class ShardedScan:
         if not on_device:
             si, sd = si.numpy(), sd.numpy()
         return self.merge(si, sd)
+
+
+class RcclComm:
+    """libmqvs's own RCCL communicator (mqvs_comm_*): one rank per GPU, the
+    exchange of mqvs_sharded_search.  unique_id() runs on one rank; its 128
+    bytes reach the others out of band (here: a torch.distributed broadcast)."""
+
+    def __init__(self, nranks: int, rank: int, uid: bytes):
+        import ctypes
+        from . import _lib
+        self._lib = _lib
+        self.nranks, self.rank = nranks, rank
+        buf = (ctypes.c_uint8 * 128).from_buffer_copy(bytes(uid))
+        h = ctypes.c_void_p()
+        _lib.check(_lib.lib.mqvs_comm_init(nranks, rank, buf, ctypes.byref(h)))
+        self._h = h
+
+    @staticmethod
+    def unique_id() -> bytes:
+        import ctypes
+        from . import _lib
+        buf = (ctypes.c_uint8 * 128)()
+        _lib.check(_lib.lib.mqvs_comm_unique_id(buf))
+        return bytes(buf)
+
+    @classmethod
+    def from_process_group(cls, group=None):
+        """Every rank of a torch.distributed group joins one communicator."""
+        import torch
+        import torch.distributed as dist
+        world = dist.get_world_size(group) if dist.is_initialized() else 1
+        rank = dist.get_rank(group) if dist.is_initialized() else 0
+        uid = cls.unique_id() if rank == 0 else bytes(128)
+        if world > 1:
+            dev = torch.device("cuda", torch.cuda.current_device()) if dist.get_backend(group) == "nccl" else "cpu"
+            t = torch.tensor(list(uid), dtype=torch.uint8, device=dev)
+            dist.broadcast(t, src=0, group=group)
+            uid = bytes(t.cpu().tolist())
+        return cls(world, rank, uid)
+
+    def sharded_search(self, segment, queries, k, filter_bitmap=None, row_exists=None, out=None, metric=None):
+        """mqvs_sharded_search: this rank's shard (`segment`, row_offset = its
+        first row) searched, the per-rank top-k all-gathered over RCCL and
+        merged on the device; every rank returns the merged [nq, k] result.
+        Bitmaps are the shard's own (its n bits)."""
+        import ctypes
+        from .vector_scan import _host_f32, _host_u8, _is_torch, _ptr, metric_id
+        from ._lib import F_DEVICE_PTRS
+        m = segment.metric if metric is None else metric_id(metric)
+        if _is_torch(queries):
+            import torch
+            nq = queries.shape[0]
+            if out is None:
+                ids = torch.empty((nq, k), dtype=torch.int64, device=queries.device)
+                dist = torch.empty((nq, k), dtype=torch.float32, device=queries.device)
+            else:
+                ids, dist = out
+            self._lib.check(self._lib.lib.mqvs_sharded_search(
+                self._h, segment._h, _ptr(queries), nq, k, m, _ptr(filter_bitmap), _ptr(row_exists), _ptr(ids),
+                _ptr(dist), F_DEVICE_PTRS, None))
+            return ids, dist
+        q = _host_f32(queries)
+        if q.ndim == 1:
+            q = q[None, :]
+        nq = q.shape[0]
+        ids = np.empty((nq, k), np.int64)
+        dist = np.empty((nq, k), np.float32)
+        self._lib.check(self._lib.lib.mqvs_sharded_search(
+            self._h, segment._h, _ptr(q), nq, k, m, _ptr(_host_u8(filter_bitmap)), _ptr(_host_u8(row_exists)),
+            _ptr(ids), _ptr(dist), 0, None))
+        return ids, dist
+
+    def free(self):
+        if getattr(self, "_h", None):
+            self._lib.check(self._lib.lib.mqvs_comm_free(self._h))
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:  # noqa: BLE001
+            pass
