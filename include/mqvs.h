@@ -331,6 +331,25 @@ int mqvs_index_info(mqvs_index_t idx, mqvs_index_info_t *out);
 int mqvs_index_search(mqvs_index_t idx, const float *queries, int32_t nq, int32_t k, const char *params,
                       const uint8_t *filter, const uint8_t *row_exists, int64_t *out_ids, float *out_dist,
                       uint32_t flags, mqvs_stream_t stream);
+/* Decoupled parts: a part merged from several source parts whose index still
+ * serves the source part's rows (the reference's VIWithMeta row_ids_map /
+ * inverted maps, VICacheObject.h:50-64).
+ * mqvs_index_set_row_ids_map: register the source part's row -> decoupled
+ *   part row map (UInt64 per source row, len >= the indexed rows); every later
+ *   mqvs_index_search on this index returns decoupled-part row ids
+ *   (VIWithColumnInPart::transferToNewRowIds, VIWithDataPart.cpp:56-67, applied
+ *   at :938-943).  NULL / len 0 clears it.  The map lives in HBM with the index.
+ * mqvs_decoupled_filter: getRealBitmap (VIUtils.cpp:479-497) -- a PREWHERE
+ *   bitmap over the decoupled part's new_rows rows -> the bitmap over this
+ *   source part's old_rows rows: old bit inverted_row_ids_map[i] is set for
+ *   every set bit i whose inverted_row_sources_map[i] == own_id.  With no
+ *   inverted map (len 0) the filter is returned as it is.  MQVS_F_DEVICE_PTRS:
+ *   all pointers on the device. */
+int mqvs_index_set_row_ids_map(mqvs_index_t idx, const uint64_t *row_ids_map, int64_t len, uint32_t flags);
+int mqvs_decoupled_filter(const uint8_t *new_filter, int64_t new_rows, const uint64_t *inverted_row_ids_map,
+                          const uint8_t *inverted_row_sources_map, int64_t inverted_len, uint32_t own_id,
+                          uint8_t *old_filter, int64_t old_rows, uint32_t flags, mqvs_stream_t stream);
+
 /* Stats of the calling thread's last mqvs_index_search (times only with
  * mqvs_set_timing(1)). */
 typedef struct {
@@ -347,6 +366,35 @@ typedef struct {
     int32_t nq, k, nprobe, num_reorder;
 } mqvs_index_search_stats;
 int mqvs_index_last_stats(mqvs_index_search_stats *out);
+
+/* ---- device-resident cache of parts (VICacheManager, VICacheManager.h:82-114)
+ * An LRU of segments (+ an optional index over each) keyed by the caller's
+ * CacheKey string, weighed by HBM bytes against max_bytes.
+ *   put      takes ownership of seg / idx (the index must be over seg); evicts
+ *            least-recently-used unheld entries to make room; a key already
+ *            present is replaced.  MQVS_ERR_MEMORY_LIMIT when the budget
+ *            cannot hold it (ownership then stays with the caller).
+ *   acquire  *seg = NULL on a miss; on a hit the entry is held (never evicted)
+ *            and becomes most recently used; the handles stay owned by the
+ *            cache.  Every hit is paired with release(key, seg).
+ *   remove   forceExpire: freed now, or at the last release if held.
+ * Thread-safe (one mutex; searches on acquired handles run lock-free). */
+typedef struct mqvs_cache *mqvs_cache_t;
+typedef struct {
+    int64_t items;        /* entries in the LRU */
+    size_t bytes;         /* their HBM bytes */
+    size_t max_bytes;
+    int64_t hits, misses, evictions;
+    int64_t pinned;       /* entries held now */
+    int64_t expired_held; /* removed / replaced entries still held */
+} mqvs_cache_stats_t;
+int mqvs_cache_create(size_t max_bytes, mqvs_cache_t *out);
+int mqvs_cache_free(mqvs_cache_t cache);
+int mqvs_cache_put(mqvs_cache_t cache, const char *key, mqvs_segment_t seg, mqvs_index_t idx);
+int mqvs_cache_acquire(mqvs_cache_t cache, const char *key, mqvs_segment_t *seg, mqvs_index_t *idx);
+int mqvs_cache_release(mqvs_cache_t cache, const char *key, mqvs_segment_t seg);
+int mqvs_cache_remove(mqvs_cache_t cache, const char *key);
+int mqvs_cache_stats(mqvs_cache_t cache, mqvs_cache_stats_t *out);
 
 /* ---- observability -------------------------------------------------------
  * Stats of the calling thread's last mqvs_search: per-launch kernel times

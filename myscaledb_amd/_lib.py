@@ -42,6 +42,9 @@ SYMBOLS = [
     "mqvs_segment_create_binary", "mqvs_search_binary", "mqvs_knn_binary_raw",
     "mqvs_segment_create_from_column", "mqvs_async_check",
     "mqvs_comm_unique_id", "mqvs_comm_init", "mqvs_comm_free", "mqvs_sharded_search",
+    "mqvs_index_set_row_ids_map", "mqvs_decoupled_filter",
+    "mqvs_cache_create", "mqvs_cache_free", "mqvs_cache_put", "mqvs_cache_acquire", "mqvs_cache_release",
+    "mqvs_cache_remove", "mqvs_cache_stats",
 ]
 
 
@@ -63,6 +66,12 @@ class IndexInfo(ctypes.Structure):
     _fields_ = [("nlist", ctypes.c_int64), ("npos", ctypes.c_int64), ("max_list", ctypes.c_int64),
                 ("rows_indexed", ctypes.c_int64), ("metric", ctypes.c_int32), ("dim", ctypes.c_int32),
                 ("hbm_bytes", ctypes.c_size_t), ("build_ms", ctypes.c_double)]
+
+
+class CacheStats(ctypes.Structure):
+    _fields_ = [("items", ctypes.c_int64), ("bytes", ctypes.c_size_t), ("max_bytes", ctypes.c_size_t),
+                ("hits", ctypes.c_int64), ("misses", ctypes.c_int64), ("evictions", ctypes.c_int64),
+                ("pinned", ctypes.c_int64), ("expired_held", ctypes.c_int64)]
 
 
 class IndexSearchStats(ctypes.Structure):
@@ -133,6 +142,15 @@ def _load():
         "mqvs_comm_init": ([I32, I32, P, P], ctypes.c_int),
         "mqvs_comm_free": ([P], ctypes.c_int),
         "mqvs_sharded_search": ([P, P, P, I32, I32, I32, P, P, P, P, U32, P], ctypes.c_int),
+        "mqvs_index_set_row_ids_map": ([P, P, I64, U32], ctypes.c_int),
+        "mqvs_decoupled_filter": ([P, I64, P, P, I64, U32, P, I64, U32, P], ctypes.c_int),
+        "mqvs_cache_create": ([ctypes.c_size_t, P], ctypes.c_int),
+        "mqvs_cache_free": ([P], ctypes.c_int),
+        "mqvs_cache_put": ([P, ctypes.c_char_p, P, P], ctypes.c_int),
+        "mqvs_cache_acquire": ([P, ctypes.c_char_p, P, P], ctypes.c_int),
+        "mqvs_cache_release": ([P, ctypes.c_char_p, P], ctypes.c_int),
+        "mqvs_cache_remove": ([P, ctypes.c_char_p], ctypes.c_int),
+        "mqvs_cache_stats": ([P, P], ctypes.c_int),
     }
     for name, (args, res) in sig.items():
         fn = getattr(L, name)

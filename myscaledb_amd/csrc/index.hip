@@ -59,6 +59,10 @@ struct mqvs_index {
     int32_t *cperm = nullptr;
     float *cpnorm = nullptr;
     int64_t *clist_off = nullptr;
+    // decoupled part (VIWithMeta::row_ids_map): old part row -> row id in the
+    // decoupled part, applied to every result (transferToNewRowIds)
+    uint64_t *row_ids_map = nullptr;
+    int64_t row_ids_len = 0;
     size_t bytes = 0;
     double build_ms = 0.0;
 };
@@ -76,7 +80,7 @@ struct ListBufs {
 struct IndexWorkspace {
     hipEvent_t ev[6] = {};
     DevBuf queries, qvars, qnorms, qmu, qlam, status, qhi, probes, cprobes, filter, exists, rows, out_ids, out_dist,
-        ord;
+        ord, dmap, dwords;
     ListBufs coarse, fine;
     void init() {
         if (ev[0]) return;
@@ -192,7 +196,7 @@ static void free_index(mqvs_index *ix) {
     if (ix->seg) (void)hipSetDevice(ix->seg->device);
     if (ix->cent) segment_release(ix->cent);
     for (void *q : {(void *)ix->plane, (void *)ix->perm, (void *)ix->pnorm, (void *)ix->list_off, (void *)ix->cplane,
-                    (void *)ix->cperm, (void *)ix->cpnorm, (void *)ix->clist_off})
+                    (void *)ix->cperm, (void *)ix->cpnorm, (void *)ix->clist_off, (void *)ix->row_ids_map})
         if (q) (void)hipFree(q);
     if (cur >= 0) (void)hipSetDevice(cur);
     delete ix;
@@ -617,6 +621,8 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     }
     dstats = (int64_t *)ws.fine.stats.get(sizeof(int64_t) * 8);
 
+    // decoupled part: results in the new part's row ids (VIWithDataPart.cpp:938-943)
+    if (dev && ix->row_ids_map) launch_map_ids(dids, (int64_t)nq * k, ix->row_ids_map, s);
     const bool async = dev && (flags & MQVS_F_ASYNC);
     if (async) {
         const bool variants_matter = !first_stage && ords > maxv;
@@ -633,6 +639,7 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
         fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not repeat within " + std::to_string(maxv) +
                                    " steps on a part of more chunks");
     if (!dev) {
+        if (ix->row_ids_map) launch_map_ids(dids, (int64_t)nq * k, ix->row_ids_map, s);
         MQVS_HIP(hipMemcpyAsync(out_ids, dids, sizeof(int64_t) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
         MQVS_HIP(hipMemcpyAsync(out_dist, ddist, sizeof(float) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
         MQVS_HIP(hipStreamSynchronize(s));
@@ -691,6 +698,73 @@ int mqvs_index_search(mqvs_index_t idx, const float *queries, int32_t nq, int32_
     return guarded([&] {
         search_index_impl(idx, queries, nq, k, params, filter, row_exists, out_ids, out_dist, flags,
                           (hipStream_t)stream);
+    });
+}
+
+int mqvs_index_set_row_ids_map(mqvs_index_t idx, const uint64_t *row_ids_map, int64_t len, uint32_t flags) {
+    return guarded([&] {
+        if (!idx) fail(MQVS_ERR_BAD_ARGUMENTS, "null index");
+        DeviceGuard guard(idx->seg->device);
+        if (idx->row_ids_map) {
+            MQVS_HIP(hipFree(idx->row_ids_map));
+            idx->bytes -= sizeof(uint64_t) * (size_t)idx->row_ids_len;
+            idx->row_ids_map = nullptr;
+            idx->row_ids_len = 0;
+        }
+        if (!row_ids_map || len <= 0) return;
+        if (len < idx->seg->row_offset + idx->seg->n)
+            fail(MQVS_ERR_BAD_ARGUMENTS, "row_ids_map shorter than the indexed part (" + std::to_string(len) + " < " +
+                                             std::to_string(idx->seg->row_offset + idx->seg->n) + ")");
+        uint64_t *m = nullptr;
+        if (hipMalloc((void **)&m, sizeof(uint64_t) * (size_t)len) != hipSuccess) {
+            (void)hipGetLastError();
+            fail(MQVS_ERR_MEMORY_LIMIT, "HBM allocation of the row id map failed");
+        }
+        MQVS_HIP(hipMemcpy(m, row_ids_map, sizeof(uint64_t) * (size_t)len,
+                           (flags & MQVS_F_DEVICE_PTRS) ? hipMemcpyDeviceToDevice : hipMemcpyHostToDevice));
+        idx->row_ids_map = m;
+        idx->row_ids_len = len;
+        idx->bytes += sizeof(uint64_t) * (size_t)len;
+    });
+}
+
+int mqvs_decoupled_filter(const uint8_t *new_filter, int64_t new_rows, const uint64_t *inverted_row_ids_map,
+                          const uint8_t *inverted_row_sources_map, int64_t inverted_len, uint32_t own_id,
+                          uint8_t *old_filter, int64_t old_rows, uint32_t flags, mqvs_stream_t stream) {
+    return guarded([&] {
+        if (new_rows < 0 || old_rows < 0 || inverted_len < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "bad sizes");
+        if ((new_rows && !new_filter) || (old_rows && !old_filter))
+            fail(MQVS_ERR_BAD_ARGUMENTS, "null bitmap");
+        if (inverted_len > 0 && (!inverted_row_ids_map || !inverted_row_sources_map))
+            fail(MQVS_ERR_BAD_ARGUMENTS, "null inverted map");
+        int dev = 0;
+        MQVS_HIP(hipGetDevice(&dev));
+        IndexWorkspace &ws = index_workspace(dev);
+        hipStream_t s = stream ? (hipStream_t)stream : thread_stream(dev);
+        const bool devp = flags & MQVS_F_DEVICE_PTRS;
+        const int64_t nb = (new_rows + 7) / 8, ob = (old_rows + 7) / 8;
+        const uint8_t *df = new_filter;
+        const uint64_t *dinv = inverted_row_ids_map;
+        const uint8_t *dsrc = inverted_row_sources_map;
+        if (!devp) {
+            auto *b = (uint8_t *)ws.dmap.get((size_t)nb + 16 + (size_t)inverted_len * 9 + 16);
+            MQVS_HIP(hipMemcpyAsync(b, new_filter, nb, hipMemcpyHostToDevice, s));
+            df = b;
+            auto *inv = (uint64_t *)(b + (nb + 15) / 16 * 16);
+            if (inverted_len) {
+                MQVS_HIP(hipMemcpyAsync(inv, inverted_row_ids_map, 8 * (size_t)inverted_len, hipMemcpyHostToDevice, s));
+                MQVS_HIP(hipMemcpyAsync((uint8_t *)(inv + inverted_len), inverted_row_sources_map, inverted_len,
+                                        hipMemcpyHostToDevice, s));
+            }
+            dinv = inv;
+            dsrc = (const uint8_t *)(inv + inverted_len);
+        }
+        auto *words = (uint32_t *)ws.dwords.get(4 * (size_t)((old_rows + 31) / 32) + 16);
+        launch_decoupled_filter(df, new_rows, inverted_len ? dinv : nullptr, dsrc, inverted_len, own_id, words,
+                                old_rows, s);
+        MQVS_HIP(hipGetLastError());
+        MQVS_HIP(hipMemcpyAsync(old_filter, words, ob, devp ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
+        if (!(devp && (flags & MQVS_F_ASYNC))) MQVS_HIP(hipStreamSynchronize(s));
     });
 }
 

@@ -585,4 +585,59 @@ void launch_count_active_chunks(const uint8_t *filter, const uint8_t *nonempty, 
     hipLaunchKernelGGL(k_sum_flags, dim3(1), dim3(256), 0, s, flags_scratch, nchunks, count);
 }
 
+// ---------------------------------------------------------------------------
+// Decoupled parts (a merged part whose vector index still lives in its source
+// parts): VIWithColumnInPart::transferToNewRowIds (VIWithDataPart.cpp:56-67)
+// and getRealBitmap (VIUtils.cpp:479-497), on the device.
+__global__ void k_map_ids(int64_t *ids, int64_t count, const uint64_t *map) {
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < count; i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t v = ids[i];
+        if (v >= 0) ids[i] = (int64_t)map[v];
+    }
+}
+
+void launch_map_ids(int64_t *ids, int64_t count, const uint64_t *map, hipStream_t s) {
+    if (count <= 0) return;
+    const int64_t blocks = std::min<int64_t>((count + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_map_ids, dim3((unsigned)blocks), dim3(256), 0, s, ids, count, map);
+}
+
+__global__ void k_copy_bits(const uint8_t *src, int64_t rows, uint32_t *words) {
+    const int64_t w = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (w * 32 >= rows) return;
+    uint32_t v = 0;
+    for (int b = 0; b < 4; ++b) {
+        const int64_t byte = w * 4 + b;
+        if (byte * 8 < rows) v |= (uint32_t)src[byte] << (8 * b);
+    }
+    const int64_t tail = rows - w * 32;
+    if (tail < 32) v &= (1u << tail) - 1u;
+    words[w] = v;
+}
+
+__global__ void k_decoupled_filter(const uint8_t *nf, int64_t new_rows, const uint64_t *inv_ids, const uint8_t *inv_src,
+                                   int64_t inv_len, uint32_t own_id, uint32_t *old_words, int64_t old_rows) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= new_rows || i >= inv_len) return;
+    if (!((nf[i >> 3] >> (i & 7)) & 1)) return;
+    if ((uint32_t)inv_src[i] != own_id) return;
+    const uint64_t r = inv_ids[i];
+    if (r < (uint64_t)old_rows) atomicOr(&old_words[r >> 5], 1u << (r & 31));
+}
+
+void launch_decoupled_filter(const uint8_t *new_filter, int64_t new_rows, const uint64_t *inv_ids,
+                             const uint8_t *inv_src, int64_t inv_len, uint32_t own_id, uint32_t *old_words,
+                             int64_t old_rows, hipStream_t s) {
+    const int64_t nw = (old_rows + 31) / 32;
+    MQVS_HIP(hipMemsetAsync(old_words, 0, 4 * (size_t)std::max<int64_t>(nw, 1), s));
+    if (!inv_ids) {  // no maps: the filter itself ("return filter")
+        if (nw) hipLaunchKernelGGL(k_copy_bits, dim3((unsigned)((nw + 255) / 256)), dim3(256), 0, s, new_filter,
+                                   std::min(new_rows, old_rows), old_words);
+        return;
+    }
+    if (new_rows > 0)
+        hipLaunchKernelGGL(k_decoupled_filter, dim3((unsigned)((new_rows + 255) / 256)), dim3(256), 0, s, new_filter,
+                           new_rows, inv_ids, inv_src, inv_len, own_id, old_words, old_rows);
+}
+
 }  // namespace mqvs

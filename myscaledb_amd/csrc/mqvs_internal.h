@@ -258,6 +258,16 @@ void launch_probe_select(const float *probe, int64_t P, int64_t ld, int nq, int 
                          int64_t row_base, const int32_t *row_list, hipStream_t s);
 void launch_cand_tau(const Cand *cand, const int *cand_count, int cand_cap, int nq, int k,
                      int metric, uint32_t *tau, const int *overflow_q, hipStream_t s);
+// decoupled parts (index.hip): ids[i] = map[ids[i]] for ids >= 0
+// (transferToNewRowIds); new-part filter -> old-part filter (getRealBitmap):
+// old bit inv_ids[i] for every set new bit i < inv_len with inv_src[i] ==
+// own_id (inv_ids null: the filter passes through unchanged); old_words is
+// zeroed first, (old_rows + 31) / 32 words.
+void launch_map_ids(int64_t *ids, int64_t count, const uint64_t *map, hipStream_t s);
+void launch_decoupled_filter(const uint8_t *new_filter, int64_t new_rows, const uint64_t *inv_ids,
+                             const uint8_t *inv_src, int64_t inv_len, uint32_t own_id, uint32_t *old_words,
+                             int64_t old_rows, hipStream_t s);
+
 // mqvs_search with device pointers on `stream` (sharded.hip)
 void search_segment(mqvs_segment *seg, const float *queries, int nq, int k, int metric, const uint8_t *filter,
                     const uint8_t *exists, int64_t *out_ids, float *out_dist, uint32_t flags, hipStream_t stream,

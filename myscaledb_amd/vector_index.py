@@ -48,6 +48,19 @@ class VectorIndex:
         check(lib.mqvs_index_build(segment._h, index_type.encode(), _params(params), ctypes.byref(h)))
         return cls(h, segment)
 
+    def set_row_ids_map(self, row_ids_map):
+        """Decoupled part (VIWithMeta::row_ids_map): source-part row -> row of
+        the decoupled part; later searches return decoupled-part row ids
+        (transferToNewRowIds, VIWithDataPart.cpp:56-67).  None clears it."""
+        if row_ids_map is None:
+            check(lib.mqvs_index_set_row_ids_map(self._h, None, 0, 0))
+            return
+        if _is_torch(row_ids_map):
+            check(lib.mqvs_index_set_row_ids_map(self._h, _ptr(row_ids_map), row_ids_map.numel(), F_DEVICE_PTRS))
+            return
+        m = np.ascontiguousarray(row_ids_map, np.uint64)
+        check(lib.mqvs_index_set_row_ids_map(self._h, _ptr(m), m.size, 0))
+
     def info(self):
         st = _lib.IndexInfo()
         check(lib.mqvs_index_info(self._h, ctypes.byref(st)))
@@ -105,3 +118,15 @@ class VectorIndex:
 
 def last_index_stats():
     return _lib.last_index_stats()
+
+
+def decoupled_filter(new_filter, new_rows, inverted_row_ids_map, inverted_row_sources_map, own_id, old_rows):
+    """getRealBitmap (VIUtils.cpp:479-497) on the GPU: a PREWHERE bitmap over
+    the decoupled part's rows -> the bitmap over one source part's rows."""
+    nf = _host_u8(new_filter)
+    inv = None if inverted_row_ids_map is None else np.ascontiguousarray(inverted_row_ids_map, np.uint64)
+    src = None if inverted_row_sources_map is None else np.ascontiguousarray(inverted_row_sources_map, np.uint8)
+    out = np.zeros((old_rows + 7) // 8, np.uint8)
+    check(lib.mqvs_decoupled_filter(_ptr(nf), new_rows, _ptr(inv), _ptr(src), 0 if inv is None else inv.size,
+                                    own_id, _ptr(out), old_rows, 0, None))
+    return out
