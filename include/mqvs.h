@@ -127,6 +127,13 @@ int mqvs_segment_generate(uint64_t seed, int32_t mode, int64_t n, int32_t d, int
 int mqvs_segment_free(mqvs_segment_t seg);
 int mqvs_segment_info(mqvs_segment_t seg, int64_t *n, int32_t *d, int32_t *metric,
                       int64_t *granule_rows, int64_t *row_offset, size_t *hbm_bytes);
+/* The segment's pre-filter planes: *split = the split built (2 / 3 / 6, see
+ * mqvs_set_prefilter) or 0 when the planes did not fit in HBM at creation --
+ * batches then run the exact fp32 MFMA path over every row (same bits, about
+ * 1/16 of the bf16 MFMA rate); *plane_bytes = their HBM bytes (included in
+ * mqvs_segment_info's hbm_bytes); *approx_ok = 1 when the pre-filter serves
+ * searches (planes present and the rows' norms finite and moderate). */
+int mqvs_segment_prefilter(mqvs_segment_t seg, int32_t *split, size_t *plane_bytes, int32_t *approx_ok);
 /* Device pointer of the resident rows (normalised rows for cosine). */
 int mqvs_segment_rows(mqvs_segment_t seg, const float **dev_rows);
 
@@ -167,7 +174,8 @@ int mqvs_knn_raw(const float *x, const float *y, int64_t d, int64_t k, int64_t n
 
 /* Exact re-rank of candidate rows (computeTopDistanceSubset contract,
  * VIWithDataPart.cpp:838-856): cand is nq*ncand segment-local row ids (-1 or
- * out-of-range = none; distinct rows per query), ncand <= 4096.  Each
+ * out-of-range = none; distinct rows per query), ncand <= 32768, k <= 16384
+ * (above 4096 candidates the records are sorted through global scratch).  Each
  * candidate gets the distance mqvs_search computes for the same batch size
  * (nq < 20 sequential formula, else BLAS form; cosine with the row's chunk
  * query variant); rows cleared in row_exists (LSB-first, n bits, or NULL)

@@ -35,7 +35,7 @@ F_TIMING = 0x100
 SYMBOLS = [
     "mqvs_abi_version", "mqvs_init", "mqvs_device_count", "mqvs_last_error",
     "mqvs_thread_release", "mqvs_segment_create", "mqvs_segment_create_device",
-    "mqvs_segment_generate", "mqvs_segment_free", "mqvs_segment_info", "mqvs_segment_rows",
+    "mqvs_segment_generate", "mqvs_segment_free", "mqvs_segment_info", "mqvs_segment_prefilter", "mqvs_segment_rows",
     "mqvs_search", "mqvs_search_ex", "mqvs_knn_raw", "mqvs_rerank", "mqvs_merge_shards", "mqvs_generate_device",
     "mqvs_last_search_stats", "mqvs_set_timing", "mqvs_set_batch_mode", "mqvs_set_gather_mode", "mqvs_set_prefilter",
     "mqvs_index_build", "mqvs_index_free", "mqvs_index_info", "mqvs_index_search", "mqvs_index_last_stats",
@@ -116,6 +116,7 @@ def _load():
         "mqvs_segment_generate": ([U64, I32, I64, I32, I32, I64, I64, P], ctypes.c_int),
         "mqvs_segment_free": ([P], ctypes.c_int),
         "mqvs_segment_info": ([P, P, P, P, P, P, P], ctypes.c_int),
+        "mqvs_segment_prefilter": ([P, P, P, P], ctypes.c_int),
         "mqvs_segment_rows": ([P, P], ctypes.c_int),
         "mqvs_search": ([P, P, I32, I32, I32, P, P, P, P, U32, P], ctypes.c_int),
         "mqvs_search_ex": ([P, P, I32, I32, I32, P, P, I64, P, P, U32, P], ctypes.c_int),

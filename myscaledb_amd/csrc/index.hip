@@ -615,7 +615,7 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
         rp.exists = dexists;
         rp.filter = nullptr;  // the scan applied the filter; candidates pass it
         rp.nonempty = seg->nonempty_bits;
-        launch_rerank_ids(rp, ix->metric, crow, R, k, seg->row_offset, dids, ddist, s);
+        launch_rerank_ids(rp, ix->metric, crow, R, k, seg->row_offset, dids, ddist, nullptr, s);
         MQVS_HIP(hipGetLastError());
         MQVS_HIP(hipEventRecord(ws.ev[5], s));
     }

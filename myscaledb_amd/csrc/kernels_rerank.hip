@@ -74,22 +74,33 @@ __device__ inline uint4 rerank_rec(const ScanParams &p, int64_t row, float raw) 
     return r;
 }
 
+// Sort the query's candidate records and write its top k.  g == null: the
+// records are recs[0, ncand) in LDS (ncand <= kSortCap); else they are
+// g[0, ncand) in the query's global scratch (2 ncand records) and recs is
+// kSortCap records of LDS for global_sort.
 template <int METRIC>
-__device__ inline void rerank_emit(uint4 *recs, int ncand, int k, int q, int64_t id_offset, int64_t *out_ids,
-                                   float *out_dist) {
-    int N = 1;
-    while (N < ncand) N <<= 1;
-    for (int i = ncand + threadIdx.x; i < N; i += SEL_THREADS)
-        recs[i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-    __syncthreads();
-    block_bitonic_sort(recs, N);
+__device__ inline void rerank_emit(uint4 *recs, uint4 *g, int ncand, int k, int q, int64_t id_offset,
+                                   int64_t *out_ids, float *out_dist) {
+    const uint4 *sorted = recs;
+    int N = ncand;
+    if (g) {
+        __syncthreads();
+        sorted = global_sort(g, g + ncand, ncand, recs);
+    } else {
+        N = 1;
+        while (N < ncand) N <<= 1;
+        for (int i = ncand + threadIdx.x; i < N; i += SEL_THREADS)
+            recs[i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        __syncthreads();
+        block_bitonic_sort(recs, N);
+    }
     const float pad = (METRIC == MQVS_METRIC_IP) ? 1.17549435e-38f : 3.40282347e+38f;
     for (int i = threadIdx.x; i < k; i += SEL_THREADS) {
         int64_t id = -1;
         float dist = pad;
-        if (i < N && recs[i].x != 0xFFFFFFFFu) {
-            id = (int64_t)recs[i].w + id_offset;
-            dist = key_to_value(METRIC, recs[i].x);
+        if (i < N && sorted[i].x != 0xFFFFFFFFu) {
+            id = (int64_t)sorted[i].w + id_offset;
+            dist = key_to_value(METRIC, sorted[i].x);
         }
         out_ids[(int64_t)q * k + i] = id;
         out_dist[(int64_t)q * k + i] = dist;
@@ -100,16 +111,18 @@ __device__ inline void rerank_emit(uint4 *recs, int ncand, int k, int q, int64_t
 template <int METRIC, bool DIRECT>
 __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids(ScanParams p, const int64_t *cand, int ncand,
                                                            int k, int64_t id_offset, int64_t *out_ids,
-                                                           float *out_dist) {
-    extern __shared__ __attribute__((aligned(16))) uint4 recs[];  // pow2 >= ncand records
+                                                           float *out_dist, uint4 *scratch) {
+    extern __shared__ __attribute__((aligned(16))) uint4 recs[];  // pow2 >= ncand (or kSortCap) records
     const int q = blockIdx.x;
     const int64_t *c = cand + (int64_t)q * ncand;
+    uint4 *g = scratch ? scratch + (int64_t)q * 2 * ncand : nullptr;
+    uint4 *dst = g ? g : recs;
     for (int i = threadIdx.x; i < ncand; i += SEL_THREADS) {
         int64_t row = c[i];
         if (!(row >= 0 && row < p.n && row_valid(p, row))) row = -1;
-        recs[i] = rerank_rec<METRIC>(p, row, row >= 0 ? cand_value<METRIC, DIRECT>(p, q, row) : 0.f);
+        dst[i] = rerank_rec<METRIC>(p, row, row >= 0 ? cand_value<METRIC, DIRECT>(p, q, row) : 0.f);
     }
-    rerank_emit<METRIC>(recs, ncand, k, q, id_offset, out_ids, out_dist);
+    rerank_emit<METRIC>(recs, g, ncand, k, q, id_offset, out_ids, out_dist);
 }
 
 // d % 4 == 0: the same per-candidate sequential chain (bit-identical), with
@@ -124,9 +137,11 @@ constexpr int kRrStride = 33;
 template <int METRIC, bool DIRECT>
 __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids_tiled(ScanParams p, const int64_t *cand, int ncand,
                                                                  int k, int64_t id_offset, int64_t *out_ids,
-                                                                 float *out_dist, int nrec) {
+                                                                 float *out_dist, int nrec, uint4 *scratch) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
     uint4 *recs = reinterpret_cast<uint4 *>(smem);
+    uint4 *g = scratch ? scratch + (int64_t)blockIdx.x * 2 * ncand : nullptr;
+    uint4 *dst = g ? g : recs;
     const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
     float *tile = reinterpret_cast<float *>(smem + (size_t)nrec * sizeof(uint4)) + wv * 64 * kRrStride;
     const int q = blockIdx.x;
@@ -226,32 +241,33 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids_tiled(ScanParams p, 
             raw = (p.qnorms[q] + p.row_norms[row]) - 2.0f * acc;
             if (raw < 0) raw = 0;
         }
-        if (i < ncand) recs[i] = rerank_rec<METRIC>(p, row, raw);
+        if (i < ncand) dst[i] = rerank_rec<METRIC>(p, row, raw);
     }
-    rerank_emit<METRIC>(recs, ncand, k, q, id_offset, out_ids, out_dist);
+    rerank_emit<METRIC>(recs, g, ncand, k, q, id_offset, out_ids, out_dist);
 }
 
 template <int M, bool DIRECT>
 static void rerank_ids_t(const ScanParams &p, const int64_t *cand, int ncand, int k, int64_t id_offset,
-                         int64_t *ids, float *dist, hipStream_t s) {
+                         int64_t *ids, float *dist, uint4 *scratch, hipStream_t s) {
     int N = 1;
     while (N < ncand) N <<= 1;
+    if (scratch) N = kSortCap;  // LDS records of global_sort
     if ((p.d & 3) == 0) {
         const size_t lds = N * sizeof(uint4) + (SEL_THREADS / 64) * 64 * kRrStride * sizeof(float);
         hipLaunchKernelGGL((k_rerank_ids_tiled<M, DIRECT>), dim3(p.nq), dim3(SEL_THREADS), lds, s, p, cand, ncand, k,
-                           id_offset, ids, dist, N);
+                           id_offset, ids, dist, N, scratch);
     } else {
         hipLaunchKernelGGL((k_rerank_ids<M, DIRECT>), dim3(p.nq), dim3(SEL_THREADS), N * sizeof(uint4), s, p, cand,
-                           ncand, k, id_offset, ids, dist);
+                           ncand, k, id_offset, ids, dist, scratch);
     }
 }
 
 void launch_rerank_ids(const ScanParams &p, int metric, const int64_t *cand, int ncand, int k,
-                       int64_t id_offset, int64_t *out_ids, float *out_dist, hipStream_t s) {
+                       int64_t id_offset, int64_t *out_ids, float *out_dist, uint4 *scratch, hipStream_t s) {
     const bool direct = p.nq < kBlasThreshold;
-#define MQVS_RR(M)                                                                  \
-    direct ? rerank_ids_t<M, true>(p, cand, ncand, k, id_offset, out_ids, out_dist, s) \
-           : rerank_ids_t<M, false>(p, cand, ncand, k, id_offset, out_ids, out_dist, s)
+#define MQVS_RR(M)                                                                           \
+    direct ? rerank_ids_t<M, true>(p, cand, ncand, k, id_offset, out_ids, out_dist, scratch, s) \
+           : rerank_ids_t<M, false>(p, cand, ncand, k, id_offset, out_ids, out_dist, scratch, s)
     switch (metric) {
         case MQVS_METRIC_L2: MQVS_RR(MQVS_METRIC_L2); break;
         case MQVS_METRIC_IP: MQVS_RR(MQVS_METRIC_IP); break;

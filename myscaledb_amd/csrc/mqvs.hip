@@ -747,12 +747,27 @@ static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const i
         fail(MQVS_ERR_NOT_IMPLEMENTED, "Metric not implemented in brute force search for Float32 Vector");
     if (cos != (seg->metric == MQVS_METRIC_COSINE))
         fail(MQVS_ERR_LOGICAL, "segment was prepared for a different metric");
-    if (k > kSortCap || ncand > kSortCap)
-        fail(MQVS_ERR_BAD_ARGUMENTS, "k and ncand must not exceed " + std::to_string(kSortCap));
+    if (k > kMaxK || ncand > kLargeCap)
+        fail(MQVS_ERR_BAD_ARGUMENTS, "k must not exceed " + std::to_string(kMaxK) + " and ncand " +
+                                         std::to_string(kLargeCap));
     if (nq > 0 && k > 0 && (!queries || !out_ids || !out_dist || (ncand > 0 && !cand)))
         fail(MQVS_ERR_BAD_ARGUMENTS, "null query, candidate or output pointer");
     g_stats = mqvs_search_stats{};
     if (nq == 0 || k == 0) return;
+    // more candidates than the LDS sort holds: each query's records are sorted
+    // through 2 ncand records of global scratch, in query sub-batches of <= 1 GB
+    const bool large = ncand > kSortCap;
+    if (large) {
+        const int qb = (int)std::max<int64_t>(1, ((int64_t)1 << 26) / (2 * (int64_t)ncand));
+        if (nq > qb) {
+            for (int q0 = 0; q0 < nq; q0 += qb) {
+                const int m = std::min(qb, nq - q0);
+                rerank_impl(seg, queries + (size_t)q0 * seg->d, m, cand + (size_t)q0 * ncand, ncand, k, metric,
+                            exists, out_ids + (size_t)q0 * k, out_dist + (size_t)q0 * k, flags, user_stream);
+            }
+            return;
+        }
+    }
 
     DeviceGuard guard(seg->device);
     Workspace &ws = workspace(seg->device);
@@ -804,7 +819,8 @@ static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const i
     p.ord_base = (int)(seg->row_offset / seg->granule);
     p.exists = dexists;
     p.nonempty = seg->nonempty_bits;
-    launch_rerank_ids(p, metric, dc, ncand, k, seg->row_offset, dids, ddist, s);
+    uint4 *scratch = large ? (uint4 *)ws.large.get(sizeof(uint4) * 2 * (size_t)ncand * nq) : nullptr;
+    launch_rerank_ids(p, metric, dc, ncand, k, seg->row_offset, dids, ddist, scratch, s);
     MQVS_HIP(hipGetLastError());
     if (dev && (flags & MQVS_F_ASYNC)) {
         launch_async_flags(nullptr, status, ords > maxv ? 1 : 0, sticky_word(ws, s), s);
@@ -1364,6 +1380,16 @@ int mqvs_segment_info(mqvs_segment_t seg, int64_t *n, int32_t *d, int32_t *metri
         if (granule_rows) *granule_rows = seg->granule;
         if (row_offset) *row_offset = seg->row_offset;
         if (hbm_bytes) *hbm_bytes = seg->bytes;
+    });
+}
+
+int mqvs_segment_prefilter(mqvs_segment_t seg, int32_t *split, size_t *plane_bytes, int32_t *approx_ok) {
+    return guarded([&] {
+        if (!seg) fail(MQVS_ERR_BAD_ARGUMENTS, "null segment");
+        const bool planes = !seg->binary && seg->rows_hi != nullptr;
+        if (split) *split = planes ? seg->split : 0;
+        if (plane_bytes) *plane_bytes = planes ? seg->plane_bytes : 0;
+        if (approx_ok) *approx_ok = !seg->binary && seg->approx_ok ? 1 : 0;
     });
 }
 

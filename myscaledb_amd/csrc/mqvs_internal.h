@@ -251,7 +251,7 @@ void launch_gather_list(const uint8_t *filter, const uint8_t *nonempty, const ui
                         int64_t chunk_rows, int tile, const int *count, const int64_t *offsets, int32_t *list,
                         hipStream_t s);
 void launch_rerank_ids(const ScanParams &p, int metric, const int64_t *cand, int ncand, int k,
-                       int64_t id_offset, int64_t *out_ids, float *out_dist, hipStream_t s);
+                       int64_t id_offset, int64_t *out_ids, float *out_dist, uint4 *scratch, hipStream_t s);
 void launch_scan_mfma(const ScanParams &p, int metric, bool probe, hipStream_t s);
 void launch_probe_select(const float *probe, int64_t P, int64_t ld, int nq, int k, int metric,
                          uint32_t *tau, int *cand_count, Cand *cand, int cand_cap,

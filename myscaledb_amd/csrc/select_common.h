@@ -240,12 +240,15 @@ __device__ inline void block_bitonic_sort(uint4 *recs, int N) {
 // passes of doubling width.  Every record's key is unique (it ends with the
 // row / list position), so a record's place in the merged run is its place
 // in its own run plus the count of smaller records in the partner run (a
-// binary search) -- no two records ever claim the same slot.
+// binary search).  Equal records (the all-ones padding, a candidate listed
+// twice) are merged stably -- left run first: a right-run record counts the
+// left run's records <= it -- so no two records ever claim the same slot.
+template <bool OR_EQUAL = false>
 __device__ inline int count_less(const uint4 *a, int n, const uint4 &e) {
     int lo = 0, hi = n;
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
-        if (rec_less(a[mid], e))
+        if (OR_EQUAL ? !rec_less(e, a[mid]) : rec_less(a[mid], e))
             lo = mid + 1;
         else
             hi = mid;
@@ -274,8 +277,8 @@ __device__ inline uint4 *global_sort(uint4 *g, uint4 *tmp, int m, uint4 *recs) {
             const int a1 = base + w < m ? base + w : m;
             const int b1 = base + 2 * w < m ? base + 2 * w : m;
             const uint4 e = src[i];
-            const int pos = i < a1 ? (i - base) + count_less(src + a1, b1 - a1, e)
-                                   : (i - a1) + count_less(src + base, a1 - base, e);
+            const int pos = i < a1 ? (i - base) + count_less<false>(src + a1, b1 - a1, e)
+                                   : (i - a1) + count_less<true>(src + base, a1 - base, e);
             dst[base + pos] = e;
         }
         __syncthreads();

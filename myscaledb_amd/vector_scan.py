@@ -149,8 +149,10 @@ class VectorScanSegment:
         b = ctypes.c_size_t()
         check(lib.mqvs_segment_info(self._h, ctypes.byref(n), ctypes.byref(d), ctypes.byref(m),
                                     ctypes.byref(g), ctypes.byref(o), ctypes.byref(b)))
+        sp, pb, ok = ctypes.c_int32(), ctypes.c_size_t(), ctypes.c_int32()
+        check(lib.mqvs_segment_prefilter(self._h, ctypes.byref(sp), ctypes.byref(pb), ctypes.byref(ok)))
         return dict(n=n.value, d=d.value, metric=m.value, granule=g.value, row_offset=o.value,
-                    hbm_bytes=b.value)
+                    hbm_bytes=b.value, prefilter=sp.value, plane_bytes=pb.value, approx_ok=bool(ok.value))
 
     def device_rows_ptr(self) -> int:
         p = ctypes.c_void_p()

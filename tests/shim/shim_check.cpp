@@ -75,6 +75,132 @@ static int errors() {
     return 0;
 }
 
+// k = 8000 (above the old 4096 cap; the reference's max_search_result_window
+// is 10000), the 1-rank RCCL sharded search, the index seam, getRealBitmap and
+// the part cache.
+static int gpu_more(const std::string &dir, const std::vector<float> &rows, const std::vector<float> &q, int n,
+                    int d, int nq, int gran, const MI::PartScan &cos_part) {
+    // large k over a 12000-row L2 part
+    const int nl = 12000, kl = 8000;
+    std::vector<float> lrows((size_t)nl * d);
+    for (int i = 0; i < nl; ++i)
+        for (int j = 0; j < d; ++j) lrows[(size_t)i * d + j] = val(i + 3, j);
+    MI::PartScan lpart(lrows.data(), nl, d, MI::toMqvsMetric(Metric::L2), gran);
+    std::vector<int64_t> lid((size_t)nq * kl);
+    std::vector<float> ldist(lid.size());
+    lpart.search(q.data(), nq, kl, nullptr, nullptr, lid.data(), ldist.data());
+    write(dir + "/bigk_ids.bin", lid.data(), lid.size() * 8);
+    write(dir + "/bigk_dist.bin", ldist.data(), ldist.size() * 4);
+    std::printf("prefilter active %d\n", lpart.prefilterActive() ? 1 : 0);
+
+    // 1-rank communicator: the sharded search == the plain search
+    const int k = 12;
+    {
+        MI::ShardComm comm(1, 0, MI::ShardComm::uniqueId(), 0);
+        std::vector<int64_t> a((size_t)nq * k), b(a.size());
+        std::vector<float> da(a.size()), db(a.size());
+        cos_part.search(q.data(), nq, k, nullptr, nullptr, a.data(), da.data());
+        comm.search(cos_part, q.data(), nq, k, nullptr, nullptr, b.data(), db.data());
+        const bool same = std::memcmp(a.data(), b.data(), a.size() * 8) == 0 &&
+                          std::memcmp(da.data(), db.data(), da.size() * 4) == 0;
+        std::printf("sharded==search %d\n", same ? 1 : 0);
+        if (!same) return 1;
+    }
+
+    // index seam: build, search, computeTopDistanceSubset, row_ids_map remap
+    {
+        MI::GpuIndex index(lpart, "MSTG", "nlist=16");
+        std::vector<int64_t> a((size_t)nq * k), b(a.size()), c(a.size());
+        std::vector<float> da(a.size()), db(a.size()), dc(a.size());
+        index.search(q.data(), nq, d, k, "nprobe=16", nullptr, nullptr, false, a.data(), da.data());
+        write(dir + "/index_ids.bin", a.data(), a.size() * 8);
+        // two-stage: first stage 64 candidates, exact re-rank
+        const int nc = 64;
+        std::vector<int64_t> fs((size_t)nq * nc);
+        std::vector<float> fd(fs.size());
+        index.search(q.data(), nq, d, nc, "nprobe=16", nullptr, nullptr, true, fs.data(), fd.data());
+        index.computeTopDistanceSubset(q.data(), nq, fs.data(), nc, k, nullptr, c.data(), dc.data());
+        write(dir + "/index_fs_ids.bin", fs.data(), fs.size() * 8);
+        write(dir + "/index_rerank_ids.bin", c.data(), c.size() * 8);
+        write(dir + "/index_rerank_dist.bin", dc.data(), dc.size() * 4);
+        std::vector<uint64_t> map((size_t)nl);
+        for (int i = 0; i < nl; ++i) map[(size_t)i] = (uint64_t)(nl - 1 - i) * 2 + 5;
+        index.setRowIdsMap(map);
+        index.search(q.data(), nq, d, k, "nprobe=16", nullptr, nullptr, false, b.data(), db.data());
+        bool ok = std::memcmp(da.data(), db.data(), da.size() * 4) == 0;
+        for (size_t i = 0; i < a.size(); ++i) ok = ok && b[i] == (a[i] < 0 ? -1 : (int64_t)map[(size_t)a[i]]);
+        std::printf("row_ids_map %d\n", ok ? 1 : 0);
+        if (!ok) return 1;
+        try {
+            index.search(q.data(), nq, d + 1, k, "", nullptr, nullptr, false, b.data(), db.data());
+            return 1;
+        } catch (const DB::Exception &e) {
+            if (e.code() != DB::ErrorCodes::LOGICAL_ERROR) return 1;
+        }
+    }
+
+    // getRealBitmap: decoupled rows 0..9 from sources (0,1,0,1,...), row i -> i/2
+    {
+        std::vector<uint8_t> nf = {0xFF, 0x03};  // rows 0..9 set
+        std::vector<uint64_t> inv(10);
+        std::vector<uint8_t> src(10);
+        for (int i = 0; i < 10; ++i) {
+            inv[(size_t)i] = (uint64_t)(i / 2);
+            src[(size_t)i] = (uint8_t)(i % 2);
+        }
+        nf[0] = 0xAD;  // rows 0,2,3,5,7 set (+8,9 from nf[1])
+        auto old0 = MI::getRealBitmap(nf, 10, inv, src, 0, 5);  // even rows 0,2,8 -> 0,1,4
+        auto old1 = MI::getRealBitmap(nf, 10, inv, src, 1, 5);  // odd rows 3,5,7,9 -> 1,2,3,4
+        const bool ok = old0.size() == 1 && old0[0] == 0x13 && old1.size() == 1 && old1[0] == 0x1E;
+        std::printf("getRealBitmap %d (%02x %02x)\n", ok ? 1 : 0, old0.empty() ? 0 : old0[0],
+                    old1.empty() ? 0 : old1[0]);
+        if (!ok) return 1;
+    }
+
+    // part cache: load = getOrSet, holders pin, LRU eviction under the budget
+    {
+        auto make = [&](int seed) {
+            std::vector<float> r((size_t)n * d);
+            for (int i = 0; i < n; ++i)
+                for (int j = 0; j < d; ++j) r[(size_t)i * d + j] = val(i + seed, j);
+            return MI::PartScan(r.data(), n, d, MI::toMqvsMetric(Metric::L2), gran);
+        };
+        const size_t one = make(1).hbmBytes();
+        MI::PartCache cache(2 * one + one / 2);
+        int loads = 0;
+        auto loader = [&](int seed) {
+            return [&, seed] {
+                ++loads;
+                return std::make_pair(make(seed), std::shared_ptr<MI::GpuIndex>());
+            };
+        };
+        {
+            auto h0 = cache.load("db.t/all_1_1_0/v", loader(1));
+            auto h0b = cache.load("db.t/all_1_1_0/v", loader(1));  // hit: no second load
+            std::vector<int64_t> a((size_t)nq * k);
+            std::vector<float> da(a.size());
+            h0->part.search(q.data(), nq, k, nullptr, nullptr, a.data(), da.data());
+        }
+        cache.load("db.t/all_2_2_0/v", loader(2));
+        cache.get("db.t/all_1_1_0/v");               // part 1 most recently used
+        cache.load("db.t/all_3_3_0/v", loader(3));  // evicts part 2
+        const bool evicted = cache.get("db.t/all_2_2_0/v") == nullptr;
+        auto st = cache.stats();
+        auto held = cache.get("db.t/all_3_3_0/v");
+        cache.forceExpire("db.t/all_3_3_0/v");
+        auto st2 = cache.stats();
+        held.reset();
+        auto st3 = cache.stats();
+        const bool ok = loads == 3 && evicted && st.items == 2 && st.evictions == 1 && st2.expired_held == 1 &&
+                        st3.expired_held == 0 && st3.items == 1;
+        std::printf("cache %d (loads %d items %lld evictions %lld)\n", ok ? 1 : 0, loads, (long long)st.items,
+                    (long long)st.evictions);
+        if (!ok) return 1;
+    }
+    (void)rows;
+    return 0;
+}
+
 static int gpu(const std::string &dir) {
     const int n = 3000, d = 24, nq = 5, k = 12, gran = 512;
     std::vector<float> rows((size_t)n * d), q((size_t)nq * d);
@@ -119,7 +245,8 @@ static int gpu(const std::string &dir) {
         std::printf("null segment code=%d\n", e.code());
         if (e.code() != DB::ErrorCodes::BAD_ARGUMENTS) return 1;
     }
-    return same ? 0 : 1;
+    if (!same) return 1;
+    return gpu_more(dir, rows, q, n, d, nq, gran, part);
 }
 
 int main(int argc, char **argv) {

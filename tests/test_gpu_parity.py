@@ -379,7 +379,7 @@ def test_rerank_errors(mq):
     seg = mq.VectorScanSegment.from_rows(np.ones((10, 4), np.float32), metric="L2", granule=8)
     try:
         with pytest.raises(MqvsError) as e:
-            seg.rerank(np.ones((1, 4), np.float32), np.zeros((1, 5000), np.int64), 3)
+            seg.rerank(np.ones((1, 4), np.float32), np.zeros((1, 40000), np.int64), 3)
         assert e.value.name == "BAD_ARGUMENTS"
         with pytest.raises(MqvsError) as e:
             seg.rerank(np.ones((1, 4), np.float32), np.zeros((1, 5), np.int64), 3, "Cosine")
@@ -515,3 +515,50 @@ def test_cosine_shards_with_skipped_chunks(mq, nq):
             got_d.append(dd)
         mi, md = mq.merge_shards(np.stack(got_i), np.stack(got_d), "Cosine")
         assert_bitwise(mi, md, ids_o, dist_o, f"cosine shards nq={nq} filter={f is not None}")
+
+
+@pytest.mark.parametrize("d,metric,nq,k,ncand", [(40, "L2", 6, 6000, 10000), (37, "IP", 25, 64, 9000),
+                                                 (40, "L2", 21, 16384, 20000)])
+def test_rerank_large_candidate_lists(mq, d, metric, nq, k, ncand):
+    """More candidates than the LDS sort (> 4096, through global scratch) and
+    k up to 16384: == the oracle's knn over exactly those rows; -1 padding when
+    fewer valid candidates than k."""
+    n = 40000
+    m = O.L2 if metric == "L2" else O.IP
+    rows = O.generate(43, 1, 0, n, d)
+    q = O.generate(44, 1, 0, nq, d)
+    rng = np.random.default_rng(6)
+    cand = np.stack([rng.choice(n, ncand, replace=False) for _ in range(nq)]).astype(np.int64)
+    cand[:, 100:110] = -1
+    seg = mq.VectorScanSegment.from_rows(rows, metric=metric, granule=1024)
+    try:
+        ids_r, dist_r = seg.rerank(q, cand, k)
+    finally:
+        seg.free()
+    ids_o = np.empty((nq, k), np.int64)
+    dist_o = np.empty((nq, k), np.float32)
+    for i in range(nq):
+        valid = np.sort(cand[i][cand[i] >= 0])
+        io, do = O.knn(q[i:i + 1], rows[valid], k, m) if nq < 20 else O.knn(q, rows[valid], k, m)
+        j = 0 if nq < 20 else i
+        ids_o[i] = np.where(io[j] >= 0, valid[np.maximum(io[j], 0)], -1)
+        dist_o[i] = do[j]
+    assert_bitwise(ids_r, dist_r, ids_o, dist_o, f"rerank {ncand} candidates k {k}")
+
+
+def test_rerank_every_row_equals_search_cosine(mq):
+    """Cosine part of 30000 rows: re-ranking every row (shuffled, > 4096
+    candidates) == mqvs_search, query variant per chunk included."""
+    n, d, k = 30000, 64, 500
+    rows = O.generate(45, 2, 0, n, d)
+    seg = mq.VectorScanSegment.from_rows(rows, metric="Cosine", granule=2048)
+    try:
+        for nq in (3, 24):
+            q = O.generate(46, 2, 0, nq, d)
+            rng = np.random.default_rng(nq)
+            cand = np.stack([rng.permutation(n) for _ in range(nq)]).astype(np.int64)
+            ids_r, dist_r = seg.rerank(q, cand, k)
+            ids_s, dist_s = seg.search(q, k)
+            assert_bitwise(ids_r, dist_r, ids_s, dist_s, f"cosine rerank all rows nq {nq}")
+    finally:
+        seg.free()

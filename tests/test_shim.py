@@ -3,7 +3,9 @@ g++ against libmqvs.so, as a MyScaleDB maintainer would use it
 (INTEGRATION.md).  CPU: status -> DB::Exception code mapping, including
 tryBruteForceSearch's NOT_IMPLEMENTED for non-float metrics
 (BruteForceSearch.h:89).  GPU: tryBruteForceSearch / PartScan::scan / rerank
-through the shim vs the oracle."""
+through the shim vs the oracle; k = 8000 (PartScan::search), the 1-rank RCCL
+ShardComm, GpuIndex (search / computeTopDistanceSubset / setRowIdsMap),
+getRealBitmap and the PartCache (load / pin / evict / forceExpire)."""
 import os
 import subprocess
 
@@ -62,3 +64,22 @@ def test_shim_gpu_matches_oracle(shim_bin, tmp_path):
                           (np.arange(nq * k) // k)[keep].astype(np.uint32))
     assert np.array_equal(rd("scan_dist.bin", np.float32).view(np.uint32),
                           do.reshape(-1)[keep].view(np.uint32))
+    for tag in ("sharded==search 1", "row_ids_map 1", "getRealBitmap 1", "cache 1", "prefilter active 1"):
+        assert tag in r.stdout, r.stdout
+    # k = 8000 over the 12000-row L2 part == the oracle's vectorScanWithoutIndex
+    nl, kl = 12000, 8000
+    i, j = np.meshgrid(np.arange(nl) + 3, np.arange(d), indexing="ij")
+    lrows = (((i * 31 + j * 17) % 23) - 11).astype(np.float32)
+    io, do = O.vector_scan(lrows, q, kl, O.L2, gran)
+    assert np.array_equal(rd("bigk_ids.bin", np.int64).reshape(nq, kl), io)
+    assert np.array_equal(rd("bigk_dist.bin", np.float32).reshape(nq, kl).view(np.uint32), do.view(np.uint32))
+    # two-stage index search: the re-ranked distances are the exact ones of the
+    # first stage's rows (oracle knn over those rows), best first
+    fs = rd("index_fs_ids.bin", np.int64).reshape(nq, 64)
+    ri = rd("index_rerank_ids.bin", np.int64).reshape(nq, 12)
+    rdist = rd("index_rerank_dist.bin", np.float32).reshape(nq, 12)
+    for qi in range(nq):
+        cand = fs[qi][fs[qi] >= 0]
+        ki, kd = O.knn(q[qi:qi + 1], lrows[cand], 12, O.L2)
+        assert np.array_equal(ri[qi], cand[ki[0]]), qi
+        assert np.array_equal(rdist[qi].view(np.uint32), kd[0].view(np.uint32)), qi
