@@ -21,11 +21,12 @@
 //                    into an XOR-swizzled image (conflict-free ds_read_b128);
 //                    PROBE / APPEND epilogues as the fp32 kernels, on the
 //                    approximate value.
-//   k_probe_select_approx  k-th best approximate value of the probe rows ->
+//   k_probe_select_wide  k-th best approximate value of the probe rows ->
 //                    per-query APPEND threshold (k-th -/+ 2B) + candidates.
-//   k_rerank_select  per query: k-th best approximate value among the
-//                    candidates, keep those within 2B, exact fp32 chain for
-//                    each, bitonic sort by the reference key, emit top-k.
+//   k_survivors      per query: k-th best approximate value among the
+//                    candidates, keep those within 2B; their exact fp32
+//                    chains are computed over the whole chip and sorted by
+//                    the reference key (kernels_rerank.hip).
 #include "select_common.h"
 
 namespace mqvs {
@@ -180,34 +181,59 @@ void launch_query_bound(const ScanParams &p, int metric, int split, const float 
 
 
 // ---------------------------------------------------------------------------
+// k-th best approximate value of each query's probe row -> its APPEND
+// threshold (k-th -/+ 2B) and the probe rows that pass it.  1024 threads per
+// query, 16 values in flight per thread (float4 x 4) in every radix pass and
+// in the append: the probe row (L2-resident) is read five times, never with
+// one dependent load in flight per thread.
+constexpr int kPsThreads = 1024;
+
 template <int METRIC>
-__global__ __launch_bounds__(SEL_THREADS) void k_probe_select_approx(const float *probe, int64_t P,
-                                                                    int64_t ld, int k,
-                                                                    const float *bq, float *thr,
-                                                                    int *cand_count, Cand *cand,
-                                                                    int cap, const int32_t *row_list) {
+__global__ __launch_bounds__(kPsThreads) void k_probe_select_wide(const float *probe, int64_t P, int64_t ld, int k,
+                                                                  const float *bq, float *thr, int *cand_count,
+                                                                  Cand *cand, int cap, const int32_t *row_list) {
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh[4];
-    const int q = blockIdx.x;
+    const int q = blockIdx.x, t = threadIdx.x;
     const float *row = probe + (int64_t)q * ld;
-    // block_radix_select_rows applies key32 (with validity); use a plain
-    // order key here
-    auto keyof = [&](int64_t i) { return okey<METRIC>(row[i]); };
-    const uint32_t th = block_radix_select(keyof, P, k, hist, sh);
-    float t;
-    if (th == 0xFFFFFFFEu)
-        t = (METRIC == MQVS_METRIC_L2) ? __builtin_inff() : -__builtin_inff();
+    uint32_t prefix = 0, mask = 0, kk = (uint32_t)k;
+    bool none = false;
+    for (int pass = 0; pass < 4; ++pass) {
+        const int shift = 24 - 8 * pass;
+        if (t < 256) hist[t] = 0;
+        __syncthreads();
+        RunHist rh;
+        for_each_f4<kPsThreads>(row, P, [&](int64_t, float raw) {
+            const uint32_t key = okey<METRIC>(raw);
+            if (key != 0xFFFFFFFFu && (key & mask) == prefix) rh.add(hist, (key >> shift) & 255u);
+        });
+        rh.flush(hist);
+        __syncthreads();
+        hist_pick(hist, kk, pass == 0, sh);
+        __syncthreads();
+        if (sh[0]) {
+            none = true;
+            break;
+        }
+        prefix |= sh[1] << shift;
+        mask |= 255u << shift;
+        kk -= sh[2];
+        __syncthreads();
+    }
+    float tt;
+    if (none)
+        tt = (METRIC == MQVS_METRIC_L2) ? __builtin_inff() : -__builtin_inff();
     else
-        t = widen<METRIC>(okey_value<METRIC>(th), bq[q]);
-    if (threadIdx.x == 0) thr[q] = t;
-    for_each_f4(row, P, [&](int64_t i, float raw) {
-        const bool take = (METRIC == MQVS_METRIC_L2) ? (raw <= t) : (raw >= t);
+        tt = widen<METRIC>(okey_value<METRIC>(prefix), bq[q]);
+    if (t == 0) thr[q] = tt;
+    for_each_f4<kPsThreads>(row, P, [&](int64_t i, float raw) {
+        const bool take = (METRIC == MQVS_METRIC_L2) ? (raw <= tt) : (raw >= tt);
         if (take) {
             const int pos = atomicAdd(&cand_count[q], 1);
             if (pos < cap) {
                 Cand c;
                 c.raw = raw;
-                c.row = row_list ? (uint32_t)row_list[i] : (uint32_t)i;  // column = scan position
+                c.row = row_list ? (uint32_t)row_list[i] : (uint32_t)i;
                 cand[(int64_t)q * cap + pos] = c;
             }
         }
@@ -218,8 +244,8 @@ template <int M>
 static void probe_select_approx_t(const float *probe, int64_t P, int64_t ld, int nq, int k,
                                   const float *bq, float *thr, int *cc, Cand *cand, int cap,
                                   const int32_t *row_list, hipStream_t s) {
-    hipLaunchKernelGGL(k_probe_select_approx<M>, dim3(nq), dim3(SEL_THREADS), 0, s, probe, P, ld, k,
-                       bq, thr, cc, cand, cap, row_list);
+    hipLaunchKernelGGL(k_probe_select_wide<M>, dim3(nq), dim3(kPsThreads), 0, s, probe, P, ld, k, bq, thr, cc, cand,
+                       cap, row_list);
 }
 
 void launch_probe_select_approx(const float *probe, int64_t P, int64_t ld, int nq, int k,
@@ -235,89 +261,25 @@ void launch_probe_select_approx(const float *probe, int64_t P, int64_t ld, int n
 #undef MQVS_PSA
 }
 
-// ---------------------------------------------------------------------------
-// exact value for one (query, row): the BLAS-branch element (fma chain), or
-// for nq < 20 (DIRECT) faiss's sequential product-then-add fvec formula in
-// kernels_scan.hip k_scan_small's order
-template <int METRIC, bool DIRECT>
-__device__ inline float exact_value(const ScanParams &p, int q, int64_t row) {
-    const int64_t chunk = p.chunk_rows > 0 ? row / p.chunk_rows : 0;
-    const int ord = chunk_ordinal(p, chunk);
-    const int v = variant_of(p, q, ord < 0 ? 0 : ord);
-    const int64_t qs = (int64_t)((p.d + 31) / 32 * 32);
-    const float *x = p.qvars + ((int64_t)q * p.maxv + v) * qs;
-    const float *y = p.rows + row * p.d;
-    float acc = 0.0f;
-    if (DIRECT) {
-        // element order 0..d-1, product then add (16-B loads when aligned)
-        auto step = [&](float a, float b) {
-            if (METRIC == MQVS_METRIC_L2) {
-                const float e = a - b;
-                acc = acc + e * e;
-            } else {
-                acc = acc + a * b;
-            }
-        };
-        int i = 0;
-        if ((p.d & 3) == 0) {
-            const float4 *x4 = reinterpret_cast<const float4 *>(x);
-            const float4 *y4 = reinterpret_cast<const float4 *>(y);
-            for (; i < (p.d >> 2); ++i) {
-                const float4 a = y4[i], b = x4[i];
-                step(a.x, b.x);
-                step(a.y, b.y);
-                step(a.z, b.z);
-                step(a.w, b.w);
-            }
-            return acc;
-        }
-        for (; i < p.d; ++i) step(y[i], x[i]);
-        return acc;
-    }
-    if ((p.d & 3) == 0) {
-        const float4 *x4 = reinterpret_cast<const float4 *>(x);
-        const float4 *y4 = reinterpret_cast<const float4 *>(y);
-        const int n4 = p.d >> 2;
-#pragma unroll 4
-        for (int i = 0; i < n4; ++i) {
-            const float4 a = x4[i], b = y4[i];
-            acc = fmaf(a.x, b.x, acc);
-            acc = fmaf(a.y, b.y, acc);
-            acc = fmaf(a.z, b.z, acc);
-            acc = fmaf(a.w, b.w, acc);
-        }
-    } else {
-        for (int i = 0; i < p.d; ++i) acc = fmaf(x[i], y[i], acc);
-    }
-    if (METRIC == MQVS_METRIC_L2) {
-        float d = (p.qnorms[q] + p.row_norms[row]) - 2.0f * acc;
-        if (d < 0) d = 0;
-        return d;
-    }
-    return acc;
-}
-
-// scratch (k > kSortCap): 2 kLargeCap records per query; more than kSortCap
-// survivors are then re-ranked and sorted in global memory (global_sort).
-template <int METRIC, bool DIRECT>
-__global__ __launch_bounds__(SEL_THREADS) void k_rerank_select(ScanParams p, const float *bq, int k,
-                                                              int64_t id_offset, int64_t *out_ids,
-                                                              float *out_dist, int *overflow, uint4 *scratch) {
-    extern __shared__ __attribute__((aligned(16))) uint4 recs[];  // kSortCap records
+// Survivors of the bound, per query (one workgroup each): the k-th best
+// approximate value a_k among the candidates, then every candidate within 2B
+// of it (widen) is compacted into surv[q * rs ...] (at most lcap; more sets
+// overflow bit 4, fewer than the appended candidates' cap bit 1).  Stats:
+// overflow[1] = max survivors, [2] = their sum, [3] = max candidates.
+template <int METRIC>
+__global__ __launch_bounds__(SEL_THREADS) void k_survivors(ScanParams p, const float *bq, int k, int *overflow,
+                                                          uint32_t *surv, int *scnt, int lcap, int64_t rs) {
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh[4];
     __shared__ int s_cnt;
     const int q = blockIdx.x;
-    uint4 *g = scratch ? scratch + (int64_t)q * 2 * kLargeCap : nullptr;
-    const int lcap = g ? kLargeCap : kSortCap;
     int n = p.cand_count[q];
     if (n > p.cand_cap) {
         if (threadIdx.x == 0) atomicOr(overflow, 1);
         n = p.cand_cap;
     }
     const Cand *c = p.cand + (int64_t)q * p.cand_cap;
-    auto keyof = [&](int64_t i) { return okey<METRIC>(c[i].raw); };
-    const uint32_t th = block_radix_select(keyof, n, k, hist, sh);
+    const uint32_t th = block_radix_select_mlp([&](int64_t i) { return okey<METRIC>(c[i].raw); }, n, k, hist, sh);
     float t;
     if (th == 0xFFFFFFFEu)
         t = (METRIC == MQVS_METRIC_L2) ? __builtin_inff() : -__builtin_inff();
@@ -325,107 +287,51 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_select(ScanParams p, con
         t = widen<METRIC>(okey_value<METRIC>(th), bq[q]);
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
+    uint32_t *out = surv + (int64_t)q * rs;
     for (int i = threadIdx.x; i < n; i += SEL_THREADS) {
         const Cand e = c[i];
         const bool take = (METRIC == MQVS_METRIC_L2) ? (e.raw <= t) : (e.raw >= t);
         if (take) {
             const int pos = atomicAdd(&s_cnt, 1);
-            if (pos < kSortCap) recs[pos] = make_uint4(0, 0, 0, e.row);
-            if (g && pos < kLargeCap) g[pos] = make_uint4(0, 0, 0, e.row);
+            if (pos < lcap) out[pos] = e.row;
         }
     }
     __syncthreads();
-    int m = s_cnt;
     if (threadIdx.x == 0) {
-        atomicMax(overflow + 1, m);      // survivors of the bound (stats)
+        const int m = s_cnt;
+        atomicMax(overflow + 1, m);
         atomicAdd(overflow + 2, m);
-        atomicMax(overflow + 3, n);      // candidates before it
-    }
-    if (m > lcap) {
-        if (threadIdx.x == 0) atomicOr(overflow, 4);
-        m = lcap;
-    }
-    // exact re-rank of the survivors (in LDS, or in the global scratch)
-    uint4 *rr = m > kSortCap ? g : recs;
-    for (int i = threadIdx.x; i < m; i += SEL_THREADS) {
-        const uint32_t row = rr[i].w;
-        const float raw = exact_value<METRIC, DIRECT>(p, q, row);
-        uint4 r;
-        r.x = key32<METRIC>(raw);
-        r.w = row;
-        if (METRIC == MQVS_METRIC_COSINE) {
-            r.y = p.chunk_rows > 0 ? (uint32_t)((int64_t)row / p.chunk_rows) : 0u;
-            r.z = ~ord_asc(raw);
-        } else {
-            r.y = 0;
-            r.z = 0;
-        }
-        rr[i] = r;
-    }
-    const float pad = (METRIC == MQVS_METRIC_IP) ? 1.17549435e-38f
-                      : (METRIC == kMetricIpRaw) ? -3.40282347e+38f
-                                                 : 3.40282347e+38f;
-    if (m > kSortCap) {
-        __syncthreads();
-        const uint4 *sorted = global_sort(g, g + kLargeCap, m, recs);
-        for (int i = threadIdx.x; i < k; i += SEL_THREADS) {
-            int64_t id = -1;
-            float dist = pad;
-            if (i < m && sorted[i].x != 0xFFFFFFFFu) {
-                id = (int64_t)sorted[i].w + id_offset;
-                dist = key_to_value(METRIC, sorted[i].x);
-            }
-            out_ids[(int64_t)q * k + i] = id;
-            out_dist[(int64_t)q * k + i] = dist;
-        }
-        return;
-    }
-    int N = 1;
-    while (N < m) N <<= 1;
-    for (int i = m + threadIdx.x; i < N; i += SEL_THREADS)
-        recs[i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
-    __syncthreads();
-    block_bitonic_sort(recs, N);
-    for (int i = threadIdx.x; i < k; i += SEL_THREADS) {
-        int64_t id = -1;
-        float dist = pad;
-        if (i < N && recs[i].x != 0xFFFFFFFFu) {
-            id = (int64_t)recs[i].w + id_offset;
-            dist = key_to_value(METRIC, recs[i].x);
-        }
-        out_ids[(int64_t)q * k + i] = id;
-        out_dist[(int64_t)q * k + i] = dist;
+        atomicMax(overflow + 3, n);
+        if (m > lcap) atomicOr(overflow, 4);
+        scnt[q] = m < lcap ? m : lcap;
     }
 }
 
-template <int M>
-static void rerank_select_t(const ScanParams &p, const float *bq, int k, int64_t id_offset,
-                            int64_t *out_ids, float *out_dist, int *overflow, uint4 *scratch, hipStream_t s) {
-    if (p.nq < kBlasThreshold)
-        hipLaunchKernelGGL((k_rerank_select<M, true>), dim3(p.nq), dim3(SEL_THREADS), kSortCap * sizeof(uint4),
-                           s, p, bq, k, id_offset, out_ids, out_dist, overflow, scratch);
-    else
-        hipLaunchKernelGGL((k_rerank_select<M, false>), dim3(p.nq), dim3(SEL_THREADS), kSortCap * sizeof(uint4),
-                           s, p, bq, k, id_offset, out_ids, out_dist, overflow, scratch);
-}
-
-void launch_rerank_select(const ScanParams &p, int metric, const float *bq, int k,
-                          int64_t id_offset, int64_t *out_ids, float *out_dist, int *overflow,
-                          uint4 *scratch, hipStream_t s) {
+// Exact re-rank of the survivors (k_survivors -> k_exact_records over the
+// whole chip -> k_sort_emit, kernels_rerank.hip).  rs: survivor / record
+// slots per query (2 lcap when lcap > kSortCap: global_sort's second buffer).
+void launch_rerank_select(const ScanParams &p, int metric, const float *bq, int k, int64_t id_offset,
+                          int64_t *out_ids, float *out_dist, int *overflow, uint32_t *surv, int *scnt,
+                          uint4 *recs, int lcap, int64_t rs, hipStream_t s) {
     switch (metric) {
         case MQVS_METRIC_L2:
-            rerank_select_t<MQVS_METRIC_L2>(p, bq, k, id_offset, out_ids, out_dist, overflow, scratch, s);
+            hipLaunchKernelGGL(k_survivors<MQVS_METRIC_L2>, dim3(p.nq), dim3(SEL_THREADS), 0, s, p, bq, k, overflow,
+                               surv, scnt, lcap, rs);
             break;
         case MQVS_METRIC_IP:
-            rerank_select_t<MQVS_METRIC_IP>(p, bq, k, id_offset, out_ids, out_dist, overflow, scratch, s);
+            hipLaunchKernelGGL(k_survivors<MQVS_METRIC_IP>, dim3(p.nq), dim3(SEL_THREADS), 0, s, p, bq, k, overflow,
+                               surv, scnt, lcap, rs);
             break;
         case MQVS_METRIC_COSINE:
-            rerank_select_t<MQVS_METRIC_COSINE>(p, bq, k, id_offset, out_ids, out_dist, overflow, scratch, s);
+            hipLaunchKernelGGL(k_survivors<MQVS_METRIC_COSINE>, dim3(p.nq), dim3(SEL_THREADS), 0, s, p, bq, k,
+                               overflow, surv, scnt, lcap, rs);
             break;
         default:
-            rerank_select_t<kMetricIpRaw>(p, bq, k, id_offset, out_ids, out_dist, overflow, scratch, s);
+            hipLaunchKernelGGL(k_survivors<kMetricIpRaw>, dim3(p.nq), dim3(SEL_THREADS), 0, s, p, bq, k, overflow,
+                               surv, scnt, lcap, rs);
             break;
     }
+    launch_exact_rerank(p, metric, surv, scnt, rs, lcap, recs, k, id_offset, out_ids, out_dist, s);
 }
 
 }  // namespace mqvs

@@ -94,7 +94,9 @@ __device__ inline void rerank_emit(uint4 *recs, uint4 *g, int ncand, int k, int 
         __syncthreads();
         block_bitonic_sort(recs, N);
     }
-    const float pad = (METRIC == MQVS_METRIC_IP) ? 1.17549435e-38f : 3.40282347e+38f;
+    const float pad = (METRIC == MQVS_METRIC_IP) ? 1.17549435e-38f
+                      : (METRIC == kMetricIpRaw) ? -3.40282347e+38f
+                                                 : 3.40282347e+38f;
     for (int i = threadIdx.x; i < k; i += SEL_THREADS) {
         int64_t id = -1;
         float dist = pad;
@@ -131,8 +133,102 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids(ScanParams p, const 
 // cache lines), prefetching the next tile into registers, and stages them
 // in LDS (row stride 33 floats: conflict-free column reads); each lane then
 // runs its chain from LDS.  Lanes of a wave run in lockstep, so the wave's
-// own LDS tile needs no barrier.
+// own LDS tile needs no barrier.  row < 0: no candidate (returns 0).
+// tile: this wave's 64 x kRrStride floats of LDS.
 constexpr int kRrStride = 33;
+
+template <int METRIC, bool DIRECT>
+__device__ inline float wave_exact(const ScanParams &p, int q, int64_t row, float *tile) {
+    const int lane = threadIdx.x & 63;
+    const int d = p.d;
+    const int64_t qs = (int64_t)((d + 31) / 32 * 32);
+    const int ntiles = (d + 31) / 32;
+    const float *x = p.qvars;
+    if (row >= 0) {
+        const int64_t chunk = p.chunk_rows > 0 ? row / p.chunk_rows : 0;
+        const int ord = chunk_ordinal(p, chunk);
+        const int v = variant_of(p, q, ord < 0 ? 0 : ord);
+        x = p.qvars + ((int64_t)q * p.maxv + v) * qs;
+    }
+    float acc = 0.0f;
+    if (__ballot(row >= 0)) {
+        // rows this lane loads: slot j*8 + lane/8, float4 column lane%8
+        int64_t lrow[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) lrow[j] = __shfl(row, j * 8 + (lane >> 3));
+        float4 ry[8], rx[8];
+        auto load = [&](int t) {
+            const int col = t * 32 + (lane & 7) * 4;
+#pragma unroll
+            for (int j = 0; j < 8; ++j)
+                ry[j] = (lrow[j] >= 0 && col < d) ? *reinterpret_cast<const float4 *>(p.rows + lrow[j] * d + col)
+                                                  : make_float4(0.f, 0.f, 0.f, 0.f);
+            // the lane's own query slice (variant of its row's chunk)
+#pragma unroll
+            for (int j = 0; j < 8; ++j) rx[j] = *reinterpret_cast<const float4 *>(x + t * 32 + 4 * j);
+        };
+        load(0);
+        for (int t = 0; t < ntiles; ++t) {
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float *dst = tile + (j * 8 + (lane >> 3)) * kRrStride + (lane & 7) * 4;
+                dst[0] = ry[j].x;
+                dst[1] = ry[j].y;
+                dst[2] = ry[j].z;
+                dst[3] = ry[j].w;
+            }
+            float xt[32];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                xt[4 * j] = rx[j].x;
+                xt[4 * j + 1] = rx[j].y;
+                xt[4 * j + 2] = rx[j].z;
+                xt[4 * j + 3] = rx[j].w;
+            }
+            if (t + 1 < ntiles) load(t + 1);
+            __builtin_amdgcn_wave_barrier();
+            const float *mine = tile + lane * kRrStride;
+            const int cols = min(32, d - t * 32);
+            if (cols == 32) {
+#pragma unroll
+                for (int cc = 0; cc < 32; ++cc) {
+                    const float a = mine[cc], b = xt[cc];
+                    if (DIRECT) {
+                        if (METRIC == MQVS_METRIC_L2) {
+                            const float e = a - b;
+                            acc = acc + e * e;
+                        } else {
+                            acc = acc + a * b;
+                        }
+                    } else {
+                        acc = fmaf(b, a, acc);
+                    }
+                }
+            } else {
+                for (int cc = 0; cc < cols; ++cc) {
+                    const float a = mine[cc], b = x[t * 32 + cc];
+                    if (DIRECT) {
+                        if (METRIC == MQVS_METRIC_L2) {
+                            const float e = a - b;
+                            acc = acc + e * e;
+                        } else {
+                            acc = acc + a * b;
+                        }
+                    } else {
+                        acc = fmaf(b, a, acc);
+                    }
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    float raw = acc;
+    if (!DIRECT && METRIC == MQVS_METRIC_L2 && row >= 0) {
+        raw = (p.qnorms[q] + p.row_norms[row]) - 2.0f * acc;
+        if (raw < 0) raw = 0;
+    }
+    return raw;
+}
 
 template <int METRIC, bool DIRECT>
 __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids_tiled(ScanParams p, const int64_t *cand, int ncand,
@@ -142,13 +238,10 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids_tiled(ScanParams p, 
     uint4 *recs = reinterpret_cast<uint4 *>(smem);
     uint4 *g = scratch ? scratch + (int64_t)blockIdx.x * 2 * ncand : nullptr;
     uint4 *dst = g ? g : recs;
-    const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+    const int wv = threadIdx.x >> 6;
     float *tile = reinterpret_cast<float *>(smem + (size_t)nrec * sizeof(uint4)) + wv * 64 * kRrStride;
     const int q = blockIdx.x;
     const int64_t *c = cand + (int64_t)q * ncand;
-    const int d = p.d;
-    const int64_t qs = (int64_t)((d + 31) / 32 * 32);
-    const int ntiles = (d + 31) / 32;
     for (int cb = 0; cb < ncand; cb += SEL_THREADS) {
         const int i = cb + threadIdx.x;
         int64_t row = -1;
@@ -156,94 +249,130 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids_tiled(ScanParams p, 
             row = c[i];
             if (!(row >= 0 && row < p.n && row_valid(p, row))) row = -1;
         }
-        const float *x = p.qvars;
-        if (row >= 0) {
-            const int64_t chunk = p.chunk_rows > 0 ? row / p.chunk_rows : 0;
-            const int ord = chunk_ordinal(p, chunk);
-            const int v = variant_of(p, q, ord < 0 ? 0 : ord);
-            x = p.qvars + ((int64_t)q * p.maxv + v) * qs;
-        }
-        float acc = 0.0f;
-        if (__ballot(row >= 0)) {
-            // rows this lane loads: slot j*8 + lane/8, float4 column lane%8
-            int64_t lrow[8];
-#pragma unroll
-            for (int j = 0; j < 8; ++j) lrow[j] = __shfl(row, j * 8 + (lane >> 3));
-            float4 ry[8], rx[8];
-            auto load = [&](int t) {
-                const int col = t * 32 + (lane & 7) * 4;
-#pragma unroll
-                for (int j = 0; j < 8; ++j)
-                    ry[j] = (lrow[j] >= 0 && col < d)
-                                ? *reinterpret_cast<const float4 *>(p.rows + lrow[j] * d + col)
-                                : make_float4(0.f, 0.f, 0.f, 0.f);
-                // the lane's own query slice (variant of its row's chunk)
-#pragma unroll
-                for (int j = 0; j < 8; ++j) rx[j] = *reinterpret_cast<const float4 *>(x + t * 32 + 4 * j);
-            };
-            load(0);
-            for (int t = 0; t < ntiles; ++t) {
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    float *dst = tile + (j * 8 + (lane >> 3)) * kRrStride + (lane & 7) * 4;
-                    dst[0] = ry[j].x;
-                    dst[1] = ry[j].y;
-                    dst[2] = ry[j].z;
-                    dst[3] = ry[j].w;
-                }
-                float xt[32];
-#pragma unroll
-                for (int j = 0; j < 8; ++j) {
-                    xt[4 * j] = rx[j].x;
-                    xt[4 * j + 1] = rx[j].y;
-                    xt[4 * j + 2] = rx[j].z;
-                    xt[4 * j + 3] = rx[j].w;
-                }
-                if (t + 1 < ntiles) load(t + 1);
-                __builtin_amdgcn_wave_barrier();
-                const float *mine = tile + lane * kRrStride;
-                const int cols = min(32, d - t * 32);
-                if (cols == 32) {
-#pragma unroll
-                    for (int cc = 0; cc < 32; ++cc) {
-                        const float a = mine[cc], b = xt[cc];
-                        if (DIRECT) {
-                            if (METRIC == MQVS_METRIC_L2) {
-                                const float e = a - b;
-                                acc = acc + e * e;
-                            } else {
-                                acc = acc + a * b;
-                            }
-                        } else {
-                            acc = fmaf(b, a, acc);
-                        }
-                    }
-                } else {
-                    for (int cc = 0; cc < cols; ++cc) {
-                        const float a = mine[cc], b = x[t * 32 + cc];
-                        if (DIRECT) {
-                            if (METRIC == MQVS_METRIC_L2) {
-                                const float e = a - b;
-                                acc = acc + e * e;
-                            } else {
-                                acc = acc + a * b;
-                            }
-                        } else {
-                            acc = fmaf(b, a, acc);
-                        }
-                    }
-                }
-                __builtin_amdgcn_wave_barrier();
-            }
-        }
-        float raw = acc;
-        if (!DIRECT && METRIC == MQVS_METRIC_L2 && row >= 0) {
-            raw = (p.qnorms[q] + p.row_norms[row]) - 2.0f * acc;
-            if (raw < 0) raw = 0;
-        }
+        const float raw = wave_exact<METRIC, DIRECT>(p, q, row, tile);
         if (i < ncand) dst[i] = rerank_rec<METRIC>(p, row, raw);
     }
     rerank_emit<METRIC>(recs, g, ncand, k, q, id_offset, out_ids, out_dist);
+}
+
+// ---------------------------------------------------------------------------
+// Exact re-rank of the pre-filter's survivors, spread over the whole chip
+// (mqvs_search path 2): query q's cnt[q] survivor rows are surv[q * rs + i];
+// their records go to recs[q * rs + i].  Work items (chunk of 256
+// survivors, query), chunk-major, walked grid-stride.
+template <int METRIC, bool DIRECT>
+__global__ __launch_bounds__(SEL_THREADS) void k_exact_records(ScanParams p, const uint32_t *surv, const int *cnt,
+                                                              int64_t rs, int chunks, uint4 *recs) {
+    __shared__ float tiles[(SEL_THREADS / 64) * 64 * kRrStride];
+    float *tile = tiles + (threadIdx.x >> 6) * 64 * kRrStride;
+    const int items = p.nq * chunks;
+    for (int it = blockIdx.x; it < items; it += gridDim.x) {
+        const int c = it / p.nq, q = it - c * p.nq;
+        const int m = cnt[q];
+        if (c * SEL_THREADS >= m) continue;  // uniform over the block
+        const int i = c * SEL_THREADS + threadIdx.x;
+        const int64_t row = i < m ? (int64_t)surv[(int64_t)q * rs + i] : -1;
+        float raw;
+        if ((p.d & 3) == 0)
+            raw = wave_exact<METRIC, DIRECT>(p, q, row, tile);
+        else
+            raw = row >= 0 ? cand_value<METRIC, DIRECT>(p, q, row) : 0.f;
+        if (i < m) recs[(int64_t)q * rs + i] = rerank_rec<METRIC>(p, row, raw);
+    }
+}
+
+// Sort each query's cnt[q] records (recs[q * rs ...]; above kSortCap through
+// global_sort with the next cnt[q] records as the second buffer) and write
+// its top k.
+// Top k of up to kSortCap records without sorting them all: the k-th
+// smallest distance key X by radix select (LDS reads), the records with key
+// <= X (k plus ties at X) compacted, and each of those placed by counting the
+// smaller ones (full record order; keys are unique per row).  More than
+// kSelCap records at <= X (mass ties): the bitonic sort of all of them.
+constexpr int kSelCap = SEL_THREADS;
+
+template <int METRIC>
+__global__ __launch_bounds__(SEL_THREADS) void k_sort_emit(uint4 *recs, const int *cnt, int64_t rs, int k,
+                                                          int64_t id_offset, int64_t *out_ids, float *out_dist) {
+    extern __shared__ __attribute__((aligned(16))) uint4 lrec[];  // kSortCap + kSelCap records
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t sh[4];
+    __shared__ int s_c;
+    const int q = blockIdx.x;
+    const int m = cnt[q];
+    uint4 *g = recs + (int64_t)q * rs;
+    if (m > kSortCap) {
+        rerank_emit<METRIC>(lrec, g, m, k, q, id_offset, out_ids, out_dist);
+        return;
+    }
+    uint4 *sel = lrec + kSortCap;
+    if (threadIdx.x == 0) s_c = 0;
+    for (int i = threadIdx.x; i < m; i += SEL_THREADS) lrec[i] = g[i];
+    __syncthreads();
+    const uint32_t X = block_radix_select([&](int64_t i) { return lrec[i].x; }, m, k, hist, sh);
+    // (0xFFFFFFFE: fewer than k valid records -- all valid ones qualify)
+    for (int i = threadIdx.x; i < m; i += SEL_THREADS) {
+        const uint4 r = lrec[i];
+        if (r.x != 0xFFFFFFFFu && r.x <= X) {
+            const int pos = atomicAdd(&s_c, 1);
+            if (pos < kSelCap) sel[pos] = r;
+        }
+    }
+    __syncthreads();
+    const int c = s_c;
+    if (c > kSelCap) {
+        rerank_emit<METRIC>(lrec, nullptr, m, k, q, id_offset, out_ids, out_dist);
+        return;
+    }
+    if ((int)threadIdx.x < c) {
+        const uint4 r = sel[threadIdx.x];
+        int rank = 0, j = 0;
+        for (; j + 4 <= c; j += 4) {
+            const uint4 a0 = sel[j], a1 = sel[j + 1], a2 = sel[j + 2], a3 = sel[j + 3];
+            rank += (rec_less(a0, r) ? 1 : 0) + (rec_less(a1, r) ? 1 : 0) + (rec_less(a2, r) ? 1 : 0) +
+                    (rec_less(a3, r) ? 1 : 0);
+        }
+        for (; j < c; ++j) rank += rec_less(sel[j], r) ? 1 : 0;
+        if (rank < k) {
+            out_ids[(int64_t)q * k + rank] = (int64_t)r.w + id_offset;
+            out_dist[(int64_t)q * k + rank] = key_to_value(METRIC, r.x);
+        }
+    }
+    const float pad = (METRIC == MQVS_METRIC_IP) ? 1.17549435e-38f
+                      : (METRIC == kMetricIpRaw) ? -3.40282347e+38f
+                                                 : 3.40282347e+38f;
+    for (int i = c + threadIdx.x; i < k; i += SEL_THREADS) {
+        out_ids[(int64_t)q * k + i] = -1;
+        out_dist[(int64_t)q * k + i] = pad;
+    }
+}
+
+void launch_exact_rerank(const ScanParams &p, int metric, const uint32_t *surv, const int *cnt, int64_t rs,
+                         int cap, uint4 *recs, int k, int64_t id_offset, int64_t *out_ids, float *out_dist,
+                         hipStream_t s) {
+    const int chunks = (cap + SEL_THREADS - 1) / SEL_THREADS;
+    const int items = p.nq * chunks;
+    const int grid = std::max(1, std::min(items, 4096));
+    const bool direct = p.nq < kBlasThreshold;
+#define MQVS_ER(M)                                                                                                \
+    do {                                                                                                          \
+        if (direct)                                                                                               \
+            hipLaunchKernelGGL((k_exact_records<M, true>), dim3(grid), dim3(SEL_THREADS), 0, s, p, surv, cnt, rs, \
+                               chunks, recs);                                                                     \
+        else                                                                                                      \
+            hipLaunchKernelGGL((k_exact_records<M, false>), dim3(grid), dim3(SEL_THREADS), 0, s, p, surv, cnt,    \
+                               rs, chunks, recs);                                                                 \
+        hipLaunchKernelGGL((k_sort_emit<M>), dim3(p.nq), dim3(SEL_THREADS), (kSortCap + kSelCap) * sizeof(uint4), s, \
+                           recs, cnt,                                                                             \
+                           rs, k, id_offset, out_ids, out_dist);                                                  \
+    } while (0)
+    switch (metric) {
+        case MQVS_METRIC_L2: MQVS_ER(MQVS_METRIC_L2); break;
+        case MQVS_METRIC_IP: MQVS_ER(MQVS_METRIC_IP); break;
+        case MQVS_METRIC_COSINE: MQVS_ER(MQVS_METRIC_COSINE); break;
+        default: MQVS_ER(kMetricIpRaw); break;
+    }
+#undef MQVS_ER
 }
 
 template <int M, bool DIRECT>

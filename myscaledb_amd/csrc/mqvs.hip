@@ -41,7 +41,8 @@ struct Workspace {
     static constexpr int kSegEv = 64;
     hipEvent_t seg_ev[kSegEv] = {};  // per main-scan segment: start, end
     DevBuf queries, qvars, qnorms, qmu, qlam, status, filter, exists, ord, probe, tau, count, cand,
-        overflow, out_ids, out_dist, misc, qhi, bq, thr, cand2, count2, gcount, goff, glist, large, sticky;
+        overflow, out_ids, out_dist, misc, qhi, bq, thr, cand2, count2, gcount, goff, glist, large, sticky, surv,
+        recs;
     int *host_flags = nullptr;  // pinned
     void init() {
         if (stream) return;
@@ -53,7 +54,8 @@ struct Workspace {
     void release() {
         DevBuf *all[] = {&queries, &qvars, &qnorms, &qmu,  &qlam,   &status,  &filter,   &exists, &ord,
                          &probe,   &tau,   &count,  &cand, &overflow, &out_ids, &out_dist, &misc,
-                         &qhi, &bq, &thr, &cand2, &count2, &gcount, &goff, &glist, &large, &sticky};
+                         &qhi, &bq, &thr, &cand2, &count2, &gcount, &goff, &glist, &large, &sticky, &surv,
+                         &recs};
         for (auto *b : all) b->release();
         if (host_flags) (void)hipHostFree(host_flags);
         host_flags = nullptr;
@@ -324,6 +326,35 @@ static int large_k_batch(int64_t n, int k) {
     return (int)std::max<int64_t>(1, std::min(by_cand, by_probe));
 }
 
+// Main-scan segmentation: the first segment is `first` probe lengths, each
+// next one `growth` times the previous; the probe aims at `target`
+// candidates.  Few queries: fewer, longer segments (each refinement is a
+// launch boundary plus a one-workgroup kernel; measured at 10M x 768, nq 1:
+// 7 segments 2.81 ms, 3 segments 2.72 ms; nq 1000 prefers 2, 2).
+// MQVS_SEG="first,growth,target" overrides (tools/ab_split.py).
+struct SegTune {
+    int64_t first = 2, growth = 2, target = 16384;
+};
+static SegTune seg_tune(int nq) {
+    SegTune v;
+    if (nq <= 4) {
+        v.first = 8;
+        v.growth = 4;
+    } else if (nq < 256) {
+        v.first = 4;
+        v.growth = 4;
+    }
+    if (const char *e = std::getenv("MQVS_SEG")) {
+        long long a = 0, b = 0, c = 0;
+        if (std::sscanf(e, "%lld,%lld,%lld", &a, &b, &c) == 3 && a >= 1 && b >= 2 && c >= 256) {
+            v.first = a;
+            v.growth = b;
+            v.target = c;
+        }
+    }
+    return v;
+}
+
 static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, int metric,
                         const uint8_t *filter, const uint8_t *exists, int64_t *out_ids,
                         float *out_dist, uint32_t flags, hipStream_t user_stream,
@@ -483,7 +514,8 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     int cap = (int)std::min<int64_t>(kCandMax, kCandBudget / std::max(nq, 1));
     cap = std::max(cap, k > kSortCap ? large_k_cap(k) : kSortCap) / 256 * 256;
     // (more candidates = more appends from the scan; 16k keeps them cheap)
-    const int64_t target_cands = std::min<int64_t>(cap / 3, std::max<int64_t>(16384, 2 * (int64_t)k));
+    const SegTune tune = seg_tune(nq);
+    const int64_t target_cands = std::min<int64_t>(cap / 3, std::max<int64_t>(tune.target, 2 * (int64_t)k));
     uint4 *large = k > kSortCap ? (uint4 *)ws.large.get(sizeof(uint4) * 2 * kLargeCap * (size_t)nq) : nullptr;
     int64_t P = scan_n;
     if (scan_n > 32768) {
@@ -604,7 +636,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         const int64_t align = aligned ? seg->granule : tile_rows;
         Cand *alt = (Cand *)ws.cand2.get(sizeof(Cand) * (size_t)nq * cap);
         int *calt = (int *)ws.count2.get(sizeof(int) * nq);
-        int64_t b = P, seg_rows = std::max<int64_t>(2 * P, align);
+        int64_t b = P, seg_rows = std::max<int64_t>(tune.first * P, align);
         int segs = 0;
         while (b < scan_n) {
             const int64_t e = std::min(scan_n, round_up(b + seg_rows, align));
@@ -613,7 +645,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
             run_scan(p, make_range(b, e, tile_rows, seg->granule, aligned), kind, metric, false, s);
             if (tev) MQVS_HIP(hipEventRecord(ws.seg_ev[2 * segs + 1], s));
             b = e;
-            seg_rows *= 2;
+            seg_rows *= tune.growth;
             ++segs;
             if (b < scan_n) {
                 launch_refine(cand, count, cap, nq, k, metric, kind == kScanBf16, bq, tau,
@@ -630,9 +662,17 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     }
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[3], s));
     MQVS_HIP(hipMemsetAsync(overflow, 0, sizeof(int) * 4, s));
-    if (kind == kScanBf16)
-        launch_rerank_select(p, metric, bq, k, seg->row_offset, dids, ddist, overflow, large, s);
-    else
+    if (kind == kScanBf16) {
+        // survivors of the bound: up to kSortCap per query (kLargeCap with
+        // the global-scratch sort for k > kSortCap)
+        const int lcap = large ? kLargeCap : kSortCap;
+        const int64_t rs = large ? 2 * (int64_t)kLargeCap : kSortCap;
+        auto *surv = (uint32_t *)ws.surv.get(sizeof(uint32_t) * (size_t)nq * rs + sizeof(int) * nq);
+        int *scnt = (int *)(surv + (size_t)nq * rs);
+        uint4 *recs = large ? large : (uint4 *)ws.recs.get(sizeof(uint4) * (size_t)nq * rs);
+        launch_rerank_select(p, metric, bq, k, seg->row_offset, dids, ddist, overflow, surv, scnt, recs, lcap, rs,
+                             s);
+    } else
         launch_final_select(cand, count, cap, nq, k, metric, seg->granule, seg->row_offset, dids, ddist,
                             overflow, large, s);
     MQVS_HIP(hipGetLastError());

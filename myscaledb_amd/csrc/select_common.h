@@ -148,8 +148,9 @@ __device__ inline uint32_t block_radix_select_mlp(KeyFn keyof, int64_t count, in
 
 // Visit every element of a float row: float4 loads, 4 in flight per thread
 // (the probe rows are megabytes; a scalar loop leaves HBM idle).
-template <typename F>
+template <int NT = SEL_THREADS, typename F>
 __device__ inline void for_each_f4(const float *row, int64_t P, F &&f) {
+    constexpr int SEL_THREADS = NT;  // block size of the caller
     const int t = threadIdx.x;
     const bool al = ((uintptr_t)row & 15) == 0;
     int64_t head = 0;
