@@ -19,8 +19,11 @@ namespace mqvs {
 
 
 
+// 1024 threads, 16 probe values in flight per thread (as k_probe_select_wide)
+constexpr int kProbeThreads = 1024;
+
 template <int METRIC>
-__global__ __launch_bounds__(SEL_THREADS) void k_probe_select(const float *probe, int64_t P,
+__global__ __launch_bounds__(kProbeThreads) void k_probe_select(const float *probe, int64_t P,
                                                              int64_t ld, int k, uint32_t *tau,
                                                              int *cand_count, Cand *cand,
                                                              int cap, int64_t row_base,
@@ -29,9 +32,9 @@ __global__ __launch_bounds__(SEL_THREADS) void k_probe_select(const float *probe
     __shared__ uint32_t sh[4];
     const int q = blockIdx.x;
     const float *row = probe + (int64_t)q * ld;
-    const uint32_t th = block_radix_select_rows<METRIC>(row, P, k, hist, sh);
+    const uint32_t th = block_radix_select_rows<METRIC, kProbeThreads>(row, P, k, hist, sh);
     if (threadIdx.x == 0) tau[q] = th;
-    for_each_f4(row, P, [&](int64_t i, float raw) {
+    for_each_f4<kProbeThreads>(row, P, [&](int64_t i, float raw) {
         const uint32_t key = key32<METRIC>(raw);
         if (key != 0xFFFFFFFFu && key <= th) {
             const int pos = atomicAdd(&cand_count[q], 1);
@@ -267,7 +270,7 @@ template <int M>
 static void probe_select_t(const float *probe, int64_t P, int64_t ld, int nq, int k,
                            uint32_t *tau, int *cc, Cand *cand, int cap, int64_t row_base,
                            const int32_t *row_list, hipStream_t s) {
-    hipLaunchKernelGGL(k_probe_select<M>, dim3(nq), dim3(SEL_THREADS), 0, s, probe, P, ld, k, tau,
+    hipLaunchKernelGGL(k_probe_select<M>, dim3(nq), dim3(kProbeThreads), 0, s, probe, P, ld, k, tau,
                        cc, cand, cap, row_base, row_list);
 }
 

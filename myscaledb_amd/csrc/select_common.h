@@ -176,7 +176,7 @@ __device__ inline void for_each_f4(const float *row, int64_t P, F &&f) {
     for (int64_t i = head + t; i < P; i += SEL_THREADS) f(i, row[i]);
 }
 
-template <int METRIC>
+template <int METRIC, int NT = SEL_THREADS>
 __device__ inline uint32_t block_radix_select_rows(const float *row, int64_t P, int k, uint32_t *hist,
                                             uint32_t *sh) {
     const int t = threadIdx.x;
@@ -186,7 +186,7 @@ __device__ inline uint32_t block_radix_select_rows(const float *row, int64_t P, 
         for (int i = t; i < 256; i += SEL_THREADS) hist[i] = 0;
         __syncthreads();
         RunHist rh;
-        for_each_f4(row, P, [&](int64_t, float raw) {
+        for_each_f4<NT>(row, P, [&](int64_t, float raw) {
             const uint32_t key = key32<METRIC>(raw);
             if (key != 0xFFFFFFFFu && (key & mask) == prefix) rh.add(hist, (key >> shift) & 255u);
         });
