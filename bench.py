@@ -40,7 +40,7 @@ def parse():
     ap.add_argument("--nq", type=int, default=1000)
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--metric", default="Cosine")
-    ap.add_argument("--mode", type=int, default=2, help="0 exact ints, 1 gauss, 2 gaussian mixture")
+    ap.add_argument("--mode", type=int, default=2, help="0 exact ints, 1 gauss, 2 gaussian mixture (4096 centres, noise 0.25), 3 hard mixture (65536 centres, noise 1.0)")
     ap.add_argument("--granule", type=int, default=8192)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -50,6 +50,13 @@ def parse():
     ap.add_argument("--no-index", action="store_true", help="skip the index (configs[2]) leg")
     ap.add_argument("--index-settings", default="nprobe=2;nprobe=3;nprobe=4;nprobe=8",
                     help="';'-separated mqvs_index_search parameter strings timed by the index leg")
+    ap.add_argument("--index-hard-mode", type=int, default=3,
+                    help="second index distribution (generator mode, 3 = 65536 centres, noise 1.0; -1 = none)")
+    ap.add_argument("--index-hard-settings",
+                    default="nprobe=8;nprobe=32;nprobe=64;nprobe=128;nprobe=256;nprobe=512;nprobe=1024",
+                    help="settings timed on the second distribution")
+    ap.add_argument("--index-pmc", default=None,
+                    help="JSON {mode: pmc_traffic.py output} of k_ivf_scan at each distribution's operating point")
     return ap.parse_args()
 
 
@@ -228,28 +235,29 @@ def cpu_baseline(O, args):
     }
 
 
-def index_leg(mq, seg, args):
-    """BASELINE configs[2] on the same resident part: an MSTG-type index
-    (mqvs_index_build) searched with nq held-out queries of the part's own
-    mixture, top-k.  Each setting: one warmup, then `steps` timed searches
-    (device sync on both sides); recall@10 against the exact FLAT result of
-    the same queries.  The operating point is the fastest setting with
-    recall@10 >= 0.95 (the configs[2] target)."""
+INDEX_PMC_DEFAULT = os.path.join(ROOT, "profiles", "r02", "index_pmc.json")
+
+
+def index_points(mq, seg, mode, settings, args):
+    """An MSTG-type index (mqvs_index_build) over `seg`, searched with nq
+    held-out generator rows of the same distribution, top-k.  Each setting:
+    one warmup, then `steps` timed searches (device sync on both sides);
+    recall@10 against the exact FLAT result of the same queries."""
     import torch
     from myscaledb_amd.vector_index import last_index_stats
     from myscaledb_amd.vector_scan import generate_device
-    n, d, nq, k = args.n, args.d, args.nq, args.k
+    n, d, nq, k = seg.n, args.d, args.nq, args.k
     t0 = time.perf_counter()
     idx = mq.VectorIndex.build(seg, "MSTG", "")
     build_s = time.perf_counter() - t0
     info = idx.info()
     qi = torch.empty((nq, d), dtype=torch.float32, device="cuda")
-    generate_device(SEED_BASE, args.mode, n, nq, d, qi)  # generator rows past the part
+    generate_device(SEED_BASE, mode, n, nq, d, qi)  # generator rows past the part
     gt = seg.search(qi, k)[0].cpu().numpy()
     ids = torch.empty((nq, k), dtype=torch.int64, device="cuda")
     dst = torch.empty((nq, k), dtype=torch.float32, device="cuda")
     points = []
-    for sp in [x for x in args.index_settings.split(";") if x]:
+    for sp in [x for x in settings.split(";") if x]:
         idx.search(qi, k, sp, out=(ids, dst))
         torch.cuda.synchronize()
         sts = []
@@ -272,17 +280,55 @@ def index_leg(mq, seg, args):
     ok = [p for p in points if p["recall_at_10"] >= 0.95]
     best = max(ok, key=lambda p: p["qps"]) if ok else max(points, key=lambda p: p["recall_at_10"])
     scan_gbs = best["scan_plane_bytes"] / (best["kernel_ms"]["scan"] * 1e-3) / 1e9
-    return {
+    roof = {"bound": "hbm", "kernel": "k_ivf_scan (bf16 MFMA list scan)",
+            "achieved": round(scan_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+            "frac": round(scan_gbs / HBM_PEAK_GBS, 4),
+            "bytes_definition": "bf16 list-plane bytes per search (every work item streams its list)",
+            "traffic": None}
+    pmc_path = args.index_pmc or INDEX_PMC_DEFAULT
+    if os.path.exists(pmc_path):
+        with open(pmc_path) as f:
+            pm = json.load(f).get(str(mode))
+        ks = [v for key, v in (pm or {}).get("kernels", {}).items() if "k_ivf_scan" in key]
+        if ks and all("hbm_bytes_per_search" in v for v in ks) and pm.get("search") == best["search"]:
+            # every k_ivf_scan launch of a search: the coarse quantizer's scan
+            # of the centroids and the list scan (reads: list plane; writes:
+            # one 8-B approximate value per (query, probed position))
+            rd = sum(v["hbm_read_bytes_per_search"] for v in ks)
+            wr = sum(v["hbm_write_bytes_per_search"] for v in ks)
+            roof["traffic"] = round(rd + wr)
+            roof["traffic_read"] = round(rd)
+            roof["traffic_write"] = round(wr)
+            roof["read_over_plane_bytes"] = round(rd / best["scan_plane_bytes"], 3)
+            roof["traffic_source"] = os.path.relpath(pmc_path, ROOT)
+    return {"generator_mode": mode, "qps": best["qps"], "recall_at_10": best["recall_at_10"],
+            "search": best["search"], "meets_0_95": bool(ok), "build_s": round(build_s, 2), "nlist": info["nlist"],
+            "index_hbm_bytes": info["hbm_bytes"], "roofline": roof, "points": points}
+
+
+def index_leg(mq, seg, args):
+    """BASELINE configs[2] on the same resident part (the bench's own
+    distribution), and on a second, IVF-hostile distribution (mode 3: 65536
+    centres with noise as large as the centres) of the same size."""
+    n, d, nq, k = args.n, args.d, args.nq, args.k
+    main = index_points(mq, seg, args.mode, args.index_settings, args)
+    out = {
         "workload": f"MSTG-type IVF index, {n // 1_000_000}M x {d} {args.metric}, batch {nq}, top-{k}, "
-                    "recall@10 >= 0.95 (BASELINE configs[2]); held-out queries of the part's mixture",
-        "qps": best["qps"], "recall_at_10": best["recall_at_10"], "search": best["search"],
-        "build_s": round(build_s, 2), "nlist": info["nlist"], "index_hbm_bytes": info["hbm_bytes"],
-        "roofline": {"bound": "hbm", "kernel": "k_ivf_scan (bf16 MFMA list scan)",
-                     "achieved": round(scan_gbs, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(scan_gbs / HBM_PEAK_GBS, 4),
-                     "bytes_definition": "bf16 list-plane bytes per search (every work item streams its list)"},
-        "points": points,
+                    "recall@10 >= 0.95 (BASELINE configs[2]); held-out queries of the part's distribution",
+        **{x: main[x] for x in ("qps", "recall_at_10", "search", "build_s", "nlist", "index_hbm_bytes", "roofline",
+                                "points", "generator_mode")},
+        "distributions": [main],
     }
+    if args.index_hard_mode >= 0 and args.index_hard_mode != args.mode:
+        import torch
+        hseg = mq.VectorScanSegment.generate(SEED_BASE, args.index_hard_mode, n, d, args.metric, args.granule)
+        try:
+            out["distributions"].append(index_points(mq, hseg, args.index_hard_mode, args.index_hard_settings, args))
+        finally:
+            hseg.free()
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+    return out
 
 
 def roofline(st, main_ms, nq, d, args):

@@ -120,7 +120,8 @@ int mqvs_segment_create_device(const float *dev_rows, int64_t n, int32_t d, int3
                                int64_t granule_rows, const uint8_t *dev_nonempty,
                                int64_t row_offset, mqvs_segment_t *out);
 /* Synthetic segment generated in HBM by the counter-based generator
- * (mode 0 exact ints in [-8,8], 1 ~N(0,1), 2 Gaussian mixture); row r of the
+ * (mode 0 exact ints in [-8,8], 1 ~N(0,1), 2 Gaussian mixture of 4096 centres
+ * with noise 0.25, 3 "hard" mixture of 65536 centres with noise 1.0); row r of the
  * segment is generator row row_offset + r. */
 int mqvs_segment_generate(uint64_t seed, int32_t mode, int64_t n, int32_t d, int32_t metric,
                           int64_t granule_rows, int64_t row_offset, mqvs_segment_t *out);

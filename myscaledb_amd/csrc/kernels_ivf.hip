@@ -395,21 +395,27 @@ __global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
     }
 }
 
-// Per query: the R best approximate values (ties at the R-th key by position,
-// so the selection is deterministic), sorted by (key, row).  Writes the rows
-// (for the exact re-rank) and, for first-stage-only searches, ids + the
-// approximate distance.  Regions up to `keycap` values keep their keys in
-// LDS for the four radix passes; longer ones stream them (4 in flight).
+// Per query: the R best approximate values, sorted by (key, row); at the R-th
+// key the lowest rows win (every row of the region is distinct).  Writes the
+// rows (for the exact re-rank) and, for first-stage-only searches, ids + the
+// approximate distance.  NT threads per query; regions up to `keycap` values
+// keep their keys in LDS for the four radix passes, longer ones stream them
+// (4 loads in flight per thread).  The records below the R-th key and those at
+// it are gathered in one pass with LDS atomics (their order does not matter:
+// they are sorted); more ties at the R-th key than kTieCap, or than the
+// record array has room for, fall back to a position-ordered pass for them.
+constexpr int kTieCap = 64;  // <= every NT the kernel is launched with
 
-template <int METRIC>
-__global__ __launch_bounds__(SEL_THREADS) void k_ivf_select(const Cand *cand, const int64_t *qstart, int R,
-                                                           int64_t *out_rows, int64_t id_offset,
-                                                           float *out_approx, int keycap) {
+template <int METRIC, int NT>
+__global__ __launch_bounds__(NT) void k_ivf_select(const Cand *cand, const int64_t *qstart, int R,
+                                                   int64_t *out_rows, int64_t id_offset, float *out_approx,
+                                                   int keycap) {
     extern __shared__ __attribute__((aligned(16))) uint4 recs[];  // pow2 >= R records, then the key cache
+    __shared__ uint4 ties[kTieCap];
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh[4];
-    __shared__ int s_wave[SEL_THREADS / 64];
-    __shared__ int s_m;
+    __shared__ int s_wave[NT / 64];
+    __shared__ int s_m, s_tie;
     int N = 1;
     while (N < R) N <<= 1;
     uint32_t *kc = reinterpret_cast<uint32_t *>(recs + N);
@@ -421,67 +427,120 @@ __global__ __launch_bounds__(SEL_THREADS) void k_ivf_select(const Cand *cand, co
         return e.row == 0xFFFFFFFFu ? 0xFFFFFFFFu : okey<METRIC>(e.raw);
     };
     const bool cached = T <= keycap;
+    if (t == 0) {
+        s_m = 0;
+        s_tie = 0;
+    }
     uint32_t th;
     if (cached) {
         int64_t i = t;
-        for (; i + 3 * SEL_THREADS < T; i += 4 * SEL_THREADS) {
-            const uint32_t k0 = gkey(i), k1 = gkey(i + SEL_THREADS), k2 = gkey(i + 2 * SEL_THREADS),
-                           k3 = gkey(i + 3 * SEL_THREADS);
+        for (; i + 3 * NT < T; i += 4 * NT) {
+            const uint32_t k0 = gkey(i), k1 = gkey(i + NT), k2 = gkey(i + 2 * NT), k3 = gkey(i + 3 * NT);
             kc[i] = k0;
-            kc[i + SEL_THREADS] = k1;
-            kc[i + 2 * SEL_THREADS] = k2;
-            kc[i + 3 * SEL_THREADS] = k3;
+            kc[i + NT] = k1;
+            kc[i + 2 * NT] = k2;
+            kc[i + 3 * NT] = k3;
         }
-        for (; i < T; i += SEL_THREADS) kc[i] = gkey(i);
+        for (; i < T; i += NT) kc[i] = gkey(i);
         __syncthreads();
-        th = block_radix_select_mlp([&](int64_t j) { return kc[j]; }, T, R, hist, sh);
+        th = block_radix_select_mlp<NT>([&](int64_t j) { return kc[j]; }, T, R, hist, sh);
     } else {
-        th = block_radix_select_mlp(gkey, T, R, hist, sh);
+        th = block_radix_select_mlp<NT>(gkey, T, R, hist, sh);
     }
-    if (t == 0) s_m = 0;
+    // fewer than R valid keys: every valid one; else those below th (fewer
+    // than R) + the ties at th (at most kTieCap kept)
+    const bool all = th == 0xFFFFFFFEu;
+    auto visit = [&](int64_t i, uint32_t key) {
+        if (key == 0xFFFFFFFFu) return;
+        if (all || key < th) {
+            const Cand e = c[i];
+            const int pos = atomicAdd(&s_m, 1);
+            if (pos < R) recs[pos] = make_uint4(key, e.row, __builtin_bit_cast(uint32_t, e.raw), 0u);
+        } else if (key == th) {
+            const Cand e = c[i];
+            const int pos = atomicAdd(&s_tie, 1);
+            if (pos < kTieCap) ties[pos] = make_uint4(key, e.row, __builtin_bit_cast(uint32_t, e.raw), 0u);
+        }
+    };
+    {
+        int64_t i = t;
+        for (; i + 3 * NT < T; i += 4 * NT) {
+            const uint32_t k0 = cached ? kc[i] : gkey(i), k1 = cached ? kc[i + NT] : gkey(i + NT),
+                           k2 = cached ? kc[i + 2 * NT] : gkey(i + 2 * NT),
+                           k3 = cached ? kc[i + 3 * NT] : gkey(i + 3 * NT);
+            visit(i, k0);
+            visit(i + NT, k1);
+            visit(i + 2 * NT, k2);
+            visit(i + 3 * NT, k3);
+        }
+        for (; i < T; i += NT) visit(i, cached ? kc[i] : gkey(i));
+    }
     __syncthreads();
-    for (int pass = 0; pass < 2; ++pass) {
-        if (th == 0xFFFFFFFEu && pass == 1) break;  // fewer than R valid: pass 0 took all
-        for (int64_t base = 0; base < T; base += SEL_THREADS) {
-            const int m0 = s_m;
-            if (m0 >= R) break;
-            const int64_t i = base + t;
-            bool flag = false;
-            uint32_t key = 0xFFFFFFFFu;
-            if (i < T) {
-                key = cached ? kc[i] : gkey(i);
-                if (th == 0xFFFFFFFEu)
-                    flag = key != 0xFFFFFFFFu;
-                else
-                    flag = pass == 0 ? key < th : key == th;
-            }
-            const uint64_t bal = __ballot(flag);
-            if (lane == 0) s_wave[wv] = __popcll(bal);
+    const int below = min(s_m, R);
+    int m = below;
+    if (!all) {
+        const int nt = s_tie;
+        if (nt <= kTieCap && below + nt <= N) {
+            // the ties after the records below th (kTieCap <= NT)
+            if (t < nt) recs[below + t] = ties[t];
+            m = below + nt;
+        } else {
+            // mass ties: the first R - below of them by position
+            if (t == 0) s_m = below;
             __syncthreads();
-            int off = m0;
-            for (int x = 0; x < wv; ++x) off += s_wave[x];
-            off += __popcll(bal & ((1ull << lane) - 1ull));
-            if (flag && off < R) {
-                const Cand e = c[i];
-                recs[off] = make_uint4(key, e.row, __builtin_bit_cast(uint32_t, e.raw), 0u);
+            for (int64_t base = 0; base < T; base += NT) {
+                const int m0 = s_m;
+                if (m0 >= R) break;
+                const int64_t i = base + t;
+                bool flag = false;
+                uint32_t key = 0xFFFFFFFFu;
+                if (i < T) {
+                    key = cached ? kc[i] : gkey(i);
+                    flag = key == th;
+                }
+                const uint64_t bal = __ballot(flag);
+                if (lane == 0) s_wave[wv] = __popcll(bal);
+                __syncthreads();
+                int off = m0;
+                for (int x = 0; x < wv; ++x) off += s_wave[x];
+                off += __popcll(bal & ((1ull << lane) - 1ull));
+                if (flag && off < R) {
+                    const Cand e = c[i];
+                    recs[off] = make_uint4(key, e.row, __builtin_bit_cast(uint32_t, e.raw), 0u);
+                }
+                __syncthreads();
+                if (t == 0) {
+                    int tot = 0;
+                    for (int x = 0; x < NT / 64; ++x) tot += s_wave[x];
+                    s_m = min(R, m0 + tot);
+                }
+                __syncthreads();
             }
-            __syncthreads();
-            if (t == 0) {
-                int tot = 0;
-                for (int x = 0; x < SEL_THREADS / 64; ++x) tot += s_wave[x];
-                s_m = min(R, m0 + tot);
-            }
-            __syncthreads();
+            m = s_m;
         }
     }
-    const int m = s_m;
+    __syncthreads();
     int Nm = 1;
     while (Nm < m) Nm <<= 1;
-    for (int i = m + t; i < Nm; i += SEL_THREADS)
-        recs[i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+    for (int i = m + t; i < Nm; i += NT) recs[i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
     __syncthreads();
-    block_bitonic_sort(recs, Nm);
-    for (int i = t; i < R; i += SEL_THREADS) {
+    // bitonic sort of recs[0, Nm) (block-wide, NT threads)
+    for (int size = 2; size <= Nm; size <<= 1) {
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = t; i < (Nm >> 1); i += NT) {
+                const int lo = 2 * stride * (i / stride) + (i % stride);
+                const int hi = lo + stride;
+                const bool up = (lo & size) == 0;
+                const uint4 a = recs[lo], b2 = recs[hi];
+                if (rec_less(b2, a) == up) {
+                    recs[lo] = b2;
+                    recs[hi] = a;
+                }
+            }
+            __syncthreads();
+        }
+    }
+    for (int i = t; i < R; i += NT) {
         const bool ok = i < m;
         const uint4 r = ok ? recs[i] : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
         if (out_approx) {
@@ -699,13 +758,23 @@ void launch_ivf_select(const Cand *cand, const int64_t *qstart, int nq, int R, i
     }
     int N = 1;
     while (N < R) N <<= 1;
-    // LDS key cache sized for the expected region length (<= 64 KiB)
+    // LDS key cache sized for the expected region length (<= 64 KiB, and
+    // within the LDS left beside the records); long regions (many probed
+    // lists) get 1024 threads per query
     int keycap = 1024;
     while (keycap < expect_len && keycap < 16384) keycap <<= 1;
+    while (keycap > 0 && sizeof(uint4) * N + sizeof(uint32_t) * keycap > 144 * 1024) keycap >>= 1;
     const size_t lds = sizeof(uint4) * N + sizeof(uint32_t) * keycap;
-#define MQVS_SEL(M)                                                                                              \
-    hipLaunchKernelGGL(k_ivf_select<M>, dim3(nq), dim3(SEL_THREADS), lds, s, cand, qstart, R, out_rows, id_offset, \
-                       out_approx, keycap)
+    const bool wide = expect_len > 16384;
+#define MQVS_SEL(M)                                                                                                 \
+    do {                                                                                                            \
+        if (wide)                                                                                                   \
+            hipLaunchKernelGGL((k_ivf_select<M, 1024>), dim3(nq), dim3(1024), lds, s, cand, qstart, R, out_rows,    \
+                               id_offset, out_approx, keycap);                                                      \
+        else                                                                                                        \
+            hipLaunchKernelGGL((k_ivf_select<M, SEL_THREADS>), dim3(nq), dim3(SEL_THREADS), lds, s, cand, qstart, R, \
+                               out_rows, id_offset, out_approx, keycap);                                            \
+    } while (0)
     switch (metric) {
         case MQVS_METRIC_L2: MQVS_SEL(MQVS_METRIC_L2); break;
         case MQVS_METRIC_IP: MQVS_SEL(MQVS_METRIC_IP); break;

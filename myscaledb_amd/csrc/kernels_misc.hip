@@ -337,11 +337,17 @@ __global__ void k_generate(uint64_t seed, int mode, int64_t row0, int64_t n, int
             v = (float)((int)(splitmix64(seed ^ idx) % 17ULL) - 8);
         } else if (mode == 1) {
             v = gen_gauss(seed, idx);
-        } else {
+        } else if (mode == 2) {
             const uint64_t c =
                 splitmix64(seed ^ 0xC0FFEEULL ^ (row * 0x100000001B3ULL)) % 4096ULL;
             const float center = gen_gauss(seed ^ 0xCE17E5ULL, c * (uint64_t)d + (uint64_t)j);
             v = center + 0.25f * gen_gauss(seed, idx);
+        } else {
+            // hard mixture: 65536 centres, noise as large as the centres
+            const uint64_t c =
+                splitmix64(seed ^ 0xC0FFEEULL ^ (row * 0x100000001B3ULL)) % 65536ULL;
+            const float center = gen_gauss(seed ^ 0xCE17E5ULL, c * (uint64_t)d + (uint64_t)j);
+            v = center + gen_gauss(seed, idx);
         }
         out[e] = v;
     }

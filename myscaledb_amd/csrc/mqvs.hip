@@ -1391,7 +1391,7 @@ int mqvs_segment_generate(uint64_t seed, int32_t mode, int64_t n, int32_t d, int
         if (!out) fail(MQVS_ERR_BAD_ARGUMENTS, "null output handle");
         *out = nullptr;
         check_seg_args(n, d, metric, granule_rows, row_offset);
-        if (mode < 0 || mode > 2) fail(MQVS_ERR_BAD_ARGUMENTS, "generator mode must be 0, 1 or 2");
+        if (mode < 0 || mode > 3) fail(MQVS_ERR_BAD_ARGUMENTS, "generator mode must be 0, 1, 2 or 3");
         mqvs_segment *s = new_segment(n, d, metric, granule_rows, row_offset);
         try {
             Workspace &ws = workspace(s->device);
@@ -1621,7 +1621,7 @@ int mqvs_merge_shards(int32_t nshards, int32_t nq, int32_t k, int32_t metric, co
 int mqvs_generate_device(uint64_t seed, int32_t mode, int64_t row0, int64_t n, int32_t d,
                          float *dev_out, mqvs_stream_t stream) {
     return guarded([&] {
-        if (mode < 0 || mode > 2 || n < 0 || d <= 0) fail(MQVS_ERR_BAD_ARGUMENTS, "bad arguments");
+        if (mode < 0 || mode > 3 || n < 0 || d <= 0) fail(MQVS_ERR_BAD_ARGUMENTS, "bad arguments");
         int dev = 0;
         MQVS_HIP(hipGetDevice(&dev));
         Workspace &ws = workspace(dev);
@@ -1660,7 +1660,7 @@ int mqvs_set_prefilter(int split) {
 }
 
 int mqvs_set_gather_mode(int mode) {
-    if (mode < 0 || mode > 2) return MQVS_ERR_BAD_ARGUMENTS;
+    if (mode < 0 || mode > 3) return MQVS_ERR_BAD_ARGUMENTS;
     g_gather_mode.store(mode);
     return MQVS_OK;
 }

@@ -108,8 +108,9 @@ __device__ inline uint32_t block_radix_select(KeyFn keyof, int64_t count, int k,
 
 // block_radix_select with the bucket search in parallel and 4 keys in
 // flight per thread (keyof(i) may read global memory).
-template <typename KeyFn>
+template <int NT = SEL_THREADS, typename KeyFn>
 __device__ inline uint32_t block_radix_select_mlp(KeyFn keyof, int64_t count, int k, uint32_t *hist, uint32_t *sh) {
+    constexpr int SEL_THREADS = NT;  // block size of the caller
     const int t = threadIdx.x;
     uint32_t prefix = 0, mask = 0, kk = (uint32_t)k;
     for (int pass = 0; pass < 4; ++pass) {

@@ -137,7 +137,7 @@ class VectorScanSegment:
 
     @classmethod
     def generate(cls, seed, mode, n, d, metric="L2", granule=DEFAULT_GRANULE, row_offset=0):
-        """Synthetic part from the counter-based generator (mode 0 exact, 1 gauss, 2 mixture)."""
+        """Synthetic part from the counter-based generator (mode 0 exact, 1 gauss, 2 mixture, 3 hard mixture)."""
         m = metric_id(metric)
         h = ctypes.c_void_p()
         check(lib.mqvs_segment_generate(seed, mode, n, d, m, granule, row_offset, ctypes.byref(h)))

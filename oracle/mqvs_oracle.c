@@ -732,12 +732,14 @@ static inline float gen_gauss(uint64_t seed, uint64_t idx) {
 }
 
 #define ORC_MIX_CENTERS 4096ULL
+#define ORC_HARD_CENTERS 65536ULL /* mode 3: hard mixture, unit noise */
 
 void orc_generate(uint64_t seed, int mode, int64_t row0, int64_t n, int64_t d,
                   float *out) {
     for (int64_t r = 0; r < n; r++) {
         const uint64_t row = (uint64_t)(row0 + r);
-        const uint64_t c = splitmix64(seed ^ 0xC0FFEEULL ^ (row * 0x100000001B3ULL)) % ORC_MIX_CENTERS;
+        const uint64_t c = splitmix64(seed ^ 0xC0FFEEULL ^ (row * 0x100000001B3ULL)) %
+                           (mode == 3 ? ORC_HARD_CENTERS : ORC_MIX_CENTERS);
         for (int64_t j = 0; j < d; j++) {
             const uint64_t idx = row * (uint64_t)d + (uint64_t)j;
             float v;
@@ -745,9 +747,12 @@ void orc_generate(uint64_t seed, int mode, int64_t row0, int64_t n, int64_t d,
                 v = (float)((int)(splitmix64(seed ^ idx) % 17ULL) - 8);
             } else if (mode == 1) {
                 v = gen_gauss(seed, idx);
-            } else {
+            } else if (mode == 2) {
                 const float center = gen_gauss(seed ^ 0xCE17E5ULL, c * (uint64_t)d + (uint64_t)j);
                 v = center + 0.25f * gen_gauss(seed, idx);
+            } else {
+                const float center = gen_gauss(seed ^ 0xCE17E5ULL, c * (uint64_t)d + (uint64_t)j);
+                v = center + gen_gauss(seed, idx);
             }
             out[r * d + j] = v;
         }

@@ -260,7 +260,7 @@ def test_knn_raw_rejects_cosine(mq):
 
 def test_device_generator_matches_oracle(mq):
     import torch
-    for mode in (0, 1, 2):
+    for mode in (0, 1, 2, 3):
         t = torch.empty((300, 77), dtype=torch.float32, device="cuda")
         from myscaledb_amd.vector_scan import generate_device
         generate_device(0x1234 + mode, mode, 12345, 300, 77, t)

@@ -41,7 +41,7 @@ def main():
         if not os.path.exists(p):
             continue
         for r in load(p):
-            m = re.search(args.kernel + r"[_a-z]*<([^>]*)>", r["Kernel_Name"])
+            m = re.search(args.kernel + r"[_a-z]*(?:<([^>]*)>)?", r["Kernel_Name"])
             if not m:
                 continue
             key = m.group(0)
