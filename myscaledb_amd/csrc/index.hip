@@ -448,7 +448,15 @@ static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, c
     // fragment then feeds two MFMAs)
     // (64-query items, QB = 4, measured slower on the dense coarse pass at
     // d = 768: its 99 KiB LDS tile leaves one workgroup per CU)
-    p.qg = (dense || E >= 24 * nlist) ? 32 : 16;
+    // Lists probed by very many queries (IVF-hostile data at large nprobe):
+    // 64-query items halve the list re-reads again (10M x 768, nq 1000,
+    // nprobe 512 = 51 queries per list: 14.4 -> 12.3 ms; at 13 per list
+    // they are slower, tools/index_qg_ab.py).
+    p.qg = (!dense && E >= 40 * nlist) ? 64 : (dense || E >= 24 * nlist) ? 32 : 16;
+    if (const char *e = std::getenv("MQVS_IVF_QG")) {  // A/B knob (tools/ab_split.py style)
+        const int v = std::atoi(e);
+        if (!dense && (v == 16 || v == 32 || v == 64)) p.qg = v;
+    }
     // work items = sum over probed lists of groups x 512-position slices
     const int64_t max_items = (E / p.qg + std::min<int64_t>(E, nlist)) * (max_list / 512 + 1);
     p.item_list = (int *)b.items.get(sizeof(int) * max_items);
