@@ -105,7 +105,13 @@ void launch_max_norm(const float *norms2, int64_t n, float *out_max, hipStream_t
 //   segment's maxima Y (|h| |r| |h6| |h-h6| |r6| |r-r6| |x|):
 //     truncation  q3 Y1 + q2 Y5 + q5 Y0 + q4 Y3 + q1 Y1
 //     accumulation 3.03 d u (q0 Y0 + q2 Y4 + q4 Y2) + 1.01 d u |x||y| (exact chain)
-//     MX internal 2^-10 (q2 Y4 + q4 Y2) (an allowance far above fp32 rounding)
+//     MX internal 2^-10 (q2 Y4 + q4 Y2): an allowance for the f8f6f4 MFMA's
+//     internal sum, measured against exact sums on adversarial e2m3 codes and
+//     every scale range (tools/mfma_acc_probe.hip,
+//     profiles/r02/probes/mfma_acc_probe.log): worst 1.5 u sum|p| over 12
+//     chained MFMAs (8.9e-8 relative), 2^14 / 1.5 below the allowance; the
+//     bf16 MFMA's worst is 95.5 u sum|p| at d = 768 against the 2.04 d u
+//     (1567 u) the bf16 terms assume
 __global__ void k_query_bound(ScanParams p, int metric, int split, int direct,
                               const float *ynorm_max, const float *qrec, const float *yrec, float *bq) {
     // one wave per query; |x| in fp64 (an upper bound after the 1.0001 slack)
@@ -129,7 +135,8 @@ __global__ void k_query_bound(ScanParams p, int metric, int split, int direct,
         // x.y - xh.yh = xh.ry + rx.yh + rx.ry (records: q[0] |xh|, q[1] |rx|,
         // q[6] |x|; Y the segment maxima); the MFMA sums d exact products, at
         // most 2 u relative per addition (2.04 d u |xh||yh|, covers
-        // round-toward-zero; measured: tools/mfma_acc_probe.hip); the exact
+        // round-toward-zero; measured worst 95.5 u sum|p| at d = 768,
+        // tools/mfma_acc_probe.hip, profiles/r02/probes/mfma_acc_probe.log); the exact
         // chain's own error 1.01 d u |x||y| + one ulp
         const float *Y = yrec;
         b = 0.f;
