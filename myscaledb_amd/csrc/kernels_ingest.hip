@@ -27,7 +27,12 @@
 
 namespace mqvs {
 
-constexpr int kRing = 65536;  // LZ4 window
+// LDS ring of the block's latest output.  16 KiB (not the 64 KiB LZ4 window)
+// so that eight decode waves fit on a CU: the decode is latency-bound per
+// wave, and a 64 KiB ring left two waves per CU.  Matches reaching further
+// back (1-2 % of them on quantised float columns) read the already-flushed
+// output from global memory (far_byte).
+constexpr int kRing = 16384;
 
 __global__ void k_block_table(const uint8_t *src, int64_t n, IngestBlock *tab, int64_t max_blocks,
                               int64_t *out) {
@@ -124,33 +129,29 @@ __device__ __forceinline__ void copy_literals(const uint8_t *s, const uint8_t *s
     byte_copy(head + 4 * nw, len);
 }
 
-// Compressed-input window for the token parse: lane l holds the dword at
-// wa + 4 l (wa 4-byte aligned), so a parse byte costs one lane shuffle
-// instead of a dependent global load; the window moves (one coalesced load)
-// when the parse leaves it.  All lanes call it with the same address.
-struct InWindow {
-    const uint8_t *end;
-    uintptr_t wa = 0;
-    uint32_t w = 0;
-    bool valid = false;
-    __device__ void load(const uint8_t *x, int lane) {
-        wa = (uintptr_t)x & ~(uintptr_t)3;
-        const uint8_t *p = (const uint8_t *)wa + 4 * lane;
-        if (p + 4 <= end) {
-            w = *reinterpret_cast<const uint32_t *>(p);
-        } else {
-            w = 0;
-            for (int k = 0; k < 4 && p + k < end; ++k) w |= (uint32_t)p[k] << (8 * k);
-        }
-        valid = true;
-    }
-    __device__ uint32_t byte(const uint8_t *x, int lane) {
-        if (!valid || (uintptr_t)x < wa || (uintptr_t)x >= wa + 256) load(x, lane);
-        const uintptr_t o = (uintptr_t)x - wa;
-        return (__shfl(w, (int)(o >> 2)) >> (8 * (o & 3))) & 255u;
-    }
-};
+// A byte of this wave's own earlier, flushed output: the stores are waited
+// for (vmcnt) by the caller; the load bypasses the non-coherent L1 (agent-
+// scope atomic load of the containing dword).
+__device__ __forceinline__ uint32_t far_byte(const uint8_t *out, int32_t pos) {
+    const uintptr_t a = (uintptr_t)(out + pos);
+    const uint32_t w = __hip_atomic_load(reinterpret_cast<const uint32_t *>(a & ~(uintptr_t)3), __ATOMIC_RELAXED,
+                                         __HIP_MEMORY_SCOPE_AGENT);
+    return (w >> (8 * (a & 3))) & 255u;
+}
 
+// The decode loop is one wave's sequential walk over the tokens, so every
+// per-sequence value (input / output positions, lengths, the window base) is
+// wave-uniform and kept in scalar registers (readfirstlane at the loop head):
+// branches are scalar, and no per-lane exec-mask bookkeeping or 64-bit vector
+// compares sit on the sequence chain.  Positions are 32-bit (a block is at
+// most 2^30 bytes; larger ones are rejected as malformed).
+//
+// Compressed-input window: two 256-B halves [wa, wa + 256) and [wa + 256,
+// wa + 512) of the block's bytes (offsets from the dword-aligned pa), lane l
+// holding the dword at wa + 4 l of each.  A parse byte is one v_readlane (the
+// offset is uniform); a short literal run is read with one lane shuffle per
+// 64 bytes.  When the parse enters the upper half the window slides by 256 B
+// and loads the next half ahead of its use.
 __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_t src_bytes, const IngestBlock *tab,
                                                       int64_t nblocks, uint8_t *dst, int *status) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
@@ -160,39 +161,111 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
         const IngestBlock blk = tab[bi];
         const uint8_t *ip0 = src + blk.src;
         uint8_t *out = dst + blk.dst;
-        const int64_t isz = blk.csize, osz = blk.usize;
         if (blk.method == 0x02) {  // stored block: one literal run (the ring copy is unused)
-            copy_literals(ip0, src_end, out, 0, osz, ring, lane);
+            copy_literals(ip0, src_end, out, 0, blk.usize, ring, lane);
             continue;
         }
-        InWindow win;
-        win.end = ip0 + isz;
-        int64_t ip = 0, op = 0;
-        bool bad = false;
-        for (;;) {
+        bool bad = blk.csize >= (1u << 30) || blk.usize >= (1u << 30);
+        const int32_t isz = bad ? 0 : (int32_t)blk.csize, osz = bad ? 0 : (int32_t)blk.usize;
+        const int32_t mis = (int32_t)((uintptr_t)ip0 & 3);
+        const uint8_t *pa = ip0 - mis;  // dword-aligned; stream bytes at [mis, mis + isz)
+        const int32_t lim = mis + isz;
+        auto ld = [&](int32_t base) -> uint32_t {
+            const int32_t q = base + 4 * lane;
+            if (q + 4 <= lim) return *reinterpret_cast<const uint32_t *>(pa + q);
+            uint32_t v = 0;
+            for (int k = 0; k < 4; ++k)
+                if (q + k < lim) v |= (uint32_t)pa[q + k] << (8 * k);
+            return v;
+        };
+        int32_t wa = -1024;
+        uint32_t w0 = 0, w1 = 0;
+        auto cover = [&](int32_t x) {  // afterwards wa <= x < wa + 256
+            if (x >= wa + 256 && x < wa + 512) {
+                wa += 256;
+                w0 = w1;
+                w1 = ld(wa + 256);
+            } else if (x < wa || x >= wa + 256) {
+                wa = x & ~3;
+                w0 = ld(wa);
+                w1 = ld(wa + 256);
+            }
+            wa = __builtin_amdgcn_readfirstlane(wa);
+        };
+        auto byte = [&](int32_t ipos) -> uint32_t {
+            const int32_t x = mis + ipos;
+            cover(x);
+            const int32_t o = __builtin_amdgcn_readfirstlane(x - wa);
+            const uint32_t v = o < 256 ? (uint32_t)__builtin_amdgcn_readlane((int)w0, o >> 2)
+                                       : (uint32_t)__builtin_amdgcn_readlane((int)w1, (o - 256) >> 2);
+            return (v >> (8 * (o & 3))) & 255u;
+        };
+        // Output goes to the LDS ring only and is flushed to global memory in
+        // runs of >= 4 KiB with dword stores; unflushed bytes stay < 4 KiB +
+        // one step (< 4.6 KiB), so the ring never overwrites them and every
+        // byte further back than kRing - 256 is already in global memory.  (One wave per
+        // workgroup: its LDS accesses complete in program order, so a ring
+        // read after a ring write sees it; the wave barriers only keep the
+        // compiler from moving them.)
+        int32_t fl = 0;  // out[0, fl) written
+        auto flush = [&](int32_t upto) {
+            const int32_t oa = (int32_t)((uintptr_t)(out + fl) & 3);
+            int32_t head = (4 - oa) & 3;
+            if (head > upto - fl) head = upto - fl;
+            if (lane < head) out[fl + lane] = ring[(fl + lane) & (kRing - 1)];
+            const int32_t p0 = fl + head, nw = (upto - p0) >> 2;
+            uint32_t *ow = reinterpret_cast<uint32_t *>(out + p0);
+            for (int32_t w = lane; w < nw; w += 64) {
+                const int32_t b = p0 + 4 * w;
+                ow[w] = (uint32_t)ring[b & (kRing - 1)] | ((uint32_t)ring[(b + 1) & (kRing - 1)] << 8) |
+                        ((uint32_t)ring[(b + 2) & (kRing - 1)] << 16) | ((uint32_t)ring[(b + 3) & (kRing - 1)] << 24);
+            }
+            const int32_t p1 = p0 + 4 * nw;
+            if (lane < upto - p1) out[p1 + lane] = ring[(p1 + lane) & (kRing - 1)];
+            fl = upto;
+        };
+        int32_t ip = 0, op = 0;
+        while (!bad) {
+            ip = __builtin_amdgcn_readfirstlane(ip);
+            op = __builtin_amdgcn_readfirstlane(op);
+            fl = __builtin_amdgcn_readfirstlane(fl);
             if (ip >= isz) {
                 bad = true;
                 break;
             }
-            const uint32_t token = win.byte(ip0 + ip++, lane);
-            int64_t len = token >> 4;
+            const uint32_t token = byte(ip++);
+            int32_t len = (int32_t)(token >> 4);
             if (len == 15) {
-                uint32_t s;
+                uint32_t sb;
                 do {
                     if (ip >= isz) {
                         bad = true;
                         break;
                     }
-                    s = win.byte(ip0 + ip++, lane);
-                    len += s;
-                } while (s == 255);
+                    sb = byte(ip++);
+                    len += (int32_t)sb;
+                } while (sb == 255 && len < (1 << 30));
                 if (bad) break;
             }
             if (len > osz - op || len > isz - ip) {
                 bad = true;
                 break;
             }
-            copy_literals(ip0 + ip, src_end, out, op, len, ring, lane);
+            if (len > 0 && len <= 256) {
+                // short run: its bytes are in the window (no global load)
+                cover(mis + ip);
+                const int32_t o0 = mis + ip - wa;
+                for (int32_t r = 0; r < len; r += 64) {
+                    const int32_t i = r + lane, o = o0 + i;
+                    const uint32_t x0 = __shfl(w0, (o >> 2) & 63), x1 = __shfl(w1, ((o - 256) >> 2) & 63);
+                    if (i < len) ring[(op + i) & (kRing - 1)] = (uint8_t)(((o < 256 ? x0 : x1) >> (8 * (o & 3))) & 255u);
+                }
+            } else if (len > 256) {
+                // long run: straight to global memory (and the ring)
+                flush(op);
+                copy_literals(ip0 + ip, src_end, out, op, len, ring, lane);
+                fl = op + len;
+            }
             op += len;
             ip += len;
             if (op == osz) break;
@@ -200,23 +273,23 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
                 bad = true;
                 break;
             }
-            const int64_t off = (int64_t)win.byte(ip0 + ip, lane) | ((int64_t)win.byte(ip0 + ip + 1, lane) << 8);
+            const int32_t off = (int32_t)(byte(ip) | (byte(ip + 1) << 8));
             ip += 2;
             if (off == 0 || off > op) {
                 bad = true;
                 break;
             }
-            int64_t mlen = token & 15;
+            int32_t mlen = (int32_t)(token & 15);
             if (mlen == 15) {
-                uint32_t s;
+                uint32_t sb;
                 do {
                     if (ip >= isz) {
                         bad = true;
                         break;
                     }
-                    s = win.byte(ip0 + ip++, lane);
-                    mlen += s;
-                } while (s == 255);
+                    sb = byte(ip++);
+                    mlen += (int32_t)sb;
+                } while (sb == 255 && mlen < (1 << 30));
                 if (bad) break;
             }
             mlen += 4;
@@ -224,37 +297,68 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
                 bad = true;
                 break;
             }
-            // Match, in chunks of up to 256 bytes: byte op + i equals byte
-            // op + i - m off for any m >= 1 (the copy replicates with period
-            // off), so chunk [d0, d0 + cnt) reads the latest off bytes before
-            // it, [op + d0 - off, op + d0), all final after the barrier.
-            // cnt <= 65536 - off keeps the chunk's ring writes off that window.
-            const int64_t chunk = off > 65280 ? 65536 - off : 256;
-            for (int64_t d0 = 0; d0 < mlen; d0 += chunk) {
-                __syncthreads();  // earlier literal / match bytes are in the ring
-                const int64_t cnt = mlen - d0 < chunk ? mlen - d0 : chunk;
-                uint8_t v[4];
+            if (mlen <= 64 && off >= mlen && off <= kRing - 64) {
+                // the common short, non-overlapping match: one step
+                __builtin_amdgcn_wave_barrier();
+                uint8_t v = 0;
+                if (lane < mlen) v = ring[(op - off + lane) & (kRing - 1)];
+                if (lane < mlen) ring[(op + lane) & (kRing - 1)] = v;
+                __builtin_amdgcn_wave_barrier();
+            } else if (off > kRing - 256) {
+                // far match (off > mlen-step, so no replication within a
+                // 256-byte step): from the flushed output
+                for (int32_t d0 = 0; d0 < mlen; d0 += 256) {
+                    if (op + d0 - fl >= 4096) flush(op + d0);
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the flushes landed)
+                    const int32_t cnt = mlen - d0 < 256 ? mlen - d0 : 256;
+                    uint32_t v[4];
 #pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int64_t i = u * 64 + lane;
-                    v[u] = 0;
-                    if (i < cnt) {
-                        const int64_t m = i / off + 1;
-                        v[u] = ring[(op + d0 + i - m * off) & (kRing - 1)];
+                    for (int u = 0; u < 4; ++u) {
+                        const int32_t i = u * 64 + lane;
+                        v[u] = i < cnt ? far_byte(out, op + d0 + i - off) : 0u;
+                    }
+                    __builtin_amdgcn_wave_barrier();
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int32_t i = u * 64 + lane;
+                        if (i < cnt) ring[(op + d0 + i) & (kRing - 1)] = (uint8_t)v[u];
+                    }
+                    __builtin_amdgcn_wave_barrier();
+                }
+            } else {
+                // Chunks of up to 256 bytes: byte op + i equals byte op + i -
+                // m off for any m >= 1 (the copy replicates with period off),
+                // so chunk [d0, d0 + cnt) reads the latest off bytes before it,
+                // [op + d0 - off, op + d0), all final.  cnt <= 65536 - off keeps
+                // the chunk's ring writes off that window.
+                const int32_t chunk = 256;  // off <= kRing - 256 here
+                for (int32_t d0 = 0; d0 < mlen; d0 += chunk) {
+                    __builtin_amdgcn_wave_barrier();
+                    if (op + d0 - fl >= 4096) {
+                        flush(op + d0);
+                        __builtin_amdgcn_wave_barrier();
+                    }
+                    const int32_t cnt = mlen - d0 < chunk ? mlen - d0 : chunk;
+                    uint8_t v[4];
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int32_t i = u * 64 + lane;
+                        v[u] = 0;
+                        if (i < cnt) v[u] = ring[(op + d0 + i - (i / off + 1) * off) & (kRing - 1)];
+                    }
+#pragma unroll
+                    for (int u = 0; u < 4; ++u) {
+                        const int32_t i = u * 64 + lane;
+                        if (i < cnt) ring[(op + d0 + i) & (kRing - 1)] = v[u];
                     }
                 }
-#pragma unroll
-                for (int u = 0; u < 4; ++u) {
-                    const int64_t i = u * 64 + lane;
-                    if (i < cnt) {
-                        out[op + d0 + i] = v[u];
-                        ring[(op + d0 + i) & (kRing - 1)] = v[u];
-                    }
-                }
+                __builtin_amdgcn_wave_barrier();
             }
-            __syncthreads();
             op += mlen;
+            if (op - fl >= 4096) flush(op);
         }
+        __builtin_amdgcn_wave_barrier();
+        flush(op);
         if (bad && lane == 0) atomicOr(status, 4);
         __syncthreads();
     }

@@ -42,7 +42,7 @@ struct Workspace {
     hipEvent_t seg_ev[kSegEv] = {};  // per main-scan segment: start, end
     DevBuf queries, qvars, qnorms, qmu, qlam, status, filter, exists, ord, probe, tau, count, cand,
         overflow, out_ids, out_dist, misc, qhi, bq, thr, cand2, count2, gcount, goff, glist, large, sticky, surv,
-        recs;
+        recs, flags;
     int *host_flags = nullptr;  // pinned
     void init() {
         if (stream) return;
@@ -55,7 +55,7 @@ struct Workspace {
         DevBuf *all[] = {&queries, &qvars, &qnorms, &qmu,  &qlam,   &status,  &filter,   &exists, &ord,
                          &probe,   &tau,   &count,  &cand, &overflow, &out_ids, &out_dist, &misc,
                          &qhi, &bq, &thr, &cand2, &count2, &gcount, &goff, &glist, &large, &sticky, &surv,
-                         &recs};
+                         &recs, &flags};
         for (auto *b : all) b->release();
         if (host_flags) (void)hipHostFree(host_flags);
         host_flags = nullptr;
@@ -258,20 +258,22 @@ static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 // ordinal (up to kMaxVariantsCap) -- one host sync, only on such parts.
 // Returns maxv; ASYNC calls cannot sync and keep the default table (their
 // outcome goes to mqvs_async_check).
+// zeroed_status: 4 ints the caller has already zeroed on this stream (saves a
+// memset launch), or null
 static int prep_variants(Workspace &ws, const float *dq, int nq, int d, bool cos, bool l2norms, int64_t ords,
                          bool may_sync, float *&qvars, float *&qnorms, int *&qmu, int *&qlam, int *&status,
-                         hipStream_t s) {
+                         hipStream_t s, int *zeroed_status = nullptr) {
     const int64_t qstride = round_up(d, 32);
     qnorms = (float *)ws.qnorms.get(sizeof(float) * nq);
     qmu = (int *)ws.qmu.get(sizeof(int) * nq);
     qlam = (int *)ws.qlam.get(sizeof(int) * nq);
-    status = (int *)ws.status.get(sizeof(int) * 4);
+    status = zeroed_status ? zeroed_status : (int *)ws.status.get(sizeof(int) * 4);
     int maxv = cos ? kMaxVariants : 1;
     for (int pass = 0; pass < 2; ++pass) {
         const size_t bytes = sizeof(float) * (size_t)nq * maxv * qstride;
         qvars = (float *)ws.qvars.get(bytes);
         MQVS_HIP(hipMemsetAsync(qvars, 0, bytes, s));
-        MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
+        if (pass > 0 || !zeroed_status) MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
         launch_query_prep(dq, nq, d, cos ? MQVS_METRIC_COSINE : MQVS_METRIC_L2, l2norms, qvars, maxv, qnorms, qmu,
                           qlam, status, s);
         MQVS_HIP(hipGetLastError());
@@ -477,8 +479,11 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     const int64_t qstride = round_up(d, 32);
     float *qvars = nullptr, *qnorms = nullptr;
     int *qmu = nullptr, *qlam = nullptr, *status = nullptr;
+    // one zeroed block for the status words: [overflow 4][status 4][count nq]
+    int *fl = (int *)ws.flags.get(sizeof(int) * (8 + (size_t)nq));
+    MQVS_HIP(hipMemsetAsync(fl, 0, sizeof(int) * (8 + (size_t)nq), s));
     const int maxv = prep_variants(ws, dq, nq, d, cos, (mfma || bf16) && metric == MQVS_METRIC_L2, ords,
-                                   !(dev && (flags & MQVS_F_ASYNC)), qvars, qnorms, qmu, qlam, status, s);
+                                   !(dev && (flags & MQVS_F_ASYNC)), qvars, qnorms, qmu, qlam, status, s, fl + 4);
 
     // ---- chunk ordinals
     const int *chunk_ord = nullptr;
@@ -550,9 +555,9 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     p.row_list = row_list;
     p.num_qblocks = (nq + kMfmaQ - 1) / kMfmaQ;
     uint32_t *tau = (uint32_t *)ws.tau.get(sizeof(uint32_t) * nq);
-    int *count = (int *)ws.count.get(sizeof(int) * nq);
+    int *count = fl + 8;  // zeroed with the status words
     Cand *cand = (Cand *)ws.cand.get(sizeof(Cand) * (size_t)nq * cap);
-    int *overflow = (int *)ws.overflow.get(sizeof(int) * 4);
+    int *overflow = fl;
     p.tau = tau;
     p.cand_count = count;
     p.cand = cand;
@@ -620,7 +625,6 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[5], s));
     run_scan(p, pr, kind, metric, true, s);
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[1], s));
-    MQVS_HIP(hipMemsetAsync(count, 0, sizeof(int) * nq, s));
     if (kind == kScanBf16)
         launch_probe_select_approx(probe, P, P, nq, k, metric, bq, (float *)p.thr, count, cand, cap, row_list,
                                    s);
@@ -661,7 +665,6 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         (void)mr;
     }
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[3], s));
-    MQVS_HIP(hipMemsetAsync(overflow, 0, sizeof(int) * 4, s));
     if (kind == kScanBf16) {
         // survivors of the bound: up to kSortCap per query (kLargeCap with
         // the global-scratch sort for k > kSortCap)
@@ -693,10 +696,15 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         launch_async_flags(overflow, status, variants_matter ? 1 : 0, sticky_word(ws, s), s);
         MQVS_HIP(hipGetLastError());
     } else {
-        MQVS_HIP(hipMemcpyAsync(ws.host_flags, overflow, sizeof(int), hipMemcpyDeviceToHost, s));
-        MQVS_HIP(hipMemcpyAsync(ws.host_flags + 1, status, sizeof(int), hipMemcpyDeviceToHost, s));
-        MQVS_HIP(hipMemcpyAsync(ws.host_flags + 4, overflow + 1, 3 * sizeof(int), hipMemcpyDeviceToHost, s));
+        // [overflow 4][status 4] in one copy -> host_flags[0] overflow bits,
+        // [1] status, [4..6] survivor / candidate stats
+        MQVS_HIP(hipMemcpyAsync(ws.host_flags + 16, fl, 8 * sizeof(int), hipMemcpyDeviceToHost, s));
         MQVS_HIP(hipStreamSynchronize(s));
+        ws.host_flags[0] = ws.host_flags[16];
+        ws.host_flags[1] = ws.host_flags[20];
+        ws.host_flags[4] = ws.host_flags[17];
+        ws.host_flags[5] = ws.host_flags[18];
+        ws.host_flags[6] = ws.host_flags[19];
         if (kind == kScanBf16) {
             st.survivors_max = ws.host_flags[4];
             st.survivors_total = (uint32_t)ws.host_flags[5];

@@ -37,14 +37,25 @@ def column_files(data_f32, sizes, block=1 << 20, method=0x82):
 
 
 @pytest.mark.parametrize("kind,block,method", [("gauss", 1 << 20, 0x82), ("quantised", 65536, 0x82),
-                                               ("repeats", 4097, 0x82), ("gauss", 300000, 0x02)])
+                                               ("repeats", 4097, 0x82), ("gauss", 300000, 0x02),
+                                               ("quantised", 1 << 20, 0x82), ("period24k", 1 << 20, 0x82),
+                                               ("period40k", 1 << 20, 0x82)])
 def test_gpu_ingest_dense(mq, kind, block, method):
+    """periodNk: the rows repeat every N KiB, so nearly every match reaches
+    back further than the decoder's 16 KiB LDS ring (its far-match path reads
+    the block's flushed output), long matches included."""
     rng = np.random.default_rng(11)
     n, d = 20000, 64
     if kind == "gauss":
         rows = rng.standard_normal((n, d)).astype(np.float32)
     elif kind == "quantised":
         rows = np.round(rng.standard_normal((n, d)), 1).astype(np.float32)
+    elif kind.startswith("period"):
+        period = (96 if kind == "period24k" else 156)  # rows of 256 B: 24576 / 39936 B
+        base = rng.standard_normal((period, d)).astype(np.float32)
+        base[::7] = np.round(base[::7], 1)
+        rows = np.tile(base, (n // period + 1, 1))[:n].copy()
+        rows[::97] += 1.0  # break some matches: fresh literals between far matches
     else:  # long matches incl. overlapping ones (runs of equal values, repeated rows)
         base = np.repeat(rng.integers(-3, 4, (n // 8, d // 4)).astype(np.float32), 4, axis=1)
         rows = np.repeat(base, 8, axis=0)
