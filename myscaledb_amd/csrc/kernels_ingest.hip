@@ -27,12 +27,13 @@
 
 namespace mqvs {
 
-// LDS ring of the block's latest output.  16 KiB (not the 64 KiB LZ4 window)
-// so that eight decode waves fit on a CU: the decode is latency-bound per
+// LDS ring of the block's latest output.  8 KiB (not the 64 KiB LZ4 window)
+// so that twenty decode waves fit on a CU: the decode is latency-bound per
 // wave, and a 64 KiB ring left two waves per CU.  Matches reaching further
-// back (1-2 % of them on quantised float columns) read the already-flushed
+// back (~6 % of them on quantised float columns) read the already-flushed
 // output from global memory (far_byte).
-constexpr int kRing = 16384;
+constexpr int kRing = 8192;
+constexpr int kFlush = 2048;  // unflushed output < kFlush + one step (< kRing - 256)
 
 __global__ void k_block_table(const uint8_t *src, int64_t n, IngestBlock *tab, int64_t max_blocks,
                               int64_t *out) {
@@ -201,9 +202,9 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
             return (v >> (8 * (o & 3))) & 255u;
         };
         // Output goes to the LDS ring only and is flushed to global memory in
-        // runs of >= 4 KiB with dword stores; unflushed bytes stay < 4 KiB +
-        // one step (< 4.6 KiB), so the ring never overwrites them and every
-        // byte further back than kRing - 256 is already in global memory.  (One wave per
+        // runs of >= kFlush bytes with dword stores; unflushed bytes stay <
+        // kFlush + one step, so the ring never overwrites them and every byte
+        // further back than kRing - 256 is already in global memory.  (One wave per
         // workgroup: its LDS accesses complete in program order, so a ring
         // read after a ring write sees it; the wave barriers only keep the
         // compiler from moving them.)
@@ -308,7 +309,7 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
                 // far match (off > mlen-step, so no replication within a
                 // 256-byte step): from the flushed output
                 for (int32_t d0 = 0; d0 < mlen; d0 += 256) {
-                    if (op + d0 - fl >= 4096) flush(op + d0);
+                    if (op + d0 - fl >= kFlush) flush(op + d0);
                     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the flushes landed)
                     const int32_t cnt = mlen - d0 < 256 ? mlen - d0 : 256;
                     uint32_t v[4];
@@ -334,7 +335,7 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
                 const int32_t chunk = 256;  // off <= kRing - 256 here
                 for (int32_t d0 = 0; d0 < mlen; d0 += chunk) {
                     __builtin_amdgcn_wave_barrier();
-                    if (op + d0 - fl >= 4096) {
+                    if (op + d0 - fl >= kFlush) {
                         flush(op + d0);
                         __builtin_amdgcn_wave_barrier();
                     }
@@ -355,7 +356,7 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
                 __builtin_amdgcn_wave_barrier();
             }
             op += mlen;
-            if (op - fl >= 4096) flush(op);
+            if (op - fl >= kFlush) flush(op);
         }
         __builtin_amdgcn_wave_barrier();
         flush(op);
