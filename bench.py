@@ -48,6 +48,7 @@ def parse():
     ap.add_argument("--no-small", action="store_true", help="skip the nq = 1 / 4 / 16 / 64 sweep")
     ap.add_argument("--pmc", default=None, help="rocprofv3 PMC summary JSON for roofline.traffic")
     ap.add_argument("--no-index", action="store_true", help="skip the index (configs[2]) leg")
+    ap.add_argument("--no-configs", action="store_true", help="skip the configs[3] shard / configs[4] hybrid leg")
     ap.add_argument("--index-settings", default="nprobe=2;nprobe=3;nprobe=4;nprobe=8",
                     help="';'-separated mqvs_index_search parameter strings timed by the index leg")
     ap.add_argument("--index-hard-mode", type=int, default=3,
@@ -413,7 +414,7 @@ def roofline(st, main_ms, nq, d, args):
     return roof
 
 
-def exact_check(mq_scan, seg, q, k, ids, dst):
+def exact_check(mq_scan, seg, q, k, ids, dst, **kw):
     """Outside the timed region: the same batch on the exact fp32 path
     (mqvs_set_batch_mode(1): fp32 MFMA fma chains over every row for nq >= 20,
     the faiss sequential formula below) and the timed path's output compared
@@ -421,7 +422,7 @@ def exact_check(mq_scan, seg, q, k, ids, dst):
     path against it."""
     mq_scan.set_batch_mode(1)
     try:
-        ei, ed = seg.search(q, k)
+        ei, ed = seg.search(q, k, **kw)
     finally:
         mq_scan.set_batch_mode(0)
     gi, gd = ids.cpu().numpy(), dst.cpu().numpy()
@@ -477,6 +478,77 @@ def small_batch_leg(mq_scan, seg, args, nqs=(1, 4, 16, 64), reps=10):
                     "survey_t_star_ms": round(t_star, 3), "survey_t_star_over_t": round(t_star / ms, 3),
                     "survivors_max": stt["survivors_max"],
                     "exact": chk})
+    return out
+
+
+def configs_leg(mq, mq_scan, args):
+    """BASELINE configs[3] (one of the 8 granule-aligned row-range shards of
+    the 100M x 1536 IP part: what each GPU of the 8-GPU configuration holds)
+    and configs[4] (50M x 768 L2, PREWHERE attr < T at 10 % and 1 %), on their
+    own parts generated in HBM after the main part is freed.  Per point: the
+    median end-to-end search time (device pointers), the main-scan time and
+    the bf16-plane bytes it read, and the exact-path check on every query."""
+    import torch
+    from myscaledb_amd import _lib
+    from myscaledb_amd.sharded import shard_rows
+    from myscaledb_amd.vector_scan import generate_device, pack_bitmap
+    k = 100
+
+    def point(seg, nq, d, mode, reps, plane_rows, **kw):
+        q = torch.empty((nq, d), dtype=torch.float32, device="cuda")
+        generate_device(SEED_QUERY, mode, 0, nq, d, q)
+        ids = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+        dst = torch.empty((nq, k), dtype=torch.float32, device="cuda")
+        seg.search(q, k, out=(ids, dst), **kw)
+        mq_scan.set_timing(True)
+        walls, sts = [], []
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            seg.search(q, k, out=(ids, dst), **kw)
+            torch.cuda.synchronize()
+            walls.append((time.perf_counter() - t0) * 1e3)
+            sts.append(_lib.last_search_stats())
+        mq_scan.set_timing(False)
+        ms = float(np.median(walls))
+        st = sts[int(np.argsort(walls)[len(walls) // 2])]
+        plane = 2.0 * plane_rows * seg_dpad(d)
+        return {"nq": nq, "ms_per_search": round(ms, 3), "qps": round(nq / (ms * 1e-3), 1),
+                "main_ms": round(st["main_ms"], 3), "gather": st["gather"], "rows_scanned": st["rows_scanned"],
+                "plane_bytes_read": plane, "end_to_end_gbs": round(plane / (ms * 1e-3) / 1e9, 1),
+                "rescans": st["rescans"], "exact": exact_check(mq_scan, seg, q, k, ids, dst, **kw)}
+
+    out = {}
+    d3 = 1536
+    r0, r1 = shard_rows(100_000_000, args.granule, 3, 8)
+    seg = mq.VectorScanSegment.generate(SEED_BASE, 1, r1 - r0, d3, "IP", args.granule, row_offset=r0)
+    try:
+        out["config3_shard"] = {
+            "workload": f"FLAT IP, rows [{r0}, {r1}) of 100M x 1536 (one of 8 row-range shards), N(0,1), top-{k}",
+            "points": [point(seg, nq, d3, 1, 5 if nq == 1000 else 10, r1 - r0) for nq in (1, 16, 1000)]}
+    finally:
+        seg.free()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    n4, d4 = 50_000_000, 768
+    seg = mq.VectorScanSegment.generate(SEED_BASE, 1, n4, d4, "L2", args.granule)
+    try:
+        attr = np.random.default_rng(0x5EED0003).integers(0, 100, size=n4, dtype=np.uint8)
+        pts = []
+        for sel in (10, 1):
+            mask = attr < sel
+            bm = torch.from_numpy(pack_bitmap(mask)).cuda()
+            for nq in (1, 16):
+                e = point(seg, nq, d4, 1, 10, int(mask.sum()), filter_bitmap=bm)
+                e["selectivity_pct"] = sel
+                pts.append(e)
+        out["config4_hybrid"] = {
+            "workload": f"FLAT L2 50M x 768, WHERE attr < T (uniform attr in [0, 100)), top-{k}",
+            "points": pts}
+    finally:
+        seg.free()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
     return out
 
 
@@ -607,7 +679,8 @@ def main():
             "dtype": "f32",
             "compute": compute,
             "data": "synthetic (counter-based %s, generated in HBM)" % {
-                0: "exact integers in [-8, 8]", 1: "N(0,1)", 2: "gaussian mixture, 4096 centres"}[args.mode],
+                0: "exact integers in [-8, 8]", 1: "N(0,1)", 2: "gaussian mixture, 4096 centres",
+                3: "gaussian mixture, 65536 centres, unit noise"}[args.mode],
             "config": {"workload": f"FLAT {args.metric} {n // 1_000_000}M x {d} Float32, batch {nq}, "
                                    f"top-{k} (BASELINE configs[1])",
                        "n": n, "d": d, "nq": nq, "k": k, "metric": args.metric, "generator_mode": args.mode,
@@ -630,6 +703,11 @@ def main():
             result["cpu_baseline"] = cpu_baseline(O, args)
         if not args.no_index and world == 1:
             result["index"] = index_leg(mq, seg, args)
+        if not args.no_configs and world == 1:
+            seg.free()  # (room for the 50M x 768 part)
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
+            result["configs"] = configs_leg(mq, mq_scan, args)
         print(json.dumps(result), flush=True)
     if comm is not None:
         comm.free()

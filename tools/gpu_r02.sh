@@ -24,10 +24,10 @@ fi
 timeout -k 10 600 python -u bench.py "$@" > gpurun_out/bench.json 2> gpurun_out/bench.err || { echo "bench failed rc=$?"; tail -30 gpurun_out/bench.err; exit 1; }
 cat gpurun_out/bench.json
 ( cd /tmp && timeout -k 10 400 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/gpurun_out/prof" -o run --output-format csv \
-    -- python "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu --no-verify --no-small --no-index "$@" \
+    -- python "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu --no-verify --no-small --no-index --no-configs "$@" \
     > "$GRAFT_REPO_ROOT/gpurun_out/prof_bench.json" 2> "$GRAFT_REPO_ROOT/gpurun_out/prof.err" )
 rc=$?; echo "rocprof rc=$rc"; [ $rc -ne 0 ] && exit 1
 [ $PMC = 0 ] && exit 0
-bash tools/gpu_pmc.sh python bench.py --steps 2 --warmup 0 --no-cpu --no-verify --no-index --no-small "$@" || exit 1
+bash tools/gpu_pmc.sh python bench.py --steps 2 --warmup 0 --no-cpu --no-verify --no-index --no-small --no-configs "$@" || exit 1
 python tools/pmc_traffic.py gpurun_out --searches 2 --nq 1000 --out gpurun_out/pmc_traffic.json > /dev/null
 echo "pmc summary rc=$?"
