@@ -381,8 +381,11 @@ int mqvs_index_last_stats(mqvs_index_search_stats *out);
  * CacheKey string, weighed by HBM bytes against max_bytes.
  *   put      takes ownership of seg / idx (the index must be over seg); evicts
  *            least-recently-used unheld entries to make room; a key already
- *            present is replaced.  MQVS_ERR_MEMORY_LIMIT when the budget
- *            cannot hold it (ownership then stays with the caller).
+ *            present is replaced (putting the same pair under its own key
+ *            again only refreshes it).  MQVS_ERR_MEMORY_LIMIT when the budget
+ *            cannot hold it, MQVS_ERR_BAD_ARGUMENTS for an index over another
+ *            segment or a handle already cached under another key (ownership
+ *            then stays with the caller).
  *   acquire  *seg = NULL on a miss; on a hit the entry is held (never evicted)
  *            and becomes most recently used; the handles stay owned by the
  *            cache.  Every hit is paired with release(key, seg).

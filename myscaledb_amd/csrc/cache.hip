@@ -102,9 +102,19 @@ int mqvs_cache_free(mqvs_cache_t c) {
 int mqvs_cache_put(mqvs_cache_t c, const char *key, mqvs_segment_t seg, mqvs_index_t idx) {
     return guarded([&] {
         if (!c || !key || !seg) fail(MQVS_ERR_BAD_ARGUMENTS, "null cache, key or segment");
+        if (idx && index_segment(idx) != seg) fail(MQVS_ERR_BAD_ARGUMENTS, "the index was not built over this segment");
         const size_t w = weight(seg, idx);
         std::lock_guard<std::mutex> lock(c->mu);
         auto found = c->map.find(key);
+        if (found != c->map.end() && found->second->seg == seg && found->second->idx == idx) {
+            c->lru.splice(c->lru.begin(), c->lru, found->second);  // the same entry again: most recently used
+            return;
+        }
+        // a handle has one owner: never two entries over the same segment / index
+        for (const std::list<Entry> *l : {&c->lru, &c->expired})
+            for (const Entry &e : *l)
+                if (e.seg == seg || (idx && e.idx == idx))
+                    fail(MQVS_ERR_BAD_ARGUMENTS, "segment or index already cached (key '" + e.key + "')");
         if (found != c->map.end()) {  // replace: the old entry leaves the map
             auto it = found->second;
             c->bytes -= it->bytes;

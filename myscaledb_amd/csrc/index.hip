@@ -68,6 +68,10 @@ struct mqvs_index {
 };
 
 namespace mqvs {
+mqvs_segment *index_segment(mqvs_index *idx) { return idx ? idx->seg : nullptr; }
+}  // namespace mqvs
+
+namespace mqvs {
 
 static thread_local mqvs_index_search_stats g_istats{};
 constexpr int64_t kCoarseChunk = 256;  // centroids per coarse "list"

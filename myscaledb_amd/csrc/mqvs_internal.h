@@ -365,6 +365,8 @@ void launch_probe_select_approx(const float *probe, int64_t P, int64_t ld, int n
 void launch_refine(const Cand *cin, const int *cnt_in, int cap, int nq, int k, int metric,
                    bool approx, const float *bq, uint32_t *tau, float *thr, Cand *cout, int *cnt_out,
                    hipStream_t s);
+// the segment an index was built over (cache.hip validates put pairs)
+mqvs_segment *index_segment(mqvs_index *idx);
 void launch_rerank_select(const ScanParams &p, int metric, const float *bq, int k, int64_t id_offset,
                           int64_t *out_ids, float *out_dist, int *overflow, uint32_t *surv, int *scnt,
                           uint4 *recs, int lcap, int64_t rs, hipStream_t s);

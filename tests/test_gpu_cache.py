@@ -122,3 +122,29 @@ def test_decoupled_part_row_ids_and_filter(mq):
     assert np.array_equal(decoupled_filter(newf, n0 + n1, None, None, 0, n0 + n1), newf)
     idx.free()
     seg.free()
+
+
+def test_cache_rejects_double_ownership(mq):
+    from myscaledb_amd._lib import MqvsError
+    from myscaledb_amd.cache import PartCache
+    cache = PartCache(1 << 34)
+    s0 = _seg(mq, 31)
+    h = s0._h
+    cache.put("a", s0)
+    s0._h = h  # a stale Python handle to the cached segment
+    with pytest.raises(MqvsError) as e:
+        cache.put("b", s0)  # the same segment under a second key
+    assert e.value.name == "BAD_ARGUMENTS"
+    cache.put("a", s0)  # the same pair again: a refresh, not a double free
+    s0._h = None
+    other = _seg(mq, 32)
+    idx = mq.VectorIndex.build(other, "MSTG", "nlist=8")
+    s1 = _seg(mq, 33)
+    with pytest.raises(MqvsError) as e:
+        cache.put("c", s1, idx)  # index over another segment
+    assert e.value.name == "BAD_ARGUMENTS"
+    idx.free()
+    other.free()
+    s1.free()
+    assert cache.stats()["items"] == 1
+    cache.free()
