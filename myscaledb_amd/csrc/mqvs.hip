@@ -523,7 +523,10 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     const int64_t target_cands = std::min<int64_t>(cap / 3, std::max<int64_t>(tune.target, 2 * (int64_t)k));
     uint4 *large = k > kSortCap ? (uint4 *)ws.large.get(sizeof(uint4) * 2 * kLargeCap * (size_t)nq) : nullptr;
     int64_t P = scan_n;
-    if (scan_n > 32768) {
+    // (small k over a part much larger than k -- e.g. the index build's
+    // top-1 k-means assignment against 10^4 centroids -- also takes a short
+    // probe: a dense probe of every row would dominate the search)
+    if (scan_n > 32768 || (k <= 16 && scan_n > 16 * tile_rows)) {
         P = (int64_t)(((double)k * (double)scan_n) / target_cands) + 1;
         // (a shorter probe is cheaper but its looser threshold sends more
         // waves of the first segments down the append path: measured net
