@@ -262,13 +262,13 @@ static int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 // memset launch), or null
 static int prep_variants(Workspace &ws, const float *dq, int nq, int d, bool cos, bool l2norms, int64_t ords,
                          bool may_sync, float *&qvars, float *&qnorms, int *&qmu, int *&qlam, int *&status,
-                         hipStream_t s, int *zeroed_status = nullptr) {
+                         hipStream_t s, int *zeroed_status = nullptr, int maxv_override = 0) {
     const int64_t qstride = round_up(d, 32);
     qnorms = (float *)ws.qnorms.get(sizeof(float) * nq);
     qmu = (int *)ws.qmu.get(sizeof(int) * nq);
     qlam = (int *)ws.qlam.get(sizeof(int) * nq);
     status = zeroed_status ? zeroed_status : (int *)ws.status.get(sizeof(int) * 4);
-    int maxv = cos ? kMaxVariants : 1;
+    int maxv = cos ? (maxv_override > 0 ? maxv_override : kMaxVariants) : 1;
     for (int pass = 0; pass < 2; ++pass) {
         const size_t bytes = sizeof(float) * (size_t)nq * maxv * qstride;
         qvars = (float *)ws.qvars.get(bytes);
@@ -277,7 +277,7 @@ static int prep_variants(Workspace &ws, const float *dq, int nq, int d, bool cos
         launch_query_prep(dq, nq, d, cos ? MQVS_METRIC_COSINE : MQVS_METRIC_L2, l2norms, qvars, maxv, qnorms, qmu,
                           qlam, status, s);
         MQVS_HIP(hipGetLastError());
-        if (pass > 0 || !cos || ords <= maxv || !may_sync) break;
+        if (pass > 0 || !cos || ords <= maxv || !may_sync || maxv_override > 0) break;
         MQVS_HIP(hipMemcpyAsync(ws.host_flags + 12, status, sizeof(int), hipMemcpyDeviceToHost, s));
         MQVS_HIP(hipStreamSynchronize(s));
         if (!ws.host_flags[12]) break;
@@ -360,7 +360,7 @@ static SegTune seg_tune(int nq) {
 static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, int metric,
                         const uint8_t *filter, const uint8_t *exists, int64_t *out_ids,
                         float *out_dist, uint32_t flags, hipStream_t user_stream,
-                        bool force_exact = false, int64_t ord_base = -1) {
+                        bool force_exact = false, int64_t ord_base = -1, int maxv_hint = 0) {
     if (!seg) fail(MQVS_ERR_BAD_ARGUMENTS, "null segment");
     if (seg->binary) fail(MQVS_ERR_LOGICAL, "binary (FixedString) segment: search it with mqvs_search_binary");
     if (nq < 0 || k < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "nq and k must be non-negative");
@@ -384,7 +384,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
                 const int m = std::min(qb, nq - q0);
                 search_impl(seg, queries + (size_t)q0 * seg->d, m, k, metric, filter, exists,
                             out_ids + (size_t)q0 * k, out_dist + (size_t)q0 * k, flags, user_stream, force_exact,
-                            ord_base);
+                            ord_base, maxv_hint);
             }
             return;
         }
@@ -482,8 +482,12 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     // one zeroed block for the status words: [overflow 4][status 4][count nq]
     int *fl = (int *)ws.flags.get(sizeof(int) * (8 + (size_t)nq));
     MQVS_HIP(hipMemsetAsync(fl, 0, sizeof(int) * (8 + (size_t)nq), s));
-    const int maxv = prep_variants(ws, dq, nq, d, cos, (mfma || bf16) && metric == MQVS_METRIC_L2, ords,
-                                   !(dev && (flags & MQVS_F_ASYNC)), qvars, qnorms, qmu, qlam, status, s, fl + 4);
+    // The query-variant table starts at kMaxVariants per query without a host
+    // round trip; a chain that does not repeat within it on a part of more
+    // chunk ordinals (rare: small-integer data) is caught from the status word
+    // read at the end, and the search re-runs with the larger table.
+    const int maxv = prep_variants(ws, dq, nq, d, cos, (mfma || bf16) && metric == MQVS_METRIC_L2, ords, false,
+                                   qvars, qnorms, qmu, qlam, status, s, fl + 4, maxv_hint);
 
     // ---- chunk ordinals
     const int *chunk_ord = nullptr;
@@ -716,13 +720,20 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         // a query whose re-normalisation does not repeat within maxv steps is
         // exact only on the part's first maxv chunk ordinals (maxv covers
         // every ordinal unless the part has more than kMaxVariantsCap chunks)
-        if (ws.host_flags[1] && ords > maxv)
+        if (ws.host_flags[1] && ords > maxv) {
+            const int want = (int)std::min<int64_t>(ords, kMaxVariantsCap);
+            if (maxv < want) {
+                search_impl(seg, queries, nq, k, metric, filter, exists, out_ids, out_dist, flags, user_stream,
+                            force_exact, ord_base, want);
+                return;
+            }
             fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not repeat within " + std::to_string(maxv) +
                                        " steps on a part of more chunks");
+        }
         if (kind == kScanBf16 && ws.host_flags[0]) {
             // the bf16 bound left too many candidates: exact fp32 path
             search_impl(seg, queries, nq, k, metric, filter, exists, out_ids, out_dist, flags,
-                        user_stream, true, ord_base);
+                        user_stream, true, ord_base, maxv);
             g_stats.rescans += 1;
             return;
         }
