@@ -484,7 +484,7 @@ def small_batch_leg(mq_scan, seg, args, nqs=(1, 4, 16, 64), reps=10):
 def configs_leg(mq, mq_scan, args):
     """BASELINE configs[3] (one of the 8 granule-aligned row-range shards of
     the 100M x 1536 IP part: what each GPU of the 8-GPU configuration holds)
-    and configs[4] (50M x 768 L2, PREWHERE attr < T at 10 % and 1 %), on their
+    and configs[4] (50M x 768 L2, PREWHERE attr < T at 100 / 50 / 10 / 1 %), on their
     own parts generated in HBM after the main part is freed.  Per point: the
     median end-to-end search time (device pointers), the main-scan time and
     the bf16-plane bytes it read, and the exact-path check on every query."""
@@ -535,10 +535,10 @@ def configs_leg(mq, mq_scan, args):
     try:
         attr = np.random.default_rng(0x5EED0003).integers(0, 100, size=n4, dtype=np.uint8)
         pts = []
-        for sel in (10, 1):
+        for sel in (100, 50, 10, 1):  # SURVEY 8(d) config 4 sweep
             mask = attr < sel
             bm = torch.from_numpy(pack_bitmap(mask)).cuda()
-            for nq in (1, 16):
+            for nq in ((1, 16) if sel <= 10 else (1,)):
                 e = point(seg, nq, d4, 1, 10, int(mask.sum()), filter_bitmap=bm)
                 e["selectivity_pct"] = sel
                 pts.append(e)

@@ -101,6 +101,11 @@ const char *mqvs_last_error(void);
 int mqvs_async_check(mqvs_stream_t stream);
 /* Release this thread's stream/workspace (optional; freed at thread exit). */
 int mqvs_thread_release(void);
+/* Library shutdown for the calling thread (SURVEY 8(b) lifecycle): waits for
+ * the thread's streams and releases its workspaces, as mqvs_thread_release.
+ * Segments, indexes, caches and communicators stay owned by the caller and
+ * are freed with their own *_free calls. */
+int mqvs_shutdown(void);
 
 /* ---- segments: one data part's Array(Float32) column resident in HBM ---- */
 /* host_rows: n*d row-major fp32; rows whose Array is empty must be FLT_MAX

@@ -34,7 +34,7 @@ F_TIMING = 0x100
 # Exported C symbols: every one of these is declared in include/mqvs.h.
 SYMBOLS = [
     "mqvs_abi_version", "mqvs_init", "mqvs_device_count", "mqvs_last_error",
-    "mqvs_thread_release", "mqvs_segment_create", "mqvs_segment_create_device",
+    "mqvs_thread_release", "mqvs_shutdown", "mqvs_segment_create", "mqvs_segment_create_device",
     "mqvs_segment_generate", "mqvs_segment_free", "mqvs_segment_info", "mqvs_segment_prefilter", "mqvs_segment_rows",
     "mqvs_search", "mqvs_search_ex", "mqvs_knn_raw", "mqvs_rerank", "mqvs_merge_shards", "mqvs_generate_device",
     "mqvs_last_search_stats", "mqvs_set_timing", "mqvs_set_batch_mode", "mqvs_set_gather_mode", "mqvs_set_prefilter",
@@ -111,6 +111,7 @@ def _load():
         "mqvs_device_count": ([P], ctypes.c_int),
         "mqvs_last_error": ([], ctypes.c_char_p),
         "mqvs_thread_release": ([], ctypes.c_int),
+        "mqvs_shutdown": ([], ctypes.c_int),
         "mqvs_segment_create": ([P, I64, I32, I32, I64, P, I64, P], ctypes.c_int),
         "mqvs_segment_create_device": ([P, I64, I32, I32, I64, P, I64, P], ctypes.c_int),
         "mqvs_segment_generate": ([U64, I32, I64, I32, I32, I64, I64, P], ctypes.c_int),

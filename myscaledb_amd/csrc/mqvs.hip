@@ -1355,6 +1355,8 @@ int mqvs_thread_release(void) {
     });
 }
 
+int mqvs_shutdown(void) { return mqvs_thread_release(); }
+
 int mqvs_segment_create(const float *host_rows, int64_t n, int32_t d, int32_t metric,
                         int64_t granule_rows, const uint8_t *nonempty, int64_t row_offset,
                         mqvs_segment_t *out) {
