@@ -406,7 +406,8 @@ __device__ inline void lds_store_b128(const void *addr, float x, uint32_t y, int
 // DIAG (diagnostic builds, wrong results; MQVS_HI_PPDIAG): 1 = row pieces
 // from the first 8 tiles only (L2-resident rows), 4 = query pieces not
 // issued, 8 = row pieces not issued, 16 = a trivial epilogue (the MFMAs stay
-// live: one compare of an accumulator sum per item).
+// live: one compare of an accumulator sum per item), 32 = the threshold
+// pre-check as OR-ed compares instead of a max tree (an A/B variant: exact).
 template <int METRIC, int NBUF, int DIAG = 0>
 __global__ __launch_bounds__(512) void k_scan_hi_pp(ScanParams p, int slots) {
     constexpr int WR = 4, WQ = 2, QB = 4, NW = 8;
@@ -598,10 +599,19 @@ __global__ __launch_bounds__(512) void k_scan_hi_pp(ScanParams p, int slots) {
                 for (int jb = 0; jb < QB; ++jb)
 #pragma unroll
                     for (int rb = 0; rb < 2; ++rb) {
-                        float mx = acc[rb][jb][0];
+                        // any of the 16 over the threshold (DIAG & 32: 16
+                        // compares OR-ed as lane masks; else an fmaxf tree)
+                        bool any = false;
+                        if constexpr ((DIAG & 32) != 0) {
 #pragma unroll
-                        for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[rb][jb][r]);
-                        if (mx >= thr[jb]) {
+                            for (int r = 0; r < 16; ++r) any |= acc[rb][jb][r] >= thr[jb];
+                        } else {
+                            float mx = acc[rb][jb][0];
+#pragma unroll
+                            for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[rb][jb][r]);
+                            any = mx >= thr[jb];
+                        }
+                        if (any) {
                             const int j = q0 + rq0 + jb * 32;
                             const int64_t rbase = cr0 + wr * 64 + rb * 32 + 4 * h;
 #pragma unroll
@@ -675,6 +685,7 @@ static bool launch_hi_pp(ScanParams p, hipStream_t s) {
         case 20: MQVS_PP(20); break;
         case 24: MQVS_PP(24); break;
         case 28: MQVS_PP(28); break;
+        case 32: MQVS_PP(32); break;
         default: MQVS_PP(0); break;
     }
 #undef MQVS_PP
