@@ -407,7 +407,8 @@ __device__ inline void lds_store_b128(const void *addr, float x, uint32_t y, int
 // from the first 8 tiles only (L2-resident rows), 4 = query pieces not
 // issued, 8 = row pieces not issued, 16 = a trivial epilogue (the MFMAs stay
 // live: one compare of an accumulator sum per item), 32 = the threshold
-// pre-check as OR-ed compares instead of a max tree (an A/B variant: exact).
+// pre-check as OR-ed compares instead of a max tree (an A/B variant: exact),
+// 64 = row pieces with the non-temporal policy (aux nt; an A/B variant: exact).
 template <int METRIC, int NBUF, int DIAG = 0>
 __global__ __launch_bounds__(512) void k_scan_hi_pp(ScanParams p, int slots) {
     constexpr int WR = 4, WQ = 2, QB = 4, NW = 8;
@@ -516,8 +517,12 @@ __global__ __launch_bounds__(512) void k_scan_hi_pp(ScanParams p, int slots) {
         for (int i = 0; i < GPW; ++i) {
             if ((DIAG & 8) && i < YPW) continue;
             if ((DIAG & 4) && i >= YPW) continue;
-            __builtin_amdgcn_global_load_lds((const void *)(src[i] + (int64_t)si * 1024),
-                                             (lds_void *)(dst + (w + i * NW) * 1024), 16, 0, 0);
+            if ((DIAG & 64) && i < YPW)
+                __builtin_amdgcn_global_load_lds((const void *)(src[i] + (int64_t)si * 1024),
+                                                 (lds_void *)(dst + (w + i * NW) * 1024), 16, 0, 2);
+            else
+                __builtin_amdgcn_global_load_lds((const void *)(src[i] + (int64_t)si * 1024),
+                                                 (lds_void *)(dst + (w + i * NW) * 1024), 16, 0, 0);
         }
         ++issued;
         if (++si == nst) {
@@ -686,6 +691,7 @@ static bool launch_hi_pp(ScanParams p, hipStream_t s) {
         case 24: MQVS_PP(24); break;
         case 28: MQVS_PP(28); break;
         case 32: MQVS_PP(32); break;
+        case 64: MQVS_PP(64); break;
         default: MQVS_PP(0); break;
     }
 #undef MQVS_PP
@@ -700,7 +706,7 @@ static bool launch_hi_pp(ScanParams p, hipStream_t s) {
 // into the fragment; a block's whole row (nst loads, 24 KiB at d = 768) is in
 // flight while the previous block feeds the MFMAs.  The query tile (NQB blocks
 // of 16 queries, every stage's B fragment: 4 VGPRs each) stays in registers.
-template <int METRIC, bool PROBE, int NQB, int NST>
+template <int METRIC, bool PROBE, int NQB, int NST, bool NT = false>
 __global__ __launch_bounds__(256) void k_scan_hi_reg(ScanParams p) {
     constexpr int RT = kBfRows;
     const int64_t ti = blockIdx.x / p.num_qblocks;
@@ -745,7 +751,16 @@ __global__ __launch_bounds__(256) void k_scan_hi_reg(ScanParams p) {
     auto load = [&](int buf, int rb) {
         const unsigned char *src = rowsrc(rb);
 #pragma unroll
-        for (int s = 0; s < NST; ++s) a[buf][s] = *reinterpret_cast<const bf16x4x2 *>(src + (int64_t)s * 1024);
+        for (int s = 0; s < NST; ++s) {
+            const bf16x4x2 *ps = reinterpret_cast<const bf16x4x2 *>(src + (int64_t)s * 1024);
+            if constexpr (NT) {
+                // streaming rows (read once per search): non-temporal loads
+                typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+                a[buf][s] = __builtin_bit_cast(bf16x4x2, __builtin_nontemporal_load(reinterpret_cast<const u32x4 *>(ps)));
+            } else {
+                a[buf][s] = *ps;
+            }
+        }
     };
     load(0, w);
 #pragma unroll
@@ -779,9 +794,21 @@ static void launch_hi_reg(ScanParams p, hipStream_t s) {
     p.num_qblocks = (p.nq + 16 * NQB - 1) / (16 * NQB);
     const int64_t grid = p.tiles * p.num_qblocks;
     if (grid < 1) return;
+    // rows streamed with non-temporal loads: 10M x 768 cosine main scan
+    // 2.55 -> 2.28 ms at nq 1 (6.0 -> 6.7 TB/s), 2.80 -> 2.55 ms at nq 16,
+    // bit-identical (profiles/r02/smallnq/nt_ab.jsonl).  A/B switch
+    // (tools/ab_split.py): MQVS_HI_NT=0 = plain loads
+    const char *nte = std::getenv("MQVS_HI_NT");
+    const bool nt = !(nte && nte[0] == '0');
     switch (p.dpad / HI_K) {
-#define MQVS_HI_REG(N_) \
-    case N_: hipLaunchKernelGGL((k_scan_hi_reg<METRIC, PROBE, NQB, N_>), dim3((unsigned)grid), dim3(256), 0, s, p); return;
+#define MQVS_HI_REG(N_)                                                                                        \
+    case N_:                                                                                                   \
+        if (nt)                                                                                                \
+            hipLaunchKernelGGL((k_scan_hi_reg<METRIC, PROBE, NQB, N_, true>), dim3((unsigned)grid), dim3(256), 0, s, \
+                               p);                                                                             \
+        else                                                                                                   \
+            hipLaunchKernelGGL((k_scan_hi_reg<METRIC, PROBE, NQB, N_>), dim3((unsigned)grid), dim3(256), 0, s, p); \
+        return;
         MQVS_HI_REG(2) MQVS_HI_REG(4) MQVS_HI_REG(6) MQVS_HI_REG(8) MQVS_HI_REG(10) MQVS_HI_REG(12)
         MQVS_HI_REG(14) MQVS_HI_REG(16) MQVS_HI_REG(18) MQVS_HI_REG(20) MQVS_HI_REG(22) MQVS_HI_REG(24)
 #undef MQVS_HI_REG

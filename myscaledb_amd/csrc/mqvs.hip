@@ -342,6 +342,10 @@ static SegTune seg_tune(int nq) {
     if (nq <= 4) {
         v.first = 8;
         v.growth = 4;
+        // one or two queries: a 4x shorter probe (its single-workgroup select
+        // 53 -> 21 us at 10M x 768; one more segment; wall median 2.80 ->
+        // 2.75 ms at nq 1, no gain at nq 4, profiles/r02/smallnq/seg_ab.jsonl)
+        if (nq <= 2) v.target = 65536;
     } else if (nq < 256) {
         v.first = 4;
         v.growth = 4;
