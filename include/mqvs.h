@@ -335,7 +335,11 @@ int mqvs_index_info(mqvs_index_t idx, mqvs_index_info_t *out);
 /* Search params (comma-separated key=value, may be NULL or ""):
  *   alpha        [1, 4]: probes nprobe(alpha) lists (more = higher recall)
  *   nprobe       lists probed per query (overrides alpha; <= min(nlist, 4096))
- *   num_reorder  candidates re-ranked exactly (default max(2k, 64), <= 4096)
+ *   num_reorder  candidates re-ranked exactly (default max(2k, 64), capped at
+ *                4096 for k <= 2048; k .. 32768; above 4096 the select and the
+ *                re-rank sort through device scratch, 2 num_reorder records of
+ *                16 B per query each, in query sub-batches of <= 1 GB)
+ * k: 1 .. 16384, as mqvs_search (max_search_result_window, Settings.h:923).
  * filter / row_exists: LSB-first bitmaps over the segment's rows, or NULL.
  * Output as mqvs_search (k per query, reference order, -1 padding).  With
  * MQVS_F_FIRST_STAGE the call returns the first stage only: the k best rows

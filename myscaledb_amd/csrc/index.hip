@@ -78,7 +78,7 @@ constexpr int64_t kCoarseChunk = 256;  // centroids per coarse "list"
 
 // plan / scan / select buffers of one list pass
 struct ListBufs {
-    DevBuf lcount, lfill, lstart, lq, items, grp, chk, nitems, qbase, qstart, cand, stats;
+    DevBuf lcount, lfill, lstart, lq, items, grp, chk, nitems, qbase, qstart, cand, stats, large;
 };
 
 struct IndexWorkspace {
@@ -483,7 +483,9 @@ static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, c
     MQVS_HIP(hipGetLastError());
     if (ev) MQVS_HIP(hipEventRecord(ev[3], s));
     const int64_t expect = dense ? npos : (int64_t)((double)nprobe * npos / std::max<int64_t>(nlist, 1) * 1.5);
-    launch_ivf_select(p.cand, p.qstart, nq, R, metric, out_rows, id_offset, out_approx, expect, s);
+    // R above kSortCap: the select sorts through 2 R records of scratch per query
+    uint4 *gscr = R > kSortCap ? (uint4 *)b.large.get(sizeof(uint4) * 2 * (size_t)R * nq) : nullptr;
+    launch_ivf_select(p.cand, p.qstart, nq, R, metric, out_rows, id_offset, out_approx, expect, s, gscr);
     MQVS_HIP(hipGetLastError());
     if (ev) MQVS_HIP(hipEventRecord(ev[4], s));
 }
@@ -495,7 +497,7 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     if (nq < 0 || k < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "nq and k must be non-negative");
     if (nq > 0 && k > 0 && (!queries || !out_ids || !out_dist))
         fail(MQVS_ERR_BAD_ARGUMENTS, "null query or output pointer");
-    if (k > kSortCap) fail(MQVS_ERR_BAD_ARGUMENTS, "k above " + std::to_string(kSortCap) + " not supported");
+    if (k > kMaxK) fail(MQVS_ERR_BAD_ARGUMENTS, "k above " + std::to_string(kMaxK) + " not supported");
     const auto pm = parse_params(params);
     check_keys(pm, {"alpha", "nprobe", "num_reorder"}, "search");
     const bool first_stage = flags & MQVS_F_FIRST_STAGE;
@@ -503,9 +505,12 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     const int nprobe = pm.count("nprobe")
                            ? (int)num_param(pm, "nprobe", 1, 1, (double)std::min<int64_t>(ix->nlist, kSortCap))
                            : nprobe_of(ix, alpha);
+    // num_reorder up to kSortCap sorts in LDS; above it (k > 2048 by default,
+    // up to kLargeCap) through global scratch
     const int R = first_stage ? k
-                              : (int)num_param(pm, "num_reorder", (double)std::min(kSortCap, std::max(2 * k, 64)),
-                                               (double)std::max(k, 1), (double)kSortCap);
+                              : (int)num_param(pm, "num_reorder",
+                                               (double)std::min(k > kSortCap / 2 ? kLargeCap : kSortCap, std::max(2 * k, 64)),
+                                               (double)std::max(k, 1), (double)kLargeCap);
     mqvs_index_search_stats st{};
     st.nq = nq;
     st.k = k;
@@ -513,6 +518,21 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     st.num_reorder = R;
     g_istats = st;
     if (nq == 0 || k == 0) return;
+    if (R > kSortCap) {
+        // the select and the re-rank each take 2 R records of scratch per
+        // query: query sub-batches of <= 1 GB of it
+        const int qb = (int)std::max<int64_t>(1, ((int64_t)1 << 26) / (2 * (int64_t)R));
+        if (nq > qb) {
+            const int d = ix->seg->d;
+            for (int q0 = 0; q0 < nq; q0 += qb) {
+                const int m = std::min(qb, nq - q0);
+                search_index_impl(ix, queries + (size_t)q0 * d, m, k, params, filter, exists,
+                                  out_ids + (size_t)q0 * k, out_dist + (size_t)q0 * k, flags, user_stream);
+            }
+            g_istats.nq = nq;
+            return;
+        }
+    }
 
     mqvs_segment *seg = ix->seg;
     DeviceGuard guard(seg->device);
@@ -627,7 +647,8 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
         rp.exists = dexists;
         rp.filter = nullptr;  // the scan applied the filter; candidates pass it
         rp.nonempty = seg->nonempty_bits;
-        launch_rerank_ids(rp, ix->metric, crow, R, k, seg->row_offset, dids, ddist, nullptr, s);
+        uint4 *rscr = R > kSortCap ? (uint4 *)ws.fine.large.get(sizeof(uint4) * 2 * (size_t)R * nq) : nullptr;
+        launch_rerank_ids(rp, ix->metric, crow, R, k, seg->row_offset, dids, ddist, rscr, s);
         MQVS_HIP(hipGetLastError());
         MQVS_HIP(hipEventRecord(ws.ev[5], s));
     }

@@ -600,6 +600,7 @@ __global__ __launch_bounds__(512) void k_scan_hi_pp(ScanParams p, int slots) {
             // 4 ms at 10M x 768, nq 1000, as much as the LDS-DMA stream; a
             // ballot-compacted walk measured slower than this one)
             if (!(DIAG & 16)) {
+                const int crn = (int)(cr1 - cr0);  // rows of the item (<= RT)
 #pragma unroll
                 for (int jb = 0; jb < QB; ++jb)
 #pragma unroll
@@ -617,13 +618,22 @@ __global__ __launch_bounds__(512) void k_scan_hi_pp(ScanParams p, int slots) {
                             any = mx >= thr[jb];
                         }
                         if (any) {
+                            // (row offsets in the tile as 32-bit values, the
+                            // 64-bit row formed only under the branch behind
+                            // an opaque copy: otherwise the compiler shares
+                            // the rows' addresses in the candidate bitmaps
+                            // across the jb blocks, hoisting 32 of them out
+                            // of the walk and spilling them at every item)
                             const int j = q0 + rq0 + jb * 32;
-                            const int64_t rbase = cr0 + wr * 64 + rb * 32 + 4 * h;
+                            const int rlb = wr * 64 + rb * 32 + 4 * h;
 #pragma unroll
                             for (int r = 0; r < 16; ++r) {
                                 const float raw = acc[rb][jb][r];
-                                const int64_t row = rbase + (r & 3) + 8 * (r >> 2);
-                                if (raw >= thr[jb] && row < cr1 && j < p.nq) {
+                                const int rl = rlb + (r & 3) + 8 * (r >> 2);
+                                if (raw >= thr[jb] && rl < crn && j < p.nq) {
+                                    int rlo = rl;
+                                    asm volatile("" : "+v"(rlo));
+                                    const int64_t row = cr0 + rlo;
                                     const int pos = lds_add_rtn(&qcount, 1);
                                     if (pos < kPpQueue)
                                         lds_store_b128(queue + pos, raw, (uint32_t)row, j);

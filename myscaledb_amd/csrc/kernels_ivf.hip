@@ -406,20 +406,27 @@ __global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
 // record array has room for, fall back to a position-ordered pass for them.
 constexpr int kTieCap = 64;  // <= every NT the kernel is launched with
 
-template <int METRIC, int NT>
+// LARGE (R above kSortCap, num_reorder / k up to kLargeCap): the records go to
+// 2 R records of global scratch per query (gscr) and are sorted there by
+// global_sort (LDS runs of kSortCap, then merge passes); NT = SEL_THREADS.
+template <int METRIC, int NT, bool LARGE = false>
 __global__ __launch_bounds__(NT) void k_ivf_select(const Cand *cand, const int64_t *qstart, int R,
                                                    int64_t *out_rows, int64_t id_offset, float *out_approx,
-                                                   int keycap) {
-    extern __shared__ __attribute__((aligned(16))) uint4 recs[];  // pow2 >= R records, then the key cache
+                                                   int keycap, uint4 *gscr) {
+    // pow2 >= R records (LARGE: kSortCap, the sort runs), then the key cache
+    extern __shared__ __attribute__((aligned(16))) uint4 recs[];
     __shared__ uint4 ties[kTieCap];
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh[4];
     __shared__ int s_wave[NT / 64];
     __shared__ int s_m, s_tie;
+    static_assert(!LARGE || NT == SEL_THREADS, "global_sort strides by SEL_THREADS");
     int N = 1;
     while (N < R) N <<= 1;
-    uint32_t *kc = reinterpret_cast<uint32_t *>(recs + N);
+    uint32_t *kc = reinterpret_cast<uint32_t *>(recs + (LARGE ? kSortCap : N));
     const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    uint4 *rr = LARGE ? gscr + (int64_t)q * 2 * R : recs;  // the records (LARGE: [0, R); [R, 2R) sort scratch)
+    const int mcap = LARGE ? R : N;                        // room for records below th + ties
     const Cand *c = cand + qstart[q];
     const int64_t T = qstart[q + 1] - qstart[q];
     auto gkey = [&](int64_t i) {
@@ -455,7 +462,7 @@ __global__ __launch_bounds__(NT) void k_ivf_select(const Cand *cand, const int64
         if (all || key < th) {
             const Cand e = c[i];
             const int pos = atomicAdd(&s_m, 1);
-            if (pos < R) recs[pos] = make_uint4(key, e.row, __builtin_bit_cast(uint32_t, e.raw), 0u);
+            if (pos < R) rr[pos] = make_uint4(key, e.row, __builtin_bit_cast(uint32_t, e.raw), 0u);
         } else if (key == th) {
             const Cand e = c[i];
             const int pos = atomicAdd(&s_tie, 1);
@@ -480,9 +487,9 @@ __global__ __launch_bounds__(NT) void k_ivf_select(const Cand *cand, const int64
     int m = below;
     if (!all) {
         const int nt = s_tie;
-        if (nt <= kTieCap && below + nt <= N) {
+        if (nt <= kTieCap && below + nt <= mcap) {
             // the ties after the records below th (kTieCap <= NT)
-            if (t < nt) recs[below + t] = ties[t];
+            if (t < nt) rr[below + t] = ties[t];
             m = below + nt;
         } else {
             // mass ties: the first R - below of them by position
@@ -506,7 +513,7 @@ __global__ __launch_bounds__(NT) void k_ivf_select(const Cand *cand, const int64
                 off += __popcll(bal & ((1ull << lane) - 1ull));
                 if (flag && off < R) {
                     const Cand e = c[i];
-                    recs[off] = make_uint4(key, e.row, __builtin_bit_cast(uint32_t, e.raw), 0u);
+                    rr[off] = make_uint4(key, e.row, __builtin_bit_cast(uint32_t, e.raw), 0u);
                 }
                 __syncthreads();
                 if (t == 0) {
@@ -520,6 +527,10 @@ __global__ __launch_bounds__(NT) void k_ivf_select(const Cand *cand, const int64
         }
     }
     __syncthreads();
+    const uint4 *sorted = recs;
+    if constexpr (LARGE) {
+        sorted = global_sort(rr, rr + R, m, recs);
+    } else {
     int Nm = 1;
     while (Nm < m) Nm <<= 1;
     for (int i = m + t; i < Nm; i += NT) recs[i] = make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
@@ -540,9 +551,10 @@ __global__ __launch_bounds__(NT) void k_ivf_select(const Cand *cand, const int64
             __syncthreads();
         }
     }
+    }
     for (int i = t; i < R; i += NT) {
         const bool ok = i < m;
-        const uint4 r = ok ? recs[i] : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
+        const uint4 r = ok ? sorted[i] : make_uint4(0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu);
         if (out_approx) {
             out_rows[(int64_t)q * R + i] = ok ? (int64_t)r.y + id_offset : -1;
             const float raw = __builtin_bit_cast(float, r.z);
@@ -736,7 +748,7 @@ void launch_ivf_scan(const IvfParams &p, int metric, int grid, hipStream_t s) {
 }
 
 void launch_ivf_select(const Cand *cand, const int64_t *qstart, int nq, int R, int metric, int64_t *out_rows,
-                       int64_t id_offset, float *out_approx, int64_t expect_len, hipStream_t s) {
+                       int64_t id_offset, float *out_approx, int64_t expect_len, hipStream_t s, uint4 *gscr) {
     if (R <= 16 && !out_approx) {
         const dim3 grid((unsigned)((nq + 3) / 4));
 #define MQVS_SMALL(M, RM_) \
@@ -756,8 +768,11 @@ void launch_ivf_select(const Cand *cand, const int64_t *qstart, int nq, int R, i
 #undef MQVS_SMALL
         return;
     }
+    const bool large = R > kSortCap;
+    if (large && !gscr) fail(MQVS_ERR_LOGICAL, "ivf select: no scratch for num_reorder above 4096");
     int N = 1;
     while (N < R) N <<= 1;
+    if (large) N = kSortCap;  // LDS: the sort runs
     // LDS key cache sized for the expected region length (<= 64 KiB, and
     // within the LDS left beside the records); long regions (many probed
     // lists) get 1024 threads per query
@@ -768,12 +783,15 @@ void launch_ivf_select(const Cand *cand, const int64_t *qstart, int nq, int R, i
     const bool wide = expect_len > 16384;
 #define MQVS_SEL(M)                                                                                                 \
     do {                                                                                                            \
-        if (wide)                                                                                                   \
+        if (large)                                                                                                  \
+            hipLaunchKernelGGL((k_ivf_select<M, SEL_THREADS, true>), dim3(nq), dim3(SEL_THREADS), lds, s, cand,     \
+                               qstart, R, out_rows, id_offset, out_approx, keycap, gscr);                           \
+        else if (wide)                                                                                              \
             hipLaunchKernelGGL((k_ivf_select<M, 1024>), dim3(nq), dim3(1024), lds, s, cand, qstart, R, out_rows,    \
-                               id_offset, out_approx, keycap);                                                      \
+                               id_offset, out_approx, keycap, nullptr);                                             \
         else                                                                                                        \
             hipLaunchKernelGGL((k_ivf_select<M, SEL_THREADS>), dim3(nq), dim3(SEL_THREADS), lds, s, cand, qstart, R, \
-                               out_rows, id_offset, out_approx, keycap);                                            \
+                               out_rows, id_offset, out_approx, keycap, nullptr);                                   \
     } while (0)
     switch (metric) {
         case MQVS_METRIC_L2: MQVS_SEL(MQVS_METRIC_L2); break;

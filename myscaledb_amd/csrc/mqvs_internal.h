@@ -412,7 +412,7 @@ void launch_ivf_plan_dense(const IvfParams &p, int64_t npos, hipStream_t s);
 void launch_ivf_scan(const IvfParams &p, int metric, int grid, hipStream_t s);
 // expect_len: typical per-query region length (sizes the LDS key cache)
 void launch_ivf_select(const Cand *cand, const int64_t *qstart, int nq, int R, int metric, int64_t *out_rows,
-                       int64_t id_offset, float *out_approx, int64_t expect_len, hipStream_t s);
+                       int64_t id_offset, float *out_approx, int64_t expect_len, hipStream_t s, uint4 *gscr = nullptr);
 void launch_ivf_pack(const float *rows, const float *norms, int d, const int32_t *perm, int64_t npos, int64_t dpad,
                      uint16_t *plane, float *pnorm, hipStream_t s);
 void launch_gather_rows(const float *src, int64_t src_ld, int d, const int64_t *idx, int64_t m, float *dst,

@@ -158,6 +158,38 @@ def test_index_two_stage(mq):
     assert np.array_equal(dist1.view(np.uint32), dist2.view(np.uint32))
 
 
+@pytest.mark.parametrize("metric,k,R,lwd", [("L2", 5000, None, None), ("Cosine", 8000, 16000, None),
+                                             ("IP", 4000, 12000, 0.3)])
+def test_index_large_k_equals_flat(mq, metric, k, R, lwd):
+    """k above 4096 (LIMIT up to max_search_result_window, Settings.h:923;
+    the reference searches k + deleted rows, MergeTreeVSManager.cpp:1565):
+    num_reorder above 4096 takes the global-scratch select and re-rank; with
+    every list probed the result equals FLAT bit for bit."""
+    n, d, nq, nlist = 30000, 64, 6, 16
+    rows = O.generate(0x5EED0001, 1, 0, n, d)
+    q = O.generate(0x5EED0002, 1, 0, nq, d)
+    ex = None
+    if lwd:
+        rng = np.random.default_rng(7)
+        ex = np.packbits((rng.random(n) >= lwd).astype(np.uint8), bitorder="little")
+    seg = mq.VectorScanSegment.from_rows(rows, metric=metric, granule=8192)
+    idx = mq.VectorIndex.build(seg, "MSTG", {"nlist": nlist})
+    try:
+        params = {"nprobe": nlist}
+        if R:
+            params["num_reorder"] = R
+        ids_i, dist_i = idx.search(q, k, params, row_exists=ex)
+        st = mq.vector_index.last_index_stats()
+        ids_f, dist_f = seg.search(q, k, row_exists=ex)
+    finally:
+        idx.free()
+        seg.free()
+    assert st["num_reorder"] == (R or min(32768, 2 * k))
+    assert (ids_i[:, k - 1] >= 0).all()
+    assert np.array_equal(ids_i, ids_f)
+    assert np.array_equal(dist_i.view(np.uint32), dist_f.view(np.uint32))
+
+
 def test_index_params_errors(mq):
     from myscaledb_amd import _lib
     seg = mq.VectorScanSegment.generate(1, 1, 2000, 16, metric="L2")
