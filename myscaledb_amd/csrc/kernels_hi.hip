@@ -27,6 +27,7 @@
 // then the MFMA work.  No __syncthreads() in the loop: its fence would drain
 // the in-flight LDS-DMA (cdna_hip_programming.md, "Pipelining across barriers").
 #include <cstdio>
+#include <atomic>
 #include <cstdlib>
 
 #include "mqvs_internal.h"
@@ -408,9 +409,27 @@ __device__ inline void lds_store_b128(const void *addr, float x, uint32_t y, int
 // issued, 8 = row pieces not issued, 16 = a trivial epilogue (the MFMAs stay
 // live: one compare of an accumulator sum per item), 32 = the threshold
 // pre-check as OR-ed compares instead of a max tree (an A/B variant: exact),
-// 64 = row pieces with the non-temporal policy (aux nt; an A/B variant: exact).
+// 64 = row pieces with the non-temporal policy (aux nt; an A/B variant: exact),
+// 256 = SYNC: the query blocks of a row tile kept within kPpLag items of each
+// other (an A/B variant: exact).  They run on different CUs of one XCD and
+// share the tile through its L2 only while they stream it at about the same
+// time; left alone they drift apart over the ~600 items of a launch and each
+// re-reads the rows from beyond the L2 (PMC: 53 GB per search from the L2's
+// misses against 15.2 GB of plane).  Every kPpSyncEvery items wave 0 reads its
+// siblings' progress words (scalar loads: lgkmcnt, so no wait on the LDS-DMA
+// ring) and sleeps while one is more than kPpLag items behind -- for at most
+// kPpSpin rounds, so the result never depends on it and nothing can deadlock.
+constexpr int kPpSyncEvery = 4, kPpLag = 1, kPpSpin = 64;
+__device__ unsigned g_pp_prog[2048];  // per workgroup: epoch << 16 | items done
+
+__device__ inline unsigned sload_glc(const unsigned *ptr) {
+    unsigned v;
+    asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(ptr) : "memory");
+    return v;
+}
+
 template <int METRIC, int NBUF, int DIAG = 0>
-__global__ __launch_bounds__(512) void k_scan_hi_pp(ScanParams p, int slots) {
+__global__ __launch_bounds__(512) void k_scan_hi_pp(ScanParams p, int slots, unsigned epoch) {
     constexpr int WR = 4, WQ = 2, QB = 4, NW = 8;
     constexpr int QT = 32 * QB * WQ;  // 256
     constexpr int RT = kBfRows;       // 256
@@ -537,6 +556,7 @@ __global__ __launch_bounds__(512) void k_scan_hi_pp(ScanParams p, int slots) {
     int64_t ti_c = ti_i;
     int sc = 0;
     int64_t gc = 0;
+    unsigned done = 0;  // items finished (SYNC)
 
     constexpr int OFF_Q = GY * 1024;
     auto frag = [&](const unsigned char *st, int r, int c) {
@@ -661,6 +681,26 @@ __global__ __launch_bounds__(512) void k_scan_hi_pp(ScanParams p, int slots) {
             sc = 0;
             int cord;
             ti_c = next_item(ti_c + tstride, cr0, cr1, cord);
+            if constexpr ((DIAG & 256) != 0) {
+                ++done;
+                if (w == 0) {
+                    if (lane == 0)
+                        __hip_atomic_store(&g_pp_prog[blockIdx.x], (epoch << 16) | done, __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_AGENT);
+                    if (done % kPpSyncEvery == 0 && nqb > 1) {
+                        for (int it = 0; it < kPpSpin; ++it) {
+                            bool behind = false;
+                            for (int b = 0; b < nqb; ++b) {
+                                if (b == qb) continue;
+                                const unsigned v = sload_glc(&g_pp_prog[xcd + 8 * (tg * nqb + b)]);
+                                if ((v >> 16) != epoch || (v & 0xFFFFu) + kPpLag < done) behind = true;
+                            }
+                            if (!behind) break;
+                            __builtin_amdgcn_s_sleep(8);
+                        }
+                    }
+                }
+            }
         }
         ++gc;
         if (grp == 0 && has_next) wait_vm<NPW, D>(pend);
@@ -692,16 +732,18 @@ static bool launch_hi_pp(ScanParams p, hipStream_t s) {
     const int slots = per_xcd / p.num_qblocks * p.num_qblocks;
     const char *dg = std::getenv("MQVS_HI_PPDIAG");
     const int diag = dg ? std::atoi(dg) : 0;
-#define MQVS_PP(DG_) \
-    hipLaunchKernelGGL((k_scan_hi_pp<METRIC, 4, DG_>), dim3((unsigned)(8 * per_xcd)), dim3(512), 0, s, p, slots)
+    static std::atomic<unsigned> launches{0};
+    const unsigned epoch = (launches.fetch_add(1, std::memory_order_relaxed) + 1) & 0xFFFFu;
+    // (the decomposition builds 17 / 20 / 24 / 28 of profiles/r02/pp_decomposition.jsonl
+    // are template arguments too: add their case to run them again)
+#define MQVS_PP(DG_)                                                                                             \
+    hipLaunchKernelGGL((k_scan_hi_pp<METRIC, 4, DG_>), dim3((unsigned)(8 * per_xcd)), dim3(512), 0, s, p, slots, \
+                       epoch)
     switch (diag) {
         case 16: MQVS_PP(16); break;
-        case 17: MQVS_PP(17); break;
-        case 20: MQVS_PP(20); break;
-        case 24: MQVS_PP(24); break;
-        case 28: MQVS_PP(28); break;
         case 32: MQVS_PP(32); break;
         case 64: MQVS_PP(64); break;
+        case 256: MQVS_PP(256); break;
         default: MQVS_PP(0); break;
     }
 #undef MQVS_PP
