@@ -487,9 +487,37 @@ __global__ __launch_bounds__(512) void k_scan_hi_pp(ScanParams p, int slots, uns
     }
 
     // item cursor helpers (items are tiles of this slot's sequence)
+    // 32-bit tile arithmetic when the part allows it: tile_range's 64-bit
+    // divisions are software sequences of ~120 instructions, three per call,
+    // and an item boundary runs two of these calls (the issue cursor in a read
+    // phase, the compute cursor after the epilogue), exposed to the partner
+    // wave at the barrier.  (DIAG & 1024: tile_range, an A/B variant.)
+    const bool t32 = (DIAG & 1024) == 0 && p.row_end + p.chunk_rows + p.tile_rows <= 0x7FFFFFFF &&
+                     p.tiles <= 0x7FFFFFFF && p.row_begin >= 0;
+    const uint32_t c0_32 = (t32 && p.tiles_per_chunk > 0) ? (uint32_t)p.row_begin / (uint32_t)p.chunk_rows : 0u;
     auto item_range = [&](int64_t ti, int64_t &r0, int64_t &r1, int &ord) -> bool {
         int64_t chunk;
-        tile_range(p, ti, r0, r1, chunk);
+        if (t32) {
+            const uint32_t tt = (uint32_t)ti, tr = (uint32_t)p.tile_rows;
+            if (p.tiles_per_chunk > 0) {
+                const uint32_t tpc = (uint32_t)p.tiles_per_chunk, cr = (uint32_t)p.chunk_rows;
+                const uint32_t qd = tt / tpc, rem = tt - qd * tpc;
+                const uint32_t c = c0_32 + qd, cs = c * cr;
+                const uint32_t a = cs + rem * tr;
+                const uint32_t e = a + tr < cs + cr ? a + tr : cs + cr;
+                r0 = a;
+                r1 = e;
+                chunk = c;
+            } else {
+                const uint32_t a = (uint32_t)p.row_begin + tt * tr;
+                r0 = a;
+                r1 = (int64_t)a + tr;
+                chunk = p.chunk_rows > 0 ? a / (uint32_t)p.chunk_rows : 0;
+            }
+            if (r1 > p.row_end) r1 = p.row_end;
+        } else {
+            tile_range(p, ti, r0, r1, chunk);
+        }
         ord = (int)chunk + p.ord_base;  // (no chunk_ord table on this path)
         return r0 < r1;
     };
@@ -744,6 +772,7 @@ static bool launch_hi_pp(ScanParams p, hipStream_t s) {
         case 32: MQVS_PP(32); break;
         case 64: MQVS_PP(64); break;
         case 256: MQVS_PP(256); break;
+        case 1024: MQVS_PP(1024); break;
         default: MQVS_PP(0); break;
     }
 #undef MQVS_PP
