@@ -276,12 +276,23 @@ int mqvs_knn_binary_raw(const uint8_t *x, const uint8_t *y, int64_t d, int64_t k
  * (MergeTreeBaseSearchManager.cpp:207-297 getTotalTopSearchResultImpl; the
  * Distributed engine's per-shard LIMIT + initiator merge,
  * StorageDistributed.cpp:1057-1060) for one part spread over GPUs.  A
- * communicator serves one search at a time. */
+ * communicator serves one search at a time.  Before any search work the
+ * ranks exchange a header (shard rows, granule, dimension, nq / k / metric,
+ * argument errors): shards out of row order, disagreeing calls or a failing
+ * rank make EVERY rank return the error instead of leaving the others in a
+ * collective; a rank whose local search fails still joins the exchange, and
+ * all ranks then fail together. */
 #define MQVS_COMM_ID_BYTES 128
 typedef struct mqvs_comm *mqvs_comm_t;
 int mqvs_comm_unique_id(uint8_t *id /* MQVS_COMM_ID_BYTES */);
 int mqvs_comm_init(int32_t nranks, int32_t rank, const uint8_t *id, mqvs_comm_t *out);
 int mqvs_comm_free(mqvs_comm_t comm);
+/* A loopback communicator group: nranks (<= 64) virtual ranks of ONE process
+ * on the current device, out[0 .. nranks-1] one handle per rank.  Each rank's
+ * mqvs_sharded_search runs on its own thread (the exchanges are device copies
+ * between host barriers); everything else is the RCCL communicator's code.
+ * For tests and single-GPU rehearsal of a multi-GPU layout; free every handle. */
+int mqvs_comm_init_loopback(int32_t nranks, mqvs_comm_t *out);
 int mqvs_sharded_search(mqvs_comm_t comm, mqvs_segment_t shard, const float *queries, int32_t nq, int32_t k,
                         int32_t metric, const uint8_t *filter, const uint8_t *row_exists, int64_t *out_ids,
                         float *out_dist, uint32_t flags, mqvs_stream_t stream);
@@ -441,7 +452,8 @@ typedef struct {
                                of selected rows (rows_scanned = list entries) */
     int32_t prefilter;      /* path 2: pre-filter split (2 = bf16 hi, 6 = bf16 + fp6 MX,
                                3 = bf16 x3) */
-    int32_t reserved;
+    int32_t batch_kernel;   /* path 2: 1 when the main scan ran the one-wave-per-SIMD batch
+                               kernel (nq > 128, contiguous rows), else 0 */
     int64_t survivors_total;/* path 2: rows re-ranked exactly (sum over queries) */
     int32_t survivors_max;  /* path 2: most rows re-ranked for one query */
     int32_t candidates_max; /* path 2: longest candidate list before the final bound */
@@ -467,6 +479,12 @@ int mqvs_set_gather_mode(int mode);
  * planes, three bf16 MFMAs (4 B per element).  All bound their error
  * rigorously and return the same bits. */
 int mqvs_set_prefilter(int split);
+/* Device scratch that one call may allocate for large-k sorts and candidate
+ * lists (default 1 GiB per buffer, at least 1 MiB): calls whose buffers would
+ * exceed it run in query sub-batches, which keep the whole call's distance
+ * formula (faiss's nx >= 20 branch) and return the same bits.  Returns the
+ * previous value; 0 leaves it unchanged. */
+size_t mqvs_set_scratch_budget(size_t bytes);
 
 #ifdef __cplusplus
 }

@@ -10,7 +10,10 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmqvs.so")
+# The release library.  Measurement tools (tools/ab_split.py) may load the
+# measurement build instead (MQVS_LIB=dbg -> libmqvs_dbg.so, `make dbg`), whose
+# kernels read A/B switches from the environment; the product never does.
+LIB_PATH = os.path.join(_HERE, "libmqvs_dbg.so" if os.environ.get("MQVS_LIB") == "dbg" else "libmqvs.so")
 
 # include/mqvs.h
 METRIC_L2, METRIC_IP, METRIC_COSINE, METRIC_HAMMING, METRIC_JACCARD = 0, 1, 2, 4, 5
@@ -38,10 +41,11 @@ SYMBOLS = [
     "mqvs_segment_generate", "mqvs_segment_free", "mqvs_segment_info", "mqvs_segment_prefilter", "mqvs_segment_rows",
     "mqvs_search", "mqvs_search_ex", "mqvs_knn_raw", "mqvs_rerank", "mqvs_merge_shards", "mqvs_generate_device",
     "mqvs_last_search_stats", "mqvs_set_timing", "mqvs_set_batch_mode", "mqvs_set_gather_mode", "mqvs_set_prefilter",
+    "mqvs_set_scratch_budget",
     "mqvs_index_build", "mqvs_index_free", "mqvs_index_info", "mqvs_index_search", "mqvs_index_last_stats",
     "mqvs_segment_create_binary", "mqvs_search_binary", "mqvs_knn_binary_raw",
     "mqvs_segment_create_from_column", "mqvs_async_check",
-    "mqvs_comm_unique_id", "mqvs_comm_init", "mqvs_comm_free", "mqvs_sharded_search",
+    "mqvs_comm_unique_id", "mqvs_comm_init", "mqvs_comm_init_loopback", "mqvs_comm_free", "mqvs_sharded_search",
     "mqvs_index_set_row_ids_map", "mqvs_decoupled_filter",
     "mqvs_cache_create", "mqvs_cache_free", "mqvs_cache_put", "mqvs_cache_acquire", "mqvs_cache_release",
     "mqvs_cache_remove", "mqvs_cache_stats",
@@ -57,7 +61,7 @@ class SearchStats(ctypes.Structure):
                 ("nq", ctypes.c_int32), ("k", ctypes.c_int32),
                 ("path", ctypes.c_int32), ("rescans", ctypes.c_int32),
                 ("segments", ctypes.c_int32), ("gather", ctypes.c_int32),
-                ("prefilter", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("prefilter", ctypes.c_int32), ("batch_kernel", ctypes.c_int32),
                 ("survivors_total", ctypes.c_int64), ("survivors_max", ctypes.c_int32),
                 ("candidates_max", ctypes.c_int32)]
 
@@ -129,6 +133,7 @@ def _load():
         "mqvs_set_timing": ([ctypes.c_int], ctypes.c_int),
         "mqvs_set_batch_mode": ([ctypes.c_int], ctypes.c_int),
         "mqvs_set_gather_mode": ([ctypes.c_int], ctypes.c_int),
+        "mqvs_set_scratch_budget": ([ctypes.c_size_t], ctypes.c_size_t),
         "mqvs_set_prefilter": ([ctypes.c_int], ctypes.c_int),
         "mqvs_index_build": ([P, ctypes.c_char_p, ctypes.c_char_p, P], ctypes.c_int),
         "mqvs_index_free": ([P], ctypes.c_int),
@@ -142,6 +147,7 @@ def _load():
         "mqvs_async_check": ([P], ctypes.c_int),
         "mqvs_comm_unique_id": ([P], ctypes.c_int),
         "mqvs_comm_init": ([I32, I32, P, P], ctypes.c_int),
+        "mqvs_comm_init_loopback": ([I32, P], ctypes.c_int),
         "mqvs_comm_free": ([P], ctypes.c_int),
         "mqvs_sharded_search": ([P, P, P, I32, I32, I32, P, P, P, P, U32, P], ctypes.c_int),
         "mqvs_index_set_row_ids_map": ([P, P, I64, U32], ctypes.c_int),

@@ -490,9 +490,12 @@ static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, c
     if (ev) MQVS_HIP(hipEventRecord(ev[4], s));
 }
 
+// formula_nq: the call's batch size, which selects the exact re-rank's
+// distance formula (0: nq; query sub-batches keep the call's, see mqvs.hip)
 static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int k, const char *params,
                               const uint8_t *filter, const uint8_t *exists, int64_t *out_ids, float *out_dist,
-                              uint32_t flags, hipStream_t user_stream) {
+                              uint32_t flags, hipStream_t user_stream, int formula_nq = 0) {
+    const int fnq = formula_nq > 0 ? formula_nq : nq;
     if (!ix) fail(MQVS_ERR_BAD_ARGUMENTS, "null index");
     if (nq < 0 || k < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "nq and k must be non-negative");
     if (nq > 0 && k > 0 && (!queries || !out_ids || !out_dist))
@@ -521,13 +524,13 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     if (R > kSortCap) {
         // the select and the re-rank each take 2 R records of scratch per
         // query: query sub-batches of <= 1 GB of it
-        const int qb = (int)std::max<int64_t>(1, ((int64_t)1 << 26) / (2 * (int64_t)R));
+        const int qb = (int)std::max<int64_t>(1, (int64_t)scratch_budget() / 16 / (2 * (int64_t)R));
         if (nq > qb) {
             const int d = ix->seg->d;
             for (int q0 = 0; q0 < nq; q0 += qb) {
                 const int m = std::min(qb, nq - q0);
                 search_index_impl(ix, queries + (size_t)q0 * d, m, k, params, filter, exists,
-                                  out_ids + (size_t)q0 * k, out_dist + (size_t)q0 * k, flags, user_stream);
+                                  out_ids + (size_t)q0 * k, out_dist + (size_t)q0 * k, flags, user_stream, fnq);
             }
             g_istats.nq = nq;
             return;
@@ -626,6 +629,7 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
         rp.n = seg->n;
         rp.d = d;
         rp.nq = nq;
+        rp.blas_nq = fnq;
         rp.qvars = qvars;
         rp.qnorms = qnorms;
         rp.qmu = qmu;

@@ -172,6 +172,12 @@ __global__ void k_query_bound(ScanParams p, int metric, int split, int direct,
         const float top = p.qnorms[j] * 1.0001f + ymax * ymax;
         const float rel = direct ? (3.0f * (float)p.d + 12.0f) * 5.9604645e-8f : 2.4e-7f;
         b = 2.0f * b + top * rel + 1e-30f;
+        if (split == kHiSplit) {
+            // the batch scan (kernels_p4.hip) starts its accumulation at
+            // -|y|^2 / 2 and forms fl(qn - 2 acc): the accumulation bound
+            // covers |y|^2 / 2 more per term, and the two final roundings
+            b += 2.0f * 2.04f * du * 0.5f * ymax * ymax + 2.4e-7f * top;
+        }
     } else if (metric == MQVS_METRIC_COSINE) {
         b = b + 2.4e-7f;  // 1 - ip rounds; ties on 1-ip may differ in ip by one ulp of 1
     }
@@ -181,7 +187,7 @@ __global__ void k_query_bound(ScanParams p, int metric, int split, int direct,
 
 void launch_query_bound(const ScanParams &p, int metric, int split, const float *ynorm_max,
                         const float *qrec, const float *yrec, float *bq, hipStream_t s) {
-    const int direct = p.nq < kBlasThreshold;
+    const int direct = !blas_formula(p);
     hipLaunchKernelGGL(k_query_bound, dim3(p.nq), dim3(64), 0, s, p, metric, split, direct, ynorm_max, qrec, yrec,
                        bq);
 }

@@ -32,6 +32,7 @@
 
 #include "mqvs_internal.h"
 #include "scan_emit.h"
+#include "tuning.h"
 
 namespace mqvs {
 
@@ -933,15 +934,31 @@ static bool launch_hi_tuned(const ScanParams &p, hipStream_t s) {
     }
 }
 
+// set when a main-scan launch of this thread took the batch kernel
+// (mqvs_search_stats.batch_kernel)
+static thread_local int g_batch_kernel_used = 0;
+int take_batch_kernel_flag() {
+    const int v = g_batch_kernel_used;
+    g_batch_kernel_used = 0;
+    return v;
+}
+
 template <int METRIC, bool PROBE>
 static void launch_hi_t(const ScanParams &p, hipStream_t s) {
     if constexpr (!PROBE)
         if (launch_hi_tuned<METRIC, PROBE>(p, s)) return;
-    if constexpr (!PROBE && METRIC != MQVS_METRIC_L2) {
-        // persistent ping-pong kernel: batches served by the 256 x 256 shape,
-        // contiguous rows, identity chunk ordinals (A/B switch MQVS_HI_PP=0)
-        const char *pp = std::getenv("MQVS_HI_PP");
-        if (!(pp && pp[0] == '0') && p.nq > 128 && !p.row_list && !p.chunk_ord && launch_hi_pp<METRIC>(p, s)) return;
+    if constexpr (!PROBE) {
+        // batches: the one-wave-per-SIMD persistent scan (kernels_p4.hip) for
+        // contiguous rows and identity chunk ordinals; measurement builds can
+        // select the 8-wave ping-pong kernel instead (MQVS_HI_PP=1) or neither
+        // (MQVS_HI_PP=0)
+        const int pp = tune_int("MQVS_HI_PP", 2);
+        if (p.nq > 128 && pp == 2 && launch_scan_p4(p, METRIC, s)) {
+            g_batch_kernel_used = 1;
+            return;
+        }
+        if constexpr (METRIC != MQVS_METRIC_L2)
+            if (p.nq > 128 && pp == 1 && !p.row_list && !p.chunk_ord && launch_hi_pp<METRIC>(p, s)) return;
     }
     const char *reg = std::getenv("MQVS_HI_REG");  // A/B switch (tools/ab_split.py): 0 = LDS kernel only
     const bool use_reg = !(reg && reg[0] == '0');

@@ -1,0 +1,573 @@
+// kernels_p4.hip -- the batch pre-filter scan (split 2, nq > 128) at ONE wave
+// per SIMD.  It replaces faiss's BLAS branch for large batches
+// (BruteForceSearch.h:80-87, exhaustive_L2sqr_blas / exhaustive_inner_product_blas)
+// as the first stage of kernels_hi.hip's bf16-hi pre-filter: the approximate
+// values it appends are re-ranked exactly afterwards (kernels_rerank.hip).
+//
+// Shape.  A persistent workgroup of 4 waves per CU walks work items of 256
+// rows x 256 queries.  Wave (wr, wq) owns 128 rows x 128 queries: 4 x 4
+// accumulators of v_mfma_f32_32x32x16_bf16 = 256 AGPRs, the whole accumulator
+// half of the register file.  Per 32-column stage a wave reads 16 fragments
+// (ds_read_b128) for 32 MFMAs: half the LDS fragment traffic per MFMA of the
+// 8-wave 64 x 128 shape (kernels_hi.hip, k_scan_hi_pp: 12 reads per 16), and
+// the stage's 32 KiB LDS-DMA image (256 rows + 256 queries x 64 B) is the same.
+//
+// Pipeline (per stage s, global stage counter over the whole launch): the
+// k-step-0 fragments of stage s are in registers at the top.  Between its 16
+// k-step-0 MFMAs the wave reads its k-step-1 fragments of stage s and issues
+// its 8 LDS-DMA pieces of stage s + D; it then waits (counted vmcnt) for its
+// own pieces of stage s + 1 and for its fragment reads (lgkmcnt(0)), and joins
+// ONE raw s_barrier: stage s + 1 is complete for every wave, and every wave is
+// done reading stage s, whose buffer the next phase re-fills (D = NBUF - 1).
+// Between the 16 k-step-1 MFMAs it reads the k-step-0 fragments of stage
+// s + 1.  The stage ring runs across item boundaries, so the next item's
+// first stages are in flight during the current item's last stages and
+// epilogue.
+//
+// First stage of an item: the k-step-0 MFMAs take C = 0 (an inline constant:
+// no accumulator zeroing) -- or, for L2, C = -|y|^2 / 2 of the block's rows,
+// read from a 1 KiB LDS copy of the item's row norms (one 4-B-per-lane
+// LDS-DMA piece per wave).  The accumulator then holds ip - |y|^2 / 2, and
+// the L2 append test qn - 2 acc <= t is a per-query threshold on acc, as for
+// IP and cosine.  The row norm enters before the products instead of after,
+// so the accumulation's error bound grows by |y|^2 / 2 per term
+// (k_query_bound adds it for L2).
+//
+// Epilogue: per query column, the maximum of the wave's 64 values (v_max3
+// chain) against the threshold; only a column over it walks its values.  A
+// candidate goes to this wave's queue in global memory at a slot given by a
+// ballot prefix count (no atomics, no LDS), flushed to the per-query lists at
+// the end of the launch.  A global atomic with return inside the loop would
+// make the wave wait for every LDS-DMA piece in flight; a full queue falls back
+// to exactly that (correct, slower).
+//
+// Items: as k_scan_hi_pp -- XCD x = blockIdx % 8 takes tiles t = x (mod 8); its
+// workgroups form groups of nqb query blocks that stream the same row tiles,
+// so a tile's rows are shared through that XCD's L2.
+#include <cstdint>
+#include <type_traits>
+#include <utility>
+
+#include "mqvs_internal.h"
+#include "scan_emit.h"
+#include "tuning.h"
+
+namespace mqvs {
+
+namespace {
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+typedef __attribute__((address_space(3))) void lds_void;
+}  // namespace
+
+constexpr int kP4Tile = 256;       // rows and queries per work item
+constexpr int kP4Stage = 32768;    // one stage: (256 rows + 256 queries) x 64 B
+constexpr int kP4QOff = 16384;     // query image within a stage
+constexpr int kP4HiK = 32;         // columns per stage
+
+// LDS image swizzle: image row r keeps its 16-B chunk c at slot
+// c ^ p4_g((r >> 2) & 3).  Conflict-free for the ds_read_b128 lane groups of
+// both the 32x32x16 fragment (lane -> row l & 31, chunk 2 kk + (l >> 5)) and
+// the 16x16x32 one (row l & 15, chunk l >> 4): in every 16-lane group the
+// (row & 3, slot) pairs are distinct.
+__device__ __host__ inline int p4_g(int x) { return (4 - x) & 3; }
+
+// s_waitcnt vmcnt(P n), n in [0, 3] at run time (P: pieces a wave issues per
+// stage; a stage that also carries a norm piece makes the wait stricter by
+// one operation, never looser)
+template <int P>
+__device__ inline void p4_wait_vm(int n) {
+    __builtin_amdgcn_sched_barrier(0);
+    if (P > 0 && n >= 3)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * P) : "memory");
+    else if (P > 0 && n == 2)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * P) : "memory");
+    else if (P > 0 && n == 1)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
+    else
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// f(integral_constant<int, 0>) ... f(integral_constant<int, N - 1>): compile-time
+// indices without relying on the unroller (the epilogue is too large for it)
+template <class F, int... I>
+__device__ inline void p4_for_impl(F &&f, std::integer_sequence<int, I...>) {
+    (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ inline void p4_for(F &&f) {
+    p4_for_impl(f, std::make_integer_sequence<int, N>{});
+}
+
+// v_max3_f32 (IEEE maxNum: a quiet NaN never wins, so a NaN value never
+// passes a threshold, as in emit_approx)
+__device__ inline float p4_max3(float a, float b, float c) {
+    float r;
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    return r;
+}
+
+__device__ inline void p4_barrier() {
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_barrier" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+}
+
+// DIAG (measurement builds only; wrong results): 4 = query pieces not issued,
+// 8 = row pieces not issued, 16 = trivial epilogue (one compare of an
+// accumulator sum per item)
+template <int METRIC, int NBUF, int DIAG = 0>
+__global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32x4 *queue, int qcap) {
+    constexpr bool L2 = METRIC == MQVS_METRIC_L2;
+    // stages in flight ahead of the one consumed: a buffer is re-filled one
+    // barrier after its last fragment reads retired (lgkmcnt(0) before it)
+    constexpr int D = NBUF - 1;
+    static_assert(D >= 1 && D <= 4, "ring depth");
+    constexpr int NORM = L2 ? 2048 : 0;  // two item-parity copies of 256 row norms
+    constexpr int NPW = 8 - ((DIAG & 8) ? 4 : 0) - ((DIAG & 4) ? 4 : 0);  // pieces per wave and stage
+    // ONE __shared__ object (an LDS access to a second object after an
+    // LDS-DMA makes the compiler wait for every DMA in flight)
+    __shared__ __attribute__((aligned(16))) unsigned char lds[NBUF * kP4Stage + NORM];
+    unsigned char *norm_lds = lds + NBUF * kP4Stage;
+
+    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    const int wr = w & 1, wq = w >> 1;
+    const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
+    const int nqb = p.num_qblocks;
+    const int ngroups = slots / nqb;
+    if (slot >= ngroups * nqb) return;  // whole workgroup, before any barrier
+    const int qb = slot % nqb, tg = slot / nqb;
+    const int q0 = qb * kP4Tile;
+    const int tstride = 8 * ngroups;
+    const int nst = (int)(p.dpad / kP4HiK);
+    const int l32 = lane & 31, h = lane >> 5;
+
+    // per-lane query constants: the four query rows of this wave's query
+    // pieces (variant cycles), the four query columns of its accumulators
+    int qj[4], qmu[4], qlam[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        int j = q0 + (w + 4 * i) * 16 + (lane >> 2);
+        if (j >= p.nq) j = 0;
+        qj[i] = j;
+        qmu[i] = 0;
+        qlam[i] = 1;
+        if (p.maxv > 1) {
+            qmu[i] = p.qmu[j];
+            qlam[i] = p.qlam[j];
+        }
+    }
+    // thresholds on the accumulator: IP / cosine acc >= t; L2 acc = ip - yn/2
+    // and the append test fl(qn - 2 acc) <= t, pre-checked as acc >= (qn - t)/2
+    // less a rounding slack (the walk applies the exact test)
+    // (slack: if fl(qn - 2 acc) <= t then acc >= (qn - t) / 2 - t u / (2 - 2u);
+    // the computed half may be u |qn - t| / 2 high; 8 u (|qn| + |t|) covers both)
+    float thr[4], tl[4], qnl[4];
+#pragma unroll
+    for (int jb = 0; jb < 4; ++jb) {
+        const int j = q0 + wq * 128 + jb * 32 + l32;
+        const float tj = j < p.nq ? p.thr[j] : 0.f;
+        tl[jb] = tj;
+        qnl[jb] = 0.f;
+        if constexpr (L2) {
+            const float qn = j < p.nq ? p.qnorms[j] : 0.f;
+            qnl[jb] = qn;
+            const float half = (qn - tj) * 0.5f;
+            thr[jb] = half - 4.8e-7f * (fabsf(qn) + fabsf(tj)) - 1e-30f;
+        } else {
+            thr[jb] = tj;
+        }
+        if (j >= p.nq) thr[jb] = __builtin_inff();  // padding queries never pass
+        asm volatile("" : "+v"(thr[jb]), "+v"(tl[jb]), "+v"(qnl[jb]));  // (the loads' waits land here)
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(qmu[i]), "+v"(qlam[i]));
+
+    // item cursors (items are tiles of this slot's sequence), in 32-bit
+    // arithmetic (the launcher checks the part allows it); every value is
+    // wave-uniform and kept in scalar registers
+    const uint32_t tr = (uint32_t)p.tile_rows, cr = (uint32_t)p.chunk_rows;
+    const uint32_t tpc = (uint32_t)p.tiles_per_chunk;
+    const uint32_t c0 = tpc > 0 ? (uint32_t)p.row_begin / cr : 0u;
+    const uint32_t rbeg = (uint32_t)p.row_begin, rend = (uint32_t)p.row_end;
+    const int ntiles = (int)p.tiles;
+    auto item_at = [&](int ti, int &r0, int &r1, int &ord) __attribute__((always_inline)) -> bool {
+        const uint32_t tt = (uint32_t)ti;
+        uint32_t a, e, c;
+        if (tpc > 0) {
+            const uint32_t qd = tt / tpc, rem = tt - qd * tpc;
+            c = c0 + qd;
+            const uint32_t cs = c * cr;
+            a = cs + rem * tr;
+            e = a + tr < cs + cr ? a + tr : cs + cr;
+        } else {
+            a = rbeg + tt * tr;
+            e = a + tr;
+            c = a / cr;
+        }
+        if (e > rend) e = rend;
+        r0 = __builtin_amdgcn_readfirstlane((int)a);
+        r1 = __builtin_amdgcn_readfirstlane((int)e);
+        ord = __builtin_amdgcn_readfirstlane((int)c) + p.ord_base;  // (no chunk_ord table on this path)
+        return r0 < r1;
+    };
+    auto next_item = [&](int ti, int &r0, int &r1, int &ord) __attribute__((always_inline)) -> int {
+        for (; ti < ntiles; ti += tstride)
+            if (item_at(ti, r0, r1, ord)) return ti;
+        return -1;
+    };
+
+    // issue cursor: item ti_i (rows [ir0, ir1), ordinal iord), next stage si
+    int ir0 = 0, ir1 = 0;
+    int iord = 0;
+    int ti_i = next_item(xcd + 8 * tg, ir0, ir1, iord);
+    if (ti_i < 0) return;  // no work (uniform)
+    const int nb = nst;
+    const uint32_t blk = (uint32_t)nb * 1024u;  // bytes of one 16-vector block over all stages
+    // DMA sources: a uniform base per stage + a 32-bit per-lane offset.
+    // Piece i < 4 is row piece pc = w + 4 i (image rows 16 pc .. +16), i >= 4
+    // query piece w + 4 (i - 4).  Lane -> image row lane >> 2 of the piece,
+    // slot lane & 3, which holds chunk (lane & 3) ^ p4_g((lane >> 4) & 3).
+    // Row tiles start on a 16-row block (the launcher checks), so row piece pc
+    // of an item is plane block ir0 / 16 + pc; a piece past the item's rows
+    // re-reads piece 0 (discarded).
+    const uint32_t lanec = (uint32_t)(lane >> 2) * 64u + (uint32_t)((lane & 3) ^ p4_g((lane >> 4) & 3)) * 16u;
+    uint32_t roff[4], qoff[4];
+    const unsigned char *rbase = nullptr;  // plane block of the item's first row (uniform)
+    const unsigned char *const qplane = reinterpret_cast<const unsigned char *>(p.q_hi);
+    uint32_t noff = 0;                      // L2: this lane's row norm, relative to the item's first row
+    const unsigned char *nbase = nullptr;
+    bool first_src = true;                  // query offsets: per item only for cosine variants
+    auto set_src = [&]() __attribute__((always_inline)) {
+        rbase = reinterpret_cast<const unsigned char *>(p.rows_hi) + (uint64_t)(uint32_t)(ir0 >> 4) * blk;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int pc = w + 4 * i;
+            roff[i] = (ir0 + pc * 16 < ir1 ? (uint32_t)pc * blk : 0u) + lanec;
+        }
+        if (p.maxv > 1 || first_src) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                int var = 0;
+                if (p.maxv > 1) var = iord < qmu[i] ? iord : qmu[i] + (iord - qmu[i]) % qlam[i];
+                const uint32_t u = (uint32_t)var * (uint32_t)p.q_vpad + (uint32_t)qj[i];
+                qoff[i] = (u >> 4) * blk + (u & 15) * 64u + (uint32_t)((lane & 3) ^ p4_g((lane >> 4) & 3)) * 16u;
+            }
+        }
+        if constexpr (L2) {
+            nbase = reinterpret_cast<const unsigned char *>(p.row_norms + ir0);
+            const int last = ir1 - 1 - ir0;
+            noff = (uint32_t)(64 * w + lane < last ? 64 * w + lane : last) * 4u;
+        }
+    };
+    set_src();
+    first_src = false;
+    int si = 0;           // next stage of the issue item
+    int issued = 0;       // stages issued (global counter)
+    int ibuf = 0;         // ring buffer of the next issued stage
+    int items_issued = 0;
+    bool live = true;     // stages left to issue (else: dummy pieces, never read)
+    // piece x of the next stage (x < 8; 8 = the L2 norm piece of an item's
+    // first stage).  Once every stage is issued the pieces keep going to the
+    // free buffer with the last sources (never read: the ring's counted waits
+    // stay uniform)
+    auto issue_piece = [&](int x) __attribute__((always_inline)) {
+        if ((DIAG & 8) && x < 4) return;
+        if ((DIAG & 4) && x >= 4 && x < 8) return;
+        unsigned char *dst = lds + ibuf * kP4Stage;
+        if (x < 4) {
+            __builtin_amdgcn_global_load_lds((const void *)(rbase + (uint32_t)si * 1024u + roff[x]),
+                                             (lds_void *)(dst + (w + 4 * x) * 1024), 16, 0, 0);
+        } else if (x < 8) {
+            __builtin_amdgcn_global_load_lds((const void *)(qplane + (uint32_t)si * 1024u + qoff[x - 4]),
+                                             (lds_void *)(dst + kP4QOff + (w + 4 * (x - 4)) * 1024), 16, 0, 0);
+        } else if constexpr (L2) {
+            __builtin_amdgcn_global_load_lds((const void *)(nbase + noff),
+                                             (lds_void *)(norm_lds + (items_issued & 1) * 1024 + w * 256), 4, 0, 0);
+        }
+    };
+    auto issue_advance = [&]() __attribute__((always_inline)) {
+        if (!live) return;
+        ++issued;
+        ibuf = ibuf + 1 == NBUF ? 0 : ibuf + 1;
+        if (++si == nst) {
+            si = 0;
+            ++items_issued;
+            int r0 = 0, r1 = 0, o = 0;
+            const int tn = next_item(ti_i + tstride, r0, r1, o);
+            if (tn >= 0) {
+                ti_i = tn;
+                ir0 = r0;
+                ir1 = r1;
+                iord = o;
+                set_src();
+            } else {
+                live = false;
+                si = nst - 1;  // dummy pieces re-read the last stage
+            }
+        }
+    };
+    auto issue_stage = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int x = 0; x < 8; ++x) issue_piece(x);
+        if (L2 && si == 0 && live) issue_piece(8);
+        issue_advance();
+    };
+
+    // compute cursor: item rows [cr0, cr1), stage sc, global stage gc
+    int cr0 = ir0, cr1 = ir1;
+    int ti_c = ti_i;
+    int gc = 0;    // stages consumed (global counter)
+    int cbuf = 0;  // ring buffer of stage gc
+    int items_done = 0;
+
+    // fragment offsets: image row R, chunk c at R * 64 + (c ^ p4_g((R >> 2) & 3)) * 16
+    const int gl = p4_g((l32 >> 2) & 3);
+    const int offa0 = l32 * 64 + ((0 + h) ^ gl) * 16;  // k-step 0: chunks 0 / 1
+    const int offa1 = l32 * 64 + ((2 + h) ^ gl) * 16;  // k-step 1: chunks 2 / 3
+    const int rowA = wr * 128 * 64, rowB = kP4QOff + wq * 128 * 64;
+    auto frag = [&](const unsigned char *st, int off) __attribute__((always_inline)) { return *reinterpret_cast<const bf16x8 *>(st + off); };
+
+    f32x16 acc[4][4];
+    int qcnt = 0;  // this wave's queue entries (wave-uniform)
+    u32x4 *wq_base = queue + (int64_t)(blockIdx.x * 4 + w) * qcap;
+
+    // prologue: D stages in flight, the first landed for everyone
+    for (int s = 0; s < D; ++s) issue_stage();
+    p4_wait_vm<NPW>(issued - 1);
+    p4_barrier();
+    bf16x8 a0[4], b0[4], a1[4], b1[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a0[i] = frag(lds, rowA + i * 32 * 64 + offa0);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) b0[i] = frag(lds, rowB + i * 32 * 64 + offa0);
+
+    // k-step-0 phase: 16 MFMAs on (a0, b0); between them the k-step-1
+    // fragments of this stage and the 8 LDS-DMA pieces of stage gc + D
+    auto k0_phase = [&](const unsigned char *st, auto first_tag) __attribute__((always_inline)) {
+        constexpr bool FIRST = decltype(first_tag)::value;
+        f32x16 cinit[4];
+        if constexpr (FIRST && L2) {
+            // C = -yn / 2 of the block's rows (the item's norms in LDS)
+            const unsigned char *nb_ = norm_lds + (items_done & 1) * 1024;
+#pragma unroll
+            for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+                for (int g = 0; g < 4; ++g) {
+                    const f32x4 v = *reinterpret_cast<const f32x4 *>(nb_ + (wr * 128 + rb * 32 + 8 * g + 4 * h) * 4);
+#pragma unroll
+                    for (int e = 0; e < 4; ++e) cinit[rb][4 * g + e] = -0.5f * v[e];
+                }
+        }
+#pragma unroll
+        for (int x = 0; x < 16; ++x) {
+            const int rb = x >> 2, jb = x & 3;
+            if constexpr (FIRST && L2)
+                acc[rb][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[rb], b0[jb], cinit[rb], 0, 0, 0);
+            else if constexpr (FIRST)
+                acc[rb][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[rb], b0[jb], f32x16{0.f}, 0, 0, 0);
+            else
+                acc[rb][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[rb], b0[jb], acc[rb][jb], 0, 0, 0);
+            if (x < 4)
+                a1[x] = frag(st, rowA + x * 32 * 64 + offa1);
+            else if (x < 8)
+                b1[x - 4] = frag(st, rowB + (x - 4) * 32 * 64 + offa1);
+            else
+                issue_piece(x - 8);
+            __builtin_amdgcn_sched_barrier(0);
+        }
+    };
+
+    // one stage: k-step-0 phase (FIRST: the item's first stage, C = 0 / the
+    // L2 norms), the issue cursor, the barrier, k-step-1 phase
+    auto do_stage = [&](auto first_tag) __attribute__((always_inline)) {
+        const unsigned char *st = lds + cbuf * kP4Stage;
+        const int nbuf_next = cbuf + 1 == NBUF ? 0 : cbuf + 1;
+        k0_phase(st, first_tag);
+        if (L2 && si == 0 && live) issue_piece(8);
+        issue_advance();
+        // own pieces of stage gc + 1 landed (younger stages may stay in
+        // flight); this stage's fragment reads retired (the next phase
+        // re-fills its buffer); then the barrier: stage gc + 1 is complete
+        // for every wave
+        const bool has_next = gc + 1 < issued;
+        p4_wait_vm<NPW>(has_next ? issued - gc - 2 : 0);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        p4_barrier();
+        // k-step-1 phase: 16 MFMAs on (a1, b1); between them the k-step-0
+        // fragments of stage gc + 1
+        const unsigned char *sn = lds + nbuf_next * kP4Stage;
+#pragma unroll
+        for (int x = 0; x < 16; ++x) {
+            const int rb = x >> 2, jb = x & 3;
+            acc[rb][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[rb], b1[jb], acc[rb][jb], 0, 0, 0);
+            if (has_next) {
+                if (x < 4)
+                    a0[x] = frag(sn, rowA + x * 32 * 64 + offa0);
+                else if (x < 8)
+                    b0[x - 4] = frag(sn, rowB + (x - 4) * 32 * 64 + offa0);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+        }
+        ++gc;
+        cbuf = nbuf_next;
+    };
+
+    // items: the first stage defines the accumulators (no phi with the last
+    // item's: they stay in place), the other stages accumulate
+    while (true) {
+        do_stage(std::integral_constant<bool, true>{});
+        for (int s = 1; s < nst; ++s) do_stage(std::integral_constant<bool, false>{});
+        // item epilogue
+        if constexpr ((DIAG & 16) != 0) {
+            float sum = 0.f;
+#pragma unroll
+            for (int rb = 0; rb < 4; ++rb)
+#pragma unroll
+                for (int jb = 0; jb < 4; ++jb)
+#pragma unroll
+                    for (int r = 0; r < 16; ++r) sum += acc[rb][jb][r];
+            if (sum == -1.2345e-30f) qcnt += 1;
+        } else {
+            const int crn = cr1 - cr0;  // rows of the item (<= 256)
+            // per 32 x 32 block: the maximum of the lane's 16 values (one
+            // v_max3 per two values; fmaxf would add a canonicalising max per
+            // value) against its query's threshold; a block with any lane over
+            // it walks its 16 values (constant accumulator indices: the
+            // accumulators stay in registers; the walk is cold code)
+            auto epi_block = [&](auto RB, auto JB) __attribute__((always_inline)) {
+                constexpr int rb = decltype(RB)::value, jb = decltype(JB)::value;
+                __builtin_amdgcn_sched_barrier(0);  // (one block's values at a time in VGPRs)
+                const int j = q0 + wq * 128 + jb * 32 + l32;
+                float mx = p4_max3(acc[rb][jb][0], acc[rb][jb][1], acc[rb][jb][2]);
+#pragma unroll
+                for (int r = 3; r < 15; r += 2) mx = p4_max3(mx, acc[rb][jb][r], acc[rb][jb][r + 1]);
+                mx = p4_max3(mx, acc[rb][jb][15], acc[rb][jb][15]);
+                // (a wave-uniform branch: the queue count is wave state)
+                if (__ballot(mx >= thr[jb]) == 0) return;
+#pragma unroll
+                for (int r = 0; r < 16; ++r) {
+                    const float x = acc[rb][jb][r];
+                    float raw = x;
+                    bool pass = x >= thr[jb];  // (padding queries: thr = +inf)
+                    if constexpr (L2) {
+                        raw = qnl[jb] - 2.0f * x;
+                        pass = pass && raw <= tl[jb];
+                    }
+                    uint64_t m = __ballot(pass);
+                    if (m == 0) continue;
+                    // the value's row, formed only here (hoisted, the 256 row
+                    // offsets of a lane would be spilled across the loop)
+                    int rbase_l = wr * 128 + 4 * h;
+                    asm volatile("" : "+v"(rbase_l));
+                    const int rl = rbase_l + rb * 32 + (r & 3) + 8 * (r >> 2);
+                    pass = pass && rl < crn;
+                    m = __ballot(pass);
+                    if (m == 0) continue;
+                    const int pre =
+                        __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+                    if (pass) {
+                        const uint32_t row = (uint32_t)(cr0 + rl);
+                        const int slot_ = qcnt + pre;
+                        if (slot_ < qcap)
+                            wq_base[slot_] = u32x4{__builtin_bit_cast(unsigned, raw), row, (unsigned)j, 0u};
+                        else  // queue full: mark the query's list overflowed (count > cap,
+                              // kept by every refine) -> the search re-runs on the exact path
+                            atomicMax(&p.cand_count[j], p.cand_cap + 1);
+                    }
+                    qcnt += __popcll(m);
+                }
+            };
+            p4_for<4>([&](auto JB) __attribute__((always_inline)) {
+                p4_for<4>([&](auto RB) __attribute__((always_inline)) { epi_block(RB, JB); });
+            });
+        }
+        ++items_done;
+        int cord;
+        ti_c = next_item(ti_c + tstride, cr0, cr1, cord);
+        if (ti_c < 0) break;
+    }
+    // flush this wave's queue to the per-query candidate lists
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int nqueue = qcnt < qcap ? qcnt : qcap;
+    for (int e = lane; e < nqueue; e += 64) {
+        const u32x4 en = __builtin_nontemporal_load(wq_base + e);  // (bypasses L1)
+        const uint32_t row = en[1];
+        emit_approx<METRIC, false>(p, (int)en[2], row, row, row_valid(p, row), __builtin_bit_cast(float, en[0]));
+    }
+}
+
+// queue entries per wave (16 B each): 2048 x 16 B x 4 waves x 256 CUs = 32 MiB
+constexpr int kP4QueueCap = 2048;
+
+size_t p4_queue_bytes() {
+    static int cus = 0;
+    if (!cus) {
+        int dev = 0;
+        MQVS_HIP(hipGetDevice(&dev));
+        MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    }
+    return (size_t)cus * 4 * kP4QueueCap * sizeof(u32x4);
+}
+
+// true when the launch was taken (batch APPEND, contiguous rows, identity
+// chunk ordinals, the queue workspace present)
+template <int METRIC>
+static bool launch_p4_t(ScanParams p, hipStream_t s) {
+    if (!p.p4_queue || p.row_list || p.chunk_ord || p.tiles < 1 || p.tile_rows != kP4Tile) return false;
+    p.num_qblocks = (p.nq + kP4Tile - 1) / kP4Tile;
+    int dev = 0, cus = 0;
+    MQVS_HIP(hipGetDevice(&dev));
+    MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int per_xcd = cus / 8;
+    if (p.num_qblocks > per_xcd) return false;
+    if (p.dpad % kP4HiK) return false;
+    // row tiles start on 16-row plane blocks; query plane offsets fit 32 bits
+    if (p.row_begin % 16 || (p.tiles_per_chunk > 0 && p.chunk_rows % 16)) return false;
+    // 32-bit item arithmetic (rows, tiles, chunk starts)
+    if (p.row_begin < 0 || p.row_end + p.chunk_rows + p.tile_rows > 0x7FFFFFFF || p.tiles > 0x3FFFFFFF ||
+        p.chunk_rows < 1)
+        return false;
+    if ((double)p.maxv * (double)p.q_vpad * (double)p.dpad * 2.0 >= 4294967296.0) return false;
+    if constexpr (METRIC == MQVS_METRIC_L2) {
+        // the norm piece is a 4-B-per-lane DMA: any row alignment works
+        if (!p.row_norms) return false;
+    }
+    const int slots = per_xcd / p.num_qblocks * p.num_qblocks;
+    auto *q = reinterpret_cast<u32x4 *>(p.p4_queue);
+    const dim3 grid((unsigned)(8 * per_xcd));
+    if constexpr (kDebugTuning) {
+        // measurement builds: ring depth and decomposition variants
+        const int nbuf = tune_int("MQVS_P4_NBUF", 4);
+        const int diag = tune_int("MQVS_P4_DIAG", 0);
+#define MQVS_P4(NB_, DG_) hipLaunchKernelGGL((k_scan_p4<METRIC, NB_, DG_>), grid, dim3(256), 0, s, p, slots, q, kP4QueueCap)
+        if (diag == 4) MQVS_P4(4, 4);
+        else if (diag == 8) MQVS_P4(4, 8);
+        else if (diag == 12) MQVS_P4(4, 12);
+        else if (diag == 16) MQVS_P4(4, 16);
+        else if (diag == 28) MQVS_P4(4, 28);
+        else if (nbuf == 5 && !(METRIC == MQVS_METRIC_L2)) {
+            if constexpr (METRIC != MQVS_METRIC_L2) MQVS_P4(5, 0);
+        }
+        else if (nbuf == 3) MQVS_P4(3, 0);
+        else MQVS_P4(4, 0);
+#undef MQVS_P4
+    } else {
+        hipLaunchKernelGGL((k_scan_p4<METRIC, 4, 0>), grid, dim3(256), 0, s, p, slots, q, kP4QueueCap);
+    }
+    return true;
+}
+
+bool launch_scan_p4(const ScanParams &p, int metric, hipStream_t s) {
+    switch (metric) {
+        case MQVS_METRIC_L2: return launch_p4_t<MQVS_METRIC_L2>(p, s);
+        case MQVS_METRIC_IP: return launch_p4_t<MQVS_METRIC_IP>(p, s);
+        case MQVS_METRIC_COSINE: return launch_p4_t<MQVS_METRIC_COSINE>(p, s);
+        default: return launch_p4_t<kMetricIpRaw>(p, s);
+    }
+}
+
+}  // namespace mqvs

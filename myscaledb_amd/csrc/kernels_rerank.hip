@@ -353,7 +353,7 @@ void launch_exact_rerank(const ScanParams &p, int metric, const uint32_t *surv, 
     const int chunks = (cap + SEL_THREADS - 1) / SEL_THREADS;
     const int items = p.nq * chunks;
     const int grid = std::max(1, std::min(items, 4096));
-    const bool direct = p.nq < kBlasThreshold;
+    const bool direct = !blas_formula(p);
 #define MQVS_ER(M)                                                                                                \
     do {                                                                                                          \
         if (direct)                                                                                               \
@@ -393,7 +393,7 @@ static void rerank_ids_t(const ScanParams &p, const int64_t *cand, int ncand, in
 
 void launch_rerank_ids(const ScanParams &p, int metric, const int64_t *cand, int ncand, int k,
                        int64_t id_offset, int64_t *out_ids, float *out_dist, uint4 *scratch, hipStream_t s) {
-    const bool direct = p.nq < kBlasThreshold;
+    const bool direct = !blas_formula(p);
 #define MQVS_RR(M)                                                                           \
     direct ? rerank_ids_t<M, true>(p, cand, ncand, k, id_offset, out_ids, out_dist, scratch, s) \
            : rerank_ids_t<M, false>(p, cand, ncand, k, id_offset, out_ids, out_dist, scratch, s)

@@ -31,6 +31,9 @@ static thread_local mqvs_search_stats g_stats{};
 // threads never switches a search's path midway (per-call flags override them).
 static std::atomic<int> g_timing{0};
 static std::atomic<int> g_prefilter{2};  // planes built by new segments (mqvs_set_prefilter)
+static std::atomic<size_t> g_scratch_budget{(size_t)1 << 30};  // bytes per scratch buffer of one call
+
+size_t scratch_budget() { return g_scratch_budget.load(std::memory_order_relaxed); }
 
 void set_error(const std::string &msg) { g_error = msg; }
 
@@ -42,7 +45,7 @@ struct Workspace {
     hipEvent_t seg_ev[kSegEv] = {};  // per main-scan segment: start, end
     DevBuf queries, qvars, qnorms, qmu, qlam, status, filter, exists, ord, probe, tau, count, cand,
         overflow, out_ids, out_dist, misc, qhi, bq, thr, cand2, count2, gcount, goff, glist, large, sticky, surv,
-        recs, flags;
+        recs, flags, p4q;
     int *host_flags = nullptr;  // pinned
     void init() {
         if (stream) return;
@@ -55,7 +58,7 @@ struct Workspace {
         DevBuf *all[] = {&queries, &qvars, &qnorms, &qmu,  &qlam,   &status,  &filter,   &exists, &ord,
                          &probe,   &tau,   &count,  &cand, &overflow, &out_ids, &out_dist, &misc,
                          &qhi, &bq, &thr, &cand2, &count2, &gcount, &goff, &glist, &large, &sticky, &surv,
-                         &recs, &flags};
+                         &recs, &flags, &p4q};
         for (auto *b : all) b->release();
         if (host_flags) (void)hipHostFree(host_flags);
         host_flags = nullptr;
@@ -323,8 +326,9 @@ static int large_k_cap(int k) { return (int)std::min<int64_t>(kCandMax, (int64_t
 static int large_k_batch(int64_t n, int k) {
     const int64_t cap = large_k_cap(k);
     const int64_t probe = std::min<int64_t>(n, (int64_t)((double)k * (double)n / (double)(cap / 3)) + 1);
-    const int64_t by_cand = ((int64_t)1 << 27) / cap;                  // 1 GB per candidate buffer
-    const int64_t by_probe = ((int64_t)1 << 28) / std::max<int64_t>(probe, 1);  // 1 GB of probe values
+    const int64_t budget = (int64_t)scratch_budget();
+    const int64_t by_cand = budget / 8 / cap;                          // 8-B candidates
+    const int64_t by_probe = budget / 4 / std::max<int64_t>(probe, 1);  // fp32 probe values
     return (int)std::max<int64_t>(1, std::min(by_cand, by_probe));
 }
 
@@ -361,10 +365,14 @@ static SegTune seg_tune(int nq) {
     return v;
 }
 
+// formula_nq: the batch size that selects faiss's distance formula (0: nq).
+// Query sub-batches of one call (large k) keep the call's formula: faiss
+// decides it from the whole batch (BruteForceSearch.h:80-87, nx >= 20).
 static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, int metric,
                         const uint8_t *filter, const uint8_t *exists, int64_t *out_ids,
                         float *out_dist, uint32_t flags, hipStream_t user_stream,
-                        bool force_exact = false, int64_t ord_base = -1, int maxv_hint = 0) {
+                        bool force_exact = false, int64_t ord_base = -1, int maxv_hint = 0, int formula_nq = 0) {
+    const int fnq = formula_nq > 0 ? formula_nq : nq;
     if (!seg) fail(MQVS_ERR_BAD_ARGUMENTS, "null segment");
     if (seg->binary) fail(MQVS_ERR_LOGICAL, "binary (FixedString) segment: search it with mqvs_search_binary");
     if (nq < 0 || k < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "nq and k must be non-negative");
@@ -388,7 +396,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
                 const int m = std::min(qb, nq - q0);
                 search_impl(seg, queries + (size_t)q0 * seg->d, m, k, metric, filter, exists,
                             out_ids + (size_t)q0 * k, out_dist + (size_t)q0 * k, flags, user_stream, force_exact,
-                            ord_base, maxv_hint);
+                            ord_base, maxv_hint, fnq);
             }
             return;
         }
@@ -461,7 +469,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     // keeps whole tiles of scattered rows in flight and gathers efficiently up
     // to ~60% selectivity, while the VALU kernel's 128-B row slices only pay
     // below ~30% (tools/sweep.py --sels, profiles/r01)
-    const bool mfma = nq >= kBlasThreshold;
+    const bool mfma = fnq >= kBlasThreshold;
     const bool bf16_ok = seg->approx_ok && !force_exact && batch_mode == 0;
     // (split 2 streams half the bytes of the fp32 rows, so it serves every
     // batch size; the older splits start at kBf16MinNq)
@@ -565,6 +573,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     p.nonempty = seg->nonempty_bits;
     p.row_list = row_list;
     p.num_qblocks = (nq + kMfmaQ - 1) / kMfmaQ;
+    p.blas_nq = fnq;
     uint32_t *tau = (uint32_t *)ws.tau.get(sizeof(uint32_t) * nq);
     int *count = fl + 8;  // zeroed with the status words
     Cand *cand = (Cand *)ws.cand.get(sizeof(Cand) * (size_t)nq * cap);
@@ -587,6 +596,8 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         p.dpad = seg->dpad;
         p.thr = (const float *)ws.thr.get(sizeof(float) * nq);
         p.split = seg->split;
+        // batch scans (kernels_p4.hip): per-wave candidate queues
+        if (seg->split == kHiSplit && nq > 128) p.p4_queue = ws.p4q.get(p4_queue_bytes());
         if (seg->split == kHiSplit) {
             // [hi: maxv x vpad x dpad x 2 B][records: nvec x kMxRec floats]
             const int64_t vpad = round_up(nq, 16);
@@ -634,6 +645,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     const Range pr = make_range(0, P, tile_rows, seg->granule, aligned);
     const Range mr = make_range(P, scan_n, tile_rows, seg->granule, aligned);
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[5], s));
+    (void)take_batch_kernel_flag();
     run_scan(p, pr, kind, metric, true, s);
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[1], s));
     if (kind == kScanBf16)
@@ -694,6 +706,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
 
     st.path = kind;
     st.prefilter = kind == kScanBf16 ? seg->split : 0;
+    st.batch_kernel = take_batch_kernel_flag();
     st.probe_rows = P;
     st.main_rows = scan_n - P;
     st.rows_scanned = scan_n;
@@ -728,7 +741,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
             const int want = (int)std::min<int64_t>(ords, kMaxVariantsCap);
             if (maxv < want) {
                 search_impl(seg, queries, nq, k, metric, filter, exists, out_ids, out_dist, flags, user_stream,
-                            force_exact, ord_base, want);
+                            force_exact, ord_base, want, fnq);
                 return;
             }
             fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not repeat within " + std::to_string(maxv) +
@@ -737,7 +750,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         if (kind == kScanBf16 && ws.host_flags[0]) {
             // the bf16 bound left too many candidates: exact fp32 path
             search_impl(seg, queries, nq, k, metric, filter, exists, out_ids, out_dist, flags,
-                        user_stream, true, ord_base, maxv);
+                        user_stream, true, ord_base, maxv, fnq);
             g_stats.rescans += 1;
             return;
         }
@@ -804,7 +817,8 @@ void search_segment(mqvs_segment *seg, const float *queries, int nq, int k, int 
 // candidate list of a query is expected to hold distinct rows.
 static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const int64_t *cand,
                         int ncand, int k, int metric, const uint8_t *exists, int64_t *out_ids,
-                        float *out_dist, uint32_t flags, hipStream_t user_stream) {
+                        float *out_dist, uint32_t flags, hipStream_t user_stream, int formula_nq = 0) {
+    const int fnq = formula_nq > 0 ? formula_nq : nq;  // (see search_impl)
     if (!seg) fail(MQVS_ERR_BAD_ARGUMENTS, "null segment");
     if (seg->binary) fail(MQVS_ERR_NOT_IMPLEMENTED, "computeTopDistanceSubset is for Float32 vectors");
     if (nq < 0 || k < 0 || ncand < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "nq, k and ncand must be non-negative");
@@ -824,12 +838,12 @@ static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const i
     // through 2 ncand records of global scratch, in query sub-batches of <= 1 GB
     const bool large = ncand > kSortCap;
     if (large) {
-        const int qb = (int)std::max<int64_t>(1, ((int64_t)1 << 26) / (2 * (int64_t)ncand));
+        const int qb = (int)std::max<int64_t>(1, (int64_t)scratch_budget() / 16 / (2 * (int64_t)ncand));
         if (nq > qb) {
             for (int q0 = 0; q0 < nq; q0 += qb) {
                 const int m = std::min(qb, nq - q0);
                 rerank_impl(seg, queries + (size_t)q0 * seg->d, m, cand + (size_t)q0 * ncand, ncand, k, metric,
-                            exists, out_ids + (size_t)q0 * k, out_dist + (size_t)q0 * k, flags, user_stream);
+                            exists, out_ids + (size_t)q0 * k, out_dist + (size_t)q0 * k, flags, user_stream, fnq);
             }
             return;
         }
@@ -862,7 +876,7 @@ static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const i
         dids = (int64_t *)ws.out_ids.get(sizeof(int64_t) * (size_t)nq * k);
         ddist = (float *)ws.out_dist.get(sizeof(float) * (size_t)nq * k);
     }
-    const bool blas = nq >= kBlasThreshold;
+    const bool blas = fnq >= kBlasThreshold;
     const int64_t ords = seg->row_offset / seg->granule + (seg->n + seg->granule - 1) / seg->granule;
     float *qvars = nullptr, *qnorms = nullptr;
     int *qmu = nullptr, *qlam = nullptr, *status = nullptr;
@@ -880,6 +894,7 @@ static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const i
     p.qmu = qmu;
     p.qlam = qlam;
     p.maxv = maxv;
+    p.blas_nq = fnq;
     p.chunk_rows = seg->granule;
     p.chunk_ord = seg->chunk_ord;
     p.ord_base = (int)(seg->row_offset / seg->granule);
@@ -1687,8 +1702,13 @@ int mqvs_set_prefilter(int split) {
     return MQVS_OK;
 }
 
+size_t mqvs_set_scratch_budget(size_t bytes) {
+    if (bytes == 0) return g_scratch_budget.load();
+    return g_scratch_budget.exchange(std::max<size_t>(bytes, (size_t)1 << 20));
+}
+
 int mqvs_set_gather_mode(int mode) {
-    if (mode < 0 || mode > 3) return MQVS_ERR_BAD_ARGUMENTS;
+    if (mode < 0 || mode > 2) return MQVS_ERR_BAD_ARGUMENTS;
     g_gather_mode.store(mode);
     return MQVS_OK;
 }

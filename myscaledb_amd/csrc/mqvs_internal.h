@@ -183,7 +183,15 @@ struct ScanParams {
     int nbits;                // d: Hamming distances == nbits are never returned
     int tau_strict;           // APPEND takes key < tau (segments after the probe) instead of <=
     unsigned long long *dbg;  // diagnostic builds only (stage timing stamps)
+    void *p4_queue;           // batch scan (kernels_p4.hip): per-wave candidate queues, p4_queue_bytes()
+    int blas_nq;              // batch size that selects faiss's distance formula (0: nq); a query
+                              // sub-batch of a larger call keeps the call's formula
 };
+
+// faiss's formula branch (distance_compute_blas_threshold) for this scan's call
+__host__ __device__ inline bool blas_formula(const ScanParams &p) {
+    return (p.blas_nq > 0 ? p.blas_nq : p.nq) >= kBlasThreshold;
+}
 
 // Row at scan position pos (-1 = padding entry of the gather list).
 __device__ inline int64_t row_at(const ScanParams &p, int64_t pos) {
@@ -359,6 +367,11 @@ void launch_scan_mx(const ScanParams &p, int metric, bool probe, hipStream_t s);
 void launch_to_hi(const float *src, int64_t rows, int d, int64_t src_stride, int64_t dpad, int64_t vgroup,
                   int64_t vpad, uint16_t *hi, float *rec, float *maxrec, hipStream_t s);
 void launch_scan_hi(const ScanParams &p, int metric, bool probe, hipStream_t s);
+// batch APPEND scan at one wave per SIMD (kernels_p4.hip): false when the
+// scan's shape is not served (gather lists, chunk-ordinal tables, no queue)
+bool launch_scan_p4(const ScanParams &p, int metric, hipStream_t s);
+size_t p4_queue_bytes();  // p4_queue workspace for the current device
+int take_batch_kernel_flag();  // 1 when a main scan since the last call ran kernels_p4 (then cleared)
 void launch_probe_select_approx(const float *probe, int64_t P, int64_t ld, int nq, int k,
                                 int metric, const float *bq, float *thr, int *cand_count,
                                 Cand *cand, int cand_cap, const int32_t *row_list, hipStream_t s);
@@ -496,6 +509,7 @@ static int guarded(F &&f) {
 
 // mqvs.hip services used by the index path
 hipStream_t thread_stream(int device);
+size_t scratch_budget();  // bytes per scratch buffer of one call (mqvs_set_scratch_budget)
 // FLAT search of a segment (MergeTreeVSManager::vectorScanWithoutIndex);
 // metric may be kMetricIpRaw (faiss knn_inner_product contract)
 void search_internal(mqvs_segment *seg, const float *queries, int nq, int k, int metric,

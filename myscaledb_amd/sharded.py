@@ -179,26 +179,37 @@ class RcclComm:
             uid = bytes(t.cpu().tolist())
         return cls(world, rank, uid)
 
-    def sharded_search(self, segment, queries, k, filter_bitmap=None, row_exists=None, out=None, metric=None):
+    def sharded_search(self, segment, queries, k, filter_bitmap=None, row_exists=None, out=None, metric=None,
+                       stream=None):
         """mqvs_sharded_search: this rank's shard (`segment`, row_offset = its
         first row) searched, the per-rank top-k all-gathered over RCCL and
         merged on the device; every rank returns the merged [nq, k] result.
-        Bitmaps are the shard's own (its n bits)."""
-        import ctypes
+        Bitmaps are the shard's own (its n bits).  Device tensors run on
+        `stream` (default: torch's current stream, so inputs written by
+        earlier torch kernels are ready)."""
         from .vector_scan import _host_f32, _host_u8, _is_torch, _ptr, metric_id
         from ._lib import F_DEVICE_PTRS
         m = segment.metric if metric is None else metric_id(metric)
         if _is_torch(queries):
             import torch
+            assert queries.is_cuda and queries.is_contiguous() and queries.dtype == torch.float32, \
+                "queries: a contiguous float32 CUDA tensor"
+            for b in (filter_bitmap, row_exists):
+                assert b is None or (b.is_cuda and b.is_contiguous() and b.dtype == torch.uint8), \
+                    "bitmaps: contiguous uint8 CUDA tensors"
             nq = queries.shape[0]
             if out is None:
                 ids = torch.empty((nq, k), dtype=torch.int64, device=queries.device)
                 dist = torch.empty((nq, k), dtype=torch.float32, device=queries.device)
             else:
                 ids, dist = out
+                assert ids.is_cuda and ids.is_contiguous() and ids.dtype == torch.int64
+                assert dist.is_cuda and dist.is_contiguous() and dist.dtype == torch.float32
+            if stream is None:
+                stream = torch.cuda.current_stream(queries.device).cuda_stream
             self._lib.check(self._lib.lib.mqvs_sharded_search(
                 self._h, segment._h, _ptr(queries), nq, k, m, _ptr(filter_bitmap), _ptr(row_exists), _ptr(ids),
-                _ptr(dist), F_DEVICE_PTRS, None))
+                _ptr(dist), F_DEVICE_PTRS, stream))
             return ids, dist
         q = _host_f32(queries)
         if q.ndim == 1:
@@ -208,7 +219,7 @@ class RcclComm:
         dist = np.empty((nq, k), np.float32)
         self._lib.check(self._lib.lib.mqvs_sharded_search(
             self._h, segment._h, _ptr(q), nq, k, m, _ptr(_host_u8(filter_bitmap)), _ptr(_host_u8(row_exists)),
-            _ptr(ids), _ptr(dist), 0, None))
+            _ptr(ids), _ptr(dist), 0, stream))
         return ids, dist
 
     def free(self):
@@ -221,3 +232,28 @@ class RcclComm:
             self.free()
         except Exception:  # noqa: BLE001
             pass
+
+
+class LoopbackComm(RcclComm):
+    """One rank of a loopback communicator group (mqvs_comm_init_loopback):
+    N virtual ranks in this process on the current GPU, the exchanges done as
+    device copies.  Each rank's sharded_search must run on its own thread
+    (the ranks meet at host barriers); the search code is the RCCL one."""
+
+    def __init__(self, handle):  # noqa: D401  (built by group())
+        from . import _lib
+        self._lib = _lib
+        self._h = handle
+
+    @classmethod
+    def group(cls, nranks: int):
+        import ctypes
+        from . import _lib
+        hs = (ctypes.c_void_p * nranks)()
+        _lib.check(_lib.lib.mqvs_comm_init_loopback(nranks, hs))
+        ranks = []
+        for r in range(nranks):
+            c = cls(ctypes.c_void_p(hs[r]))
+            c.nranks, c.rank = nranks, r
+            ranks.append(c)
+        return ranks

@@ -406,6 +406,13 @@ def set_gather_mode(mode: int):
     check(lib.mqvs_set_gather_mode(int(mode)))
 
 
+def set_scratch_budget(nbytes: int) -> int:
+    """Device scratch per buffer of one call (large-k sorts, candidate lists);
+    larger calls run in query sub-batches with the same bits
+    (mqvs_set_scratch_budget).  Returns the previous value; 0 only reads it."""
+    return int(lib.mqvs_set_scratch_budget(int(nbytes)))
+
+
 def set_prefilter(split: int):
     """Pre-filter planes of segments created after the call: 2 = bf16 hi
     plane only (default), 6 = bf16 hi + block-scaled fp6 cross plane, 3 = bf16

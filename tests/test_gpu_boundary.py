@@ -264,3 +264,35 @@ def test_cosine_long_normalisation_chains(mq, nq):
         _eq(ri, rd, io, do, f"cosine long chains nq {nq} rerank")
     finally:
         seg.free()
+
+
+@pytest.mark.parametrize("metric", ["L2", "IP", "Cosine"])
+def test_sub_batches_keep_the_calls_formula(mq, metric):
+    """A call split into query sub-batches (large k under a small scratch
+    budget) keeps the distance formula of the WHOLE call: faiss picks the
+    BLAS branch from nx >= 20 (BruteForceSearch.h:80-87), so a 25-query call
+    whose sub-batches hold 6, 6, 6, 6 and 1 queries still ranks with the BLAS
+    form -- the oracle's bits.  Same for computeTopDistanceSubset (31 queries
+    in sub-batches of 21 and 10)."""
+    from myscaledb_amd.vector_scan import set_scratch_budget
+    seed = zlib.crc32(("subbatch_" + metric).encode())
+    n, d, nq, k, gran = 50000, 24, 25, 5000, 4096
+    rows = O.generate(seed, 1, 0, n, d)
+    q = O.generate(seed + 1, 1, 0, nq, d)
+    io, do = O.vector_scan(rows, q, k, O.METRICS[metric], gran, fast=True)
+    rows2 = O.generate(seed + 2, 1, 0, 6000, d)
+    q2 = O.generate(seed + 3, 1, 0, 31, d)
+    io2, do2 = O.vector_scan(rows2, q2, 100, O.METRICS[metric], gran, fast=True)
+    prev = set_scratch_budget(4 << 20)
+    seg = mq.VectorScanSegment.from_rows(rows, metric=metric, granule=gran)
+    seg2 = mq.VectorScanSegment.from_rows(rows2, metric=metric, granule=gran)
+    try:
+        ig, dg = seg.search(q, k)
+        _eq(ig, dg, io, do, f"{metric} k={k} nq={nq} in sub-batches")
+        cand = np.tile(np.arange(6000, dtype=np.int64)[None, :], (31, 1))
+        ri, rd = seg2.rerank(q2, cand, 100)
+        _eq(ri, rd, io2, do2, f"{metric} rerank 31 queries in sub-batches")
+    finally:
+        set_scratch_budget(prev)
+        seg.free()
+        seg2.free()
