@@ -457,7 +457,7 @@ static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, c
     // nprobe 512 = 51 queries per list: 14.4 -> 12.3 ms; at 13 per list
     // they are slower, tools/index_qg_ab.py).
     p.qg = (!dense && E >= 40 * nlist) ? 64 : (dense || E >= 24 * nlist) ? 32 : 16;
-    if (const char *e = std::getenv("MQVS_IVF_QG")) {  // A/B knob (tools/ab_split.py style)
+    if (const char *e = tune_env("MQVS_IVF_QG")) {  // A/B knob (tools/ab_split.py style)
         const int v = std::atoi(e);
         if (!dense && (v == 16 || v == 32 || v == 64)) p.qg = v;
     }

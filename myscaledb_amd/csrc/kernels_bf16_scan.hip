@@ -430,7 +430,7 @@ static void launch_shape(ScanParams p, hipStream_t s) {
 // Tuning override (tools/tune_bf16.py, cosine APPEND split-3 launches only):
 // MQVS_BF16_TUNE="WQ,QB,VAR" picks the workgroup shape and schedule variant.
 static bool tune_override(int &wq, int &qb, int &var) {
-    const char *e = std::getenv("MQVS_BF16_TUNE");
+    const char *e = tune_env("MQVS_BF16_TUNE");
     if (!e || !*e) return false;
     return std::sscanf(e, "%d,%d,%d", &wq, &qb, &var) == 3;
 }

@@ -275,7 +275,7 @@ __global__ __launch_bounds__(256) void k_scan_binary_co(ScanParams p) {
 
 static int64_t bin_grid_cap() {
     static const int64_t cap = [] {
-        const char *e = std::getenv("MQVS_BIN_GRID");  // tuning knob (tools/binary_sweep.py)
+        const char *e = tune_env("MQVS_BIN_GRID");  // tuning knob (tools/binary_sweep.py)
         return e ? std::max<int64_t>(64, std::atoll(e)) : (int64_t)4096;
     }();
     return cap;
@@ -284,7 +284,7 @@ static int64_t bin_grid_cap() {
 template <int METRIC, bool PROBE>
 static void scan_binary_t(const ScanParams &p, hipStream_t s) {
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>(p.tiles, bin_grid_cap()));
-    if (p.nq <= 8 && !std::getenv("MQVS_BIN_NOCO")) {
+    if (p.nq <= 8 && !tune_env("MQVS_BIN_NOCO")) {
         switch (p.code_words / 4) {
             case 1: hipLaunchKernelGGL((k_scan_binary_co<METRIC, PROBE, 1>), dim3(grid), dim3(256), 0, s, p); return;
             case 2: hipLaunchKernelGGL((k_scan_binary_co<METRIC, PROBE, 2>), dim3(grid), dim3(256), 0, s, p); return;

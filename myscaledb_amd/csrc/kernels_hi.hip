@@ -759,7 +759,7 @@ static bool launch_hi_pp(ScanParams p, hipStream_t s) {
     const int per_xcd = cus / 8;
     if (p.num_qblocks > per_xcd || p.tiles < 1) return false;
     const int slots = per_xcd / p.num_qblocks * p.num_qblocks;
-    const char *dg = std::getenv("MQVS_HI_PPDIAG");
+    const char *dg = tune_env("MQVS_HI_PPDIAG");
     const int diag = dg ? std::atoi(dg) : 0;
     static std::atomic<unsigned> launches{0};
     const unsigned epoch = (launches.fetch_add(1, std::memory_order_relaxed) + 1) & 0xFFFFu;
@@ -768,13 +768,17 @@ static bool launch_hi_pp(ScanParams p, hipStream_t s) {
 #define MQVS_PP(DG_)                                                                                             \
     hipLaunchKernelGGL((k_scan_hi_pp<METRIC, 4, DG_>), dim3((unsigned)(8 * per_xcd)), dim3(512), 0, s, p, slots, \
                        epoch)
-    switch (diag) {
-        case 16: MQVS_PP(16); break;
-        case 32: MQVS_PP(32); break;
-        case 64: MQVS_PP(64); break;
-        case 256: MQVS_PP(256); break;
-        case 1024: MQVS_PP(1024); break;
-        default: MQVS_PP(0); break;
+    if constexpr (kDebugTuning) {  // (diagnostic variants: measurement builds only)
+        switch (diag) {
+            case 16: MQVS_PP(16); break;
+            case 32: MQVS_PP(32); break;
+            case 64: MQVS_PP(64); break;
+            case 256: MQVS_PP(256); break;
+            case 1024: MQVS_PP(1024); break;
+            default: MQVS_PP(0); break;
+        }
+    } else {
+        MQVS_PP(0);
     }
 #undef MQVS_PP
     return true;
@@ -880,7 +884,7 @@ static void launch_hi_reg(ScanParams p, hipStream_t s) {
     // 2.55 -> 2.28 ms at nq 1 (6.0 -> 6.7 TB/s), 2.80 -> 2.55 ms at nq 16,
     // bit-identical (profiles/r02/smallnq/nt_ab.jsonl).  A/B switch
     // (tools/ab_split.py): MQVS_HI_NT=0 = plain loads
-    const char *nte = std::getenv("MQVS_HI_NT");
+    const char *nte = tune_env("MQVS_HI_NT");
     const bool nt = !(nte && nte[0] == '0');
     switch (p.dpad / HI_K) {
 #define MQVS_HI_REG(N_)                                                                                        \
@@ -916,7 +920,7 @@ static void launch_hi_shape(ScanParams p, hipStream_t s) {
 // Tuning override (tools/ab_split.py --tunes): MQVS_HI_TUNE="WQ,QB,NBUF[,PP[,DIAG]]"
 template <int METRIC, bool PROBE>
 static bool launch_hi_tuned(const ScanParams &p, hipStream_t s) {
-    const char *e = std::getenv("MQVS_HI_TUNE");
+    const char *e = tune_env("MQVS_HI_TUNE");
     int wq, qb, nbuf, pp = 0, diag = 0;
     if (!e || !*e || std::sscanf(e, "%d,%d,%d,%d,%d", &wq, &qb, &nbuf, &pp, &diag) < 3) return false;
     switch ((((wq * 10 + qb) * 10 + nbuf) * 100 + pp) * 100 + diag) {
@@ -960,7 +964,7 @@ static void launch_hi_t(const ScanParams &p, hipStream_t s) {
         if constexpr (METRIC != MQVS_METRIC_L2)
             if (p.nq > 128 && pp == 1 && !p.row_list && !p.chunk_ord && launch_hi_pp<METRIC>(p, s)) return;
     }
-    const char *reg = std::getenv("MQVS_HI_REG");  // A/B switch (tools/ab_split.py): 0 = LDS kernel only
+    const char *reg = tune_env("MQVS_HI_REG");  // A/B switch (tools/ab_split.py): 0 = LDS kernel only
     const bool use_reg = !(reg && reg[0] == '0');
     if (use_reg && p.nq <= 32 && p.dpad <= kHiRegMaxDpad) {
         if (p.nq <= 16)

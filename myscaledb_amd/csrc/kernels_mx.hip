@@ -479,7 +479,7 @@ static void launch_mx_shape(ScanParams p, hipStream_t s) {
     int64_t grid = (L + 7) / 8 * 8;
     // XCD grouping (experimental, MQVS_MX_XCD=g with g in {2, 4, 8})
     p.xcd_mode = 0;
-    if (const char *e = std::getenv("MQVS_MX_XCD")) {
+    if (const char *e = tune_env("MQVS_MX_XCD")) {
         const int g = std::atoi(e);
         if ((g == 2 || g == 4 || g == 8) && p.num_qblocks >= g) {
             p.xcd_mode = g;
@@ -494,7 +494,7 @@ static void launch_mx_shape(ScanParams p, hipStream_t s) {
 // Tuning override (tools/tune_bf16.py): MQVS_MX_TUNE="WQ,QB,VAR"
 template <int METRIC, bool PROBE>
 static bool launch_mx_tuned(const ScanParams &p, hipStream_t s) {
-    const char *e = std::getenv("MQVS_MX_TUNE");
+    const char *e = tune_env("MQVS_MX_TUNE");
     int wq, qb, var;
     if (!e || !*e || std::sscanf(e, "%d,%d,%d", &wq, &qb, &var) != 3) return false;
     switch ((wq * 10 + qb) * 1000 + var) {

@@ -44,6 +44,7 @@
 // Items: as k_scan_hi_pp -- XCD x = blockIdx % 8 takes tiles t = x (mod 8); its
 // workgroups form groups of nqb query blocks that stream the same row tiles,
 // so a tile's rows are shared through that XCD's L2.
+#include <atomic>
 #include <cstdint>
 #include <type_traits>
 #include <utility>
@@ -106,8 +107,25 @@ __device__ inline void p4_for(F &&f) {
 // passes a threshold, as in emit_approx)
 __device__ inline float p4_max3(float a, float b, float c) {
     float r;
-    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
+    asm volatile("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(a), "v"(b), "v"(c));
     return r;
+}
+// an accumulator value (in an AGPR) copied to a VGPR, in program order
+__device__ inline float p4_aread(float a) {
+    float r;
+    asm volatile("v_accvgpr_read_b32 %0, %1" : "=v"(r) : "a"(a));
+    return r;
+}
+// four of them in one ordered statement (the compiler pads every inline asm
+// with a hazard s_nop; one per four reads)
+__device__ inline f32x4 p4_aread4(float a, float b, float c, float d) {
+    float x, y, z, w;
+    asm volatile(
+        "v_accvgpr_read_b32 %0, %4\n\tv_accvgpr_read_b32 %1, %5\n\t"
+        "v_accvgpr_read_b32 %2, %6\n\tv_accvgpr_read_b32 %3, %7"
+        : "=v"(x), "=v"(y), "=v"(z), "=v"(w)
+        : "a"(a), "a"(b), "a"(c), "a"(d));
+    return f32x4{x, y, z, w};
 }
 
 __device__ inline void p4_barrier() {
@@ -117,8 +135,8 @@ __device__ inline void p4_barrier() {
 }
 
 // DIAG (measurement builds only; wrong results): 4 = query pieces not issued,
-// 8 = row pieces not issued, 16 = trivial epilogue (one compare of an
-// accumulator sum per item)
+// 8 = row pieces not issued, 16 = no threshold tests (the accumulators are
+// kept live by one read per block), 32 = threshold tests without walks
 template <int METRIC, int NBUF, int DIAG = 0>
 __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32x4 *queue, int qcap) {
     constexpr bool L2 = METRIC == MQVS_METRIC_L2;
@@ -127,13 +145,16 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
     constexpr int D = NBUF - 1;
     static_assert(D >= 1 && D <= 4, "ring depth");
     constexpr int NORM = L2 ? 2048 : 0;  // two item-parity copies of 256 row norms
+    constexpr int WSCR = 4 * 64 * 16 * 4;  // epilogue walk scratch: 16 values per lane and wave
     constexpr int NPW = 8 - ((DIAG & 8) ? 4 : 0) - ((DIAG & 4) ? 4 : 0);  // pieces per wave and stage
     // ONE __shared__ object (an LDS access to a second object after an
     // LDS-DMA makes the compiler wait for every DMA in flight)
-    __shared__ __attribute__((aligned(16))) unsigned char lds[NBUF * kP4Stage + NORM];
+    __shared__ __attribute__((aligned(16))) unsigned char lds[NBUF * kP4Stage + NORM + WSCR];
     unsigned char *norm_lds = lds + NBUF * kP4Stage;
 
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
+    // (the wave index through readfirstlane: known wave-uniform, so branches
+    // on it are scalar)
+    const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
     const int wr = w & 1, wq = w >> 1;
     const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
     const int nqb = p.num_qblocks;
@@ -144,15 +165,15 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
     const int tstride = 8 * ngroups;
     const int nst = (int)(p.dpad / kP4HiK);
     const int l32 = lane & 31, h = lane >> 5;
+    float *wscr = reinterpret_cast<float *>(lds + NBUF * kP4Stage + NORM) + w * 1024;
 
     // per-lane query constants: the four query rows of this wave's query
     // pieces (variant cycles), the four query columns of its accumulators
-    int qj[4], qmu[4], qlam[4];
+    int qmu[4], qlam[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
         int j = q0 + (w + 4 * i) * 16 + (lane >> 2);
         if (j >= p.nq) j = 0;
-        qj[i] = j;
         qmu[i] = 0;
         qlam[i] = 1;
         if (p.maxv > 1) {
@@ -234,33 +255,43 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
     // Row tiles start on a 16-row block (the launcher checks), so row piece pc
     // of an item is plane block ir0 / 16 + pc; a piece past the item's rows
     // re-reads piece 0 (discarded).
-    const uint32_t lanec = (uint32_t)(lane >> 2) * 64u + (uint32_t)((lane & 3) ^ p4_g((lane >> 4) & 3)) * 16u;
     uint32_t roff[4], qoff[4];
     const unsigned char *rbase = nullptr;  // plane block of the item's first row (uniform)
     const unsigned char *const qplane = reinterpret_cast<const unsigned char *>(p.q_hi);
     uint32_t noff = 0;                      // L2: this lane's row norm, relative to the item's first row
     const unsigned char *nbase = nullptr;
     bool first_src = true;                  // query offsets: per item only for cosine variants
+    // (the per-lane constants are re-derived from an opaque copy of the lane
+    // index at every item: hoisted out of the item loop they were spilled,
+    // and every reload from scratch waits for the whole LDS-DMA ring)
     auto set_src = [&]() __attribute__((always_inline)) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const uint32_t lc = (uint32_t)(ln >> 2) * 64u + (uint32_t)((ln & 3) ^ p4_g((ln >> 4) & 3)) * 16u;
         rbase = reinterpret_cast<const unsigned char *>(p.rows_hi) + (uint64_t)(uint32_t)(ir0 >> 4) * blk;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
             const int pc = w + 4 * i;
-            roff[i] = (ir0 + pc * 16 < ir1 ? (uint32_t)pc * blk : 0u) + lanec;
+            roff[i] = (ir0 + pc * 16 < ir1 ? (uint32_t)pc * blk : 0u) + lc;
         }
         if (p.maxv > 1 || first_src) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
+                int j = q0 + (w + 4 * i) * 16 + (ln >> 2);
+                if (j >= p.nq) j = 0;
                 int var = 0;
-                if (p.maxv > 1) var = iord < qmu[i] ? iord : qmu[i] + (iord - qmu[i]) % qlam[i];
-                const uint32_t u = (uint32_t)var * (uint32_t)p.q_vpad + (uint32_t)qj[i];
-                qoff[i] = (u >> 4) * blk + (u & 15) * 64u + (uint32_t)((lane & 3) ^ p4_g((lane >> 4) & 3)) * 16u;
+                if (p.maxv > 1) {
+                    const int mu = qmu[i], lam = qlam[i];
+                    var = iord < mu ? iord : mu + (iord - mu) % lam;
+                }
+                const uint32_t u = (uint32_t)var * (uint32_t)p.q_vpad + (uint32_t)j;
+                qoff[i] = (u >> 4) * blk + (u & 15) * 64u + (uint32_t)((ln & 3) ^ p4_g((ln >> 4) & 3)) * 16u;
             }
         }
         if constexpr (L2) {
             nbase = reinterpret_cast<const unsigned char *>(p.row_norms + ir0);
             const int last = ir1 - 1 - ir0;
-            noff = (uint32_t)(64 * w + lane < last ? 64 * w + lane : last) * 4u;
+            noff = (uint32_t)(64 * w + ln < last ? 64 * w + ln : last) * 4u;
         }
     };
     set_src();
@@ -345,48 +376,129 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
 #pragma unroll
     for (int i = 0; i < 4; ++i) b0[i] = frag(lds, rowB + i * 32 * 64 + offa0);
 
-    // k-step-0 phase: 16 MFMAs on (a0, b0); between them the k-step-1
-    // fragments of this stage and the 8 LDS-DMA pieces of stage gc + D
-    auto k0_phase = [&](const unsigned char *st, auto first_tag) __attribute__((always_inline)) {
-        constexpr bool FIRST = decltype(first_tag)::value;
-        f32x16 cinit[4];
-        if constexpr (FIRST && L2) {
-            // C = -yn / 2 of the block's rows (the item's norms in LDS)
-            const unsigned char *nb_ = norm_lds + (items_done & 1) * 1024;
+    // The threshold test of one 32 x 32 block (rows rb, queries jb) of the
+    // item whose rows start at ecr0 (ecrn of them): the maximum of the lane's
+    // 16 values (v_maximum3_f32: no canonicalising max per value as with
+    // fmaxf; a NaN value can only come from a NaN query, whose values all fail
+    // the threshold either way) against its query's threshold; a block with
+    // any lane over it walks its values.  The tests run in the MFMA gaps of
+    // the stages around an item boundary (below), not as an epilogue of their
+    // own.
+    auto check_block = [&](auto RB, auto JB, int ecr0, int ecrn) __attribute__((always_inline)) {
+        constexpr int rb = decltype(RB)::value, jb = decltype(JB)::value;
+        if constexpr ((DIAG & 16) != 0) {
+            // (diagnostic: keep the accumulators live, test nothing)
+            const f32x16 blk = acc[rb][jb];
+            if (p4_aread(blk[0]) == -1.2345e-30f) qcnt += 1;
+            return;
+        }
+        const int j = q0 + wq * 128 + jb * 32 + l32;
+        // (the block read in order, four values per statement: the compiler's
+        // own reads are hoisted together and spill)
+        const f32x16 blk = acc[rb][jb];
+        f32x4 v4[4];
 #pragma unroll
-            for (int rb = 0; rb < 4; ++rb)
+        for (int g = 0; g < 4; ++g) v4[g] = p4_aread4(blk[4 * g], blk[4 * g + 1], blk[4 * g + 2], blk[4 * g + 3]);
+        float mx = v4[0][0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mx = __builtin_elementwise_maximum(mx, v4[r >> 2][r & 3]);
+        // (a wave-uniform branch: the queue count is wave state)
+        if (__ballot(mx >= thr[jb]) == 0) return;
+        if constexpr ((DIAG & 32) != 0) {  // (diagnostic: tests without walks)
+            qcnt += 1;
+            return;
+        }
+        // the walk (rare): each lane's mask of values at or over the
+        // threshold; the values go to this wave's LDS scratch and a rolled loop
+        // takes one set bit per lane and round (rounds = the largest count in
+        // the wave, mostly 1).  (Unrolled over registers, the walks make the
+        // compiler spill, and every reload from scratch memory waits for the
+        // whole LDS-DMA ring.)
+        const float th = thr[jb], tj = tl[jb], qn = qnl[jb];
+        unsigned m16 = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) m16 |= (v4[r >> 2][r & 3] >= th ? 1u : 0u) << r;  // (padding: thr = +inf)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) *reinterpret_cast<f32x4 *>(wscr + lane * 16 + 4 * g) = v4[g];
+        const int rbl = wr * 128 + rb * 32 + 4 * h;
+#pragma unroll 1
+        while (__ballot(m16 != 0u) != 0) {
+            bool pass = m16 != 0u;
+            const int r = pass ? __builtin_ctz(m16) : 0;
+            m16 &= m16 - 1u;
+            const float x = wscr[lane * 16 + r];
+            float raw = x;
+            if constexpr (L2) {
+                raw = qn - 2.0f * x;
+                pass = pass && raw <= tj;
+            }
+            const int rl = rbl + (r & 3) + 8 * (r >> 2);
+            pass = pass && rl < ecrn;
+            const uint64_t m = __ballot(pass);
+            if (m == 0) continue;
+            const int pre =
+                __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+            if (pass) {
+                const uint32_t row = (uint32_t)(ecr0 + rl);
+                const int slot_ = qcnt + pre;
+                if (slot_ < qcap)
+                    wq_base[slot_] = u32x4{__builtin_bit_cast(unsigned, raw), row, (unsigned)j, 0u};
+                else  // queue full: the direct append (its returned slot makes
+                      // this wave wait for its LDS-DMA in flight: correct, slower)
+                    emit_approx<METRIC, false>(p, j, row, row, row_valid(p, row), raw);
+            }
+            qcnt += __popcll(m);
+        }
+    };
+
+    int pcr0 = 0, pcrn = 0;  // rows of the previous item (its blocks 8..15 are tested in the next one)
+
+    // k-step-0 phase: 16 MFMAs on (a0, b0); between them the k-step-1
+    // fragments of this stage and the 8 LDS-DMA pieces of stage gc + D.
+    // FIRST (the item's first stage): the MFMAs take C = 0, or -yn/2 of the
+    // block's rows for L2, and with EPI2 the previous item's blocks 8..15 are
+    // tested right before their first MFMA overwrites them.
+    auto k0_phase = [&](const unsigned char *st, auto first_tag, auto epi_tag) __attribute__((always_inline)) {
+        constexpr bool FIRST = decltype(first_tag)::value, EPI2 = decltype(epi_tag)::value;
+        f32x16 cinit;
+        p4_for<16>([&](auto X) __attribute__((always_inline)) {
+            constexpr int x = decltype(X)::value, rb = x >> 2, jb = x & 3;
+            if constexpr (FIRST && EPI2 && x >= 8)
+                check_block(std::integral_constant<int, rb>{}, std::integral_constant<int, jb>{}, pcr0, pcrn);
+            if constexpr (FIRST && L2 && jb == 0) {
+                // C = -yn / 2 of the block's rows (the item's norms in LDS)
+                const unsigned char *nb_ = norm_lds + (items_done & 1) * 1024;
 #pragma unroll
                 for (int g = 0; g < 4; ++g) {
                     const f32x4 v = *reinterpret_cast<const f32x4 *>(nb_ + (wr * 128 + rb * 32 + 8 * g + 4 * h) * 4);
 #pragma unroll
-                    for (int e = 0; e < 4; ++e) cinit[rb][4 * g + e] = -0.5f * v[e];
+                    for (int e = 0; e < 4; ++e) cinit[4 * g + e] = -0.5f * v[e];
                 }
-        }
-#pragma unroll
-        for (int x = 0; x < 16; ++x) {
-            const int rb = x >> 2, jb = x & 3;
+            }
             if constexpr (FIRST && L2)
-                acc[rb][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[rb], b0[jb], cinit[rb], 0, 0, 0);
+                acc[rb][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[rb], b0[jb], cinit, 0, 0, 0);
             else if constexpr (FIRST)
                 acc[rb][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[rb], b0[jb], f32x16{0.f}, 0, 0, 0);
             else
                 acc[rb][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a0[rb], b0[jb], acc[rb][jb], 0, 0, 0);
-            if (x < 4)
+            if constexpr (x < 4)
                 a1[x] = frag(st, rowA + x * 32 * 64 + offa1);
-            else if (x < 8)
+            else if constexpr (x < 8)
                 b1[x - 4] = frag(st, rowB + (x - 4) * 32 * 64 + offa1);
             else
                 issue_piece(x - 8);
             __builtin_amdgcn_sched_barrier(0);
-        }
+        });
     };
 
-    // one stage: k-step-0 phase (FIRST: the item's first stage, C = 0 / the
-    // L2 norms), the issue cursor, the barrier, k-step-1 phase
-    auto do_stage = [&](auto first_tag) __attribute__((always_inline)) {
+    // one stage: k-step-0 phase, the issue cursor, the barrier, k-step-1
+    // phase.  LAST (the item's last stage): blocks 0..7 are tested two MFMAs
+    // after their final one, in the k-step-1 phase's gaps.
+    auto do_stage = [&](auto first_tag, auto epi_tag, auto last_tag) __attribute__((always_inline)) {
+        constexpr bool LAST = decltype(last_tag)::value;
         const unsigned char *st = lds + cbuf * kP4Stage;
         const int nbuf_next = cbuf + 1 == NBUF ? 0 : cbuf + 1;
-        k0_phase(st, first_tag);
+        k0_phase(st, first_tag, epi_tag);
         if (L2 && si == 0 && live) issue_piece(8);
         issue_advance();
         // own pieces of stage gc + 1 landed (younger stages may stay in
@@ -400,96 +512,50 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
         // k-step-1 phase: 16 MFMAs on (a1, b1); between them the k-step-0
         // fragments of stage gc + 1
         const unsigned char *sn = lds + nbuf_next * kP4Stage;
-#pragma unroll
-        for (int x = 0; x < 16; ++x) {
-            const int rb = x >> 2, jb = x & 3;
+        const int crn = cr1 - cr0;
+        p4_for<16>([&](auto X) __attribute__((always_inline)) {
+            constexpr int x = decltype(X)::value, rb = x >> 2, jb = x & 3;
             acc[rb][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[rb], b1[jb], acc[rb][jb], 0, 0, 0);
             if (has_next) {
-                if (x < 4)
+                if constexpr (x < 4)
                     a0[x] = frag(sn, rowA + x * 32 * 64 + offa0);
-                else if (x < 8)
+                else if constexpr (x < 8)
                     b0[x - 4] = frag(sn, rowB + (x - 4) * 32 * 64 + offa0);
             }
+            if constexpr (LAST && x >= 2 && x < 10)
+                check_block(std::integral_constant<int, ((x - 2) >> 2)>{}, std::integral_constant<int, (x - 2) & 3>{},
+                            cr0, crn);
             __builtin_amdgcn_sched_barrier(0);
-        }
+        });
         ++gc;
         cbuf = nbuf_next;
     };
 
     // items: the first stage defines the accumulators (no phi with the last
-    // item's: they stay in place), the other stages accumulate
+    // item's: they stay in place), the other stages accumulate; nst >= 2
+    using T = std::integral_constant<bool, true>;
+    using F = std::integral_constant<bool, false>;
+    bool first_item = true;
     while (true) {
-        do_stage(std::integral_constant<bool, true>{});
-        for (int s = 1; s < nst; ++s) do_stage(std::integral_constant<bool, false>{});
-        // item epilogue
-        if constexpr ((DIAG & 16) != 0) {
-            float sum = 0.f;
-#pragma unroll
-            for (int rb = 0; rb < 4; ++rb)
-#pragma unroll
-                for (int jb = 0; jb < 4; ++jb)
-#pragma unroll
-                    for (int r = 0; r < 16; ++r) sum += acc[rb][jb][r];
-            if (sum == -1.2345e-30f) qcnt += 1;
-        } else {
-            const int crn = cr1 - cr0;  // rows of the item (<= 256)
-            // per 32 x 32 block: the maximum of the lane's 16 values (one
-            // v_max3 per two values; fmaxf would add a canonicalising max per
-            // value) against its query's threshold; a block with any lane over
-            // it walks its 16 values (constant accumulator indices: the
-            // accumulators stay in registers; the walk is cold code)
-            auto epi_block = [&](auto RB, auto JB) __attribute__((always_inline)) {
-                constexpr int rb = decltype(RB)::value, jb = decltype(JB)::value;
-                __builtin_amdgcn_sched_barrier(0);  // (one block's values at a time in VGPRs)
-                const int j = q0 + wq * 128 + jb * 32 + l32;
-                float mx = p4_max3(acc[rb][jb][0], acc[rb][jb][1], acc[rb][jb][2]);
-#pragma unroll
-                for (int r = 3; r < 15; r += 2) mx = p4_max3(mx, acc[rb][jb][r], acc[rb][jb][r + 1]);
-                mx = p4_max3(mx, acc[rb][jb][15], acc[rb][jb][15]);
-                // (a wave-uniform branch: the queue count is wave state)
-                if (__ballot(mx >= thr[jb]) == 0) return;
-#pragma unroll
-                for (int r = 0; r < 16; ++r) {
-                    const float x = acc[rb][jb][r];
-                    float raw = x;
-                    bool pass = x >= thr[jb];  // (padding queries: thr = +inf)
-                    if constexpr (L2) {
-                        raw = qnl[jb] - 2.0f * x;
-                        pass = pass && raw <= tl[jb];
-                    }
-                    uint64_t m = __ballot(pass);
-                    if (m == 0) continue;
-                    // the value's row, formed only here (hoisted, the 256 row
-                    // offsets of a lane would be spilled across the loop)
-                    int rbase_l = wr * 128 + 4 * h;
-                    asm volatile("" : "+v"(rbase_l));
-                    const int rl = rbase_l + rb * 32 + (r & 3) + 8 * (r >> 2);
-                    pass = pass && rl < crn;
-                    m = __ballot(pass);
-                    if (m == 0) continue;
-                    const int pre =
-                        __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
-                    if (pass) {
-                        const uint32_t row = (uint32_t)(cr0 + rl);
-                        const int slot_ = qcnt + pre;
-                        if (slot_ < qcap)
-                            wq_base[slot_] = u32x4{__builtin_bit_cast(unsigned, raw), row, (unsigned)j, 0u};
-                        else  // queue full: mark the query's list overflowed (count > cap,
-                              // kept by every refine) -> the search re-runs on the exact path
-                            atomicMax(&p.cand_count[j], p.cand_cap + 1);
-                    }
-                    qcnt += __popcll(m);
-                }
-            };
-            p4_for<4>([&](auto JB) __attribute__((always_inline)) {
-                p4_for<4>([&](auto RB) __attribute__((always_inline)) { epi_block(RB, JB); });
-            });
-        }
+        if (first_item)
+            do_stage(T{}, F{}, F{});
+        else
+            do_stage(T{}, T{}, F{});
+        for (int s = 1; s + 1 < nst; ++s) do_stage(F{}, F{}, F{});
+        do_stage(F{}, F{}, T{});
+        pcr0 = cr0;
+        pcrn = cr1 - cr0;
+        first_item = false;
         ++items_done;
         int cord;
         ti_c = next_item(ti_c + tstride, cr0, cr1, cord);
         if (ti_c < 0) break;
     }
+    // blocks 8..15 of the last item
+    p4_for<8>([&](auto X) __attribute__((always_inline)) {
+        constexpr int x = decltype(X)::value + 8;
+        check_block(std::integral_constant<int, (x >> 2)>{}, std::integral_constant<int, (x & 3)>{}, pcr0, pcrn);
+    });
     // flush this wave's queue to the per-query candidate lists
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int nqueue = qcnt < qcap ? qcnt : qcap;
@@ -500,8 +566,8 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
     }
 }
 
-// queue entries per wave (16 B each): 2048 x 16 B x 4 waves x 256 CUs = 32 MiB
-constexpr int kP4QueueCap = 2048;
+// queue entries per wave (16 B each): 4096 x 16 B x 4 waves x 256 CUs = 64 MiB
+constexpr int kP4QueueCap = 4096;
 
 size_t p4_queue_bytes() {
     static int cus = 0;
@@ -543,15 +609,14 @@ static bool launch_p4_t(ScanParams p, hipStream_t s) {
         // measurement builds: ring depth and decomposition variants
         const int nbuf = tune_int("MQVS_P4_NBUF", 4);
         const int diag = tune_int("MQVS_P4_DIAG", 0);
-#define MQVS_P4(NB_, DG_) hipLaunchKernelGGL((k_scan_p4<METRIC, NB_, DG_>), grid, dim3(256), 0, s, p, slots, q, kP4QueueCap)
+#define MQVS_P4(NB_, DG_)                                                                                     \
+    hipLaunchKernelGGL((k_scan_p4<METRIC, NB_, DG_>), grid, dim3(256), 0, s, p, slots, q, kP4QueueCap)
         if (diag == 4) MQVS_P4(4, 4);
         else if (diag == 8) MQVS_P4(4, 8);
         else if (diag == 12) MQVS_P4(4, 12);
         else if (diag == 16) MQVS_P4(4, 16);
         else if (diag == 28) MQVS_P4(4, 28);
-        else if (nbuf == 5 && !(METRIC == MQVS_METRIC_L2)) {
-            if constexpr (METRIC != MQVS_METRIC_L2) MQVS_P4(5, 0);
-        }
+        else if (diag == 32) MQVS_P4(4, 32);
         else if (nbuf == 3) MQVS_P4(3, 0);
         else MQVS_P4(4, 0);
 #undef MQVS_P4

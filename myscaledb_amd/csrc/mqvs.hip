@@ -354,7 +354,7 @@ static SegTune seg_tune(int nq) {
         v.first = 4;
         v.growth = 4;
     }
-    if (const char *e = std::getenv("MQVS_SEG")) {
+    if (const char *e = tune_env("MQVS_SEG")) {
         long long a = 0, b = 0, c = 0;
         if (std::sscanf(e, "%lld,%lld,%lld", &a, &b, &c) == 3 && a >= 1 && b >= 2 && c >= 256) {
             v.first = a;

@@ -9,6 +9,7 @@
 #include <algorithm>
 
 #include "../../include/mqvs.h"
+#include "tuning.h"
 
 struct mqvs_segment {
     int device = 0;
