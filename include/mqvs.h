@@ -133,8 +133,8 @@ int mqvs_segment_generate(uint64_t seed, int32_t mode, int64_t n, int32_t d, int
 int mqvs_segment_free(mqvs_segment_t seg);
 int mqvs_segment_info(mqvs_segment_t seg, int64_t *n, int32_t *d, int32_t *metric,
                       int64_t *granule_rows, int64_t *row_offset, size_t *hbm_bytes);
-/* The segment's pre-filter planes: *split = the split built (2 / 3 / 6, see
- * mqvs_set_prefilter) or 0 when the planes did not fit in HBM at creation --
+/* The segment's pre-filter planes: *split = 2 (the bf16 plane, see
+ * mqvs_set_prefilter) or 0 when the planes were off or did not fit in HBM --
  * batches then run the exact fp32 MFMA path over every row (same bits, about
  * 1/16 of the bf16 MFMA rate); *plane_bytes = their HBM bytes (included in
  * mqvs_segment_info's hbm_bytes); *approx_ok = 1 when the pre-filter serves
@@ -450,8 +450,7 @@ typedef struct {
     int32_t segments;       /* main-scan segments (threshold refinements + 1) */
     int32_t gather;         /* 1: selective PREWHERE, the scan walked the gather list
                                of selected rows (rows_scanned = list entries) */
-    int32_t prefilter;      /* path 2: pre-filter split (2 = bf16 hi, 6 = bf16 + fp6 MX,
-                               3 = bf16 x3) */
+    int32_t prefilter;      /* path 2: pre-filter split (2 = bf16 hi) */
     int32_t batch_kernel;   /* path 2: 1 when the main scan ran the one-wave-per-SIMD batch
                                kernel (nq > 128, contiguous rows), else 0 */
     int64_t survivors_total;/* path 2: rows re-ranked exactly (sum over queries) */
@@ -473,11 +472,10 @@ int mqvs_set_batch_mode(int mode);
  * bits. */
 int mqvs_set_gather_mode(int mode);
 /* Pre-filter planes built by segments created AFTER the call: 2 = bf16 hi
- * plane only, one bf16 MFMA product bounded by measured residual norms
- * (default; 2 B per element), 6 = bf16 hi plane + block-scaled fp6 cross
- * plane, cross terms on the MX MFMA (3.5 B per element), 3 = bf16 hi + lo
- * planes, three bf16 MFMAs (4 B per element).  All bound their error
- * rigorously and return the same bits. */
+ * plane, one bf16 MFMA product bounded by measured residual norms (default;
+ * 2 B per element), 0 = no planes (batches run the exact fp32 MFMA path over
+ * every row).  Other values (rounds 1-2 also had 3 and 6) are
+ * MQVS_ERR_BAD_ARGUMENTS.  Both return the same bits. */
 int mqvs_set_prefilter(int split);
 /* Device scratch that one call may allocate for large-k sorts and candidate
  * lists (default 1 GiB per buffer, at least 1 MiB): calls whose buffers would

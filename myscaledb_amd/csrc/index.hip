@@ -599,7 +599,7 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
         maxv = (int)std::min<int64_t>(ords, kMaxVariantsCap);
     }
     uint16_t *qhi = (uint16_t *)ws.qhi.get(sizeof(uint16_t) * (size_t)nq * ix->dpad);
-    launch_to_bf16(qvars, nq, d, (int64_t)maxv * qstride, qhi, nullptr, ix->dpad, s);
+    launch_to_bf16(qvars, nq, d, (int64_t)maxv * qstride, qhi, ix->dpad, s);
     MQVS_HIP(hipGetLastError());
 
     // ---- coarse: the nprobe nearest centroids, by the same list pass over

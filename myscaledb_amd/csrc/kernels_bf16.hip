@@ -36,32 +36,23 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef __attribute__((address_space(3))) void lds_void;
 
 // ---------------------------------------------------------------------------
-__global__ void k_to_bf16(const float *src, int64_t rows, int d, int64_t sstride, uint16_t *hi,
-                          uint16_t *lo, int64_t dpad) {
+__global__ void k_to_bf16(const float *src, int64_t rows, int d, int64_t sstride, uint16_t *hi, int64_t dpad) {
     const int64_t total = rows * dpad;
     for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total;
          e += (int64_t)gridDim.x * blockDim.x) {
         const int64_t r = e / dpad;
         const int c = (int)(e - r * dpad);
-        uint16_t vh = 0, vl = 0;
-        if (c < d) {
-            const float x = src[r * sstride + c];
-            vh = f32_to_bf16_rn(x);
-            // x - hi is exact in fp32 (hi is x rounded to 8 significant bits)
-            vl = f32_to_bf16_rn(x - __builtin_bit_cast(float, (uint32_t)vh << 16));
-        }
-        hi[e] = vh;
-        if (lo) lo[e] = vl;
+        hi[e] = c < d ? f32_to_bf16_rn(src[r * sstride + c]) : (uint16_t)0;
     }
 }
 
-void launch_to_bf16(const float *src, int64_t rows, int d, int64_t sstride, uint16_t *dst_hi,
-                    uint16_t *dst_lo, int64_t dpad, hipStream_t s) {
+void launch_to_bf16(const float *src, int64_t rows, int d, int64_t sstride, uint16_t *dst_hi, int64_t dpad,
+                    hipStream_t s) {
     int64_t blocks = (rows * dpad + 255) / 256;
     if (blocks > 65536) blocks = 65536;
     if (blocks < 1) return;
     hipLaunchKernelGGL(k_to_bf16, dim3((unsigned)blocks), dim3(256), 0, s, src, rows, d, sstride,
-                       dst_hi, dst_lo, dpad);
+                       dst_hi, dpad);
 }
 
 // max_r sqrt(|y_r|^2) (non-negative floats: max of the bit patterns)
@@ -91,47 +82,23 @@ void launch_max_norm(const float *norms2, int64_t n, float *out_max, hipStream_t
 // Per-query bound on |approx - exact| in the metric's raw value:
 //   IP / cosine: B = c(d) * |x|max_over_used_variants * |y|max
 //   L2 (BLAS):   raw = (xn + yn) - 2 ip -> 2 B + 2 ulp of the result
-//   split 3: truncation |xl yl| + |xh ey| + |ex y| <= 3.03 2^-16 |x||y|; the
-//   three products are exact in fp32 and summed into ONE accumulator: 3d terms
-//   with sum |t| <= 1.008 |x||y| -> 3.03 d u, plus d u for the exact chain.
-//   split 1: element rounding 2^-8 per side -> (2^-7 + 2^-16) |x||y| + 2 d u.
 //   direct (nq < 20: the exact value is faiss's sequential product-then-add
 //   formula, not the BLAS form): IP/cosine as above ((d+1) u |x||y| for the
 //   sequential sum is inside the constants); L2 compares the BLAS-form
 //   approximation with fl(sum (y-x)^2), so add the norms' rounding (d u each)
 //   and the direct sum's own error ((d+3) u (|x|+|y|)^2 <= 2 (d+3) u top):
 //   2 B + (3 d + 12) u top.
-//   split 6 (kernels_mx.hip): from the query variant's norm record q and the
-//   segment's maxima Y (|h| |r| |h6| |h-h6| |r6| |r-r6| |x|):
-//     truncation  q3 Y1 + q2 Y5 + q5 Y0 + q4 Y3 + q1 Y1
-//     accumulation 3.03 d u (q0 Y0 + q2 Y4 + q4 Y2) + 1.01 d u |x||y| (exact chain)
-//     MX internal 2^-10 (q2 Y4 + q4 Y2): an allowance for the f8f6f4 MFMA's
-//     internal sum, measured against exact sums on adversarial e2m3 codes and
-//     every scale range (tools/mfma_acc_probe.hip,
-//     profiles/r02/probes/mfma_acc_probe.log): worst 1.5 u sum|p| over 12
-//     chained MFMAs (8.9e-8 relative), 2^14 / 1.5 below the allowance; the
-//     bf16 MFMA's worst is 95.5 u sum|p| at d = 768 against the 2.04 d u
-//     (1567 u) the bf16 terms assume
-__global__ void k_query_bound(ScanParams p, int metric, int split, int direct,
-                              const float *ynorm_max, const float *qrec, const float *yrec, float *bq) {
-    // one wave per query; |x| in fp64 (an upper bound after the 1.0001 slack)
-    const int j = blockIdx.x;
-    const int lane = threadIdx.x;
-    const int64_t qs = (int64_t)((p.d + 31) / 32 * 32);
+__global__ void k_query_bound(ScanParams p, int metric, int direct, const float *ynorm_max, const float *qrec,
+                              const float *yrec, float *bq) {
+    // one thread per query (|x| from the variants' norm records)
+    const int j = blockIdx.x * blockDim.x + threadIdx.x;
+    if (j >= p.nq) return;
     const int nv = p.maxv <= 1 ? 1 : p.qmu[j] + p.qlam[j];
     float xmax = 0.f;
-    for (int v = 0; v < (split == kMxSplit || split == kHiSplit ? 0 : nv); ++v) {
-        const float *x = p.qvars + ((int64_t)j * p.maxv + v) * qs;
-        double s = 0.0;
-        for (int i = lane; i < p.d; i += 64) s += (double)x[i] * (double)x[i];
-        for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off);
-        xmax = fmaxf(xmax, (float)sqrt(s));
-    }
-    if (lane != 0) return;
     const float ymax = *ynorm_max * (1.0f + 6e-8f * (float)p.d + 1e-6f);  // fp32 |y|^2 chain error
     const float du = (float)p.d * 5.9604645e-8f;
     float b;
-    if (split == kHiSplit) {
+    {
         // x.y - xh.yh = xh.ry + rx.yh + rx.ry (records: q[0] |xh|, q[1] |rx|,
         // q[6] |x|; Y the segment maxima); the MFMA sums d exact products, at
         // most 2 u relative per addition (2.04 d u |xh||yh|, covers
@@ -148,36 +115,15 @@ __global__ void k_query_bound(ScanParams p, int metric, int split, int direct,
             b = fmaxf(b, bv * 1.0001f);
         }
         b += 1e-30f;
-    } else if (split == kMxSplit) {
-        const float *Y = yrec;
-        b = 0.f;
-        for (int v = 0; v < nv; ++v) {
-            const float *q = qrec + ((int64_t)j * p.maxv + v) * kMxRec;
-            xmax = fmaxf(xmax, q[6]);
-            const float trunc = q[3] * Y[1] + q[2] * Y[5] + q[5] * Y[0] + q[4] * Y[3] + q[1] * Y[1];
-            const float mx = q[2] * Y[4] + q[4] * Y[2];
-            const float terms = q[0] * Y[0] + mx;
-            const float bv = trunc + 9.765625e-4f * mx + 3.03f * du * terms + 1.01f * du * q[6] * ymax +
-                             1.2e-7f * q[6] * ymax;
-            b = fmaxf(b, bv * 1.0001f);
-        }
-        b += 1e-30f;
-    } else {
-        const float acc_term = (split == 3 ? 4.1f : 2.04f) * du;
-        const float c = split == 3 ? 3.1f * 1.5258789e-5f + acc_term + 1.2e-7f
-                                   : 0.0078125f + 1.6e-5f + acc_term + 1e-7f;
-        b = c * (xmax * 1.0001f) * ymax + 1e-30f;
     }
     if (metric == MQVS_METRIC_L2) {
         const float top = p.qnorms[j] * 1.0001f + ymax * ymax;
         const float rel = direct ? (3.0f * (float)p.d + 12.0f) * 5.9604645e-8f : 2.4e-7f;
         b = 2.0f * b + top * rel + 1e-30f;
-        if (split == kHiSplit) {
-            // the batch scan (kernels_p4.hip) starts its accumulation at
-            // -|y|^2 / 2 and forms fl(qn - 2 acc): the accumulation bound
-            // covers |y|^2 / 2 more per term, and the two final roundings
-            b += 2.0f * 2.04f * du * 0.5f * ymax * ymax + 2.4e-7f * top;
-        }
+        // the batch scan (kernels_p4.hip) starts its accumulation at -|y|^2 / 2
+        // and forms fl(qn - 2 acc): the accumulation bound covers |y|^2 / 2
+        // more per term, and the two final roundings
+        b += 2.0f * 2.04f * du * 0.5f * ymax * ymax + 2.4e-7f * top;
     } else if (metric == MQVS_METRIC_COSINE) {
         b = b + 2.4e-7f;  // 1 - ip rounds; ties on 1-ip may differ in ip by one ulp of 1
     }
@@ -185,11 +131,10 @@ __global__ void k_query_bound(ScanParams p, int metric, int split, int direct,
     bq[j] = b;
 }
 
-void launch_query_bound(const ScanParams &p, int metric, int split, const float *ynorm_max,
-                        const float *qrec, const float *yrec, float *bq, hipStream_t s) {
+void launch_query_bound(const ScanParams &p, int metric, const float *ynorm_max, const float *qrec,
+                        const float *yrec, float *bq, hipStream_t s) {
     const int direct = !blas_formula(p);
-    hipLaunchKernelGGL(k_query_bound, dim3(p.nq), dim3(64), 0, s, p, metric, split, direct, ynorm_max, qrec, yrec,
-                       bq);
+    hipLaunchKernelGGL(k_query_bound, dim3((unsigned)((p.nq + 255) / 256)), dim3(256), 0, s, p, metric, direct, ynorm_max, qrec, yrec, bq);
 }
 
 

@@ -10,13 +10,12 @@
 // The margin this leaves around the k-th value (~0.004 of |x||y|) admits a
 // few hundred extra rows per query on the Gaussian / mixture parts measured;
 // every one of them is re-ranked with the exact fp32 chain, so the output is
-// bit-identical to the fp32 path.  Against the bf16 + fp6-MX pre-filter
-// (kernels_mx.hip, split 6) this streams 2 B per element instead of 3.5 and
-// issues 2 MFMAs per 32-column stage and 32x32 block instead of 3 -- the MX
-// kernel was bound by exactly that L2 -> LDS stream.
+// bit-identical to the fp32 path.  (Rounds 1-2 also kept a hi + lo split and
+// a bf16 + fp6-MX split; both streamed more bytes per element for the same
+// survivors and were removed in round 3.)
 //
-// Planes are row-blocked as the MX hi plane (16 vectors x 32 columns = 1 KiB
-// contiguous): vector u, stage s at byte ((u >> 4) nst + s) 1024 + (u & 15) 64.
+// Planes are row-blocked (16 vectors x 32 columns = 1 KiB contiguous):
+// vector u, stage s at byte ((u >> 4) nst + s) 1024 + (u & 15) 64.
 //
 // Scan pipeline: a ring of NBUF LDS stages (stage = 32 columns of the 256-row
 // tile and of the QT-query tile, filled by global_load_lds_dwordx4 in 1 KiB

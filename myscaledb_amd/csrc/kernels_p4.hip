@@ -78,15 +78,18 @@ __device__ __host__ inline int p4_g(int x) { return (4 - x) & 3; }
 // s_waitcnt vmcnt(P n), n in [0, 3] at run time (P: pieces a wave issues per
 // stage; a stage that also carries a norm piece makes the wait stricter by
 // one operation, never looser)
-template <int P>
-__device__ inline void p4_wait_vm(int n) {
+// (X: pieces of a half-issued stage on top, when any is wanted)
+template <int P, int X = 0>
+__device__ inline void p4_wait_vm(int n, bool any = true) {
     __builtin_amdgcn_sched_barrier(0);
-    if (P > 0 && n >= 3)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * P) : "memory");
-    else if (P > 0 && n == 2)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * P) : "memory");
-    else if (P > 0 && n == 1)
-        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P) : "memory");
+    if (P > 0 && any && n >= 3)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(3 * P + X) : "memory");
+    else if (P > 0 && any && n == 2)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(2 * P + X) : "memory");
+    else if (P > 0 && any && n == 1)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(P + X) : "memory");
+    else if (P > 0 && any && X > 0)
+        asm volatile("s_waitcnt vmcnt(%0)" ::"n"(X) : "memory");
     else
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -134,12 +137,19 @@ __device__ inline void p4_barrier() {
     __builtin_amdgcn_sched_barrier(0);
 }
 
+// PL: where a stage's 8 LDS-DMA pieces go: 0 = k-step-0 phase slots 8..15;
+// 1 = slots 8..11 of both phases; 2 = slots 8, 10, 12, 14 of both phases
+// (the ds_read-free gaps)
 // DIAG (measurement builds only; wrong results): 4 = query pieces not issued,
 // 8 = row pieces not issued, 16 = no threshold tests (the accumulators are
-// kept live by one read per block), 32 = threshold tests without walks
-template <int METRIC, int NBUF, int DIAG = 0>
-__global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32x4 *queue, int qcap) {
+// kept live by one read per block), 32 = threshold tests without walks,
+// 128 = no stage barrier, 256 = no fragment-read wait before it, 512 = cosine
+// query variant 0 for every chunk
+template <int METRIC, int NBUF, int DIAG = 0, int PL = 0>
+__global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32x4 *queue, int qcap, int tmap) {
     constexpr bool L2 = METRIC == MQVS_METRIC_L2;
+    // cache policy of the row / query pieces (PL bits 4 / 8: nt)
+    constexpr int RPOL = (PL & 4) ? 2 : 0, QPOL = (PL & 8) ? 2 : 0;
     // stages in flight ahead of the one consumed: a buffer is re-filled one
     // barrier after its last fragment reads retired (lgkmcnt(0) before it)
     constexpr int D = NBUF - 1;
@@ -244,7 +254,11 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
     // issue cursor: item ti_i (rows [ir0, ir1), ordinal iord), next stage si
     int ir0 = 0, ir1 = 0;
     int iord = 0;
-    int ti_i = next_item(xcd + 8 * tg, ir0, ir1, iord);
+    // tile sequence of group tg of XCD x: t = start + 8 G j (G groups per
+    // XCD).  tmap 1: start = x G + tg -- the XCD's groups work on G
+    // consecutive tiles at a time (one chunk: one cosine query variant in the
+    // XCD's L2); tmap 0: start = x + 8 tg
+    int ti_i = next_item(tmap ? xcd * ngroups + tg : xcd + 8 * tg, ir0, ir1, iord);
     if (ti_i < 0) return;  // no work (uniform)
     const int nb = nst;
     const uint32_t blk = (uint32_t)nb * 1024u;  // bytes of one 16-vector block over all stages
@@ -280,7 +294,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
                 int j = q0 + (w + 4 * i) * 16 + (ln >> 2);
                 if (j >= p.nq) j = 0;
                 int var = 0;
-                if (p.maxv > 1) {
+                if (p.maxv > 1 && (DIAG & 512) == 0) {
                     const int mu = qmu[i], lam = qlam[i];
                     var = iord < mu ? iord : mu + (iord - mu) % lam;
                 }
@@ -311,10 +325,10 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
         unsigned char *dst = lds + ibuf * kP4Stage;
         if (x < 4) {
             __builtin_amdgcn_global_load_lds((const void *)(rbase + (uint32_t)si * 1024u + roff[x]),
-                                             (lds_void *)(dst + (w + 4 * x) * 1024), 16, 0, 0);
+                                             (lds_void *)(dst + (w + 4 * x) * 1024), 16, 0, RPOL);
         } else if (x < 8) {
             __builtin_amdgcn_global_load_lds((const void *)(qplane + (uint32_t)si * 1024u + qoff[x - 4]),
-                                             (lds_void *)(dst + kP4QOff + (w + 4 * (x - 4)) * 1024), 16, 0, 0);
+                                             (lds_void *)(dst + kP4QOff + (w + 4 * (x - 4)) * 1024), 16, 0, QPOL);
         } else if constexpr (L2) {
             __builtin_amdgcn_global_load_lds((const void *)(nbase + noff),
                                              (lds_void *)(norm_lds + (items_issued & 1) * 1024 + w * 256), 4, 0, 0);
@@ -485,8 +499,12 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
                 a1[x] = frag(st, rowA + x * 32 * 64 + offa1);
             else if constexpr (x < 8)
                 b1[x - 4] = frag(st, rowB + (x - 4) * 32 * 64 + offa1);
-            else
+            else if constexpr ((PL & 3) == 0)
                 issue_piece(x - 8);
+            else if constexpr ((PL & 3) == 1 && x < 12)
+                issue_piece(x - 8);
+            else if constexpr ((PL & 3) == 2 && (x & 1) == 0)
+                issue_piece((x - 8) >> 1);
             __builtin_amdgcn_sched_barrier(0);
         });
     };
@@ -500,15 +518,17 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
         const int nbuf_next = cbuf + 1 == NBUF ? 0 : cbuf + 1;
         k0_phase(st, first_tag, epi_tag);
         if (L2 && si == 0 && live) issue_piece(8);
-        issue_advance();
+        if constexpr ((PL & 3) == 0) issue_advance();
         // own pieces of stage gc + 1 landed (younger stages may stay in
         // flight); this stage's fragment reads retired (the next phase
         // re-fills its buffer); then the barrier: stage gc + 1 is complete
         // for every wave
         const bool has_next = gc + 1 < issued;
-        p4_wait_vm<NPW>(has_next ? issued - gc - 2 : 0);
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        p4_barrier();
+        // (PL > 0: the other half of stage gc + D is issued in the next phase;
+        // its first half is younger than stage gc + 1's pieces)
+        p4_wait_vm<NPW, (PL & 3) == 0 ? 0 : NPW / 2>(issued - gc - 2, has_next);
+        if constexpr ((DIAG & 256) == 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        if constexpr ((DIAG & 128) == 0) p4_barrier();
         // k-step-1 phase: 16 MFMAs on (a1, b1); between them the k-step-0
         // fragments of stage gc + 1
         const unsigned char *sn = lds + nbuf_next * kP4Stage;
@@ -522,11 +542,16 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
                 else if constexpr (x < 8)
                     b0[x - 4] = frag(sn, rowB + (x - 4) * 32 * 64 + offa0);
             }
+            if constexpr ((PL & 3) == 1 && x >= 8 && x < 12)
+                issue_piece(x - 4);
+            else if constexpr ((PL & 3) == 2 && x >= 8 && (x & 1) == 0)
+                issue_piece(4 + ((x - 8) >> 1));
             if constexpr (LAST && x >= 2 && x < 10)
                 check_block(std::integral_constant<int, ((x - 2) >> 2)>{}, std::integral_constant<int, (x - 2) & 3>{},
                             cr0, crn);
             __builtin_amdgcn_sched_barrier(0);
         });
+        if constexpr ((PL & 3) != 0) issue_advance();
         ++gc;
         cbuf = nbuf_next;
     };
@@ -605,23 +630,35 @@ static bool launch_p4_t(ScanParams p, hipStream_t s) {
     const int slots = per_xcd / p.num_qblocks * p.num_qblocks;
     auto *q = reinterpret_cast<u32x4 *>(p.p4_queue);
     const dim3 grid((unsigned)(8 * per_xcd));
+    const int tmap = tune_int("MQVS_P4_MAP", 0);
     if constexpr (kDebugTuning) {
         // measurement builds: ring depth and decomposition variants
         const int nbuf = tune_int("MQVS_P4_NBUF", 4);
         const int diag = tune_int("MQVS_P4_DIAG", 0);
-#define MQVS_P4(NB_, DG_)                                                                                     \
-    hipLaunchKernelGGL((k_scan_p4<METRIC, NB_, DG_>), grid, dim3(256), 0, s, p, slots, q, kP4QueueCap)
-        if (diag == 4) MQVS_P4(4, 4);
-        else if (diag == 8) MQVS_P4(4, 8);
-        else if (diag == 12) MQVS_P4(4, 12);
-        else if (diag == 16) MQVS_P4(4, 16);
-        else if (diag == 28) MQVS_P4(4, 28);
-        else if (diag == 32) MQVS_P4(4, 32);
-        else if (nbuf == 3) MQVS_P4(3, 0);
-        else MQVS_P4(4, 0);
+        const int pl = tune_int("MQVS_P4_PL", 0);
+#define MQVS_P4(NB_, DG_, PL_)                                                                                     \
+    hipLaunchKernelGGL((k_scan_p4<METRIC, NB_, DG_, PL_>), grid, dim3(256), 0, s, p, slots, q, kP4QueueCap, tmap)
+        if (diag == 4) MQVS_P4(4, 4, 0);
+        else if (diag == 8) MQVS_P4(4, 8, 0);
+        else if (diag == 12) MQVS_P4(4, 12, 0);
+        else if (diag == 16) MQVS_P4(4, 16, 0);
+        else if (diag == 28) MQVS_P4(4, 28, 0);
+        else if (diag == 32) MQVS_P4(4, 32, 0);
+        else if (diag == 128) MQVS_P4(4, 128, 0);
+        else if (diag == 256) MQVS_P4(4, 256, 0);
+        else if (diag == 384) MQVS_P4(4, 384, 0);
+        else if (diag == 156) MQVS_P4(4, 156, 0);
+        else if (diag == 512) MQVS_P4(4, 512, 0);
+        else if (nbuf == 3) MQVS_P4(3, 0, 0);
+        else if (pl == 1) MQVS_P4(4, 0, 1);
+        else if (pl == 2) MQVS_P4(4, 0, 2);
+        else if (pl == 4) MQVS_P4(4, 0, 4);
+        else if (pl == 6) MQVS_P4(4, 0, 6);
+        else if (pl == 8) MQVS_P4(4, 0, 8);
+        else MQVS_P4(4, 0, 0);
 #undef MQVS_P4
     } else {
-        hipLaunchKernelGGL((k_scan_p4<METRIC, 4, 0>), grid, dim3(256), 0, s, p, slots, q, kP4QueueCap);
+        hipLaunchKernelGGL((k_scan_p4<METRIC, 4, 0>), grid, dim3(256), 0, s, p, slots, q, kP4QueueCap, tmap);
     }
     return true;
 }

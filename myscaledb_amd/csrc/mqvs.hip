@@ -110,37 +110,15 @@ static void prepare_segment(mqvs_segment *s, const uint8_t *dev_nonempty_bytes,
     const int64_t nr = std::max<int64_t>(s->n, 1);
     const int64_t nr16 = (nr + 15) / 16 * 16;  // row-blocked planes: blocks of 16 rows
     const int split = g_prefilter.load(std::memory_order_relaxed);
-    const size_t hb = (size_t)(split == kBfSplit ? nr : nr16) * s->dpad * sizeof(uint16_t);
-    const size_t xb = (size_t)nr16 * (s->dpad / 32) * 48;
-    bool ok = hipMalloc((void **)&s->rows_hi, hb) == hipSuccess;
-    if (split == kMxSplit) {
-        ok = ok && hipMalloc((void **)&s->rows_x6, xb) == hipSuccess &&
-             hipMalloc((void **)&s->rows_sc, (size_t)nr * 2) == hipSuccess;
-    } else if (split == kBfSplit) {
-        ok = ok && hipMalloc((void **)&s->rows_lo, hb) == hipSuccess;
-    }
-    if (ok) {
-        if (split == kHiSplit) {
-            s->bytes += hb;
-            launch_to_hi(s->rows, s->n, s->d, s->d, s->dpad, 1, nr16, s->rows_hi, nullptr, s->ynorm_max + 4, st);
-        } else if (split == kMxSplit) {
-            s->bytes += hb + xb + (size_t)nr * 2;
-            launch_to_mx(s->rows, s->n, s->d, s->d, s->dpad, 1, nr16, true, s->rows_hi, s->rows_x6, s->rows_sc,
-                         nullptr, s->ynorm_max + 4, st);
-        } else {
-            s->bytes += 2 * hb;
-            launch_to_bf16(s->rows, s->n, s->d, s->d, s->rows_hi, s->rows_lo, s->dpad, st);
-        }
+    const size_t hb = (size_t)nr16 * s->dpad * sizeof(uint16_t);
+    if (split == kHiSplit && hipMalloc((void **)&s->rows_hi, hb) == hipSuccess) {
+        s->bytes += hb;
+        launch_to_hi(s->rows, s->n, s->d, s->d, s->dpad, 1, nr16, s->rows_hi, nullptr, s->ynorm_max + 4, st);
         s->split = split;
-        s->plane_bytes = split == kHiSplit ? hb : split == kMxSplit ? hb + xb + (size_t)nr * 2 : 2 * hb;
+        s->plane_bytes = hb;
     } else {
-        (void)hipGetLastError();  // no room: exact fp32 batch path only
-        for (void *q : {(void *)s->rows_hi, (void *)s->rows_lo, (void *)s->rows_x6, (void *)s->rows_sc})
-            if (q) (void)hipFree(q);
+        (void)hipGetLastError();  // no room (or planes off): exact fp32 batch path only
         s->rows_hi = nullptr;
-        s->rows_lo = nullptr;
-        s->rows_x6 = nullptr;
-        s->rows_sc = nullptr;
     }
     MQVS_HIP(hipGetLastError());
     float ymax = 0.f;
@@ -191,9 +169,6 @@ static void free_segment(mqvs_segment *s) {
     if (s->norms) (void)hipFree(s->norms);
     if (s->nonempty_bits) (void)hipFree(s->nonempty_bits);
     if (s->rows_hi) (void)hipFree(s->rows_hi);
-    if (s->rows_lo) (void)hipFree(s->rows_lo);
-    if (s->rows_x6) (void)hipFree(s->rows_x6);
-    if (s->rows_sc) (void)hipFree(s->rows_sc);
     if (s->ynorm_max) (void)hipFree(s->ynorm_max);
     if (s->chunk_ord) (void)hipFree(s->chunk_ord);
     if (s->codes) (void)hipFree(s->codes);
@@ -238,12 +213,8 @@ static void run_scan(ScanParams p, const Range &r, int kind, int metric, bool pr
     p.tile_rows = kind == kScanSmall ? kSmallRows : kind == kScanBf16 ? kBfRows : kMfmaRows;
     if (kind == kScanMfma32)
         launch_scan_mfma(p, metric, probe, st);
-    else if (kind == kScanBf16 && p.split == kHiSplit)
-        launch_scan_hi(p, metric, probe, st);
-    else if (kind == kScanBf16 && p.split == kMxSplit)
-        launch_scan_mx(p, metric, probe, st);
     else if (kind == kScanBf16)
-        launch_scan_bf16(p, metric, probe, kBfSplit, st);
+        launch_scan_hi(p, metric, probe, st);
     else
         launch_scan_small(p, metric, probe, st);
     MQVS_HIP(hipGetLastError());
@@ -463,17 +434,17 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
 
     // ---- kernel choice
     // faiss's formula branch is set by nq (kBlasThreshold); the bf16
-    // pre-filter serves both branches from kBf16MinNq queries up (its exact
-    // re-rank uses the branch's formula), the exact kernels the rest.  A
+    // pre-filter serves both branches (its exact re-rank uses the branch's
+    // formula) whenever the segment has its plane, the exact kernels the rest.  A
     // gathered (selective) scan prefers the bf16 kernel at any nq: its LDS-DMA
     // keeps whole tiles of scattered rows in flight and gathers efficiently up
     // to ~60% selectivity, while the VALU kernel's 128-B row slices only pay
     // below ~30% (tools/sweep.py --sels, profiles/r01)
     const bool mfma = fnq >= kBlasThreshold;
     const bool bf16_ok = seg->approx_ok && !force_exact && batch_mode == 0;
-    // (split 2 streams half the bytes of the fp32 rows, so it serves every
-    // batch size; the older splits start at kBf16MinNq)
-    bool bf16 = bf16_ok && nq >= (seg->split == kHiSplit ? 1 : kBf16MinNq);
+    // (the bf16 plane streams half the bytes of the fp32 rows, so it serves
+    // every batch size)
+    bool bf16 = bf16_ok;
     bool gather = false;
     if (selected >= 0) {
         if (gather_mode == 2)
@@ -588,17 +559,16 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
 
     float *bq = nullptr;
     if (kind == kScanBf16) {
-        // split planes of the query variants + per-query error bound
+        // bf16 plane of the query variants + per-query error bound
         const int64_t nvec = (int64_t)nq * maxv;
-        const size_t qe = (size_t)nvec * seg->dpad;
         bq = (float *)ws.bq.get(sizeof(float) * nq);
         p.rows_hi = seg->rows_hi;
         p.dpad = seg->dpad;
         p.thr = (const float *)ws.thr.get(sizeof(float) * nq);
         p.split = seg->split;
         // batch scans (kernels_p4.hip): per-wave candidate queues
-        if (seg->split == kHiSplit && nq > 128) p.p4_queue = ws.p4q.get(p4_queue_bytes());
-        if (seg->split == kHiSplit) {
+        if (nq > 128) p.p4_queue = ws.p4q.get(p4_queue_bytes());
+        {
             // [hi: maxv x vpad x dpad x 2 B][records: nvec x kMxRec floats]
             const int64_t vpad = round_up(nq, 16);
             const int64_t pvec = (int64_t)maxv * vpad;
@@ -609,35 +579,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
             launch_to_hi(qvars, nvec, d, qstride, seg->dpad, maxv, vpad, qhi, qrec, nullptr, s);
             p.q_vpad = vpad;
             p.q_hi = qhi;
-            launch_query_bound(p, metric, kHiSplit, seg->ynorm_max, qrec, seg->ynorm_max + 4, bq, s);
-        } else if (seg->split == kMxSplit) {
-            // [hi: maxv x vpad x dpad x 2 B][fp6: maxv x vpad x dpad/32 x 48 B]
-            // [scales: nvec x 2][records: nvec x kMxRec floats]
-            const int64_t vpad = round_up(nq, 16);
-            const int64_t pvec = (int64_t)maxv * vpad;
-            const size_t o_x6 = (size_t)round_up(pvec * seg->dpad * 2, 256);
-            const size_t o_sc = (size_t)round_up((int64_t)(o_x6 + (size_t)pvec * (seg->dpad / 32) * 48), 256);
-            const size_t o_rec = (size_t)round_up((int64_t)(o_sc + (size_t)nvec * 2), 256);
-            auto *base = (unsigned char *)ws.qhi.get(o_rec + sizeof(float) * kMxRec * (size_t)nvec);
-            auto *qhi = (uint16_t *)base;
-            auto *qx6 = base + o_x6;
-            auto *qsc = base + o_sc;
-            auto *qrec = (float *)(base + o_rec);
-            launch_to_mx(qvars, nvec, d, qstride, seg->dpad, maxv, vpad, false, qhi, qx6, qsc, qrec, nullptr, s);
-            p.q_vpad = vpad;
-            p.q_hi = qhi;
-            p.rows_x6 = seg->rows_x6;
-            p.rows_sc = seg->rows_sc;
-            p.q_x6 = qx6;
-            p.q_sc = qsc;
-            launch_query_bound(p, metric, kMxSplit, seg->ynorm_max, qrec, seg->ynorm_max + 4, bq, s);
-        } else {
-            uint16_t *qhi = (uint16_t *)ws.qhi.get(2 * sizeof(uint16_t) * qe);
-            launch_to_bf16(qvars, nvec, d, qstride, qhi, qhi + qe, seg->dpad, s);
-            p.rows_lo = seg->rows_lo;
-            p.q_hi = qhi;
-            p.q_lo = qhi + qe;
-            launch_query_bound(p, metric, kBfSplit, seg->ynorm_max, nullptr, nullptr, bq, s);
+            launch_query_bound(p, metric, seg->ynorm_max, qrec, seg->ynorm_max + 4, bq, s);
         }
         MQVS_HIP(hipGetLastError());
     }
@@ -1697,7 +1639,7 @@ int mqvs_set_batch_mode(int mode) {
 }
 
 int mqvs_set_prefilter(int split) {
-    if (split != kHiSplit && split != kBfSplit && split != kMxSplit) return MQVS_ERR_BAD_ARGUMENTS;
+    if (split != kHiSplit && split != 0) return MQVS_ERR_BAD_ARGUMENTS;
     g_prefilter.store(split);
     return MQVS_OK;
 }

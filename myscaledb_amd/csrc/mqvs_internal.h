@@ -21,11 +21,8 @@ struct mqvs_segment {
     float *rows = nullptr;
     float *norms = nullptr;          // |y|^2 per row (fvec_norm_L2sqr order)
     uint16_t *rows_hi = nullptr;     // bf16 rounding of the rows, [n][dpad]
-    uint16_t *rows_lo = nullptr;     // bf16 rounding of (row - hi), [n][dpad] (split 3)
-    uint8_t *rows_x6 = nullptr;      // fp6 cross plane [n][dpad/32][48 B] (split 6)
-    uint8_t *rows_sc = nullptr;      // E8M0 scales [n][2] (split 6)
     float *ynorm_max = nullptr;      // device scalar: max_r |y_r|; splits 2, 6: + [kMxRec] norm maxima at +16 B
-    int split = 0;                   // pre-filter planes built: 2, 3, 6, 0 = none
+    int split = 0;                   // pre-filter planes built: 2 (bf16 hi), 0 = none
     int64_t dpad = 0;
     bool approx_ok = false;          // bf16 pre-filter usable for this segment
     size_t plane_bytes = 0;          // HBM of the pre-filter planes (0: none built)
@@ -54,8 +51,7 @@ constexpr int64_t kCandMax = 1 << 20;     // candidate slots per query
 constexpr int kSmallRows = 256;      // rows per tile, VALU scan
 constexpr int kMfmaRows = 128;       // rows per tile, MFMA scan
 constexpr int kMfmaQ = 128;          // queries per tile, MFMA scan
-constexpr int kBfRows = 256;         // rows per tile, bf16 MFMA scan (kernels_bf16_scan.hip)
-constexpr int kBf16MinNq = 8;        // bf16 pre-filter from this batch size up (tools/sweep.py)
+constexpr int kBfRows = 256;         // rows per tile, bf16 pre-filter scans (kernels_hi.hip)
 // Internal metric id: raw faiss inner product (knn_inner_product: every
 // ip > -FLT_MAX enters the heap), used by mqvs_knn_raw only.  The operator
 // path (mqvs_search) applies searchWrapper's FLT_MIN cut instead.
@@ -156,21 +152,11 @@ struct ScanParams {
     int cand_cap;
     int num_qblocks;        // MFMA: query blocks
     // bf16 pre-filter path (nq >= 20): hi bf16 planes, row stride dpad
-    const uint16_t *rows_hi;  // [n][dpad]
-    const uint16_t *rows_lo;  // [n][dpad] bf16(x - hi) (split 3)
-    const uint16_t *q_hi;     // [nq][maxv][dpad]
-    const uint16_t *q_lo;     // [nq][maxv][dpad] (split 3)
+    const uint16_t *rows_hi;  // row-blocked [n/16][dpad/32][16][32] (launch_to_hi)
+    const uint16_t *q_hi;     // query variants, same layout, vector v q_vpad + j
     int64_t dpad;
-    // MX pre-filter (kernels_mx.hip): fp6 cross planes, [vec][dpad/32][48 B]
-    // (two 32-element e2m3 halves per 32 columns, layout in kernels_mx.hip),
-    // E8M0 scale per vector and half [vec][2]
-    const uint8_t *rows_x6;   // halves (bf16 residual, hi)
-    const uint8_t *rows_sc;
-    const uint8_t *q_x6;      // halves (hi, bf16 residual), plane vector v q_vpad + j
-    const uint8_t *q_sc;      // [nq][maxv][2]
-    int64_t q_vpad;           // nq rounded up to 16 (MX query planes)
-    int xcd_mode;             // MX scan workgroup -> XCD grouping (kernels_mx.hip)
-    int split;                // pre-filter planes of the scan: kHiSplit, kBfSplit, kMxSplit
+    int64_t q_vpad;           // nq rounded up to 16 (query planes)
+    int split;                // pre-filter planes of the scan: kHiSplit
     const float *thr;         // [nq] APPEND threshold on the approximate raw value
     // gather mode (selective PREWHERE): the scan walks positions of this list
     // of selected rows instead of rows; each chunk's rows are padded with -1 to
@@ -341,30 +327,19 @@ void launch_hamming_to_int(const int64_t *ids, float *dist, int64_t m, hipStream
 
 // bf16 pre-filter path (kernels_bf16.hip)
 constexpr int kBfK = 64;    // bf16 planes padded to a multiple of this
-constexpr int kBfSplit = 3; // hi*hi + hi*lo + lo*hi (see kernels_bf16_scan.hip)
-constexpr int kMxSplit = 6; // bf16 hi*hi + fp6-MX (hi*res + res*hi) (kernels_mx.hip)
-constexpr int kHiSplit = 2; // bf16 hi*hi only, bound from measured residual norms (kernels_hi.hip)
-constexpr int kMxRec = 8;   // floats per vector in the MX norm records (kernels_mx.hip)
-// dst_hi = bf16_rn(x); dst_lo (optional) = bf16_rn(x - hi)
-void launch_to_bf16(const float *src, int64_t rows, int d, int64_t src_stride, uint16_t *dst_hi,
-                    uint16_t *dst_lo, int64_t dpad, hipStream_t s);
+constexpr int kHiSplit = 2; // bf16 hi*hi, bound from measured residual norms (kernels_hi.hip)
+constexpr int kMxRec = 8;   // floats per vector in the norm records (launch_to_hi)
+// dst_hi = bf16_rn(x), row-major [rows][dpad] (the index's list planes)
+void launch_to_bf16(const float *src, int64_t rows, int d, int64_t src_stride, uint16_t *dst_hi, int64_t dpad,
+                    hipStream_t s);
 void launch_max_norm(const float *norms2, int64_t n, float *out_max, hipStream_t s);
-// split 6: qrec [nq][maxv][kMxRec] query-variant norms, yrec [kMxRec] segment maxima
-void launch_query_bound(const ScanParams &p, int metric, int split, const float *ynorm_max,
-                        const float *qrec, const float *yrec, float *bq, hipStream_t s);
-void launch_scan_bf16(const ScanParams &p, int metric, bool probe, int split, hipStream_t s);
-// MX pre-filter (kernels_mx.hip).  to_mx: bf16 hi plane [rows][dpad], fp6
-// cross plane, scales, and per-vector norm records (rec, optional) / their
-// maxima over the vectors (maxrec, optional, atomic); res_first: rows
-// (residual half first) vs queries (hi half first)
-// planes are row-blocked (16 vectors x 32 columns contiguous, kernels_mx.hip);
-// source vector v goes to plane vector (v % vgroup) vpad + v / vgroup
-void launch_to_mx(const float *src, int64_t rows, int d, int64_t src_stride, int64_t dpad, int64_t vgroup,
-                  int64_t vpad, bool res_first, uint16_t *hi, uint8_t *x6, uint8_t *sc, float *rec, float *maxrec,
-                  hipStream_t s);
-void launch_scan_mx(const ScanParams &p, int metric, bool probe, hipStream_t s);
-// split 2 (kernels_hi.hip): row-blocked bf16 hi plane as the MX one + records
-// [|h|, |r|, -, -, -, -, |x|] per vector (rec) / maxima (maxrec, atomic)
+// qrec [nq][maxv][kMxRec] query-variant norm records, yrec [kMxRec] segment maxima
+void launch_query_bound(const ScanParams &p, int metric, const float *ynorm_max, const float *qrec,
+                        const float *yrec, float *bq, hipStream_t s);
+// split 2 (kernels_hi.hip): row-blocked bf16 hi plane (16 vectors x 32
+// columns contiguous; source vector v goes to plane vector
+// (v % vgroup) vpad + v / vgroup) + records [|h|, |r|, -, -, -, -, |x|] per
+// vector (rec) / maxima (maxrec, atomic)
 void launch_to_hi(const float *src, int64_t rows, int d, int64_t src_stride, int64_t dpad, int64_t vgroup,
                   int64_t vpad, uint16_t *hi, float *rec, float *maxrec, hipStream_t s);
 void launch_scan_hi(const ScanParams &p, int metric, bool probe, hipStream_t s);

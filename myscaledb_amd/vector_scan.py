@@ -415,8 +415,8 @@ def set_scratch_budget(nbytes: int) -> int:
 
 def set_prefilter(split: int):
     """Pre-filter planes of segments created after the call: 2 = bf16 hi
-    plane only (default), 6 = bf16 hi + block-scaled fp6 cross plane, 3 = bf16
-    hi + lo planes (mqvs_set_prefilter).  All return the same bits."""
+    plane (default), 0 = none -- batches then run the exact fp32 MFMA path
+    (mqvs_set_prefilter).  Both return the same bits."""
     check(lib.mqvs_set_prefilter(int(split)))
 
 

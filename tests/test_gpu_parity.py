@@ -168,11 +168,13 @@ def test_gpu_vs_oracle_fp32_batch_mode(mq, cfg):
 
 
 @pytest.mark.parametrize("cfg", BATCH, ids=[c[0] for c in BATCH])
-def test_gpu_vs_oracle_split3_prefilter(mq, cfg):
-    """nq >= 8 through the split-3 pre-filter (bf16 hi + lo planes, three bf16
-    MFMAs; the default is split 6, bf16 + fp6-MX cross terms): same bits."""
+def test_gpu_vs_oracle_without_planes(mq, cfg):
+    """Segments built without the bf16 plane (mqvs_set_prefilter(0), as when
+    the plane does not fit in HBM): nq < 20 on the VALU kernel, nq >= 20 on the
+    fp32 MFMA kernel over every row; the default (split 2) is the bf16
+    pre-filter + exact re-rank.  Same bits."""
     from myscaledb_amd.vector_scan import set_prefilter
-    set_prefilter(3)
+    set_prefilter(0)
     try:
         run_parity(mq, cfg)
     finally:
@@ -195,25 +197,21 @@ def _wide_range_part(seed, n, d, nq, near):
     return rows, q
 
 
-@pytest.mark.parametrize("split", [6, 3])
 @pytest.mark.parametrize("metric", ["L2", "IP", "Cosine"])
-@pytest.mark.parametrize("nq", [12, 40])
-def test_prefilter_wide_dynamic_range(mq, split, metric, nq):
+@pytest.mark.parametrize("nq", [12, 40, 200])
+def test_prefilter_wide_dynamic_range(mq, metric, nq):
     """The pre-filter bound holds on adversarial magnitudes: bit-identical to
     the oracle (the bound is computed from measured quantisation norms, so
     poorly represented data only widens the candidate window)."""
-    from myscaledb_amd.vector_scan import set_prefilter
     rows, q = _wide_range_part(1000 + nq, 6000, 96, nq, near=300)
     m = O.METRICS[metric]
     ids_o, dist_o = O.vector_scan(rows, q, 50, m, 1024, fast=True)
-    set_prefilter(split)
+    seg = mq.VectorScanSegment.from_rows(rows, metric=metric, granule=1024)
     try:
-        seg = mq.VectorScanSegment.from_rows(rows, metric=metric, granule=1024)
         ids_g, dist_g = seg.search(q, 50, metric)
-        seg.free()
     finally:
-        set_prefilter(2)
-    assert_bitwise(ids_g, dist_g, ids_o, dist_o, f"wide split={split} {metric} nq={nq}")
+        seg.free()
+    assert_bitwise(ids_g, dist_g, ids_o, dist_o, f"wide {metric} nq={nq}")
 
 
 def run_parity(mq, cfg):
@@ -416,24 +414,26 @@ def test_merge_parts_mode_matches_oracle(mq, metric):
 
 def test_path_selection(mq):
     """Default (bf16-hi planes, split 2): the bf16 pre-filter serves every
-    batch size (path 2; it streams half the bytes of the fp32 rows).  Split-6 /
-    split-3 segments: nq < 8 VALU direct formula (path 0), nq >= 8 path 2.
-    Batch mode 1: exact kernels only (VALU below 20, fp32 MFMA from 20)."""
+    batch size (path 2; it streams half the bytes of the fp32 rows).  A
+    segment without planes (mqvs_set_prefilter(0)): VALU direct formula below
+    nq 20 (path 0), fp32 MFMA from 20 (path 1).  Batch mode 1: exact kernels
+    only, the same split."""
     from myscaledb_amd import _lib
     from myscaledb_amd.vector_scan import set_batch_mode, set_prefilter
     rows = O.generate(3, 1, 0, 4000, 64)
     seg = mq.VectorScanSegment.from_rows(rows, metric="L2", granule=512)
-    set_prefilter(6)
+    set_prefilter(0)
     try:
         seg6 = mq.VectorScanSegment.from_rows(rows, metric="L2", granule=512)
     finally:
         set_prefilter(2)
     try:
+        assert seg6.info()["prefilter"] == 0 and seg.info()["prefilter"] == 2
         for nq in (1, 7, 8, 20):
             seg.search(O.generate(4, 1, 0, nq, 64), 10)
             st = _lib.last_search_stats()
             assert st["path"] == 2 and st["prefilter"] == 2, nq
-        for nq, want in ((7, 0), (8, 2), (19, 2), (20, 2)):
+        for nq, want in ((7, 0), (8, 0), (19, 0), (20, 1)):
             seg6.search(O.generate(4, 1, 0, nq, 64), 10)
             assert _lib.last_search_stats()["path"] == want, nq
         set_batch_mode(1)
@@ -463,26 +463,20 @@ def test_cosine_slow_normalisation_cycle(mq, nq):
     assert_bitwise(ids_g, dist_g, ids_o, dist_o, f"slow cycle nq={nq}")
 
 
-@pytest.mark.parametrize("split", [6, 3])
-def test_prefilter_no_exact_fallback(mq, split):
-    """Both pre-filters keep the survivors within the re-rank's capacity on
+def test_prefilter_no_exact_fallback(mq):
+    """The pre-filter keeps the survivors within the re-rank's capacity on
     ordinary data (no silent fallback to the exact fp32 path: rescans 0)."""
     from myscaledb_amd import _lib
-    from myscaledb_amd.vector_scan import set_prefilter
-    set_prefilter(split)
-    try:
-        for metric, mode in (("L2", 1), ("IP", 1), ("Cosine", 1)):
-            rows = O.generate(11, mode, 0, 30000, 256)
-            seg = mq.VectorScanSegment.from_rows(rows, metric=metric, granule=8192)
-            try:
-                for nq in (8, 64, 300):
-                    seg.search(O.generate(12, mode, 0, nq, 256), 100)
-                    st = _lib.last_search_stats()
-                    assert st["path"] == 2 and st["rescans"] == 0, (metric, nq, st)
-            finally:
-                seg.free()
-    finally:
-        set_prefilter(2)
+    for metric, mode in (("L2", 1), ("IP", 1), ("Cosine", 1)):
+        rows = O.generate(11, mode, 0, 30000, 256)
+        seg = mq.VectorScanSegment.from_rows(rows, metric=metric, granule=8192)
+        try:
+            for nq in (1, 8, 64, 300):
+                seg.search(O.generate(12, mode, 0, nq, 256), 100)
+                st = _lib.last_search_stats()
+                assert st["path"] == 2 and st["rescans"] == 0, (metric, nq, st)
+        finally:
+            seg.free()
 
 
 @pytest.mark.parametrize("nq", [3, 12, 40])
