@@ -179,6 +179,17 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
 
     // per-lane query constants: the four query rows of this wave's query
     // pieces (variant cycles), the four query columns of its accumulators
+    // Cosine variants: with the ordinal planes (p.q_ord, built when every
+    // query's chain fits them) a chunk's queries are ONE contiguous plane,
+    // chosen per item; otherwise each lane picks its query's variant.
+    int om0 = 0, oln = 1;
+    bool ordm = false;
+    if (p.q_ord_desc) {
+        om0 = __builtin_amdgcn_readfirstlane(p.q_ord_desc[0]);
+        oln = __builtin_amdgcn_readfirstlane(p.q_ord_desc[1]);
+        ordm = __builtin_amdgcn_readfirstlane(p.q_ord_desc[2]) != 0;
+    }
+    const bool pervar = p.maxv > 1 && !ordm;
     int qmu[4], qlam[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -186,7 +197,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
         if (j >= p.nq) j = 0;
         qmu[i] = 0;
         qlam[i] = 1;
-        if (p.maxv > 1) {
+        if (pervar) {
             qmu[i] = p.qmu[j];
             qlam[i] = p.qlam[j];
         }
@@ -271,7 +282,8 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
     // re-reads piece 0 (discarded).
     uint32_t roff[4], qoff[4];
     const unsigned char *rbase = nullptr;  // plane block of the item's first row (uniform)
-    const unsigned char *const qplane = reinterpret_cast<const unsigned char *>(p.q_hi);
+    const unsigned char *qplane = reinterpret_cast<const unsigned char *>(ordm ? p.q_ord : p.q_hi);
+    const uint64_t pstride = (uint64_t)(p.q_vpad >> 4) * blk;  // bytes of one ordinal plane
     uint32_t noff = 0;                      // L2: this lane's row norm, relative to the item's first row
     const unsigned char *nbase = nullptr;
     bool first_src = true;                  // query offsets: per item only for cosine variants
@@ -288,13 +300,17 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
             const int pc = w + 4 * i;
             roff[i] = (ir0 + pc * 16 < ir1 ? (uint32_t)pc * blk : 0u) + lc;
         }
-        if (p.maxv > 1 || first_src) {
+        if (ordm) {
+            const int pl = iord < om0 ? iord : om0 + (iord - om0) % oln;
+            qplane = reinterpret_cast<const unsigned char *>(p.q_ord) + (uint64_t)pl * pstride;
+        }
+        if (pervar || first_src) {
 #pragma unroll
             for (int i = 0; i < 4; ++i) {
                 int j = q0 + (w + 4 * i) * 16 + (ln >> 2);
                 if (j >= p.nq) j = 0;
                 int var = 0;
-                if (p.maxv > 1 && (DIAG & 512) == 0) {
+                if (pervar && (DIAG & 512) == 0) {
                     const int mu = qmu[i], lam = qlam[i];
                     var = iord < mu ? iord : mu + (iord - mu) % lam;
                 }
@@ -602,6 +618,84 @@ size_t p4_queue_bytes() {
         MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     }
     return (size_t)cus * 4 * kP4QueueCap * sizeof(u32x4);
+}
+
+// Cosine ordinal planes.  Query j uses variant v_j(o) = o < mu_j ? o :
+// mu_j + (o - mu_j) % lam_j at chunk ordinal o.  With m0 = max mu_j and
+// L = lcm(lam_j), every o >= m0 with (o - m0) % L = c uses the variants of
+// o' = m0 + c, so m0 + L planes hold every chunk's queries contiguously
+// (plane pl = o for o < m0, m0 + (o - m0) % L after).  desc = {m0, L, ok}.
+__global__ void k_ord_desc(const int *qmu, const int *qlam, int nq, int pcap, int *desc) {
+    __shared__ int smu;
+    __shared__ unsigned long long slam;
+    if (threadIdx.x == 0) {
+        smu = 0;
+        slam = 0;
+    }
+    __syncthreads();
+    int mu = 0;
+    unsigned long long lm = 0;
+    for (int j = threadIdx.x; j < nq; j += blockDim.x) {
+        mu = max(mu, qmu[j]);
+        const int l = qlam[j];
+        lm |= (l >= 1 && l <= 63) ? (1ull << l) : 1ull;  // (bit 0: a cycle too long to serve)
+    }
+    atomicMax(&smu, mu);
+    atomicOr(&slam, lm);
+    __syncthreads();
+    if (threadIdx.x != 0) return;
+    long long L = 1;
+    bool ok = (slam & 1ull) == 0;
+    for (int l = 2; l < 64 && ok; ++l) {
+        if (!((slam >> l) & 1ull)) continue;
+        long long a = L, b = l;
+        while (b) {
+            const long long t = a % b;
+            a = b;
+            b = t;
+        }
+        L = L / a * l;
+        ok = L <= pcap;
+    }
+    ok = ok && (long long)smu + L <= pcap;
+    desc[0] = smu;
+    desc[1] = ok ? (int)L : 1;
+    desc[2] = ok ? 1 : 0;
+}
+
+// one thread per 16 B of a plane vector's stage: (plane, vector, stage, quarter)
+__global__ void k_ord_gather(const uint16_t *qhi, uint16_t *qord, const int *qmu, const int *qlam, int nq,
+                             int64_t vpad, int nst, const int *desc) {
+    if (!desc[2]) return;
+    const int np = desc[0] + desc[1];
+    const int64_t per_vec = (int64_t)nst * 4, per_plane = vpad * per_vec;
+    const int64_t total = (int64_t)np * per_plane;
+    const unsigned char *src = reinterpret_cast<const unsigned char *>(qhi);
+    unsigned char *dst = reinterpret_cast<unsigned char *>(qord);
+    for (int64_t e = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; e < total; e += (int64_t)gridDim.x * blockDim.x) {
+        const int pl = (int)(e / per_plane);
+        const int64_t rem = e - (int64_t)pl * per_plane;
+        const int64_t j = rem / per_vec;
+        const int r2 = (int)(rem - j * per_vec), st = r2 >> 2, qt = r2 & 3;
+        int v = 0;
+        if (j < nq) {
+            const int mu = qmu[j], lam = qlam[j];
+            v = pl < mu ? pl : mu + (pl - mu) % lam;
+        }
+        const int64_t us = (int64_t)v * vpad + j, ud = (int64_t)pl * vpad + j;
+        const int64_t os = (((us >> 4) * nst + st) << 10) + (us & 15) * 64 + qt * 16;
+        const int64_t od = (((ud >> 4) * nst + st) << 10) + (ud & 15) * 64 + qt * 16;
+        *reinterpret_cast<u32x4 *>(dst + od) = *reinterpret_cast<const u32x4 *>(src + os);
+    }
+}
+
+void launch_ord_planes(const uint16_t *q_hi, uint16_t *q_ord, int *desc, const int *qmu, const int *qlam, int nq,
+                       int64_t vpad, int64_t dpad, int pcap, hipStream_t s) {
+    hipLaunchKernelGGL(k_ord_desc, dim3(1), dim3(256), 0, s, qmu, qlam, nq, pcap, desc);
+    const int64_t total = (int64_t)pcap * vpad * (dpad / kP4HiK) * 4;
+    const int64_t blocks = std::min<int64_t>((total + 255) / 256, 8192);
+    hipLaunchKernelGGL(k_ord_gather, dim3((unsigned)std::max<int64_t>(blocks, 1)), dim3(256), 0, s, q_hi, q_ord, qmu,
+                       qlam, nq, vpad, (int)(dpad / kP4HiK), desc);
 }
 
 // true when the launch was taken (batch APPEND, contiguous rows, identity

@@ -45,7 +45,7 @@ struct Workspace {
     hipEvent_t seg_ev[kSegEv] = {};  // per main-scan segment: start, end
     DevBuf queries, qvars, qnorms, qmu, qlam, status, filter, exists, ord, probe, tau, count, cand,
         overflow, out_ids, out_dist, misc, qhi, bq, thr, cand2, count2, gcount, goff, glist, large, sticky, surv,
-        recs, flags, p4q;
+        recs, flags, p4q, qord;
     int *host_flags = nullptr;  // pinned
     void init() {
         if (stream) return;
@@ -58,7 +58,7 @@ struct Workspace {
         DevBuf *all[] = {&queries, &qvars, &qnorms, &qmu,  &qlam,   &status,  &filter,   &exists, &ord,
                          &probe,   &tau,   &count,  &cand, &overflow, &out_ids, &out_dist, &misc,
                          &qhi, &bq, &thr, &cand2, &count2, &gcount, &goff, &glist, &large, &sticky, &surv,
-                         &recs, &flags, &p4q};
+                         &recs, &flags, &p4q, &qord};
         for (auto *b : all) b->release();
         if (host_flags) (void)hipHostFree(host_flags);
         host_flags = nullptr;
@@ -580,6 +580,19 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
             p.q_vpad = vpad;
             p.q_hi = qhi;
             launch_query_bound(p, metric, seg->ynorm_max, qrec, seg->ynorm_max + 4, bq, s);
+            // cosine batches: a chunk's query variants as one contiguous plane
+            // (kernels_p4.hip; up to 32 planes within the scratch budget; the
+            // scan keeps per-query variant reads when the chains need more)
+            const int64_t plane = vpad * seg->dpad * 2;
+            const int pcap = (int)std::min<int64_t>({kP4OrdPlanesMax, maxv, (int64_t)(scratch_budget() / plane)});
+            if (p.p4_queue && metric == MQVS_METRIC_COSINE && maxv > 1 && pcap >= 2 && tune_int("MQVS_P4_ORD", 1)) {
+                const size_t pb = (size_t)round_up((int64_t)pcap * plane, 256);
+                auto *ob = (unsigned char *)ws.qord.get(pb + 256);
+                auto *desc = (int *)(ob + pb);
+                launch_ord_planes(qhi, (uint16_t *)ob, desc, qmu, qlam, nq, vpad, seg->dpad, pcap, s);
+                p.q_ord = (const uint16_t *)ob;
+                p.q_ord_desc = desc;
+            }
         }
         MQVS_HIP(hipGetLastError());
     }

@@ -156,6 +156,10 @@ struct ScanParams {
     const uint16_t *q_hi;     // query variants, same layout, vector v q_vpad + j
     int64_t dpad;
     int64_t q_vpad;           // nq rounded up to 16 (query planes)
+    // cosine ordinal planes (kernels_p4.hip): plane pl holds every query's
+    // variant for chunk ordinals of class pl; desc = {m0, lam, ok}
+    const uint16_t *q_ord;
+    const int *q_ord_desc;
     int split;                // pre-filter planes of the scan: kHiSplit
     const float *thr;         // [nq] APPEND threshold on the approximate raw value
     // gather mode (selective PREWHERE): the scan walks positions of this list
@@ -346,6 +350,11 @@ void launch_scan_hi(const ScanParams &p, int metric, bool probe, hipStream_t s);
 // batch APPEND scan at one wave per SIMD (kernels_p4.hip): false when the
 // scan's shape is not served (gather lists, chunk-ordinal tables, no queue)
 bool launch_scan_p4(const ScanParams &p, int metric, hipStream_t s);
+// cosine ordinal planes for the batch kernel: at most pcap planes, built on
+// the device from q_hi / qmu / qlam (desc[2] = 0 when the chains need more)
+constexpr int kP4OrdPlanesMax = 32;
+void launch_ord_planes(const uint16_t *q_hi, uint16_t *q_ord, int *desc, const int *qmu, const int *qlam, int nq,
+                       int64_t vpad, int64_t dpad, int pcap, hipStream_t s);
 size_t p4_queue_bytes();  // p4_queue workspace for the current device
 int take_batch_kernel_flag();  // 1 when a main scan since the last call ran kernels_p4 (then cleared)
 void launch_probe_select_approx(const float *probe, int64_t P, int64_t ld, int nq, int k,

@@ -111,3 +111,32 @@ def test_batch_kernel_many_candidates(mq):
     ids_g, dist_g = seg.search(q, k, "L2")
     seg.free()
     assert_bitwise(ids_g, dist_g, ids_o, dist_o, "all ties")
+
+
+@pytest.mark.parametrize("slow,budget", [(False, None), (True, None), (True, 1 << 20)])
+def test_batch_kernel_cosine_ordinal_planes(mq, slow, budget):
+    """Cosine batches read a chunk's query variants as one contiguous ordinal
+    plane when every query's re-normalisation chain fits the planes (max mu +
+    lcm of the cycle lengths, at most 32 within the scratch budget).  A query
+    whose chain first repeats at step 16 (generator mode 2, seed 12, d 256,
+    query 259) needs 16 planes; under a 1 MiB budget only 9 fit and the scan
+    keeps per-query variant reads.  Every case must equal the oracle's
+    per-chunk re-normalisation (VIWithDataPart.h:358) bit for bit on 40
+    chunks."""
+    from myscaledb_amd import _lib
+    from myscaledb_amd.vector_scan import set_scratch_budget
+    q = O.generate(12, 2, 0, 300, 256)
+    queries = np.concatenate([q[259:260], q[:199]]) if slow else q[:200]
+    rows = O.generate(77, 2, 0, 40960, 256)
+    ids_o, dist_o = O.vector_scan(rows, queries, 20, O.COSINE, 1024, fast=True)
+    seg = mq.VectorScanSegment.from_rows(rows, metric="Cosine", granule=1024)
+    old = set_scratch_budget(budget) if budget else None
+    try:
+        ids_g, dist_g = seg.search(queries, 20, "Cosine")
+        st = _lib.last_search_stats()
+    finally:
+        if old:
+            set_scratch_budget(old)
+        seg.free()
+    assert st["batch_kernel"] == 1, st
+    assert_bitwise(ids_g, dist_g, ids_o, dist_o, f"ordinal planes slow={slow}")
