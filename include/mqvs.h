@@ -483,6 +483,13 @@ int mqvs_set_prefilter(int split);
  * formula (faiss's nx >= 20 branch) and return the same bits.  Returns the
  * previous value; 0 leaves it unchanged. */
 size_t mqvs_set_scratch_budget(size_t bytes);
+/* Achievable HBM read rate of this device (a bench utility: the measured
+ * denominator of the scan's HBM fraction).  A STREAM-like read
+ * sweep -- every lane loads 16 B, 4 loads in flight, grid-stride, 8
+ * workgroups of 256 per CU -- over a fresh device buffer of `bytes` (>= 1 MiB;
+ * >= 4 GiB defeats the 256 MiB Infinity Cache), best of `reps` timed passes
+ * after one warm-up: *gbs = bytes / best time (1e9 B/s), *best_ms (optional). */
+int mqvs_measure_read_bandwidth(size_t bytes, int32_t reps, double *gbs, double *best_ms);
 
 #ifdef __cplusplus
 }

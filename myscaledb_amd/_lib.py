@@ -41,7 +41,7 @@ SYMBOLS = [
     "mqvs_segment_generate", "mqvs_segment_free", "mqvs_segment_info", "mqvs_segment_prefilter", "mqvs_segment_rows",
     "mqvs_search", "mqvs_search_ex", "mqvs_knn_raw", "mqvs_rerank", "mqvs_merge_shards", "mqvs_generate_device",
     "mqvs_last_search_stats", "mqvs_set_timing", "mqvs_set_batch_mode", "mqvs_set_gather_mode", "mqvs_set_prefilter",
-    "mqvs_set_scratch_budget",
+    "mqvs_set_scratch_budget", "mqvs_measure_read_bandwidth",
     "mqvs_index_build", "mqvs_index_free", "mqvs_index_info", "mqvs_index_search", "mqvs_index_last_stats",
     "mqvs_segment_create_binary", "mqvs_search_binary", "mqvs_knn_binary_raw",
     "mqvs_segment_create_from_column", "mqvs_async_check",
@@ -134,6 +134,7 @@ def _load():
         "mqvs_set_batch_mode": ([ctypes.c_int], ctypes.c_int),
         "mqvs_set_gather_mode": ([ctypes.c_int], ctypes.c_int),
         "mqvs_set_scratch_budget": ([ctypes.c_size_t], ctypes.c_size_t),
+        "mqvs_measure_read_bandwidth": ([ctypes.c_size_t, ctypes.c_int32, P, P], ctypes.c_int),
         "mqvs_set_prefilter": ([ctypes.c_int], ctypes.c_int),
         "mqvs_index_build": ([P, ctypes.c_char_p, ctypes.c_char_p, P], ctypes.c_int),
         "mqvs_index_free": ([P], ctypes.c_int),

@@ -724,7 +724,7 @@ static bool launch_p4_t(ScanParams p, hipStream_t s) {
     const int slots = per_xcd / p.num_qblocks * p.num_qblocks;
     auto *q = reinterpret_cast<u32x4 *>(p.p4_queue);
     const dim3 grid((unsigned)(8 * per_xcd));
-    const int tmap = tune_int("MQVS_P4_MAP", 0);
+    const int tmap = tune_int("MQVS_P4_MAP", 1);
     if constexpr (kDebugTuning) {
         // measurement builds: ring depth and decomposition variants
         const int nbuf = tune_int("MQVS_P4_NBUF", 4);

@@ -1657,6 +1657,21 @@ int mqvs_set_prefilter(int split) {
     return MQVS_OK;
 }
 
+int mqvs_measure_read_bandwidth(size_t bytes, int32_t reps, double *gbs, double *best_ms) {
+    return guarded([&] {
+        if (!gbs || bytes < ((size_t)1 << 20) || reps < 1) fail(MQVS_ERR_BAD_ARGUMENTS, "bad read-sweep arguments");
+        hipStream_t s = nullptr;
+        MQVS_HIP(hipStreamCreateWithFlags(&s, hipStreamNonBlocking));
+        try {
+            *gbs = measure_read_sweep(bytes, reps, s, best_ms);
+        } catch (...) {
+            (void)hipStreamDestroy(s);
+            throw;
+        }
+        MQVS_HIP(hipStreamDestroy(s));
+    });
+}
+
 size_t mqvs_set_scratch_budget(size_t bytes) {
     if (bytes == 0) return g_scratch_budget.load();
     return g_scratch_budget.exchange(std::max<size_t>(bytes, (size_t)1 << 20));

@@ -494,6 +494,7 @@ static int guarded(F &&f) {
 
 // mqvs.hip services used by the index path
 hipStream_t thread_stream(int device);
+double measure_read_sweep(size_t bytes, int reps, hipStream_t s, double *best_ms);
 size_t scratch_budget();  // bytes per scratch buffer of one call (mqvs_set_scratch_budget)
 // FLAT search of a segment (MergeTreeVSManager::vectorScanWithoutIndex);
 // metric may be kMetricIpRaw (faiss knn_inner_product contract)

@@ -413,6 +413,14 @@ def set_scratch_budget(nbytes: int) -> int:
     return int(lib.mqvs_set_scratch_budget(int(nbytes)))
 
 
+def measure_read_bandwidth(nbytes: int = 8 << 30, reps: int = 5):
+    """Achievable HBM read rate (GB/s) of the current device by a STREAM-like
+    read sweep (mqvs_measure_read_bandwidth); returns (gbs, best_ms)."""
+    g, m = ctypes.c_double(), ctypes.c_double()
+    check(lib.mqvs_measure_read_bandwidth(int(nbytes), int(reps), ctypes.byref(g), ctypes.byref(m)))
+    return g.value, m.value
+
+
 def set_prefilter(split: int):
     """Pre-filter planes of segments created after the call: 2 = bf16 hi
     plane (default), 0 = none -- batches then run the exact fp32 MFMA path
