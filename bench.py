@@ -22,7 +22,9 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, f32 MFMA (= VALU) dense p
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md, bf16 MFMA dense peak (no sparsity)
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md, HBM3E spec peak
 ROOT = os.path.dirname(os.path.abspath(__file__))
-PMC_DEFAULT = "profiles/r02/pmc_traffic.json"
+PMC_DEFAULT = "profiles/r03/pmc_traffic.json"
+PMC_NQ1_DEFAULT = "profiles/r03/pmc_nq1.json"
+BLAS_RISK_DEFAULT = "profiles/r03/blas_order_risk.json"
 
 
 def seg_dpad(d):
@@ -40,7 +42,7 @@ def parse():
     ap.add_argument("--nq", type=int, default=1000)
     ap.add_argument("--k", type=int, default=100)
     ap.add_argument("--metric", default="Cosine")
-    ap.add_argument("--mode", type=int, default=2, help="0 exact ints, 1 gauss, 2 gaussian mixture (4096 centres, noise 0.25), 3 hard mixture (65536 centres, noise 1.0)")
+    ap.add_argument("--mode", type=int, default=1, help="0 exact ints, 1 gauss, 2 gaussian mixture (4096 centres, noise 0.25), 3 hard mixture (65536 centres, noise 1.0)")
     ap.add_argument("--granule", type=int, default=8192)
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu", action="store_true")
@@ -49,6 +51,10 @@ def parse():
     ap.add_argument("--pmc", default=None, help="rocprofv3 PMC summary JSON for roofline.traffic")
     ap.add_argument("--no-index", action="store_true", help="skip the index (configs[2]) leg")
     ap.add_argument("--no-configs", action="store_true", help="skip the configs[3] shard / configs[4] hybrid leg")
+    ap.add_argument("--no-config1-points", action="store_true",
+                    help="skip the extra configs[1] points (L2 metric, second distribution)")
+    ap.add_argument("--read-sweep-gib", type=float, default=8.0,
+                    help="buffer of the HBM read sweep (mqvs_measure_read_bandwidth); 0 = skip")
     ap.add_argument("--index-settings", default="nprobe=2;nprobe=3;nprobe=4;nprobe=8",
                     help="';'-separated mqvs_index_search parameter strings timed by the index leg")
     ap.add_argument("--index-hard-mode", type=int, default=3,
@@ -332,6 +338,27 @@ def index_leg(mq, seg, args):
     return out
 
 
+def _pmc_kernel(path, want, nq=None, sum_all=False):
+    """The per-search PMC figures of kernel `want` from a committed
+    tools/pmc_traffic.py summary (None when absent or for another nq).
+    sum_all: the HBM bytes of every matching template (probe + main scan)."""
+    if not os.path.exists(path):
+        return None
+    with open(path) as f:
+        pmc = json.load(f)
+    if nq is not None and pmc.get("nq") not in (None, nq):
+        return None
+    hits = [(name, k) for name, k in pmc.get("kernels", {}).items() if want in name and "hbm_bytes_per_search" in k]
+    if not hits:
+        return None
+    name, kinfo = max(hits, key=lambda h: h[1]["hbm_bytes_per_search"])
+    out = dict(kinfo, kernel=name, source=os.path.relpath(path, ROOT))
+    if sum_all:
+        out["hbm_bytes_per_search"] = sum(k["hbm_bytes_per_search"] for _, k in hits)
+        out["kernel"] = " + ".join(n for n, _ in hits)
+    return out
+
+
 def roofline(st, main_ms, nq, d, args):
     """The dominant kernel's roofline from one search's stats: all main-scan
     launches of the search, timed with HIP events on the search stream."""
@@ -339,12 +366,14 @@ def roofline(st, main_ms, nq, d, args):
     dp = seg_dpad(d)
     sec = main_ms * 1e-3
     pf = st.get("prefilter", 0)
+    want = None
     if st["path"] == 2 and pf == 2:
-        # bf16-hi pre-filter (kernels_hi.hip): ONE bf16 MFMA product per fp32
-        # MAC over the row-blocked bf16 plane (2 B per element)
+        # bf16-hi pre-filter (kernels_hi.hip / kernels_p4.hip): ONE bf16 MFMA
+        # product per fp32 MAC over the row-blocked bf16 plane (2 B per element)
         plane = 2.0 * rows * dp
         flop = 2.0 * nq * rows * dp
         if nq <= 64:
+            want = "k_scan_hi_reg" if nq <= 32 else "k_scan_hi<"
             kern = "k_scan_hi_reg (bf16 16x16x32, operands straight from HBM into registers)" if nq <= 32 else \
                 "k_scan_hi<metric,APPEND,WQ=1,QB=2,NBUF=3>"
             roof = {"bound": "hbm", "kernel": kern, "achieved": round(plane / sec / 1e9, 1), "peak": HBM_PEAK_GBS,
@@ -353,9 +382,13 @@ def roofline(st, main_ms, nq, d, args):
         else:
             qt = 256 if nq > 128 else 128
             stream = 2.0 * rows * dp * -(-nq // qt) + 2.0 * nq * dp * -(-rows // 256)
-            kern = ("k_scan_hi_pp<metric,NBUF=4> (persistent ping-pong, bf16 32x32x16)"
-                    if st["path"] == 2 and args.metric != "L2" else
-                    "k_scan_hi<metric,APPEND,WQ=2,QB=4,NBUF=4> (bf16 32x32x16)")
+            if st.get("batch_kernel"):
+                want = "k_scan_p4"
+                kern = ("k_scan_p4<metric,NBUF=4> (one wave per SIMD, 128x128 rows x queries per wave, 256 AGPR "
+                        "accumulators, bf16 32x32x16, LDS-DMA ring)")
+            else:
+                want = "k_scan_hi<"
+                kern = "k_scan_hi<metric,APPEND,WQ=2,QB=4,NBUF=4> (bf16 32x32x16)"
             roof = {"bound": "mfma", "kernel": kern,
                     "achieved": round(flop / sec / 1e12, 2), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
                     "frac": round(flop / sec / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4), "traffic": None,
@@ -366,23 +399,6 @@ def roofline(st, main_ms, nq, d, args):
                     "l2_to_lds_bytes": stream}
         roof["per_search"] = {"rows": rows, "flop": flop, "plane_bytes": plane, "ms": round(main_ms, 3),
                               "launches": st["segments"]}
-    elif st["path"] == 2 and pf == 6:
-        # bf16 + fp6-MX pre-filter (kernels_mx.hip): 2 bf16 32x32x16 + 1 MX
-        # 32x32x64 (the cycles of one bf16 32x32x16) per 32-column stage
-        alg = 2.0 * nq * rows * d
-        flop = 1.5 * alg
-        roof = {"bound": "mfma", "kernel": "k_scan_mx<metric,APPEND,WQ=2,QB=4,VAR=3>",
-                "achieved": round(flop / sec / 1e12, 2), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(flop / sec / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                "flop_definition": "bf16-cycle-equivalent MFMA flops = 1.5 * 2*nq*rows*d",
-                "per_search": {"rows": rows, "flop": flop, "ms": round(main_ms, 3), "launches": st["segments"]}}
-    elif st["path"] == 2:
-        flop = 3.0 * 2.0 * nq * rows * d
-        roof = {"bound": "mfma", "kernel": "k_scan_bf16<metric,APPEND,split=3>",
-                "achieved": round(flop / sec / 1e12, 2), "peak": BF16_MFMA_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(flop / sec / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4), "traffic": None,
-                "flop_definition": "executed bf16 MFMA flops = 3 x 2*nq*rows*d",
-                "per_search": {"rows": rows, "flop": flop, "ms": round(main_ms, 3), "launches": st["segments"]}}
     elif st["path"] == 1:
         flop = 2.0 * nq * rows * d
         roof = {"bound": "mfma", "kernel": "k_scan_mfma (fp32, APPEND)", "achieved": round(flop / sec / 1e12, 2),
@@ -394,23 +410,18 @@ def roofline(st, main_ms, nq, d, args):
         roof = {"bound": "hbm", "kernel": "k_scan_small (APPEND)", "achieved": round(byts / sec / 1e9, 1),
                 "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": round(byts / sec / 1e9 / HBM_PEAK_GBS, 4),
                 "traffic": None, "per_search": {"rows": rows, "bytes": byts, "ms": round(main_ms, 3)}}
-    pmc_path = args.pmc or os.path.join(ROOT, PMC_DEFAULT)
-    if st["path"] == 2 and os.path.exists(pmc_path):
+    pm = _pmc_kernel(args.pmc or os.path.join(ROOT, PMC_DEFAULT), want, nq) if want else None
+    if pm:
         # HBM bytes of the same kernel from a committed rocprofv3 --pmc run of
-        # this workload (tools/gpu_pmc.sh + tools/pmc_traffic.py)
-        with open(pmc_path) as f:
-            pmc = json.load(f)
-        want = {2: "k_scan_hi", 6: "k_scan_mx<", 3: "k_scan_bf16<"}.get(pf, "?")
-        if pmc.get("nq") in (None, nq):
-            for name, kinfo in pmc.get("kernels", {}).items():
-                append = "false" in name or "_pp<" in name  # (the persistent kernel is APPEND only)
-                if want in name and append and "hbm_bytes_per_search" in kinfo:
-                    roof["traffic"] = round(kinfo["hbm_bytes_per_search"])
-                    roof["traffic_unit"] = "HBM bytes per search (all main-scan launches)"
-                    roof["traffic_source"] = os.path.relpath(pmc_path, ROOT)
-                    for extra in ("clock_ghz", "mfma_busy_frac", "l2_hit_rate"):
-                        if extra in kinfo:
-                            roof["pmc_" + extra] = kinfo[extra]
+        # this workload (tools/gpu_pmc.sh + tools/pmc_traffic.py), per search
+        roof["traffic"] = round(pm["hbm_bytes_per_search"])
+        roof["traffic_unit"] = "HBM bytes per search (all main-scan launches)"
+        roof["traffic_source"] = pm["source"]
+        if "per_search" in roof and roof["per_search"].get("plane_bytes"):
+            roof["traffic_over_plane"] = round(pm["hbm_bytes_per_search"] / roof["per_search"]["plane_bytes"], 3)
+        for extra in ("clock_ghz", "mfma_busy_frac", "l2_hit_rate", "avg_launch_ms"):
+            if extra in pm:
+                roof["pmc_" + extra] = pm[extra]
     return roof
 
 
@@ -483,6 +494,57 @@ def small_batch_leg(mq_scan, seg, args, nqs=(1, 4, 16, 64), reps=10):
                     "survey_t_star_ms": round(t_star, 3), "survey_t_star_over_t": round(t_star / ms, 3),
                     "survivors_max": stt["survivors_max"],
                     "exact": chk})
+    return out
+
+
+def config1_points(mq, mq_scan, args):
+    """Further configs[1] points: the same 10M x 768
+    batch of 1000 under the L2 metric, and cosine on the other generator
+    distribution (mode 2 when the headline runs mode 1), each on its own part
+    generated in HBM after the main part is freed: QPS, main-scan time,
+    survivors, rescans and the exact-path check on every query."""
+    import torch
+    from myscaledb_amd import _lib
+    from myscaledb_amd.vector_scan import generate_device
+    n, d, nq, k, g = args.n, args.d, args.nq, args.k, args.granule
+    other = 2 if args.mode != 2 else 1
+    out = []
+    for metric, mode in (("L2", args.mode), (args.metric, other)):
+        seg = mq.VectorScanSegment.generate(SEED_BASE, mode, n, d, metric, g)
+        try:
+            q = torch.empty((nq, d), dtype=torch.float32, device="cuda")
+            generate_device(SEED_QUERY, mode, 0, nq, d, q)
+            ids = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+            dst = torch.empty((nq, k), dtype=torch.float32, device="cuda")
+            for _ in range(2):
+                seg.search(q, k, out=(ids, dst))
+            walls, sts = [], []
+            for _ in range(5):
+                torch.cuda.synchronize()
+                t0 = time.perf_counter()
+                seg.search(q, k, out=(ids, dst))
+                torch.cuda.synchronize()
+                walls.append((time.perf_counter() - t0) * 1e3)
+            mq_scan.set_timing(True)
+            for _ in range(3):
+                seg.search(q, k, out=(ids, dst))
+                torch.cuda.synchronize()
+                sts.append(_lib.last_search_stats())
+            mq_scan.set_timing(False)
+            ms = float(np.median(walls))
+            st = sorted(sts, key=lambda s_: s_["total_ms"])[len(sts) // 2]
+            flop = 2.0 * nq * st["main_rows"] * seg_dpad(d)
+            out.append({"workload": f"FLAT {metric} {n // 1_000_000}M x {d}, batch {nq}, top-{k}, generator mode {mode}",
+                        "metric": metric, "generator_mode": mode, "ms_per_search": round(ms, 3),
+                        "qps": round(nq / (ms * 1e-3), 1), "main_ms": round(st["main_ms"], 3),
+                        "main_bf16_frac": round(flop / (st["main_ms"] * 1e-3) / 1e12 / BF16_MFMA_PEAK_TFLOPS, 4),
+                        "batch_kernel": st.get("batch_kernel"), "survivors_max": st["survivors_max"],
+                        "survivors_mean": round(st["survivors_total"] / nq, 1), "candidates_max": st["candidates_max"],
+                        "rescans": st["rescans"], "exact_check": exact_check(mq_scan, seg, q, k, ids, dst)})
+        finally:
+            seg.free()
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
     return out
 
 
@@ -668,11 +730,9 @@ def main():
     if rank == 0:
         qps = nq / (ms / 1000.0)
         pf = st.get("prefilter") if st["path"] == 2 else None
-        compute = {2: "bf16-hi MFMA pre-filter (one bf16 product, rigorous error bound from measured residual "
-                      "norms) + exact f32 fma-chain re-rank of the survivors",
-                   6: "bf16 + fp6-MX split MFMA pre-filter (rigorous error bound) + exact f32 fma-chain re-rank",
-                   3: "bf16x3 split MFMA pre-filter (rigorous error bound) + exact f32 fma-chain re-rank"}.get(
-            pf, "f32 MFMA fma chain" if st["path"] == 1 else "f32 VALU, product then add")
+        compute = ("bf16-hi MFMA pre-filter (one bf16 product, rigorous error bound from measured residual norms) + "
+                   "exact f32 fma-chain re-rank of the survivors") if pf == 2 else (
+            "f32 MFMA fma chain" if st["path"] == 1 else "f32 VALU, product then add")
         result = {
             "metric": "QPS (FLAT brute force, batch top-k)",
             "value": round(qps, 2),
@@ -700,26 +760,69 @@ def main():
             "stats_last_step": {kk: (round(v, 3) if isinstance(v, float) else v) for kk, v in st.items()},
             "roofline": roof,
         }
-        if not args.no_verify and world == 1:
-            # and the oracle's own formula on sampled rows (pins the exact path)
-            ok, nchk = verify_sample(_oracle(), ids.cpu().numpy(), dst.cpu().numpy(), q.cpu().numpy(), args)
-            result["oracle_sample"] = {"queries": nchk, "bitwise_and_no_better_sample": ok}
+        if args.read_sweep_gib > 0 and world == 1:
+            # the measured HBM read peak of this device (same process, same
+            # GPU): the denominator of frac_measured_peak below
+            gbs, bms = mq_scan.measure_read_bandwidth(int(args.read_sweep_gib * (1 << 30)), 5)
+            result["hbm_read_sweep"] = {"gbs": round(gbs, 1), "bytes": int(args.read_sweep_gib * (1 << 30)),
+                                        "best_ms": round(bms, 3), "frac_of_8tbs": round(gbs / HBM_PEAK_GBS, 4),
+                                        "kernel": "k_read_sweep (16 B per lane, 4 loads in flight, grid-stride, "
+                                                  "8 x 256-thread workgroups per CU)"}
         if not args.no_small and world == 1:
             result["small_batch"] = small_batch_leg(mq_scan, seg, args)
+            p1 = [x for x in result["small_batch"] if x["nq"] == 1]
+            if p1:
+                # the north-star nq = 1 point: HBM-bound scan of
+                # the bf16 plane, against 8 TB/s and the measured read peak
+                p1 = p1[0]
+                plane = p1["bytes_read"]
+                nq1 = {"ms": p1["main_ms"], "ms_end_to_end": p1["ms_per_search"], "plane_bytes": plane,
+                       "kernel": "k_scan_hi_reg (bf16 16x16x32, operands straight from HBM into registers)",
+                       "achieved_gbs": p1["main_gbs"], "frac_8tbs": p1["hbm_frac_main"],
+                       "frac_end_to_end_8tbs": p1["hbm_frac_end_to_end"], "exact": p1["exact"]["ids_equal"] and
+                       p1["exact"]["dist_bitwise_equal"]}
+                if "hbm_read_sweep" in result:
+                    nq1["measured_peak_gbs"] = result["hbm_read_sweep"]["gbs"]
+                    nq1["frac_measured_peak"] = round(p1["main_gbs"] / result["hbm_read_sweep"]["gbs"], 4)
+                pm = _pmc_kernel(os.path.join(ROOT, PMC_NQ1_DEFAULT), "k_scan_hi_reg", 1, sum_all=True)
+                if pm:
+                    nq1["pmc_hbm_bytes"] = round(pm["hbm_bytes_per_search"])
+                    nq1["pmc_over_plane"] = round(pm["hbm_bytes_per_search"] / plane, 4)
+                    nq1["pmc_source"] = pm["source"]
+                result["roofline"]["nq1"] = nq1
         if not args.no_cpu and world == 1:
+            # the CPU leg: the oracle (the reference's CPU path restated) timed
+            # on the host cores, and -- as the checker only -- its formula on
+            # sampled rows of the timed output (pins the exact path)
             O = _oracle()
             result["cpu_baseline"] = cpu_baseline(O, args)
+            if not args.no_verify:
+                ok, nchk = verify_sample(O, ids.cpu().numpy(), dst.cpu().numpy(), q.cpu().numpy(), args)
+                result["oracle_sample"] = {"queries": nchk, "bitwise_and_no_better_sample": ok}
         if not args.no_index and world == 1:
             result["index"] = index_leg(mq, seg, args)
-        if not args.no_configs and world == 1:
-            seg.free()  # (room for the 50M x 768 part)
+        risk = os.path.join(ROOT, BLAS_RISK_DEFAULT)
+        if os.path.exists(risk):
+            # parity risk of the unpinned BLAS-branch order (tools/blas_order_risk.py,
+            # committed run of this config): queries whose top-k would change
+            # if faiss's sgemm blocked K
+            with open(risk) as f:
+                rk = json.load(f)
+            result["blas_order_risk"] = dict(rk, source=os.path.relpath(risk, ROOT))
+        if (not args.no_configs or not args.no_config1_points) and world == 1:
+            seg.free()  # (room for the next parts)
+            seg = None
             torch.cuda.synchronize()
             torch.cuda.empty_cache()
+        if not args.no_config1_points and world == 1:
+            result["config1_points"] = config1_points(mq, mq_scan, args)
+        if not args.no_configs and world == 1:
             result["configs"] = configs_leg(mq, mq_scan, args)
         print(json.dumps(result), flush=True)
     if comm is not None:
         comm.free()
-    seg.free()
+    if seg is not None:
+        seg.free()
     if dist_on:
         tdist.barrier()
         tdist.destroy_process_group()

@@ -372,6 +372,23 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
             return;
         }
     }
+    if (maxv_hint > kMaxVariants) {
+        // a grown cosine variant table (chains that did not repeat within the
+        // default table): its fp32 variants and their bf16 plane are
+        // maxv x (4 qstride + 2 dpad) bytes per query -- query sub-batches
+        // keep them within the scratch budget (same formula, same bits)
+        const int64_t per_q = (int64_t)maxv_hint * (round_up(seg->d, 32) * 4 + round_up(seg->d, kBfK) * 2);
+        const int64_t qb = std::max<int64_t>(1, (int64_t)scratch_budget() / per_q);
+        if (nq > qb) {
+            for (int q0 = 0; q0 < nq; q0 += (int)qb) {
+                const int m = (int)std::min<int64_t>(qb, nq - q0);
+                search_impl(seg, queries + (size_t)q0 * seg->d, m, k, metric, filter, exists,
+                            out_ids + (size_t)q0 * k, out_dist + (size_t)q0 * k, flags, user_stream, force_exact,
+                            ord_base, maxv_hint, fnq);
+            }
+            return;
+        }
+    }
 
     DeviceGuard guard(seg->device);
     Workspace &ws = workspace(seg->device);

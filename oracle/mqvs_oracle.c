@@ -55,6 +55,21 @@ float orc_gemm_dot(const float *x, const float *y, int64_t d) {
     return res;
 }
 
+/* The same element under an sgemm that blocks K (kc = kb): each block is an
+ * fma chain from zero, added to C in block order (C = 0 + part_0 + part_1 ...).
+ * Not the assumed reference arithmetic: the parity-risk measurement of the
+ * BLAS-branch assumption (tools/blas_order_risk.py). */
+float orc_gemm_dot_blocked(const float *x, const float *y, int64_t d, int64_t kb) {
+    float res = 0.0f;
+    for (int64_t b = 0; b < d; b += kb) {
+        float part = 0.0f;
+        const int64_t e = b + kb < d ? b + kb : d;
+        for (int64_t i = b; i < e; i++) part = fmaf(x[i], y[i], part);
+        res = res + part;
+    }
+    return res;
+}
+
 /* VectorDataset<Float>::normalize, VectorDataset.h:98-117:
  *   sum += p[d]*p[d] (separate mul/add), skip if sum < FLT_EPSILON,
  *   sum = sqrt(sum), p[d] /= sum. */

@@ -40,6 +40,7 @@ float orc_l2sqr(const float *x, const float *y, int64_t d);
 float orc_inner_product(const float *x, const float *y, int64_t d);
 float orc_norm_l2sqr(const float *x, int64_t d);
 float orc_gemm_dot(const float *x, const float *y, int64_t d);
+float orc_gemm_dot_blocked(const float *x, const float *y, int64_t d, int64_t kb);
 
 /* VectorDataset<Float>::normalize (VectorDataset.h:98-117), in place. */
 void orc_normalize(float *data, int64_t n, int64_t d);

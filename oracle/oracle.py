@@ -64,6 +64,8 @@ def lib():
         L.orc_generate.argtypes = [ctypes.c_uint64, ctypes.c_int, I64, I64, I64, P]
         L.orc_gemm_dot.argtypes = [P, P, I64]
         L.orc_gemm_dot.restype = ctypes.c_float
+        L.orc_gemm_dot_blocked.argtypes = [P, P, I64, I64]
+        L.orc_gemm_dot_blocked.restype = ctypes.c_float
         L.orc_norm_l2sqr.argtypes = [P, I64]
         L.orc_norm_l2sqr.restype = ctypes.c_float
         L.orc_l2sqr.argtypes = [P, P, I64]
@@ -286,6 +288,13 @@ def gemm_dot(x, y):
     """fma-chain dot (the BLAS-branch sgemm element, nq >= 20)."""
     x, y = _f32(x), _f32(y)
     return np.float32(lib().orc_gemm_dot(_p(x), _p(y), x.shape[0]))
+
+
+def gemm_dot_blocked(x, y, kb):
+    """sgemm-style K-blocked element (blocks of kb, each an fma chain, summed
+    in order): the BLAS-order parity-risk model, not the reference formula."""
+    x, y = _f32(x), _f32(y)
+    return np.float32(lib().orc_gemm_dot_blocked(_p(x), _p(y), x.shape[0], int(kb)))
 
 
 def norm_l2sqr(x):

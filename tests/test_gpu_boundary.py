@@ -242,17 +242,22 @@ def test_async_overflow_is_reported(mq):
         seg2.free()
 
 
-@pytest.mark.parametrize("nq", [5, 24])
-def test_cosine_long_normalisation_chains(mq, nq):
+@pytest.mark.parametrize("nq,budget", [(5, None), (24, None), (24, 1 << 20)])
+def test_cosine_long_normalisation_chains(mq, nq, budget):
     """Small-integer queries whose fp32 re-normalisation chain does not repeat
     within the default 32 variants (a third of them at d = 768) on a part of
     60 granule chunks: the variant table grows to one per chunk ordinal and
-    the result equals the oracle's per-chunk re-normalisation bit for bit."""
+    the result equals the oracle's per-chunk re-normalisation bit for bit.
+    Under a 1 MiB scratch budget the grown table (60 x 4.5 KiB per query) is
+    built in query sub-batches of 3 that keep the 24-query call's BLAS
+    formula."""
+    from myscaledb_amd.vector_scan import set_scratch_budget
     n, d, k, gran = 60 * 64, 768, 40, 64
     rows = O.generate(0x5EED0001, 0, 0, n, d)
     q = O.generate(0x5EED0002, 0, 0, nq, d)
     io, do = O.vector_scan(rows, q, k, O.COSINE, gran, fast=True)
     seg = mq.VectorScanSegment.from_rows(rows, metric="Cosine", granule=gran)
+    old = set_scratch_budget(budget) if budget else None
     try:
         ig, dg = seg.search(q, k)
         _eq(ig, dg, io, do, f"cosine long chains nq {nq}")
@@ -263,6 +268,8 @@ def test_cosine_long_normalisation_chains(mq, nq):
         ri, rd = seg.rerank(q, cand, k)
         _eq(ri, rd, io, do, f"cosine long chains nq {nq} rerank")
     finally:
+        if old:
+            set_scratch_budget(old)
         seg.free()
 
 

@@ -30,7 +30,7 @@ def main():
     ap.add_argument("root", help="directory holding pmc1/ pmc2/ pmc3/ (gpurun_out)")
     ap.add_argument("--searches", type=int, required=True)
     ap.add_argument("--nq", type=int, default=None, help="batch size of the profiled searches")
-    ap.add_argument("--kernel", default="k_scan_(?:bf16|mx|hi)")
+    ap.add_argument("--kernel", default="k_scan_(?:hi|p4)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -55,6 +55,9 @@ def main():
         k = {}
         launches = max(len(v) for v in disp[key].values())
         k["launches"] = launches
+        durs = [v for (kk, tag), dd in dur.items() if kk == key for v in dd.values()]
+        if durs:
+            k["avg_launch_ms"] = round(sum(durs) / len(durs) / 1e6, 4)
         if "FETCH_SIZE" in c:
             rd = 2.0 * c["FETCH_SIZE"] * 1024
             wr = c.get("WRITE_SIZE", 0.0) * 1024
