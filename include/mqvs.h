@@ -325,9 +325,9 @@ int mqvs_generate_device(uint64_t seed, int32_t mode, int64_t row0, int64_t n, i
  *   metric_type  L2 | IP | Cosine (must match the segment's metric family;
  *                default: the segment's metric)
  *   alpha        default search alpha (MSTG's accuracy knob, [1, 4], default 3)
- *   nlist        lists (default about n / 1000)
+ *   nlist        lists (default about n / 256, at most 65536)
  *   kmeans_iters k-means iterations (default 8)
- *   sample       k-means training rows (default min(n, 64 * nlist))
+ *   sample       k-means training rows (default min(n, max(16 nlist, min(64 nlist, 2^20))))
  * Unknown keys fail with MQVS_ERR_BAD_ARGUMENTS. */
 typedef struct mqvs_index *mqvs_index_t;
 int mqvs_index_build(mqvs_segment_t seg, const char *index_type, const char *params, mqvs_index_t *out);
@@ -344,7 +344,8 @@ typedef struct {
 } mqvs_index_info_t;
 int mqvs_index_info(mqvs_index_t idx, mqvs_index_info_t *out);
 /* Search params (comma-separated key=value, may be NULL or ""):
- *   alpha        [1, 4]: probes nprobe(alpha) lists (more = higher recall)
+ *   alpha        [1, 4]: probes nprobe(alpha) lists (more = higher recall; alpha 3:
+ *                max(4, nlist / 256, lists of 4096 rows), doubling per unit)
  *   nprobe       lists probed per query (overrides alpha; <= min(nlist, 4096))
  *   num_reorder  candidates re-ranked exactly (default max(2k, 64), capped at
  *                4096 for k <= 2048; k .. 32768; above 4096 the select and the

@@ -75,6 +75,7 @@ namespace mqvs {
 
 static thread_local mqvs_index_search_stats g_istats{};
 constexpr int64_t kCoarseChunk = 256;  // centroids per coarse "list"
+constexpr int64_t kCoarseFlatLists = 16384;  // more lists: the coarse step is a FLAT search
 
 // plan / scan / select buffers of one list pass
 struct ListBufs {
@@ -84,7 +85,7 @@ struct ListBufs {
 struct IndexWorkspace {
     hipEvent_t ev[6] = {};
     DevBuf queries, qvars, qnorms, qmu, qlam, status, qhi, probes, cprobes, filter, exists, rows, out_ids, out_dist,
-        ord, dmap, dwords;
+        ord, dmap, dwords, pdist;
     ListBufs coarse, fine;
     void init() {
         if (ev[0]) return;
@@ -154,9 +155,11 @@ static void check_keys(const std::map<std::string, std::string> &m, const std::v
     }
 }
 
-// nprobe for a search alpha: nprobe(3) = base, doubling per unit of alpha
+// nprobe for a search alpha: nprobe(3) = base, doubling per unit of alpha;
+// the base probes 1/256 of the lists and at least 4 lists and 4096 rows
 static int nprobe_of(const mqvs_index *ix, double alpha) {
-    const double base = std::max<double>(4.0, std::ceil((double)ix->nlist / 256.0));
+    const double rows = (double)std::max<int64_t>(ix->rows_indexed, 1);
+    const double base = std::max({4.0, std::ceil((double)ix->nlist / 256.0), std::ceil(4096.0 * ix->nlist / rows)});
     const double np = std::ceil(base * std::pow(2.0, alpha - 3.0));
     return (int)std::max<double>(1.0, std::min<double>(np, (double)std::min<int64_t>(ix->nlist, kSortCap)));
 }
@@ -261,12 +264,18 @@ static mqvs_index *build_impl(mqvs_segment *seg, const char *index_type, const c
     }
     const int64_t n = seg->n;
     const int d = seg->d;
-    const int64_t dflt_nlist = std::max<int64_t>(1, std::min<int64_t>(65536, (n + 500) / 1000));
+    // lists of about 256 rows (at most 65536 lists): fine enough that data of
+    // many small clusters (generator mode 3: 65536 centres of ~150 rows)
+    // keeps its neighbours in one or two lists; n / 1000 left mode 3 needing
+    // 512 of 10000 lists for recall 0.95 (profiles/r03/index)
+    const int64_t dflt_nlist = std::max<int64_t>(1, std::min<int64_t>(65536, (n + 128) / 256));
     const int64_t L = (int64_t)num_param(pm, "nlist", (double)dflt_nlist, 1, 1 << 20);
     if (n > 0 && L > n) fail(MQVS_ERR_BAD_ARGUMENTS, "nlist must not exceed the number of rows");
     const int iters = (int)num_param(pm, "kmeans_iters", 8, 0, 1000);
-    const int64_t S = std::max<int64_t>(std::min<int64_t>(n, (int64_t)num_param(pm, "sample",
-                                                                                 (double)std::min<int64_t>(n, 64 * L),
+    // training sample: 64 rows per list up to 1M rows, at least 16 per list
+    // (65536 lists: 1M rows, build 9.7 -> 4.1 s at equal recall, profiles/r03/index)
+    const int64_t dflt_sample = std::min<int64_t>(n, std::max<int64_t>(16 * L, std::min<int64_t>(64 * L, 1 << 20)));
+    const int64_t S = std::max<int64_t>(std::min<int64_t>(n, (int64_t)num_param(pm, "sample", (double)dflt_sample,
                                                                                  1, 1e12)),
                                         std::min<int64_t>(n, L));
 
@@ -606,9 +615,20 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     // the centroid chunks (every query probes every chunk)
     const int64_t *cprobes = nullptr;  // dense plan: probe r of every query is chunk r
     int64_t *probes = (int64_t *)ws.probes.get(sizeof(int64_t) * (size_t)nq * nprobe);
-    list_pass(ws.coarse, ix->cplane, ix->cperm, ix->cpnorm, ix->clist_off, ix->cnl, ix->cnpos, ix->cmax, ix->dpad,
-              ix->metric, qhi, qnorms, nq, cprobes, (int)ix->cnl, nullptr, nullptr, nprobe, probes, 0, nullptr,
-              nullptr, s, true);
+    // many lists: the FLAT batch search of the centroid segment (exact
+    // top-nprobe; ranking by the raw inner product for IP and cosine parts):
+    // 65536 lists, nq 1000: 1.26 -> 0.67 ms; few lists: the list pass over
+    // the centroid chunks (10000 lists: 0.28 ms vs 0.50, the FLAT path's
+    // fixed stages dominate; profiles/r03/index)
+    if (tune_int("MQVS_IVF_COARSE", ix->nlist > kCoarseFlatLists ? 1 : 0) == 1) {
+        float *pd = (float *)ws.pdist.get(sizeof(float) * (size_t)nq * nprobe);
+        search_internal(ix->cent, dq, nq, nprobe, ix->coarse_metric, nullptr, nullptr, probes, pd,
+                        MQVS_F_DEVICE_PTRS | (flags & MQVS_F_ASYNC), s);
+    } else {
+        list_pass(ws.coarse, ix->cplane, ix->cperm, ix->cpnorm, ix->clist_off, ix->cnl, ix->cnpos, ix->cmax,
+                  ix->dpad, ix->metric, qhi, qnorms, nq, cprobes, (int)ix->cnl, nullptr, nullptr, nprobe, probes, 0,
+                  nullptr, nullptr, s, true);
+    }
     MQVS_HIP(hipEventRecord(ws.ev[1], s));
 
     // ---- fine: the probed lists

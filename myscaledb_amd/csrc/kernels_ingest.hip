@@ -10,20 +10,21 @@
 //                   decompressed size).  One thread walks the headers; a
 //                   1 MiB block costs one dependent 25-B read.
 //   k_decode_blocks one 64-lane workgroup per block.  LZ4 (LZ4_decompress_faster
-//                   .cpp:480-640 block format): every lane parses the token
-//                   stream in lock-step (uniform control flow); long literal
-//                   runs are copied as whole output dwords (copy_literals),
-//                   match bytes up to 256 per step.  Matches read from a
-//                   64 KiB LDS ring of the block's latest output (LZ4 offsets
-//                   are < 2^16), never from global memory, so no global
-//                   read-after-write ordering is needed; an overlapping match
-//                   (offset < length) is copied in steps of min(offset, 256).
+//                   .cpp:480-640 block format): the token stream is parsed in
+//                   lock-step (uniform control flow) into groups of up to 64
+//                   sequences, one per lane; a group's literal runs are then
+//                   copied at once and its matches in dependency rounds
+//                   (a lane per sequence).  Long literal runs go as whole
+//                   output dwords (copy_literals), long matches 256 bytes per
+//                   step.  Matches read from an 8 KiB LDS ring of the block's
+//                   latest output, farther ones from the flushed output.
 //   k_block_checksum CityHash128 v1.0.2 of every block (one lane per block),
 //                   compared with the stored 16-B checksum.
 //   k_sizes_scan_*  array sizes (UInt64 per row) -> element offsets.
 //   k_array_rows    the copy loop of :1381-1393: FLT_MAX fill, first
 //                   min(size, d) elements of a non-empty array, nonempty flag.
 #include "mqvs_internal.h"
+#include "tuning.h"
 
 namespace mqvs {
 
@@ -34,6 +35,10 @@ namespace mqvs {
 // output from global memory (far_byte).
 constexpr int kRing = 8192;
 constexpr int kFlush = 2048;  // unflushed output < kFlush + one step (< kRing - 256)
+// a group holds sequences of at most kGrpLit literals and kGrpMatch match
+// bytes: 64 of them write < kRing - kFlush - 256 bytes
+constexpr int kGrpLit = 32, kGrpMatch = 36;
+static_assert(64 * (kGrpLit + kGrpMatch) + kFlush + 256 < kRing, "group output must fit the ring");
 
 __global__ void k_block_table(const uint8_t *src, int64_t n, IngestBlock *tab, int64_t max_blocks,
                               int64_t *out) {
@@ -153,6 +158,10 @@ __device__ __forceinline__ uint32_t far_byte(const uint8_t *out, int32_t pos) {
 // offset is uniform); a short literal run is read with one lane shuffle per
 // 64 bytes.  When the parse enters the upper half the window slides by 256 B
 // and loads the next half ahead of its use.
+// DIAG (measurement builds only; wrong output): 1 = parse only (no group
+// copies), 2 = far bytes from the ring (no global reads), 4 = every match in
+// one round (no dependency order)
+template <int DIAG>
 __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_t src_bytes, const IngestBlock *tab,
                                                       int64_t nblocks, uint8_t *dst, int *status) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
@@ -226,36 +235,13 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
             fl = upto;
         };
         int32_t ip = 0, op = 0;
-        while (!bad) {
-            ip = __builtin_amdgcn_readfirstlane(ip);
-            op = __builtin_amdgcn_readfirstlane(op);
-            fl = __builtin_amdgcn_readfirstlane(fl);
-            if (ip >= isz) {
-                bad = true;
-                break;
-            }
-            const uint32_t token = byte(ip++);
-            int32_t len = (int32_t)(token >> 4);
-            if (len == 15) {
-                uint32_t sb;
-                do {
-                    if (ip >= isz) {
-                        bad = true;
-                        break;
-                    }
-                    sb = byte(ip++);
-                    len += (int32_t)sb;
-                } while (sb == 255 && len < (1 << 30));
-                if (bad) break;
-            }
-            if (len > osz - op || len > isz - ip) {
-                bad = true;
-                break;
-            }
+        // A sequence too long for a group (see the parse below): literals at
+        // op, the wave-wide paths of the round-2 decoder
+        auto big_literals = [&](int32_t lip, int32_t len) {
             if (len > 0 && len <= 256) {
                 // short run: its bytes are in the window (no global load)
-                cover(mis + ip);
-                const int32_t o0 = mis + ip - wa;
+                cover(mis + lip);
+                const int32_t o0 = mis + lip - wa;
                 for (int32_t r = 0; r < len; r += 64) {
                     const int32_t i = r + lane, o = o0 + i;
                     const uint32_t x0 = __shfl(w0, (o >> 2) & 63), x1 = __shfl(w1, ((o - 256) >> 2) & 63);
@@ -264,48 +250,12 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
             } else if (len > 256) {
                 // long run: straight to global memory (and the ring)
                 flush(op);
-                copy_literals(ip0 + ip, src_end, out, op, len, ring, lane);
+                copy_literals(ip0 + lip, src_end, out, op, len, ring, lane);
                 fl = op + len;
             }
-            op += len;
-            ip += len;
-            if (op == osz) break;
-            if (isz - ip < 2) {
-                bad = true;
-                break;
-            }
-            const int32_t off = (int32_t)(byte(ip) | (byte(ip + 1) << 8));
-            ip += 2;
-            if (off == 0 || off > op) {
-                bad = true;
-                break;
-            }
-            int32_t mlen = (int32_t)(token & 15);
-            if (mlen == 15) {
-                uint32_t sb;
-                do {
-                    if (ip >= isz) {
-                        bad = true;
-                        break;
-                    }
-                    sb = byte(ip++);
-                    mlen += (int32_t)sb;
-                } while (sb == 255 && mlen < (1 << 30));
-                if (bad) break;
-            }
-            mlen += 4;
-            if (mlen > osz - op) {
-                bad = true;
-                break;
-            }
-            if (mlen <= 64 && off >= mlen && off <= kRing - 64) {
-                // the common short, non-overlapping match: one step
-                __builtin_amdgcn_wave_barrier();
-                uint8_t v = 0;
-                if (lane < mlen) v = ring[(op - off + lane) & (kRing - 1)];
-                if (lane < mlen) ring[(op + lane) & (kRing - 1)] = v;
-                __builtin_amdgcn_wave_barrier();
-            } else if (off > kRing - 256) {
+        };
+        auto big_match = [&](int32_t off, int32_t mlen) {
+            if (off > kRing - 256) {
                 // far match (off > mlen-step, so no replication within a
                 // 256-byte step): from the flushed output
                 for (int32_t d0 = 0; d0 < mlen; d0 += 256) {
@@ -330,16 +280,14 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
                 // Chunks of up to 256 bytes: byte op + i equals byte op + i -
                 // m off for any m >= 1 (the copy replicates with period off),
                 // so chunk [d0, d0 + cnt) reads the latest off bytes before it,
-                // [op + d0 - off, op + d0), all final.  cnt <= 65536 - off keeps
-                // the chunk's ring writes off that window.
-                const int32_t chunk = 256;  // off <= kRing - 256 here
-                for (int32_t d0 = 0; d0 < mlen; d0 += chunk) {
+                // [op + d0 - off, op + d0), all final.
+                for (int32_t d0 = 0; d0 < mlen; d0 += 256) {
                     __builtin_amdgcn_wave_barrier();
                     if (op + d0 - fl >= kFlush) {
                         flush(op + d0);
                         __builtin_amdgcn_wave_barrier();
                     }
-                    const int32_t cnt = mlen - d0 < chunk ? mlen - d0 : chunk;
+                    const int32_t cnt = mlen - d0 < 256 ? mlen - d0 : 256;
                     uint8_t v[4];
 #pragma unroll
                     for (int u = 0; u < 4; ++u) {
@@ -355,7 +303,176 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
                 }
                 __builtin_amdgcn_wave_barrier();
             }
-            op += mlen;
+        };
+        // Parse, then execute, in groups of up to 64 sequences.  The parse is
+        // the block's only sequential chain: it walks the tokens (uniform,
+        // scalar) and leaves sequence g's fields in lane g, no
+        // byte moved.  The group then runs with a lane per sequence: every
+        // literal run at once (they depend on nothing), then the matches in
+        // rounds -- a match whose source bytes end at or below the first
+        // unfinished match's output is copied in the current round (the first
+        // unfinished one always is), so each round makes progress and most
+        // groups finish in a few (on quantised floats ~80 % of the matches
+        // read output older than their group).  A match reads byte
+        // src + (t mod off) for output byte t: the replication of an
+        // overlapping match (off < length) needs no ordering of its own.
+        // Sequences longer than kGrpLit / kGrpMatch end the group and take the
+        // wave-wide paths above.
+        bool last_seen = false;
+        while (!bad && !last_seen) {
+            ip = __builtin_amdgcn_readfirstlane(ip);
+            op = __builtin_amdgcn_readfirstlane(op);
+            fl = __builtin_amdgcn_readfirstlane(fl);
+            int32_t g = 0, rel = 0;
+            int32_t vpk = 0, vrel = 0, vlip = 0;
+            bool big = false;
+            int32_t b_lip = 0, b_ll = 0, b_off = 0, b_ml = 0;
+            while (g < 64) {
+                ip = __builtin_amdgcn_readfirstlane(ip);
+                rel = __builtin_amdgcn_readfirstlane(rel);
+                const int32_t o = op + rel;
+                if (ip >= isz) {
+                    bad = true;
+                    break;
+                }
+                const uint32_t token = byte(ip++);
+                int32_t ll = (int32_t)(token >> 4);
+                if (ll == 15) {
+                    uint32_t sb;
+                    do {
+                        if (ip >= isz) {
+                            bad = true;
+                            break;
+                        }
+                        sb = byte(ip++);
+                        ll += (int32_t)sb;
+                    } while (sb == 255 && ll < (1 << 30));
+                    if (bad) break;
+                }
+                if (ll > osz - o || ll > isz - ip) {
+                    bad = true;
+                    break;
+                }
+                const int32_t lip = ip;
+                ip += ll;
+                int32_t off = 0, ml = 0;
+                const bool last = o + ll == osz;  // the block's final, literals-only sequence
+                if (!last) {
+                    if (isz - ip < 2) {
+                        bad = true;
+                        break;
+                    }
+                    off = (int32_t)(byte(ip) | (byte(ip + 1) << 8));
+                    ip += 2;
+                    if (off == 0 || off > o + ll) {
+                        bad = true;
+                        break;
+                    }
+                    ml = (int32_t)(token & 15);
+                    if (ml == 15) {
+                        uint32_t sb;
+                        do {
+                            if (ip >= isz) {
+                                bad = true;
+                                break;
+                            }
+                            sb = byte(ip++);
+                            ml += (int32_t)sb;
+                        } while (sb == 255 && ml < (1 << 30));
+                        if (bad) break;
+                    }
+                    ml += 4;
+                    if (ml > osz - o - ll) {
+                        bad = true;
+                        break;
+                    }
+                }
+                last_seen = last;
+                if (ll > kGrpLit || ml > kGrpMatch) {
+                    big = true;
+                    b_lip = lip;
+                    b_ll = ll;
+                    b_off = off;
+                    b_ml = ml;
+                    break;
+                }
+                const int32_t pk = (int32_t)((uint32_t)off | ((uint32_t)ll << 16) | ((uint32_t)ml << 22));
+                const bool mine = lane == g;  // (one compare, three v_cndmask)
+                vpk = mine ? pk : vpk;
+                vrel = mine ? rel : vrel;
+                vlip = mine ? lip : vlip;
+                rel += ll + ml;
+                ++g;
+                if (last) break;
+            }
+            if (bad) break;
+            g = __builtin_amdgcn_readfirstlane(g);
+            rel = __builtin_amdgcn_readfirstlane(rel);
+            if (g > 0 && (DIAG & 1) == 0) {
+                const bool act = lane < g;
+                const uint32_t pk = (uint32_t)vpk;
+                const int32_t off = act ? (int32_t)(pk & 0xffffu) : 0;
+                const int32_t ll = act ? (int32_t)((pk >> 16) & 63u) : 0;
+                const int32_t ml = act ? (int32_t)(pk >> 22) : 0;
+                const int32_t dst = op + vrel;  // the sequence's literals
+                const int32_t mdst = dst + ll;  // its match
+                // literal runs: bytes of the compressed input (cached: the
+                // parse window just read them)
+                for (int32_t t0 = 0; __ballot(ll > t0) != 0; t0 += 8) {
+                    uint32_t v[8];
+#pragma unroll
+                    for (int u = 0; u < 8; ++u) v[u] = t0 + u < ll ? (uint32_t)ip0[vlip + t0 + u] : 0u;
+#pragma unroll
+                    for (int u = 0; u < 8; ++u)
+                        if (t0 + u < ll) ring[(dst + t0 + u) & (kRing - 1)] = (uint8_t)v[u];
+                }
+                // bytes below far_lim may be overwritten in the ring by this
+                // group: they come from the flushed output (all of it is: the
+                // unflushed tail is < kFlush bytes behind the group's start)
+                const int32_t far_lim = op + rel - kRing;
+                const int32_t src = mdst - off;
+                const int32_t need_end = off < ml ? mdst : src + ml;
+                if ((DIAG & 2) == 0 && __ballot(ml > 0 && src < far_lim) != 0)
+                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+                bool fin = ml == 0;
+                while (true) {
+                    const uint64_t und = __ballot(!fin);
+                    if (und == 0) break;
+                    const int32_t lo = __builtin_amdgcn_readlane(mdst, (int)__builtin_ctzll(und));
+                    const bool go = !fin && ((DIAG & 4) != 0 || need_end <= lo);
+                    if (go) {
+                        int32_t k = 0;  // (t mod off)
+                        for (int32_t t0 = 0; t0 < ml; t0 += 12) {
+                            uint32_t v[12];
+#pragma unroll
+                            for (int u = 0; u < 12; ++u) {
+                                v[u] = 0;
+                                if (t0 + u < ml) {
+                                    const int32_t q = src + k;
+                                    v[u] = (DIAG & 2) != 0 || q >= far_lim ? (uint32_t)ring[q & (kRing - 1)]
+                                                                           : far_byte(out, q);
+                                    k = k + 1 == off ? 0 : k + 1;
+                                }
+                            }
+#pragma unroll
+                            for (int u = 0; u < 12; ++u)
+                                if (t0 + u < ml) ring[(mdst + t0 + u) & (kRing - 1)] = (uint8_t)v[u];
+                        }
+                    }
+                    fin = fin || go;
+                }
+                __builtin_amdgcn_wave_barrier();
+            }
+            op += rel;
+            if (big) {
+                if (op - fl >= kFlush) flush(op);
+                big_literals(b_lip, b_ll);
+                op += b_ll;
+                if (b_ml > 0) {
+                    big_match(b_off, b_ml);
+                    op += b_ml;
+                }
+            }
             if (op - fl >= kFlush) flush(op);
         }
         __builtin_amdgcn_wave_barrier();
@@ -660,7 +777,16 @@ void launch_decode_blocks(const uint8_t *src, int64_t src_bytes, const IngestBlo
                           int *status, hipStream_t s) {
     if (nblocks <= 0) return;
     const int grid = (int)std::min<int64_t>(nblocks, 4096);
-    hipLaunchKernelGGL(k_decode_blocks, dim3(grid), dim3(64), 0, s, src, src_bytes, tab, nblocks, dst, status);
+    // (diagnostics on the big stream only: the array sizes must decode)
+    const int diag = kDebugTuning && nblocks > 64 ? tune_int("MQVS_LZ4_DIAG", 0) : 0;
+    if (kDebugTuning && diag == 1)
+        hipLaunchKernelGGL(k_decode_blocks<1>, dim3(grid), dim3(64), 0, s, src, src_bytes, tab, nblocks, dst, status);
+    else if (kDebugTuning && diag == 2)
+        hipLaunchKernelGGL(k_decode_blocks<2>, dim3(grid), dim3(64), 0, s, src, src_bytes, tab, nblocks, dst, status);
+    else if (kDebugTuning && diag == 6)
+        hipLaunchKernelGGL(k_decode_blocks<6>, dim3(grid), dim3(64), 0, s, src, src_bytes, tab, nblocks, dst, status);
+    else
+        hipLaunchKernelGGL(k_decode_blocks<0>, dim3(grid), dim3(64), 0, s, src, src_bytes, tab, nblocks, dst, status);
 }
 
 void launch_block_checksum(const uint8_t *src, const IngestBlock *tab, int64_t nblocks, int flag, int *status,

@@ -39,11 +39,16 @@ def column_files(data_f32, sizes, block=1 << 20, method=0x82):
 @pytest.mark.parametrize("kind,block,method", [("gauss", 1 << 20, 0x82), ("quantised", 65536, 0x82),
                                                ("repeats", 4097, 0x82), ("gauss", 300000, 0x02),
                                                ("quantised", 1 << 20, 0x82), ("period24k", 1 << 20, 0x82),
-                                               ("period40k", 1 << 20, 0x82)])
+                                               ("period40k", 1 << 20, 0x82), ("mixed", 1 << 20, 0x82),
+                                               ("mixed", 70000, 0x82)])
 def test_gpu_ingest_dense(mq, kind, block, method):
     """periodNk: the rows repeat every N KiB, so nearly every match reaches
-    back further than the decoder's 16 KiB LDS ring (its far-match path reads
-    the block's flushed output), long matches included."""
+    back further than the decoder's 8 KiB LDS ring (its far-match path reads
+    the block's flushed output), long matches included.  mixed: 16-float
+    pieces of four kinds (fresh gaussian = literal runs of every length,
+    quantised = short matches, copies of a recent piece = longer and
+    overlapping matches, constant runs), so the decoder's groups of short
+    sequences alternate with the wave-wide long-sequence paths."""
     rng = np.random.default_rng(11)
     n, d = 20000, 64
     if kind == "gauss":
@@ -56,6 +61,18 @@ def test_gpu_ingest_dense(mq, kind, block, method):
         base[::7] = np.round(base[::7], 1)
         rows = np.tile(base, (n // period + 1, 1))[:n].copy()
         rows[::97] += 1.0  # break some matches: fresh literals between far matches
+    elif kind == "mixed":
+        pieces = rng.integers(0, 4, n * d // 16)
+        flat = np.round(rng.standard_normal(n * d), 1).astype(np.float32)
+        g = rng.standard_normal(n * d).astype(np.float32)
+        for i in np.nonzero(pieces == 0)[0]:
+            flat[16 * i:16 * i + 16] = g[16 * i:16 * i + 16]
+        for i in np.nonzero(pieces == 2)[0]:
+            j = max(0, i - int(rng.integers(1, 40)))
+            flat[16 * i:16 * i + 16] = flat[16 * j:16 * j + 16]
+        for i in np.nonzero(pieces == 3)[0]:
+            flat[16 * i:16 * i + 16] = flat[16 * i - 1] if i else 0.5
+        rows = flat.reshape(n, d)
     else:  # long matches incl. overlapping ones (runs of equal values, repeated rows)
         base = np.repeat(rng.integers(-3, 4, (n // 8, d // 4)).astype(np.float32), 4, axis=1)
         rows = np.repeat(base, 8, axis=0)
