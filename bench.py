@@ -55,14 +55,14 @@ def parse():
                     help="skip the extra configs[1] points (L2 metric, second distribution)")
     ap.add_argument("--read-sweep-gib", type=float, default=8.0,
                     help="buffer of the HBM read sweep (mqvs_measure_read_bandwidth); 0 = skip")
-    ap.add_argument("--index-settings", default="nprobe=2;nprobe=3;nprobe=4;nprobe=8",
+    ap.add_argument("--index-settings", default="nprobe=4;nprobe=8;nprobe=16",
                     help="';'-separated mqvs_index_search parameter strings timed by the index leg")
     ap.add_argument("--index-mode", type=int, default=2,
                     help="index distribution (generator mode; 2 = 4096 centres, noise 0.25)")
     ap.add_argument("--index-hard-mode", type=int, default=3,
                     help="second index distribution (generator mode, 3 = 65536 centres, noise 1.0; -1 = none)")
     ap.add_argument("--index-hard-settings",
-                    default="nprobe=8;nprobe=32;nprobe=64;nprobe=128;nprobe=256;nprobe=512;nprobe=1024",
+                    default="nprobe=1;nprobe=2;nprobe=4;nprobe=8",
                     help="settings timed on the second distribution")
     ap.add_argument("--index-pmc", default=None,
                     help="JSON {mode: pmc_traffic.py output} of k_ivf_scan at each distribution's operating point")
@@ -244,7 +244,7 @@ def cpu_baseline(O, args):
     }
 
 
-INDEX_PMC_DEFAULT = os.path.join(ROOT, "profiles", "r02", "index_pmc.json")
+INDEX_PMC_DEFAULT = os.path.join(ROOT, "profiles", "r03", "index_pmc.json")
 
 
 def index_points(mq, seg, mode, settings, args):

@@ -145,26 +145,51 @@ __device__ __forceinline__ uint32_t far_byte(const uint8_t *out, int32_t pos) {
     return (w >> (8 * (a & 3))) & 255u;
 }
 
-// The decode loop is one wave's sequential walk over the tokens, so every
-// per-sequence value (input / output positions, lengths, the window base) is
-// wave-uniform and kept in scalar registers (readfirstlane at the loop head):
-// branches are scalar, and no per-lane exec-mask bookkeeping or 64-bit vector
-// compares sit on the sequence chain.  Positions are 32-bit (a block is at
-// most 2^30 bytes; larger ones are rejected as malformed).
+// The decoder stages a block's compressed bytes in LDS kChunk at a time (plus
+// kLook bytes of look-ahead) and parses each chunk with all 64 lanes: the
+// chunk is cut into 64 segments of kSeg bytes and lane i parses the tokens
+// that START in segment i.  A lane cannot know where its first token starts,
+// so it first parses speculatively from each of the segment's first kStarts
+// bytes (pass A), recording each parse's first kSpec token positions with the
+// output / record counts before them: an LZ4 parse started at an arbitrary
+// byte mostly falls into the true token chain within a few tokens.  A uniform walk over the 64 lanes then
+// chains the true entries -- segment i's entry is segment i-1's exit; when
+// the entry is among lane i's recorded positions its exit and counts follow,
+// otherwise the segment is re-parsed from the entry right there -- and each
+// lane re-parses its segment from its true entry (pass B), writing one record
+// per sequence (literal position and length, offset, match length, output
+// position) to LDS.  The records then run in order, up to 64 at a time, one
+// lane per sequence: every literal run at once (they depend on nothing), then
+// the matches in rounds -- a match is copied in the first round in which no
+// unfinished match before it writes its source bytes (the first unfinished
+// one always can be), so each round makes progress.  A match reads
+// byte src + (t mod off) for output byte t, so the replication of an
+// overlapping match (off < length) needs no ordering of its own.  Sequences
+// longer than kGrpLit / kGrpMatch end a group and take wave-wide paths.
+// (The round-2 decoder parsed tokens one at a time in scalar registers: ~500
+// cycles per sequence on quantised floats, 0.25 s for a 3 GB column.)
 //
-// Compressed-input window: two 256-B halves [wa, wa + 256) and [wa + 256,
-// wa + 512) of the block's bytes (offsets from the dword-aligned pa), lane l
-// holding the dword at wa + 4 l of each.  A parse byte is one v_readlane (the
-// offset is uniform); a short literal run is read with one lane shuffle per
-// 64 bytes.  When the parse enters the upper half the window slides by 256 B
-// and loads the next half ahead of its use.
-// DIAG (measurement builds only; wrong output): 1 = parse only (no group
-// copies), 2 = far bytes from the ring (no global reads), 4 = every match in
-// one round (no dependency order)
+// Output goes to an LDS ring only and is flushed to global memory in runs of
+// >= kFlush bytes with dword stores; unflushed bytes stay < kFlush + one
+// group, so the ring never overwrites them and every byte further back than
+// the ring is already in global memory (far matches read it there).  (One
+// wave per workgroup: its LDS accesses complete in program order, so a read
+// after a write sees it; the wave barriers only keep the compiler from moving
+// them.)  Positions are 32-bit (larger blocks are rejected as malformed).
+//
+// DIAG (measurement builds only; wrong output): 1 = parse only (no copies);
+// 2 = staging only, 4 = staging + pass A, 8 = staging + pass A + chain
+// (2, 4, 8: no status)
+constexpr int kChunk = 2048, kLook = 256, kSeg = kChunk / 64, kSpec = 4, kStarts = 4;
+constexpr int kMaxRec = kChunk / 3 + 2;  // tokens starting in a chunk (>= 3 bytes each but the last)
 template <int DIAG>
 __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_t src_bytes, const IngestBlock *tab,
                                                       int64_t nblocks, uint8_t *dst, int *status) {
     __shared__ __attribute__((aligned(16))) uint8_t ring[kRing];
+    __shared__ __attribute__((aligned(16))) uint32_t cinw[(kChunk + kLook) / 4 + 2];
+    __shared__ __attribute__((aligned(16))) uint4 recs[kMaxRec];
+    __shared__ uint16_t roff[kMaxRec];
+    const uint8_t *cin = reinterpret_cast<const uint8_t *>(cinw);
     const uint8_t *src_end = src + src_bytes;
     const int lane = threadIdx.x;
     for (int64_t bi = blockIdx.x; bi < nblocks; bi += gridDim.x) {
@@ -180,43 +205,63 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
         const int32_t mis = (int32_t)((uintptr_t)ip0 & 3);
         const uint8_t *pa = ip0 - mis;  // dword-aligned; stream bytes at [mis, mis + isz)
         const int32_t lim = mis + isz;
-        auto ld = [&](int32_t base) -> uint32_t {
-            const int32_t q = base + 4 * lane;
-            if (q + 4 <= lim) return *reinterpret_cast<const uint32_t *>(pa + q);
-            uint32_t v = 0;
-            for (int k = 0; k < 4; ++k)
-                if (q + k < lim) v |= (uint32_t)pa[q + k] << (8 * k);
-            return v;
+        int32_t cb = 0, clen = 0;  // LDS holds pa bytes [cb, cb + clen)
+        // byte `pos` of the block's compressed stream (per lane; pos < isz)
+        auto B = [&](int32_t pos) -> uint32_t {
+            const int32_t r = mis + pos - cb;
+            return (r >= 0 && r < clen) ? (uint32_t)cin[r] : (uint32_t)ip0[pos];
         };
-        int32_t wa = -1024;
-        uint32_t w0 = 0, w1 = 0;
-        auto cover = [&](int32_t x) {  // afterwards wa <= x < wa + 256
-            if (x >= wa + 256 && x < wa + 512) {
-                wa += 256;
-                w0 = w1;
-                w1 = ld(wa + 256);
-            } else if (x < wa || x >= wa + 256) {
-                wa = x & ~3;
-                w0 = ld(wa);
-                w1 = ld(wa + 256);
+        // one token at p: false when it runs past the stream (or, for a
+        // speculative parse, past the staged bytes: a parse inside a long
+        // literal run must not chase global memory); last = the literals-only
+        // final sequence (its literals end the stream)
+        auto tok = [&](int32_t p, int32_t &lip, int32_t &ll, int32_t &off, int32_t &ml, bool &last, int32_t &next,
+                       bool spec) -> bool {
+            bool miss = false;
+            auto rd = [&](int32_t pos) -> uint32_t {
+                const int32_t r = mis + pos - cb;
+                if (r >= 0 && r < clen) return (uint32_t)cin[r];
+                if (spec) {
+                    miss = true;
+                    return 0u;
+                }
+                return (uint32_t)ip0[pos];
+            };
+            const uint32_t t = rd(p);
+            int32_t q = p + 1;
+            ll = (int32_t)(t >> 4);
+            if (ll == 15) {
+                uint32_t b;
+                do {
+                    if (q >= isz) return false;
+                    b = rd(q++);
+                    ll += (int32_t)b;
+                } while (b == 255 && ll < (1 << 30));
             }
-            wa = __builtin_amdgcn_readfirstlane(wa);
+            if (miss || ll > isz - q) return false;
+            lip = q;
+            q += ll;
+            off = 0;
+            ml = 0;
+            last = q == isz;
+            if (!last) {
+                if (isz - q < 2) return false;
+                off = (int32_t)(rd(q) | (rd(q + 1) << 8));
+                q += 2;
+                ml = (int32_t)(t & 15);
+                if (ml == 15) {
+                    uint32_t b;
+                    do {
+                        if (q >= isz) return false;
+                        b = rd(q++);
+                        ml += (int32_t)b;
+                    } while (b == 255 && ml < (1 << 30));
+                }
+                ml += 4;
+            }
+            next = q;
+            return !miss;
         };
-        auto byte = [&](int32_t ipos) -> uint32_t {
-            const int32_t x = mis + ipos;
-            cover(x);
-            const int32_t o = __builtin_amdgcn_readfirstlane(x - wa);
-            const uint32_t v = o < 256 ? (uint32_t)__builtin_amdgcn_readlane((int)w0, o >> 2)
-                                       : (uint32_t)__builtin_amdgcn_readlane((int)w1, (o - 256) >> 2);
-            return (v >> (8 * (o & 3))) & 255u;
-        };
-        // Output goes to the LDS ring only and is flushed to global memory in
-        // runs of >= kFlush bytes with dword stores; unflushed bytes stay <
-        // kFlush + one step, so the ring never overwrites them and every byte
-        // further back than kRing - 256 is already in global memory.  (One wave per
-        // workgroup: its LDS accesses complete in program order, so a ring
-        // read after a ring write sees it; the wave barriers only keep the
-        // compiler from moving them.)
         int32_t fl = 0;  // out[0, fl) written
         auto flush = [&](int32_t upto) {
             const int32_t oa = (int32_t)((uintptr_t)(out + fl) & 3);
@@ -234,25 +279,18 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
             if (lane < upto - p1) out[p1 + lane] = ring[(p1 + lane) & (kRing - 1)];
             fl = upto;
         };
-        int32_t ip = 0, op = 0;
-        // A sequence too long for a group (see the parse below): literals at
-        // op, the wave-wide paths of the round-2 decoder
+        int32_t op = 0;  // output written to the ring so far (uniform)
+        // a long sequence (wave-wide): literals [lip, lip + len) at op, then
+        // its match
         auto big_literals = [&](int32_t lip, int32_t len) {
-            if (len > 0 && len <= 256) {
-                // short run: its bytes are in the window (no global load)
-                cover(mis + lip);
-                const int32_t o0 = mis + lip - wa;
-                for (int32_t r = 0; r < len; r += 64) {
-                    const int32_t i = r + lane, o = o0 + i;
-                    const uint32_t x0 = __shfl(w0, (o >> 2) & 63), x1 = __shfl(w1, ((o - 256) >> 2) & 63);
-                    if (i < len) ring[(op + i) & (kRing - 1)] = (uint8_t)(((o < 256 ? x0 : x1) >> (8 * (o & 3))) & 255u);
-                }
-            } else if (len > 256) {
-                // long run: straight to global memory (and the ring)
+            if (len > 256) {
                 flush(op);
                 copy_literals(ip0 + lip, src_end, out, op, len, ring, lane);
                 fl = op + len;
+                return;
             }
+            for (int32_t r = 0; r < len; r += 64)
+                if (r + lane < len) ring[(op + r + lane) & (kRing - 1)] = (uint8_t)B(lip + r + lane);
         };
         auto big_match = [&](int32_t off, int32_t mlen) {
             if (off > kRing - 256) {
@@ -277,10 +315,9 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
                     __builtin_amdgcn_wave_barrier();
                 }
             } else {
-                // Chunks of up to 256 bytes: byte op + i equals byte op + i -
-                // m off for any m >= 1 (the copy replicates with period off),
-                // so chunk [d0, d0 + cnt) reads the latest off bytes before it,
-                // [op + d0 - off, op + d0), all final.
+                // chunks of up to 256 bytes: byte op + i equals byte op + i -
+                // m off for any m >= 1, so chunk [d0, d0 + cnt) reads the
+                // latest off bytes before it, all final
                 for (int32_t d0 = 0; d0 < mlen; d0 += 256) {
                     __builtin_amdgcn_wave_barrier();
                     if (op + d0 - fl >= kFlush) {
@@ -304,179 +341,330 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
                 __builtin_amdgcn_wave_barrier();
             }
         };
-        // Parse, then execute, in groups of up to 64 sequences.  The parse is
-        // the block's only sequential chain: it walks the tokens (uniform,
-        // scalar) and leaves sequence g's fields in lane g, no
-        // byte moved.  The group then runs with a lane per sequence: every
-        // literal run at once (they depend on nothing), then the matches in
-        // rounds -- a match whose source bytes end at or below the first
-        // unfinished match's output is copied in the current round (the first
-        // unfinished one always is), so each round makes progress and most
-        // groups finish in a few (on quantised floats ~80 % of the matches
-        // read output older than their group).  A match reads byte
-        // src + (t mod off) for output byte t: the replication of an
-        // overlapping match (off < length) needs no ordering of its own.
-        // Sequences longer than kGrpLit / kGrpMatch end the group and take the
-        // wave-wide paths above.
-        bool last_seen = false;
-        while (!bad && !last_seen) {
-            ip = __builtin_amdgcn_readfirstlane(ip);
+        int32_t E = 0;  // the next true token position (uniform)
+        bool done = false;
+        // the staged words of the next chunk to parse, loaded while the
+        // current one is parsed and run
+        constexpr int kStageW = (kChunk + kLook) / 256 + 1;
+        uint32_t pv[kStageW];
+        int32_t pcs = -1, pcb = 0;
+        auto prefetch = [&](int32_t c) {
+            pcs = c;
+            pcb = (mis + c) & ~3;
+#pragma unroll
+            for (int u = 0; u < kStageW; ++u) {
+                const int32_t q = pcb + 4 * (u * 64 + lane);
+                pv[u] = 0;
+                if (q + 4 <= lim) {
+                    pv[u] = *reinterpret_cast<const uint32_t *>(pa + q);
+                } else {
+                    for (int k = 0; k < 4; ++k)
+                        if (q + k < lim) pv[u] |= (uint32_t)pa[q + k] << (8 * k);
+                }
+            }
+        };
+        if (isz > 0) prefetch(0);
+        int32_t ncs = 0;
+        for (int32_t cs = 0; cs < isz && !bad && !done; cs = ncs) {
+            E = __builtin_amdgcn_readfirstlane(E);
             op = __builtin_amdgcn_readfirstlane(op);
             fl = __builtin_amdgcn_readfirstlane(fl);
-            int32_t g = 0, rel = 0;
-            int32_t vpk = 0, vrel = 0, vlip = 0;
-            bool big = false;
-            int32_t b_lip = 0, b_ll = 0, b_off = 0, b_ml = 0;
-            while (g < 64) {
-                ip = __builtin_amdgcn_readfirstlane(ip);
-                rel = __builtin_amdgcn_readfirstlane(rel);
-                const int32_t o = op + rel;
-                if (ip >= isz) {
-                    bad = true;
-                    break;
+            ncs = cs + kChunk;
+            if (E >= cs + kChunk) continue;  // inside a long literal run
+            // ---- stage [cs, cs + kChunk + kLook) of the stream
+            if (pcs != cs) prefetch(cs);
+            __builtin_amdgcn_wave_barrier();
+            cb = pcb;
+            clen = lim - cb < kChunk + kLook + 4 ? lim - cb : kChunk + kLook + 4;
+#pragma unroll
+            for (int u = 0; u < kStageW; ++u)
+                if (u * 64 + lane < (int)(sizeof(cinw) / 4)) cinw[u * 64 + lane] = pv[u];
+            __builtin_amdgcn_wave_barrier();
+            if (DIAG & 2) continue;
+            const int32_t s0 = cs + kSeg * lane, s1 = s0 + kSeg;  // this lane's segment
+            // ---- pass A: speculative parses of the segment from its first
+            // kStarts bytes (one start per byte: on quantised floats, tokens
+            // of 3 bytes, a parse started in the wrong byte phase stays in it
+            // -- offsets below 4096 read as tokens without literals -- and
+            // missed the true chain for 2 of 3 segments; from 4 starts the
+            // true entry is a start or a recorded position for 99.9 %)
+            int32_t rp[kStarts][kSpec], rc[kStarts][kSpec], xs[kStarts], ts[kStarts], ns[kStarts];
+#pragma unroll
+            for (int c = 0; c < kStarts; ++c) {
+                int32_t x = s0 + c, t = 0, nn = 0;
+#pragma unroll
+                for (int j = 0; j < kSpec; ++j) {
+                    rp[c][j] = -1;
+                    rc[c][j] = 0;
                 }
-                const uint32_t token = byte(ip++);
-                int32_t ll = (int32_t)(token >> 4);
-                if (ll == 15) {
-                    uint32_t sb;
-                    do {
-                        if (ip >= isz) {
+                if (s1 > E) {
+                    while (x < s1 && x < isz) {
+#pragma unroll
+                        for (int j = 0; j < kSpec; ++j)
+                            if (nn == j) {
+                                rp[c][j] = x;
+                                rc[c][j] = t;
+                            }
+                        int32_t lip, ll, off, ml, nx;
+                        bool last;
+                        if (!tok(x, lip, ll, off, ml, last, nx, true)) {
+                            x = -1;  // runs off the stream: not the true chain
+                            break;
+                        }
+                        t += ll + ml;
+                        ++nn;
+                        x = nx;
+                        if (last) break;
+                    }
+                }
+                xs[c] = x;
+                ts[c] = t;
+                ns[c] = nn;
+            }
+            if (DIAG & 4) {
+                if (__ballot(xs[0] == 12345 && ts[1] == 7 && ns[2] == 9 && xs[3] == 3) != 0) bad = true;
+                continue;
+            }
+            // ---- the true chain over the segments (uniform)
+            int32_t vE = 0, vO = 0, vR = 0;
+            int32_t R = 0, O = op;
+            for (int i = 0; i < 64 && !bad; ++i) {
+                const int32_t si = cs + kSeg * i, ei = si + kSeg;
+                vE = lane == i ? E : vE;
+                vO = lane == i ? O : vO;
+                vR = lane == i ? R : vR;
+                if (E >= ei || E >= isz) continue;  // no true token starts in segment i
+                bool hit = false;
+                const int32_t dl = E - si;
+                if (dl < kStarts) {
+                    // the common case: a parse started at the entry
+                    int32_t hx = -1, ht = 0, hn = 0;
+#pragma unroll
+                    for (int c = 0; c < kStarts; ++c)
+                        if (c == dl) {
+                            hx = __builtin_amdgcn_readlane(xs[c], i);
+                            ht = __builtin_amdgcn_readlane(ts[c], i);
+                            hn = __builtin_amdgcn_readlane(ns[c], i);
+                        }
+                    if (hx >= 0) {
+                        hit = true;
+                        O += ht;
+                        R += hn;
+                        E = hx;
+                    }
+                }
+                if (!hit) {
+                    // a later recorded position of some parse
+#pragma unroll
+                    for (int c = 0; c < kStarts; ++c)
+#pragma unroll
+                        for (int j = 1; j < kSpec; ++j) {
+                            if (hit) continue;
+                            const int32_t nc = __builtin_amdgcn_readlane(ns[c], i);
+                            const int32_t xc = __builtin_amdgcn_readlane(xs[c], i);
+                            if (j < nc && xc >= 0 && __builtin_amdgcn_readlane(rp[c][j], i) == E) {
+                                hit = true;
+                                O += __builtin_amdgcn_readlane(ts[c], i) - __builtin_amdgcn_readlane(rc[c][j], i);
+                                R += nc - j;
+                                E = xc;
+                            }
+                        }
+                }
+                if (!hit) {
+                    // no parse met the entry: re-parse the segment here
+                    // (uniform arguments: every lane computes the same)
+                    int32_t p = E;
+                    while (p < ei && p < isz) {
+                        int32_t lip, ll, off, ml, nx;
+                        bool last;
+                        if (!tok(p, lip, ll, off, ml, last, nx, false)) {
                             bad = true;
                             break;
                         }
-                        sb = byte(ip++);
-                        ll += (int32_t)sb;
-                    } while (sb == 255 && ll < (1 << 30));
-                    if (bad) break;
-                }
-                if (ll > osz - o || ll > isz - ip) {
-                    bad = true;
-                    break;
-                }
-                const int32_t lip = ip;
-                ip += ll;
-                int32_t off = 0, ml = 0;
-                const bool last = o + ll == osz;  // the block's final, literals-only sequence
-                if (!last) {
-                    if (isz - ip < 2) {
-                        bad = true;
-                        break;
+                        O += ll + ml;
+                        ++R;
+                        p = __builtin_amdgcn_readfirstlane(nx);
+                        if (last) break;
                     }
-                    off = (int32_t)(byte(ip) | (byte(ip + 1) << 8));
-                    ip += 2;
-                    if (off == 0 || off > o + ll) {
-                        bad = true;
-                        break;
-                    }
-                    ml = (int32_t)(token & 15);
-                    if (ml == 15) {
-                        uint32_t sb;
-                        do {
-                            if (ip >= isz) {
-                                bad = true;
-                                break;
-                            }
-                            sb = byte(ip++);
-                            ml += (int32_t)sb;
-                        } while (sb == 255 && ml < (1 << 30));
-                        if (bad) break;
-                    }
-                    ml += 4;
-                    if (ml > osz - o - ll) {
-                        bad = true;
-                        break;
-                    }
+                    E = p;
                 }
-                last_seen = last;
-                if (ll > kGrpLit || ml > kGrpMatch) {
-                    big = true;
-                    b_lip = lip;
-                    b_ll = ll;
-                    b_off = off;
-                    b_ml = ml;
-                    break;
-                }
-                const int32_t pk = (int32_t)((uint32_t)off | ((uint32_t)ll << 16) | ((uint32_t)ml << 22));
-                const bool mine = lane == g;  // (one compare, three v_cndmask)
-                vpk = mine ? pk : vpk;
-                vrel = mine ? rel : vrel;
-                vlip = mine ? lip : vlip;
-                rel += ll + ml;
-                ++g;
-                if (last) break;
+                E = __builtin_amdgcn_readfirstlane(E);
+                O = __builtin_amdgcn_readfirstlane(O);
+                R = __builtin_amdgcn_readfirstlane(R);
             }
-            if (bad) break;
-            g = __builtin_amdgcn_readfirstlane(g);
-            rel = __builtin_amdgcn_readfirstlane(rel);
-            if (g > 0 && (DIAG & 1) == 0) {
-                const bool act = lane < g;
-                const uint32_t pk = (uint32_t)vpk;
-                const int32_t off = act ? (int32_t)(pk & 0xffffu) : 0;
-                const int32_t ll = act ? (int32_t)((pk >> 16) & 63u) : 0;
-                const int32_t ml = act ? (int32_t)(pk >> 22) : 0;
-                const int32_t dst = op + vrel;  // the sequence's literals
-                const int32_t mdst = dst + ll;  // its match
-                // literal runs: bytes of the compressed input (cached: the
-                // parse window just read them)
-                for (int32_t t0 = 0; __ballot(ll > t0) != 0; t0 += 8) {
-                    uint32_t v[8];
-#pragma unroll
-                    for (int u = 0; u < 8; ++u) v[u] = t0 + u < ll ? (uint32_t)ip0[vlip + t0 + u] : 0u;
-#pragma unroll
-                    for (int u = 0; u < 8; ++u)
-                        if (t0 + u < ll) ring[(dst + t0 + u) & (kRing - 1)] = (uint8_t)v[u];
+            if (bad || R > kMaxRec) {
+                bad = true;
+                break;
+            }
+            if (DIAG & 8) {
+                if (__ballot(vE == 12345 && vO == 7 && vR == 9) != 0) bad = true;
+                E = cs + kChunk;
+                continue;
+            }
+            // ---- pass B: records from the true entries
+            bool lbad = false;
+            {
+                int32_t p = vE, o = vO, r = vR;
+                while (p < s1 && p < isz) {
+                    int32_t lip, ll, off, ml, nx;
+                    bool last;
+                    if (!tok(p, lip, ll, off, ml, last, nx, false) || ll > osz - o || (!last && (off == 0 || off > o + ll)) ||
+                        ml > osz - o - ll || r >= kMaxRec) {
+                        lbad = true;
+                        break;
+                    }
+                    recs[r] = uint4{(uint32_t)lip, (uint32_t)o, (uint32_t)ll, (uint32_t)ml};
+                    roff[r] = (uint16_t)off;
+                    ++r;
+                    o += ll + ml;
+                    p = nx;
+                    if (last) break;
                 }
-                // bytes below far_lim may be overwritten in the ring by this
-                // group: they come from the flushed output (all of it is: the
-                // unflushed tail is < kFlush bytes behind the group's start)
-                const int32_t far_lim = op + rel - kRing;
-                const int32_t src = mdst - off;
-                const int32_t need_end = off < ml ? mdst : src + ml;
-                if ((DIAG & 2) == 0 && __ballot(ml > 0 && src < far_lim) != 0)
-                    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-                bool fin = ml == 0;
-                while (true) {
-                    const uint64_t und = __ballot(!fin);
-                    if (und == 0) break;
-                    const int32_t lo = __builtin_amdgcn_readlane(mdst, (int)__builtin_ctzll(und));
-                    const bool go = !fin && ((DIAG & 4) != 0 || need_end <= lo);
-                    if (go) {
-                        int32_t k = 0;  // (t mod off)
-                        for (int32_t t0 = 0; t0 < ml; t0 += 12) {
-                            uint32_t v[12];
+            }
+            if (__ballot(lbad) != 0) {
+                bad = true;
+                break;
+            }
+            done = E >= isz;
+            // the next chunk holding a token start: its bytes load while this
+            // one's records are written and run
+            ncs = E - E % kChunk > cs ? E - E % kChunk : cs + kChunk;
+            if (!done) prefetch(ncs);
+            __builtin_amdgcn_wave_barrier();
+            if (DIAG & 1) {
+                op = O;
+                continue;
+            }
+            // ---- run the records, up to 64 at a time
+            for (int32_t r0 = 0; r0 < R;) {
+                r0 = __builtin_amdgcn_readfirstlane(r0);
+                op = __builtin_amdgcn_readfirstlane(op);
+                const int32_t jr = r0 + lane;
+                uint4 rec = uint4{0u, (uint32_t)op, 0u, 0u};
+                int32_t off = 0;
+                if (jr < R) {
+                    rec = recs[jr];
+                    off = roff[jr];
+                }
+                const int32_t ll = (int32_t)rec.z, ml = (int32_t)rec.w;
+                const bool live = jr < R;
+                const uint64_t bm = __ballot(live && (ll > kGrpLit || ml > kGrpMatch));
+                const int32_t avail = R - r0 < 64 ? R - r0 : 64;
+                const int g = bm ? (int)__builtin_ctzll(bm) : avail;
+                if (g > 0) {
+                    const bool act = lane < g;
+                    const int32_t dst_ = (int32_t)rec.y;  // the sequence's literals
+                    const int32_t gl = act ? ll : 0, gm = act ? ml : 0;
+                    const int32_t mdst = dst_ + gl;  // its match
+                    const int32_t gend = __builtin_amdgcn_readlane(mdst + gm, g - 1);
+                    // literal runs (bytes of the staged input, mostly)
+                    for (int32_t t0 = 0; __ballot(gl > t0) != 0; t0 += 8) {
+                        uint32_t v[8];
 #pragma unroll
-                            for (int u = 0; u < 12; ++u) {
-                                v[u] = 0;
-                                if (t0 + u < ml) {
-                                    const int32_t q = src + k;
-                                    v[u] = (DIAG & 2) != 0 || q >= far_lim ? (uint32_t)ring[q & (kRing - 1)]
-                                                                           : far_byte(out, q);
-                                    k = k + 1 == off ? 0 : k + 1;
+                        for (int u = 0; u < 8; ++u) v[u] = t0 + u < gl ? B((int32_t)rec.x + t0 + u) : 0u;
+#pragma unroll
+                        for (int u = 0; u < 8; ++u)
+                            if (t0 + u < gl) ring[(dst_ + t0 + u) & (kRing - 1)] = (uint8_t)v[u];
+                    }
+                    // bytes below far_lim may be overwritten in the ring by
+                    // this group: they come from the flushed output (all of
+                    // it is: the unflushed tail is < kFlush bytes behind the
+                    // group's start)
+                    const int32_t far_lim = gend - kRing;
+                    const int32_t srcp = mdst - off;
+                    const bool far = gm > 0 && srcp < far_lim;
+                    // far matches: their bytes, as dwords of the flushed
+                    // output re-aligned to the source (off > gm: no
+                    // replication), loaded before the rounds
+                    uint32_t fw[kGrpMatch / 4 + 1];
+#pragma unroll
+                    for (int i = 0; i < kGrpMatch / 4 + 1; ++i) fw[i] = 0;
+                    if (__ballot(far) != 0) {
+                        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // (the flushes landed)
+                        const uintptr_t fa = (uintptr_t)(out + (far ? srcp : 0));
+                        const uint32_t *wp = reinterpret_cast<const uint32_t *>(fa & ~(uintptr_t)3);
+                        const uint32_t sh = (uint32_t)(fa & 3);
+                        uint32_t raw[kGrpMatch / 4 + 2];
+#pragma unroll
+                        for (int i = 0; i < kGrpMatch / 4 + 2; ++i)
+                            raw[i] = far && 4 * i < gm + (int)sh
+                                         ? __hip_atomic_load(wp + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)
+                                         : 0u;
+#pragma unroll
+                        for (int i = 0; i < kGrpMatch / 4 + 1; ++i) fw[i] = __builtin_amdgcn_alignbyte(raw[i + 1], raw[i], sh);
+                    }
+                    // A match is copied once no unfinished match writes its
+                    // source bytes: the lanes before it whose match ends
+                    // past its source start (a binary search over the lanes'
+                    // ordered match ends), [kl, lane).  Literal bytes are all
+                    // written already.
+                    // (sources before the group -- far ones included -- and the
+                    // replicated prefix of an overlapping match: no lanes)
+                    const int32_t need_end = off < gm ? mdst : srcp + gm;
+                    const int32_t mend = mdst + gm;
+                    int kl = 0, kh = 0;  // lanes [kl, kh): match end > srcp, match start < need_end
+#pragma unroll
+                    for (int st = 32; st >= 1; st >>= 1) {
+                        const int cl = kl + st - 1, ch = kh + st - 1;
+                        const int32_t el = __shfl(mend, cl < 64 ? cl : 63);
+                        const int32_t sh_ = __shfl(mdst, ch < 64 ? ch : 63);
+                        if (kl + st <= lane && el <= srcp) kl += st;
+                        if (kh + st <= lane && sh_ < need_end) kh += st;
+                    }
+                    auto below = [](int x) -> uint64_t { return x <= 0 ? 0ull : (~0ull >> (64 - x)); };
+                    const uint64_t deps = kh > kl ? below(kh) & ~below(kl) : 0ull;
+                    bool fin = gm == 0;
+                    while (true) {
+                        const uint64_t und = __ballot(!fin);
+                        if (und == 0) break;
+                        const bool go = !fin && (und & deps) == 0;
+                        if (go) {
+                            int32_t k = 0;  // (t mod off)
+#pragma unroll
+                            for (int c = 0; c < (kGrpMatch + 11) / 12; ++c) {
+                                if (12 * c >= gm) break;
+                                uint32_t v[12];
+#pragma unroll
+                                for (int u = 0; u < 12; ++u) {
+                                    const int t = 12 * c + u;
+                                    v[u] = 0;
+                                    if (t < gm) {
+                                        v[u] = far ? (fw[t >> 2] >> (8 * (t & 3))) & 255u
+                                                   : (uint32_t)ring[(srcp + k) & (kRing - 1)];
+                                        k = k + 1 == off ? 0 : k + 1;
+                                    }
                                 }
-                            }
 #pragma unroll
-                            for (int u = 0; u < 12; ++u)
-                                if (t0 + u < ml) ring[(mdst + t0 + u) & (kRing - 1)] = (uint8_t)v[u];
+                                for (int u = 0; u < 12; ++u)
+                                    if (12 * c + u < gm) ring[(mdst + 12 * c + u) & (kRing - 1)] = (uint8_t)v[u];
+                            }
                         }
+                        fin = fin || go;
                     }
-                    fin = fin || go;
+                    __builtin_amdgcn_wave_barrier();
+                    op = gend;
+                    r0 += g;
                 }
-                __builtin_amdgcn_wave_barrier();
-            }
-            op += rel;
-            if (big) {
+                if (bm) {  // the long sequence at lane g
+                    const int32_t blip = __builtin_amdgcn_readlane((int)rec.x, g);
+                    const int32_t bll = __builtin_amdgcn_readlane(ll, g), bml = __builtin_amdgcn_readlane(ml, g);
+                    const int32_t boff = __builtin_amdgcn_readlane(off, g);
+                    if (op - fl >= kFlush) flush(op);
+                    big_literals(blip, bll);
+                    op += bll;
+                    if (bml > 0) {
+                        big_match(boff, bml);
+                        op += bml;
+                    }
+                    r0 += 1;
+                }
                 if (op - fl >= kFlush) flush(op);
-                big_literals(b_lip, b_ll);
-                op += b_ll;
-                if (b_ml > 0) {
-                    big_match(b_off, b_ml);
-                    op += b_ml;
-                }
             }
-            if (op - fl >= kFlush) flush(op);
         }
+        bad = bad || !done || op != osz;
+        if (DIAG & 14) bad = false;
         __builtin_amdgcn_wave_barrier();
-        flush(op);
+        if (!bad) flush(op);
         if (bad && lane == 0) atomicOr(status, 4);
         __syncthreads();
     }
@@ -783,8 +971,10 @@ void launch_decode_blocks(const uint8_t *src, int64_t src_bytes, const IngestBlo
         hipLaunchKernelGGL(k_decode_blocks<1>, dim3(grid), dim3(64), 0, s, src, src_bytes, tab, nblocks, dst, status);
     else if (kDebugTuning && diag == 2)
         hipLaunchKernelGGL(k_decode_blocks<2>, dim3(grid), dim3(64), 0, s, src, src_bytes, tab, nblocks, dst, status);
-    else if (kDebugTuning && diag == 6)
-        hipLaunchKernelGGL(k_decode_blocks<6>, dim3(grid), dim3(64), 0, s, src, src_bytes, tab, nblocks, dst, status);
+    else if (kDebugTuning && diag == 4)
+        hipLaunchKernelGGL(k_decode_blocks<4>, dim3(grid), dim3(64), 0, s, src, src_bytes, tab, nblocks, dst, status);
+    else if (kDebugTuning && diag == 8)
+        hipLaunchKernelGGL(k_decode_blocks<8>, dim3(grid), dim3(64), 0, s, src, src_bytes, tab, nblocks, dst, status);
     else
         hipLaunchKernelGGL(k_decode_blocks<0>, dim3(grid), dim3(64), 0, s, src, src_bytes, tab, nblocks, dst, status);
 }
