@@ -33,11 +33,11 @@ namespace mqvs {
 // wave, and a 64 KiB ring left two waves per CU.  Matches reaching further
 // back (~6 % of them on quantised float columns) read the already-flushed
 // output from global memory (far_byte).
-constexpr int kRing = 8192;
-constexpr int kFlush = 2048;  // unflushed output < kFlush + one step (< kRing - 256)
+constexpr int kRing = 4096;
+constexpr int kFlush = 1024;  // unflushed output < kFlush + one step (< kRing - 256)
 // a group holds sequences of at most kGrpLit literals and kGrpMatch match
 // bytes: 64 of them write < kRing - kFlush - 256 bytes
-constexpr int kGrpLit = 32, kGrpMatch = 36;
+constexpr int kGrpLit = 16, kGrpMatch = 27;
 static_assert(64 * (kGrpLit + kGrpMatch) + kFlush + 256 < kRing, "group output must fit the ring");
 
 __global__ void k_block_table(const uint8_t *src, int64_t n, IngestBlock *tab, int64_t max_blocks,
@@ -180,7 +180,7 @@ __device__ __forceinline__ uint32_t far_byte(const uint8_t *out, int32_t pos) {
 // DIAG (measurement builds only; wrong output): 1 = parse only (no copies);
 // 2 = staging only, 4 = staging + pass A, 8 = staging + pass A + chain
 // (2, 4, 8: no status)
-constexpr int kChunk = 2048, kLook = 256, kSeg = kChunk / 64, kSpec = 4, kStarts = 4;
+constexpr int kChunk = 1024, kLook = 256, kSeg = kChunk / 64, kSpec = 4, kStarts = 4;
 constexpr int kMaxRec = kChunk / 3 + 2;  // tokens starting in a chunk (>= 3 bytes each but the last)
 template <int DIAG>
 __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_t src_bytes, const IngestBlock *tab,
@@ -343,27 +343,6 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
         };
         int32_t E = 0;  // the next true token position (uniform)
         bool done = false;
-        // the staged words of the next chunk to parse, loaded while the
-        // current one is parsed and run
-        constexpr int kStageW = (kChunk + kLook) / 256 + 1;
-        uint32_t pv[kStageW];
-        int32_t pcs = -1, pcb = 0;
-        auto prefetch = [&](int32_t c) {
-            pcs = c;
-            pcb = (mis + c) & ~3;
-#pragma unroll
-            for (int u = 0; u < kStageW; ++u) {
-                const int32_t q = pcb + 4 * (u * 64 + lane);
-                pv[u] = 0;
-                if (q + 4 <= lim) {
-                    pv[u] = *reinterpret_cast<const uint32_t *>(pa + q);
-                } else {
-                    for (int k = 0; k < 4; ++k)
-                        if (q + k < lim) pv[u] |= (uint32_t)pa[q + k] << (8 * k);
-                }
-            }
-        };
-        if (isz > 0) prefetch(0);
         int32_t ncs = 0;
         for (int32_t cs = 0; cs < isz && !bad && !done; cs = ncs) {
             E = __builtin_amdgcn_readfirstlane(E);
@@ -372,13 +351,27 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
             ncs = cs + kChunk;
             if (E >= cs + kChunk) continue;  // inside a long literal run
             // ---- stage [cs, cs + kChunk + kLook) of the stream
-            if (pcs != cs) prefetch(cs);
             __builtin_amdgcn_wave_barrier();
-            cb = pcb;
+            cb = (mis + cs) & ~3;
             clen = lim - cb < kChunk + kLook + 4 ? lim - cb : kChunk + kLook + 4;
+            {
+                constexpr int kStageW = (kChunk + kLook) / 256 + 1;
+                uint32_t v[kStageW];
 #pragma unroll
-            for (int u = 0; u < kStageW; ++u)
-                if (u * 64 + lane < (int)(sizeof(cinw) / 4)) cinw[u * 64 + lane] = pv[u];
+                for (int u = 0; u < kStageW; ++u) {
+                    const int32_t q = cb + 4 * (u * 64 + lane);
+                    v[u] = 0;
+                    if (q + 4 <= lim) {
+                        v[u] = *reinterpret_cast<const uint32_t *>(pa + q);
+                    } else {
+                        for (int k = 0; k < 4; ++k)
+                            if (q + k < lim) v[u] |= (uint32_t)pa[q + k] << (8 * k);
+                    }
+                }
+#pragma unroll
+                for (int u = 0; u < kStageW; ++u)
+                    if (u * 64 + lane < (int)(sizeof(cinw) / 4)) cinw[u * 64 + lane] = v[u];
+            }
             __builtin_amdgcn_wave_barrier();
             if (DIAG & 2) continue;
             const int32_t s0 = cs + kSeg * lane, s1 = s0 + kSeg;  // this lane's segment
@@ -426,14 +419,15 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
                 continue;
             }
             // ---- the true chain over the segments (uniform)
-            int32_t vE = 0, vO = 0, vR = 0;
+            // (segments without a true token start keep vE = isz: no pass B;
+            // the walk visits only the segments the chain enters)
+            int32_t vE = isz, vO = 0, vR = 0;
             int32_t R = 0, O = op;
-            for (int i = 0; i < 64 && !bad; ++i) {
+            for (int i = (E - cs) / kSeg; i < 64 && E < isz && !bad; i = (E - cs) / kSeg) {
                 const int32_t si = cs + kSeg * i, ei = si + kSeg;
                 vE = lane == i ? E : vE;
                 vO = lane == i ? O : vO;
                 vR = lane == i ? R : vR;
-                if (E >= ei || E >= isz) continue;  // no true token starts in segment i
                 bool hit = false;
                 const int32_t dl = E - si;
                 if (dl < kStarts) {
@@ -526,10 +520,8 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
                 break;
             }
             done = E >= isz;
-            // the next chunk holding a token start: its bytes load while this
-            // one's records are written and run
+            // the next chunk holding a token start
             ncs = E - E % kChunk > cs ? E - E % kChunk : cs + kChunk;
-            if (!done) prefetch(ncs);
             __builtin_amdgcn_wave_barrier();
             if (DIAG & 1) {
                 op = O;

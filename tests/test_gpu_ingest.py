@@ -43,7 +43,7 @@ def column_files(data_f32, sizes, block=1 << 20, method=0x82):
                                                ("mixed", 70000, 0x82)])
 def test_gpu_ingest_dense(mq, kind, block, method):
     """periodNk: the rows repeat every N KiB, so nearly every match reaches
-    back further than the decoder's 8 KiB LDS ring (its far-match path reads
+    back further than the decoder's 4 KiB LDS ring (its far-match path reads
     the block's flushed output), long matches included.  mixed: 16-float
     pieces of four kinds (fresh gaussian = literal runs of every length,
     quantised = short matches, copies of a recent piece = longer and
