@@ -355,434 +355,6 @@ __global__ __launch_bounds__(256 * WQ) void k_scan_hi(ScanParams p) {
         }
 }
 
-// ---------------------------------------------------------------------------
-// Persistent ping-pong scan (batch APPEND, Cosine / IP, contiguous rows).
-//
-// Measured on k_scan_hi (10M rows, nq 1000, d 256 .. 1536): main-scan time
-// = ~6 ms + ~5 ms per 256 dimensions, i.e. every workgroup pays ~10 us outside
-// its K loop (a cold prologue that waits for its first stages, the epilogue,
-// the launch), a third of the search at d = 768.  Here one workgroup per CU
-// walks a sequence of (row tile, query block) items, and the LDS-DMA stage
-// ring runs ACROSS items: the next item's first stages are in flight while
-// the current item's last stages and epilogue run.  The two waves of each
-// SIMD (query halves wq = 0 / 1) run one barrier apart (read phase of one
-// against MFMA phase of the other, see k_scan_hi's PP notes).
-//
-// Epilogue without global memory: values over the query's threshold go to an
-// LDS queue (ds atomics only), flushed to the candidate lists once at the end
-// of the launch -- a global atomic's returned slot would make the wave wait
-// for every LDS-DMA piece issued before it.  Thresholds and the cosine
-// variant cycle of the workgroup's queries are loaded once (a workgroup keeps
-// one query block).  A full queue falls back to the global append.
-//
-// Items: XCD x = blockIdx % 8 holds the tiles t = x (mod 8); its S slots split
-// into S / nqb groups of nqb query blocks, group g taking tiles
-// x + 8 (g + (S / nqb) i): the query blocks of a tile run together on one XCD
-// and share its rows through that L2.
-constexpr int kPpQueue = 1984;  // LDS candidate queue entries (16 B)
-
-struct PpEntry {
-    float raw;
-    uint32_t row;
-    int j;
-    int pad;
-};
-
-// LDS queue append by inline asm: a compiler-visible LDS access here would
-// get a wait for every LDS-DMA piece in flight (the waitcnt pass cannot tell
-// that the queue and the stage ring do not overlap)
-__device__ inline int lds_add_rtn(const void *addr, int v) {
-    int r;
-    const unsigned a = (unsigned)(size_t)(lds_void *)addr;
-    asm volatile("ds_add_rtn_u32 %0, %1, %2\n\ts_waitcnt lgkmcnt(0)" : "=v"(r) : "v"(a), "v"(v) : "memory");
-    return r;
-}
-__device__ inline void lds_store_b128(const void *addr, float x, uint32_t y, int z) {
-    const unsigned a = (unsigned)(size_t)(lds_void *)addr;
-    typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-    const u32x4 v = {__builtin_bit_cast(unsigned, x), y, (unsigned)z, 0u};
-    asm volatile("ds_write_b128 %0, %1" ::"v"(a), "v"(v) : "memory");
-}
-
-// DIAG (diagnostic builds, wrong results; MQVS_HI_PPDIAG): 1 = row pieces
-// from the first 8 tiles only (L2-resident rows), 4 = query pieces not
-// issued, 8 = row pieces not issued, 16 = a trivial epilogue (the MFMAs stay
-// live: one compare of an accumulator sum per item), 32 = the threshold
-// pre-check as OR-ed compares instead of a max tree (an A/B variant: exact),
-// 64 = row pieces with the non-temporal policy (aux nt; an A/B variant: exact),
-// 256 = SYNC: the query blocks of a row tile kept within kPpLag items of each
-// other (an A/B variant: exact).  They run on different CUs of one XCD and
-// share the tile through its L2 only while they stream it at about the same
-// time; left alone they drift apart over the ~600 items of a launch and each
-// re-reads the rows from beyond the L2 (PMC: 53 GB per search from the L2's
-// misses against 15.2 GB of plane).  Every kPpSyncEvery items wave 0 reads its
-// siblings' progress words (scalar loads: lgkmcnt, so no wait on the LDS-DMA
-// ring) and sleeps while one is more than kPpLag items behind -- for at most
-// kPpSpin rounds, so the result never depends on it and nothing can deadlock.
-constexpr int kPpSyncEvery = 4, kPpLag = 1, kPpSpin = 64;
-__device__ unsigned g_pp_prog[2048];  // per workgroup: epoch << 16 | items done
-
-__device__ inline unsigned sload_glc(const unsigned *ptr) {
-    unsigned v;
-    asm volatile("s_load_dword %0, %1, 0x0 glc\n\ts_waitcnt lgkmcnt(0)" : "=s"(v) : "s"(ptr) : "memory");
-    return v;
-}
-
-template <int METRIC, int NBUF, int DIAG = 0>
-__global__ __launch_bounds__(512) void k_scan_hi_pp(ScanParams p, int slots, unsigned epoch) {
-    constexpr int WR = 4, WQ = 2, QB = 4, NW = 8;
-    constexpr int QT = 32 * QB * WQ;  // 256
-    constexpr int RT = kBfRows;       // 256
-    constexpr int GY = RT / 16, GQ = QT / 16, G = GY + GQ;
-    constexpr int GPW = G / NW;       // 4 pieces per wave and stage
-    constexpr int YPW = GY / NW;      // 2 of them row pieces
-    constexpr int STAGE = G * 1024;
-    constexpr int D = NBUF - 2;       // stages in flight ahead of the one read
-    static_assert(D >= 1 && GY % NW == 0, "shape");
-    constexpr int NPW = GPW - ((DIAG & 8) ? YPW : 0) - ((DIAG & 4) ? GPW - YPW : 0);  // pieces per wave, stage
-    // ONE __shared__ object: the stage ring, the candidate queue and its
-    // counter (an LDS access to a second object after an LDS-DMA makes the
-    // compiler wait for every DMA in flight, cdna_hip_programming.md)
-    __shared__ __attribute__((aligned(16))) unsigned char lds[NBUF * STAGE + kPpQueue * 16 + 16];
-    PpEntry *queue = reinterpret_cast<PpEntry *>(lds + NBUF * STAGE);
-    int &qcount = *reinterpret_cast<int *>(lds + NBUF * STAGE + kPpQueue * 16);
-
-    const int t = threadIdx.x, lane = t & 63, w = t >> 6;
-    const int wr = w % WR, wq = w / WR;
-    const int grp = wq;  // waves w and w + 4 share a SIMD
-    const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
-    const int nqb = p.num_qblocks;
-    const int ngroups = slots / nqb;
-    if (slot >= ngroups * nqb) return;  // whole workgroup, before any barrier
-    const int qb = slot % nqb, tg = slot / nqb;
-    const int q0 = qb * QT;
-    const int64_t tstride = 8 * (int64_t)ngroups;
-    const int nb = (int)(p.dpad / HI_K);
-    const int nst = nb;
-    if (t == 0) qcount = 0;
-
-    // per-lane constants: the two query rows of this wave's Q pieces (their
-    // variant cycle), the four query columns of its accumulators (thresholds)
-    int qj[2], qmu[2] = {0, 0}, qlam[2] = {1, 1};
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-        int j = q0 + (w + i * NW) * 16 + (lane >> 2);
-        if (j >= p.nq) j = 0;
-        qj[i] = j;
-        if (p.maxv > 1) {
-            qmu[i] = p.qmu[j];
-            qlam[i] = p.qlam[j];
-        }
-        asm volatile("" : "+v"(qmu[i]), "+v"(qlam[i]));  // (the loads' waits land here, before the ring)
-    }
-    const int h = lane >> 5, l32 = lane & 31;
-    const int ra0 = wr * 64 + l32;
-    const int rq0 = wq * 32 * QB + l32;
-    float thr[QB];
-#pragma unroll
-    for (int jb = 0; jb < QB; ++jb) {
-        const int j = q0 + rq0 + jb * 32;
-        thr[jb] = j < p.nq ? p.thr[j] : __builtin_inff();  // (never taken)
-        asm volatile("" : "+v"(thr[jb]));
-    }
-
-    // item cursor helpers (items are tiles of this slot's sequence)
-    // 32-bit tile arithmetic when the part allows it: tile_range's 64-bit
-    // divisions are software sequences of ~120 instructions, three per call,
-    // and an item boundary runs two of these calls (the issue cursor in a read
-    // phase, the compute cursor after the epilogue), exposed to the partner
-    // wave at the barrier.  (DIAG & 1024: tile_range, an A/B variant.)
-    const bool t32 = (DIAG & 1024) == 0 && p.row_end + p.chunk_rows + p.tile_rows <= 0x7FFFFFFF &&
-                     p.tiles <= 0x7FFFFFFF && p.row_begin >= 0;
-    const uint32_t c0_32 = (t32 && p.tiles_per_chunk > 0) ? (uint32_t)p.row_begin / (uint32_t)p.chunk_rows : 0u;
-    auto item_range = [&](int64_t ti, int64_t &r0, int64_t &r1, int &ord) -> bool {
-        int64_t chunk;
-        if (t32) {
-            const uint32_t tt = (uint32_t)ti, tr = (uint32_t)p.tile_rows;
-            if (p.tiles_per_chunk > 0) {
-                const uint32_t tpc = (uint32_t)p.tiles_per_chunk, cr = (uint32_t)p.chunk_rows;
-                const uint32_t qd = tt / tpc, rem = tt - qd * tpc;
-                const uint32_t c = c0_32 + qd, cs = c * cr;
-                const uint32_t a = cs + rem * tr;
-                const uint32_t e = a + tr < cs + cr ? a + tr : cs + cr;
-                r0 = a;
-                r1 = e;
-                chunk = c;
-            } else {
-                const uint32_t a = (uint32_t)p.row_begin + tt * tr;
-                r0 = a;
-                r1 = (int64_t)a + tr;
-                chunk = p.chunk_rows > 0 ? a / (uint32_t)p.chunk_rows : 0;
-            }
-            if (r1 > p.row_end) r1 = p.row_end;
-        } else {
-            tile_range(p, ti, r0, r1, chunk);
-        }
-        ord = (int)chunk + p.ord_base;  // (no chunk_ord table on this path)
-        return r0 < r1;
-    };
-    auto next_item = [&](int64_t ti, int64_t &r0, int64_t &r1, int &ord) -> int64_t {
-        for (; ti < p.tiles; ti += tstride)
-            if (item_range(ti, r0, r1, ord)) return ti;
-        return -1;
-    };
-
-    // issue cursor: item ti_i (rows [ir0, ir1), ordinal iord), next stage si
-    int64_t ir0 = 0, ir1 = 0;
-    int iord = 0;
-    int64_t ti_i = next_item(xcd + 8 * (int64_t)tg, ir0, ir1, iord);
-    if (ti_i < 0) return;  // no work (uniform)
-    const unsigned char *src[GPW];
-    auto set_src = [&]() {
-#pragma unroll
-        for (int i = 0; i < GPW; ++i) {
-            const int g = w + i * NW;
-            const int r = (i < YPW ? g : g - GY) * 16 + (lane >> 2);
-            const int c = hswz(r, lane & 3);
-            int64_t u;
-            const uint16_t *plane;
-            if (i < YPW) {
-                u = ir0 + r < ir1 ? ir0 + r : ir0;  // padding rows: any real row, discarded
-                if (DIAG & 1) u = ((ir0 / RT) & 7) * RT + r;
-                plane = p.rows_hi;
-            } else {
-                const int k = i - YPW;
-                const int var = p.maxv <= 1 ? 0 : (iord < qmu[k] ? iord : qmu[k] + (iord - qmu[k]) % qlam[k]);
-                u = (int64_t)var * p.q_vpad + qj[k];
-                plane = p.q_hi;
-            }
-            src[i] = reinterpret_cast<const unsigned char *>(plane) + ((u >> 4) * nb * 1024 + (u & 15) * 64 + c * 16);
-        }
-    };
-    set_src();
-    int si = 0;
-    int64_t issued = 0;  // stages issued so far (global stage counter)
-    auto issue_next = [&]() {
-        if (ti_i < 0) return;
-        unsigned char *dst = lds + (int)(issued % NBUF) * STAGE;
-#pragma unroll
-        for (int i = 0; i < GPW; ++i) {
-            if ((DIAG & 8) && i < YPW) continue;
-            if ((DIAG & 4) && i >= YPW) continue;
-            if ((DIAG & 64) && i < YPW)
-                __builtin_amdgcn_global_load_lds((const void *)(src[i] + (int64_t)si * 1024),
-                                                 (lds_void *)(dst + (w + i * NW) * 1024), 16, 0, 2);
-            else
-                __builtin_amdgcn_global_load_lds((const void *)(src[i] + (int64_t)si * 1024),
-                                                 (lds_void *)(dst + (w + i * NW) * 1024), 16, 0, 0);
-        }
-        ++issued;
-        if (++si == nst) {
-            si = 0;
-            ti_i = next_item(ti_i + tstride, ir0, ir1, iord);
-            if (ti_i >= 0) set_src();
-        }
-    };
-
-    // compute cursor: item rows [cr0, cr1), stage sc, global stage gc
-    int64_t cr0 = ir0, cr1 = ir1;
-    int64_t ti_c = ti_i;
-    int sc = 0;
-    int64_t gc = 0;
-    unsigned done = 0;  // items finished (SYNC)
-
-    constexpr int OFF_Q = GY * 1024;
-    auto frag = [&](const unsigned char *st, int r, int c) {
-        return *reinterpret_cast<const bf16x8 *>(st + r * 64 + hswz(r, c) * 16);
-    };
-    f32x16 acc[2][QB];
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int jb = 0; jb < QB; ++jb) acc[i][jb] = f32x16{0};
-
-    // prologue: D stages in flight, the first landed for everyone
-    for (int s = 0; s < D; ++s) issue_next();
-    {
-        const int64_t pend = issued - 1 < D - 1 ? issued - 1 : D - 1;
-        wait_vm<NPW, D>((int)pend);
-    }
-    __syncthreads();  // (qcount = 0 visible; no DMA wait hidden in it: all waited above)
-    if (grp == 1) raw_barrier();
-    while (true) {
-        // read phase (the partner wave computes meanwhile): the first half
-        // (16 columns) of the stage's fragments; the second half is read
-        // inside the MFMA phase, after the first half's MFMAs have issued
-        // (keeps the fragments at 24 VGPRs: acc takes 128)
-        const unsigned char *st = lds + (int)(gc % NBUF) * STAGE;
-        bf16x8 ah[2], bh[QB];
-#pragma unroll
-        for (int i = 0; i < 2; ++i) ah[i] = frag(st, ra0 + 32 * i, h);
-#pragma unroll
-        for (int jb = 0; jb < QB; ++jb) bh[jb] = frag(st + OFF_Q, rq0 + 32 * jb, h);
-        __builtin_amdgcn_sched_barrier(0);
-        issue_next();
-        const bool has_next = gc + 1 < issued;
-        // pieces issued after stage gc+1 may stay in flight
-        const int pend = has_next ? (int)(issued - gc - 2) : 0;
-        if (grp == 1 && has_next) wait_vm<NPW, D>(pend);
-        raw_barrier();
-        __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int jb = 0; jb < QB; ++jb)
-                acc[i][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[jb], acc[i][jb], 0, 0, 0);
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < 2; ++i) ah[i] = frag(st, ra0 + 32 * i, 2 + h);
-#pragma unroll
-        for (int jb = 0; jb < QB; ++jb) bh[jb] = frag(st + OFF_Q, rq0 + 32 * jb, 2 + h);
-#pragma unroll
-        for (int i = 0; i < 2; ++i)
-#pragma unroll
-            for (int jb = 0; jb < QB; ++jb)
-                acc[i][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(ah[i], bh[jb], acc[i][jb], 0, 0, 0);
-        __builtin_amdgcn_s_setprio(0);
-        if (++sc == nst) {
-            // item epilogue: values over the threshold -> LDS queue.  A
-            // candidate is rare (a few per item and query block), so each
-            // block of 16 values of a query column is first tested with ONE
-            // compare of their max (v_max3 chains); only a block over the
-            // threshold walks its values (per-value branches everywhere cost
-            // 4 ms at 10M x 768, nq 1000, as much as the LDS-DMA stream; a
-            // ballot-compacted walk measured slower than this one)
-            if (!(DIAG & 16)) {
-                const int crn = (int)(cr1 - cr0);  // rows of the item (<= RT)
-#pragma unroll
-                for (int jb = 0; jb < QB; ++jb)
-#pragma unroll
-                    for (int rb = 0; rb < 2; ++rb) {
-                        // any of the 16 over the threshold (DIAG & 32: 16
-                        // compares OR-ed as lane masks; else an fmaxf tree)
-                        bool any = false;
-                        if constexpr ((DIAG & 32) != 0) {
-#pragma unroll
-                            for (int r = 0; r < 16; ++r) any |= acc[rb][jb][r] >= thr[jb];
-                        } else {
-                            float mx = acc[rb][jb][0];
-#pragma unroll
-                            for (int r = 1; r < 16; ++r) mx = fmaxf(mx, acc[rb][jb][r]);
-                            any = mx >= thr[jb];
-                        }
-                        if (any) {
-                            // (row offsets in the tile as 32-bit values, the
-                            // 64-bit row formed only under the branch behind
-                            // an opaque copy: otherwise the compiler shares
-                            // the rows' addresses in the candidate bitmaps
-                            // across the jb blocks, hoisting 32 of them out
-                            // of the walk and spilling them at every item)
-                            const int j = q0 + rq0 + jb * 32;
-                            const int rlb = wr * 64 + rb * 32 + 4 * h;
-#pragma unroll
-                            for (int r = 0; r < 16; ++r) {
-                                const float raw = acc[rb][jb][r];
-                                const int rl = rlb + (r & 3) + 8 * (r >> 2);
-                                if (raw >= thr[jb] && rl < crn && j < p.nq) {
-                                    int rlo = rl;
-                                    asm volatile("" : "+v"(rlo));
-                                    const int64_t row = cr0 + rlo;
-                                    const int pos = lds_add_rtn(&qcount, 1);
-                                    if (pos < kPpQueue)
-                                        lds_store_b128(queue + pos, raw, (uint32_t)row, j);
-                                    else
-                                        emit_approx<METRIC, false>(p, j, row, row, row_valid(p, row), raw);
-                                }
-                            }
-                        }
-                    }
-            }
-            if (DIAG & 16) {
-                float sum = 0.f;
-#pragma unroll
-                for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-                    for (int jb = 0; jb < QB; ++jb)
-#pragma unroll
-                        for (int r = 0; r < 16; ++r) sum += acc[rb][jb][r];
-                if (sum == -1.2345e-30f) lds_add_rtn(&qcount, 1);
-            }
-#pragma unroll
-            for (int rb = 0; rb < 2; ++rb)
-#pragma unroll
-                for (int jb = 0; jb < QB; ++jb) acc[rb][jb] = f32x16{0};
-            sc = 0;
-            int cord;
-            ti_c = next_item(ti_c + tstride, cr0, cr1, cord);
-            if constexpr ((DIAG & 256) != 0) {
-                ++done;
-                if (w == 0) {
-                    if (lane == 0)
-                        __hip_atomic_store(&g_pp_prog[blockIdx.x], (epoch << 16) | done, __ATOMIC_RELAXED,
-                                           __HIP_MEMORY_SCOPE_AGENT);
-                    if (done % kPpSyncEvery == 0 && nqb > 1) {
-                        for (int it = 0; it < kPpSpin; ++it) {
-                            bool behind = false;
-                            for (int b = 0; b < nqb; ++b) {
-                                if (b == qb) continue;
-                                const unsigned v = sload_glc(&g_pp_prog[xcd + 8 * (tg * nqb + b)]);
-                                if ((v >> 16) != epoch || (v & 0xFFFFu) + kPpLag < done) behind = true;
-                            }
-                            if (!behind) break;
-                            __builtin_amdgcn_s_sleep(8);
-                        }
-                    }
-                }
-            }
-        }
-        ++gc;
-        if (grp == 0 && has_next) wait_vm<NPW, D>(pend);
-        raw_barrier();
-        if (!has_next) break;
-    }
-    if (grp == 0) raw_barrier();
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // (asm queue stores retired)
-    __syncthreads();
-    const int nqueue = qcount < kPpQueue ? qcount : kPpQueue;
-    for (int e = t; e < nqueue; e += 512) {
-        const PpEntry en = queue[e];
-        emit_approx<METRIC, false>(p, en.j, en.row, en.row, row_valid(p, en.row), en.raw);
-    }
-}
-
-template <int METRIC>
-static bool launch_hi_pp(ScanParams p, hipStream_t s) {
-    constexpr int QT = 256;
-    p.num_qblocks = (p.nq + QT - 1) / QT;
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        MQVS_HIP(hipGetDevice(&dev));
-        MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    }
-    const int per_xcd = cus / 8;
-    if (p.num_qblocks > per_xcd || p.tiles < 1) return false;
-    const int slots = per_xcd / p.num_qblocks * p.num_qblocks;
-    const char *dg = tune_env("MQVS_HI_PPDIAG");
-    const int diag = dg ? std::atoi(dg) : 0;
-    static std::atomic<unsigned> launches{0};
-    const unsigned epoch = (launches.fetch_add(1, std::memory_order_relaxed) + 1) & 0xFFFFu;
-    // (the decomposition builds 17 / 20 / 24 / 28 of profiles/r02/pp_decomposition.jsonl
-    // are template arguments too: add their case to run them again)
-#define MQVS_PP(DG_)                                                                                             \
-    hipLaunchKernelGGL((k_scan_hi_pp<METRIC, 4, DG_>), dim3((unsigned)(8 * per_xcd)), dim3(512), 0, s, p, slots, \
-                       epoch)
-    if constexpr (kDebugTuning) {  // (diagnostic variants: measurement builds only)
-        switch (diag) {
-            case 16: MQVS_PP(16); break;
-            case 32: MQVS_PP(32); break;
-            case 64: MQVS_PP(64); break;
-            case 256: MQVS_PP(256); break;
-            case 1024: MQVS_PP(1024); break;
-            default: MQVS_PP(0); break;
-        }
-    } else {
-        MQVS_PP(0);
-    }
-#undef MQVS_PP
-    return true;
-}
-
 // Small batches (nq <= 32): HBM-bound, so no LDS staging at all.  The 256-row
 // tile is 16 row blocks of 16 rows; wave w takes blocks w, w+4, w+8, w+12.  A
 // row block's 32-column stage is ONE contiguous KiB of the row-blocked plane
@@ -952,16 +524,15 @@ static void launch_hi_t(const ScanParams &p, hipStream_t s) {
         if (launch_hi_tuned<METRIC, PROBE>(p, s)) return;
     if constexpr (!PROBE) {
         // batches: the one-wave-per-SIMD persistent scan (kernels_p4.hip) for
-        // contiguous rows and identity chunk ordinals; measurement builds can
-        // select the 8-wave ping-pong kernel instead (MQVS_HI_PP=1) or neither
-        // (MQVS_HI_PP=0)
+        // contiguous rows and identity chunk ordinals (measurement builds:
+        // MQVS_HI_PP=0 selects k_scan_hi instead).  (Round 2's 8-wave
+        // ping-pong kernel k_scan_hi_pp, 16.7 ms at nq 1000 against 13.5, is
+        // retired; profiles/r03/baseline_r02_kernels_ab.jsonl.)
         const int pp = tune_int("MQVS_HI_PP", 2);
         if (p.nq > 128 && pp == 2 && launch_scan_p4(p, METRIC, s)) {
             g_batch_kernel_used = 1;
             return;
         }
-        if constexpr (METRIC != MQVS_METRIC_L2)
-            if (p.nq > 128 && pp == 1 && !p.row_list && !p.chunk_ord && launch_hi_pp<METRIC>(p, s)) return;
     }
     const char *reg = tune_env("MQVS_HI_REG");  // A/B switch (tools/ab_split.py): 0 = LDS kernel only
     const bool use_reg = !(reg && reg[0] == '0');

@@ -8,8 +8,8 @@
 // rows x 256 queries.  Wave (wr, wq) owns 128 rows x 128 queries: 4 x 4
 // accumulators of v_mfma_f32_32x32x16_bf16 = 256 AGPRs, the whole accumulator
 // half of the register file.  Per 32-column stage a wave reads 16 fragments
-// (ds_read_b128) for 32 MFMAs: half the LDS fragment traffic per MFMA of the
-// 8-wave 64 x 128 shape (kernels_hi.hip, k_scan_hi_pp: 12 reads per 16), and
+// (ds_read_b128) for 32 MFMAs: half the LDS fragment traffic per MFMA of
+// round 2's 8-wave 64 x 128 shape (k_scan_hi_pp: 12 reads per 16), and
 // the stage's 32 KiB LDS-DMA image (256 rows + 256 queries x 64 B) is the same.
 //
 // Pipeline (per stage s, global stage counter over the whole launch): the
@@ -41,7 +41,7 @@
 // make the wave wait for every LDS-DMA piece in flight; a full queue falls back
 // to exactly that (correct, slower).
 //
-// Items: as k_scan_hi_pp -- XCD x = blockIdx % 8 takes tiles t = x (mod 8); its
+// Items: XCD x = blockIdx % 8 takes tiles t = x (mod 8); its
 // workgroups form groups of nqb query blocks that stream the same row tiles,
 // so a tile's rows are shared through that XCD's L2.
 #include <atomic>

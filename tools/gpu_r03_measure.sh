@@ -37,6 +37,7 @@ for step in $STEPS; do
           -- python "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu --no-verify --no-index --no-configs \
           --no-config1-points > "$GRAFT_REPO_ROOT/$O/prof_bench.json" 2> "$GRAFT_REPO_ROOT/$O/prof.err" ) \
         || { echo "rocprof failed"; tail -20 $O/prof.err; exit 1; }
+      python tools/pp_per_search.py $O/prof/run_kernel_trace.csv > $O/bench_p4_per_search.txt && tail -4 $O/bench_p4_per_search.txt
       echo "rocprof done" ;;
   esac
 done
