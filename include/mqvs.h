@@ -140,6 +140,21 @@ int mqvs_segment_info(mqvs_segment_t seg, int64_t *n, int32_t *d, int32_t *metri
  * mqvs_segment_info's hbm_bytes); *approx_ok = 1 when the pre-filter serves
  * searches (planes present and the rows' norms finite and moderate). */
 int mqvs_segment_prefilter(mqvs_segment_t seg, int32_t *split, size_t *plane_bytes, int32_t *approx_ok);
+/* Where the segment's Float32 rows live.  host = 1 moves them to pinned host
+ * memory mapped into the device's address space: HBM then holds the bf16
+ * pre-filter plane, the norms and the maps (2 B per element instead of 6), so
+ * a part about 3x larger fits.  Searches keep the same pipeline and return the
+ * same bits; the exact re-rank reads its survivors' rows over PCIe (a few
+ * hundred rows per query), while paths that read every row (no plane, no
+ * pre-filter, mqvs_set_batch_mode(1), index build) stream the whole part over
+ * PCIe: correct, slow.  host = 0 moves the rows back into HBM.  The caller
+ * keeps searches on the segment from running meanwhile, and changes the
+ * residency before handing the segment to the part cache (its weight is
+ * taken at put).  *host (mqvs_segment_rows_host) = 1 when the rows are in host
+ * memory.  (No reference counterpart: MyScaleDB re-reads the column from disk
+ * per search, MergeTreeVSManager.cpp:1348-1393.) */
+int mqvs_segment_set_rows_host(mqvs_segment_t seg, int32_t host);
+int mqvs_segment_rows_host(mqvs_segment_t seg, int32_t *host);
 /* Device pointer of the resident rows (normalised rows for cosine). */
 int mqvs_segment_rows(mqvs_segment_t seg, const float **dev_rows);
 

@@ -263,6 +263,10 @@ public:
         return ok != 0;
     }
 
+    /// Float32 rows to pinned host memory (HBM keeps the bf16 plane: a part
+    /// ~3x larger fits; same results) or back (mqvs_segment_set_rows_host).
+    void setRowsHost(bool host) { check(mqvs_segment_set_rows_host(seg->h, host ? 1 : 0)); }
+
     /// Raw top-k: ids / dist nq*k (caller-owned), -1 / FLT_MAX (FLT_MIN for IP)
     /// padded.  filter: PREWHERE bitmap, row_exists: lightweight-delete mask
     /// (LSB-first, n bits, or nullptr).  flags: MQVS_F_* (per call).

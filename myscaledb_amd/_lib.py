@@ -39,6 +39,7 @@ SYMBOLS = [
     "mqvs_abi_version", "mqvs_init", "mqvs_device_count", "mqvs_last_error",
     "mqvs_thread_release", "mqvs_shutdown", "mqvs_segment_create", "mqvs_segment_create_device",
     "mqvs_segment_generate", "mqvs_segment_free", "mqvs_segment_info", "mqvs_segment_prefilter", "mqvs_segment_rows",
+    "mqvs_segment_set_rows_host", "mqvs_segment_rows_host",
     "mqvs_search", "mqvs_search_ex", "mqvs_knn_raw", "mqvs_rerank", "mqvs_merge_shards", "mqvs_generate_device",
     "mqvs_last_search_stats", "mqvs_set_timing", "mqvs_set_batch_mode", "mqvs_set_gather_mode", "mqvs_set_prefilter",
     "mqvs_set_scratch_budget", "mqvs_measure_read_bandwidth",
@@ -123,6 +124,8 @@ def _load():
         "mqvs_segment_info": ([P, P, P, P, P, P, P], ctypes.c_int),
         "mqvs_segment_prefilter": ([P, P, P, P], ctypes.c_int),
         "mqvs_segment_rows": ([P, P], ctypes.c_int),
+        "mqvs_segment_set_rows_host": ([P, ctypes.c_int32], ctypes.c_int),
+        "mqvs_segment_rows_host": ([P, P], ctypes.c_int),
         "mqvs_search": ([P, P, I32, I32, I32, P, P, P, P, U32, P], ctypes.c_int),
         "mqvs_search_ex": ([P, P, I32, I32, I32, P, P, I64, P, P, U32, P], ctypes.c_int),
         "mqvs_knn_raw": ([P, P, I64, I64, I64, I64, I32, P, P], ctypes.c_int),

@@ -165,7 +165,10 @@ static void free_segment(mqvs_segment *s) {
     int cur = -1;
     (void)hipGetDevice(&cur);
     (void)hipSetDevice(s->device);
-    if (s->rows) (void)hipFree(s->rows);
+    if (s->rows_host)
+        (void)hipHostFree(s->rows_host);
+    else if (s->rows)
+        (void)hipFree(s->rows);
     if (s->norms) (void)hipFree(s->norms);
     if (s->nonempty_bits) (void)hipFree(s->nonempty_bits);
     if (s->rows_hi) (void)hipFree(s->rows_hi);
@@ -1445,6 +1448,53 @@ int mqvs_segment_prefilter(mqvs_segment_t seg, int32_t *split, size_t *plane_byt
         if (split) *split = planes ? seg->split : 0;
         if (plane_bytes) *plane_bytes = planes ? seg->plane_bytes : 0;
         if (approx_ok) *approx_ok = !seg->binary && seg->approx_ok ? 1 : 0;
+    });
+}
+
+int mqvs_segment_set_rows_host(mqvs_segment_t seg, int32_t host) {
+    return guarded([&] {
+        if (!seg) fail(MQVS_ERR_BAD_ARGUMENTS, "null segment");
+        if (seg->binary) fail(MQVS_ERR_LOGICAL, "binary segment has no Float32 rows");
+        if ((host != 0) == (seg->rows_host != nullptr)) return;
+        DeviceGuard guard(seg->device);
+        const size_t bytes = sizeof(float) * (size_t)std::max<int64_t>(seg->n, 1) * (size_t)seg->d;
+        MQVS_HIP(hipDeviceSynchronize());  // (work queued on the rows, e.g. by the segment's creation)
+        if (host) {
+            void *h = nullptr;
+            if (hipHostMalloc(&h, bytes, hipHostMallocMapped) != hipSuccess)
+                fail(MQVS_ERR_MEMORY_LIMIT, "pinned host memory for the rows (" + std::to_string(bytes) + " bytes)");
+            void *dptr = nullptr;
+            const hipError_t e1 = hipMemcpy(h, seg->rows, bytes, hipMemcpyDeviceToHost);
+            const hipError_t e2 = e1 == hipSuccess ? hipHostGetDevicePointer(&dptr, h, 0) : e1;
+            if (e2 != hipSuccess) {
+                (void)hipHostFree(h);
+                MQVS_HIP(e2);
+            }
+            (void)hipFree(seg->rows);
+            seg->rows = static_cast<float *>(dptr);
+            seg->rows_host = h;
+            seg->bytes -= std::min(seg->bytes, bytes);
+        } else {
+            float *d = nullptr;
+            if (hipMalloc((void **)&d, bytes) != hipSuccess)
+                fail(MQVS_ERR_MEMORY_LIMIT, "HBM for the rows (" + std::to_string(bytes) + " bytes)");
+            const hipError_t e = hipMemcpy(d, seg->rows_host, bytes, hipMemcpyHostToDevice);
+            if (e != hipSuccess) {
+                (void)hipFree(d);
+                MQVS_HIP(e);
+            }
+            (void)hipHostFree(seg->rows_host);
+            seg->rows_host = nullptr;
+            seg->rows = d;
+            seg->bytes += bytes;
+        }
+    });
+}
+
+int mqvs_segment_rows_host(mqvs_segment_t seg, int32_t *host) {
+    return guarded([&] {
+        if (!seg || !host) fail(MQVS_ERR_BAD_ARGUMENTS, "null argument");
+        *host = seg->rows_host != nullptr ? 1 : 0;
     });
 }
 

@@ -18,7 +18,8 @@ struct mqvs_segment {
     int metric = 0;
     int64_t granule = 0;
     int64_t row_offset = 0;
-    float *rows = nullptr;
+    float *rows = nullptr;           // device address (HBM, or mapped pinned host memory)
+    void *rows_host = nullptr;       // the pinned host allocation when the rows live in host memory
     float *norms = nullptr;          // |y|^2 per row (fvec_norm_L2sqr order)
     uint16_t *rows_hi = nullptr;     // bf16 rounding of the rows, [n][dpad]
     float *ynorm_max = nullptr;      // device scalar: max_r |y_r|; splits 2, 6: + [kMxRec] norm maxima at +16 B

@@ -151,8 +151,17 @@ class VectorScanSegment:
                                     ctypes.byref(g), ctypes.byref(o), ctypes.byref(b)))
         sp, pb, ok = ctypes.c_int32(), ctypes.c_size_t(), ctypes.c_int32()
         check(lib.mqvs_segment_prefilter(self._h, ctypes.byref(sp), ctypes.byref(pb), ctypes.byref(ok)))
+        rh = ctypes.c_int32()
+        check(lib.mqvs_segment_rows_host(self._h, ctypes.byref(rh)))
         return dict(n=n.value, d=d.value, metric=m.value, granule=g.value, row_offset=o.value,
-                    hbm_bytes=b.value, prefilter=sp.value, plane_bytes=pb.value, approx_ok=bool(ok.value))
+                    hbm_bytes=b.value, prefilter=sp.value, plane_bytes=pb.value, approx_ok=bool(ok.value),
+                    rows_host=bool(rh.value))
+
+    def set_rows_host(self, host: bool = True):
+        """mqvs_segment_set_rows_host: the Float32 rows to pinned host memory
+        (HBM keeps the bf16 plane; same results, survivors re-ranked over
+        PCIe) or back into HBM."""
+        check(lib.mqvs_segment_set_rows_host(self._h, 1 if host else 0))
 
     def device_rows_ptr(self) -> int:
         p = ctypes.c_void_p()
