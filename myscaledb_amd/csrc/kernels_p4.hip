@@ -343,7 +343,14 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
             __builtin_amdgcn_global_load_lds((const void *)(rbase + (uint32_t)si * 1024u + roff[x]),
                                              (lds_void *)(dst + (w + 4 * x) * 1024), 16, 0, RPOL);
         } else if (x < 8) {
-            __builtin_amdgcn_global_load_lds((const void *)(qplane + (uint32_t)si * 1024u + qoff[x - 4]),
+            // (a uniform base in SGPRs and one 32-bit lane offset: the
+            // saddr form of the load, no 64-bit address add per piece)
+            const uint32_t vo = (uint32_t)si * 1024u + qoff[x - 4];
+            const uint64_t qb = (uint64_t)qplane;
+            const unsigned char *qbase = reinterpret_cast<const unsigned char *>(
+                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(qb >> 32)) << 32) |
+                (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)qb));
+            __builtin_amdgcn_global_load_lds((const void *)(qbase + vo),
                                              (lds_void *)(dst + kP4QOff + (w + 4 * (x - 4)) * 1024), 16, 0, QPOL);
         } else if constexpr (L2) {
             __builtin_amdgcn_global_load_lds((const void *)(nbase + noff),
@@ -552,7 +559,10 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
         p4_for<16>([&](auto X) __attribute__((always_inline)) {
             constexpr int x = decltype(X)::value, rb = x >> 2, jb = x & 3;
             acc[rb][jb] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a1[rb], b1[jb], acc[rb][jb], 0, 0, 0);
-            if (has_next) {
+            // (the next stage's fragments are read unconditionally: past the
+            // last stage they are stale ring bytes, never used; a branch per
+            // gap cost 2.2 % of the main scan, profiles/r03/p4_next_reads_ab.jsonl)
+            {
                 if constexpr (x < 4)
                     a0[x] = frag(sn, rowA + x * 32 * 64 + offa0);
                 else if constexpr (x < 8)
