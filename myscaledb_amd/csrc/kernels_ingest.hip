@@ -343,6 +343,97 @@ __global__ __launch_bounds__(64) void k_decode_blocks(const uint8_t *src, int64_
         };
         int32_t E = 0;  // the next true token position (uniform)
         bool done = false;
+        // Nearly incompressible blocks (ratio below 8/7: a few long literal
+        // runs, e.g. 167 sequences of ~6 KB per MiB of Gaussian floats): the
+        // tokens one at a time, uniformly, from a 256-B window of the stream
+        // held one dword per lane -- the chunked parse would stage and parse
+        // a chunk per token.
+        if ((int64_t)isz * 8 >= (int64_t)osz * 7) {
+            int32_t wa = -(1 << 30);
+            uint32_t wv = 0;
+            auto wbyte = [&](int32_t pos) -> uint32_t {  // uniform pos < isz
+                const int32_t x = mis + pos;
+                if (x < wa || x >= wa + 256) {
+                    wa = x & ~3;
+                    const int32_t q = wa + 4 * lane;
+                    wv = 0;
+                    if (q + 4 <= lim) {
+                        wv = *reinterpret_cast<const uint32_t *>(pa + q);
+                    } else {
+                        for (int k = 0; k < 4; ++k)
+                            if (q + k < lim) wv |= (uint32_t)pa[q + k] << (8 * k);
+                    }
+                    wa = __builtin_amdgcn_readfirstlane(wa);
+                }
+                const int32_t o = x - wa;
+                return ((uint32_t)__builtin_amdgcn_readlane((int)wv, o >> 2) >> (8 * (o & 3))) & 255u;
+            };
+            int32_t p = 0;
+            while (!bad && !done) {
+                p = __builtin_amdgcn_readfirstlane(p);
+                op = __builtin_amdgcn_readfirstlane(op);
+                fl = __builtin_amdgcn_readfirstlane(fl);
+                if (p >= isz) {
+                    bad = true;
+                    break;
+                }
+                const uint32_t t = wbyte(p);
+                int32_t q = p + 1, ll = (int32_t)(t >> 4);
+                if (ll == 15) {
+                    uint32_t b;
+                    do {
+                        if (q >= isz) {
+                            bad = true;
+                            break;
+                        }
+                        b = wbyte(q++);
+                        ll += (int32_t)b;
+                    } while (b == 255 && ll < (1 << 30));
+                    if (bad) break;
+                }
+                if (ll > isz - q || ll > osz - op) {
+                    bad = true;
+                    break;
+                }
+                const int32_t lip = q;
+                q += ll;
+                if (op - fl >= kFlush) flush(op);
+                big_literals(lip, ll);
+                op += ll;
+                if (q == isz) {  // the final, literals-only sequence
+                    done = true;
+                    break;
+                }
+                if (isz - q < 2) {
+                    bad = true;
+                    break;
+                }
+                const int32_t off = (int32_t)(wbyte(q) | (wbyte(q + 1) << 8));
+                q += 2;
+                int32_t ml = (int32_t)(t & 15);
+                if (ml == 15) {
+                    uint32_t b;
+                    do {
+                        if (q >= isz) {
+                            bad = true;
+                            break;
+                        }
+                        b = wbyte(q++);
+                        ml += (int32_t)b;
+                    } while (b == 255 && ml < (1 << 30));
+                    if (bad) break;
+                }
+                ml += 4;
+                if (off == 0 || off > op || ml > osz - op) {
+                    bad = true;
+                    break;
+                }
+                big_match(off, ml);
+                op += ml;
+                if (op - fl >= kFlush) flush(op);
+                p = q;
+            }
+        }
         int32_t ncs = 0;
         for (int32_t cs = 0; cs < isz && !bad && !done; cs = ncs) {
             E = __builtin_amdgcn_readfirstlane(E);
