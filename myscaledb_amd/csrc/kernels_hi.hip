@@ -49,50 +49,72 @@ __device__ inline float hi_sqrt_up(double s) { return (float)(sqrt(s) * (1.0 + 1
 // ---------------------------------------------------------------------------
 // quantisation: source vector v -> plane vector u = (v % vgroup) vpad + v / vgroup
 // record (kMxRec floats, the MX record's slots): [0] |h|, [1] |r|, [6] |x|
+// One wave per vector, grid-stride over the vectors; the segment maxima of
+// |h|, |r|, |x| are reduced per workgroup and published with three atomics
+// per workgroup (one atomic per vector on the same three words serialised:
+// 340 ms for 10M x 768, profiles/r03/bench_kernel_stats.csv).
 __global__ __launch_bounds__(256) void k_to_hi(const float *src, int64_t rows, int d, int64_t sstride, int64_t dpad,
                                                int64_t vgroup, int64_t vpad, uint16_t *hi, float *rec,
                                                float *maxrec) {
-    const int lane = threadIdx.x & 63;
-    const int64_t v = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    if (v >= rows) return;  // whole wave
-    const float *x = src + v * sstride;
+    __shared__ unsigned smax[4][3];
+    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int nb = (int)(dpad / HI_K);
-    const int64_t u = (v % vgroup) * vpad + v / vgroup;
-    uint16_t *hu = hi + (u >> 4) * nb * 512 + (u & 15) * 32;
-    double nx = 0, nh = 0, nr = 0;
-    for (int64_t i = lane; i < dpad; i += 64) {
-        const float xv = i < d ? x[i] : 0.f;
-        const uint16_t hb = f32_to_bf16_rn(xv);
-        const float hv = __builtin_bit_cast(float, (uint32_t)hb << 16);
-        const float rv = xv - hv;  // exact
-        hu[(i >> 5) * 512 + (i & 31)] = hb;
-        nx += (double)xv * xv;
-        nh += (double)hv * hv;
-        nr += (double)rv * rv;
-    }
-    for (int off = 32; off > 0; off >>= 1) {
-        nx += __shfl_xor(nx, off);
-        nh += __shfl_xor(nh, off);
-        nr += __shfl_xor(nr, off);
-    }
-    if (lane == 0) {
-        float r[kMxRec] = {hi_sqrt_up(nh), hi_sqrt_up(nr), 0.f, 0.f, 0.f, 0.f, hi_sqrt_up(nx), 0.f};
-#pragma unroll
-        for (int t = 0; t < kMxRec; ++t) {
-            if (rec) rec[v * kMxRec + t] = r[t];
-            if (maxrec && (t < 2 || t == 6)) {
-                // non-negative floats order as their bit patterns; NaN -> +inf
-                const unsigned b = (r[t] == r[t]) ? __builtin_bit_cast(unsigned, r[t]) : 0x7F800000u;
-                atomicMax(reinterpret_cast<unsigned *>(maxrec) + t, b);
-            }
+    unsigned m[3] = {0u, 0u, 0u};  // running maxima (bit patterns of non-negative floats; NaN -> +inf)
+    for (int64_t v = (int64_t)blockIdx.x * 4 + w; v < rows; v += (int64_t)gridDim.x * 4) {
+        const float *x = src + v * sstride;
+        const int64_t u = (v % vgroup) * vpad + v / vgroup;
+        uint16_t *hu = hi + (u >> 4) * nb * 512 + (u & 15) * 32;
+        double nx = 0, nh = 0, nr = 0;
+        for (int64_t i = lane; i < dpad; i += 64) {
+            const float xv = i < d ? x[i] : 0.f;
+            const uint16_t hb = f32_to_bf16_rn(xv);
+            const float hv = __builtin_bit_cast(float, (uint32_t)hb << 16);
+            const float rv = xv - hv;  // exact
+            hu[(i >> 5) * 512 + (i & 31)] = hb;
+            nx += (double)xv * xv;
+            nh += (double)hv * hv;
+            nr += (double)rv * rv;
         }
+        for (int off = 32; off > 0; off >>= 1) {
+            nx += __shfl_xor(nx, off);
+            nh += __shfl_xor(nh, off);
+            nr += __shfl_xor(nr, off);
+        }
+        const float r[kMxRec] = {hi_sqrt_up(nh), hi_sqrt_up(nr), 0.f, 0.f, 0.f, 0.f, hi_sqrt_up(nx), 0.f};
+        if (rec && lane < kMxRec) {
+            float rv = 0.f;
+#pragma unroll
+            for (int t = 0; t < kMxRec; ++t)
+                if (lane == t) rv = r[t];
+            rec[v * kMxRec + lane] = rv;
+        }
+        const int slot[3] = {0, 1, 6};
+#pragma unroll
+        for (int t = 0; t < 3; ++t) {
+            const float f = r[slot[t]];
+            const unsigned bits = (f == f) ? __builtin_bit_cast(unsigned, f) : 0x7F800000u;
+            m[t] = bits > m[t] ? bits : m[t];
+        }
+    }
+    if (!maxrec) return;
+    if (lane == 0)
+        for (int t = 0; t < 3; ++t) smax[w][t] = m[t];
+    __syncthreads();
+    if (threadIdx.x < 3) {
+        const int t = threadIdx.x;
+        unsigned b = smax[0][t];
+        for (int ww = 1; ww < 4; ++ww) b = smax[ww][t] > b ? smax[ww][t] : b;
+        atomicMax(reinterpret_cast<unsigned *>(maxrec) + (t == 2 ? 6 : t), b);
     }
 }
 
 void launch_to_hi(const float *src, int64_t rows, int d, int64_t src_stride, int64_t dpad, int64_t vgroup,
                   int64_t vpad, uint16_t *hi, float *rec, float *maxrec, hipStream_t s) {
     if (rows <= 0) return;
-    const int64_t blocks = (rows + 3) / 4;
+    int dev = 0, cus = 0;
+    MQVS_HIP(hipGetDevice(&dev));
+    MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int64_t blocks = std::min<int64_t>((rows + 3) / 4, (int64_t)cus * 16);
     hipLaunchKernelGGL(k_to_hi, dim3((unsigned)blocks), dim3(256), 0, s, src, rows, d, src_stride, dpad, vgroup, vpad,
                        hi, rec, maxrec);
 }
