@@ -10,7 +10,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/r03
 mkdir -p $O
-STEPS="${*:-pmc risk bench}"
+STEPS="${*:-pmc pmc4 risk bench}"
 pmc_set() {  # tag, searches, args...
   local tag=$1 s=$2; shift 2
   bash tools/gpu_pmc.sh python tools/pmc_search.py --searches "$s" "$@" || return 1
@@ -23,9 +23,11 @@ for step in $STEPS; do
       python tools/pmc_traffic.py $O/pmc_config1 --searches 3 --nq 1000 --out $O/pmc_traffic.json > /dev/null || exit 1
       pmc_set nq1 4 --nq 1 || exit 1
       python tools/pmc_traffic.py $O/pmc_nq1 --searches 5 --nq 1 --out $O/pmc_nq1.json > /dev/null || exit 1
+      echo "pmc done"; cat $O/pmc_traffic.json $O/pmc_nq1.json | grep -E "hbm_bytes_per_search|avg_launch|clock|mfma_busy|k_scan" ;;
+    pmc4)
       pmc_set config4 4 --nq 1 --n 50000000 --metric L2 --selectivity 100 || exit 1
       python tools/pmc_traffic.py $O/pmc_config4 --searches 5 --nq 1 --out $O/pmc_config4_sel100.json > /dev/null || exit 1
-      echo "pmc done"; cat $O/pmc_traffic.json $O/pmc_nq1.json $O/pmc_config4_sel100.json | grep -E "hbm_bytes_per_search|avg_launch|clock|mfma_busy|k_scan" ;;
+      echo "pmc4 done"; grep -E "hbm_bytes_per_search|avg_launch|k_scan" $O/pmc_config4_sel100.json ;;
     risk)
       timeout -k 10 600 python -u tools/blas_order_risk.py --out $O/blas_order_risk.json > $O/blas_order_risk.log 2>&1 \
         || { echo "risk failed"; tail -20 $O/blas_order_risk.log; exit 1; }
