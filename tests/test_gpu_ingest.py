@@ -40,7 +40,8 @@ def column_files(data_f32, sizes, block=1 << 20, method=0x82):
                                                ("repeats", 4097, 0x82), ("gauss", 300000, 0x02),
                                                ("quantised", 1 << 20, 0x82), ("period24k", 1 << 20, 0x82),
                                                ("period40k", 1 << 20, 0x82), ("mixed", 1 << 20, 0x82),
-                                               ("mixed", 70000, 0x82)])
+                                               ("mixed", 70000, 0x82), ("sparse_rle", 1 << 20, 0x82),
+                                               ("sparse_rle", 65536, 0x82)])
 def test_gpu_ingest_dense(mq, kind, block, method):
     """periodNk: the rows repeat every N KiB, so nearly every match reaches
     back further than the decoder's 4 KiB LDS ring (its far-match path reads
@@ -48,7 +49,9 @@ def test_gpu_ingest_dense(mq, kind, block, method):
     pieces of four kinds (fresh gaussian = literal runs of every length,
     quantised = short matches, copies of a recent piece = longer and
     overlapping matches, constant runs), so the decoder's groups of short
-    sequences alternate with the wave-wide long-sequence paths."""
+    sequences alternate with the wave-wide long-sequence paths.  sparse_rle:
+    blocks compressed to >= 7/8 of their size take the token-at-a-time path,
+    with overlapping and far matches."""
     rng = np.random.default_rng(11)
     n, d = 20000, 64
     if kind == "gauss":
@@ -61,6 +64,13 @@ def test_gpu_ingest_dense(mq, kind, block, method):
         base[::7] = np.round(base[::7], 1)
         rows = np.tile(base, (n // period + 1, 1))[:n].copy()
         rows[::97] += 1.0  # break some matches: fresh literals between far matches
+    elif kind == "sparse_rle":
+        # nearly incompressible (the decoder's one-token-at-a-time path): Gaussian
+        # rows, every 37th with runs of one repeated float (overlapping matches,
+        # off = 4) and every 53rd a copy of an earlier row (far matches)
+        rows = rng.standard_normal((n, d)).astype(np.float32)
+        rows[::37, 8:40] = rows[::37, 7:8]
+        rows[53::53] = rows[:-53:53][: len(rows[53::53])]
     elif kind == "mixed":
         pieces = rng.integers(0, 4, n * d // 16)
         flat = np.round(rng.standard_normal(n * d), 1).astype(np.float32)
