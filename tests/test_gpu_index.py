@@ -230,3 +230,25 @@ def test_index_torch_device_pointers(mq):
         seg.free()
     assert np.array_equal(ids_d.cpu().numpy(), ids_h)
     assert np.array_equal(dist_d.cpu().numpy().view(np.uint32), dist_h.view(np.uint32))
+
+
+def test_index_many_lists(mq):
+    """More than 16384 lists (the strided plan kernel, k_plan_lists, and the
+    FLAT coarse step): the returned rows carry their exact distances and the
+    recall against FLAT is high when many lists are probed."""
+    n, d, nq, k, nlist = 60000, 32, 50, 10, 20000
+    seg = mq.VectorScanSegment.generate(0x5EED0001, 2, n, d, metric="L2")
+    q = O.generate(0x5EED0001, 2, n, nq, d)
+    idx = mq.VectorIndex.build(seg, "MSTG", {"nlist": nlist})
+    try:
+        assert idx.info()["nlist"] == nlist
+        ids_i, dist_i = idx.search(q, k, {"nprobe": 4096, "num_reorder": 400})
+        ids_f, _ = seg.search(q, k)
+        ids_r, dist_r = seg.rerank(q, ids_i, k)
+    finally:
+        idx.free()
+        seg.free()
+    recall = np.mean([len(set(ids_i[i]) & set(ids_f[i])) for i in range(nq)]) / k
+    assert recall >= 0.9, recall
+    assert np.array_equal(ids_r, ids_i)
+    assert np.array_equal(dist_r.view(np.uint32), dist_i.view(np.uint32))
