@@ -4,15 +4,25 @@ FLAT cosine over 10M x 768 Float32, batch of 1000 queries, top-100.
 
 One step = one batch search of `--nq` queries over the whole part (every rank
 scans its granule-aligned row-range shard; with N > 1 the per-shard top-k are
-all-gathered over RCCL and merged).  Strong scaling: the 10M-row part is fixed
-and split over N GPUs.  Inputs are generated in HBM (counter-based generator,
-the oracle's bit-identical twin) before the timed region.
+all-gathered over RCCL and merged inside libmqvs, mqvs_sharded_search).  Strong
+scaling: the 10M-row part is fixed and split over N GPUs.  Inputs are generated
+in HBM (counter-based generator, the oracle's bit-identical twin) before the
+timed region.
+
+`--gpus N` (N > 1) without a launcher's WORLD_SIZE starts
+`torch.distributed.run --nproc-per-node N` on this script as a CHILD process
+before anything touches the GPU, and exits with its return code; rank 0's JSON
+line reaches stdout through the inherited descriptor.  With N > 1 the line
+also carries BASELINE configs[3] (FLAT IP, 1536-d, 12.5M rows per GPU: the
+full 100M part at N = 8, a labelled 12.5M x N subset below) searched through
+the same sharded path.
 
 Prints ONE JSON line on rank 0 (see the driver contract in the task README).
 """
 import argparse
 import json
 import os
+import sys
 import time
 
 import numpy as np
@@ -35,6 +45,10 @@ def seg_dpad(d):
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--dry-run", action="store_true",
+                    help="launch only: every rank prints its RANK / LOCAL_RANK / WORLD_SIZE and exits (no GPU)")
+    ap.add_argument("--no-config3-sharded", action="store_true",
+                    help="N > 1: skip the configs[3] (100M x 1536 IP over 8 GPUs) leg")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=10_000_000)
@@ -631,11 +645,124 @@ def configs_leg(mq, mq_scan, args):
     return out
 
 
+def _max_over_ranks(x):
+    import torch
+    import torch.distributed as tdist
+    t = torch.tensor([x], dtype=torch.float64, device="cuda")
+    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sharded_point(comm, seg, q, k, reps, mq_scan):
+    """One batch size through mqvs_sharded_search on every rank: the first
+    call runs the validated path, the timed ones the one-sync fast path; the
+    time is the slowest rank's.  Then the same sharded search on the exact
+    fp32 path of every rank (mqvs_set_batch_mode(1)) and the timed output
+    compared with it on ALL queries (ids and distance bits, every rank)."""
+    import torch
+    import torch.distributed as tdist
+    nq = q.shape[0]
+    ids = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+    dst = torch.empty((nq, k), dtype=torch.float32, device="cuda")
+    for _ in range(2):
+        comm.sharded_search(seg, q, k, out=(ids, dst))
+    before = comm.stats()
+    tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        comm.sharded_search(seg, q, k, out=(ids, dst))
+    torch.cuda.synchronize()
+    ms = _max_over_ranks((time.perf_counter() - t0) * 1e3 / reps)
+    after = comm.stats()
+    mq_scan.set_batch_mode(1)
+    try:
+        ei, ed = comm.sharded_search(seg, q, k)
+    finally:
+        mq_scan.set_batch_mode(0)
+    same = bool(torch.equal(ids, ei)) and bool(torch.equal(dst.view(torch.int32), ed.view(torch.int32)))
+    all_same = _max_over_ranks(0.0 if same else 1.0) == 0.0
+    return {"nq": nq, "ms_per_search": round(ms, 3), "qps": round(nq / (ms * 1e-3), 1),
+            "fast_path_calls": after["fast_calls"] - before["fast_calls"],
+            "redo_calls": after["redo_calls"] - before["redo_calls"],
+            "exact": {"queries": nq, "ids_and_dist_bits_equal_on_every_rank": all_same}}
+
+
+def sharded_legs(mq, mq_scan, comm, seg, args, rank, world):
+    """N > 1, on every rank (collectives): the small batches of the configs[1]
+    part through the sharded path, then BASELINE configs[3] -- FLAT IP over a
+    1536-d part, 12.5M rows per GPU generated in HBM: the full 100M x 1536
+    part at N >= 8, a 12.5M x N subset below (100M needs >= 8
+    shards of this size) -- at nq 1 / 16 / 1000, each point checked against
+    the exact path on every query."""
+    import torch
+    from myscaledb_amd.sharded import shard_rows
+    from myscaledb_amd.vector_scan import generate_device
+    out = {}
+    pts = []
+    for nq in (1, 16):
+        q = torch.empty((nq, args.d), dtype=torch.float32, device="cuda")
+        generate_device(SEED_QUERY, args.mode, 0, nq, args.d, q)
+        e = sharded_point(comm, seg, q, args.k, 20, mq_scan)
+        plane = 2.0 * args.n * seg_dpad(args.d)
+        e["aggregate_plane_tb_s"] = round(plane / (e["ms_per_search"] * 1e-3) / 1e12, 3)
+        pts.append(e)
+    out["small_batch_sharded"] = pts
+    if args.no_config3_sharded:
+        return out
+    d3, per = 1536, 12_500_000
+    total = 100_000_000 if world >= 8 else per * world
+    r0, r1 = shard_rows(total, args.granule, rank, world)
+    seg3 = mq.VectorScanSegment.generate(SEED_BASE, 1, r1 - r0, d3, "IP", args.granule, row_offset=r0)
+    try:
+        pts = []
+        for nq in (1, 16, 1000):
+            q = torch.empty((nq, d3), dtype=torch.float32, device="cuda")
+            generate_device(SEED_QUERY, 1, 0, nq, d3, q)
+            e = sharded_point(comm, seg3, q, 100, 5 if nq == 1000 else 10, mq_scan)
+            plane = 2.0 * total * seg_dpad(d3)
+            e["plane_bytes_read"] = plane
+            e["aggregate_plane_tb_s"] = round(plane / (e["ms_per_search"] * 1e-3) / 1e12, 3)
+            e["frac_of_n_x_8tbs"] = round(plane / (e["ms_per_search"] * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4)
+            pts.append(e)
+    finally:
+        seg3.free()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    out["config3_sharded"] = {
+        "workload": (f"FLAT IP {total / 1e6:g}M x {d3} (N(0,1)) over {world} GPUs, top-100, "
+                     + ("BASELINE configs[3] at full size" if total == 100_000_000 else
+                        f"scaled subset of BASELINE configs[3]'s 100M rows: {per / 1e6:g}M rows per GPU")),
+        "rows": total, "rows_per_gpu_rank0": r1 - r0 if rank == 0 else None, "full_size": total == 100_000_000,
+        "points": pts}
+    return out
+
+
+def launch_ranks(args):
+    """`--gpus N` run directly (the driver's N > 1 contract starts us under
+    torch.distributed.run itself): start that launcher as a child process --
+    never exec, and before any GPU call -- and return its exit code."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr", "127.0.0.1", "--master-port", str(port), os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.run(cmd, env=dict(os.environ)).returncode
+
+
 def main():
     args = parse()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.dry_run:
+        print(json.dumps({"dry_run": True, "rank": rank, "local_rank": local, "world_size": world,
+                          "gpus_arg": args.gpus}), flush=True)
+        return
     import torch
     torch.cuda.set_device(local)
     dist_on = world > 1
@@ -669,7 +796,8 @@ def main():
         try:
             from myscaledb_amd.sharded import RcclComm
             comm = RcclComm.from_process_group()
-            exchange = "mqvs_sharded_search (libmqvs RCCL all-gather + device merge)"
+            exchange = (f"mqvs_sharded_search (libmqvs RCCL communicator of {comm.nranks} ranks: one all-gather "
+                        "of headers + per-rank top-k, device merge, one host sync per search)")
         except Exception as e:  # noqa: BLE001
             comm, exchange = None, f"torch.distributed all_gather + mqvs_merge_shards ({type(e).__name__})"
 
@@ -735,6 +863,8 @@ def main():
         else:
             exact = exact_check(mq_scan, seg, q, k, ids, dst)
 
+    extra = sharded_legs(mq, mq_scan, comm, seg, args, rank, world) if comm is not None and world > 1 else {}
+
     result = None
     if rank == 0:
         qps = nq / (ms / 1000.0)
@@ -746,7 +876,7 @@ def main():
             "metric": "QPS (FLAT brute force, batch top-k)",
             "value": round(qps, 2),
             "unit": "queries/s",
-            "n_gpus": world,
+            "n_gpus": comm.nranks if comm is not None else world,
             "steps": args.steps,
             "warmup": args.warmup,
             "ms_per_step": round(ms, 3),
@@ -769,6 +899,7 @@ def main():
             "stats_last_step": {kk: (round(v, 3) if isinstance(v, float) else v) for kk, v in st.items()},
             "roofline": roof,
         }
+        result.update(extra)
         if args.read_sweep_gib > 0 and world == 1:
             # the measured HBM read peak of this device (same process, same
             # GPU): the denominator of frac_measured_peak below
@@ -801,12 +932,22 @@ def main():
                     nq1["pmc_over_plane"] = round(pm["hbm_bytes_per_search"] / plane, 4)
                     nq1["pmc_source"] = pm["source"]
                 result["roofline"]["nq1"] = nq1
+                # (scalars at the top level of roofline: the driver's record
+                # keeps those, not the nested dict)
+                for key, val in (("nq1_ms", nq1["ms"]), ("nq1_ms_end_to_end", nq1["ms_end_to_end"]),
+                                 ("nq1_frac_8tbs", nq1["frac_8tbs"]),
+                                 ("nq1_frac_end_to_end_8tbs", nq1["frac_end_to_end_8tbs"]),
+                                 ("nq1_pmc_over_plane", nq1.get("pmc_over_plane")),
+                                 ("nq1_frac_measured_peak", nq1.get("frac_measured_peak")),
+                                 ("nq1_exact", nq1["exact"])):
+                    result["roofline"][key] = val
         if not args.no_cpu and world == 1:
             # the CPU leg: the oracle (the reference's CPU path restated) timed
             # on the host cores, and -- as the checker only -- its formula on
             # sampled rows of the timed output (pins the exact path)
             O = _oracle()
             result["cpu_baseline"] = cpu_baseline(O, args)
+            result["cpu_baseline"]["one_thread_qps"] = result["cpu_baseline"]["one_thread"]["qps"]
             if not args.no_verify:
                 ok, nchk = verify_sample(O, ids.cpu().numpy(), dst.cpu().numpy(), q.cpu().numpy(), args)
                 result["oracle_sample"] = {"queries": nchk, "bitwise_and_no_better_sample": ok}

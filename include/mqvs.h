@@ -296,7 +296,15 @@ int mqvs_knn_binary_raw(const uint8_t *x, const uint8_t *y, int64_t d, int64_t k
  * argument errors): shards out of row order, disagreeing calls or a failing
  * rank make EVERY rank return the error instead of leaving the others in a
  * collective; a rank whose local search fails still joins the exchange, and
- * all ranks then fail together. */
+ * all ranks then fail together.
+ * Host syncs: a call equal to the last call every rank completed together
+ * (same shard, nq, k, metric and bitmap presence) synchronises the host ONCE
+ * (header, local search, exchange and merge enqueued back to back; the
+ * exchanged table is read at the end).  The first call, a changed call, or a
+ * call whose local search needs a host-driven fallback or whose cosine
+ * chunk-ordinal bases changed (filters that empty whole chunks) runs the
+ * validated path: header exchange and sync, local search, exchange and sync.
+ * MQVS_F_ASYNC is ignored (the call always ends with the merged result). */
 #define MQVS_COMM_ID_BYTES 128
 typedef struct mqvs_comm *mqvs_comm_t;
 int mqvs_comm_unique_id(uint8_t *id /* MQVS_COMM_ID_BYTES */);
@@ -311,6 +319,9 @@ int mqvs_comm_init_loopback(int32_t nranks, mqvs_comm_t *out);
 int mqvs_sharded_search(mqvs_comm_t comm, mqvs_segment_t shard, const float *queries, int32_t nq, int32_t k,
                         int32_t metric, const uint8_t *filter, const uint8_t *row_exists, int64_t *out_ids,
                         float *out_dist, uint32_t flags, mqvs_stream_t stream);
+/* Calls of this communicator that took the one-sync fast path, and how many
+ * of those were re-run on the validated path. */
+int mqvs_comm_stats(mqvs_comm_t comm, int64_t *fast_calls, int64_t *redo_calls);
 
 /* Fill a device buffer with generator rows [row0, row0+n) (for queries). */
 int mqvs_generate_device(uint64_t seed, int32_t mode, int64_t row0, int64_t n, int32_t d,

@@ -10,10 +10,12 @@ import ctypes
 import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# The release library.  Measurement tools (tools/ab_split.py) may load the
-# measurement build instead (MQVS_LIB=dbg -> libmqvs_dbg.so, `make dbg`), whose
-# kernels read A/B switches from the environment; the product never does.
-LIB_PATH = os.path.join(_HERE, "libmqvs_dbg.so" if os.environ.get("MQVS_LIB") == "dbg" else "libmqvs.so")
+# The release library; nothing in the environment selects another one.  The
+# measurement build (libmqvs_dbg.so, `make dbg`: kernels that read A/B switches
+# from the environment) is loaded only by a tool that calls
+# use_measurement_build() explicitly, before its first library call.
+LIB_PATH = os.path.join(_HERE, "libmqvs.so")
+DBG_LIB_PATH = os.path.join(_HERE, "libmqvs_dbg.so")
 
 # include/mqvs.h
 METRIC_L2, METRIC_IP, METRIC_COSINE, METRIC_HAMMING, METRIC_JACCARD = 0, 1, 2, 4, 5
@@ -46,7 +48,7 @@ SYMBOLS = [
     "mqvs_index_build", "mqvs_index_free", "mqvs_index_info", "mqvs_index_search", "mqvs_index_last_stats",
     "mqvs_segment_create_binary", "mqvs_search_binary", "mqvs_knn_binary_raw",
     "mqvs_segment_create_from_column", "mqvs_async_check",
-    "mqvs_comm_unique_id", "mqvs_comm_init", "mqvs_comm_init_loopback", "mqvs_comm_free", "mqvs_sharded_search",
+    "mqvs_comm_unique_id", "mqvs_comm_init", "mqvs_comm_init_loopback", "mqvs_comm_free", "mqvs_sharded_search", "mqvs_comm_stats",
     "mqvs_index_set_row_ids_map", "mqvs_decoupled_filter",
     "mqvs_cache_create", "mqvs_cache_free", "mqvs_cache_put", "mqvs_cache_acquire", "mqvs_cache_release",
     "mqvs_cache_remove", "mqvs_cache_stats",
@@ -101,13 +103,13 @@ def _share_hip_runtime_with_torch():
         pass
 
 
-def _load():
+def _load(path=LIB_PATH):
     _share_hip_runtime_with_torch()
-    if not os.path.exists(LIB_PATH):
+    if not os.path.exists(path):
         raise ImportError(
-            f"{LIB_PATH} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+            f"{path} is missing: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
             " (the HIP path has no CPU fallback)")
-    L = ctypes.CDLL(LIB_PATH)
+    L = ctypes.CDLL(path)
     P, I32, I64, U32, U64 = (ctypes.c_void_p, ctypes.c_int32, ctypes.c_int64, ctypes.c_uint32,
                              ctypes.c_uint64)
     sig = {
@@ -154,6 +156,7 @@ def _load():
         "mqvs_comm_init_loopback": ([I32, P], ctypes.c_int),
         "mqvs_comm_free": ([P], ctypes.c_int),
         "mqvs_sharded_search": ([P, P, P, I32, I32, I32, P, P, P, P, U32, P], ctypes.c_int),
+        "mqvs_comm_stats": ([P, P, P], ctypes.c_int),
         "mqvs_index_set_row_ids_map": ([P, P, I64, U32], ctypes.c_int),
         "mqvs_decoupled_filter": ([P, I64, P, P, I64, U32, P, I64, U32, P], ctypes.c_int),
         "mqvs_cache_create": ([ctypes.c_size_t, P], ctypes.c_int),
@@ -171,7 +174,25 @@ def _load():
     return L
 
 
-lib = _load()
+class _Lib:
+    """The loaded library's functions (attribute access forwards to the CDLL)."""
+
+    def __init__(self, cdll, path):
+        self._cdll, self.path = cdll, path
+
+    def __getattr__(self, name):
+        return getattr(self._cdll, name)
+
+
+lib = _Lib(_load(), LIB_PATH)
+
+
+def use_measurement_build():
+    """For measurement tools only (tools/ab_split.py --dbg and the like): route
+    every later call of this process to libmqvs_dbg.so, whose kernels read A/B
+    switches (some of them diagnostic builds with wrong results) from the
+    environment.  The product path and the tests never call this."""
+    lib._cdll, lib.path = _load(DBG_LIB_PATH), DBG_LIB_PATH
 
 
 # DB::ErrorCodes the reference throws for the same conditions

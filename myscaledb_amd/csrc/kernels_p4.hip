@@ -620,13 +620,12 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
 // queue entries per wave (16 B each): 4096 x 16 B x 4 waves x 256 CUs = 64 MiB
 constexpr int kP4QueueCap = 4096;
 
+// (the current device's CU count, queried per call: launch_p4 sizes its grid
+// from the same query, so the queue always covers blockIdx * 4 + wave)
 size_t p4_queue_bytes() {
-    static int cus = 0;
-    if (!cus) {
-        int dev = 0;
-        MQVS_HIP(hipGetDevice(&dev));
-        MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-    }
+    int dev = 0, cus = 0;
+    MQVS_HIP(hipGetDevice(&dev));
+    MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     return (size_t)cus * 4 * kP4QueueCap * sizeof(u32x4);
 }
 

@@ -47,6 +47,7 @@ struct Workspace {
         overflow, out_ids, out_dist, misc, qhi, bq, thr, cand2, count2, gcount, goff, glist, large, sticky, surv,
         recs, flags, p4q, qord;
     int *host_flags = nullptr;  // pinned
+    bool pending_timing = false, pending_bf16 = false;  // search_collect_stats
     void init() {
         if (stream) return;
         MQVS_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
@@ -293,6 +294,30 @@ static int *sticky_word(Workspace &ws, hipStream_t s) {
 
 int *async_sticky(int device, hipStream_t s) { return sticky_word(workspace(device), s); }
 
+// per-stage times of the search just synchronised (HIP events on its stream)
+static void read_search_times(Workspace &ws, mqvs_search_stats &st) {
+    float a = 0, b = 0, c = 0, e = 0, f = 0;
+    MQVS_HIP(hipEventElapsedTime(&a, ws.ev[5], ws.ev[1]));
+    MQVS_HIP(hipEventElapsedTime(&b, ws.ev[1], ws.ev[2]));
+    MQVS_HIP(hipEventElapsedTime(&c, ws.ev[2], ws.ev[3]));
+    MQVS_HIP(hipEventElapsedTime(&e, ws.ev[3], ws.ev[4]));
+    MQVS_HIP(hipEventElapsedTime(&f, ws.ev[0], ws.ev[4]));
+    st.probe_ms = a;
+    st.probe_select_ms = b;
+    // main_ms: the scan kernels only; refine_ms: the refinements between
+    float scan = 0.f;
+    const int ns = std::min(st.segments, Workspace::kSegEv / 2);
+    for (int i = 0; i < ns; ++i) {
+        float x = 0.f;
+        MQVS_HIP(hipEventElapsedTime(&x, ws.seg_ev[2 * i], ws.seg_ev[2 * i + 1]));
+        scan += x;
+    }
+    st.main_ms = ns > 0 ? scan : c;
+    st.refine_ms = ns > 0 ? c - scan : 0.0;
+    st.final_ms = e;
+    st.total_ms = f;
+}
+
 // Large k (above the LDS sort): the global-scratch sort of the final select,
 // and query sub-batches small enough that the candidate lists and the dense
 // probe matrix stay within a fixed HBM budget.
@@ -342,10 +367,15 @@ static SegTune seg_tune(int nq) {
 // formula_nq: the batch size that selects faiss's distance formula (0: nq).
 // Query sub-batches of one call (large k) keep the call's formula: faiss
 // decides it from the whole batch (BruteForceSearch.h:80-87, nx >= 20).
+// async_word (ASYNC calls only): where the search's fallback flags go instead
+// of the thread's sticky word (the sharded search exchanges them); the
+// survivor counts and event times are then collected by search_collect_stats
+// after the caller's own stream sync.
 static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, int metric,
                         const uint8_t *filter, const uint8_t *exists, int64_t *out_ids,
                         float *out_dist, uint32_t flags, hipStream_t user_stream,
-                        bool force_exact = false, int64_t ord_base = -1, int maxv_hint = 0, int formula_nq = 0) {
+                        bool force_exact = false, int64_t ord_base = -1, int maxv_hint = 0, int formula_nq = 0,
+                        int *async_word = nullptr) {
     const int fnq = formula_nq > 0 ? formula_nq : nq;
     if (!seg) fail(MQVS_ERR_BAD_ARGUMENTS, "null segment");
     if (seg->binary) fail(MQVS_ERR_LOGICAL, "binary (FixedString) segment: search it with mqvs_search_binary");
@@ -370,7 +400,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
                 const int m = std::min(qb, nq - q0);
                 search_impl(seg, queries + (size_t)q0 * seg->d, m, k, metric, filter, exists,
                             out_ids + (size_t)q0 * k, out_dist + (size_t)q0 * k, flags, user_stream, force_exact,
-                            ord_base, maxv_hint, fnq);
+                            ord_base, maxv_hint, fnq, async_word);
             }
             return;
         }
@@ -387,7 +417,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
                 const int m = (int)std::min<int64_t>(qb, nq - q0);
                 search_impl(seg, queries + (size_t)q0 * seg->d, m, k, metric, filter, exists,
                             out_ids + (size_t)q0 * k, out_dist + (size_t)q0 * k, flags, user_stream, force_exact,
-                            ord_base, maxv_hint, fnq);
+                            ord_base, maxv_hint, fnq, async_word);
             }
             return;
         }
@@ -689,11 +719,21 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     st.k = k;
 
     const bool async = dev && (flags & MQVS_F_ASYNC);
+    ws.pending_timing = false;
     if (async) {
         // no host fallback possible: leave the outcome for mqvs_async_check
+        // (or the caller's word)
         const bool variants_matter = ords > maxv;
-        launch_async_flags(overflow, status, variants_matter ? 1 : 0, sticky_word(ws, s), s);
+        launch_async_flags(overflow, status, variants_matter ? 1 : 0, async_word ? async_word : sticky_word(ws, s),
+                           s);
         MQVS_HIP(hipGetLastError());
+        if (async_word) {
+            // the survivor stats land in pinned memory, read after the
+            // caller's sync (search_collect_stats)
+            MQVS_HIP(hipMemcpyAsync(ws.host_flags + 16, fl, 8 * sizeof(int), hipMemcpyDeviceToHost, s));
+            ws.pending_timing = timing;
+            ws.pending_bf16 = kind == kScanBf16;
+        }
     } else {
         // [overflow 4][status 4] in one copy -> host_flags[0] overflow bits,
         // [1] status, [4..6] survivor / candidate stats
@@ -750,30 +790,22 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
             MQVS_HIP(hipMemcpyAsync(out_dist, ddist, sizeof(float) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
             MQVS_HIP(hipStreamSynchronize(s));
         }
-        if (timing) {
-            float a = 0, b = 0, c = 0, e = 0, f = 0;
-            MQVS_HIP(hipEventElapsedTime(&a, ws.ev[5], ws.ev[1]));
-            MQVS_HIP(hipEventElapsedTime(&b, ws.ev[1], ws.ev[2]));
-            MQVS_HIP(hipEventElapsedTime(&c, ws.ev[2], ws.ev[3]));
-            MQVS_HIP(hipEventElapsedTime(&e, ws.ev[3], ws.ev[4]));
-            MQVS_HIP(hipEventElapsedTime(&f, ws.ev[0], ws.ev[4]));
-            st.probe_ms = a;
-            st.probe_select_ms = b;
-            // main_ms: the scan kernels only; refine_ms: the refinements between
-            float scan = 0.f;
-            const int ns = std::min(st.segments, Workspace::kSegEv / 2);
-            for (int i = 0; i < ns; ++i) {
-                float x = 0.f;
-                MQVS_HIP(hipEventElapsedTime(&x, ws.seg_ev[2 * i], ws.seg_ev[2 * i + 1]));
-                scan += x;
-            }
-            st.main_ms = ns > 0 ? scan : c;
-            st.refine_ms = ns > 0 ? c - scan : 0.0;
-            st.final_ms = e;
-            st.total_ms = f;
-        }
+        if (timing) read_search_times(ws, st);
     }
     g_stats = st;
+}
+
+// the stats of this thread's last search_segment_async on `device`, once the
+// caller has synchronised its stream
+void search_collect_stats(int device) {
+    Workspace &ws = workspace(device);
+    if (ws.pending_bf16) {
+        g_stats.survivors_max = ws.host_flags[17];
+        g_stats.survivors_total = (uint32_t)ws.host_flags[18];
+        g_stats.candidates_max = ws.host_flags[19];
+    }
+    if (ws.pending_timing) read_search_times(ws, g_stats);
+    ws.pending_timing = ws.pending_bf16 = false;
 }
 
 // the search for other translation units (sharded.hip): device pointers,
@@ -783,6 +815,16 @@ void search_segment(mqvs_segment *seg, const float *queries, int nq, int k, int 
                     int64_t ord_base) {
     search_impl(seg, queries, nq, k, metric, filter, exists, out_ids, out_dist, flags | MQVS_F_DEVICE_PTRS, stream,
                 false, ord_base);
+}
+
+// the same without any host sync: fallback flags OR-ed into *flag_word
+// (bit 0 candidate overflow, bit 1 cosine variant table too short), stats
+// collected by search_collect_stats after the caller's sync
+void search_segment_async(mqvs_segment *seg, const float *queries, int nq, int k, int metric, const uint8_t *filter,
+                          const uint8_t *exists, int64_t *out_ids, float *out_dist, uint32_t flags,
+                          hipStream_t stream, int64_t ord_base, int *flag_word) {
+    search_impl(seg, queries, nq, k, metric, filter, exists, out_ids, out_dist,
+                flags | MQVS_F_DEVICE_PTRS | MQVS_F_ASYNC, stream, false, ord_base, 0, 0, flag_word);
 }
 
 // Exact re-rank of caller-given candidate rows (computeTopDistanceSubset

@@ -272,6 +272,14 @@ void launch_decoupled_filter(const uint8_t *new_filter, int64_t new_rows, const 
 void search_segment(mqvs_segment *seg, const float *queries, int nq, int k, int metric, const uint8_t *filter,
                     const uint8_t *exists, int64_t *out_ids, float *out_dist, uint32_t flags, hipStream_t stream,
                     int64_t ord_base);
+// the same, asynchronous: no host sync; the fallback flags (bit 0 candidate
+// overflow, bit 1 cosine variant table too short) are OR-ed into *flag_word,
+// and search_collect_stats(device) fills the thread's stats after the
+// caller's stream sync
+void search_segment_async(mqvs_segment *seg, const float *queries, int nq, int k, int metric, const uint8_t *filter,
+                          const uint8_t *exists, int64_t *out_ids, float *out_dist, uint32_t flags,
+                          hipStream_t stream, int64_t ord_base, int *flag_word);
+void search_collect_stats(int device);
 // number of granule chunks of [0, n) the reference searches (a non-empty row
 // that, under a PREWHERE filter, passes it and is not deleted) -> *count
 void launch_count_active_chunks(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists, int64_t n,

@@ -4,7 +4,8 @@
 // below returns its default there, so no variable in a server's environment
 // can change a kernel or select a diagnostic build.  The measurement build
 // (`make dbg` -> libmqvs_dbg.so, compiled with -DMQVS_DEBUG_TUNING) reads
-// them with getenv; tools/ab_split.py loads it through MQVS_LIB=dbg.
+// them with getenv; tools load it only through an explicit
+// myscaledb_amd._lib.use_measurement_build() call (their --dbg option).
 #pragma once
 
 #include <cstdlib>

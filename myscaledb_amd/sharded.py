@@ -222,6 +222,14 @@ class RcclComm:
             _ptr(ids), _ptr(dist), 0, stream))
         return ids, dist
 
+    def stats(self):
+        """{'fast_calls': searches that synchronised the host once, 'redo_calls':
+        those of them re-run on the validated path} (mqvs_comm_stats)."""
+        import ctypes
+        f, r = ctypes.c_int64(), ctypes.c_int64()
+        self._lib.check(self._lib.lib.mqvs_comm_stats(self._h, ctypes.byref(f), ctypes.byref(r)))
+        return {"fast_calls": f.value, "redo_calls": r.value}
+
     def free(self):
         if getattr(self, "_h", None):
             self._lib.check(self._lib.lib.mqvs_comm_free(self._h))

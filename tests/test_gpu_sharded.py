@@ -100,6 +100,9 @@ LOOP = [
     ("ip_w8_exact",      8,     40960, 8,  3,  50,   "IP",     0,   1024, None, 0.1, 0.0),
     ("l2_w2_bigk",       2,     16384, 16, 4,  3000, "L2",     1,   4096, None, None, 0.0),
     ("cos_w4_batch",     4,     40000, 32, 150, 20,  "Cosine", 1,   1024, 0.9,  None, 0.0),
+    # cosine batch with no filter and no empty chunks: the one-wave-per-SIMD
+    # batch kernel with the ordinal planes and a non-zero ordinal base per rank
+    ("cos_w4_batch_plain", 4,   262144, 64, 200, 20, "Cosine", 1,   2048, None, None, 0.0),
 ]
 
 
@@ -140,18 +143,32 @@ def test_loopback_ranks_equal_oracle(mq, cfg):
                 row_offset=r0)))
 
         def one(r):
+            # the same call three times: the first runs the validated path
+            # (header exchange + sync), the repeats the one-sync fast path
+            from myscaledb_amd import _lib
             r0, r1, seg = segs[r]
-            return ranks[r].sharded_search(seg, q, k, filter_bitmap=slice_bitmap(flt, n, r0, r1),
-                                           row_exists=slice_bitmap(rex, n, r0, r1))
+            res = []
+            for _ in range(3):
+                res.append(ranks[r].sharded_search(seg, q, k, filter_bitmap=slice_bitmap(flt, n, r0, r1),
+                                                   row_exists=slice_bitmap(rex, n, r0, r1)))
+            return res, ranks[r].stats(), _lib.last_search_stats()
 
         out, errs = _run_ranks(ranks, one)
         for e in errs:
             if e is not None:
                 raise e
         for r in range(world):
-            ig, dg = out[r]
-            bad = np.argwhere((ig != io) | (dg.view(np.uint32) != do.view(np.uint32)))
-            assert len(bad) == 0, f"{name} rank {r}: {len(bad)} slots differ, first {tuple(bad[0])}"
+            res, cst, sst = out[r]
+            for i, (ig, dg) in enumerate(res):
+                bad = np.argwhere((ig != io) | (dg.view(np.uint32) != do.view(np.uint32)))
+                assert len(bad) == 0, f"{name} rank {r} call {i}: {len(bad)} slots differ, first {tuple(bad[0])}"
+            assert cst["fast_calls"] == 2, cst
+            if metric != "Cosine" or filt is None:
+                # (cosine with chunk-emptying filters re-runs: the guessed
+                # ordinal bases are wrong; every other case stays on one sync)
+                assert cst["redo_calls"] == 0, cst
+            if name == "cos_w4_batch_plain":
+                assert sst["batch_kernel"] == 1, sst
     finally:
         for _, _, s in segs:
             s.free()
@@ -206,3 +223,67 @@ def test_comm_errors(comm):
     from myscaledb_amd.sharded import RcclComm
     with pytest.raises(MqvsError):
         RcclComm(2, 5, bytes(128))
+
+
+def test_loopback_rank_failing_after_header_fails_everywhere(mq):
+    """a rank whose LOCAL SEARCH fails (after the header exchange
+    validated the call: here its shard was prepared for cosine, the call asks
+    for L2) still joins the list exchange; every rank returns an error, none
+    hangs, and the next valid call works."""
+    from myscaledb_amd._lib import MqvsError
+    from myscaledb_amd.sharded import LoopbackComm
+    n, d, gran = 8192, 16, 1024
+    rows = O.generate(9, 1, 0, n, d)
+    q = O.generate(10, 1, 0, 5, d)
+    ranks = LoopbackComm.group(2)
+    good = [mq.VectorScanSegment.from_rows(rows[:4096], metric="L2", granule=gran, row_offset=0),
+            mq.VectorScanSegment.from_rows(rows[4096:], metric="L2", granule=gran, row_offset=4096)]
+    bad = mq.VectorScanSegment.from_rows(rows[4096:], metric="Cosine", granule=gran, row_offset=4096)
+    try:
+        _, errs = _run_ranks(ranks, lambda r: ranks[r].sharded_search(good[0] if r == 0 else bad, q, 10,
+                                                                      metric="L2"))
+        assert all(isinstance(e, MqvsError) for e in errs), errs
+        assert "rank 1" in str(errs[0]) and "different metric" in str(errs[1]), errs
+        io, do = O.vector_scan(rows, q, 10, O.METRICS["L2"], gran, fast=True)
+        out, errs = _run_ranks(ranks, lambda r: ranks[r].sharded_search(good[r], q, 10))
+        assert errs == [None, None], errs
+        for ig, dg in out:
+            assert np.array_equal(ig, io) and np.array_equal(dg.view(np.uint32), do.view(np.uint32))
+    finally:
+        for s_ in good + [bad]:
+            s_.free()
+        for c in ranks:
+            c.free()
+
+
+def test_loopback_ranks_on_different_paths_fail_then_recover(mq):
+    """Rank 0 repeats the last validated call (fast path: header, search and
+    list exchange enqueued without a sync) while rank 1 changes k (validated
+    path: header exchange + sync).  Rank 1 sees rank 0's fast flag, joins the
+    pending list exchange, and both fail; the next agreeing call succeeds."""
+    from myscaledb_amd._lib import MqvsError
+    from myscaledb_amd.sharded import LoopbackComm
+    n, d, gran = 8192, 16, 1024
+    rows = O.generate(11, 1, 0, n, d)
+    q = O.generate(12, 1, 0, 4, d)
+    ranks = LoopbackComm.group(2)
+    segs = [mq.VectorScanSegment.from_rows(rows[:4096], metric="IP", granule=gran, row_offset=0),
+            mq.VectorScanSegment.from_rows(rows[4096:], metric="IP", granule=gran, row_offset=4096)]
+    try:
+        _, errs = _run_ranks(ranks, lambda r: ranks[r].sharded_search(segs[r], q, 10))
+        assert errs == [None, None], errs
+        _, errs = _run_ranks(ranks, lambda r: ranks[r].sharded_search(segs[r], q, 10 if r == 0 else 12))
+        assert all(isinstance(e, MqvsError) for e in errs), errs
+        assert all("disagree" in str(e) for e in errs), errs
+        io, do = O.vector_scan(rows, q, 12, O.METRICS["IP"], gran, fast=True)
+        for _ in range(2):
+            out, errs = _run_ranks(ranks, lambda r: ranks[r].sharded_search(segs[r], q, 12))
+            assert errs == [None, None], errs
+            for ig, dg in out:
+                assert np.array_equal(ig, io) and np.array_equal(dg.view(np.uint32), do.view(np.uint32))
+        assert ranks[0].stats()["fast_calls"] == 2  # the failed repeat and the last call
+    finally:
+        for s_ in segs:
+            s_.free()
+        for c in ranks:
+            c.free()

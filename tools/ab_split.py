@@ -30,10 +30,15 @@ def main():
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--no-exact", action="store_true")
     ap.add_argument("--qseed", type=lambda s: int(s, 0), default=0x5EED0002)
+    ap.add_argument("--dbg", action="store_true",
+                    help="load the measurement build libmqvs_dbg.so (reads MQVS_* A/B switches)")
     args = ap.parse_args()
     import torch
     import myscaledb_amd as mq
     from myscaledb_amd import _lib
+    if args.dbg:
+        from myscaledb_amd import _lib as _mq_lib
+        _mq_lib.use_measurement_build()
     from myscaledb_amd.vector_scan import generate_device, set_timing, set_prefilter, set_batch_mode
     mq.init(0)
     tunes = [t for t in args.tunes.split(";") if t] or [""]

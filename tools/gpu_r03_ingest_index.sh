@@ -31,12 +31,12 @@ for step in $STEPS; do
       run m3_16384 300 python -u tools/index_sweep.py --mode 3 --build nlist=16384 --search "nprobe=4;nprobe=8;nprobe=16;nprobe=32;nprobe=64" --reps 3 ;;
     sweep)
       S="nprobe=1;nprobe=2;nprobe=4;nprobe=8;nprobe=16;nprobe=32"
-      run m3_65536_flat 300 env MQVS_LIB=dbg MQVS_IVF_COARSE=1 python -u tools/index_sweep.py --mode 3 --build nlist=65536 --search "$S" --reps 3
-      run m3_65536_list 300 env MQVS_LIB=dbg MQVS_IVF_COARSE=0 python -u tools/index_sweep.py --mode 3 --build nlist=65536 --search "nprobe=1;nprobe=2" --reps 3
-      run m2_65536 300 env MQVS_LIB=dbg python -u tools/index_sweep.py --mode 2 --build nlist=65536 --search "$S" --reps 3
-      run m2_16384 300 env MQVS_LIB=dbg python -u tools/index_sweep.py --mode 2 --build nlist=16384 --search "$S" --reps 3
-      run m3_65536_s1m 300 env MQVS_LIB=dbg python -u tools/index_sweep.py --mode 3 --build nlist=65536,sample=1048576 --search "nprobe=1;nprobe=2;nprobe=4" --reps 3
-      run m2_10000_flat 300 env MQVS_LIB=dbg python -u tools/index_sweep.py --mode 2 --build nlist=10000 --search "nprobe=2;nprobe=4;nprobe=8" --reps 3 ;;
+      run m3_65536_flat 300 env MQVS_IVF_COARSE=1 python -u tools/index_sweep.py --dbg --mode 3 --build nlist=65536 --search "$S" --reps 3
+      run m3_65536_list 300 env MQVS_IVF_COARSE=0 python -u tools/index_sweep.py --dbg --mode 3 --build nlist=65536 --search "nprobe=1;nprobe=2" --reps 3
+      run m2_65536 300 python -u tools/index_sweep.py --dbg --mode 2 --build nlist=65536 --search "$S" --reps 3
+      run m2_16384 300 python -u tools/index_sweep.py --dbg --mode 2 --build nlist=16384 --search "$S" --reps 3
+      run m3_65536_s1m 300 python -u tools/index_sweep.py --dbg --mode 3 --build nlist=65536,sample=1048576 --search "nprobe=1;nprobe=2;nprobe=4" --reps 3
+      run m2_10000_flat 300 python -u tools/index_sweep.py --dbg --mode 2 --build nlist=10000 --search "nprobe=2;nprobe=4;nprobe=8" --reps 3 ;;
   esac
 done
 exit 0

@@ -26,10 +26,15 @@ def main():
                     help="';'-separated search param strings")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--query-seed", type=lambda x: int(x, 0), default=0x5EED0001)
+    ap.add_argument("--dbg", action="store_true",
+                    help="load the measurement build libmqvs_dbg.so (reads MQVS_* A/B switches)")
     args = ap.parse_args()
     import numpy as np
     import torch
     import myscaledb_amd as mq
+    if args.dbg:
+        from myscaledb_amd import _lib as _mq_lib
+        _mq_lib.use_measurement_build()
     from myscaledb_amd.vector_index import last_index_stats
     from myscaledb_amd.vector_scan import generate_device
     mq.init(0)

@@ -23,10 +23,15 @@ def main():
     ap.add_argument("--d", type=int, default=768)
     ap.add_argument("--kind", default="gauss,quantised")
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--dbg", action="store_true",
+                    help="load the measurement build libmqvs_dbg.so (reads MQVS_* A/B switches)")
     args = ap.parse_args()
     import numpy as np
     import torch
     import myscaledb_amd as mq
+    if args.dbg:
+        from myscaledb_amd import _lib as _mq_lib
+        _mq_lib.use_measurement_build()
     from oracle import oracle as O
     mq.init(0)
     n, d = args.n, args.d
