@@ -140,7 +140,8 @@ void launch_query_bound(const ScanParams &p, int metric, const float *ynorm_max,
 
 // ---------------------------------------------------------------------------
 // k-th best approximate value of each query's probe row -> its APPEND
-// threshold (k-th -/+ 2B) and the probe rows that pass it.  1024 threads per
+// threshold (k-th -/+ 2B) and the probe rows that pass it (cand null: the
+// threshold only -- the batch probe's per-half-tile maxima, kernels_p4.hip).  1024 threads per
 // query, 16 values in flight per thread (float4 x 4) in every radix pass and
 // in the append: the probe row (L2-resident) is read five times, never with
 // one dependent load in flight per thread.
@@ -184,6 +185,7 @@ __global__ __launch_bounds__(kPsThreads) void k_probe_select_wide(const float *p
     else
         tt = widen<METRIC>(okey_value<METRIC>(prefix), bq[q]);
     if (t == 0) thr[q] = tt;
+    if (!cand) return;  // (the batch probe's maxima: threshold only)
     for_each_f4<kPsThreads>(row, P, [&](int64_t i, float raw) {
         const bool take = (METRIC == MQVS_METRIC_L2) ? (raw <= tt) : (raw >= tt);
         if (take) {

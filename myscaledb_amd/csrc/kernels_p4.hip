@@ -41,6 +41,15 @@
 // make the wave wait for every LDS-DMA piece in flight; a full queue falls back
 // to exactly that (correct, slower).
 //
+// PROBE (p.p4_gmax set): the same scan over the probe rows, with no threshold
+// tests: per query and 128-row half tile (one wave's rows of an item) the
+// best approximate value is written to p4_gmax[q][2 t + wr] as a raw metric
+// value (L2: fl(qn - 2 acc)).  The k-th best of those maxima is the k-th best
+// of k actual rows, so k_probe_select_wide turns it into an append threshold
+// with the same guarantee as the dense probe matrix it replaces (at nq 1000:
+// 2.8 MB written instead of 360 MB); the main scan then covers the probe rows
+// too.
+//
 // Items: XCD x = blockIdx % 8 takes tiles t = x (mod 8); its
 // workgroups form groups of nqb query blocks that stream the same row tiles,
 // so a tile's rows are shared through that XCD's L2.
@@ -145,7 +154,7 @@ __device__ inline void p4_barrier() {
 // kept live by one read per block), 32 = threshold tests without walks,
 // 128 = no stage barrier, 256 = no fragment-read wait before it, 512 = cosine
 // query variant 0 for every chunk
-template <int METRIC, int NBUF, int DIAG = 0, int PL = 0>
+template <int METRIC, int NBUF, int DIAG = 0, int PL = 0, bool PROBE = false>
 __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32x4 *queue, int qcap, int tmap) {
     constexpr bool L2 = METRIC == MQVS_METRIC_L2;
     // cache policy of the row / query pieces (PL bits 4 / 8: nt)
@@ -400,6 +409,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
     auto frag = [&](const unsigned char *st, int off) __attribute__((always_inline)) { return *reinterpret_cast<const bf16x8 *>(st + off); };
 
     f32x16 acc[4][4];
+    float gmx[4] = {-__builtin_inff(), -__builtin_inff(), -__builtin_inff(), -__builtin_inff()};  // PROBE
     int qcnt = 0;  // this wave's queue entries (wave-uniform)
     u32x4 *wq_base = queue + (int64_t)(blockIdx.x * 4 + w) * qcap;
 
@@ -421,8 +431,42 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
     // any lane over it walks its values.  The tests run in the MFMA gaps of
     // the stages around an item boundary (below), not as an epilogue of their
     // own.
-    auto check_block = [&](auto RB, auto JB, int ecr0, int ecrn) __attribute__((always_inline)) {
+    auto check_block = [&](auto RB, auto JB, int ecr0, int ecrn, int eti) __attribute__((always_inline)) {
         constexpr int rb = decltype(RB)::value, jb = decltype(JB)::value;
+        if constexpr (PROBE) {
+            // the lane's best value of the block (rows past the item: -inf),
+            // folded into its query's running maximum; after the wave's last
+            // row block the two half-waves' maxima combine and lanes 0..31
+            // write one raw value per query
+            const f32x16 blk = acc[rb][jb];
+            f32x4 v4[4];
+#pragma unroll
+            for (int g = 0; g < 4; ++g)
+                v4[g] = p4_aread4(blk[4 * g], blk[4 * g + 1], blk[4 * g + 2], blk[4 * g + 3]);
+            if (ecrn < kP4Tile) {
+                const int rbl = wr * 128 + rb * 32 + 4 * h;
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (rbl + (r & 3) + 8 * (r >> 2) >= ecrn) v4[r >> 2][r & 3] = -__builtin_inff();
+            }
+            float mx = v4[0][0];
+#pragma unroll
+            for (int r = 1; r < 16; ++r) mx = __builtin_elementwise_maximum(mx, v4[r >> 2][r & 3]);
+            gmx[jb] = __builtin_elementwise_maximum(gmx[jb], mx);
+            if constexpr (rb == 3) {
+                const float o = __shfl_xor(gmx[jb], 32);
+                const float v = __builtin_elementwise_maximum(gmx[jb], o);
+                const int j = q0 + wq * 128 + jb * 32 + l32;
+                if (h == 0 && j < p.nq) {
+                    float raw = v;
+                    if constexpr (L2) raw = qnl[jb] - 2.0f * v;
+                    if (v == -__builtin_inff()) raw = __builtin_nanf("");
+                    p.p4_gmax[(int64_t)j * p.p4_gld + 2 * eti + wr] = raw;
+                }
+                gmx[jb] = -__builtin_inff();
+            }
+            return;
+        }
         if constexpr ((DIAG & 16) != 0) {
             // (diagnostic: keep the accumulators live, test nothing)
             const f32x16 blk = acc[rb][jb];
@@ -488,7 +532,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
         }
     };
 
-    int pcr0 = 0, pcrn = 0;  // rows of the previous item (its blocks 8..15 are tested in the next one)
+    int pcr0 = 0, pcrn = 0, pti = 0;  // the previous item (its blocks 8..15 are tested in the next one)
 
     // k-step-0 phase: 16 MFMAs on (a0, b0); between them the k-step-1
     // fragments of this stage and the 8 LDS-DMA pieces of stage gc + D.
@@ -501,7 +545,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
         p4_for<16>([&](auto X) __attribute__((always_inline)) {
             constexpr int x = decltype(X)::value, rb = x >> 2, jb = x & 3;
             if constexpr (FIRST && EPI2 && x >= 8)
-                check_block(std::integral_constant<int, rb>{}, std::integral_constant<int, jb>{}, pcr0, pcrn);
+                check_block(std::integral_constant<int, rb>{}, std::integral_constant<int, jb>{}, pcr0, pcrn, pti);
             if constexpr (FIRST && L2 && jb == 0) {
                 // C = -yn / 2 of the block's rows (the item's norms in LDS)
                 const unsigned char *nb_ = norm_lds + (items_done & 1) * 1024;
@@ -574,7 +618,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
                 issue_piece(4 + ((x - 8) >> 1));
             if constexpr (LAST && x >= 2 && x < 10)
                 check_block(std::integral_constant<int, ((x - 2) >> 2)>{}, std::integral_constant<int, (x - 2) & 3>{},
-                            cr0, crn);
+                            cr0, crn, ti_c);
             __builtin_amdgcn_sched_barrier(0);
         });
         if constexpr ((PL & 3) != 0) issue_advance();
@@ -596,6 +640,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
         do_stage(F{}, F{}, T{});
         pcr0 = cr0;
         pcrn = cr1 - cr0;
+        pti = ti_c;
         first_item = false;
         ++items_done;
         int cord;
@@ -605,8 +650,9 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
     // blocks 8..15 of the last item
     p4_for<8>([&](auto X) __attribute__((always_inline)) {
         constexpr int x = decltype(X)::value + 8;
-        check_block(std::integral_constant<int, (x >> 2)>{}, std::integral_constant<int, (x & 3)>{}, pcr0, pcrn);
+        check_block(std::integral_constant<int, (x >> 2)>{}, std::integral_constant<int, (x & 3)>{}, pcr0, pcrn, pti);
     });
+    if constexpr (PROBE) return;
     // flush this wave's queue to the per-query candidate lists
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     const int nqueue = qcnt < qcap ? qcnt : qcap;
@@ -764,6 +810,39 @@ static bool launch_p4_t(ScanParams p, hipStream_t s) {
         hipLaunchKernelGGL((k_scan_p4<METRIC, 4, 0>), grid, dim3(256), 0, s, p, slots, q, kP4QueueCap, tmap);
     }
     return true;
+}
+
+// the batch probe (PROBE above): the same launch conditions; false when the
+// probe rows cannot take the batch kernel (the caller runs the dense probe)
+template <int METRIC>
+static bool launch_p4_probe_t(ScanParams p, hipStream_t s) {
+    if (!p.p4_queue || !p.p4_gmax || p.row_list || p.chunk_ord || p.tiles < 1 || p.tile_rows != kP4Tile) return false;
+    p.num_qblocks = (p.nq + kP4Tile - 1) / kP4Tile;
+    int dev = 0, cus = 0;
+    MQVS_HIP(hipGetDevice(&dev));
+    MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int per_xcd = cus / 8;
+    if (p.num_qblocks > per_xcd || p.dpad % kP4HiK) return false;
+    if (p.row_begin % 16 || (p.tiles_per_chunk > 0 && p.chunk_rows % 16)) return false;
+    if (p.row_begin < 0 || p.row_end + p.chunk_rows + p.tile_rows > 0x7FFFFFFF || p.tiles > 0x3FFFFFFF ||
+        p.chunk_rows < 1)
+        return false;
+    if ((double)p.maxv * (double)p.q_vpad * (double)p.dpad * 2.0 >= 4294967296.0) return false;
+    if (p.p4_gld < 2 * p.tiles) return false;
+    if (METRIC == MQVS_METRIC_L2 && !p.row_norms) return false;
+    const int slots = per_xcd / p.num_qblocks * p.num_qblocks;
+    hipLaunchKernelGGL((k_scan_p4<METRIC, 4, 0, 0, true>), dim3((unsigned)(8 * per_xcd)), dim3(256), 0, s, p, slots,
+                       reinterpret_cast<u32x4 *>(p.p4_queue), kP4QueueCap, 1);
+    return true;
+}
+
+bool launch_scan_p4_probe(const ScanParams &p, int metric, hipStream_t s) {
+    switch (metric) {
+        case MQVS_METRIC_L2: return launch_p4_probe_t<MQVS_METRIC_L2>(p, s);
+        case MQVS_METRIC_IP: return launch_p4_probe_t<MQVS_METRIC_IP>(p, s);
+        case MQVS_METRIC_COSINE: return launch_p4_probe_t<MQVS_METRIC_COSINE>(p, s);
+        default: return launch_p4_probe_t<kMetricIpRaw>(p, s);
+    }
 }
 
 bool launch_scan_p4(const ScanParams &p, int metric, hipStream_t s) {

@@ -603,9 +603,6 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     p.cand_count = count;
     p.cand = cand;
     p.cand_cap = cap;
-    float *probe = (float *)ws.probe.get(sizeof(float) * (size_t)nq * P);
-    p.probe = probe;
-    p.probe_ld = P;
 
     float *bq = nullptr;
     if (kind == kScanBf16) {
@@ -648,14 +645,45 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     }
 
     const Range pr = make_range(0, P, tile_rows, seg->granule, aligned);
-    const Range mr = make_range(P, scan_n, tile_rows, seg->granule, aligned);
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[5], s));
     (void)take_batch_kernel_flag();
-    run_scan(p, pr, kind, metric, true, s);
+    // The batch probe (kernels_p4.hip PROBE): the batch kernel over the probe
+    // rows writes one best value per (query, 128-row half tile) instead of the
+    // dense [nq][P] matrix; the threshold comes from the k-th of those maxima
+    // and the main scan then starts at row 0 (the probe rows are re-scanned,
+    // ~P / n of the main scan).  Otherwise the dense probe and its select,
+    // which also appends the probe rows that pass.
+    bool bprobe = false;
+    float *probe = nullptr;
+    int64_t probe_cols = P, probe_ld = P;
+    if (kind == kScanBf16 && p.p4_queue && !row_list && P < scan_n && pr.tiles > 0) {
+        const int64_t gld = round_up(2 * pr.tiles, 4);
+        probe = (float *)ws.probe.get(sizeof(float) * (size_t)nq * gld);
+        ScanParams pp = p;
+        pp.row_begin = pr.begin;
+        pp.row_end = pr.end;
+        pp.tiles = pr.tiles;
+        pp.tiles_per_chunk = pr.tiles_per_chunk;
+        pp.tile_rows = kBfRows;
+        pp.p4_gmax = probe;
+        pp.p4_gld = gld;
+        bprobe = launch_scan_p4_probe(pp, metric, s);
+        MQVS_HIP(hipGetLastError());
+        if (bprobe) {
+            probe_cols = 2 * pr.tiles;
+            probe_ld = gld;
+        }
+    }
+    if (!bprobe) {
+        probe = (float *)ws.probe.get(sizeof(float) * (size_t)nq * P);
+        p.probe = probe;
+        p.probe_ld = P;
+        run_scan(p, pr, kind, metric, true, s);
+    }
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[1], s));
     if (kind == kScanBf16)
-        launch_probe_select_approx(probe, P, P, nq, k, metric, bq, (float *)p.thr, count, cand, cap, row_list,
-                                   s);
+        launch_probe_select_approx(probe, probe_cols, probe_ld, nq, k, metric, bq, (float *)p.thr, count,
+                                   bprobe ? nullptr : cand, cap, row_list, s);
     else
         launch_probe_select(probe, P, P, nq, k, metric, tau, count, cand, cap, 0, row_list, s);
     MQVS_HIP(hipGetLastError());
@@ -668,10 +696,12 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         const int64_t align = aligned ? seg->granule : tile_rows;
         Cand *alt = (Cand *)ws.cand2.get(sizeof(Cand) * (size_t)nq * cap);
         int *calt = (int *)ws.count2.get(sizeof(int) * nq);
-        int64_t b = P, seg_rows = std::max<int64_t>(tune.first * P, align);
+        // (the batch probe appended nothing: the first segment also covers
+        // the probe rows)
+        int64_t b = bprobe ? 0 : P, seg_rows = std::max<int64_t>(tune.first * P, align);
         int segs = 0;
         while (b < scan_n) {
-            const int64_t e = std::min(scan_n, round_up(b + seg_rows, align));
+            const int64_t e = std::min(scan_n, round_up(b + seg_rows + (segs == 0 && bprobe ? P : 0), align));
             const bool tev = timing && 2 * segs + 1 < Workspace::kSegEv;
             if (tev) MQVS_HIP(hipEventRecord(ws.seg_ev[2 * segs], s));
             run_scan(p, make_range(b, e, tile_rows, seg->granule, aligned), kind, metric, false, s);
@@ -690,7 +720,6 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
             }
         }
         st.segments = segs;
-        (void)mr;
     }
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[3], s));
     if (kind == kScanBf16) {
@@ -713,7 +742,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     st.prefilter = kind == kScanBf16 ? seg->split : 0;
     st.batch_kernel = take_batch_kernel_flag();
     st.probe_rows = P;
-    st.main_rows = scan_n - P;
+    st.main_rows = bprobe ? scan_n : scan_n - P;
     st.rows_scanned = scan_n;
     st.nq = nq;
     st.k = k;

@@ -176,6 +176,9 @@ struct ScanParams {
     int tau_strict;           // APPEND takes key < tau (segments after the probe) instead of <=
     unsigned long long *dbg;  // diagnostic builds only (stage timing stamps)
     void *p4_queue;           // batch scan (kernels_p4.hip): per-wave candidate queues, p4_queue_bytes()
+    float *p4_gmax;           // batch PROBE (kernels_p4.hip): [nq][p4_gld] best approximate value per
+                              // (query, 128-row half tile), as a raw metric value; NaN = no row
+    int64_t p4_gld;
     int blas_nq;              // batch size that selects faiss's distance formula (0: nq); a query
                               // sub-batch of a larger call keeps the call's formula
 };
@@ -359,6 +362,9 @@ void launch_scan_hi(const ScanParams &p, int metric, bool probe, hipStream_t s);
 // batch APPEND scan at one wave per SIMD (kernels_p4.hip): false when the
 // scan's shape is not served (gather lists, chunk-ordinal tables, no queue)
 bool launch_scan_p4(const ScanParams &p, int metric, hipStream_t s);
+// the batch probe (p.p4_gmax, p.p4_gld >= 2 p.tiles): false when the rows
+// cannot take the batch kernel
+bool launch_scan_p4_probe(const ScanParams &p, int metric, hipStream_t s);
 // cosine ordinal planes for the batch kernel: at most pcap planes, built on
 // the device from q_hi / qmu / qlam (desc[2] = 0 when the chains need more)
 constexpr int kP4OrdPlanesMax = 32;
