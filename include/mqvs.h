@@ -510,6 +510,30 @@ int mqvs_set_prefilter(int split);
  * formula (faiss's nx >= 20 branch) and return the same bits.  Returns the
  * previous value; 0 leaves it unchanged. */
 size_t mqvs_set_scratch_budget(size_t bytes);
+/* Process-wide cap on the device memory of all threads' search workspaces
+ * (each calling thread keeps one per device: query variants, candidate lists,
+ * sort scratch -- about 1 GB at nq 1000).  The reference admits 2 x physical
+ * cores concurrent scans (MergeTreeVSManager.cpp:972-975); here a workspace
+ * growth that would pass the cap first frees idle threads' workspaces, then
+ * waits until running searches finish and give theirs back (a search that
+ * ends while others wait frees its workspace).  Only when every running
+ * search is waiting does one go over the cap (counted in over_budget) instead
+ * of deadlocking.  Default: a quarter of the device memory.  Returns the
+ * previous value; 0 leaves it unchanged.  (Index-search buffers and segments
+ * are not counted.) */
+size_t mqvs_set_workspace_budget(size_t bytes);
+typedef struct {
+    size_t budget;       /* the cap */
+    size_t held;         /* device bytes of all workspaces now */
+    size_t peak;         /* most held at once (since the last reset) */
+    int64_t waits;       /* growths that waited for memory */
+    int64_t trims;       /* workspaces freed for others */
+    int64_t over_budget; /* growths let over the cap (every running search waiting) */
+    int32_t active;      /* threads inside a search now */
+    int32_t workspaces;  /* workspaces registered (threads x devices) */
+} mqvs_workspace_stats_t;
+/* reset_peak: restart peak (at held) and the counters after reading */
+int mqvs_workspace_stats(mqvs_workspace_stats_t *out, int32_t reset_peak);
 /* Achievable HBM read rate of this device (a bench utility: the measured
  * denominator of the scan's HBM fraction).  A STREAM-like read
  * sweep -- every lane loads 16 B, 4 loads in flight, grid-stride, 8

@@ -44,7 +44,7 @@ SYMBOLS = [
     "mqvs_segment_set_rows_host", "mqvs_segment_rows_host",
     "mqvs_search", "mqvs_search_ex", "mqvs_knn_raw", "mqvs_rerank", "mqvs_merge_shards", "mqvs_generate_device",
     "mqvs_last_search_stats", "mqvs_set_timing", "mqvs_set_batch_mode", "mqvs_set_gather_mode", "mqvs_set_prefilter",
-    "mqvs_set_scratch_budget", "mqvs_measure_read_bandwidth",
+    "mqvs_set_scratch_budget", "mqvs_measure_read_bandwidth", "mqvs_set_workspace_budget", "mqvs_workspace_stats",
     "mqvs_index_build", "mqvs_index_free", "mqvs_index_info", "mqvs_index_search", "mqvs_index_last_stats",
     "mqvs_segment_create_binary", "mqvs_search_binary", "mqvs_knn_binary_raw",
     "mqvs_segment_create_from_column", "mqvs_async_check",
@@ -79,6 +79,12 @@ class CacheStats(ctypes.Structure):
     _fields_ = [("items", ctypes.c_int64), ("bytes", ctypes.c_size_t), ("max_bytes", ctypes.c_size_t),
                 ("hits", ctypes.c_int64), ("misses", ctypes.c_int64), ("evictions", ctypes.c_int64),
                 ("pinned", ctypes.c_int64), ("expired_held", ctypes.c_int64)]
+
+
+class WorkspaceStats(ctypes.Structure):
+    _fields_ = [("budget", ctypes.c_size_t), ("held", ctypes.c_size_t), ("peak", ctypes.c_size_t),
+                ("waits", ctypes.c_int64), ("trims", ctypes.c_int64), ("over_budget", ctypes.c_int64),
+                ("active", ctypes.c_int32), ("workspaces", ctypes.c_int32)]
 
 
 class IndexSearchStats(ctypes.Structure):
@@ -139,6 +145,8 @@ def _load(path=LIB_PATH):
         "mqvs_set_batch_mode": ([ctypes.c_int], ctypes.c_int),
         "mqvs_set_gather_mode": ([ctypes.c_int], ctypes.c_int),
         "mqvs_set_scratch_budget": ([ctypes.c_size_t], ctypes.c_size_t),
+        "mqvs_set_workspace_budget": ([ctypes.c_size_t], ctypes.c_size_t),
+        "mqvs_workspace_stats": ([P, ctypes.c_int32], ctypes.c_int),
         "mqvs_measure_read_bandwidth": ([ctypes.c_size_t, ctypes.c_int32, P, P], ctypes.c_int),
         "mqvs_set_prefilter": ([ctypes.c_int], ctypes.c_int),
         "mqvs_index_build": ([P, ctypes.c_char_p, ctypes.c_char_p, P], ctypes.c_int),
@@ -231,6 +239,18 @@ def last_search_stats():
     st = SearchStats()
     check(lib.mqvs_last_search_stats(ctypes.byref(st)))
     return {f: getattr(st, f) for f, _ in SearchStats._fields_}
+
+
+def workspace_stats(reset_peak=False):
+    """mqvs_workspace_stats as a dict (bytes and counters of the workspace budget)."""
+    st = WorkspaceStats()
+    check(lib.mqvs_workspace_stats(ctypes.byref(st), 1 if reset_peak else 0))
+    return {f: getattr(st, f) for f, _ in WorkspaceStats._fields_}
+
+
+def set_workspace_budget(nbytes):
+    """mqvs_set_workspace_budget: returns the previous cap (0 leaves it unchanged)."""
+    return lib.mqvs_set_workspace_budget(int(nbytes))
 
 
 def last_index_stats():

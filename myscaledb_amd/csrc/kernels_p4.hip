@@ -663,6 +663,441 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
     }
 }
 
+// ---------------------------------------------------------------------------
+// k_scan_p4m: the same scan on v_mfma_f32_16x16x32_bf16.  Items, ring, DMA
+// pieces, stage barrier and queue are those of k_scan_p4; only the tile inside
+// a wave changes: its 128 rows x 128 queries are 8 x 8 blocks of 16 x 16 (64
+// f32x4 accumulators = the same 256 AGPRs), and a 32-column stage is ONE
+// k-step (lane l: row / query l & 15, chunk l >> 4 of the stage image).  The
+// 64 MFMAs of a stage run as two phases of 32: phase 0 = row blocks 0..3
+// (reading this stage's A fragments 4..7 and issuing the DMA pieces of stage
+// s + D in its gaps), barrier, phase 1 = row blocks 4..7, query block by query
+// block, each B fragment re-read for the next stage right after its last MFMA
+// here (with A 0..3: the next stage's fragments, 16 x 4 VGPRs as before).
+// Why: on random data the chip holds a higher clock on this shape than on
+// 32x32x16 at the same cycles per flop (MI355X_MICROARCH.md, DVFS give-back
+// item 7).  Threshold tests: per query block, the 16 values of four row blocks
+// (row blocks 0..3 in the last stage's phase 1, 4..7 in the next item's first
+// phase 0, before their first MFMA overwrites them).
+template <int METRIC, int NBUF, bool PROBE = false>
+__global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u32x4 *queue, int qcap, int tmap) {
+    constexpr bool L2 = METRIC == MQVS_METRIC_L2;
+    constexpr int D = NBUF - 1;
+    static_assert(D >= 1 && D <= 4, "ring depth");
+    constexpr int NORM = L2 ? 2048 : 0;
+    constexpr int WSCR = 4 * 64 * 16 * 4;
+    constexpr int QTAB = L2 ? kP4Tile * 8 : 0;  // L2: (threshold, |q|^2) of the item's queries for the walks
+    constexpr int NPW = 8;
+    __shared__ __attribute__((aligned(16))) unsigned char lds[NBUF * kP4Stage + NORM + WSCR + QTAB];
+    unsigned char *norm_lds = lds + NBUF * kP4Stage;
+    float *qtab = reinterpret_cast<float *>(lds + NBUF * kP4Stage + NORM + WSCR);
+
+    const int t = threadIdx.x, lane = t & 63, w = __builtin_amdgcn_readfirstlane(t >> 6);
+    const int wr = w & 1, wq = w >> 1;
+    const int xcd = blockIdx.x % 8, slot = blockIdx.x / 8;
+    const int nqb = p.num_qblocks;
+    const int ngroups = slots / nqb;
+    if (slot >= ngroups * nqb) return;
+    const int qb = slot % nqb, tg = slot / nqb;
+    const int q0 = qb * kP4Tile;
+    const int tstride = 8 * ngroups;
+    const int nst = (int)(p.dpad / kP4HiK);
+    const int l16 = lane & 15, g4 = lane >> 4;
+    float *wscr = reinterpret_cast<float *>(lds + NBUF * kP4Stage + NORM) + w * 1024;
+
+    int om0 = 0, oln = 1;
+    bool ordm = false;
+    if (p.q_ord_desc) {
+        om0 = __builtin_amdgcn_readfirstlane(p.q_ord_desc[0]);
+        oln = __builtin_amdgcn_readfirstlane(p.q_ord_desc[1]);
+        ordm = __builtin_amdgcn_readfirstlane(p.q_ord_desc[2]) != 0;
+    }
+    const bool pervar = p.maxv > 1 && !ordm;
+    int qmu[4], qlam[4];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+        int j = q0 + (w + 4 * i) * 16 + (lane >> 2);
+        if (j >= p.nq) j = 0;
+        qmu[i] = 0;
+        qlam[i] = 1;
+        if (pervar) {
+            qmu[i] = p.qmu[j];
+            qlam[i] = p.qlam[j];
+        }
+    }
+    // thresholds of the lane's query in each of the wave's 8 query blocks (as
+    // k_scan_p4: L2 pre-checks acc >= (qn - t) / 2 less a rounding slack); the
+    // L2 walk's exact test reads t and |q|^2 from an LDS table (registers are
+    // scarce here, walks rare)
+    float thr[8];
+#pragma unroll
+    for (int jb = 0; jb < 8; ++jb) {
+        const int j = q0 + wq * 128 + jb * 16 + l16;
+        const float tj = j < p.nq ? p.thr[j] : 0.f;
+        if constexpr (L2) {
+            const float qn = j < p.nq ? p.qnorms[j] : 0.f;
+            const float half = (qn - tj) * 0.5f;
+            thr[jb] = half - 4.8e-7f * (fabsf(qn) + fabsf(tj)) - 1e-30f;
+        } else {
+            thr[jb] = tj;
+        }
+        if (j >= p.nq) thr[jb] = __builtin_inff();
+        asm volatile("" : "+v"(thr[jb]));
+    }
+    if constexpr (L2) {
+        // (written before the first LDS-DMA; the prologue barrier orders it)
+        const int j = q0 + t;
+        qtab[2 * t] = j < p.nq ? p.thr[j] : 0.f;
+        qtab[2 * t + 1] = j < p.nq ? p.qnorms[j] : 0.f;
+        __syncthreads();
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) asm volatile("" : "+v"(qmu[i]), "+v"(qlam[i]));
+
+    const uint32_t tr = (uint32_t)p.tile_rows, cr = (uint32_t)p.chunk_rows;
+    const uint32_t tpc = (uint32_t)p.tiles_per_chunk;
+    const uint32_t c0 = tpc > 0 ? (uint32_t)p.row_begin / cr : 0u;
+    const uint32_t rbeg = (uint32_t)p.row_begin, rend = (uint32_t)p.row_end;
+    const int ntiles = (int)p.tiles;
+    auto item_at = [&](int ti, int &r0, int &r1, int &ord) __attribute__((always_inline)) -> bool {
+        const uint32_t tt = (uint32_t)ti;
+        uint32_t a, e, c;
+        if (tpc > 0) {
+            const uint32_t qd = tt / tpc, rem = tt - qd * tpc;
+            c = c0 + qd;
+            const uint32_t cs = c * cr;
+            a = cs + rem * tr;
+            e = a + tr < cs + cr ? a + tr : cs + cr;
+        } else {
+            a = rbeg + tt * tr;
+            e = a + tr;
+            c = a / cr;
+        }
+        if (e > rend) e = rend;
+        r0 = __builtin_amdgcn_readfirstlane((int)a);
+        r1 = __builtin_amdgcn_readfirstlane((int)e);
+        ord = __builtin_amdgcn_readfirstlane((int)c) + p.ord_base;
+        return r0 < r1;
+    };
+    auto next_item = [&](int ti, int &r0, int &r1, int &ord) __attribute__((always_inline)) -> int {
+        for (; ti < ntiles; ti += tstride)
+            if (item_at(ti, r0, r1, ord)) return ti;
+        return -1;
+    };
+
+    int ir0 = 0, ir1 = 0;
+    int iord = 0;
+    int ti_i = next_item(tmap ? xcd * ngroups + tg : xcd + 8 * tg, ir0, ir1, iord);
+    if (ti_i < 0) return;
+    const int nb = nst;
+    const uint32_t blk = (uint32_t)nb * 1024u;
+    uint32_t roff[4], qoff[4];
+    const unsigned char *rbase = nullptr;
+    const unsigned char *qplane = reinterpret_cast<const unsigned char *>(ordm ? p.q_ord : p.q_hi);
+    const uint64_t pstride = (uint64_t)(p.q_vpad >> 4) * blk;
+    uint32_t noff = 0;
+    const unsigned char *nbase = nullptr;
+    bool first_src = true;
+    auto set_src = [&]() __attribute__((always_inline)) {
+        int ln = lane;
+        asm volatile("" : "+v"(ln));
+        const uint32_t lc = (uint32_t)(ln >> 2) * 64u + (uint32_t)((ln & 3) ^ p4_g((ln >> 4) & 3)) * 16u;
+        rbase = reinterpret_cast<const unsigned char *>(p.rows_hi) + (uint64_t)(uint32_t)(ir0 >> 4) * blk;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int pc = w + 4 * i;
+            roff[i] = (ir0 + pc * 16 < ir1 ? (uint32_t)pc * blk : 0u) + lc;
+        }
+        if (ordm) {
+            const int pl = iord < om0 ? iord : om0 + (iord - om0) % oln;
+            qplane = reinterpret_cast<const unsigned char *>(p.q_ord) + (uint64_t)pl * pstride;
+        }
+        if (pervar || first_src) {
+#pragma unroll
+            for (int i = 0; i < 4; ++i) {
+                int j = q0 + (w + 4 * i) * 16 + (ln >> 2);
+                if (j >= p.nq) j = 0;
+                int var = 0;
+                if (pervar) {
+                    const int mu = qmu[i], lam = qlam[i];
+                    var = iord < mu ? iord : mu + (iord - mu) % lam;
+                }
+                const uint32_t u = (uint32_t)var * (uint32_t)p.q_vpad + (uint32_t)j;
+                qoff[i] = (u >> 4) * blk + (u & 15) * 64u + (uint32_t)((ln & 3) ^ p4_g((ln >> 4) & 3)) * 16u;
+            }
+        }
+        if constexpr (L2) {
+            nbase = reinterpret_cast<const unsigned char *>(p.row_norms + ir0);
+            const int last = ir1 - 1 - ir0;
+            noff = (uint32_t)(64 * w + ln < last ? 64 * w + ln : last) * 4u;
+        }
+    };
+    set_src();
+    first_src = false;
+    int si = 0, issued = 0, ibuf = 0, items_issued = 0;
+    bool live = true;
+    auto issue_piece = [&](int x) __attribute__((always_inline)) {
+        unsigned char *dst = lds + ibuf * kP4Stage;
+        if (x < 4) {
+            __builtin_amdgcn_global_load_lds((const void *)(rbase + (uint32_t)si * 1024u + roff[x]),
+                                             (lds_void *)(dst + (w + 4 * x) * 1024), 16, 0, 0);
+        } else if (x < 8) {
+            const uint32_t vo = (uint32_t)si * 1024u + qoff[x - 4];
+            const uint64_t qb_ = (uint64_t)qplane;
+            const unsigned char *qbase = reinterpret_cast<const unsigned char *>(
+                ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(qb_ >> 32)) << 32) |
+                (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)qb_));
+            __builtin_amdgcn_global_load_lds((const void *)(qbase + vo),
+                                             (lds_void *)(dst + kP4QOff + (w + 4 * (x - 4)) * 1024), 16, 0, 0);
+        } else if constexpr (L2) {
+            __builtin_amdgcn_global_load_lds((const void *)(nbase + noff),
+                                             (lds_void *)(norm_lds + (items_issued & 1) * 1024 + w * 256), 4, 0, 0);
+        }
+    };
+    auto issue_advance = [&]() __attribute__((always_inline)) {
+        if (!live) return;
+        ++issued;
+        ibuf = ibuf + 1 == NBUF ? 0 : ibuf + 1;
+        if (++si == nst) {
+            si = 0;
+            ++items_issued;
+            int r0 = 0, r1 = 0, o = 0;
+            const int tn = next_item(ti_i + tstride, r0, r1, o);
+            if (tn >= 0) {
+                ti_i = tn;
+                ir0 = r0;
+                ir1 = r1;
+                iord = o;
+                set_src();
+            } else {
+                live = false;
+                si = nst - 1;
+            }
+        }
+    };
+    auto issue_stage = [&]() __attribute__((always_inline)) {
+#pragma unroll
+        for (int x = 0; x < 8; ++x) issue_piece(x);
+        if (L2 && si == 0 && live) issue_piece(8);
+        issue_advance();
+    };
+
+    int cr0 = ir0, cr1 = ir1;
+    int ti_c = ti_i;
+    int gc = 0, cbuf = 0, items_done = 0;
+
+    // fragment offset: image row R = 16 i + (l & 15), chunk l >> 4
+    const int offm = l16 * 64 + (g4 ^ p4_g((l16 >> 2) & 3)) * 16;
+    const int rowA = wr * 128 * 64, rowB = kP4QOff + wq * 128 * 64;
+    auto frag = [&](const unsigned char *st, int off) __attribute__((always_inline)) {
+        return *reinterpret_cast<const bf16x8 *>(st + off);
+    };
+
+    f32x4 acc[8][8];
+    float gmx[8];  // PROBE: the lane's running best per query block
+#pragma unroll
+    for (int jb = 0; jb < 8; ++jb) gmx[jb] = -__builtin_inff();
+    int qcnt = 0;
+    u32x4 *wq_base = queue + (int64_t)(blockIdx.x * 4 + w) * qcap;
+
+    for (int s = 0; s < D; ++s) issue_stage();
+    p4_wait_vm<NPW>(issued - 1);
+    p4_barrier();
+    bf16x8 a[8], b[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) a[i] = frag(lds, rowA + i * 16 * 64 + offm);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) b[i] = frag(lds, rowB + i * 16 * 64 + offm);
+
+    // the test of query block jb over row blocks 4 hf .. 4 hf + 3 (16 values
+    // per lane, all of its query l & 15) of the item at rows ecr0 (ecrn rows)
+    auto check = [&](auto HF, auto JB, int ecr0, int ecrn, int eti) __attribute__((always_inline)) {
+        constexpr int hf = decltype(HF)::value, jb = decltype(JB)::value;
+        f32x4 v4[4];
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+            const f32x4 bk = acc[4 * hf + g][jb];
+            v4[g] = p4_aread4(bk[0], bk[1], bk[2], bk[3]);
+        }
+        // value v4[g][i]: row wr 128 + (4 hf + g) 16 + 4 g4 + i
+        const int rbl = wr * 128 + hf * 64 + 4 * g4;
+        if constexpr (PROBE) {
+            if (ecrn < kP4Tile) {
+#pragma unroll
+                for (int r = 0; r < 16; ++r)
+                    if (rbl + 16 * (r >> 2) + (r & 3) >= ecrn) v4[r >> 2][r & 3] = -__builtin_inff();
+            }
+        }
+        float mx = v4[0][0];
+#pragma unroll
+        for (int r = 1; r < 16; ++r) mx = __builtin_elementwise_maximum(mx, v4[r >> 2][r & 3]);
+        const int j = q0 + wq * 128 + jb * 16 + l16;
+        if constexpr (PROBE) {
+            gmx[jb] = __builtin_elementwise_maximum(gmx[jb], mx);
+            if constexpr (hf == 1) {
+                float v = __builtin_elementwise_maximum(gmx[jb], __shfl_xor(gmx[jb], 16));
+                v = __builtin_elementwise_maximum(v, __shfl_xor(v, 32));
+                if (g4 == 0 && j < p.nq) {
+                    float raw = v;
+                    if constexpr (L2) raw = qtab[2 * (j - q0) + 1] - 2.0f * v;
+                    if (v == -__builtin_inff()) raw = __builtin_nanf("");
+                    p.p4_gmax[(int64_t)j * p.p4_gld + 2 * eti + wr] = raw;
+                }
+                gmx[jb] = -__builtin_inff();
+            }
+            return;
+        }
+        if (__ballot(mx >= thr[jb]) == 0) return;
+        const float th = thr[jb];
+        float tj = 0.f, qn = 0.f;
+        if constexpr (L2) {
+            tj = qtab[2 * (j - q0)];
+            qn = qtab[2 * (j - q0) + 1];
+        }
+        unsigned m16 = 0;
+#pragma unroll
+        for (int r = 0; r < 16; ++r) m16 |= (v4[r >> 2][r & 3] >= th ? 1u : 0u) << r;
+#pragma unroll
+        for (int g = 0; g < 4; ++g) *reinterpret_cast<f32x4 *>(wscr + lane * 16 + 4 * g) = v4[g];
+#pragma unroll 1
+        while (__ballot(m16 != 0u) != 0) {
+            bool pass = m16 != 0u;
+            const int r = pass ? __builtin_ctz(m16) : 0;
+            m16 &= m16 - 1u;
+            const float x = wscr[lane * 16 + r];
+            float raw = x;
+            if constexpr (L2) {
+                raw = qn - 2.0f * x;
+                pass = pass && raw <= tj;
+            }
+            const int rl = rbl + 16 * (r >> 2) + (r & 3);
+            pass = pass && rl < ecrn;
+            const uint64_t m = __ballot(pass);
+            if (m == 0) continue;
+            const int pre =
+                __builtin_amdgcn_mbcnt_hi((unsigned)(m >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)m, 0u));
+            if (pass) {
+                const uint32_t row = (uint32_t)(ecr0 + rl);
+                const int slot_ = qcnt + pre;
+                if (slot_ < qcap)
+                    wq_base[slot_] = u32x4{__builtin_bit_cast(unsigned, raw), row, (unsigned)j, 0u};
+                else
+                    emit_approx<METRIC, false>(p, j, row, row, row_valid(p, row), raw);
+            }
+            qcnt += __popcll(m);
+        }
+    };
+
+    int pcr0 = 0, pcrn = 0, pti = 0;
+
+    // C of an item's first MFMA on a row block: 0, or -|y|^2 / 2 of its rows
+    auto cinit = [&](int rb) __attribute__((always_inline)) -> f32x4 {
+        if constexpr (L2) {
+            const unsigned char *nb_ = norm_lds + (items_done & 1) * 1024;
+            const f32x4 v = *reinterpret_cast<const f32x4 *>(nb_ + (wr * 128 + rb * 16 + 4 * g4) * 4);
+            return f32x4{-0.5f * v[0], -0.5f * v[1], -0.5f * v[2], -0.5f * v[3]};
+        } else {
+            return f32x4{0.f, 0.f, 0.f, 0.f};
+        }
+    };
+
+    // phase 0: row blocks 0..3 x query blocks 0..7; in its gaps this stage's
+    // A fragments 4..7, the DMA pieces of stage gc + D and (EPI) the tests of
+    // the previous item's row blocks 4..7
+    auto phase0 = [&](const unsigned char *st, auto first_tag, auto epi_tag) __attribute__((always_inline)) {
+        constexpr bool FIRST = decltype(first_tag)::value, EPI = decltype(epi_tag)::value;
+        f32x4 ci = f32x4{0.f, 0.f, 0.f, 0.f};
+        p4_for<32>([&](auto X) __attribute__((always_inline)) {
+            constexpr int x = decltype(X)::value, rb = x >> 3, jb = x & 7;
+            if constexpr (FIRST && EPI && (x & 3) == 1)
+                check(std::integral_constant<int, 1>{}, std::integral_constant<int, (x >> 2)>{}, pcr0, pcrn, pti);
+            if constexpr (FIRST && jb == 0) ci = cinit(rb);
+            if constexpr (FIRST)
+                acc[rb][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[jb], ci, 0, 0, 0);
+            else
+                acc[rb][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[jb], acc[rb][jb], 0, 0, 0);
+            if constexpr (x < 4)
+                a[4 + x] = frag(st, rowA + (4 + x) * 16 * 64 + offm);
+            else if constexpr (x >= 8 && (x - 8) % 3 == 0 && (x - 8) / 3 < 8)
+                issue_piece((x - 8) / 3);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+    };
+
+    // phase 1: row blocks 4..7, query block by query block; the next stage's
+    // B fragment jb right after its last MFMA here, its A fragments 0..3 in
+    // between; LAST: the tests of this item's row blocks 0..3
+    // (FIRST: row block by row block instead, so that one C value is live at
+    // a time; the B fragments are then re-read in the last eight gaps)
+    auto phase1 = [&](const unsigned char *sn, auto first_tag, auto last_tag, int crn) __attribute__((always_inline)) {
+        constexpr bool FIRST = decltype(first_tag)::value, LAST = decltype(last_tag)::value;
+        f32x4 ci = f32x4{0.f, 0.f, 0.f, 0.f};
+        p4_for<32>([&](auto X) __attribute__((always_inline)) {
+            constexpr int x = decltype(X)::value;
+            constexpr int jb = FIRST ? (x & 7) : (x >> 2), rb = FIRST ? 4 + (x >> 3) : 4 + (x & 3);
+            if constexpr (FIRST && jb == 0) ci = cinit(rb);
+            if constexpr (FIRST)
+                acc[rb][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[jb], ci, 0, 0, 0);
+            else
+                acc[rb][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[jb], acc[rb][jb], 0, 0, 0);
+            if constexpr (FIRST ? rb == 7 : (x & 3) == 3)
+                b[jb] = frag(sn, rowB + jb * 16 * 64 + offm);
+            else if constexpr ((x & 3) == 1 && (x >> 2) < 4)
+                a[x >> 2] = frag(sn, rowA + (x >> 2) * 16 * 64 + offm);
+            if constexpr (LAST && (x & 3) == 2)
+                check(std::integral_constant<int, 0>{}, std::integral_constant<int, jb>{}, cr0, crn, ti_c);
+            __builtin_amdgcn_sched_barrier(0);
+        });
+    };
+
+    auto do_stage = [&](auto first_tag, auto epi_tag, auto last_tag) __attribute__((always_inline)) {
+        const unsigned char *st = lds + cbuf * kP4Stage;
+        const int nbuf_next = cbuf + 1 == NBUF ? 0 : cbuf + 1;
+        phase0(st, first_tag, epi_tag);
+        if (L2 && si == 0 && live) issue_piece(8);
+        issue_advance();
+        const bool has_next = gc + 1 < issued;
+        p4_wait_vm<NPW>(issued - gc - 2, has_next);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        p4_barrier();
+        phase1(lds + nbuf_next * kP4Stage, first_tag, last_tag, cr1 - cr0);
+        ++gc;
+        cbuf = nbuf_next;
+    };
+
+    using T = std::integral_constant<bool, true>;
+    using F = std::integral_constant<bool, false>;
+    bool first_item = true;
+    while (true) {
+        if (first_item)
+            do_stage(T{}, F{}, F{});
+        else
+            do_stage(T{}, T{}, F{});
+        for (int s = 1; s + 1 < nst; ++s) do_stage(F{}, F{}, F{});
+        do_stage(F{}, F{}, T{});
+        pcr0 = cr0;
+        pcrn = cr1 - cr0;
+        pti = ti_c;
+        first_item = false;
+        ++items_done;
+        int cord;
+        ti_c = next_item(ti_c + tstride, cr0, cr1, cord);
+        if (ti_c < 0) break;
+    }
+    // row blocks 4..7 of the last item
+    p4_for<8>([&](auto X) __attribute__((always_inline)) {
+        check(std::integral_constant<int, 1>{}, std::integral_constant<int, decltype(X)::value>{}, pcr0, pcrn, pti);
+    });
+    if constexpr (PROBE) return;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    const int nqueue = qcnt < qcap ? qcnt : qcap;
+    for (int e = lane; e < nqueue; e += 64) {
+        const u32x4 en = __builtin_nontemporal_load(wq_base + e);
+        const uint32_t row = en[1];
+        emit_approx<METRIC, false>(p, (int)en[2], row, row, row_valid(p, row), __builtin_bit_cast(float, en[0]));
+    }
+}
+
 // queue entries per wave (16 B each): 4096 x 16 B x 4 waves x 256 CUs = 64 MiB
 constexpr int kP4QueueCap = 4096;
 
@@ -753,6 +1188,22 @@ void launch_ord_planes(const uint16_t *q_hi, uint16_t *q_ord, int *desc, const i
                        qlam, nq, vpad, (int)(dpad / kP4HiK), desc);
 }
 
+// the batch kernels' launch conditions (sets p.num_qblocks)
+static bool p4_ok(ScanParams &p) {
+    if (!p.p4_queue || p.row_list || p.chunk_ord || p.tiles < 1 || p.tile_rows != kP4Tile) return false;
+    p.num_qblocks = (p.nq + kP4Tile - 1) / kP4Tile;
+    int dev = 0, cus = 0;
+    MQVS_HIP(hipGetDevice(&dev));
+    MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    if (p.num_qblocks > cus / 8 || p.dpad % kP4HiK) return false;
+    if (p.row_begin % 16 || (p.tiles_per_chunk > 0 && p.chunk_rows % 16)) return false;
+    if (p.row_begin < 0 || p.row_end + p.chunk_rows + p.tile_rows > 0x7FFFFFFF || p.tiles > 0x3FFFFFFF ||
+        p.chunk_rows < 1)
+        return false;
+    if ((double)p.maxv * (double)p.q_vpad * (double)p.dpad * 2.0 >= 4294967296.0) return false;
+    return true;
+}
+
 // true when the launch was taken (batch APPEND, contiguous rows, identity
 // chunk ordinals, the queue workspace present)
 template <int METRIC>
@@ -812,27 +1263,44 @@ static bool launch_p4_t(ScanParams p, hipStream_t s) {
     return true;
 }
 
-// the batch probe (PROBE above): the same launch conditions; false when the
-// probe rows cannot take the batch kernel (the caller runs the dense probe)
+// the batch kernel actually launched: k_scan_p4 (32x32x16) or, with
+// kP4M16, k_scan_p4m (16x16x32)
+// 16x16x32 by default: main scan at nq 1000 -4.2 % (cosine) / -6.1 % (L2)
+// against k_scan_p4, bit-identical results (profiles/r04/m16_ab.jsonl)
+constexpr int kP4M16Default = 1;
 template <int METRIC>
-static bool launch_p4_probe_t(ScanParams p, hipStream_t s) {
-    if (!p.p4_queue || !p.p4_gmax || p.row_list || p.chunk_ord || p.tiles < 1 || p.tile_rows != kP4Tile) return false;
-    p.num_qblocks = (p.nq + kP4Tile - 1) / kP4Tile;
+static bool launch_p4_any(const ScanParams &p, hipStream_t s) {
+    if (tune_int("MQVS_P4_M16", kP4M16Default) == 0) return launch_p4_t<METRIC>(p, s);
+    ScanParams c = p;
+    if (!p4_ok(c)) return false;
+    if (METRIC == MQVS_METRIC_L2 && !c.row_norms) return false;
     int dev = 0, cus = 0;
     MQVS_HIP(hipGetDevice(&dev));
     MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const int per_xcd = cus / 8;
-    if (p.num_qblocks > per_xcd || p.dpad % kP4HiK) return false;
-    if (p.row_begin % 16 || (p.tiles_per_chunk > 0 && p.chunk_rows % 16)) return false;
-    if (p.row_begin < 0 || p.row_end + p.chunk_rows + p.tile_rows > 0x7FFFFFFF || p.tiles > 0x3FFFFFFF ||
-        p.chunk_rows < 1)
-        return false;
-    if ((double)p.maxv * (double)p.q_vpad * (double)p.dpad * 2.0 >= 4294967296.0) return false;
-    if (p.p4_gld < 2 * p.tiles) return false;
+    const int slots = per_xcd / c.num_qblocks * c.num_qblocks;
+    hipLaunchKernelGGL((k_scan_p4m<METRIC, 4>), dim3((unsigned)(8 * per_xcd)), dim3(256), 0, s, c, slots,
+                       reinterpret_cast<u32x4 *>(c.p4_queue), kP4QueueCap, tune_int("MQVS_P4_MAP", 1));
+    return true;
+}
+
+// the batch probe (PROBE above): the same launch conditions; false when the
+// probe rows cannot take the batch kernel (the caller runs the dense probe)
+template <int METRIC>
+static bool launch_p4_probe_t(ScanParams p, hipStream_t s) {
+    if (!p.p4_gmax || p.p4_gld < 2 * p.tiles || !p4_ok(p)) return false;
     if (METRIC == MQVS_METRIC_L2 && !p.row_norms) return false;
+    int dev = 0, cus = 0;
+    MQVS_HIP(hipGetDevice(&dev));
+    MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int per_xcd = cus / 8;
     const int slots = per_xcd / p.num_qblocks * p.num_qblocks;
-    hipLaunchKernelGGL((k_scan_p4<METRIC, 4, 0, 0, true>), dim3((unsigned)(8 * per_xcd)), dim3(256), 0, s, p, slots,
-                       reinterpret_cast<u32x4 *>(p.p4_queue), kP4QueueCap, 1);
+    const dim3 grid((unsigned)(8 * per_xcd));
+    auto *q = reinterpret_cast<u32x4 *>(p.p4_queue);
+    if (tune_int("MQVS_P4_M16", kP4M16Default))
+        hipLaunchKernelGGL((k_scan_p4m<METRIC, 4, true>), grid, dim3(256), 0, s, p, slots, q, kP4QueueCap, 1);
+    else
+        hipLaunchKernelGGL((k_scan_p4<METRIC, 4, 0, 0, true>), grid, dim3(256), 0, s, p, slots, q, kP4QueueCap, 1);
     return true;
 }
 
@@ -847,10 +1315,10 @@ bool launch_scan_p4_probe(const ScanParams &p, int metric, hipStream_t s) {
 
 bool launch_scan_p4(const ScanParams &p, int metric, hipStream_t s) {
     switch (metric) {
-        case MQVS_METRIC_L2: return launch_p4_t<MQVS_METRIC_L2>(p, s);
-        case MQVS_METRIC_IP: return launch_p4_t<MQVS_METRIC_IP>(p, s);
-        case MQVS_METRIC_COSINE: return launch_p4_t<MQVS_METRIC_COSINE>(p, s);
-        default: return launch_p4_t<kMetricIpRaw>(p, s);
+        case MQVS_METRIC_L2: return launch_p4_any<MQVS_METRIC_L2>(p, s);
+        case MQVS_METRIC_IP: return launch_p4_any<MQVS_METRIC_IP>(p, s);
+        case MQVS_METRIC_COSINE: return launch_p4_any<MQVS_METRIC_COSINE>(p, s);
+        default: return launch_p4_any<kMetricIpRaw>(p, s);
     }
 }
 

@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <condition_variable>
 #include <cstring>
 #include <map>
 #include <mutex>
@@ -38,6 +39,48 @@ size_t scratch_budget() { return g_scratch_budget.load(std::memory_order_relaxed
 void set_error(const std::string &msg) { g_error = msg; }
 
 
+// ---------------------------------------------------------------------------
+// Workspace HBM budget (mqvs_set_workspace_budget).  The reference admits up
+// to 2 x physical cores concurrent scans (MergeTreeVSManager.cpp:972-975,
+// ScanThreadLimiter.h:25-58), each of which here keeps a per-thread device
+// workspace (~1 GB at nq 1000).  A call is admitted with a reservation of
+// the workspace it is expected to grow to (its thread's last call, or the last
+// call of any thread); when that would take the sum of all workspaces and
+// reservations past the budget, idle workspaces (threads between calls) are
+// freed first, then the call waits until running calls finish and give their
+// memory back (a call that ends while others wait frees its workspace).
+// Growth beyond the reservation passes the same gate inside the call; only
+// if every running call is then waiting does it go over the budget (counted)
+// rather than deadlock.
+struct Workspace;
+struct WsGate {
+    std::mutex mu;
+    std::condition_variable cv;
+    size_t held = 0, peak = 0;  // device bytes of all workspaces
+    size_t reserved = 0;        // admitted calls' expected growth not yet allocated
+    size_t typical = 0;         // the last finished call's workspace (a new thread's estimate)
+    int active = 0;             // threads inside a call
+    int blocked = 0;            // of them, waiting for memory
+    int admitting = 0;          // threads waiting to start a call
+    int64_t waits = 0, trims = 0, over = 0;
+    std::vector<Workspace *> all;
+};
+static WsGate &gate() {
+    static WsGate *g = new WsGate();  // (leaked: workspaces of exited threads stay registered)
+    return *g;
+}
+static std::atomic<size_t> g_ws_budget{0};  // 0 = not set: a quarter of the device's memory, fixed at first use
+static size_t ws_budget() {
+    size_t b = g_ws_budget.load(std::memory_order_relaxed);
+    if (b) return b;
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess || tot == 0) tot = (size_t)64 << 30;
+    b = tot / 4;
+    size_t expect = 0;
+    g_ws_budget.compare_exchange_strong(expect, b);
+    return g_ws_budget.load(std::memory_order_relaxed);
+}
+
 struct Workspace {
     hipStream_t stream = nullptr;
     hipEvent_t ev[6] = {};
@@ -48,28 +91,196 @@ struct Workspace {
         recs, flags, p4q, qord;
     int *host_flags = nullptr;  // pinned
     bool pending_timing = false, pending_bf16 = false;  // search_collect_stats
-    void init() {
+    int device = 0;
+    std::mutex use;     // held by the owning thread during a call (WsCall); trimmers only try_lock it
+    hipStream_t last = nullptr;  // the stream of the current call (the caller's, or `stream`)
+    hipEvent_t done = nullptr;   // recorded on it at the end of every call: a trimmer waits for it
+    int depth = 0;      // the owner's nested calls
+    size_t held = 0;    // device bytes of the buffers (the gate's share of this workspace)
+    size_t resv = 0;    // the current call's reservation left
+    size_t call_peak = 0, recent = 0;  // most held during the current / the last call
+    void init(int dev) {
         if (stream) return;
+        device = dev;
         MQVS_HIP(hipStreamCreateWithFlags(&stream, hipStreamNonBlocking));
         for (auto &e : ev) MQVS_HIP(hipEventCreate(&e));
         for (auto &e : seg_ev) MQVS_HIP(hipEventCreate(&e));
+        MQVS_HIP(hipEventCreateWithFlags(&done, hipEventDisableTiming));
         MQVS_HIP(hipHostMalloc((void **)&host_flags, 64 * sizeof(int), hipHostMallocDefault));
+        WsGate &g = gate();
+        std::lock_guard<std::mutex> lk(g.mu);
+        g.all.push_back(this);
     }
-    void release() {
+    // the buffers, sticky word included (gate accounting is the caller's)
+    size_t free_buffers(bool keep_sticky) {
         DevBuf *all[] = {&queries, &qvars, &qnorms, &qmu,  &qlam,   &status,  &filter,   &exists, &ord,
                          &probe,   &tau,   &count,  &cand, &overflow, &out_ids, &out_dist, &misc,
                          &qhi, &bq, &thr, &cand2, &count2, &gcount, &goff, &glist, &large, &sticky, &surv,
                          &recs, &flags, &p4q, &qord};
-        for (auto *b : all) b->release();
+        size_t b = 0;
+        for (auto *x : all) {
+            if (keep_sticky && x == &sticky) continue;
+            b += x->cap;
+            x->release();
+        }
+        return b;
+    }
+    // free every buffer but the ASYNC sticky word, once the last call's work
+    // has drained -- on whichever stream it ran, the caller's included (an
+    // ASYNC call returns with its kernels in flight) -- (gate mutex held by
+    // the caller)
+    size_t trim() {
+        int cur = -1;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(device);
+        (void)hipEventSynchronize(done);
+        (void)hipStreamSynchronize(stream);
+        const size_t b = free_buffers(true);
+        held = sticky.cap;
+        if (cur >= 0) (void)hipSetDevice(cur);
+        return b;
+    }
+    void release() {
+        {
+            WsGate &g = gate();
+            std::lock_guard<std::mutex> lk(g.mu);
+            g.all.erase(std::remove(g.all.begin(), g.all.end(), this), g.all.end());
+            g.held -= std::min(g.held, held);
+            held = 0;
+        }
+        (void)free_buffers(false);
         if (host_flags) (void)hipHostFree(host_flags);
         host_flags = nullptr;
         for (auto &e : ev)
             if (e) (void)hipEventDestroy(e);
         for (auto &e : seg_ev)
             if (e) (void)hipEventDestroy(e);
+        if (done) (void)hipEventDestroy(done);
+        done = nullptr;
         if (stream) (void)hipStreamDestroy(stream);
         stream = nullptr;
     }
+    void *get(DevBuf &b, size_t bytes);
+};
+
+// gate mutex held: free idle workspaces of other threads until `need` more
+// bytes fit under the budget
+static void trim_idle(WsGate &g, Workspace *me, size_t need, size_t budget) {
+    for (Workspace *w : g.all) {
+        if (g.held + g.reserved + need <= budget) return;
+        if (w == me || w->held <= w->sticky.cap || !w->use.try_lock()) continue;
+        const size_t b = w->trim();
+        w->use.unlock();
+        g.held -= std::min(g.held, b);
+        ++g.trims;
+    }
+}
+
+void *Workspace::get(DevBuf &b, size_t bytes) {
+    if (bytes == 0) bytes = 16;
+    if (bytes <= b.cap) return b.p;
+    const size_t old = b.cap, delta = bytes - old;
+    {
+        WsGate &g = gate();
+        std::unique_lock<std::mutex> lk(g.mu);
+        // the admitted reservation first
+        const size_t take = std::min(delta, resv);
+        resv -= take;
+        g.reserved -= std::min(g.reserved, take);
+        const size_t rest = delta - take;
+        g.held += take;
+        held += take;
+        if (rest) {
+            const size_t B = ws_budget();
+            bool counted = false;
+            while (g.held + g.reserved + rest > B) {
+                trim_idle(g, this, rest, B);
+                if (g.held + g.reserved + rest <= B) break;
+                const int others = g.active - g.blocked - (depth > 0 ? 1 : 0);
+                if (others <= 0) {
+                    ++g.over;  // every running call waits: go over rather than deadlock
+                    break;
+                }
+                if (!counted) ++g.waits;
+                counted = true;
+                ++g.blocked;
+                g.cv.wait(lk);
+                --g.blocked;
+            }
+            g.held += rest;
+            held += rest;
+        }
+        call_peak = std::max(call_peak, held);
+        g.peak = std::max(g.peak, g.held);
+    }
+    try {
+        b.get(bytes);
+    } catch (...) {
+        // (the old buffer is gone too)
+        WsGate &g = gate();
+        std::lock_guard<std::mutex> lk(g.mu);
+        g.held -= std::min(g.held, bytes);
+        held -= std::min(held, bytes);
+        g.cv.notify_all();
+        throw;
+    }
+    return b.p;
+}
+
+// one call of the owning thread on its workspace (nests): counted as running;
+// at the end, if other calls wait for memory (or the gate is over budget), the
+// workspace is freed for them
+struct WsCall {
+    Workspace &ws;
+    explicit WsCall(Workspace &w) : ws(w) {
+        if (ws.depth++ != 0) return;
+        ws.use.lock();
+        WsGate &g = gate();
+        std::unique_lock<std::mutex> lk(g.mu);
+        // admission: reserve the expected workspace
+        const size_t B = ws_budget();
+        const size_t need = std::max(ws.recent ? ws.recent : g.typical, ws.held);
+        const size_t extra = need - ws.held;
+        bool counted = false;
+        while (g.held + g.reserved + extra > B) {
+            trim_idle(g, &ws, extra, B);
+            if (g.held + g.reserved + extra <= B || g.active == 0) break;  // (nobody to wait for)
+            if (!counted) ++g.waits;
+            counted = true;
+            ++g.admitting;
+            g.cv.wait(lk);
+            --g.admitting;
+        }
+        ++g.active;
+        ws.resv = extra;
+        g.reserved += extra;
+        ws.call_peak = ws.held;
+    }
+    ~WsCall() {
+        if (--ws.depth != 0) return;
+        (void)hipEventRecord(ws.done, ws.last ? ws.last : ws.stream);
+        ws.last = nullptr;
+        WsGate &g = gate();
+        {
+            std::lock_guard<std::mutex> lk(g.mu);
+            --g.active;
+            g.reserved -= std::min(g.reserved, ws.resv);
+            ws.resv = 0;
+            ws.recent = ws.call_peak;
+            g.typical = ws.call_peak;
+            const size_t B = g_ws_budget.load(std::memory_order_relaxed);
+            if ((g.blocked > 0 || g.admitting > 0 || (B && g.held > B)) && ws.held > ws.sticky.cap &&
+                hipEventQuery(ws.done) == hipSuccess) {
+                const size_t b = ws.trim();
+                g.held -= std::min(g.held, b);
+                ++g.trims;
+            }
+            g.cv.notify_all();
+        }
+        ws.use.unlock();
+    }
+    WsCall(const WsCall &) = delete;
+    WsCall &operator=(const WsCall &) = delete;
 };
 
 static thread_local std::map<int, Workspace> *g_ws = nullptr;
@@ -77,7 +288,7 @@ static thread_local std::map<int, Workspace> *g_ws = nullptr;
 static Workspace &workspace(int device) {
     if (!g_ws) g_ws = new std::map<int, Workspace>();  // leaked at exit on purpose
     Workspace &w = (*g_ws)[device];
-    w.init();
+    w.init(device);
     return w;
 }
 
@@ -242,14 +453,14 @@ static int prep_variants(Workspace &ws, const float *dq, int nq, int d, bool cos
                          bool may_sync, float *&qvars, float *&qnorms, int *&qmu, int *&qlam, int *&status,
                          hipStream_t s, int *zeroed_status = nullptr, int maxv_override = 0) {
     const int64_t qstride = round_up(d, 32);
-    qnorms = (float *)ws.qnorms.get(sizeof(float) * nq);
-    qmu = (int *)ws.qmu.get(sizeof(int) * nq);
-    qlam = (int *)ws.qlam.get(sizeof(int) * nq);
-    status = zeroed_status ? zeroed_status : (int *)ws.status.get(sizeof(int) * 4);
+    qnorms = (float *)ws.get(ws.qnorms, sizeof(float) * nq);
+    qmu = (int *)ws.get(ws.qmu, sizeof(int) * nq);
+    qlam = (int *)ws.get(ws.qlam, sizeof(int) * nq);
+    status = zeroed_status ? zeroed_status : (int *)ws.get(ws.status, sizeof(int) * 4);
     int maxv = cos ? (maxv_override > 0 ? maxv_override : kMaxVariants) : 1;
     for (int pass = 0; pass < 2; ++pass) {
         const size_t bytes = sizeof(float) * (size_t)nq * maxv * qstride;
-        qvars = (float *)ws.qvars.get(bytes);
+        qvars = (float *)ws.get(ws.qvars, bytes);
         MQVS_HIP(hipMemsetAsync(qvars, 0, bytes, s));
         if (pass > 0 || !zeroed_status) MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
         launch_query_prep(dq, nq, d, cos ? MQVS_METRIC_COSINE : MQVS_METRIC_L2, l2norms, qvars, maxv, qnorms, qmu,
@@ -286,7 +497,7 @@ static bool call_timing(uint32_t flags) {
 // mqvs_async_check reads and clears.
 static int *sticky_word(Workspace &ws, hipStream_t s) {
     if (!ws.sticky.p) {
-        ws.sticky.get(16);
+        ws.get(ws.sticky, 16);
         MQVS_HIP(hipMemsetAsync(ws.sticky.p, 0, 16, s));
     }
     return (int *)ws.sticky.p;
@@ -337,6 +548,7 @@ static int large_k_batch(int64_t n, int k) {
 // launch boundary plus a one-workgroup kernel; measured at 10M x 768, nq 1:
 // 7 segments 2.81 ms, 3 segments 2.72 ms; nq 1000 prefers 2, 2).
 // MQVS_SEG="first,growth,target" overrides (tools/ab_split.py).
+constexpr int64_t kMinSegRows = 65536;
 struct SegTune {
     int64_t first = 2, growth = 2, target = 16384;
 };
@@ -425,7 +637,9 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
 
     DeviceGuard guard(seg->device);
     Workspace &ws = workspace(seg->device);
+    WsCall ws_call(ws);
     hipStream_t s = user_stream ? (hipStream_t)user_stream : ws.stream;
+    ws.last = s;
     const bool dev = flags & MQVS_F_DEVICE_PTRS;
     const int64_t n = seg->n;
     const int d = seg->d;
@@ -439,16 +653,16 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     const float *dq = queries;
     const uint8_t *dfilter = filter, *dexists = exists;
     if (!dev) {
-        float *q = (float *)ws.queries.get(sizeof(float) * (size_t)nq * d);
+        float *q = (float *)ws.get(ws.queries, sizeof(float) * (size_t)nq * d);
         MQVS_HIP(hipMemcpyAsync(q, queries, sizeof(float) * (size_t)nq * d, hipMemcpyHostToDevice, s));
         dq = q;
         if (filter) {
-            auto *f = (uint8_t *)ws.filter.get(bm_bytes);
+            auto *f = (uint8_t *)ws.get(ws.filter, bm_bytes);
             MQVS_HIP(hipMemcpyAsync(f, filter, bm_bytes, hipMemcpyHostToDevice, s));
             dfilter = f;
         }
         if (exists) {
-            auto *f = (uint8_t *)ws.exists.get(bm_bytes);
+            auto *f = (uint8_t *)ws.get(ws.exists, bm_bytes);
             MQVS_HIP(hipMemcpyAsync(f, exists, bm_bytes, hipMemcpyHostToDevice, s));
             dexists = f;
         }
@@ -456,8 +670,8 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     int64_t *dids = out_ids;
     float *ddist = out_dist;
     if (!dev) {
-        dids = (int64_t *)ws.out_ids.get(sizeof(int64_t) * (size_t)nq * k);
-        ddist = (float *)ws.out_dist.get(sizeof(float) * (size_t)nq * k);
+        dids = (int64_t *)ws.get(ws.out_ids, sizeof(int64_t) * (size_t)nq * k);
+        ddist = (float *)ws.get(ws.out_dist, sizeof(float) * (size_t)nq * k);
     }
 
     // ---- selective PREWHERE: count the rows that pass (filter, non-empty,
@@ -470,8 +684,8 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     int64_t *goff = nullptr;
     if (dfilter && gather_mode != 0 && n > 0) {
         const int64_t nch = (n + seg->granule - 1) / seg->granule;
-        gcount = (int *)ws.gcount.get(sizeof(int) * nch);
-        goff = (int64_t *)ws.goff.get(sizeof(int64_t) * (nch + 2));
+        gcount = (int *)ws.get(ws.gcount, sizeof(int) * nch);
+        goff = (int64_t *)ws.get(ws.goff, sizeof(int64_t) * (nch + 2));
         launch_gather_count(dfilter, seg->nonempty_bits, dexists, n, seg->granule, kSmallRows, gcount, goff,
                             goff + nch, s);
         MQVS_HIP(hipGetLastError());
@@ -513,7 +727,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     float *qvars = nullptr, *qnorms = nullptr;
     int *qmu = nullptr, *qlam = nullptr, *status = nullptr;
     // one zeroed block for the status words: [overflow 4][status 4][count nq]
-    int *fl = (int *)ws.flags.get(sizeof(int) * (8 + (size_t)nq));
+    int *fl = (int *)ws.get(ws.flags, sizeof(int) * (8 + (size_t)nq));
     MQVS_HIP(hipMemsetAsync(fl, 0, sizeof(int) * (8 + (size_t)nq), s));
     // The query-variant table starts at kMaxVariants per query without a host
     // round trip; a chain that does not repeat within it on a part of more
@@ -527,7 +741,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     if (dfilter) {
         if (cos) {
             const int64_t nch = (n + seg->granule - 1) / seg->granule;
-            int *o = (int *)ws.ord.get(sizeof(int) * std::max<int64_t>(nch, 1));
+            int *o = (int *)ws.get(ws.ord, sizeof(int) * std::max<int64_t>(nch, 1));
             launch_chunk_ordinals(dfilter, seg->nonempty_bits, dexists, n, seg->granule, 1, o, s);
             MQVS_HIP(hipGetLastError());
             chunk_ord = o;
@@ -540,7 +754,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     const int32_t *row_list = nullptr;
     int64_t scan_n = n;  // scan positions: rows, or gather-list entries
     if (gather) {
-        int32_t *list = (int32_t *)ws.glist.get(sizeof(int32_t) * std::max<int64_t>(gpadded, 1));
+        int32_t *list = (int32_t *)ws.get(ws.glist, sizeof(int32_t) * std::max<int64_t>(gpadded, 1));
         launch_gather_list(dfilter, seg->nonempty_bits, dexists, n, seg->granule, kSmallRows, gcount, goff, list,
                            s);
         MQVS_HIP(hipGetLastError());
@@ -558,7 +772,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     // (more candidates = more appends from the scan; 16k keeps them cheap)
     const SegTune tune = seg_tune(nq);
     const int64_t target_cands = std::min<int64_t>(cap / 3, std::max<int64_t>(tune.target, 2 * (int64_t)k));
-    uint4 *large = k > kSortCap ? (uint4 *)ws.large.get(sizeof(uint4) * 2 * kLargeCap * (size_t)nq) : nullptr;
+    uint4 *large = k > kSortCap ? (uint4 *)ws.get(ws.large, sizeof(uint4) * 2 * kLargeCap * (size_t)nq) : nullptr;
     int64_t P = scan_n;
     // (small k over a part much larger than k -- e.g. the index build's
     // top-1 k-means assignment against 10^4 centroids -- also takes a short
@@ -595,9 +809,9 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     p.row_list = row_list;
     p.num_qblocks = (nq + kMfmaQ - 1) / kMfmaQ;
     p.blas_nq = fnq;
-    uint32_t *tau = (uint32_t *)ws.tau.get(sizeof(uint32_t) * nq);
+    uint32_t *tau = (uint32_t *)ws.get(ws.tau, sizeof(uint32_t) * nq);
     int *count = fl + 8;  // zeroed with the status words
-    Cand *cand = (Cand *)ws.cand.get(sizeof(Cand) * (size_t)nq * cap);
+    Cand *cand = (Cand *)ws.get(ws.cand, sizeof(Cand) * (size_t)nq * cap);
     int *overflow = fl;
     p.tau = tau;
     p.cand_count = count;
@@ -608,19 +822,19 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     if (kind == kScanBf16) {
         // bf16 plane of the query variants + per-query error bound
         const int64_t nvec = (int64_t)nq * maxv;
-        bq = (float *)ws.bq.get(sizeof(float) * nq);
+        bq = (float *)ws.get(ws.bq, sizeof(float) * nq);
         p.rows_hi = seg->rows_hi;
         p.dpad = seg->dpad;
-        p.thr = (const float *)ws.thr.get(sizeof(float) * nq);
+        p.thr = (const float *)ws.get(ws.thr, sizeof(float) * nq);
         p.split = seg->split;
         // batch scans (kernels_p4.hip): per-wave candidate queues
-        if (nq > 128) p.p4_queue = ws.p4q.get(p4_queue_bytes());
+        if (nq > 128) p.p4_queue = ws.get(ws.p4q, p4_queue_bytes());
         {
             // [hi: maxv x vpad x dpad x 2 B][records: nvec x kMxRec floats]
             const int64_t vpad = round_up(nq, 16);
             const int64_t pvec = (int64_t)maxv * vpad;
             const size_t o_rec = (size_t)round_up(pvec * seg->dpad * 2, 256);
-            auto *base = (unsigned char *)ws.qhi.get(o_rec + sizeof(float) * kMxRec * (size_t)nvec);
+            auto *base = (unsigned char *)ws.get(ws.qhi, o_rec + sizeof(float) * kMxRec * (size_t)nvec);
             auto *qhi = (uint16_t *)base;
             auto *qrec = (float *)(base + o_rec);
             launch_to_hi(qvars, nvec, d, qstride, seg->dpad, maxv, vpad, qhi, qrec, nullptr, s);
@@ -634,7 +848,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
             const int pcap = (int)std::min<int64_t>({kP4OrdPlanesMax, maxv, (int64_t)(scratch_budget() / plane)});
             if (p.p4_queue && metric == MQVS_METRIC_COSINE && maxv > 1 && pcap >= 2 && tune_int("MQVS_P4_ORD", 1)) {
                 const size_t pb = (size_t)round_up((int64_t)pcap * plane, 256);
-                auto *ob = (unsigned char *)ws.qord.get(pb + 256);
+                auto *ob = (unsigned char *)ws.get(ws.qord, pb + 256);
                 auto *desc = (int *)(ob + pb);
                 launch_ord_planes(qhi, (uint16_t *)ob, desc, qmu, qlam, nq, vpad, seg->dpad, pcap, s);
                 p.q_ord = (const uint16_t *)ob;
@@ -658,7 +872,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     int64_t probe_cols = P, probe_ld = P;
     if (kind == kScanBf16 && p.p4_queue && !row_list && P < scan_n && pr.tiles > 0) {
         const int64_t gld = round_up(2 * pr.tiles, 4);
-        probe = (float *)ws.probe.get(sizeof(float) * (size_t)nq * gld);
+        probe = (float *)ws.get(ws.probe, sizeof(float) * (size_t)nq * gld);
         ScanParams pp = p;
         pp.row_begin = pr.begin;
         pp.row_end = pr.end;
@@ -675,7 +889,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         }
     }
     if (!bprobe) {
-        probe = (float *)ws.probe.get(sizeof(float) * (size_t)nq * P);
+        probe = (float *)ws.get(ws.probe, sizeof(float) * (size_t)nq * P);
         p.probe = probe;
         p.probe_ld = P;
         run_scan(p, pr, kind, metric, true, s);
@@ -694,11 +908,15 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     // probe's threshold is loose, e.g. clustered data)
     {
         const int64_t align = aligned ? seg->granule : tile_rows;
-        Cand *alt = (Cand *)ws.cand2.get(sizeof(Cand) * (size_t)nq * cap);
-        int *calt = (int *)ws.count2.get(sizeof(int) * nq);
+        Cand *alt = (Cand *)ws.get(ws.cand2, sizeof(Cand) * (size_t)nq * cap);
+        int *calt = (int *)ws.get(ws.count2, sizeof(int) * nq);
         // (the batch probe appended nothing: the first segment also covers
         // the probe rows)
-        int64_t b = bprobe ? 0 : P, seg_rows = std::max<int64_t>(tune.first * P, align);
+        // (a segment of fewer than kMinSegRows rows cannot fill the chip --
+        // 256 tiles -- and costs a launch and a refinement: small-k searches
+        // over mid-size parts, e.g. the index's coarse step, 39063 centroids
+        // at k = nprobe, used to run 7 segments of 2..64 tiles)
+        int64_t b = bprobe ? 0 : P, seg_rows = std::max<int64_t>({tune.first * P, align, kMinSegRows});
         int segs = 0;
         while (b < scan_n) {
             const int64_t e = std::min(scan_n, round_up(b + seg_rows + (segs == 0 && bprobe ? P : 0), align));
@@ -727,9 +945,9 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         // the global-scratch sort for k > kSortCap)
         const int lcap = large ? kLargeCap : kSortCap;
         const int64_t rs = large ? 2 * (int64_t)kLargeCap : kSortCap;
-        auto *surv = (uint32_t *)ws.surv.get(sizeof(uint32_t) * (size_t)nq * rs + sizeof(int) * nq);
+        auto *surv = (uint32_t *)ws.get(ws.surv, sizeof(uint32_t) * (size_t)nq * rs + sizeof(int) * nq);
         int *scnt = (int *)(surv + (size_t)nq * rs);
-        uint4 *recs = large ? large : (uint4 *)ws.recs.get(sizeof(uint4) * (size_t)nq * rs);
+        uint4 *recs = large ? large : (uint4 *)ws.get(ws.recs, sizeof(uint4) * (size_t)nq * rs);
         launch_rerank_select(p, metric, bq, k, seg->row_offset, dids, ddist, overflow, surv, scnt, recs, lcap, rs,
                              s);
     } else
@@ -828,6 +1046,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
 // caller has synchronised its stream
 void search_collect_stats(int device) {
     Workspace &ws = workspace(device);
+    WsCall ws_call(ws);
     if (ws.pending_bf16) {
         g_stats.survivors_max = ws.host_flags[17];
         g_stats.survivors_total = (uint32_t)ws.host_flags[18];
@@ -897,7 +1116,9 @@ static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const i
 
     DeviceGuard guard(seg->device);
     Workspace &ws = workspace(seg->device);
+    WsCall ws_call(ws);
     hipStream_t s = user_stream ? (hipStream_t)user_stream : ws.stream;
+    ws.last = s;
     const bool dev = flags & MQVS_F_DEVICE_PTRS;
     const int d = seg->d;
     const float *dq = queries;
@@ -906,21 +1127,21 @@ static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const i
     int64_t *dids = out_ids;
     float *ddist = out_dist;
     if (!dev) {
-        float *q = (float *)ws.queries.get(sizeof(float) * (size_t)nq * d);
+        float *q = (float *)ws.get(ws.queries, sizeof(float) * (size_t)nq * d);
         MQVS_HIP(hipMemcpyAsync(q, queries, sizeof(float) * (size_t)nq * d, hipMemcpyHostToDevice, s));
         dq = q;
-        int64_t *c = (int64_t *)ws.misc.get(sizeof(int64_t) * std::max<size_t>((size_t)nq * ncand, 1));
+        int64_t *c = (int64_t *)ws.get(ws.misc, sizeof(int64_t) * std::max<size_t>((size_t)nq * ncand, 1));
         if (ncand > 0)
             MQVS_HIP(hipMemcpyAsync(c, cand, sizeof(int64_t) * (size_t)nq * ncand, hipMemcpyHostToDevice, s));
         dc = c;
         if (exists) {
             const int64_t bm = (seg->n + 7) / 8;
-            auto *f = (uint8_t *)ws.exists.get(bm);
+            auto *f = (uint8_t *)ws.get(ws.exists, bm);
             MQVS_HIP(hipMemcpyAsync(f, exists, bm, hipMemcpyHostToDevice, s));
             dexists = f;
         }
-        dids = (int64_t *)ws.out_ids.get(sizeof(int64_t) * (size_t)nq * k);
-        ddist = (float *)ws.out_dist.get(sizeof(float) * (size_t)nq * k);
+        dids = (int64_t *)ws.get(ws.out_ids, sizeof(int64_t) * (size_t)nq * k);
+        ddist = (float *)ws.get(ws.out_dist, sizeof(float) * (size_t)nq * k);
     }
     const bool blas = fnq >= kBlasThreshold;
     const int64_t ords = seg->row_offset / seg->granule + (seg->n + seg->granule - 1) / seg->granule;
@@ -946,7 +1167,7 @@ static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const i
     p.ord_base = (int)(seg->row_offset / seg->granule);
     p.exists = dexists;
     p.nonempty = seg->nonempty_bits;
-    uint4 *scratch = large ? (uint4 *)ws.large.get(sizeof(uint4) * 2 * (size_t)ncand * nq) : nullptr;
+    uint4 *scratch = large ? (uint4 *)ws.get(ws.large, sizeof(uint4) * 2 * (size_t)ncand * nq) : nullptr;
     launch_rerank_ids(p, metric, dc, ncand, k, seg->row_offset, dids, ddist, scratch, s);
     MQVS_HIP(hipGetLastError());
     if (dev && (flags & MQVS_F_ASYNC)) {
@@ -1043,24 +1264,26 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
 
     DeviceGuard guard(seg->device);
     Workspace &ws = workspace(seg->device);
+    WsCall ws_call(ws);
     hipStream_t s = user_stream ? (hipStream_t)user_stream : ws.stream;
+    ws.last = s;
     const bool dev = flags & MQVS_F_DEVICE_PTRS;
     const int64_t n = seg->n;
     const int64_t bm_bytes = (n + 7) / 8;
     const bool timing = call_timing(flags);
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[0], s));
 
-    uint32_t *qc = (uint32_t *)ws.queries.get((size_t)nq * seg->code_words * 4);
+    uint32_t *qc = (uint32_t *)ws.get(ws.queries, (size_t)nq * seg->code_words * 4);
     upload_codes(qc, seg->code_words, queries, seg->code_bytes, nq, dev, s);
     const uint8_t *dfilter = filter, *dexists = exists;
     if (!dev) {
         if (filter) {
-            auto *f = (uint8_t *)ws.filter.get(bm_bytes);
+            auto *f = (uint8_t *)ws.get(ws.filter, bm_bytes);
             MQVS_HIP(hipMemcpyAsync(f, filter, bm_bytes, hipMemcpyHostToDevice, s));
             dfilter = f;
         }
         if (exists) {
-            auto *f = (uint8_t *)ws.exists.get(bm_bytes);
+            auto *f = (uint8_t *)ws.get(ws.exists, bm_bytes);
             MQVS_HIP(hipMemcpyAsync(f, exists, bm_bytes, hipMemcpyHostToDevice, s));
             dexists = f;
         }
@@ -1068,8 +1291,8 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
     int64_t *dids = out_ids;
     float *ddist = out_dist;
     if (!dev) {
-        dids = (int64_t *)ws.out_ids.get(sizeof(int64_t) * (size_t)nq * k);
-        ddist = (float *)ws.out_dist.get(sizeof(float) * (size_t)nq * k);
+        dids = (int64_t *)ws.get(ws.out_ids, sizeof(int64_t) * (size_t)nq * k);
+        ddist = (float *)ws.get(ws.out_dist, sizeof(float) * (size_t)nq * k);
     }
 
     // candidate capacity and probe size as the float path (mqvs.hip search_impl)
@@ -1077,7 +1300,7 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
     int cap = (int)std::min<int64_t>(kCandMax, kCandBudget / std::max(nq, 1));
     cap = std::max(cap, k > kSortCap ? large_k_cap(k) : kSortCap) / 256 * 256;
     const int64_t target_cands = std::min<int64_t>(cap / 3, std::max<int64_t>(16384, 2 * (int64_t)k));
-    uint4 *large = k > kSortCap ? (uint4 *)ws.large.get(sizeof(uint4) * 2 * kLargeCap * (size_t)nq) : nullptr;
+    uint4 *large = k > kSortCap ? (uint4 *)ws.get(ws.large, sizeof(uint4) * 2 * kLargeCap * (size_t)nq) : nullptr;
     int64_t P = n;
     if (n > 32768) {
         P = (int64_t)(((double)k * (double)n) / target_cands) + 1;
@@ -1099,15 +1322,15 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
     p.qcodes = qc;
     p.code_words = seg->code_words;
     p.nbits = seg->d;
-    uint32_t *tau = (uint32_t *)ws.tau.get(sizeof(uint32_t) * nq);
-    int *count = (int *)ws.count.get(sizeof(int) * nq);
-    Cand *cand = (Cand *)ws.cand.get(sizeof(Cand) * (size_t)nq * cap);
-    int *overflow = (int *)ws.overflow.get(sizeof(int) * 4);
+    uint32_t *tau = (uint32_t *)ws.get(ws.tau, sizeof(uint32_t) * nq);
+    int *count = (int *)ws.get(ws.count, sizeof(int) * nq);
+    Cand *cand = (Cand *)ws.get(ws.cand, sizeof(Cand) * (size_t)nq * cap);
+    int *overflow = (int *)ws.get(ws.overflow, sizeof(int) * 4);
     p.tau = tau;
     p.cand_count = count;
     p.cand = cand;
     p.cand_cap = cap;
-    p.probe = (float *)ws.probe.get(sizeof(float) * (size_t)nq * std::max<int64_t>(P, 1));
+    p.probe = (float *)ws.get(ws.probe, sizeof(float) * (size_t)nq * std::max<int64_t>(P, 1));
     p.probe_ld = P;
     auto scan = [&](int64_t b, int64_t e, bool probe, bool strict) {
         const Range r = make_range(b, e, tile_rows, seg->granule, false);
@@ -1130,8 +1353,8 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
     MQVS_HIP(hipGetLastError());
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[2], s));
     {
-        Cand *alt = (Cand *)ws.cand2.get(sizeof(Cand) * (size_t)nq * cap);
-        int *calt = (int *)ws.count2.get(sizeof(int) * nq);
+        Cand *alt = (Cand *)ws.get(ws.cand2, sizeof(Cand) * (size_t)nq * cap);
+        int *calt = (int *)ws.get(ws.count2, sizeof(int) * nq);
         // segments grow x4: each refine costs a launch, and appends per
         // segment stay near (growth x k) with the threshold refined
         int64_t b = P, seg_rows = std::max<int64_t>(2 * P, tile_rows);
@@ -1272,6 +1495,7 @@ static mqvs_segment *ingest_column(const uint8_t *data_bin, int64_t data_bytes, 
     mqvs_segment *seg = new_segment(n, d, metric, granule, row_offset);
     try {
         Workspace &ws = workspace(seg->device);
+        WsCall ws_call(ws);
         hipStream_t s = ws.stream;
         IngestTmp tmp;
         const uint8_t *dd = data_bin, *ds = sizes_bin;
@@ -1414,6 +1638,7 @@ int mqvs_thread_release(void) {
         if (!g_ws) return;
         for (auto &kv : *g_ws) {
             (void)hipSetDevice(kv.first);
+            std::lock_guard<std::mutex> lk(kv.second.use);
             kv.second.release();
         }
         g_ws->clear();
@@ -1433,12 +1658,13 @@ int mqvs_segment_create(const float *host_rows, int64_t n, int32_t d, int32_t me
         mqvs_segment *s = new_segment(n, d, metric, granule_rows, row_offset);
         try {
             Workspace &ws = workspace(s->device);
+            WsCall ws_call(ws);
             if (n > 0)
                 MQVS_HIP(hipMemcpyAsync(s->rows, host_rows, sizeof(float) * (size_t)n * d,
                                         hipMemcpyHostToDevice, ws.stream));
             const uint8_t *dne = nullptr;
             if (nonempty && n > 0 && !all_nonempty(nonempty, n)) {
-                auto *b = (uint8_t *)ws.misc.get((size_t)n);
+                auto *b = (uint8_t *)ws.get(ws.misc, (size_t)n);
                 MQVS_HIP(hipMemcpyAsync(b, nonempty, (size_t)n, hipMemcpyHostToDevice, ws.stream));
                 dne = b;
             }
@@ -1462,6 +1688,7 @@ int mqvs_segment_create_device(const float *dev_rows, int64_t n, int32_t d, int3
         mqvs_segment *s = new_segment(n, d, metric, granule_rows, row_offset);
         try {
             Workspace &ws = workspace(s->device);
+            WsCall ws_call(ws);
             if (n > 0)
                 MQVS_HIP(hipMemcpyAsync(s->rows, dev_rows, sizeof(float) * (size_t)n * d,
                                         hipMemcpyDeviceToDevice, ws.stream));
@@ -1484,6 +1711,7 @@ int mqvs_segment_generate(uint64_t seed, int32_t mode, int64_t n, int32_t d, int
         mqvs_segment *s = new_segment(n, d, metric, granule_rows, row_offset);
         try {
             Workspace &ws = workspace(s->device);
+            WsCall ws_call(ws);
             launch_generate(seed, mode, row_offset, n, d, s->rows, ws.stream);
             MQVS_HIP(hipGetLastError());
             prepare_segment(s, nullptr, ws.stream);
@@ -1614,6 +1842,7 @@ int mqvs_knn_raw(const float *x, const float *y, int64_t d, int64_t k, int64_t n
         mqvs_segment *s = new_segment(ny, (int)d, metric, ny, 0);
         try {
             Workspace &ws = workspace(s->device);
+            WsCall ws_call(ws);
             MQVS_HIP(hipMemcpyAsync(s->rows, y, sizeof(float) * (size_t)ny * d, hipMemcpyHostToDevice,
                                     ws.stream));
             prepare_segment(s, nullptr, ws.stream);
@@ -1647,6 +1876,7 @@ int mqvs_segment_create_binary(const uint8_t *codes, int64_t n, int32_t dim_bits
         try {
             if (n > 0 && !codes) fail(MQVS_ERR_BAD_ARGUMENTS, "null codes");
             Workspace &ws = workspace(s->device);
+            WsCall ws_call(ws);
             upload_codes(s->codes, s->code_words, codes, s->code_bytes, n, (flags & MQVS_F_DEVICE_PTRS) != 0,
                          ws.stream);
             MQVS_HIP(hipStreamSynchronize(ws.stream));
@@ -1689,12 +1919,13 @@ int mqvs_knn_binary_raw(const uint8_t *x, const uint8_t *y, int64_t d, int64_t k
         mqvs_segment *s = new_binary_segment(ny, (int32_t)d, metric, ny, 0);
         try {
             Workspace &ws = workspace(s->device);
+            WsCall ws_call(ws);
             upload_codes(s->codes, s->code_words, y, s->code_bytes, ny, false, ws.stream);
             const size_t m = (size_t)nx * k;
-            auto *b = (char *)ws.misc.get(m * 12 + 16);
+            auto *b = (char *)ws.get(ws.misc, m * 12 + 16);
             auto *di = (int64_t *)b;
             auto *dd = (float *)(b + m * 8);
-            auto *qd = (uint8_t *)ws.glist.get((size_t)nx * (d / 8));
+            auto *qd = (uint8_t *)ws.get(ws.glist, (size_t)nx * (d / 8));
             MQVS_HIP(hipMemcpyAsync(qd, x, (size_t)nx * (d / 8), hipMemcpyHostToDevice, ws.stream));
             search_binary_impl(s, qd, (int)nx, (int)k, metric, nullptr, nullptr, di, dd, MQVS_F_DEVICE_PTRS,
                                nullptr);
@@ -1721,7 +1952,9 @@ int mqvs_merge_shards(int32_t nshards, int32_t nq, int32_t k, int32_t metric, co
         int dev = 0;
         MQVS_HIP(hipGetDevice(&dev));
         Workspace &ws = workspace(dev);
+        WsCall ws_call(ws);
         hipStream_t s = stream ? (hipStream_t)stream : ws.stream;
+        ws.last = s;
         const size_t nin = (size_t)nshards * nq * k, nout = (size_t)nq * k;
         const int64_t *di = in_ids;
         const float *dd = in_dist;
@@ -1729,7 +1962,7 @@ int mqvs_merge_shards(int32_t nshards, int32_t nq, int32_t k, int32_t metric, co
         float *od = out_dist;
         const bool devp = flags & MQVS_F_DEVICE_PTRS;
         if (!devp) {
-            auto *b = (char *)ws.misc.get(nin * 12 + nout * 12 + 64);
+            auto *b = (char *)ws.get(ws.misc, nin * 12 + nout * 12 + 64);
             auto *bi = (int64_t *)b;
             auto *bd = (float *)(b + nin * 8);
             oi = (int64_t *)(b + nin * 12 + 16 - (nin * 12) % 16);
@@ -1742,7 +1975,7 @@ int mqvs_merge_shards(int32_t nshards, int32_t nq, int32_t k, int32_t metric, co
         // binary distances (Hamming, Jaccard) are ascending finite values: the L2 order
         const int order = (metric == MQVS_METRIC_HAMMING || metric == MQVS_METRIC_JACCARD) ? MQVS_METRIC_L2 : metric;
         uint4 *scratch = (int64_t)nshards * k > kSortCap
-                             ? (uint4 *)ws.large.get(sizeof(uint4) * 2 * (size_t)nshards * k * nq)
+                             ? (uint4 *)ws.get(ws.large, sizeof(uint4) * 2 * (size_t)nshards * k * nq)
                              : nullptr;
         launch_merge_shards(nshards, nq, k, order, di, dd, oi, od, (flags & MQVS_F_PART_MERGE) != 0, scratch, s);
         MQVS_HIP(hipGetLastError());
@@ -1761,7 +1994,9 @@ int mqvs_generate_device(uint64_t seed, int32_t mode, int64_t row0, int64_t n, i
         int dev = 0;
         MQVS_HIP(hipGetDevice(&dev));
         Workspace &ws = workspace(dev);
+        WsCall ws_call(ws);
         hipStream_t s = stream ? (hipStream_t)stream : ws.stream;
+        ws.last = s;
         launch_generate(seed, mode, row0, n, d, dev_out, s);
         MQVS_HIP(hipGetLastError());
         MQVS_HIP(hipStreamSynchronize(s));
@@ -1810,6 +2045,38 @@ int mqvs_measure_read_bandwidth(size_t bytes, int32_t reps, double *gbs, double 
     });
 }
 
+size_t mqvs_set_workspace_budget(size_t bytes) {
+    const size_t prev = ws_budget();
+    if (bytes) {
+        g_ws_budget.store(bytes, std::memory_order_relaxed);
+        WsGate &g = gate();
+        std::lock_guard<std::mutex> lk(g.mu);
+        g.cv.notify_all();
+    }
+    return prev;
+}
+
+int mqvs_workspace_stats(mqvs_workspace_stats_t *out, int32_t reset_peak) {
+    return guarded([&] {
+        if (!out) fail(MQVS_ERR_BAD_ARGUMENTS, "null stats");
+        const size_t b = ws_budget();
+        WsGate &g = gate();
+        std::lock_guard<std::mutex> lk(g.mu);
+        out->budget = b;
+        out->held = g.held;
+        out->peak = g.peak;
+        out->waits = g.waits;
+        out->trims = g.trims;
+        out->over_budget = g.over;
+        out->active = g.active;
+        out->workspaces = (int32_t)g.all.size();
+        if (reset_peak) {
+            g.peak = g.held;
+            g.waits = g.trims = g.over = 0;
+        }
+    });
+}
+
 size_t mqvs_set_scratch_budget(size_t bytes) {
     if (bytes == 0) return g_scratch_budget.load();
     return g_scratch_budget.exchange(std::max<size_t>(bytes, (size_t)1 << 20));
@@ -1831,7 +2098,9 @@ int mqvs_async_check(mqvs_stream_t stream) {
         int dev = 0;
         MQVS_HIP(hipGetDevice(&dev));
         Workspace &ws = workspace(dev);
+        WsCall ws_call(ws);
         hipStream_t s = stream ? (hipStream_t)stream : ws.stream;
+        ws.last = s;
         MQVS_HIP(hipStreamSynchronize(s));
         if (!ws.sticky.p) return;
         int word = 0;

@@ -67,3 +67,52 @@ def test_concurrent_searches_match_sequential(mq):
         assert np.array_equal(dg.view(np.uint32), de.view(np.uint32)), j
     for s in segs.values():
         s.free()
+
+
+def test_workspace_budget_bounds_concurrent_batches(mq):
+    """64 threads each run nq 1000 batches on a 1M-row
+    part under a 3 GiB workspace cap (each batch's workspace is ~0.7 GB, so
+    at most a few fit at once): growths wait for running searches to give
+    their workspace back, the cap is never passed, and every result equals
+    the sequential one bit for bit."""
+    from myscaledb_amd import _lib
+    n, d, gran, k = 1_000_000, 128, 8192, 100
+    seg = mq.VectorScanSegment.generate(0x5EED0101, 1, n, d, "Cosine", gran)
+    qs = [O.generate(0x5EED0202 + i, 1, 0, 1000, d) for i in range(4)]
+    expected = [seg.search(q, k) for q in qs]
+    _lib.check(_lib.lib.mqvs_thread_release())  # (this thread's workspace out of the way)
+    cap = 3 << 30
+    prev = _lib.set_workspace_budget(cap)
+    _lib.workspace_stats(reset_peak=True)
+    results, errors = {}, []
+
+    def worker(tid):
+        try:
+            mq.init(0)
+            for rep in range(2):
+                j = (tid + rep) % len(qs)
+                results[(tid, rep)] = (j, seg.search(qs[j], k))
+            _lib.check(_lib.lib.mqvs_thread_release())
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    try:
+        threads = [threading.Thread(target=worker, args=(t,)) for t in range(64)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout=300)
+            assert not t.is_alive(), "a search thread did not finish"
+        st = _lib.workspace_stats()
+    finally:
+        _lib.set_workspace_budget(prev)
+        seg.free()
+    assert not errors, errors[:3]
+    assert len(results) == 128
+    for (tid, rep), (j, (ig, dg)) in results.items():
+        ie, de = expected[j]
+        assert np.array_equal(ig, ie), (tid, rep)
+        assert np.array_equal(dg.view(np.uint32), de.view(np.uint32)), (tid, rep)
+    assert st["over_budget"] == 0, st
+    assert st["peak"] <= cap, st
+    assert st["waits"] > 0, st  # (the cap did bind)
