@@ -406,9 +406,9 @@ def roofline(st, main_ms, nq, d, args):
             qt = 256 if nq > 128 else 128
             stream = 2.0 * rows * dp * -(-nq // qt) + 2.0 * nq * dp * -(-rows // 256)
             if st.get("batch_kernel"):
-                want = "k_scan_p4"
-                kern = ("k_scan_p4<metric,NBUF=4> (one wave per SIMD, 128x128 rows x queries per wave, 256 AGPR "
-                        "accumulators, bf16 32x32x16, LDS-DMA ring)")
+                want = "k_scan_p4m"
+                kern = ("k_scan_p4m<metric,NBUF=4> (one wave per SIMD, 128x128 rows x queries per wave as 8x8 blocks "
+                        "of bf16 16x16x32, 256 AGPR accumulators, LDS-DMA ring)")
             else:
                 want = "k_scan_hi<"
                 kern = "k_scan_hi<metric,APPEND,WQ=2,QB=4,NBUF=4> (bf16 32x32x16)"

@@ -85,7 +85,7 @@ struct ListBufs {
 struct IndexWorkspace {
     hipEvent_t ev[6] = {};
     DevBuf queries, qvars, qnorms, qmu, qlam, status, qhi, probes, cprobes, filter, exists, rows, out_ids, out_dist,
-        ord, dmap, dwords, pdist;
+        ord, dmap, dwords, pdist, cqhi, gmax;
     ListBufs coarse, fine;
     void init() {
         if (ev[0]) return;
@@ -620,7 +620,53 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     // 65536 lists, nq 1000: 1.26 -> 0.67 ms; few lists: the list pass over
     // the centroid chunks (10000 lists: 0.28 ms vs 0.50, the FLAT path's
     // fixed stages dominate; profiles/r03/index)
-    if (tune_int("MQVS_IVF_COARSE", ix->nlist > kCoarseFlatLists ? 1 : 0) == 1) {
+    // Default (nprobe <= 62 and the centroid plane present): the batch kernel
+    // scores every (query, centroid) on bf16 and keeps the best of each
+    // 16-centroid group; the nprobe + 2 best groups per query then get exact
+    // fp32 values and the nprobe best of those are the probes
+    // (k_coarse_pick).  65536 or 39063 lists at nq 1000: one batch-kernel
+    // launch and one pick instead of mqvs_search's whole pipeline.
+    bool picked = false;
+    const int cmode = tune_int("MQVS_IVF_COARSE", 2);
+    if (cmode == 2 && nprobe + 2 <= kCoarsePickMaxT && ix->cent && ix->cent->rows_hi && ix->cent->rows) {
+        mqvs_segment *cs = ix->cent;
+        const int64_t vpad = rup(nq, 16);
+        auto *cq = (uint16_t *)ws.cqhi.get(sizeof(uint16_t) * (size_t)vpad * cs->dpad);
+        // (variant 0 of every query: the raw query, or the normalised one for
+        // cosine -- centroids of cosine parts are normalised: same ranking as
+        // the raw inner product)
+        launch_to_hi(qvars, nq, d, (int64_t)maxv * qstride, cs->dpad, 1, vpad, cq, nullptr, nullptr, s);
+        MQVS_HIP(hipGetLastError());
+        ScanParams cp{};
+        cp.rows_hi = cs->rows_hi;
+        cp.row_norms = cs->norms;
+        cp.n = cs->n;
+        cp.d = d;
+        cp.dpad = cs->dpad;
+        cp.nq = nq;
+        cp.q_hi = cq;
+        cp.q_vpad = vpad;
+        cp.maxv = 1;
+        cp.qnorms = qnorms;
+        cp.chunk_rows = cs->granule;
+        cp.row_begin = 0;
+        cp.row_end = cs->n;
+        cp.tile_rows = 256;
+        cp.tiles = (cs->n + 255) / 256;
+        cp.tiles_per_chunk = 0;
+        const int64_t gld = rup(16 * cp.tiles, 4);
+        cp.p4_gmax = (float *)ws.gmax.get(sizeof(float) * (size_t)nq * gld);
+        cp.p4_gld = gld;
+        if (launch_scan_p4_groups(cp, ix->coarse_metric, s)) {
+            MQVS_HIP(hipGetLastError());
+            launch_coarse_pick(cp.p4_gmax, gld, 16 * cp.tiles, nprobe + 2, nprobe, ix->coarse_metric, qvars,
+                               (int64_t)maxv * qstride, cs->rows, cs->norms, cs->n, d, nq, probes, s);
+            MQVS_HIP(hipGetLastError());
+            picked = true;
+        }
+    }
+    if (picked) {
+    } else if (tune_int("MQVS_IVF_COARSE", ix->nlist > kCoarseFlatLists ? 1 : 0) == 1) {
         float *pd = (float *)ws.pdist.get(sizeof(float) * (size_t)nq * nprobe);
         search_internal(ix->cent, dq, nq, nprobe, ix->coarse_metric, nullptr, nullptr, probes, pd,
                         MQVS_F_DEVICE_PTRS | (flags & MQVS_F_ASYNC), s);

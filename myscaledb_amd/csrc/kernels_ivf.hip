@@ -869,4 +869,85 @@ void launch_centroid_mean(const float *rows, int d, const int32_t *order, const 
     if (nlist > 0) hipLaunchKernelGGL(k_centroid_mean, dim3(nlist), dim3(256), 0, s, rows, d, order, off, cent);
 }
 
+// ---------------------------------------------------------------------------
+// The coarse step's pick (index.hip): per query, from the batch probe's best
+// approximate value of every 16-centroid group (kernels_p4.hip, GRP 16), the
+// T best groups -- every centroid among the query's T best lies in one of
+// them (a group outside holds nothing better than the T-th group maximum) --
+// then the exact fp32 value of each centroid of those groups and the nprobe
+// best.  One workgroup per query; T <= kCoarsePickMaxT.
+
+template <int METRIC>  // MQVS_METRIC_L2 or kMetricIpRaw (the coarse metric)
+__global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T,
+                                                             int nprobe, const float *q, int64_t qld,
+                                                             const float *cent, const float *cnorm, int64_t ncent,
+                                                             int d, int64_t *probes) {
+    __shared__ uint32_t hist[256];
+    __shared__ uint32_t sh[4];
+    __shared__ int s_grp[kCoarsePickMaxT];
+    __shared__ int s_ng;
+    __shared__ uint4 recs[16 * kCoarsePickMaxT];
+    const int qi = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const float *row = gmax + (int64_t)qi * gld;
+    auto keyof = [&](int64_t i) { return okey<METRIC>(row[i]); };
+    const uint32_t th = block_radix_select(keyof, ngroups, T, hist, sh);
+    if (t == 0) s_ng = 0;
+    __syncthreads();
+    // the groups strictly better than the T-th, then its ties up to T
+    for (int pass = 0; pass < 2; ++pass) {
+        for (int64_t i = t; i < ngroups; i += SEL_THREADS) {
+            const uint32_t k = keyof(i);
+            if (k == 0xFFFFFFFFu) continue;
+            const bool take = th == 0xFFFFFFFEu ? pass == 0 : (pass == 0 ? k < th : k == th);
+            if (!take) continue;
+            const int slot = atomicAdd(&s_ng, 1);
+            if (slot < T) s_grp[slot] = (int)i;
+        }
+        __syncthreads();
+    }
+    const int ng = min(s_ng, T);
+    // exact values of the groups' centroids: one wave per centroid at a time,
+    // lanes over the columns
+    const float *qv = q + (int64_t)qi * qld;
+    const int M = 16 * ng;
+    for (int c = wv; c < M; c += SEL_THREADS / 64) {
+        const int64_t r = (int64_t)s_grp[c >> 4] * 16 + (c & 15);
+        float dot = 0.f;
+        if (r < ncent) {
+            const float *y = cent + r * d;
+            for (int e = lane; e < d; e += 64) dot = fmaf(qv[e], y[e], dot);
+        }
+        for (int off = 32; off > 0; off >>= 1) dot += __shfl_xor(dot, off);
+        if (lane == 0) {
+            uint32_t key = 0xFFFFFFFFu;
+            if (r < ncent) {
+                const float v = METRIC == MQVS_METRIC_L2 ? cnorm[r] - 2.0f * dot : dot;
+                key = okey<METRIC>(v);
+            }
+            recs[c] = uint4{key, (uint32_t)(r < ncent ? r : 0xFFFFFFFFu), 0u, 0u};
+        }
+    }
+    int N = 1;
+    while (N < M) N <<= 1;
+    for (int c = M + t; c < N; c += SEL_THREADS) recs[c] = uint4{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+    __syncthreads();
+    block_bitonic_sort(recs, N);
+    for (int j = t; j < nprobe; j += SEL_THREADS) {
+        const uint4 e = j < M ? recs[j] : uint4{0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u};
+        probes[(int64_t)qi * nprobe + j] = e.x == 0xFFFFFFFFu ? -1 : (int64_t)e.y;
+    }
+}
+
+void launch_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T, int nprobe, int metric,
+                        const float *q, int64_t qld, const float *cent, const float *cnorm, int64_t ncent, int d,
+                        int nq, int64_t *probes, hipStream_t s) {
+    if (nq <= 0) return;
+    if (metric == MQVS_METRIC_L2)
+        hipLaunchKernelGGL(k_coarse_pick<MQVS_METRIC_L2>, dim3(nq), dim3(SEL_THREADS), 0, s, gmax, gld, ngroups, T,
+                           nprobe, q, qld, cent, cnorm, ncent, d, probes);
+    else
+        hipLaunchKernelGGL(k_coarse_pick<kMetricIpRaw>, dim3(nq), dim3(SEL_THREADS), 0, s, gmax, gld, ngroups, T,
+                           nprobe, q, qld, cent, cnorm, ncent, d, probes);
+}
+
 }  // namespace mqvs

@@ -220,7 +220,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
 #pragma unroll
     for (int jb = 0; jb < 4; ++jb) {
         const int j = q0 + wq * 128 + jb * 32 + l32;
-        const float tj = j < p.nq ? p.thr[j] : 0.f;
+        const float tj = j < p.nq && !PROBE ? p.thr[j] : 0.f;
         tl[jb] = tj;
         qnl[jb] = 0.f;
         if constexpr (L2) {
@@ -679,7 +679,15 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
 // item 7).  Threshold tests: per query block, the 16 values of four row blocks
 // (row blocks 0..3 in the last stage's phase 1, 4..7 in the next item's first
 // phase 0, before their first MFMA overwrites them).
-template <int METRIC, int NBUF, bool PROBE = false>
+// GRP (PROBE only): 0 = one value per (query, 128-row half tile) as k_scan_p4's
+// probe; 16 = one per (query, 16-row block), p4_gmax[q][16 t + 8 wr + rb]
+// (the index's coarse step, kernels_ivf.hip k_coarse_pick)
+// L7: the next stage's B fragment 7 is read in the first gaps of its phase 0
+// instead of the last gap of phase 1 (the compiler drains every LDS read in
+// flight before a stage's first MFMA: the drain then waits for a read issued
+// four MFMAs earlier, not one), and phase 0's A fragments 4..7 and DMA pieces
+// move later
+template <int METRIC, int NBUF, bool PROBE = false, int GRP = 0, int L7 = 0>
 __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u32x4 *queue, int qcap, int tmap) {
     constexpr bool L2 = METRIC == MQVS_METRIC_L2;
     constexpr int D = NBUF - 1;
@@ -733,7 +741,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
 #pragma unroll
     for (int jb = 0; jb < 8; ++jb) {
         const int j = q0 + wq * 128 + jb * 16 + l16;
-        const float tj = j < p.nq ? p.thr[j] : 0.f;
+        const float tj = j < p.nq && !PROBE ? p.thr[j] : 0.f;  // (a probe has no thresholds)
         if constexpr (L2) {
             const float qn = j < p.nq ? p.qnorms[j] : 0.f;
             const float half = (qn - tj) * 0.5f;
@@ -747,7 +755,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
     if constexpr (L2) {
         // (written before the first LDS-DMA; the prologue barrier orders it)
         const int j = q0 + t;
-        qtab[2 * t] = j < p.nq ? p.thr[j] : 0.f;
+        qtab[2 * t] = j < p.nq && !PROBE ? p.thr[j] : 0.f;
         qtab[2 * t + 1] = j < p.nq ? p.qnorms[j] : 0.f;
         __syncthreads();
     }
@@ -907,7 +915,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
 #pragma unroll
     for (int i = 0; i < 4; ++i) a[i] = frag(lds, rowA + i * 16 * 64 + offm);
 #pragma unroll
-    for (int i = 0; i < 8; ++i) b[i] = frag(lds, rowB + i * 16 * 64 + offm);
+    for (int i = 0; i < (L7 ? 7 : 8); ++i) b[i] = frag(lds, rowB + i * 16 * 64 + offm);
 
     // the test of query block jb over row blocks 4 hf .. 4 hf + 3 (16 values
     // per lane, all of its query l & 15) of the item at rows ecr0 (ecrn rows)
@@ -928,10 +936,27 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
                     if (rbl + 16 * (r >> 2) + (r & 3) >= ecrn) v4[r >> 2][r & 3] = -__builtin_inff();
             }
         }
+        const int j = q0 + wq * 128 + jb * 16 + l16;
+        if constexpr (PROBE && GRP == 16) {
+            // the four lanes of query l16 hold the block's 16 rows
+#pragma unroll
+            for (int g = 0; g < 4; ++g) {
+                float m = __builtin_elementwise_maximum(__builtin_elementwise_maximum(v4[g][0], v4[g][1]),
+                                                        __builtin_elementwise_maximum(v4[g][2], v4[g][3]));
+                m = __builtin_elementwise_maximum(m, __shfl_xor(m, 16));
+                m = __builtin_elementwise_maximum(m, __shfl_xor(m, 32));
+                if (g4 == 0 && j < p.nq) {
+                    float raw = m;
+                    if constexpr (L2) raw = qtab[2 * (j - q0) + 1] - 2.0f * m;
+                    if (m == -__builtin_inff()) raw = __builtin_nanf("");
+                    p.p4_gmax[(int64_t)j * p.p4_gld + 16 * eti + 8 * wr + 4 * hf + g] = raw;
+                }
+            }
+            return;
+        }
         float mx = v4[0][0];
 #pragma unroll
         for (int r = 1; r < 16; ++r) mx = __builtin_elementwise_maximum(mx, v4[r >> 2][r & 3]);
-        const int j = q0 + wq * 128 + jb * 16 + l16;
         if constexpr (PROBE) {
             gmx[jb] = __builtin_elementwise_maximum(gmx[jb], mx);
             if constexpr (hf == 1) {
@@ -1016,10 +1041,19 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
                 acc[rb][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[jb], ci, 0, 0, 0);
             else
                 acc[rb][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[jb], acc[rb][jb], 0, 0, 0);
-            if constexpr (x < 4)
-                a[4 + x] = frag(st, rowA + (4 + x) * 16 * 64 + offm);
-            else if constexpr (x >= 8 && (x - 8) % 3 == 0 && (x - 8) / 3 < 8)
-                issue_piece((x - 8) / 3);
+            if constexpr (L7) {
+                if constexpr (x == 1)
+                    b[7] = frag(st, rowB + 7 * 16 * 64 + offm);
+                else if constexpr (x >= 12 && x < 16)
+                    a[x - 8] = frag(st, rowA + (x - 8) * 16 * 64 + offm);
+                else if constexpr (x >= 16 && (x & 1) == 0)
+                    issue_piece((x - 16) >> 1);
+            } else {
+                if constexpr (x >= 2 && x < 6)
+                    a[2 + x] = frag(st, rowA + (2 + x) * 16 * 64 + offm);
+                else if constexpr (x >= 8 && (x - 8) % 3 == 0 && (x - 8) / 3 < 8)
+                    issue_piece((x - 8) / 3);
+            }
             __builtin_amdgcn_sched_barrier(0);
         });
     };
@@ -1040,7 +1074,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
                 acc[rb][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[jb], ci, 0, 0, 0);
             else
                 acc[rb][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[jb], acc[rb][jb], 0, 0, 0);
-            if constexpr (FIRST ? rb == 7 : (x & 3) == 3)
+            if constexpr ((FIRST ? rb == 7 : (x & 3) == 3) && !(L7 && jb == 7))
                 b[jb] = frag(sn, rowB + jb * 16 * 64 + offm);
             else if constexpr ((x & 3) == 1 && (x >> 2) < 4)
                 a[x >> 2] = frag(sn, rowA + (x >> 2) * 16 * 64 + offm);
@@ -1073,7 +1107,16 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
             do_stage(T{}, F{}, F{});
         else
             do_stage(T{}, T{}, F{});
-        for (int s = 1; s + 1 < nst; ++s) do_stage(F{}, F{}, F{});
+        // (two stages per iteration: at a loop header the compiler drains
+        // every LDS read in flight -- the next stage's last fragment, read in
+        // the last gap -- so a stage boundary inside the body keeps counted
+        // waits)
+        int s = 1;
+        for (; s + 2 < nst; s += 2) {
+            do_stage(F{}, F{}, F{});
+            do_stage(F{}, F{}, F{});
+        }
+        if (s + 1 < nst) do_stage(F{}, F{}, F{});
         do_stage(F{}, F{}, T{});
         pcr0 = cr0;
         pcrn = cr1 - cr0;
@@ -1189,8 +1232,9 @@ void launch_ord_planes(const uint16_t *q_hi, uint16_t *q_ord, int *desc, const i
 }
 
 // the batch kernels' launch conditions (sets p.num_qblocks)
-static bool p4_ok(ScanParams &p) {
-    if (!p.p4_queue || p.row_list || p.chunk_ord || p.tiles < 1 || p.tile_rows != kP4Tile) return false;
+static bool p4_ok(ScanParams &p, bool need_queue = true) {
+    if ((need_queue && !p.p4_queue) || p.row_list || p.chunk_ord || p.tiles < 1 || p.tile_rows != kP4Tile)
+        return false;
     p.num_qblocks = (p.nq + kP4Tile - 1) / kP4Tile;
     int dev = 0, cus = 0;
     MQVS_HIP(hipGetDevice(&dev));
@@ -1271,6 +1315,7 @@ constexpr int kP4M16Default = 1;
 template <int METRIC>
 static bool launch_p4_any(const ScanParams &p, hipStream_t s) {
     if (tune_int("MQVS_P4_M16", kP4M16Default) == 0) return launch_p4_t<METRIC>(p, s);
+    const int l7 = tune_int("MQVS_P4M_L7", 0);
     ScanParams c = p;
     if (!p4_ok(c)) return false;
     if (METRIC == MQVS_METRIC_L2 && !c.row_norms) return false;
@@ -1279,8 +1324,12 @@ static bool launch_p4_any(const ScanParams &p, hipStream_t s) {
     MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const int per_xcd = cus / 8;
     const int slots = per_xcd / c.num_qblocks * c.num_qblocks;
-    hipLaunchKernelGGL((k_scan_p4m<METRIC, 4>), dim3((unsigned)(8 * per_xcd)), dim3(256), 0, s, c, slots,
-                       reinterpret_cast<u32x4 *>(c.p4_queue), kP4QueueCap, tune_int("MQVS_P4_MAP", 1));
+    if (l7)
+        hipLaunchKernelGGL((k_scan_p4m<METRIC, 4, false, 0, 1>), dim3((unsigned)(8 * per_xcd)), dim3(256), 0, s, c,
+                           slots, reinterpret_cast<u32x4 *>(c.p4_queue), kP4QueueCap, tune_int("MQVS_P4_MAP", 1));
+    else
+        hipLaunchKernelGGL((k_scan_p4m<METRIC, 4>), dim3((unsigned)(8 * per_xcd)), dim3(256), 0, s, c, slots,
+                           reinterpret_cast<u32x4 *>(c.p4_queue), kP4QueueCap, tune_int("MQVS_P4_MAP", 1));
     return true;
 }
 
@@ -1288,7 +1337,7 @@ static bool launch_p4_any(const ScanParams &p, hipStream_t s) {
 // probe rows cannot take the batch kernel (the caller runs the dense probe)
 template <int METRIC>
 static bool launch_p4_probe_t(ScanParams p, hipStream_t s) {
-    if (!p.p4_gmax || p.p4_gld < 2 * p.tiles || !p4_ok(p)) return false;
+    if (!p.p4_gmax || p.p4_gld < 2 * p.tiles || !p4_ok(p, false)) return false;
     if (METRIC == MQVS_METRIC_L2 && !p.row_norms) return false;
     int dev = 0, cus = 0;
     MQVS_HIP(hipGetDevice(&dev));
@@ -1302,6 +1351,24 @@ static bool launch_p4_probe_t(ScanParams p, hipStream_t s) {
     else
         hipLaunchKernelGGL((k_scan_p4<METRIC, 4, 0, 0, true>), grid, dim3(256), 0, s, p, slots, q, kP4QueueCap, 1);
     return true;
+}
+
+template <int METRIC>
+static bool launch_p4_groups_t(ScanParams p, hipStream_t s) {
+    if (!p.p4_gmax || p.p4_gld < 16 * p.tiles || !p4_ok(p, false)) return false;
+    if (METRIC == MQVS_METRIC_L2 && !p.row_norms) return false;
+    int dev = 0, cus = 0;
+    MQVS_HIP(hipGetDevice(&dev));
+    MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int per_xcd = cus / 8;
+    const int slots = per_xcd / p.num_qblocks * p.num_qblocks;
+    hipLaunchKernelGGL((k_scan_p4m<METRIC, 4, true, 16>), dim3((unsigned)(8 * per_xcd)), dim3(256), 0, s, p, slots,
+                       nullptr, kP4QueueCap, 1);
+    return true;
+}
+
+bool launch_scan_p4_groups(const ScanParams &p, int metric, hipStream_t s) {
+    return metric == MQVS_METRIC_L2 ? launch_p4_groups_t<MQVS_METRIC_L2>(p, s) : launch_p4_groups_t<kMetricIpRaw>(p, s);
 }
 
 bool launch_scan_p4_probe(const ScanParams &p, int metric, hipStream_t s) {

@@ -430,6 +430,18 @@ void launch_ivf_pack(const float *rows, const float *norms, int d, const int32_t
                      uint16_t *plane, float *pnorm, hipStream_t s);
 void launch_gather_rows(const float *src, int64_t src_ld, int d, const int64_t *idx, int64_t m, float *dst,
                         hipStream_t s);
+constexpr int kCoarsePickMaxT = 64;  // groups a coarse pick may take per query
+// the coarse step's pick from the batch probe's 16-centroid group maxima
+// (kernels_ivf.hip): per query the T best groups (T <= 64), the exact values
+// of their centroids (coarse metric: L2 or kMetricIpRaw), the nprobe best ->
+// probes[q][0, nprobe) (-1 when fewer)
+void launch_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T, int nprobe, int metric,
+                        const float *q, int64_t qld, const float *cent, const float *cnorm, int64_t ncent, int d,
+                        int nq, int64_t *probes, hipStream_t s);
+// the batch probe by 16-row groups (kernels_p4.hip): p.p4_gmax[q][16 t + r]
+// = the best value of rows [16 r, 16 r + 16) of tile t (p.p4_gld >= 16
+// p.tiles); false when the rows cannot take the batch kernel
+bool launch_scan_p4_groups(const ScanParams &p, int metric, hipStream_t s);
 void launch_centroid_mean(const float *rows, int d, const int32_t *order, const int64_t *off, int nlist, float *cent,
                           hipStream_t s);
 

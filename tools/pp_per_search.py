@@ -1,27 +1,36 @@
 #!/usr/bin/env python3
-"""Per-search sums of the batch-scan launches (k_scan_p4 by default) in a
-rocprofv3 kernel trace (the bench's rocprof run: six main-scan launches per
-search).
-  python tools/pp_per_search.py gpurun_out/r03/prof/run_kernel_trace.csv [kernel] > profiles/r03/bench_p4_per_search.txt"""
+"""Per-search sums of the batch-scan launches in a rocprofv3 kernel trace of
+the bench (its --kernel-trace run).  A search is one batch-probe launch
+(`k_scan_p4m<..., true, ...>`) followed by its main-scan segments
+(`k_scan_p4m<..., false, ...>`); the main-scan launches are summed per search.
+  python tools/pp_per_search.py gpurun_out/r04/prof/run_kernel_trace.csv > profiles/r04/bench_p4m_per_search.txt"""
 import csv
 import sys
 
 
-def main(path, kernel="k_scan_p4", per_search=6):
-    durs = []
+def main(path, kernel="k_scan_p4m"):
+    ev = []
     with open(path) as f:
         for row in csv.DictReader(f):
-            if kernel in row["Kernel_Name"]:
-                durs.append((int(row["Start_Timestamp"]), (int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) / 1e6))
-    durs.sort()
-    ms = [d for _, d in durs]
+            name = row["Kernel_Name"]
+            if kernel not in name:
+                continue
+            t0, t1 = int(row["Start_Timestamp"]), int(row["End_Timestamp"])
+            ev.append((t0, (t1 - t0) / 1e6, "true" in name.split("(")[0]))
+    ev.sort()
+    searches, cur = [], None
+    for _, ms, probe in ev:
+        if probe:
+            cur = {"probe_ms": ms, "main": []}
+            searches.append(cur)
+        elif cur is not None:
+            cur["main"].append(ms)
     print(f"{kernel} launches of the rocprofv3 --kernel-trace run of the bench")
     print("(bench.py --steps 3 --warmup 1 --no-cpu --no-verify --no-index --no-configs --no-config1-points):")
-    print("six launches (main-scan segments) per search; search 0 = warmup, then the timed steps.")
-    print("search  sum_ms  per-launch ms")
-    for s in range(len(ms) // per_search):
-        part = ms[s * per_search:(s + 1) * per_search]
-        print(s, round(sum(part), 3), [round(x, 3) for x in part])
+    print("per search: the batch probe, then the main-scan segments; search 0 = warmup, then the timed steps.")
+    print("search  main_sum_ms  probe_ms  main per-launch ms")
+    for i, s in enumerate(searches):
+        print(i, round(sum(s["main"]), 3), round(s["probe_ms"], 3), [round(x, 3) for x in s["main"]])
 
 
 if __name__ == "__main__":
