@@ -476,9 +476,26 @@ public:
                                   dist, 0, nullptr));
     }
 
+    /// Searches that synchronised the host once (a repeat of the last call
+    /// every rank completed), and how many of them re-ran on the validated path.
+    std::pair<int64_t, int64_t> stats() const
+    {
+        int64_t fast = 0, redo = 0;
+        check(mqvs_comm_stats(comm, &fast, &redo));
+        return {fast, redo};
+    }
+
 private:
     mqvs_comm_t comm = nullptr;
 };
+
+/// Cap on the device memory of all threads' search workspaces (the
+/// ScanThreadLimiter's 2 x cores concurrent scans, MergeTreeVSManager.cpp:972-975):
+/// searches wait for memory instead of failing.  Returns the previous cap.
+inline size_t setWorkspaceBudget(size_t bytes)
+{
+    return mqvs_set_workspace_budget(bytes);
+}
 
 /// VICacheManager (VICacheManager.h:82-114) on the device: parts (+ index)
 /// resident in HBM, LRU under max_bytes, pinned while a Holder lives.
