@@ -687,7 +687,12 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
 // flight before a stage's first MFMA: the drain then waits for a read issued
 // four MFMAs earlier, not one), and phase 0's A fragments 4..7 and DMA pieces
 // move later
-template <int METRIC, int NBUF, bool PROBE = false, int GRP = 0, int L7 = 0>
+// STG: waves 2 and 3 issue their DMA pieces in phase 1 instead of phase 0, so
+// that two waves, not four, contend for the CU's address path in each phase
+// (a piece's issue cost grows with the pieces in flight around it,
+// MI355X_MICROARCH.md constants table); the counted waits follow each wave's
+// own issue count, so they need no change
+template <int METRIC, int NBUF, bool PROBE = false, int GRP = 0, int L7 = 0, int STG = 0>
 __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u32x4 *queue, int qcap, int tmap) {
     constexpr bool L2 = METRIC == MQVS_METRIC_L2;
     constexpr int D = NBUF - 1;
@@ -1046,13 +1051,15 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
                     b[7] = frag(st, rowB + 7 * 16 * 64 + offm);
                 else if constexpr (x >= 12 && x < 16)
                     a[x - 8] = frag(st, rowA + (x - 8) * 16 * 64 + offm);
-                else if constexpr (x >= 16 && (x & 1) == 0)
-                    issue_piece((x - 16) >> 1);
+                else if constexpr (x >= 16 && (x & 1) == 0) {
+                    if (!STG || w < 2) issue_piece((x - 16) >> 1);
+                }
             } else {
                 if constexpr (x >= 2 && x < 6)
                     a[2 + x] = frag(st, rowA + (2 + x) * 16 * 64 + offm);
-                else if constexpr (x >= 8 && (x - 8) % 3 == 0 && (x - 8) / 3 < 8)
-                    issue_piece((x - 8) / 3);
+                else if constexpr (x >= 8 && (x - 8) % 3 == 0 && (x - 8) / 3 < 8) {
+                    if (!STG || w < 2) issue_piece((x - 8) / 3);
+                }
             }
             __builtin_amdgcn_sched_barrier(0);
         });
@@ -1078,6 +1085,9 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
                 b[jb] = frag(sn, rowB + jb * 16 * 64 + offm);
             else if constexpr ((x & 3) == 1 && (x >> 2) < 4)
                 a[x >> 2] = frag(sn, rowA + (x >> 2) * 16 * 64 + offm);
+            if constexpr (STG && (x & 3) == 2) {
+                if (w >= 2) issue_piece(x >> 2);
+            }
             if constexpr (LAST && (x & 3) == 2)
                 check(std::integral_constant<int, 0>{}, std::integral_constant<int, jb>{}, cr0, crn, ti_c);
             __builtin_amdgcn_sched_barrier(0);
@@ -1088,13 +1098,19 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
         const unsigned char *st = lds + cbuf * kP4Stage;
         const int nbuf_next = cbuf + 1 == NBUF ? 0 : cbuf + 1;
         phase0(st, first_tag, epi_tag);
-        if (L2 && si == 0 && live) issue_piece(8);
-        issue_advance();
+        if (!STG || w < 2) {
+            if (L2 && si == 0 && live) issue_piece(8);
+            issue_advance();
+        }
         const bool has_next = gc + 1 < issued;
         p4_wait_vm<NPW>(issued - gc - 2, has_next);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         p4_barrier();
         phase1(lds + nbuf_next * kP4Stage, first_tag, last_tag, cr1 - cr0);
+        if (STG && w >= 2) {
+            if (L2 && si == 0 && live) issue_piece(8);
+            issue_advance();
+        }
         ++gc;
         cbuf = nbuf_next;
     };
@@ -1315,7 +1331,7 @@ constexpr int kP4M16Default = 1;
 template <int METRIC>
 static bool launch_p4_any(const ScanParams &p, hipStream_t s) {
     if (tune_int("MQVS_P4_M16", kP4M16Default) == 0) return launch_p4_t<METRIC>(p, s);
-    const int l7 = tune_int("MQVS_P4M_L7", 0);
+    const int l7 = tune_int("MQVS_P4M_L7", 0), stg = tune_int("MQVS_P4M_STG", 0);
     ScanParams c = p;
     if (!p4_ok(c)) return false;
     if (METRIC == MQVS_METRIC_L2 && !c.row_norms) return false;
@@ -1324,9 +1340,18 @@ static bool launch_p4_any(const ScanParams &p, hipStream_t s) {
     MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const int per_xcd = cus / 8;
     const int slots = per_xcd / c.num_qblocks * c.num_qblocks;
-    if (l7)
-        hipLaunchKernelGGL((k_scan_p4m<METRIC, 4, false, 0, 1>), dim3((unsigned)(8 * per_xcd)), dim3(256), 0, s, c,
-                           slots, reinterpret_cast<u32x4 *>(c.p4_queue), kP4QueueCap, tune_int("MQVS_P4_MAP", 1));
+    const dim3 grid((unsigned)(8 * per_xcd));
+    auto *qq = reinterpret_cast<u32x4 *>(c.p4_queue);
+    const int tmap = tune_int("MQVS_P4_MAP", 1);
+    if (kDebugTuning && l7 && stg)
+        hipLaunchKernelGGL((k_scan_p4m<METRIC, 4, false, 0, 1, 1>), grid, dim3(256), 0, s, c, slots, qq, kP4QueueCap,
+                           tmap);
+    else if (kDebugTuning && stg)
+        hipLaunchKernelGGL((k_scan_p4m<METRIC, 4, false, 0, 0, 1>), grid, dim3(256), 0, s, c, slots, qq, kP4QueueCap,
+                           tmap);
+    else if (kDebugTuning && l7)
+        hipLaunchKernelGGL((k_scan_p4m<METRIC, 4, false, 0, 1>), grid, dim3(256), 0, s, c, slots, qq, kP4QueueCap,
+                           tmap);
     else
         hipLaunchKernelGGL((k_scan_p4m<METRIC, 4>), dim3((unsigned)(8 * per_xcd)), dim3(256), 0, s, c, slots,
                            reinterpret_cast<u32x4 *>(c.p4_queue), kP4QueueCap, tune_int("MQVS_P4_MAP", 1));

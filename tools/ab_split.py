@@ -62,8 +62,8 @@ def main():
                         truth[nq] = (ids.cpu().numpy(), dist.cpu().numpy())
                         set_batch_mode(0)
                     for tune in tunes:
-                        if tune:
-                            key, val = tune.split("=", 1)
+                        for kv in [x for x in tune.split("+") if x]:  # ('+' joins several settings)
+                            key, val = kv.split("=", 1)
                             os.environ[key] = val
                         ids, dist = seg.search(q, args.k)
                         torch.cuda.synchronize()
@@ -84,8 +84,8 @@ def main():
                             seg.search(q, args.k)
                             sts.append(_lib.last_search_stats())
                         set_timing(False)
-                        if tune:
-                            del os.environ[tune.split("=", 1)[0]]
+                        for kv in [x for x in tune.split("+") if x]:
+                            del os.environ[kv.split("=", 1)[0]]
                         st = min(sts, key=lambda s: s["total_ms"])
                         print(json.dumps({
                             "split": split, "tune": tune, "metric": metric, "mode": mode, "nq": nq,
