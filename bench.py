@@ -69,7 +69,7 @@ def parse():
                     help="skip the extra configs[1] points (L2 metric, second distribution)")
     ap.add_argument("--read-sweep-gib", type=float, default=8.0,
                     help="buffer of the HBM read sweep (mqvs_measure_read_bandwidth); 0 = skip")
-    ap.add_argument("--index-settings", default="nprobe=4;nprobe=8;nprobe=16",
+    ap.add_argument("--index-settings", default="nprobe=1;nprobe=2;nprobe=4;nprobe=8;nprobe=16",
                     help="';'-separated mqvs_index_search parameter strings timed by the index leg")
     ap.add_argument("--index-mode", type=int, default=2,
                     help="index distribution (generator mode; 2 = 4096 centres, noise 0.25)")

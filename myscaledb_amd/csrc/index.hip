@@ -33,6 +33,7 @@
 #include <cstring>
 #include <map>
 #include <string>
+#include <chrono>
 #include <vector>
 
 #include "mqvs_internal.h"
@@ -65,6 +66,7 @@ struct mqvs_index {
     int64_t row_ids_len = 0;
     size_t bytes = 0;
     double build_ms = 0.0;
+    int np95 = 0;                  // nprobe measured to reach recall@10 0.95 on the build's sample (0: not measured)
 };
 
 namespace mqvs {
@@ -159,7 +161,12 @@ static void check_keys(const std::map<std::string, std::string> &m, const std::v
 // the base probes 1/256 of the lists and at least 4 lists and 4096 rows
 static int nprobe_of(const mqvs_index *ix, double alpha) {
     const double rows = (double)std::max<int64_t>(ix->rows_indexed, 1);
-    const double base = std::max({4.0, std::ceil((double)ix->nlist / 256.0), std::ceil(4096.0 * ix->nlist / rows)});
+    // (an index whose list count was chosen from its data knows the nprobe
+    // that reached recall@10 0.95 on the build's sample: alpha 3 probes 1.5x
+    // that, a margin for queries unlike the part's own rows)
+    const double base = ix->np95 > 0 ? (double)(ix->np95 + std::max(1, ix->np95 / 2))
+                                     : std::max({4.0, std::ceil((double)ix->nlist / 256.0),
+                                                 std::ceil(4096.0 * ix->nlist / rows)});
     const double np = std::ceil(base * std::pow(2.0, alpha - 3.0));
     return (int)std::max<double>(1.0, std::min<double>(np, (double)std::min<int64_t>(ix->nlist, kSortCap)));
 }
@@ -238,6 +245,12 @@ struct TmpBuf {
     }
 };
 
+static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int k, const char *params,
+                              const uint8_t *filter, const uint8_t *exists, int64_t *out_ids, float *out_dist,
+                              uint32_t flags, hipStream_t user_stream, int formula_nq);
+static mqvs_index *build_auto(mqvs_segment *seg, const char *index_type, const char *params);
+constexpr int64_t kAutoNlistMinRows = 1 << 20;  // smaller parts take the default list count
+
 static mqvs_index *build_impl(mqvs_segment *seg, const char *index_type, const char *params) {
     if (!seg) fail(MQVS_ERR_BAD_ARGUMENTS, "null segment");
     if (seg->binary) fail(MQVS_ERR_NOT_IMPLEMENTED, "vector index over binary vectors is not implemented");
@@ -264,6 +277,7 @@ static mqvs_index *build_impl(mqvs_segment *seg, const char *index_type, const c
     }
     const int64_t n = seg->n;
     const int d = seg->d;
+    if (!pm.count("nlist") && n >= kAutoNlistMinRows && !seg->nonempty_bits) return build_auto(seg, index_type, params);
     // lists of about 256 rows (at most 65536 lists): fine enough that data of
     // many small clusters (generator mode 3: 65536 centres of ~150 rows)
     // keeps its neighbours in one or two lists; n / 1000 left mode 3 needing
@@ -425,6 +439,133 @@ static mqvs_index *build_impl(mqvs_segment *seg, const char *index_type, const c
     return ix;
 }
 
+// ---- the list count from the data ------------------------------------------
+// Without an explicit nlist, a part of at least 2^20 rows gets its list count
+// from a sample: the fine default (about 256 rows per list) is built, and m =
+// 1000 of the part's own rows are searched as queries against it at growing
+// nprobe until recall@10 against their exact FLAT top-10 reaches 0.95.  If that
+// takes more than 2 probes -- the data's clusters are larger than the lists,
+// so a query's neighbours spread over many of them and every search pays the
+// coarse step and plan of many small lists -- a coarse index (about 2048 rows
+// per list) is built and evaluated the same way, and the faster of the two at
+// recall 0.95 is kept (its nprobe becomes alpha 3's).  Data of many small
+// clusters (generator mode 3) keeps the fine lists; data of few large ones
+// (mode 2: 4096 centres over 10M rows) gets the coarse ones.
+struct IndexEval {
+    int nprobe = 0;  // 0: recall 0.95 not reached
+    double ms = 1e30;
+    double recall = 0.0;
+};
+
+// recall@10 of the sample's queries (rows of the part): the query row itself
+// is dropped from both lists, so the figure is that of held-out queries
+constexpr int kEvalK = 11;
+static double sample_recall(const std::vector<int64_t> &got, const std::vector<int64_t> &gt,
+                            const std::vector<int64_t> &self, int m) {
+    int64_t hit = 0;
+    for (int q = 0; q < m; ++q) {
+        int64_t g[kEvalK], t[kEvalK];
+        int ng = 0, nt = 0;
+        for (int a = 0; a < kEvalK; ++a) {
+            const int64_t x = got[(size_t)q * kEvalK + a], y = gt[(size_t)q * kEvalK + a];
+            if (x != self[q] && ng < 10) g[ng++] = x;
+            if (y != self[q] && nt < 10) t[nt++] = y;
+        }
+        for (int a = 0; a < ng; ++a)
+            for (int b = 0; b < nt; ++b) hit += g[a] >= 0 && g[a] == t[b];
+    }
+    return (double)hit / (10.0 * m);
+}
+
+static IndexEval eval_index(mqvs_index *ix, const float *dq, int m, const std::vector<int64_t> &gt,
+                            const std::vector<int64_t> &self, int64_t *dids, float *ddist, hipStream_t s) {
+    IndexEval r;
+    std::vector<int64_t> got((size_t)m * kEvalK);
+    hipEvent_t e0, e1;
+    MQVS_HIP(hipEventCreate(&e0));
+    MQVS_HIP(hipEventCreate(&e1));
+    try {
+        for (int np : {1, 2, 3, 4, 6, 8, 12, 16, 24, 32, 48, 64}) {
+            if (np > std::min<int64_t>(ix->nlist, kSortCap)) break;
+            const std::string sp = "nprobe=" + std::to_string(np);
+            search_index_impl(ix, dq, m, kEvalK, sp.c_str(), nullptr, nullptr, dids, ddist, MQVS_F_DEVICE_PTRS, s, 0);
+            MQVS_HIP(hipMemcpyAsync(got.data(), dids, sizeof(int64_t) * got.size(), hipMemcpyDeviceToHost, s));
+            MQVS_HIP(hipStreamSynchronize(s));
+            r.recall = sample_recall(got, gt, self, m);
+            if (r.recall < 0.95) continue;
+            r.nprobe = np;
+            for (int rep = 0; rep < 3; ++rep) {
+                MQVS_HIP(hipEventRecord(e0, s));
+                search_index_impl(ix, dq, m, kEvalK, sp.c_str(), nullptr, nullptr, dids, ddist, MQVS_F_DEVICE_PTRS, s,
+                                  0);
+                MQVS_HIP(hipEventRecord(e1, s));
+                MQVS_HIP(hipStreamSynchronize(s));
+                float ms = 0.f;
+                MQVS_HIP(hipEventElapsedTime(&ms, e0, e1));
+                r.ms = std::min(r.ms, (double)ms);
+            }
+            break;
+        }
+    } catch (...) {
+        (void)hipEventDestroy(e0);
+        (void)hipEventDestroy(e1);
+        throw;
+    }
+    (void)hipEventDestroy(e0);
+    (void)hipEventDestroy(e1);
+    return r;
+}
+
+static mqvs_index *build_auto(mqvs_segment *seg, const char *index_type, const char *params) {
+    const int64_t n = seg->n;
+    const int d = seg->d;
+    const std::string base = params ? std::string(params) : std::string();
+    auto with_nlist = [&](int64_t L) { return (base.empty() ? "" : base + ",") + "nlist=" + std::to_string(L); };
+    const int64_t fine = std::max<int64_t>(1, std::min<int64_t>(65536, (n + 128) / 256));
+    const int64_t coarse = std::max<int64_t>(1, (n + 1024) / 2048);
+    const auto t0 = std::chrono::steady_clock::now();
+    mqvs_index *a = build_impl(seg, index_type, with_nlist(fine).c_str());
+    mqvs_index *b = nullptr;
+    try {
+        DeviceGuard guard(seg->device);
+        hipStream_t s = thread_stream(seg->device);
+        // the sample: m evenly spaced rows of the part as queries, their exact
+        // FLAT top-10 as ground truth (the index's metric)
+        const int m = (int)std::min<int64_t>(1000, n);
+        std::vector<int64_t> idx(m);
+        for (int i = 0; i < m; ++i) idx[i] = (int64_t)(((__int128)(2 * i + 1) * n) / (2 * m));
+        TmpBuf didx(sizeof(int64_t) * m), dq(sizeof(float) * (size_t)m * d),
+            dids(sizeof(int64_t) * (size_t)m * kEvalK), ddist(sizeof(float) * (size_t)m * kEvalK);
+        MQVS_HIP(hipMemcpyAsync(didx.p, idx.data(), sizeof(int64_t) * m, hipMemcpyHostToDevice, s));
+        launch_gather_rows(seg->rows, d, d, didx.as<int64_t>(), m, dq.as<float>(), s);
+        MQVS_HIP(hipGetLastError());
+        search_internal(seg, dq.as<float>(), m, kEvalK, a->metric, nullptr, nullptr, dids.as<int64_t>(),
+                        ddist.as<float>(), MQVS_F_DEVICE_PTRS, s);
+        std::vector<int64_t> gt((size_t)m * kEvalK);
+        MQVS_HIP(hipMemcpyAsync(gt.data(), dids.p, sizeof(int64_t) * gt.size(), hipMemcpyDeviceToHost, s));
+        MQVS_HIP(hipStreamSynchronize(s));
+        std::vector<int64_t> self(m);
+        for (int i = 0; i < m; ++i) self[i] = seg->row_offset + idx[i];
+        const IndexEval ea = eval_index(a, dq.as<float>(), m, gt, self, dids.as<int64_t>(), ddist.as<float>(), s);
+        a->np95 = ea.nprobe;
+        if ((ea.nprobe == 0 || ea.nprobe > 2) && coarse < fine) {
+            b = build_impl(seg, index_type, with_nlist(coarse).c_str());
+            const IndexEval eb = eval_index(b, dq.as<float>(), m, gt, self, dids.as<int64_t>(), ddist.as<float>(), s);
+            b->np95 = eb.nprobe;
+            if (eb.nprobe > 0 && eb.ms < ea.ms) std::swap(a, b);
+            free_index(b);
+            b = nullptr;
+        }
+        // (the build time of the chosen index covers both builds and the sample)
+        a->build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
+    } catch (...) {
+        free_index(a);
+        if (b) free_index(b);
+        throw;
+    }
+    return a;
+}
+
 // ---- search -----------------------------------------------------------------
 
 // One list pass: plan + bf16 MFMA scan + select of nq queries over a list
@@ -503,7 +644,7 @@ static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, c
 // distance formula (0: nq; query sub-batches keep the call's, see mqvs.hip)
 static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int k, const char *params,
                               const uint8_t *filter, const uint8_t *exists, int64_t *out_ids, float *out_dist,
-                              uint32_t flags, hipStream_t user_stream, int formula_nq = 0) {
+                              uint32_t flags, hipStream_t user_stream, int formula_nq) {
     const int fnq = formula_nq > 0 ? formula_nq : nq;
     if (!ix) fail(MQVS_ERR_BAD_ARGUMENTS, "null index");
     if (nq < 0 || k < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "nq and k must be non-negative");
@@ -800,7 +941,7 @@ int mqvs_index_search(mqvs_index_t idx, const float *queries, int32_t nq, int32_
                       uint32_t flags, mqvs_stream_t stream) {
     return guarded([&] {
         search_index_impl(idx, queries, nq, k, params, filter, row_exists, out_ids, out_dist, flags,
-                          (hipStream_t)stream);
+                          (hipStream_t)stream, 0);
     });
 }
 

@@ -682,17 +682,11 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
 // GRP (PROBE only): 0 = one value per (query, 128-row half tile) as k_scan_p4's
 // probe; 16 = one per (query, 16-row block), p4_gmax[q][16 t + 8 wr + rb]
 // (the index's coarse step, kernels_ivf.hip k_coarse_pick)
-// L7: the next stage's B fragment 7 is read in the first gaps of its phase 0
-// instead of the last gap of phase 1 (the compiler drains every LDS read in
-// flight before a stage's first MFMA: the drain then waits for a read issued
-// four MFMAs earlier, not one), and phase 0's A fragments 4..7 and DMA pieces
-// move later
-// STG: waves 2 and 3 issue their DMA pieces in phase 1 instead of phase 0, so
-// that two waves, not four, contend for the CU's address path in each phase
-// (a piece's issue cost grows with the pieces in flight around it,
-// MI355X_MICROARCH.md constants table); the counted waits follow each wave's
-// own issue count, so they need no change
-template <int METRIC, int NBUF, bool PROBE = false, int GRP = 0, int L7 = 0, int STG = 0>
+// (Measured and dropped, profiles/r04/p4m_l7_stg_ab.jsonl: the next stage's
+// B fragment 7 read at the start of phase 0 instead of the end of phase 1,
+// +0.4..2.4 % main scan; waves 2 and 3 issuing their DMA pieces in phase 1,
+// +15 %.)
+template <int METRIC, int NBUF, bool PROBE = false, int GRP = 0>
 __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u32x4 *queue, int qcap, int tmap) {
     constexpr bool L2 = METRIC == MQVS_METRIC_L2;
     constexpr int D = NBUF - 1;
@@ -920,7 +914,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
 #pragma unroll
     for (int i = 0; i < 4; ++i) a[i] = frag(lds, rowA + i * 16 * 64 + offm);
 #pragma unroll
-    for (int i = 0; i < (L7 ? 7 : 8); ++i) b[i] = frag(lds, rowB + i * 16 * 64 + offm);
+    for (int i = 0; i < 8; ++i) b[i] = frag(lds, rowB + i * 16 * 64 + offm);
 
     // the test of query block jb over row blocks 4 hf .. 4 hf + 3 (16 values
     // per lane, all of its query l & 15) of the item at rows ecr0 (ecrn rows)
@@ -1046,21 +1040,10 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
                 acc[rb][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[jb], ci, 0, 0, 0);
             else
                 acc[rb][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[jb], acc[rb][jb], 0, 0, 0);
-            if constexpr (L7) {
-                if constexpr (x == 1)
-                    b[7] = frag(st, rowB + 7 * 16 * 64 + offm);
-                else if constexpr (x >= 12 && x < 16)
-                    a[x - 8] = frag(st, rowA + (x - 8) * 16 * 64 + offm);
-                else if constexpr (x >= 16 && (x & 1) == 0) {
-                    if (!STG || w < 2) issue_piece((x - 16) >> 1);
-                }
-            } else {
-                if constexpr (x >= 2 && x < 6)
-                    a[2 + x] = frag(st, rowA + (2 + x) * 16 * 64 + offm);
-                else if constexpr (x >= 8 && (x - 8) % 3 == 0 && (x - 8) / 3 < 8) {
-                    if (!STG || w < 2) issue_piece((x - 8) / 3);
-                }
-            }
+            if constexpr (x >= 2 && x < 6)
+                a[2 + x] = frag(st, rowA + (2 + x) * 16 * 64 + offm);
+            else if constexpr (x >= 8 && (x - 8) % 3 == 0 && (x - 8) / 3 < 8)
+                issue_piece((x - 8) / 3);
             __builtin_amdgcn_sched_barrier(0);
         });
     };
@@ -1081,13 +1064,10 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
                 acc[rb][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[jb], ci, 0, 0, 0);
             else
                 acc[rb][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[jb], acc[rb][jb], 0, 0, 0);
-            if constexpr ((FIRST ? rb == 7 : (x & 3) == 3) && !(L7 && jb == 7))
+            if constexpr (FIRST ? rb == 7 : (x & 3) == 3)
                 b[jb] = frag(sn, rowB + jb * 16 * 64 + offm);
             else if constexpr ((x & 3) == 1 && (x >> 2) < 4)
                 a[x >> 2] = frag(sn, rowA + (x >> 2) * 16 * 64 + offm);
-            if constexpr (STG && (x & 3) == 2) {
-                if (w >= 2) issue_piece(x >> 2);
-            }
             if constexpr (LAST && (x & 3) == 2)
                 check(std::integral_constant<int, 0>{}, std::integral_constant<int, jb>{}, cr0, crn, ti_c);
             __builtin_amdgcn_sched_barrier(0);
@@ -1098,19 +1078,13 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
         const unsigned char *st = lds + cbuf * kP4Stage;
         const int nbuf_next = cbuf + 1 == NBUF ? 0 : cbuf + 1;
         phase0(st, first_tag, epi_tag);
-        if (!STG || w < 2) {
-            if (L2 && si == 0 && live) issue_piece(8);
-            issue_advance();
-        }
+        if (L2 && si == 0 && live) issue_piece(8);
+        issue_advance();
         const bool has_next = gc + 1 < issued;
         p4_wait_vm<NPW>(issued - gc - 2, has_next);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
         p4_barrier();
         phase1(lds + nbuf_next * kP4Stage, first_tag, last_tag, cr1 - cr0);
-        if (STG && w >= 2) {
-            if (L2 && si == 0 && live) issue_piece(8);
-            issue_advance();
-        }
         ++gc;
         cbuf = nbuf_next;
     };
@@ -1331,7 +1305,7 @@ constexpr int kP4M16Default = 1;
 template <int METRIC>
 static bool launch_p4_any(const ScanParams &p, hipStream_t s) {
     if (tune_int("MQVS_P4_M16", kP4M16Default) == 0) return launch_p4_t<METRIC>(p, s);
-    const int l7 = tune_int("MQVS_P4M_L7", 0), stg = tune_int("MQVS_P4M_STG", 0);
+
     ScanParams c = p;
     if (!p4_ok(c)) return false;
     if (METRIC == MQVS_METRIC_L2 && !c.row_norms) return false;
@@ -1343,18 +1317,7 @@ static bool launch_p4_any(const ScanParams &p, hipStream_t s) {
     const dim3 grid((unsigned)(8 * per_xcd));
     auto *qq = reinterpret_cast<u32x4 *>(c.p4_queue);
     const int tmap = tune_int("MQVS_P4_MAP", 1);
-    if (kDebugTuning && l7 && stg)
-        hipLaunchKernelGGL((k_scan_p4m<METRIC, 4, false, 0, 1, 1>), grid, dim3(256), 0, s, c, slots, qq, kP4QueueCap,
-                           tmap);
-    else if (kDebugTuning && stg)
-        hipLaunchKernelGGL((k_scan_p4m<METRIC, 4, false, 0, 0, 1>), grid, dim3(256), 0, s, c, slots, qq, kP4QueueCap,
-                           tmap);
-    else if (kDebugTuning && l7)
-        hipLaunchKernelGGL((k_scan_p4m<METRIC, 4, false, 0, 1>), grid, dim3(256), 0, s, c, slots, qq, kP4QueueCap,
-                           tmap);
-    else
-        hipLaunchKernelGGL((k_scan_p4m<METRIC, 4>), dim3((unsigned)(8 * per_xcd)), dim3(256), 0, s, c, slots,
-                           reinterpret_cast<u32x4 *>(c.p4_queue), kP4QueueCap, tune_int("MQVS_P4_MAP", 1));
+    hipLaunchKernelGGL((k_scan_p4m<METRIC, 4>), grid, dim3(256), 0, s, c, slots, qq, kP4QueueCap, tmap);
     return true;
 }
 

@@ -12,7 +12,7 @@ run() {  # tag, seconds, command...
   echo "== $tag"; cut -c1-330 $O/$tag.jsonl
 }
 run m3 300 python -u tools/index_sweep.py --mode 3 --search "nprobe=1;nprobe=2;nprobe=4" --reps 5
-run m2 300 python -u tools/index_sweep.py --mode 2 --search "nprobe=4;nprobe=8;nprobe=16" --reps 5
+run m2 300 python -u tools/index_sweep.py --mode 2 --search "nprobe=1;nprobe=2;nprobe=4;nprobe=8" --reps 5
 if [ "${1:-}" = ab ]; then
   run m3_flat 300 env MQVS_IVF_COARSE=1 python -u tools/index_sweep.py --dbg --mode 3 --search "nprobe=1;nprobe=2" --reps 5
 fi

@@ -10,7 +10,7 @@ cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/r04
 mkdir -p $O
-STEPS="${*:-pmc pmc4 risk bench}"
+STEPS="${*:-pmc pmc4 index bench}"
 pmc_set() {  # tag, searches, args...
   local tag=$1 s=$2; shift 2
   bash tools/gpu_pmc.sh python tools/pmc_search.py --searches "$s" "$@" || return 1
@@ -28,6 +28,9 @@ for step in $STEPS; do
       pmc_set config4 4 --nq 1 --n 50000000 --metric L2 --selectivity 100 || exit 1
       python tools/pmc_traffic.py $O/pmc_config4 --searches 5 --nq 1 --out $O/pmc_config4_sel100.json > /dev/null || exit 1
       echo "pmc4 done"; grep -E "hbm_bytes_per_search|avg_launch|k_scan" $O/pmc_config4_sel100.json ;;
+    index)
+      bash tools/gpu_index_pmc.sh 2:nprobe=1 3:nprobe=1 > $O/index_pmc.log 2>&1 || { echo "index pmc failed"; tail -20 $O/index_pmc.log; exit 1; }
+      cp gpurun_out/index_pmc.json $O/index_pmc.json && grep -E "hbm_bytes_per_search|search" $O/index_pmc.json | head -8 ;;
     risk)
       timeout -k 10 600 python -u tools/blas_order_risk.py --out $O/blas_order_risk.json > $O/blas_order_risk.log 2>&1 \
         || { echo "risk failed"; tail -20 $O/blas_order_risk.log; exit 1; }
