@@ -32,8 +32,8 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, f32 MFMA (= VALU) dense p
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md, bf16 MFMA dense peak (no sparsity)
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md, HBM3E spec peak
 ROOT = os.path.dirname(os.path.abspath(__file__))
-PMC_DEFAULT = "profiles/r03/pmc_traffic.json"
-PMC_NQ1_DEFAULT = "profiles/r03/pmc_nq1.json"
+PMC_DEFAULT = "profiles/r04/pmc_traffic.json"
+PMC_NQ1_DEFAULT = "profiles/r04/pmc_nq1.json"
 BLAS_RISK_DEFAULT = "profiles/r03/blas_order_risk.json"
 
 
@@ -63,6 +63,7 @@ def parse():
     ap.add_argument("--no-verify", action="store_true", help="skip the full-size exact-path comparison")
     ap.add_argument("--no-small", action="store_true", help="skip the nq = 1 / 4 / 16 / 64 sweep")
     ap.add_argument("--pmc", default=None, help="rocprofv3 PMC summary JSON for roofline.traffic")
+    ap.add_argument("--pmc-nq1", default=None, help="rocprofv3 PMC summary JSON of the nq = 1 scan (roofline.nq1)")
     ap.add_argument("--no-index", action="store_true", help="skip the index (configs[2]) leg")
     ap.add_argument("--no-configs", action="store_true", help="skip the configs[3] shard / configs[4] hybrid leg")
     ap.add_argument("--no-config1-points", action="store_true",
@@ -258,7 +259,7 @@ def cpu_baseline(O, args):
     }
 
 
-INDEX_PMC_DEFAULT = os.path.join(ROOT, "profiles", "r03", "index_pmc.json")
+INDEX_PMC_DEFAULT = os.path.join(ROOT, "profiles", "r04", "index_pmc.json")
 
 
 def index_points(mq, seg, mode, settings, args):
@@ -926,7 +927,7 @@ def main():
                 if "hbm_read_sweep" in result:
                     nq1["measured_peak_gbs"] = result["hbm_read_sweep"]["gbs"]
                     nq1["frac_measured_peak"] = round(p1["main_gbs"] / result["hbm_read_sweep"]["gbs"], 4)
-                pm = _pmc_kernel(os.path.join(ROOT, PMC_NQ1_DEFAULT), "k_scan_hi_reg", 1, sum_all=True)
+                pm = _pmc_kernel(args.pmc_nq1 or os.path.join(ROOT, PMC_NQ1_DEFAULT), "k_scan_hi_reg", 1, sum_all=True)
                 if pm:
                     nq1["pmc_hbm_bytes"] = round(pm["hbm_bytes_per_search"])
                     nq1["pmc_over_plane"] = round(pm["hbm_bytes_per_search"] / plane, 4)

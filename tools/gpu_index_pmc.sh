@@ -11,7 +11,7 @@ for spec in "$@"; do
     mode=${spec%%:*}; search=${spec#*:}
     rm -rf gpurun_out/pmc1 gpurun_out/pmc2 gpurun_out/pmc3
     bash tools/gpu_pmc.sh python tools/index_search_run.py --mode "$mode" --search "$search" --searches 2 || exit 1
-    python tools/pmc_traffic.py gpurun_out --searches 2 --nq 1000 --kernel k_ivf_scan \
+    python tools/pmc_traffic.py gpurun_out --searches 2 --last 2 --nq 1000 --kernel k_ivf_scan \
         --out "gpurun_out/index_pmc/mode$mode.json" > /dev/null || exit 1
     python - "$mode" "$search" <<'PY' || exit 1
 import json, sys

@@ -36,7 +36,8 @@ for step in $STEPS; do
         || { echo "risk failed"; tail -20 $O/blas_order_risk.log; exit 1; }
       grep -A4 per_block $O/blas_order_risk.json ;;
     bench)
-      timeout -k 10 900 python -u bench.py > $O/bench.json 2> $O/bench.err || { echo "bench failed rc=$?"; tail -30 $O/bench.err; exit 1; }
+      timeout -k 10 900 python -u bench.py --pmc $O/pmc_traffic.json --pmc-nq1 $O/pmc_nq1.json --index-pmc $O/index_pmc.json \
+        > $O/bench.json 2> $O/bench.err || { echo "bench failed rc=$?"; tail -30 $O/bench.err; exit 1; }
       head -c 3000 $O/bench.json; echo
       ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/prof" -o run --output-format csv \
           -- python "$GRAFT_REPO_ROOT/bench.py" --steps 3 --warmup 1 --no-cpu --no-verify --no-index --no-configs \

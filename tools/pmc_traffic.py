@@ -31,6 +31,9 @@ def main():
     ap.add_argument("--searches", type=int, required=True)
     ap.add_argument("--nq", type=int, default=None, help="batch size of the profiled searches")
     ap.add_argument("--kernel", default="k_scan_(?:hi|p4)")
+    ap.add_argument("--last", type=int, default=0,
+                    help="keep only the last N dispatches of each kernel per pass (drops e.g. an index "
+                         "build's own scans that precede the profiled searches)")
     ap.add_argument("--out", default=None)
     args = ap.parse_args()
     agg = collections.defaultdict(lambda: collections.defaultdict(float))
@@ -40,17 +43,29 @@ def main():
         p = os.path.join(args.root, tag, "run_counter_collection.csv")
         if not os.path.exists(p):
             continue
-        for r in load(p):
+        rows = load(p)
+        if args.last:
+            ids = collections.defaultdict(set)
+            for r in rows:
+                m = re.search(args.kernel + r"[_a-z]*(?:<([^>]*)>)?", r["Kernel_Name"])
+                if m:
+                    ids[m.group(0)].add(int(r["Dispatch_Id"]))
+            keep = {k: set(sorted(v)[-args.last:]) for k, v in ids.items()}
+        for r in rows:
             m = re.search(args.kernel + r"[_a-z]*(?:<([^>]*)>)?", r["Kernel_Name"])
             if not m:
                 continue
             key = m.group(0)
+            if args.last and int(r["Dispatch_Id"]) not in keep[key]:
+                continue
             agg[key][r["Counter_Name"]] += float(r["Counter_Value"])
             disp[key][tag].add(r["Dispatch_Id"])
             dur[(key, tag)][r["Dispatch_Id"]] = int(r["End_Timestamp"]) - int(r["Start_Timestamp"])
     out = {"source": "rocprofv3 --pmc (separate passes: SQ/GRBM, FETCH_SIZE, WRITE_SIZE+TCC)",
            "fetch_correction": "bytes = 2*FETCH_SIZE*1024 + WRITE_SIZE*1024 (gfx950)",
            "searches": args.searches, "nq": args.nq, "kernels": {}}
+    if args.last:
+        out["last_dispatches"] = args.last
     for key, c in agg.items():
         k = {}
         launches = max(len(v) for v in disp[key].values())
