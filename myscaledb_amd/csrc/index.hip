@@ -86,12 +86,21 @@ struct ListBufs {
 
 struct IndexWorkspace {
     hipEvent_t ev[6] = {};
+    // the cosine variant chain runs on `side` between fork and join (created
+    // on the workspace's device: index_workspace is called under its guard)
+    hipEvent_t fork = nullptr, join = nullptr;
+    hipStream_t side = nullptr;
+    int64_t *host = nullptr;  // pinned: the search's stats [4] and status word (one sync, no staging copies)
     DevBuf queries, qvars, qnorms, qmu, qlam, status, qhi, probes, cprobes, filter, exists, rows, out_ids, out_dist,
         ord, dmap, dwords, pdist, cqhi, gmax;
     ListBufs coarse, fine;
     void init() {
         if (ev[0]) return;
         for (auto &e : ev) MQVS_HIP(hipEventCreate(&e));
+        MQVS_HIP(hipEventCreateWithFlags(&fork, hipEventDisableTiming));
+        MQVS_HIP(hipEventCreateWithFlags(&join, hipEventDisableTiming));
+        MQVS_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
+        MQVS_HIP(hipHostMalloc((void **)&host, 8 * sizeof(int64_t), hipHostMallocDefault));
     }
 };
 
@@ -247,7 +256,7 @@ struct TmpBuf {
 
 static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int k, const char *params,
                               const uint8_t *filter, const uint8_t *exists, int64_t *out_ids, float *out_dist,
-                              uint32_t flags, hipStream_t user_stream, int formula_nq);
+                              uint32_t flags, hipStream_t user_stream, int formula_nq, int maxv_hint = 0);
 static mqvs_index *build_auto(mqvs_segment *seg, const char *index_type, const char *params);
 constexpr int64_t kAutoNlistMinRows = 1 << 20;  // smaller parts take the default list count
 
@@ -622,7 +631,9 @@ static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, c
     // a query's region is at most min(nprobe * longest list, every position)
     const int64_t cap = (int64_t)nq * std::min<int64_t>((int64_t)nprobe * max_list, npos);
     p.cand = (Cand *)b.cand.get(sizeof(Cand) * (size_t)std::max<int64_t>(cap, 1));
-    p.stats = (int64_t *)b.stats.get(sizeof(int64_t) * 8);
+    const int64_t plan_wgs = (nlist + 4095) / 4096;  // k_plan_lists_* workgroups (>= 4096 lists each)
+    p.stats = (int64_t *)b.stats.get(sizeof(int64_t) * (8 + 3 * plan_wgs));
+    p.bsum = p.stats + 8;
     if (dense)
         launch_ivf_plan_dense(p, npos, s);
     else
@@ -644,7 +655,7 @@ static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, c
 // distance formula (0: nq; query sub-batches keep the call's, see mqvs.hip)
 static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int k, const char *params,
                               const uint8_t *filter, const uint8_t *exists, int64_t *out_ids, float *out_dist,
-                              uint32_t flags, hipStream_t user_stream, int formula_nq) {
+                              uint32_t flags, hipStream_t user_stream, int formula_nq, int maxv_hint) {
     const int fnq = formula_nq > 0 ? formula_nq : nq;
     if (!ix) fail(MQVS_ERR_BAD_ARGUMENTS, "null index");
     if (nq < 0 || k < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "nq and k must be non-negative");
@@ -722,31 +733,36 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     }
 
     // ---- query prep: cosine re-normalisation variants (the re-rank uses the
-    // row's chunk variant, as mqvs_search does), |q|^2
-    // (a part with more chunks than kMaxVariants whose chains did not repeat
-    // gets one variant per chunk ordinal, as in mqvs_search: one host sync)
+    // row's chunk variant, as mqvs_search does), |q|^2.  The variant table
+    // starts at kMaxVariants per query with no host round trip; a chain that
+    // does not repeat within it on a part of more chunk ordinals (rare:
+    // small-integer data) is caught from the status word read at the end, and
+    // the search re-runs with the larger table (as mqvs_search does).  The
+    // table is not cleared: every variant a reader can select (ordinal < mu +
+    // lambda, or < maxv when the chain did not repeat) is written by the prep.
     const int64_t ords = seg->row_offset / seg->granule + (seg->n + seg->granule - 1) / seg->granule;
-    const bool may_sync = !(dev && (flags & MQVS_F_ASYNC)) && !first_stage;
-    int maxv = cos ? kMaxVariants : 1;
+    const int maxv = cos ? (maxv_hint > 0 ? maxv_hint : kMaxVariants) : 1;
     const int64_t qstride = rup(d, 32);
-    float *qvars = nullptr;
+    float *qvars = (float *)ws.qvars.get(sizeof(float) * (size_t)nq * maxv * qstride);
     float *qnorms = (float *)ws.qnorms.get(sizeof(float) * nq);
     int *qmu = (int *)ws.qmu.get(sizeof(int) * nq);
     int *qlam = (int *)ws.qlam.get(sizeof(int) * nq);
     int *status = (int *)ws.status.get(sizeof(int) * 4);
-    for (int pass = 0; pass < 2; ++pass) {
-        qvars = (float *)ws.qvars.get(sizeof(float) * (size_t)nq * maxv * qstride);
-        MQVS_HIP(hipMemsetAsync(qvars, 0, sizeof(float) * (size_t)nq * maxv * qstride, s));
-        MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
-        launch_query_prep(dq, nq, d, cos ? MQVS_METRIC_COSINE : MQVS_METRIC_L2, ix->metric == MQVS_METRIC_L2, qvars,
-                          maxv, qnorms, qmu, qlam, status, s);
+    MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
+    // Cosine: only variant 0 is needed before the exact re-rank (coarse step,
+    // list scan), so the rest of the chain -- a sequential fp32 sum per
+    // normalisation, up to kMaxVariants of them: 60-130 us at nq 1000 -- runs
+    // on the side stream meanwhile and is joined before the re-rank.
+    const bool split = cos && !first_stage;
+    launch_query_prep(dq, nq, d, cos ? MQVS_METRIC_COSINE : MQVS_METRIC_L2, ix->metric == MQVS_METRIC_L2, qvars, maxv,
+                      qnorms, qmu, qlam, status, s, split ? 1 : 0);
+    MQVS_HIP(hipGetLastError());
+    if (split) {
+        MQVS_HIP(hipEventRecord(ws.fork, s));
+        MQVS_HIP(hipStreamWaitEvent(ws.side, ws.fork, 0));
+        launch_query_prep(dq, nq, d, MQVS_METRIC_COSINE, false, qvars, maxv, qnorms, qmu, qlam, status, ws.side, 2);
         MQVS_HIP(hipGetLastError());
-        if (pass > 0 || !cos || ords <= maxv || !may_sync) break;
-        int hs = 0;
-        MQVS_HIP(hipMemcpyAsync(&hs, status, sizeof(int), hipMemcpyDeviceToHost, s));
-        MQVS_HIP(hipStreamSynchronize(s));
-        if (!hs) break;
-        maxv = (int)std::min<int64_t>(ords, kMaxVariantsCap);
+        MQVS_HIP(hipEventRecord(ws.join, ws.side));
     }
     uint16_t *qhi = (uint16_t *)ws.qhi.get(sizeof(uint16_t) * (size_t)nq * ix->dpad);
     launch_to_bf16(qvars, nq, d, (int64_t)maxv * qstride, qhi, ix->dpad, s);
@@ -829,7 +845,8 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
         int64_t *crow = (int64_t *)ws.rows.get(sizeof(int64_t) * (size_t)nq * R);
         list_pass(ws.fine, ix->plane, ix->perm, ix->pnorm, ix->list_off, ix->nlist, ix->npos, ix->max_list, ix->dpad,
                   ix->metric, qhi, qnorms, nq, probes, nprobe, dfilter, dexists, R, crow, 0, nullptr, ws.ev, s);
-        // ---- exact re-rank
+        // ---- exact re-rank (needs the whole variant chain)
+        if (split) MQVS_HIP(hipStreamWaitEvent(s, ws.join, 0));
         ScanParams rp{};
         rp.rows = seg->rows;
         rp.row_norms = seg->norms;
@@ -874,14 +891,22 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
         MQVS_HIP(hipGetLastError());
         return;
     }
-    int64_t hs[4] = {0, 0, 0, 0};
-    MQVS_HIP(hipMemcpyAsync(hs, dstats, sizeof(hs), hipMemcpyDeviceToHost, s));
-    int hstatus = 0;
-    MQVS_HIP(hipMemcpyAsync(&hstatus, status, sizeof(int), hipMemcpyDeviceToHost, s));
+    int64_t *hs = ws.host;
+    int *hst = reinterpret_cast<int *>(ws.host + 4);
+    MQVS_HIP(hipMemcpyAsync(hs, dstats, sizeof(int64_t) * 4, hipMemcpyDeviceToHost, s));
+    MQVS_HIP(hipMemcpyAsync(hst, status, sizeof(int), hipMemcpyDeviceToHost, s));
     MQVS_HIP(hipStreamSynchronize(s));
-    if (hstatus && !first_stage && ords > maxv)
+    const int hstatus = *hst;
+    if (hstatus && !first_stage && ords > maxv) {
+        const int want = (int)std::min<int64_t>(ords, kMaxVariantsCap);
+        if (maxv < want) {
+            search_index_impl(ix, queries, nq, k, params, filter, exists, out_ids, out_dist, flags, user_stream, fnq,
+                              want);
+            return;
+        }
         fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not repeat within " + std::to_string(maxv) +
                                    " steps on a part of more chunks");
+    }
     if (!dev) {
         if (ix->row_ids_map) launch_map_ids(dids, (int64_t)nq * k, ix->row_ids_map, s);
         MQVS_HIP(hipMemcpyAsync(out_ids, dids, sizeof(int64_t) * (size_t)nq * k, hipMemcpyDeviceToHost, s));

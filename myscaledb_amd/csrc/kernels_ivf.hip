@@ -85,16 +85,21 @@ __global__ __launch_bounds__(256) void k_plan_count(IvfParams p) {
     }
 }
 
-// nlist <= 16 x kPlanThreads: wave w owns lists [w S, (w + 1) S) (S a
-// multiple of 64) and walks them 64 at a time, lane l on list w S + 64 s + l,
-// so every load is coalesced; the (pair count, length) of its <= 16 steps stay
-// in registers.  The three prefix sums (pairs, work items, streamed rows) are
-// wave scans with a carry, then one combine over the 16 wave totals.
+// Workgroup b owns lists [b 16 kPlanThreads, (b + 1) 16 kPlanThreads): wave
+// w of it owns S of them (S a multiple of 64) and walks them 64 at a time,
+// lane l on list w S + 64 s + l, so every load is coalesced; the (pair count,
+// length) of its <= 16 steps stay in registers.  The three prefix sums (pairs,
+// work items, streamed rows) are wave scans with a carry, then one combine
+// over the 16 wave totals and, with more than one workgroup, the totals of the
+// workgroups before (bsum, written by the SUMS pass of the same kernel).
+// (One workgroup walking 39063 lists took 0.074 ms; three take ~0.01.)
+template <bool SUMS>
 __global__ __launch_bounds__(kPlanThreads) void k_plan_lists_reg(IvfParams p) {
     constexpr int ST = 16;
     constexpr int NWV = kPlanThreads / 64;
     __shared__ int64_t sh[3][NWV];
-    const int L = p.nlist;
+    const int base = blockIdx.x * ST * kPlanThreads;
+    const int L = min(p.nlist - base, ST * kPlanThreads);
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int S = ((L + NWV - 1) / NWV + 63) / 64 * 64;
     const int qs = p.qg == 64 ? 6 : p.qg == 32 ? 5 : 4;  // qg is 16, 32 or 64
@@ -103,8 +108,8 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_lists_reg(IvfParams p) {
     for (int u = 0; u < ST; ++u) {
         const int i = wv * S + 64 * u + lane;
         const bool in = 64 * u < S && i < L;
-        cnt[u] = in ? p.lcount[i] : 0;
-        len[u] = in ? (int)(p.list_off[i + 1] - p.list_off[i]) : 0;
+        cnt[u] = in ? p.lcount[base + i] : 0;
+        len[u] = in ? (int)(p.list_off[base + i + 1] - p.list_off[base + i]) : 0;
     }
     auto items_of = [&](int u) { return (int64_t)((cnt[u] + p.qg - 1) >> qs) * ((len[u] + kIvfChunk - 1) / kIvfChunk); };
     auto rows_of = [&](int u) { return (int64_t)((cnt[u] + p.qg - 1) >> qs) * len[u]; };
@@ -126,6 +131,14 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_lists_reg(IvfParams p) {
         sh[2][wv] = w2;
     }
     __syncthreads();
+    if (SUMS) {
+        if (t < 3) {
+            int64_t v = 0;
+            for (int w = 0; w < NWV; ++w) v += sh[t][w];
+            p.bsum[3 * blockIdx.x + t] = v;
+        }
+        return;
+    }
     int64_t c0 = 0, c1 = 0, t1 = 0, t2 = 0;
     for (int w = 0; w < NWV; ++w) {
         if (w < wv) {
@@ -134,6 +147,17 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_lists_reg(IvfParams p) {
         }
         t1 += sh[1][w];
         t2 += sh[2][w];
+    }
+    if (gridDim.x > 1) {
+        t1 = t2 = 0;
+        for (int b = 0; b < (int)gridDim.x; ++b) {
+            if (b < (int)blockIdx.x) {
+                c0 += p.bsum[3 * b];
+                c1 += p.bsum[3 * b + 1];
+            }
+            t1 += p.bsum[3 * b + 1];
+            t2 += p.bsum[3 * b + 2];
+        }
     }
 #pragma unroll
     for (int u = 0; u < ST; ++u) {
@@ -149,13 +173,14 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_lists_reg(IvfParams p) {
         }
         const int i = wv * S + 64 * u + lane;
         if (i < L) {
-            p.lstart[i] = c0 + i0 - v0;
+            p.lstart[base + i] = c0 + i0 - v0;
+            p.lfill[base + i] = 0;  // the scatter's cursors (no memset of their own)
             int64_t r1 = c1 + i1 - v1;
             const int g = (cnt[u] + p.qg - 1) >> qs;
             const int nc = (len[u] + kIvfChunk - 1) / kIvfChunk;
             for (int j = 0; j < g; ++j)
                 for (int cc = 0; cc < nc; ++cc) {
-                    p.item_list[r1] = i;
+                    p.item_list[r1] = base + i;
                     p.item_grp[r1] = j;
                     p.item_chk[r1] = cc;
                     ++r1;
@@ -164,7 +189,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_lists_reg(IvfParams p) {
         c0 += __shfl(i0, 63);
         c1 += __shfl(i1, 63);
     }
-    if (t == 0) {
+    if (t == 0 && blockIdx.x == 0) {
         *p.nitems = (int)t1;
         p.stats[1] = t1;
         p.stats[2] = t2 * p.dpad * 2;
@@ -172,11 +197,114 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_lists_reg(IvfParams p) {
     }
 }
 
-// nlist > 16 x kPlanThreads: the same wave-strided layout (lane l of wave w
-// on list w S + 64 s + l: coalesced loads) with the per-list values loaded
-// again in the second pass instead of kept in registers.  (A contiguous run of
-// lists per thread made every load of a wave touch 64 different lines:
-// 0.27 ms of plan at 39063 lists against 0.05 at 10000.)
+// Workgroup b owns kPlanBlk lists: their (pair count, length) are staged in
+// LDS by coalesced loads, then thread t walks lists [kPlanPer t, kPlanPer (t +
+// 1)) sequentially, so the block does one wave scan per prefix sum instead of
+// one per 64 lists (the register walk above: 35 us for 39063 lists in 3
+// workgroups).  Multi-workgroup carries as above (bsum, SUMS pass).
+constexpr int kPlanPer = 4;
+constexpr int kPlanBlk = kPlanPer * kPlanThreads;
+
+__device__ __forceinline__ int64_t wave_incl_scan(int64_t v) {
+    const int lane = threadIdx.x & 63;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(v, o);
+        if (lane >= o) v += y;
+    }
+    return v;
+}
+
+template <bool SUMS>
+__global__ __launch_bounds__(kPlanThreads) void k_plan_lists_blk(IvfParams p) {
+    constexpr int NWV = kPlanThreads / 64;
+    __shared__ int s_cnt[kPlanBlk], s_len[kPlanBlk];
+    __shared__ int64_t sh[3][NWV];
+    const int base = blockIdx.x * kPlanBlk;
+    const int L = min(p.nlist - base, kPlanBlk);
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int qs = p.qg == 64 ? 6 : p.qg == 32 ? 5 : 4;  // qg is 16, 32 or 64
+    for (int i = t; i < kPlanBlk; i += kPlanThreads) {
+        const bool in = i < L;
+        s_cnt[i] = in ? p.lcount[base + i] : 0;
+        s_len[i] = in ? (int)(p.list_off[base + i + 1] - p.list_off[base + i]) : 0;
+    }
+    __syncthreads();
+    int64_t a0 = 0, a1 = 0, a2 = 0;
+#pragma unroll
+    for (int r = 0; r < kPlanPer; ++r) {
+        const int c = s_cnt[kPlanPer * t + r], l = s_len[kPlanPer * t + r];
+        const int64_t g = (c + p.qg - 1) >> qs;
+        a0 += c;
+        a1 += g * ((l + kIvfChunk - 1) / kIvfChunk);
+        a2 += g * l;
+    }
+    const int64_t i0 = wave_incl_scan(a0), i1 = wave_incl_scan(a1), i2 = wave_incl_scan(a2);
+    if (lane == 63) {
+        sh[0][wv] = i0;
+        sh[1][wv] = i1;
+        sh[2][wv] = i2;
+    }
+    __syncthreads();
+    if (SUMS) {
+        if (t < 3) {
+            int64_t v = 0;
+            for (int w = 0; w < NWV; ++w) v += sh[t][w];
+            p.bsum[3 * blockIdx.x + t] = v;
+        }
+        return;
+    }
+    int64_t c0 = i0 - a0, c1 = i1 - a1, t1 = 0, t2 = 0;
+    for (int w = 0; w < NWV; ++w) {
+        if (w < wv) {
+            c0 += sh[0][w];
+            c1 += sh[1][w];
+        }
+        t1 += sh[1][w];
+        t2 += sh[2][w];
+    }
+    if (gridDim.x > 1) {
+        t1 = t2 = 0;
+        for (int b = 0; b < (int)gridDim.x; ++b) {
+            if (b < (int)blockIdx.x) {
+                c0 += p.bsum[3 * b];
+                c1 += p.bsum[3 * b + 1];
+            }
+            t1 += p.bsum[3 * b + 1];
+            t2 += p.bsum[3 * b + 2];
+        }
+    }
+#pragma unroll
+    for (int r = 0; r < kPlanPer; ++r) {
+        const int li = kPlanPer * t + r;
+        if (li >= L) break;
+        const int c = s_cnt[li], l = s_len[li];
+        const int g = (c + p.qg - 1) >> qs;
+        const int nc = (l + kIvfChunk - 1) / kIvfChunk;
+        p.lstart[base + li] = c0;
+        p.lfill[base + li] = 0;  // the scatter's cursors (no memset of their own)
+        for (int j = 0; j < g; ++j)
+            for (int cc = 0; cc < nc; ++cc) {
+                p.item_list[c1] = base + li;
+                p.item_grp[c1] = j;
+                p.item_chk[c1] = cc;
+                ++c1;
+            }
+        c0 += c;
+    }
+    if (t == 0 && blockIdx.x == 0) {
+        *p.nitems = (int)t1;
+        p.stats[1] = t1;
+        p.stats[2] = t2 * p.dpad * 2;
+        p.stats[3] = (int64_t)p.nq * p.nprobe;
+    }
+}
+
+// One workgroup for any nlist: the same wave-strided layout with the per-list
+// values loaded again in the second pass instead of kept in registers.  Kept
+// for A/B (MQVS_IVF_PLAN=1, measurement build); the default is
+// k_plan_lists_blk above.  (A contiguous run of lists per
+// thread made every load of a wave touch 64 different lines: 0.27 ms of plan
+// at 39063 lists against 0.05 at 10000.)
 __global__ __launch_bounds__(kPlanThreads) void k_plan_lists(IvfParams p) {
     constexpr int NWV = kPlanThreads / 64;
     __shared__ int64_t sh[3][NWV];
@@ -238,6 +366,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_lists(IvfParams p) {
         const int i = wv * S + 64 * u + lane;
         if (i < L) {
             p.lstart[i] = c0 + i0 - v0;
+            p.lfill[i] = 0;
             int64_t r1 = c1 + i1 - v1;
             const int g = (cnt + p.qg - 1) >> qs;
             const int nc = (len + kIvfChunk - 1) / kIvfChunk;
@@ -750,15 +879,22 @@ void launch_iota_probes(int64_t *probes, int nq, int np, hipStream_t s) {
 }
 
 void launch_ivf_plan(const IvfParams &p, hipStream_t s) {
-    MQVS_HIP(hipMemsetAsync(p.lcount, 0, sizeof(int) * p.nlist, s));
-    MQVS_HIP(hipMemsetAsync(p.lfill, 0, sizeof(int) * p.nlist, s));
+    MQVS_HIP(hipMemsetAsync(p.lcount, 0, sizeof(int) * p.nlist, s));  // (lfill: zeroed by the list pass)
     const int64_t E = (int64_t)p.nq * p.nprobe;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((std::max(E, (int64_t)p.nq) + 255) / 256, 2048));
     hipLaunchKernelGGL(k_plan_count, dim3(grid), dim3(256), 0, s, p);
-    if (p.nlist <= 16 * kPlanThreads)
-        hipLaunchKernelGGL(k_plan_lists_reg, dim3(1), dim3(kPlanThreads), 0, s, p);
-    else
+    const int plan = tune_int("MQVS_IVF_PLAN", 0);  // A/B (measurement build): 1 one workgroup, 2 register walk
+    if (plan == 1) {
         hipLaunchKernelGGL(k_plan_lists, dim3(1), dim3(kPlanThreads), 0, s, p);
+    } else if (plan == 2) {
+        const int nb = (p.nlist + 16 * kPlanThreads - 1) / (16 * kPlanThreads);
+        if (nb > 1) hipLaunchKernelGGL(k_plan_lists_reg<true>, dim3(nb), dim3(kPlanThreads), 0, s, p);
+        hipLaunchKernelGGL(k_plan_lists_reg<false>, dim3(std::max(nb, 1)), dim3(kPlanThreads), 0, s, p);
+    } else {
+        const int nb = (p.nlist + kPlanBlk - 1) / kPlanBlk;
+        if (nb > 1) hipLaunchKernelGGL(k_plan_lists_blk<true>, dim3(nb), dim3(kPlanThreads), 0, s, p);
+        hipLaunchKernelGGL(k_plan_lists_blk<false>, dim3(std::max(nb, 1)), dim3(kPlanThreads), 0, s, p);
+    }
     hipLaunchKernelGGL(k_plan_scatter, dim3(grid), dim3(256), 0, s, p);
     hipLaunchKernelGGL(k_plan_queries, dim3(1), dim3(kPlanThreads), 0, s, p);
 }
@@ -876,8 +1012,17 @@ void launch_centroid_mean(const float *rows, int d, const int32_t *order, const 
 // them (a group outside holds nothing better than the T-th group maximum) --
 // then the exact fp32 value of each centroid of those groups and the nprobe
 // best.  One workgroup per query; T <= kCoarsePickMaxT.
+//
+// The group keys are staged in LDS once (up to kPickStage groups: 131072
+// lists), so the four radix passes read LDS, not L2.  The exact values are
+// computed a wave per kPickU centroids with float4 loads (kPickU x d/256
+// independent 16-B loads per lane in flight; the pick is latency-bound, not
+// bandwidth-bound: 48-160 centroids x 3 KB per query).  The nprobe best are
+// placed by rank counting (M <= 256) or the LDS bitonic sort.
+constexpr int kPickStage = 8192;
+constexpr int kPickU = 4;
 
-template <int METRIC>  // MQVS_METRIC_L2 or kMetricIpRaw (the coarse metric)
+template <int METRIC, bool STAGED>  // METRIC: MQVS_METRIC_L2 or kMetricIpRaw (the coarse metric)
 __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T,
                                                              int nprobe, const float *q, int64_t qld,
                                                              const float *cent, const float *cnorm, int64_t ncent,
@@ -885,13 +1030,26 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh[4];
     __shared__ int s_grp[kCoarsePickMaxT];
-    __shared__ int s_ng;
-    __shared__ uint4 recs[16 * kCoarsePickMaxT];
+    __shared__ int s_ng, s_valid;
+    // dynamic LDS: recs [pow2 >= 16 T] then (STAGED) keys [ngroups], sized per
+    // launch so small pickups keep many workgroups per CU
+    extern __shared__ uint4 dyn[];
+    uint4 *recs = dyn;
+    int NR = 1;
+    while (NR < 16 * T) NR <<= 1;
+    uint32_t *keys = reinterpret_cast<uint32_t *>(dyn + NR);
     const int qi = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const float *row = gmax + (int64_t)qi * gld;
-    auto keyof = [&](int64_t i) { return okey<METRIC>(row[i]); };
-    const uint32_t th = block_radix_select(keyof, ngroups, T, hist, sh);
-    if (t == 0) s_ng = 0;
+    if (STAGED) {
+        for_each_f4(row, ngroups, [&](int64_t i, float v) { keys[i] = okey<METRIC>(v); });
+        __syncthreads();
+    }
+    auto keyof = [&](int64_t i) { return STAGED ? keys[i] : okey<METRIC>(row[i]); };
+    const uint32_t th = block_radix_select_mlp(keyof, ngroups, T, hist, sh);
+    if (t == 0) {
+        s_ng = 0;
+        s_valid = 0;
+    }
     __syncthreads();
     // the groups strictly better than the T-th, then its ties up to T
     for (int pass = 0; pass < 2; ++pass) {
@@ -906,26 +1064,83 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
         __syncthreads();
     }
     const int ng = min(s_ng, T);
-    // exact values of the groups' centroids: one wave per centroid at a time,
-    // lanes over the columns
-    const float *qv = q + (int64_t)qi * qld;
     const int M = 16 * ng;
-    for (int c = wv; c < M; c += SEL_THREADS / 64) {
-        const int64_t r = (int64_t)s_grp[c >> 4] * 16 + (c & 15);
-        float dot = 0.f;
-        if (r < ncent) {
-            const float *y = cent + r * d;
-            for (int e = lane; e < d; e += 64) dot = fmaf(qv[e], y[e], dot);
+    // exact values: wave wv scores centroids c0 .. c0 + kPickU - 1, lanes over
+    // float4 columns (scalar columns when d or the rows are not 16-B aligned)
+    const float *qv = q + (int64_t)qi * qld;
+    const bool v4 = (d & 3) == 0 && (((uintptr_t)cent | (uintptr_t)qv) & 15) == 0;
+    for (int c0 = wv * kPickU; c0 < M; c0 += (SEL_THREADS / 64) * kPickU) {
+        int64_t r[kPickU];
+        float dot[kPickU];
+#pragma unroll
+        for (int u = 0; u < kPickU; ++u) {
+            const int c = c0 + u;
+            r[u] = c < M ? (int64_t)s_grp[c >> 4] * 16 + (c & 15) : ncent;
+            if (r[u] >= ncent) r[u] = -1;
+            dot[u] = 0.f;
         }
-        for (int off = 32; off > 0; off >>= 1) dot += __shfl_xor(dot, off);
-        if (lane == 0) {
-            uint32_t key = 0xFFFFFFFFu;
-            if (r < ncent) {
-                const float v = METRIC == MQVS_METRIC_L2 ? cnorm[r] - 2.0f * dot : dot;
-                key = okey<METRIC>(v);
+        if (v4) {
+            const float4 *q4 = reinterpret_cast<const float4 *>(qv);
+            for (int j = lane; j < (d >> 2); j += 64) {
+                const float4 x = q4[j];
+                float4 y[kPickU];
+#pragma unroll
+                for (int u = 0; u < kPickU; ++u)
+                    y[u] = r[u] >= 0 ? reinterpret_cast<const float4 *>(cent + r[u] * d)[j] : float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                for (int u = 0; u < kPickU; ++u) {
+                    dot[u] = fmaf(x.x, y[u].x, dot[u]);
+                    dot[u] = fmaf(x.y, y[u].y, dot[u]);
+                    dot[u] = fmaf(x.z, y[u].z, dot[u]);
+                    dot[u] = fmaf(x.w, y[u].w, dot[u]);
+                }
             }
-            recs[c] = uint4{key, (uint32_t)(r < ncent ? r : 0xFFFFFFFFu), 0u, 0u};
+        } else {
+            for (int e = lane; e < d; e += 64) {
+                const float x = qv[e];
+#pragma unroll
+                for (int u = 0; u < kPickU; ++u)
+                    if (r[u] >= 0) dot[u] = fmaf(x, cent[r[u] * d + e], dot[u]);
+            }
         }
+#pragma unroll
+        for (int u = 0; u < kPickU; ++u) {
+            float v = dot[u];
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            dot[u] = v;
+        }
+        if (lane < kPickU) {
+            float dv = dot[0];
+            int64_t rv = r[0];
+#pragma unroll
+            for (int u = 1; u < kPickU; ++u)
+                if (lane == u) {
+                    dv = dot[u];
+                    rv = r[u];
+                }
+            const int c = c0 + lane;
+            if (c < M) {
+                uint32_t key = 0xFFFFFFFFu;
+                if (rv >= 0) key = okey<METRIC>(METRIC == MQVS_METRIC_L2 ? cnorm[rv] - 2.0f * dv : dv);
+                recs[c] = uint4{key, (uint32_t)(rv >= 0 ? rv : 0xFFFFFFFFu), 0u, 0u};
+                if (key != 0xFFFFFFFFu) atomicAdd(&s_valid, 1);
+            }
+        }
+    }
+    __syncthreads();
+    const int nvalid = s_valid;
+    if (M <= 256) {
+        // rank counting: valid records are unique (key, centroid), so each
+        // lands on its own rank; the invalid ones are not placed
+        for (int c = t; c < M; c += SEL_THREADS) {
+            const uint4 e = recs[c];
+            if (e.x == 0xFFFFFFFFu) continue;
+            int rank = 0;
+            for (int o = 0; o < M; ++o) rank += rec_less(recs[o], e) ? 1 : 0;
+            if (rank < nprobe) probes[(int64_t)qi * nprobe + rank] = (int64_t)e.y;
+        }
+        for (int j = nvalid + t; j < nprobe; j += SEL_THREADS) probes[(int64_t)qi * nprobe + j] = -1;
+        return;
     }
     int N = 1;
     while (N < M) N <<= 1;
@@ -942,12 +1157,19 @@ void launch_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T, 
                         const float *q, int64_t qld, const float *cent, const float *cnorm, int64_t ncent, int d,
                         int nq, int64_t *probes, hipStream_t s) {
     if (nq <= 0) return;
-    if (metric == MQVS_METRIC_L2)
-        hipLaunchKernelGGL(k_coarse_pick<MQVS_METRIC_L2>, dim3(nq), dim3(SEL_THREADS), 0, s, gmax, gld, ngroups, T,
-                           nprobe, q, qld, cent, cnorm, ncent, d, probes);
-    else
-        hipLaunchKernelGGL(k_coarse_pick<kMetricIpRaw>, dim3(nq), dim3(SEL_THREADS), 0, s, gmax, gld, ngroups, T,
-                           nprobe, q, qld, cent, cnorm, ncent, d, probes);
+#define MQVS_PICK(M, ST)                                                                                             \
+    hipLaunchKernelGGL((k_coarse_pick<M, ST>), dim3(nq), dim3(SEL_THREADS), lds, s, gmax, gld, ngroups, T, nprobe, q, \
+                       qld, cent, cnorm, ncent, d, probes)
+    const bool staged = ngroups <= kPickStage;
+    size_t nr = 1;
+    while (nr < (size_t)16 * T) nr <<= 1;
+    const size_t lds = nr * sizeof(uint4) + (staged ? sizeof(uint32_t) * (size_t)ngroups : 0);
+    if (metric == MQVS_METRIC_L2) {
+        if (staged) MQVS_PICK(MQVS_METRIC_L2, true); else MQVS_PICK(MQVS_METRIC_L2, false);
+    } else {
+        if (staged) MQVS_PICK(kMetricIpRaw, true); else MQVS_PICK(kMetricIpRaw, false);
+    }
+#undef MQVS_PICK
 }
 
 }  // namespace mqvs

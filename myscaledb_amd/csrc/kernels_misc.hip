@@ -122,10 +122,16 @@ __device__ __forceinline__ float seq_sq_sum(const float (&x)[J], int d) {
     return acc;
 }
 
-// J > 0: d <= 64 J, the query in registers
+// J > 0: d <= 64 J, the query in registers.
+// phase 0: everything.  Cosine searches whose first consumers need only
+// variant 0 split the work: phase 1 writes variant 0 (and |q|^2 = 0); phase 2,
+// launched after it (on a side stream, concurrent with the coarse step and the
+// list scan), walks the rest of the chain -- it compares against the stored
+// variant 0 but does not rewrite it -- and writes mu, lambda and the status.
 template <int J>
 __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d, int metric, int blas, float *qvars,
-                                                   int maxv, float *qnorms, int *qmu, int *qlam, int *status) {
+                                                   int maxv, float *qnorms, int *qmu, int *qlam, int *status,
+                                                   int phase) {
     const int j = blockIdx.x;
     const int lane = threadIdx.x;
     const int64_t qs = (int64_t)((d + 31) / 32 * 32);
@@ -138,6 +144,7 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
         x[u] = i < d ? src[i] : 0.0f;
     }
     if (metric != MQVS_METRIC_COSINE) {
+        if (phase == 2) return;
 #pragma unroll
         for (int u = 0; u < J; ++u)
             if (lane + 64 * u < d) v0[lane + 64 * u] = x[u];
@@ -162,11 +169,15 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
 #pragma unroll
             for (int u = 0; u < J; ++u) x[u] = x[u] / sr;
         }
-        if (v < maxv) {
+        if (v < maxv && (phase != 2 || v > 0)) {
             float *cur = v0 + (int64_t)v * qs;
 #pragma unroll
             for (int u = 0; u < J; ++u)
                 if (lane + 64 * u < d) cur[lane + 64 * u] = x[u];
+        }
+        if (phase == 1) {
+            if (lane == 0 && qnorms) qnorms[j] = 0.0f;
+            return;
         }
         uint64_t h = 0;
 #pragma unroll
@@ -207,9 +218,11 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
 }
 
 // generic d: elements in LDS, lane 0 walks the sequential sums
+// (phase 1 does everything here, phase 2 nothing)
 __global__ __launch_bounds__(64) void k_query_prep_lds(const float *q, int nq, int d, int metric, int blas,
                                                        float *qvars, int maxv, float *qnorms, int *qmu, int *qlam,
-                                                       int *status) {
+                                                       int *status, int phase) {
+    if (phase == 2) return;
     extern __shared__ __attribute__((aligned(16))) float qbuf[];
     const int j = blockIdx.x;
     const int lane = threadIdx.x;
@@ -280,13 +293,13 @@ __global__ __launch_bounds__(64) void k_query_prep_lds(const float *q, int nq, i
 }
 
 void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, float *qvars, int maxv,
-                       float *qnorms, int *qmu, int *qlam, int *status, hipStream_t s) {
+                       float *qnorms, int *qmu, int *qlam, int *status, hipStream_t s, int phase) {
     if (metric != MQVS_METRIC_COSINE) maxv = 1;
     const size_t lds = (size_t)((d + 31) / 32 * 32 + 4) * sizeof(float);
     const size_t sig = (size_t)(maxv + 1) * sizeof(uint64_t);
 #define MQVS_QP(J)                                                                                               \
     hipLaunchKernelGGL(k_query_prep<J>, dim3(nq), dim3(64), sig, s, q, nq, d, metric, blas ? 1 : 0, qvars, maxv, \
-                       qnorms, qmu, qlam, status)
+                       qnorms, qmu, qlam, status, phase)
     if (d <= 128)
         MQVS_QP(2);
     else if (d <= 256)
@@ -301,7 +314,7 @@ void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, flo
         MQVS_QP(24);
     else
         hipLaunchKernelGGL(k_query_prep_lds, dim3(nq), dim3(64), lds, s, q, nq, d, metric, blas ? 1 : 0, qvars, maxv,
-                           qnorms, qmu, qlam, status);
+                           qnorms, qmu, qlam, status, phase);
 #undef MQVS_QP
 }
 

@@ -306,8 +306,9 @@ void launch_merge_shards(int nshards, int nq, int k, int metric, const int64_t *
 void launch_normalize_rows(float *rows, int64_t n, int d, hipStream_t s);
 void launch_row_norms(const float *rows, int64_t n, int d, float *norms, hipStream_t s);
 // maxv: variants stored per query (1 unless cosine)
+// phase: 0 everything; 1 variant 0 only; 2 the rest of the chain (after 1)
 void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, float *qvars, int maxv,
-                       float *qnorms, int *qmu, int *qlam, int *status, hipStream_t s);
+                       float *qnorms, int *qmu, int *qlam, int *status, hipStream_t s, int phase = 0);
 void launch_generate(uint64_t seed, int mode, int64_t row0, int64_t n, int d, float *out,
                      hipStream_t s);
 void launch_pack_nonempty(const uint8_t *bytes, int64_t n, uint8_t *bits, hipStream_t s);
@@ -417,6 +418,7 @@ struct IvfParams {
     int64_t *qstart;          // [nq+1] start of each query's region
     Cand *cand;               // approximate values, one per (pair, list position)
     int64_t *stats;           // [4] values written, items, plane bytes, pairs
+    int64_t *bsum;            // [3 * plan workgroups] per-workgroup list totals (k_plan_lists_reg)
 };
 
 void launch_ivf_plan(const IvfParams &p, hipStream_t s);
