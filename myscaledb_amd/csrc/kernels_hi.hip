@@ -14,8 +14,10 @@
 // a bf16 + fp6-MX split; both streamed more bytes per element for the same
 // survivors and were removed in round 3.)
 //
-// Planes are row-blocked (16 vectors x 32 columns = 1 KiB contiguous):
-// vector u, stage s at byte ((u >> 4) nst + s) 1024 + (u & 15) 64.
+// Planes are row-blocked in groups of 16 vectors (mqvs_internal.h,
+// kPlaneSlab): vector u, stage s (32 columns) at byte (u >> 4) nst 1024 +
+// plane_step_off(s) + plane_vec_off(u & 15); a stage's 16-vector piece is
+// 1 KiB contiguous (kPlaneSlab 32).
 //
 // Scan pipeline: a ring of NBUF LDS stages (stage = 32 columns of the 256-row
 // tile and of the QT-query tile, filled by global_load_lds_dwordx4 in 1 KiB
@@ -63,14 +65,14 @@ __global__ __launch_bounds__(256) void k_to_hi(const float *src, int64_t rows, i
     for (int64_t v = (int64_t)blockIdx.x * 4 + w; v < rows; v += (int64_t)gridDim.x * 4) {
         const float *x = src + v * sstride;
         const int64_t u = (v % vgroup) * vpad + v / vgroup;
-        uint16_t *hu = hi + (u >> 4) * nb * 512 + (u & 15) * 32;
+        uint16_t *hu = hi + (u >> 4) * nb * 512 + plane_vec_off((uint32_t)(u & 15)) / 2;
         double nx = 0, nh = 0, nr = 0;
         for (int64_t i = lane; i < dpad; i += 64) {
             const float xv = i < d ? x[i] : 0.f;
             const uint16_t hb = f32_to_bf16_rn(xv);
             const float hv = __builtin_bit_cast(float, (uint32_t)hb << 16);
             const float rv = xv - hv;  // exact
-            hu[(i >> 5) * 512 + (i & 31)] = hb;
+            hu[plane_step_off((uint32_t)(i >> 5)) / 2 + (i & 31)] = hb;
             nx += (double)xv * xv;
             nh += (double)hv * hv;
             nr += (double)rv * rv;
@@ -251,7 +253,8 @@ __global__ __launch_bounds__(256 * WQ) void k_scan_hi(ScanParams p) {
             u = (int64_t)variant_of(p, j, ord) * p.q_vpad + j;
             plane = p.q_hi;
         }
-        src[i] = reinterpret_cast<const unsigned char *>(plane) + ((u >> 4) * nb * 1024 + (u & 15) * 64 + c * 16);
+        src[i] = reinterpret_cast<const unsigned char *>(plane) +
+                 ((u >> 4) * nb * 1024 + plane_vec_off((uint32_t)(u & 15)) + c * 16);
     }
     static_assert(GY % NW == 0, "row pieces: whole rounds of the waves");
     constexpr int YPW = GY / NW;  // pieces i < YPW are row pieces, the rest query pieces
@@ -261,7 +264,7 @@ __global__ __launch_bounds__(256 * WQ) void k_scan_hi(ScanParams p) {
         for (int i = 0; i < GPW; ++i) {
             if ((DIAG & 8) && i < YPW) continue;
             if ((DIAG & 4) && i >= YPW) continue;
-            __builtin_amdgcn_global_load_lds((const void *)(src[i] + (int64_t)s * 1024),
+            __builtin_amdgcn_global_load_lds((const void *)(src[i] + plane_step_off((uint32_t)s)),
                                              (lds_void *)(dst + (w + i * NW) * 1024), 16, 0, 0);
         }
     };
@@ -416,22 +419,23 @@ __global__ __launch_bounds__(256) void k_scan_hi_reg(ScanParams p) {
         if (j >= p.nq) j = 0;
         const int64_t u = (int64_t)variant_of(p, j, ord) * p.q_vpad + j;
         const unsigned char *qs = reinterpret_cast<const unsigned char *>(p.q_hi) + (u >> 4) * nb * 1024 +
-                                  (u & 15) * 64 + c * 16;
+                                  plane_vec_off((uint32_t)(u & 15)) + c * 16;
 #pragma unroll
-        for (int s = 0; s < NST; ++s) qf[jb][s] = *reinterpret_cast<const bf16x4x2 *>(qs + (int64_t)s * 1024);
+        for (int s = 0; s < NST; ++s) qf[jb][s] = *reinterpret_cast<const bf16x4x2 *>(qs + plane_step_off(s));
     }
     auto rowsrc = [&](int rb) {
         const int64_t gp = r0 + 16 * rb + l16;
         int64_t u = gp < r1 ? row_at(p, gp) : -1;
         if (u < 0) u = row_at(p, r0);  // padding: any real row, results discarded
-        return reinterpret_cast<const unsigned char *>(p.rows_hi) + (u >> 4) * nb * 1024 + (u & 15) * 64 + c * 16;
+        return reinterpret_cast<const unsigned char *>(p.rows_hi) + (u >> 4) * nb * 1024 +
+               plane_vec_off((uint32_t)(u & 15)) + c * 16;
     };
     bf16x4x2 a[2][NST];
     auto load = [&](int buf, int rb) {
         const unsigned char *src = rowsrc(rb);
 #pragma unroll
         for (int s = 0; s < NST; ++s) {
-            const bf16x4x2 *ps = reinterpret_cast<const bf16x4x2 *>(src + (int64_t)s * 1024);
+            const bf16x4x2 *ps = reinterpret_cast<const bf16x4x2 *>(src + plane_step_off(s));
             if constexpr (NT) {
                 // streaming rows (read once per search): non-temporal loads
                 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));

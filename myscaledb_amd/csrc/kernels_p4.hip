@@ -302,7 +302,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
     auto set_src = [&]() __attribute__((always_inline)) {
         int ln = lane;
         asm volatile("" : "+v"(ln));
-        const uint32_t lc = (uint32_t)(ln >> 2) * 64u + (uint32_t)((ln & 3) ^ p4_g((ln >> 4) & 3)) * 16u;
+        const uint32_t lc = plane_vec_off((uint32_t)(ln >> 2)) + (uint32_t)((ln & 3) ^ p4_g((ln >> 4) & 3)) * 16u;
         rbase = reinterpret_cast<const unsigned char *>(p.rows_hi) + (uint64_t)(uint32_t)(ir0 >> 4) * blk;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -324,7 +324,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
                     var = iord < mu ? iord : mu + (iord - mu) % lam;
                 }
                 const uint32_t u = (uint32_t)var * (uint32_t)p.q_vpad + (uint32_t)j;
-                qoff[i] = (u >> 4) * blk + (u & 15) * 64u + (uint32_t)((ln & 3) ^ p4_g((ln >> 4) & 3)) * 16u;
+                qoff[i] = (u >> 4) * blk + plane_vec_off(u & 15) + (uint32_t)((ln & 3) ^ p4_g((ln >> 4) & 3)) * 16u;
             }
         }
         if constexpr (L2) {
@@ -349,12 +349,12 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
         if ((DIAG & 4) && x >= 4 && x < 8) return;
         unsigned char *dst = lds + ibuf * kP4Stage;
         if (x < 4) {
-            __builtin_amdgcn_global_load_lds((const void *)(rbase + (uint32_t)si * 1024u + roff[x]),
+            __builtin_amdgcn_global_load_lds((const void *)(rbase + plane_step_off((uint32_t)si) + roff[x]),
                                              (lds_void *)(dst + (w + 4 * x) * 1024), 16, 0, RPOL);
         } else if (x < 8) {
             // (a uniform base in SGPRs and one 32-bit lane offset: the
             // saddr form of the load, no 64-bit address add per piece)
-            const uint32_t vo = (uint32_t)si * 1024u + qoff[x - 4];
+            const uint32_t vo = plane_step_off((uint32_t)si) + qoff[x - 4];
             const uint64_t qb = (uint64_t)qplane;
             const unsigned char *qbase = reinterpret_cast<const unsigned char *>(
                 ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(qb >> 32)) << 32) |
@@ -808,7 +808,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
     auto set_src = [&]() __attribute__((always_inline)) {
         int ln = lane;
         asm volatile("" : "+v"(ln));
-        const uint32_t lc = (uint32_t)(ln >> 2) * 64u + (uint32_t)((ln & 3) ^ p4_g((ln >> 4) & 3)) * 16u;
+        const uint32_t lc = plane_vec_off((uint32_t)(ln >> 2)) + (uint32_t)((ln & 3) ^ p4_g((ln >> 4) & 3)) * 16u;
         rbase = reinterpret_cast<const unsigned char *>(p.rows_hi) + (uint64_t)(uint32_t)(ir0 >> 4) * blk;
 #pragma unroll
         for (int i = 0; i < 4; ++i) {
@@ -830,7 +830,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
                     var = iord < mu ? iord : mu + (iord - mu) % lam;
                 }
                 const uint32_t u = (uint32_t)var * (uint32_t)p.q_vpad + (uint32_t)j;
-                qoff[i] = (u >> 4) * blk + (u & 15) * 64u + (uint32_t)((ln & 3) ^ p4_g((ln >> 4) & 3)) * 16u;
+                qoff[i] = (u >> 4) * blk + plane_vec_off(u & 15) + (uint32_t)((ln & 3) ^ p4_g((ln >> 4) & 3)) * 16u;
             }
         }
         if constexpr (L2) {
@@ -846,10 +846,10 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
     auto issue_piece = [&](int x) __attribute__((always_inline)) {
         unsigned char *dst = lds + ibuf * kP4Stage;
         if (x < 4) {
-            __builtin_amdgcn_global_load_lds((const void *)(rbase + (uint32_t)si * 1024u + roff[x]),
+            __builtin_amdgcn_global_load_lds((const void *)(rbase + plane_step_off((uint32_t)si) + roff[x]),
                                              (lds_void *)(dst + (w + 4 * x) * 1024), 16, 0, 0);
         } else if (x < 8) {
-            const uint32_t vo = (uint32_t)si * 1024u + qoff[x - 4];
+            const uint32_t vo = plane_step_off((uint32_t)si) + qoff[x - 4];
             const uint64_t qb_ = (uint64_t)qplane;
             const unsigned char *qbase = reinterpret_cast<const unsigned char *>(
                 ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((int)(uint32_t)(qb_ >> 32)) << 32) |
@@ -1206,8 +1206,8 @@ __global__ void k_ord_gather(const uint16_t *qhi, uint16_t *qord, const int *qmu
             v = pl < mu ? pl : mu + (pl - mu) % lam;
         }
         const int64_t us = (int64_t)v * vpad + j, ud = (int64_t)pl * vpad + j;
-        const int64_t os = (((us >> 4) * nst + st) << 10) + (us & 15) * 64 + qt * 16;
-        const int64_t od = (((ud >> 4) * nst + st) << 10) + (ud & 15) * 64 + qt * 16;
+        const int64_t os = (((us >> 4) * nst) << 10) + plane_step_off(st) + plane_vec_off((uint32_t)(us & 15)) + qt * 16;
+        const int64_t od = (((ud >> 4) * nst) << 10) + plane_step_off(st) + plane_vec_off((uint32_t)(ud & 15)) + qt * 16;
         *reinterpret_cast<u32x4 *>(dst + od) = *reinterpret_cast<const u32x4 *>(src + os);
     }
 }

@@ -344,6 +344,24 @@ void launch_hamming_to_int(const int64_t *ids, float *dist, int64_t m, hipStream
 
 // bf16 pre-filter path (kernels_bf16.hip)
 constexpr int kBfK = 64;    // bf16 planes padded to a multiple of this
+// bf16 plane layout (rows_hi, q_hi, q_ord; written by launch_to_hi): vectors
+// in groups of 16; a group is dpad / kPlaneSlab column slabs back to back, each
+// [16 vectors][kPlaneSlab columns] with one vector's slab columns contiguous.
+// Readers address k-step s (32 columns) of vector v16 of a group at
+// plane_step_off(s) + plane_vec_off(v16).  kPlaneSlab = 32: a stage's piece
+// of 16 vectors is 1 KiB contiguous (8 whole 128-B lines per wave
+// instruction).  64 would give each vector one whole 128-B line per slab, so
+// a gathered row (selective PREWHERE) would fetch none of its neighbour's
+// bytes -- measured in round 4 (profiles/r04/layout/bench_slab64.json, every
+// GPU test green): the 10 % configs[4] main scan 2.29 -> 1.88 ms, but the
+// streaming scans read 16 half lines per instruction and slowed: nq 1 full
+// scan 10.9 -> 13.9 ms (50M x 768), nq 1000 batch 12.6 -> 13.6 ms.
+constexpr int kPlaneSlab = 32;
+static_assert(kBfK % kPlaneSlab == 0, "dpad is a whole number of slabs");
+__host__ __device__ constexpr uint32_t plane_vec_off(uint32_t v16) { return v16 * (uint32_t)(kPlaneSlab * 2); }
+__host__ __device__ constexpr uint32_t plane_step_off(uint32_t s) {
+    return (s / (uint32_t)(kPlaneSlab / 32)) * (16u * kPlaneSlab * 2) + (s % (uint32_t)(kPlaneSlab / 32)) * 64u;
+}
 constexpr int kHiSplit = 2; // bf16 hi*hi, bound from measured residual norms (kernels_hi.hip)
 constexpr int kMxRec = 8;   // floats per vector in the norm records (launch_to_hi)
 // dst_hi = bf16_rn(x), row-major [rows][dpad] (the index's list planes)
