@@ -397,142 +397,198 @@ void launch_pack_nonempty(const uint8_t *bytes, int64_t n, uint8_t *bits, hipStr
     hipLaunchKernelGGL(k_pack, dim3((unsigned)blocks), dim3(256), 0, s, bytes, n, bits);
 }
 
+// Bitmap words: bits [32 w, 32 w + 32) of an LSB-first byte bitmap of nbits
+// bits (bits at or past nbits read 0).  The row-selection kernels below work a
+// word (32 rows) per lane and a wave per granule chunk: round 3's row-per-
+// thread loops with a block barrier per 256 rows took 60-90 us each on a
+// 50M-row part (6104 chunks), more than a 1 %-selective scan itself.
+__device__ inline uint32_t bm_word(const uint8_t *bm, int64_t nbits, int64_t w) {
+    const int64_t b0 = 4 * w, nbytes = (nbits + 7) >> 3;
+    uint32_t v = 0;
+    if (b0 + 4 <= nbytes && (((uintptr_t)(bm + b0)) & 3) == 0) {
+        v = *reinterpret_cast<const uint32_t *>(bm + b0);
+    } else {
+        for (int i = 0; i < 4; ++i)
+            if (b0 + i < nbytes) v |= (uint32_t)bm[b0 + i] << (8 * i);
+    }
+    const int64_t hi = nbits - 32 * w;
+    if (hi < 32) v &= hi <= 0 ? 0u : ((1u << hi) - 1u);
+    return v;
+}
+
+// rows of word w inside [r0, r1)
+__device__ inline uint32_t range_mask(int64_t w, int64_t r0, int64_t r1) {
+    const int64_t b = 32 * w;
+    uint32_t m = 0xFFFFFFFFu;
+    if (r0 > b) m = r0 - b >= 32 ? 0u : m & (0xFFFFFFFFu << (r0 - b));
+    if (r1 < b + 32) m = r1 <= b ? 0u : m & ((1u << (r1 - b)) - 1u);
+    return m;
+}
+
+// selected rows of word w: filter (or every row when null) & non-empty & live
+__device__ inline uint32_t sel_word(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists,
+                                    int64_t n, int64_t w) {
+    uint32_t v = filter ? bm_word(filter, n, w) : range_mask(w, 0, n);
+    if (nonempty) v &= bm_word(nonempty, n, w);
+    if (exists) v &= bm_word(exists, n, w);
+    return v;
+}
+
+__device__ inline int64_t wave_excl_scan64(int64_t v, int64_t &total) {
+    const int lane = threadIdx.x & 63;
+    int64_t inc = v;
+    for (int o = 1; o < 64; o <<= 1) {
+        const int64_t y = __shfl_up(inc, o);
+        if (lane >= o) inc += y;
+    }
+    total = __shfl(inc, 63);
+    return inc - v;
+}
+
 // Chunk ordinals: which granule chunks the reference actually hands to
 // searchWrapper, and how many such calls came before each.
 //  no-filter mode (require_filter = 0): a chunk is searched iff one of its
 //    arrays is non-empty (MergeTreeVSManager.cpp:1364-1368 skips src_vec.empty());
 //  filter mode: a mark is searched iff it keeps >= 1 selected non-empty live
 //    row (:1179-1183).
+// One wave per chunk, four chunks per workgroup.
 __global__ __launch_bounds__(256) void k_chunk_active(const uint8_t *filter,
                                                        const uint8_t *nonempty,
                                                        const uint8_t *exists, int64_t n,
-                                                       int64_t chunk_rows, int require_filter,
+                                                       int64_t chunk_rows, int64_t nchunks, int require_filter,
                                                        int *flag) {
-    __shared__ int any;
-    const int64_t c = blockIdx.x;
-    if (threadIdx.x == 0) any = 0;
-    __syncthreads();
+    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (c >= nchunks) return;
     const int64_t r0 = c * chunk_rows;
     const int64_t r1 = r0 + chunk_rows < n ? r0 + chunk_rows : n;
-    int mine = 0;
-    for (int64_t r = r0 + threadIdx.x; r < r1 && !mine; r += 256) {
-        bool ok = nonempty ? bit_test(nonempty, r) : true;
+    uint32_t any = 0;
+    for (int64_t w = (r0 >> 5) + lane; w < ((r1 + 31) >> 5) && !any; w += 64) {
+        uint32_t v = range_mask(w, r0, r1);
+        if (nonempty) v &= bm_word(nonempty, n, w);
         if (require_filter) {
-            ok = ok && bit_test(filter, r);
-            if (exists) ok = ok && bit_test(exists, r);
+            v &= bm_word(filter, n, w);
+            if (exists) v &= bm_word(exists, n, w);
         }
-        mine = ok ? 1 : 0;
+        any |= v;
     }
-    if (mine) atomicOr(&any, 1);
-    __syncthreads();
-    if (threadIdx.x == 0) flag[c] = any;
+    const bool hit = __any(any != 0);
+    if (lane == 0) flag[c] = hit ? 1 : 0;
 }
 
-__global__ __launch_bounds__(256) void k_exclusive_ord(int *flag_ord, int64_t nchunks) {
-    __shared__ int sums[256];
-    __shared__ int carry;
-    if (threadIdx.x == 0) carry = 0;
+// One workgroup of kScanThreads: thread t owns a contiguous run of chunks;
+// the run sums are scanned by waves, then over the wave totals.
+constexpr int kScanThreads = 1024;
+template <class Val, class Out>
+__device__ void run_scan(int64_t nchunks, Val val, Out out, int64_t *sh, int64_t &grand) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    const int64_t per = (nchunks + kScanThreads - 1) / kScanThreads;
+    const int64_t b = t * per, e = b + per < nchunks ? b + per : nchunks;
+    int64_t s = 0;
+    for (int64_t i = b; i < e; ++i) s += val(i);
+    int64_t wt = 0;
+    const int64_t ex = wave_excl_scan64(s, wt);
+    if (lane == 0) sh[wv] = wt;
     __syncthreads();
-    for (int64_t base = 0; base < nchunks; base += 256) {
-        const int64_t c = base + threadIdx.x;
-        const int f = c < nchunks ? flag_ord[c] : 0;
-        sums[threadIdx.x] = f;
-        __syncthreads();
-        for (int off = 1; off < 256; off <<= 1) {
-            int v = threadIdx.x >= off ? sums[threadIdx.x - off] : 0;
-            __syncthreads();
-            sums[threadIdx.x] += v;
-            __syncthreads();
-        }
-        const int incl = sums[threadIdx.x];
-        if (c < nchunks) flag_ord[c] = f ? carry + incl - 1 : -1;
-        __syncthreads();
-        if (threadIdx.x == 255) carry += incl;
-        __syncthreads();
+    int64_t before = 0, all = 0;
+    for (int w = 0; w < kScanThreads / 64; ++w) {
+        if (w < wv) before += sh[w];
+        all += sh[w];
     }
+    int64_t run = before + ex;
+    for (int64_t i = b; i < e; ++i) {
+        const int64_t v = val(i);
+        out(i, run, v);
+        run += v;
+    }
+    grand = all;
+    __syncthreads();
+}
+
+__global__ __launch_bounds__(kScanThreads) void k_exclusive_ord(int *flag_ord, int64_t nchunks) {
+    __shared__ int64_t sh[kScanThreads / 64];
+    int64_t tot = 0;
+    run_scan(
+        nchunks, [&](int64_t i) -> int64_t { return flag_ord[i] ? 1 : 0; },
+        [&](int64_t i, int64_t before, int64_t v) { flag_ord[i] = v ? (int)before : -1; }, sh, tot);
 }
 
 // ---------------------------------------------------------------------------
 // Gather list of a selective PREWHERE scan: the rows that pass the filter,
 // are non-empty and not deleted, chunk by chunk in row order, each chunk's
 // run padded with -1 to a multiple of `tile` entries.
-__device__ inline bool row_selected(const uint8_t *filter, const uint8_t *nonempty,
-                                    const uint8_t *exists, int64_t r) {
-    return bit_test(filter, r) && (!nonempty || bit_test(nonempty, r)) && (!exists || bit_test(exists, r));
-}
-
 __global__ __launch_bounds__(256) void k_chunk_count(const uint8_t *filter, const uint8_t *nonempty,
                                                       const uint8_t *exists, int64_t n, int64_t chunk_rows,
-                                                      int *count) {
-    const int64_t c = blockIdx.x;
+                                                      int64_t nchunks, int *count) {
+    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (c >= nchunks) return;
     const int64_t r0 = c * chunk_rows;
     const int64_t r1 = r0 + chunk_rows < n ? r0 + chunk_rows : n;
-    int total = 0;
-    for (int64_t base = r0; base < r1; base += 256) {
-        const int64_t r = base + threadIdx.x;
-        total += __syncthreads_count(r < r1 && row_selected(filter, nonempty, exists, r));
-    }
-    if (threadIdx.x == 0) count[c] = total;
+    int cnt = 0;
+    for (int64_t w = (r0 >> 5) + lane; w < ((r1 + 31) >> 5); w += 64)
+        cnt += __popc(sel_word(filter, nonempty, exists, n, w) & range_mask(w, r0, r1));
+    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+    if (lane == 0) count[c] = cnt;
 }
 
 // offsets[c] = sum of padded counts before c; totals[0] = padded list
 // length, totals[1] = selected rows
-__global__ __launch_bounds__(256) void k_pad_scan(const int *count, int64_t nchunks, int tile,
-                                                   int64_t *offsets, int64_t *totals) {
-    __shared__ int64_t sums[256];
-    __shared__ int64_t carry, selected;
-    if (threadIdx.x == 0) carry = selected = 0;
-    __syncthreads();
-    for (int64_t base = 0; base < nchunks; base += 256) {
-        const int64_t c = base + threadIdx.x;
-        const int cnt = c < nchunks ? count[c] : 0;
-        const int64_t padded = (int64_t)(cnt + tile - 1) / tile * tile;
-        sums[threadIdx.x] = padded;
-        __syncthreads();
-        for (int off = 1; off < 256; off <<= 1) {
-            const int64_t v = threadIdx.x >= off ? sums[threadIdx.x - off] : 0;
-            __syncthreads();
-            sums[threadIdx.x] += v;
-            __syncthreads();
-        }
-        if (c < nchunks) offsets[c] = carry + sums[threadIdx.x] - padded;
-        if (cnt) atomicAdd((unsigned long long *)&selected, (unsigned long long)cnt);
-        __syncthreads();
-        if (threadIdx.x == 255) carry += sums[255];
-        __syncthreads();
-    }
+__global__ __launch_bounds__(kScanThreads) void k_pad_scan(const int *count, int64_t nchunks, int tile,
+                                                            int64_t *offsets, int64_t *totals) {
+    __shared__ int64_t sh[kScanThreads / 64];
+    int64_t padded_total = 0, selected = 0;
+    run_scan(
+        nchunks, [&](int64_t i) -> int64_t { return (int64_t)(count[i] + tile - 1) / tile * tile; },
+        [&](int64_t i, int64_t before, int64_t) { offsets[i] = before; }, sh, padded_total);
+    run_scan(
+        nchunks, [&](int64_t i) -> int64_t { return count[i]; }, [&](int64_t, int64_t, int64_t) {}, sh, selected);
     if (threadIdx.x == 0) {
-        totals[0] = carry;
+        totals[0] = padded_total;
         totals[1] = selected;
     }
 }
 
+// one wave per chunk: lane l takes 4 consecutive words of each 256-word round,
+// a wave scan of their counts places its rows
 __global__ __launch_bounds__(256) void k_compact_rows(const uint8_t *filter, const uint8_t *nonempty,
                                                        const uint8_t *exists, int64_t n, int64_t chunk_rows,
-                                                       const int *count, const int64_t *offsets, int tile,
-                                                       int32_t *list) {
-    __shared__ int wsum[4];
-    const int64_t c = blockIdx.x;
+                                                       int64_t nchunks, const int *count, const int64_t *offsets,
+                                                       int tile, int32_t *list) {
+    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (c >= nchunks) return;
     const int64_t r0 = c * chunk_rows;
     const int64_t r1 = r0 + chunk_rows < n ? r0 + chunk_rows : n;
-    const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     int32_t *out = list + offsets[c];
-    int run = 0;
-    for (int64_t base = r0; base < r1; base += 256) {
-        const int64_t r = base + threadIdx.x;
-        const bool ok = r < r1 && row_selected(filter, nonempty, exists, r);
-        const unsigned long long m = __ballot(ok);
-        if (lane == 0) wsum[w] = __popcll(m);
-        __syncthreads();
-        int before = run;
-        for (int i = 0; i < w; ++i) before += wsum[i];
-        if (ok) out[before + __popcll(m & ((1ull << lane) - 1ull))] = (int32_t)r;
-        run += wsum[0] + wsum[1] + wsum[2] + wsum[3];
-        __syncthreads();
+    int64_t run = 0;
+    const int64_t w0 = r0 >> 5, w1 = (r1 + 31) >> 5;
+    for (int64_t base = w0; base < w1; base += 256) {
+        uint32_t v[4];
+        int64_t cnt = 0;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int64_t w = base + 4 * lane + i;
+            v[i] = w < w1 ? sel_word(filter, nonempty, exists, n, w) & range_mask(w, r0, r1) : 0u;
+            cnt += __popc(v[i]);
+        }
+        int64_t tot = 0;
+        int64_t pos = run + wave_excl_scan64(cnt, tot);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            uint32_t m = v[i];
+            const int64_t rb = 32 * (base + 4 * lane + i);
+            while (m) {
+                const int bit = __ffs(m) - 1;
+                m &= m - 1;
+                out[pos++] = (int32_t)(rb + bit);
+            }
+        }
+        run += tot;
     }
     const int cnt = count[c];
     const int padded = (cnt + tile - 1) / tile * tile;
-    for (int i = cnt + threadIdx.x; i < padded; i += 256) out[i] = -1;
+    for (int i = cnt + lane; i < padded; i += 64) out[i] = -1;
 }
 
 void launch_gather_count(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists, int64_t n,
@@ -540,9 +596,9 @@ void launch_gather_count(const uint8_t *filter, const uint8_t *nonempty, const u
                          hipStream_t s) {
     const int64_t nchunks = (n + chunk_rows - 1) / chunk_rows;
     if (nchunks < 1) return;
-    hipLaunchKernelGGL(k_chunk_count, dim3((unsigned)nchunks), dim3(256), 0, s, filter, nonempty, exists, n,
-                       chunk_rows, count);
-    hipLaunchKernelGGL(k_pad_scan, dim3(1), dim3(256), 0, s, count, nchunks, tile, offsets, totals);
+    hipLaunchKernelGGL(k_chunk_count, dim3((unsigned)((nchunks + 3) / 4)), dim3(256), 0, s, filter, nonempty, exists,
+                       n, chunk_rows, nchunks, count);
+    hipLaunchKernelGGL(k_pad_scan, dim3(1), dim3(kScanThreads), 0, s, count, nchunks, tile, offsets, totals);
 }
 
 void launch_gather_list(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists, int64_t n,
@@ -550,8 +606,8 @@ void launch_gather_list(const uint8_t *filter, const uint8_t *nonempty, const ui
                         hipStream_t s) {
     const int64_t nchunks = (n + chunk_rows - 1) / chunk_rows;
     if (nchunks < 1) return;
-    hipLaunchKernelGGL(k_compact_rows, dim3((unsigned)nchunks), dim3(256), 0, s, filter, nonempty, exists, n,
-                       chunk_rows, count, offsets, tile, list);
+    hipLaunchKernelGGL(k_compact_rows, dim3((unsigned)((nchunks + 3) / 4)), dim3(256), 0, s, filter, nonempty, exists,
+                       n, chunk_rows, nchunks, count, offsets, tile, list);
 }
 
 void launch_chunk_ordinals(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists,
@@ -559,9 +615,9 @@ void launch_chunk_ordinals(const uint8_t *filter, const uint8_t *nonempty, const
                            hipStream_t s) {
     const int64_t nchunks = (n + chunk_rows - 1) / chunk_rows;
     if (nchunks < 1) return;
-    hipLaunchKernelGGL(k_chunk_active, dim3((unsigned)nchunks), dim3(256), 0, s, filter, nonempty,
-                       exists, n, chunk_rows, require_filter, ord);
-    hipLaunchKernelGGL(k_exclusive_ord, dim3(1), dim3(256), 0, s, ord, nchunks);
+    hipLaunchKernelGGL(k_chunk_active, dim3((unsigned)((nchunks + 3) / 4)), dim3(256), 0, s, filter, nonempty,
+                       exists, n, chunk_rows, nchunks, require_filter, ord);
+    hipLaunchKernelGGL(k_exclusive_ord, dim3(1), dim3(kScanThreads), 0, s, ord, nchunks);
 }
 
 // ---------------------------------------------------------------------------
@@ -599,8 +655,8 @@ void launch_count_active_chunks(const uint8_t *filter, const uint8_t *nonempty, 
                                 int64_t chunk_rows, int *flags_scratch, int64_t *count, hipStream_t s) {
     const int64_t nchunks = (n + chunk_rows - 1) / chunk_rows;
     if (nchunks > 0)
-        hipLaunchKernelGGL(k_chunk_active, dim3((unsigned)nchunks), dim3(256), 0, s, filter, nonempty, exists, n,
-                           chunk_rows, filter ? 1 : 0, flags_scratch);
+        hipLaunchKernelGGL(k_chunk_active, dim3((unsigned)((nchunks + 3) / 4)), dim3(256), 0, s, filter, nonempty,
+                           exists, n, chunk_rows, nchunks, filter ? 1 : 0, flags_scratch);
     hipLaunchKernelGGL(k_sum_flags, dim3(1), dim3(256), 0, s, flags_scratch, nchunks, count);
 }
 

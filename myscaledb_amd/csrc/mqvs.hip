@@ -682,43 +682,25 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     int64_t selected = -1, gpadded = 0;
     int *gcount = nullptr;
     int64_t *goff = nullptr;
+    // Cosine pads each chunk's run to whole tiles (a tile's query variant is
+    // its chunk's); L2 / IP have one variant, so their list is dense and only
+    // its end is padded (at 1 % selectivity per-chunk padding made the list
+    // 3x the selected rows: 82 rows per 8192-row chunk, padded to 256)
+    const int gtile = cos ? (int)kSmallRows : 1;
     if (dfilter && gather_mode != 0 && n > 0) {
         const int64_t nch = (n + seg->granule - 1) / seg->granule;
         gcount = (int *)ws.get(ws.gcount, sizeof(int) * nch);
         goff = (int64_t *)ws.get(ws.goff, sizeof(int64_t) * (nch + 2));
-        launch_gather_count(dfilter, seg->nonempty_bits, dexists, n, seg->granule, kSmallRows, gcount, goff,
-                            goff + nch, s);
+        launch_gather_count(dfilter, seg->nonempty_bits, dexists, n, seg->granule, gtile, gcount, goff, goff + nch,
+                            s);
         MQVS_HIP(hipGetLastError());
-        int64_t *htot = reinterpret_cast<int64_t *>(ws.host_flags + 8);
-        MQVS_HIP(hipMemcpyAsync(htot, goff + nch, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-        MQVS_HIP(hipStreamSynchronize(s));
-        gpadded = htot[0];
-        selected = htot[1];
+        // read back after the query prep and chunk ordinals are queued (the
+        // host round trip overlaps them)
+        MQVS_HIP(hipMemcpyAsync(ws.host_flags + 8, goff + nch, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        selected = 0;
     }
-
-    // ---- kernel choice
-    // faiss's formula branch is set by nq (kBlasThreshold); the bf16
-    // pre-filter serves both branches (its exact re-rank uses the branch's
-    // formula) whenever the segment has its plane, the exact kernels the rest.  A
-    // gathered (selective) scan prefers the bf16 kernel at any nq: its LDS-DMA
-    // keeps whole tiles of scattered rows in flight and gathers efficiently up
-    // to ~60% selectivity, while the VALU kernel's 128-B row slices only pay
-    // below ~30% (tools/sweep.py --sels, profiles/r01)
     const bool mfma = fnq >= kBlasThreshold;
     const bool bf16_ok = seg->approx_ok && !force_exact && batch_mode == 0;
-    // (the bf16 plane streams half the bytes of the fp32 rows, so it serves
-    // every batch size)
-    bool bf16 = bf16_ok;
-    bool gather = false;
-    if (selected >= 0) {
-        if (gather_mode == 2)
-            gather = bf16 || !mfma;
-        else if (bf16_ok && 10 * selected <= 6 * n)
-            gather = bf16 = true;
-        else if (!bf16 && !mfma && 10 * selected <= 3 * n)
-            gather = true;
-    }
-    const int kind = bf16 ? kScanBf16 : !mfma ? kScanSmall : kScanMfma32;
 
     // ---- query prep
     const int64_t ords = (ord_base >= 0 ? ord_base : seg->row_offset / seg->granule) +
@@ -732,8 +714,9 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     // The query-variant table starts at kMaxVariants per query without a host
     // round trip; a chain that does not repeat within it on a part of more
     // chunk ordinals (rare: small-integer data) is caught from the status word
-    // read at the end, and the search re-runs with the larger table.
-    const int maxv = prep_variants(ws, dq, nq, d, cos, (mfma || bf16) && metric == MQVS_METRIC_L2, ords, false,
+    // read at the end, and the search re-runs with the larger table.  (The
+    // kernel choice below never changes bf16 from bf16_ok.)
+    const int maxv = prep_variants(ws, dq, nq, d, cos, (mfma || bf16_ok) && metric == MQVS_METRIC_L2, ords, false,
                                    qvars, qnorms, qmu, qlam, status, s, fl + 4, maxv_hint);
 
     // ---- chunk ordinals
@@ -749,15 +732,44 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     } else {
         chunk_ord = seg->chunk_ord;
     }
+    if (selected >= 0) {
+        MQVS_HIP(hipStreamSynchronize(s));
+        const int64_t *htot = reinterpret_cast<const int64_t *>(ws.host_flags + 8);
+        gpadded = round_up(htot[0], kSmallRows);
+        selected = htot[1];
+    }
+
+    // ---- kernel choice
+    // faiss's formula branch is set by nq (kBlasThreshold); the bf16
+    // pre-filter serves both branches (its exact re-rank uses the branch's
+    // formula) whenever the segment has its plane, the exact kernels the rest.  A
+    // gathered (selective) scan prefers the bf16 kernel at any nq: its LDS-DMA
+    // keeps whole tiles of scattered rows in flight and gathers efficiently up
+    // to ~60% selectivity, while the VALU kernel's 128-B row slices only pay
+    // below ~30% (tools/sweep.py --sels, profiles/r01)
+    // (the bf16 plane streams half the bytes of the fp32 rows, so it serves
+    // every batch size)
+    bool bf16 = bf16_ok;
+    bool gather = false;
+    if (selected >= 0) {
+        if (gather_mode == 2)
+            gather = bf16 || !mfma;
+        else if (bf16_ok && 10 * selected <= 6 * n)
+            gather = bf16 = true;
+        else if (!bf16 && !mfma && 10 * selected <= 3 * n)
+            gather = true;
+    }
+    const int kind = bf16 ? kScanBf16 : !mfma ? kScanSmall : kScanMfma32;
 
     // ---- gather list of the selected rows
     const int32_t *row_list = nullptr;
     int64_t scan_n = n;  // scan positions: rows, or gather-list entries
     if (gather) {
         int32_t *list = (int32_t *)ws.get(ws.glist, sizeof(int32_t) * std::max<int64_t>(gpadded, 1));
-        launch_gather_list(dfilter, seg->nonempty_bits, dexists, n, seg->granule, kSmallRows, gcount, goff, list,
-                           s);
+        launch_gather_list(dfilter, seg->nonempty_bits, dexists, n, seg->granule, gtile, gcount, goff, list, s);
         MQVS_HIP(hipGetLastError());
+        if (gpadded > selected && gtile == 1)  // the dense list's tail: -1 entries up to a whole tile
+            MQVS_HIP(hipMemsetAsync(list + selected, 0xFF, sizeof(int32_t) * (size_t)(gpadded - selected), s));
         row_list = list;
         scan_n = gpadded;
         st.gather = 1;
