@@ -49,7 +49,7 @@ struct mqvs_index {
     int64_t dpad = 0;
     float alpha = 3.0f;            // default search alpha
     mqvs_segment *cent = nullptr;  // centroid segment (k-means assignment during the build)
-    uint16_t *plane = nullptr;     // [npos][dpad] bf16 rows in list order
+    uint16_t *plane = nullptr;     // bf16 rows in list order, [npos/16][dpad/32][16][32] (k_ivf_pack)
     int32_t *perm = nullptr;       // [npos] row of each position, -1 = padding
     float *pnorm = nullptr;        // [npos] |y|^2
     int64_t *list_off = nullptr;   // [nlist+1]

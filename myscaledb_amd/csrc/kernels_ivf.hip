@@ -4,7 +4,8 @@
 //
 // Layout.  The part's rows are partitioned into `nlist` lists by a k-means
 // coarse quantizer.  The lists are stored back to back as one bf16 plane in
-// list order ([npos][dpad], each list padded to a multiple of 16 positions),
+// list order (each list padded to a multiple of 16 positions; blocked as
+// [npos / 16][dpad / 32][16][32], 1 KiB pieces like the FLAT plane),
 // with perm[pos] = segment row (-1 = padding) and pnorm[pos] = |y|^2.
 //
 // Search (one batch of nq queries, each probing nprobe lists):
@@ -506,7 +507,12 @@ __global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
 #pragma unroll
         for (int j = 0; j < QB; ++j) ent[j] = s_ent[16 * j + l16];
         for (int b = chk * (kIvfChunk / 16) + w; b < nb; b += 4) {
-            const uint16_t *rp = p.plane + (pos0 + (int64_t)b * 16 + l16) * p.dpad + c * 8;
+            // the plane is blocked like the FLAT pre-filter plane: 16 positions
+            // x 32 columns = 1 KiB per piece (k_ivf_pack), so each fragment
+            // load of a wave reads one contiguous KiB (8 whole 128-B lines);
+            // round 3's row-major plane made it 16 half lines (measured
+            // neutral: configs[2] mode 2 scan 0.68 ms either way)
+            const uint16_t *rp = p.plane + ((pos0 >> 4) + (int64_t)b) * 16 * p.dpad + l16 * 32 + c * 8;
             ivf_f32x4 acc[QB];
 #pragma unroll
             for (int j = 0; j < QB; ++j) acc[j] = ivf_f32x4{0.f, 0.f, 0.f, 0.f};
@@ -516,8 +522,8 @@ __global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
                 for (int u = 0; u < kIvfWin; ++u) {
                     const int64_t kw = ((int64_t)grp * kIvfWin + u) * 64;
                     if (kw < p.dpad) {
-                        dst[2 * u] = *reinterpret_cast<const ivf_bf16x8 *>(rp + kw);
-                        dst[2 * u + 1] = *reinterpret_cast<const ivf_bf16x8 *>(rp + kw + 32);
+                        dst[2 * u] = *reinterpret_cast<const ivf_bf16x8 *>(rp + (kw >> 5) * 512);
+                        dst[2 * u + 1] = *reinterpret_cast<const ivf_bf16x8 *>(rp + ((kw >> 5) + 1) * 512);
                     }
                 }
             };
@@ -827,7 +833,10 @@ __global__ __launch_bounds__(256) void k_ivf_pack(const float *rows, const float
         o.y = v[2] | ((uint32_t)v[3] << 16);
         o.z = v[4] | ((uint32_t)v[5] << 16);
         o.w = v[6] | ((uint32_t)v[7] << 16);
-        reinterpret_cast<uint4 *>(plane + pos * dpad)[cc] = o;
+        // 16-position blocks of 32-column pieces (1 KiB each): see k_ivf_scan
+        const int64_t col0 = cc * 8;
+        *reinterpret_cast<uint4 *>(plane + ((pos >> 4) * (dpad / 32) + (col0 >> 5)) * 512 + (pos & 15) * 32 +
+                                   (col0 & 31)) = o;
         if (cc == 0) pnorm[pos] = row >= 0 ? norms[row] : 0.f;
     }
 }
