@@ -36,7 +36,12 @@ for step in $STEPS; do
         || { echo "risk failed"; tail -20 $O/blas_order_risk.log; exit 1; }
       grep -A4 per_block $O/blas_order_risk.json ;;
     bench)
-      timeout -k 10 900 python -u bench.py --pmc $O/pmc_traffic.json --pmc-nq1 $O/pmc_nq1.json --index-pmc $O/index_pmc.json \
+      # this session's PMC summaries when it made them, else the committed ones
+      PA=()
+      [ -f $O/pmc_traffic.json ] && PA+=(--pmc $O/pmc_traffic.json)
+      [ -f $O/pmc_nq1.json ] && PA+=(--pmc-nq1 $O/pmc_nq1.json)
+      [ -f $O/index_pmc.json ] && PA+=(--index-pmc $O/index_pmc.json)
+      timeout -k 10 900 python -u bench.py "${PA[@]}" \
         > $O/bench.json 2> $O/bench.err || { echo "bench failed rc=$?"; tail -30 $O/bench.err; exit 1; }
       head -c 3000 $O/bench.json; echo
       ( cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/prof" -o run --output-format csv \
