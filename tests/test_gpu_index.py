@@ -113,6 +113,32 @@ def test_index_exhaustive_equals_flat(mq, cfg):
     assert np.array_equal(dist_i.view(np.uint32), dist_f.view(np.uint32)), name
 
 
+@pytest.mark.parametrize("nq", [5, 24])
+def test_index_cosine_long_normalisation_chains(mq, nq):
+    """Small-integer queries whose fp32 cosine re-normalisation chain does not
+    repeat within the default variant table, on a part of 60 granule chunks:
+    the index search queues no host round trip for it (the chain's tail runs
+    on a side stream), finds it from the status word at its final sync and
+    re-runs with one variant per chunk ordinal.  The exhaustive setting then
+    equals the oracle's per-chunk re-normalisation bit for bit (the FLAT
+    counterpart: test_gpu_boundary.py::test_cosine_long_normalisation_chains)."""
+    n, d, k, gran = 60 * 64, 768, 40, 64
+    rows = O.generate(0x5EED0001, 0, 0, n, d)
+    q = O.generate(0x5EED0002, 0, 0, nq, d)
+    io, do = O.vector_scan(rows, q, k, O.COSINE, gran, fast=True)
+    seg = mq.VectorScanSegment.from_rows(rows, metric="Cosine", granule=gran)
+    idx = mq.VectorIndex.build(seg, "MSTG", {"nlist": 16})
+    try:
+        ids, dist = idx.search(q, k, {"nprobe": 16, "num_reorder": 4096})
+        ids2, dist2 = idx.search(q, k, {"nprobe": 16, "num_reorder": 4096})  # warm workspace: same bits
+    finally:
+        idx.free()
+        seg.free()
+    for a, b in ((ids, dist), (ids2, dist2)):
+        assert np.array_equal(a, io)
+        assert np.array_equal(b.view(np.uint32), do.view(np.uint32))
+
+
 @pytest.mark.parametrize("metric", ["L2", "IP", "Cosine"])
 def test_index_recall_default_params(mq, metric):
     """Gaussian-mixture part, default nlist / alpha: recall@10 >= 0.95 against
