@@ -757,13 +757,20 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     launch_query_prep(dq, nq, d, cos ? MQVS_METRIC_COSINE : MQVS_METRIC_L2, ix->metric == MQVS_METRIC_L2, qvars, maxv,
                       qnorms, qmu, qlam, status, s, split ? 1 : 0);
     MQVS_HIP(hipGetLastError());
-    if (split) {
+    // The chain starts after the coarse step: beside the coarse batch kernel
+    // it slowed that kernel by ~20 us, beside the plan and the list scan it
+    // costs less (mode 3, nprobe 1: 0.564 -> 0.544 ms per batch,
+    // profiles/r04/index/fork_ab.jsonl).  MQVS_IVF_FORK=0 (measurement build):
+    // start it right after variant 0.
+    const bool late_fork = tune_int("MQVS_IVF_FORK", 1) == 1;
+    auto fork_chain = [&]() {
         MQVS_HIP(hipEventRecord(ws.fork, s));
         MQVS_HIP(hipStreamWaitEvent(ws.side, ws.fork, 0));
         launch_query_prep(dq, nq, d, MQVS_METRIC_COSINE, false, qvars, maxv, qnorms, qmu, qlam, status, ws.side, 2);
         MQVS_HIP(hipGetLastError());
         MQVS_HIP(hipEventRecord(ws.join, ws.side));
-    }
+    };
+    if (split && !late_fork) fork_chain();
     uint16_t *qhi = (uint16_t *)ws.qhi.get(sizeof(uint16_t) * (size_t)nq * ix->dpad);
     launch_to_bf16(qvars, nq, d, (int64_t)maxv * qstride, qhi, ix->dpad, s);
     MQVS_HIP(hipGetLastError());
@@ -833,6 +840,7 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
                   nullptr, nullptr, s, true);
     }
     MQVS_HIP(hipEventRecord(ws.ev[1], s));
+    if (split && late_fork) fork_chain();
 
     // ---- fine: the probed lists
     int64_t *dstats = nullptr;

@@ -1090,19 +1090,30 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
         }
         if (v4) {
             const float4 *q4 = reinterpret_cast<const float4 *>(qv);
-            for (int j = lane; j < (d >> 2); j += 64) {
-                const float4 x = q4[j];
-                float4 y[kPickU];
+            // three column steps per round: 3 kPickU independent 16-B loads
+            // per lane in flight (d = 768 is one round)
+            const int n4 = d >> 2;
+            for (int j0 = lane; j0 < n4; j0 += 3 * 64) {
+                float4 x[3], y[3][kPickU];
 #pragma unroll
-                for (int u = 0; u < kPickU; ++u)
-                    y[u] = r[u] >= 0 ? reinterpret_cast<const float4 *>(cent + r[u] * d)[j] : float4{0.f, 0.f, 0.f, 0.f};
+                for (int t = 0; t < 3; ++t) {
+                    const int j = j0 + 64 * t;
+                    const bool in = j < n4;
+                    x[t] = in ? q4[j] : float4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-                for (int u = 0; u < kPickU; ++u) {
-                    dot[u] = fmaf(x.x, y[u].x, dot[u]);
-                    dot[u] = fmaf(x.y, y[u].y, dot[u]);
-                    dot[u] = fmaf(x.z, y[u].z, dot[u]);
-                    dot[u] = fmaf(x.w, y[u].w, dot[u]);
+                    for (int u = 0; u < kPickU; ++u)
+                        y[t][u] = in && r[u] >= 0 ? reinterpret_cast<const float4 *>(cent + r[u] * d)[j]
+                                                  : float4{0.f, 0.f, 0.f, 0.f};
                 }
+#pragma unroll
+                for (int t = 0; t < 3; ++t)
+#pragma unroll
+                    for (int u = 0; u < kPickU; ++u) {
+                        dot[u] = fmaf(x[t].x, y[t][u].x, dot[u]);
+                        dot[u] = fmaf(x[t].y, y[t][u].y, dot[u]);
+                        dot[u] = fmaf(x[t].z, y[t][u].z, dot[u]);
+                        dot[u] = fmaf(x[t].w, y[t][u].w, dot[u]);
+                    }
             }
         } else {
             for (int e = lane; e < d; e += 64) {
