@@ -456,19 +456,30 @@ static mqvs_index *build_impl(mqvs_segment *seg, const char *index_type, const c
 // takes more than 2 probes -- the data's clusters are larger than the lists,
 // so a query's neighbours spread over many of them and every search pays the
 // coarse step and plan of many small lists -- a coarse index (about 2048 rows
-// per list) is built and evaluated the same way, and the faster of the two at
-// recall 0.95 is kept (its nprobe becomes alpha 3's).  Data of many small
-// clusters (generator mode 3) keeps the fine lists; data of few large ones
-// (mode 2: 4096 centres over 10M rows) gets the coarse ones.
+// per list) is built and evaluated the same way, and the faster of the two is
+// kept (its recall-0.95 nprobe becomes alpha 3's).  The two are compared at
+// the nprobe reaching recall 0.97 on the sample (0.95 if neither does): the
+// sample's own rows are easier queries than held-out ones, and at 0.95 a
+// borderline fine index (mode 2: 0.95 on the sample at nprobe 4, 0.9498 on
+// held-out queries) won by a few per cent and then needed twice the probes in
+// use.  Data of many small clusters (generator mode 3) keeps the fine lists;
+// data of few large ones (mode 2: 4096 centres over 10M rows) gets the coarse
+// ones.
 struct IndexEval {
-    int nprobe = 0;  // 0: recall 0.95 not reached
-    double ms = 1e30;
+    int nprobe = 0;  // recall 0.95 (0: not reached)
+    int nprobe97 = 0;  // recall 0.97 (0: not reached)
+    double ms = 1e30;  // a batch of the sample at nprobe97 (nprobe when 0.97 is not reached)
     double recall = 0.0;
 };
 
 // recall@10 of the sample's queries (rows of the part): the query row itself
 // is dropped from both lists, so the figure is that of held-out queries
 constexpr int kEvalK = 11;
+// the timed searches of an operating point return the top-100 (a typical
+// LIMIT: the re-rank and select then cost what they cost in use; timed at k =
+// 11 the two list counts of a large-cluster part measured within a few per
+// cent of each other, and the choice between them flipped with kernel changes)
+constexpr int kEvalTimeK = 100;
 static double sample_recall(const std::vector<int64_t> &got, const std::vector<int64_t> &gt,
                             const std::vector<int64_t> &self, int m) {
     int64_t hit = 0;
@@ -500,20 +511,29 @@ static IndexEval eval_index(mqvs_index *ix, const float *dq, int m, const std::v
             search_index_impl(ix, dq, m, kEvalK, sp.c_str(), nullptr, nullptr, dids, ddist, MQVS_F_DEVICE_PTRS, s, 0);
             MQVS_HIP(hipMemcpyAsync(got.data(), dids, sizeof(int64_t) * got.size(), hipMemcpyDeviceToHost, s));
             MQVS_HIP(hipStreamSynchronize(s));
-            r.recall = sample_recall(got, gt, self, m);
-            if (r.recall < 0.95) continue;
-            r.nprobe = np;
+            const double rc = sample_recall(got, gt, self, m);
+            if (rc >= 0.95 && r.nprobe == 0) {
+                r.nprobe = np;
+                r.recall = rc;
+            }
+            if (rc >= 0.97) {
+                r.nprobe97 = np;
+                break;
+            }
+        }
+        const int tnp = r.nprobe97 ? r.nprobe97 : r.nprobe;
+        if (tnp > 0) {
+            const std::string sp = "nprobe=" + std::to_string(tnp);
             for (int rep = 0; rep < 3; ++rep) {
                 MQVS_HIP(hipEventRecord(e0, s));
-                search_index_impl(ix, dq, m, kEvalK, sp.c_str(), nullptr, nullptr, dids, ddist, MQVS_F_DEVICE_PTRS, s,
-                                  0);
+                search_index_impl(ix, dq, m, (int)std::min<int64_t>(kEvalTimeK, ix->seg->n), sp.c_str(), nullptr,
+                                  nullptr, dids, ddist, MQVS_F_DEVICE_PTRS, s, 0);
                 MQVS_HIP(hipEventRecord(e1, s));
                 MQVS_HIP(hipStreamSynchronize(s));
                 float ms = 0.f;
                 MQVS_HIP(hipEventElapsedTime(&ms, e0, e1));
                 r.ms = std::min(r.ms, (double)ms);
             }
-            break;
         }
     } catch (...) {
         (void)hipEventDestroy(e0);
@@ -544,7 +564,7 @@ static mqvs_index *build_auto(mqvs_segment *seg, const char *index_type, const c
         std::vector<int64_t> idx(m);
         for (int i = 0; i < m; ++i) idx[i] = (int64_t)(((__int128)(2 * i + 1) * n) / (2 * m));
         TmpBuf didx(sizeof(int64_t) * m), dq(sizeof(float) * (size_t)m * d),
-            dids(sizeof(int64_t) * (size_t)m * kEvalK), ddist(sizeof(float) * (size_t)m * kEvalK);
+            dids(sizeof(int64_t) * (size_t)m * kEvalTimeK), ddist(sizeof(float) * (size_t)m * kEvalTimeK);
         MQVS_HIP(hipMemcpyAsync(didx.p, idx.data(), sizeof(int64_t) * m, hipMemcpyHostToDevice, s));
         launch_gather_rows(seg->rows, d, d, didx.as<int64_t>(), m, dq.as<float>(), s);
         MQVS_HIP(hipGetLastError());
@@ -561,7 +581,11 @@ static mqvs_index *build_auto(mqvs_segment *seg, const char *index_type, const c
             b = build_impl(seg, index_type, with_nlist(coarse).c_str());
             const IndexEval eb = eval_index(b, dq.as<float>(), m, gt, self, dids.as<int64_t>(), ddist.as<float>(), s);
             b->np95 = eb.nprobe;
-            if (eb.nprobe > 0 && eb.ms < ea.ms) std::swap(a, b);
+            // (times are comparable only at the same target: an index that
+            // reaches 0.97 within 64 probes beats one that does not)
+            const bool a97 = ea.nprobe97 > 0, b97 = eb.nprobe97 > 0;
+            const bool b_better = a97 != b97 ? b97 : (eb.nprobe > 0 && eb.ms < ea.ms);
+            if (b_better) std::swap(a, b);
             free_index(b);
             b = nullptr;
         }
