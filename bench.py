@@ -314,7 +314,8 @@ def index_points(mq, seg, mode, settings, args):
         with open(pmc_path) as f:
             pm = json.load(f).get(str(mode))
         ks = [v for key, v in (pm or {}).get("kernels", {}).items() if "k_ivf_scan" in key]
-        if ks and all("hbm_bytes_per_search" in v for v in ks) and pm.get("search") == best["search"]:
+        same_index = pm is not None and pm.get("nlist") in (None, info["nlist"])  # (older summaries: no nlist)
+        if ks and all("hbm_bytes_per_search" in v for v in ks) and pm.get("search") == best["search"] and same_index:
             # every k_ivf_scan launch of a search: the coarse quantizer's scan
             # of the centroids and the list scan (reads: list plane; writes:
             # one 8-B approximate value per (query, probed position))

@@ -10,14 +10,18 @@ mkdir -p gpurun_out/index_pmc
 for spec in "$@"; do
     mode=${spec%%:*}; search=${spec#*:}
     rm -rf gpurun_out/pmc1 gpurun_out/pmc2 gpurun_out/pmc3
-    bash tools/gpu_pmc.sh python tools/index_search_run.py --mode "$mode" --search "$search" --searches 2 || exit 1
+    bash tools/gpu_pmc.sh python tools/index_search_run.py --mode "$mode" --search "$search" --searches 2 \
+        --info-out "$R/gpurun_out/index_pmc/mode${mode}_info.json" || exit 1
     python tools/pmc_traffic.py gpurun_out --searches 2 --last 2 --nq 1000 --kernel k_ivf_scan \
         --out "gpurun_out/index_pmc/mode$mode.json" > /dev/null || exit 1
     python - "$mode" "$search" <<'PY' || exit 1
-import json, sys
+import json, os, sys
 mode, search = sys.argv[1], sys.argv[2]
 p = "gpurun_out/index_pmc/mode%s.json" % mode
 d = json.load(open(p)); d["search"] = search; d["mode"] = int(mode)
+info = "gpurun_out/index_pmc/mode%s_info.json" % mode
+if os.path.exists(info):
+    d["nlist"] = json.load(open(info))["nlist"]  # (the last pass's build)
 json.dump(d, open(p, "w"), indent=1)
 PY
 done
@@ -25,7 +29,7 @@ rm -rf gpurun_out/pmc1 gpurun_out/pmc2 gpurun_out/pmc3  # raw CSVs: every dispat
 python - <<'PY'
 import glob, json
 out = {}
-for p in sorted(glob.glob("gpurun_out/index_pmc/mode*.json")):
+for p in sorted(glob.glob("gpurun_out/index_pmc/mode[0-9].json")):
     d = json.load(open(p)); out[str(d["mode"])] = d
 json.dump(out, open("gpurun_out/index_pmc.json", "w"), indent=1)
 for m, d in out.items():

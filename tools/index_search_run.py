@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--mode", type=int, default=2)
     ap.add_argument("--search", default="nprobe=2")
     ap.add_argument("--searches", type=int, default=2)
+    ap.add_argument("--info-out", default=None)
     args = ap.parse_args()
     import torch
     import myscaledb_amd as mq
@@ -35,6 +36,10 @@ def main():
         idx.search(q, args.k, args.search)
     torch.cuda.synchronize()
     print("ok", args.mode, args.search, idx.info()["nlist"])
+    if args.info_out:  # the index actually built (the summary records it; bench.py matches it)
+        import json
+        with open(args.info_out, "w") as f:
+            json.dump({"mode": args.mode, "search": args.search, "nlist": idx.info()["nlist"]}, f)
 
 
 if __name__ == "__main__":
