@@ -99,7 +99,10 @@ const char *mqvs_last_error(void);
  * fallback (its results are then invalid: repeat it synchronously).  Clears
  * the record.  Callers that used several streams synchronise them first. */
 int mqvs_async_check(mqvs_stream_t stream);
-/* Release this thread's stream/workspace (optional; freed at thread exit). */
+/* Release this thread's streams and workspaces -- the FLAT search workspace
+ * and the index search workspace (its scratch, events and the side stream of
+ * the cosine variant chain) -- after their last searches' kernels finish
+ * (optional; a pool thread that retires should call it). */
 int mqvs_thread_release(void);
 /* Library shutdown for the calling thread (SURVEY 8(b) lifecycle): waits for
  * the thread's streams and releases its workspaces, as mqvs_thread_release.

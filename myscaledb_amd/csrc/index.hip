@@ -82,6 +82,11 @@ constexpr int64_t kCoarseFlatLists = 16384;  // more lists: the coarse step is a
 // plan / scan / select buffers of one list pass
 struct ListBufs {
     DevBuf lcount, lfill, lstart, lq, items, grp, chk, nitems, qbase, qstart, cand, stats, large;
+    void release() {
+        for (DevBuf *b : {&lcount, &lfill, &lstart, &lq, &items, &grp, &chk, &nitems, &qbase, &qstart, &cand, &stats,
+                          &large})
+            b->release();
+    }
 };
 
 struct IndexWorkspace {
@@ -102,9 +107,43 @@ struct IndexWorkspace {
         MQVS_HIP(hipStreamCreateWithFlags(&side, hipStreamNonBlocking));
         MQVS_HIP(hipHostMalloc((void **)&host, 8 * sizeof(int64_t), hipHostMallocDefault));
     }
+    // after the last search's kernels (ev[5] ends every search, ASYNC ones
+    // included; the side stream's chain is joined before it)
+    void release() {
+        if (!ev[0]) return;
+        (void)hipEventSynchronize(ev[5]);
+        if (side) (void)hipStreamSynchronize(side);
+        for (DevBuf *b : {&queries, &qvars, &qnorms, &qmu, &qlam, &status, &qhi, &probes, &cprobes, &filter, &exists,
+                          &rows, &out_ids, &out_dist, &ord, &dmap, &dwords, &pdist, &cqhi, &gmax})
+            b->release();
+        coarse.release();
+        fine.release();
+        for (auto &e : ev) {
+            (void)hipEventDestroy(e);
+            e = nullptr;
+        }
+        (void)hipEventDestroy(fork);
+        (void)hipEventDestroy(join);
+        (void)hipStreamDestroy(side);
+        (void)hipHostFree(host);
+        fork = join = nullptr;
+        side = nullptr;
+        host = nullptr;
+    }
 };
 
 static thread_local std::map<int, IndexWorkspace> *g_iws = nullptr;
+
+// mqvs_thread_release: the calling thread's index workspaces (scratch,
+// events, side stream, pinned words)
+void index_thread_release() {
+    if (!g_iws) return;
+    for (auto &kv : *g_iws) {
+        (void)hipSetDevice(kv.first);
+        kv.second.release();
+    }
+    g_iws->clear();
+}
 
 static IndexWorkspace &index_workspace(int device) {
     if (!g_iws) g_iws = new std::map<int, IndexWorkspace>();  // leaked at exit on purpose

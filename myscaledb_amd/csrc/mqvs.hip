@@ -1647,6 +1647,7 @@ int mqvs_device_count(int *count) {
 
 int mqvs_thread_release(void) {
     return guarded([&] {
+        index_thread_release();
         if (!g_ws) return;
         for (auto &kv : *g_ws) {
             (void)hipSetDevice(kv.first);

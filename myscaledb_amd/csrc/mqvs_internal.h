@@ -455,6 +455,7 @@ constexpr int kCoarsePickMaxT = 64;  // groups a coarse pick may take per query
 // (kernels_ivf.hip): per query the T best groups (T <= 64), the exact values
 // of their centroids (coarse metric: L2 or kMetricIpRaw), the nprobe best ->
 // probes[q][0, nprobe) (-1 when fewer)
+void index_thread_release();  // index.hip: the calling thread's index workspaces
 void launch_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T, int nprobe, int metric,
                         const float *q, int64_t qld, const float *cent, const float *cnorm, int64_t ncent, int d,
                         int nq, int64_t *probes, hipStream_t s);

@@ -139,6 +139,37 @@ def test_index_cosine_long_normalisation_chains(mq, nq):
         assert np.array_equal(b.view(np.uint32), do.view(np.uint32))
 
 
+def test_index_search_after_thread_release(mq):
+    """mqvs_thread_release also frees the calling thread's index workspace
+    (scratch, events, the variant chain's side stream): searches before and
+    after it, from this thread and from a fresh one, return the same bits."""
+    import threading
+    from myscaledb_amd import _lib
+    n, d, nq, k = 20000, 96, 40, 30
+    seg = mq.VectorScanSegment.generate(0x5EED0001, 2, n, d, metric="Cosine")
+    q = O.generate(0x5EED0001, 2, n, nq, d)
+    idx = mq.VectorIndex.build(seg, "MSTG", {"nlist": 64})
+    out = {}
+    try:
+        out["a"] = idx.search(q, k, {"nprobe": 4})
+        _lib.check(_lib.lib.mqvs_thread_release())
+        out["b"] = idx.search(q, k, {"nprobe": 4})
+
+        def worker():
+            out["c"] = idx.search(q, k, {"nprobe": 4})
+            _lib.check(_lib.lib.mqvs_thread_release())
+
+        t = threading.Thread(target=worker)
+        t.start()
+        t.join()
+    finally:
+        idx.free()
+        seg.free()
+    for key in ("b", "c"):
+        assert np.array_equal(out[key][0], out["a"][0]), key
+        assert np.array_equal(out[key][1].view(np.uint32), out["a"][1].view(np.uint32)), key
+
+
 @pytest.mark.parametrize("metric", ["L2", "IP", "Cosine"])
 def test_index_recall_default_params(mq, metric):
     """Gaussian-mixture part, default nlist / alpha: recall@10 >= 0.95 against
