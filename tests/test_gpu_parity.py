@@ -234,6 +234,45 @@ def run_parity(mq, cfg):
     assert_bitwise(ids_g, dist_g, ids_o, dist_o, name)
 
 
+@pytest.mark.parametrize("metric", ["L2", "IP", "Cosine"])
+@pytest.mark.parametrize("sel", [0.01, 0.1])
+def test_gather_unaligned_device_bitmaps(mq, metric, sel):
+    """Device filter and delete bitmaps at byte offsets 1 and 3 (the
+    word-per-lane selection kernels fall back to byte loads), a granule of 1000
+    rows (chunks not on 32-row words) and a part whose length is not a whole
+    word: the gather list (dense for L2/IP, per-chunk padded for cosine), the
+    masked scan and the oracle agree bit for bit."""
+    import torch
+    from myscaledb_amd.vector_scan import set_gather_mode
+    n, d, nq, k, gran = 50021, 64, 3, 40, 1000
+    rows = O.generate(0x5EED0001, 1, 0, n, d)
+    queries = O.generate(0x5EED0002, 1, 0, nq, d)
+    rng = np.random.default_rng(int(sel * 1000) + len(metric))
+    flt = mq.pack_bitmap(rng.random(n) < sel)
+    rex = mq.pack_bitmap(rng.random(n) >= 0.1)
+    io, do = O.vector_scan(rows, queries, k, O.METRICS[metric], gran, filter_bits=flt, row_exists_bits=rex,
+                           fast=True)
+
+    def at_offset(bits, off):
+        buf = torch.zeros(len(bits) + 8, dtype=torch.uint8, device="cuda")
+        buf[off:off + len(bits)] = torch.from_numpy(np.ascontiguousarray(bits)).cuda()
+        return buf[off:off + len(bits)]
+
+    fdev, edev = at_offset(flt, 1), at_offset(rex, 3)
+    assert fdev.data_ptr() % 4 == 1 and edev.data_ptr() % 4 == 3
+    q = torch.from_numpy(queries).cuda()
+    seg = mq.VectorScanSegment.from_rows(rows, metric=metric, granule=gran)
+    try:
+        for gmode in (2, 0):
+            set_gather_mode(gmode)
+            ids, dist = seg.search(q, k, metric, fdev, edev)
+            torch.cuda.synchronize()
+            assert_bitwise(ids.cpu().numpy(), dist.cpu().numpy(), io, do, f"{metric} sel {sel} gather {gmode}")
+    finally:
+        set_gather_mode(1)
+        seg.free()
+
+
 def test_knn_raw_matches_oracle(mq):
     """tryBruteForceSearch contract: faiss layout, raw IP (negatives kept)."""
     rng = np.random.default_rng(7)
