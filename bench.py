@@ -49,6 +49,13 @@ def parse():
                     help="launch only: every rank prints its RANK / LOCAL_RANK / WORLD_SIZE and exits (no GPU)")
     ap.add_argument("--no-config3-sharded", action="store_true",
                     help="N > 1: skip the configs[3] (100M x 1536 IP over 8 GPUs) leg")
+    ap.add_argument("--loopback", type=int, default=0,
+                    help="rehearse the N-rank sequence of --gpus N on ONE GPU: N virtual ranks (threads) over a "
+                         "loopback communicator (mqvs_comm_init_loopback); prints the N-rank lines")
+    ap.add_argument("--config3-rows", type=int, default=0,
+                    help="configs[3] rows per rank (default: 12.5M per GPU, the full 100M part at N = 8)")
+    ap.add_argument("--inject-leg-failure", default="",
+                    help="testing: 'config3:R' makes rank R fail the configs[3] leg (fail-soft drill)")
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--n", type=int, default=10_000_000)
@@ -647,97 +654,196 @@ def configs_leg(mq, mq_scan, args):
     return out
 
 
-def _max_over_ranks(x):
-    import torch
-    import torch.distributed as tdist
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-    return float(t.item())
+# ---------------------------------------------------------------------------
+# ranks: one process per GPU (torch.distributed) or, for the one-GPU
+# rehearsal, one thread per virtual rank of a loopback communicator
+
+class LegError(Exception):
+    """A leg step failed on some rank: every rank raises it together."""
 
 
-def sharded_point(comm, seg, q, k, reps, mq_scan):
+class DistCtx:
+    """Rank of a torch.distributed job (one process per GPU)."""
+
+    def __init__(self, rank, world):
+        import torch.distributed as tdist
+        self.tdist, self.rank, self.world = tdist, rank, world
+
+    def barrier(self):
+        self.tdist.barrier()
+
+    def max(self, x):
+        import torch
+        t = torch.tensor([float(x)], dtype=torch.float64, device="cuda")
+        self.tdist.all_reduce(t, op=self.tdist.ReduceOp.MAX)
+        return float(t.item())
+
+    def all_ok(self, ok):
+        return self.max(0.0 if ok else 1.0) == 0.0
+
+    def process_wide(self, fn):
+        fn()  # (every process holds its own library state)
+
+
+class LoopShared:
+    def __init__(self, n, timeout=900.0):
+        import threading
+        self.n = n
+        self.bar = threading.Barrier(n, timeout=timeout)
+        self.vals = [0.0] * n
+
+
+class LoopCtx:
+    """Virtual rank r of a loopback group: a thread of this process.  The
+    library's process-wide switches (timing, batch mode) are set once by rank
+    0 between barriers.  A barrier times out (BrokenBarrierError) rather than
+    hang when a rank dies outside a step."""
+
+    def __init__(self, shared, rank):
+        self.sh, self.rank, self.world = shared, rank, shared.n
+
+    def barrier(self):
+        self.sh.bar.wait()
+
+    def max(self, x):
+        self.sh.vals[self.rank] = float(x)
+        self.sh.bar.wait()
+        m = max(self.sh.vals)
+        self.sh.bar.wait()
+        return m
+
+    def all_ok(self, ok):
+        return self.max(0.0 if ok else 1.0) == 0.0
+
+    def process_wide(self, fn):
+        self.sh.bar.wait()
+        if self.rank == 0:
+            fn()
+        self.sh.bar.wait()
+
+
+def step_all(ctx, fn, what):
+    """fn() on every rank, then one collective status: all ranks return, or
+    all raise LegError together (a rank's failure before a collective would
+    otherwise leave the others waiting in it)."""
+    try:
+        r, err = fn(), None
+    except Exception as e:  # noqa: BLE001
+        r, err = None, f"{what}: {type(e).__name__}: {e}"
+    if not ctx.all_ok(err is None):
+        raise LegError(err or f"{what}: failed on another rank")
+    return r
+
+
+def sharded_point(ctx, comm, seg, q, k, reps, mq_scan):
     """One batch size through mqvs_sharded_search on every rank: the first
     call runs the validated path, the timed ones the one-sync fast path; the
     time is the slowest rank's.  Then the same sharded search on the exact
     fp32 path of every rank (mqvs_set_batch_mode(1)) and the timed output
     compared with it on ALL queries (ids and distance bits, every rank)."""
     import torch
-    import torch.distributed as tdist
     nq = q.shape[0]
     ids = torch.empty((nq, k), dtype=torch.int64, device="cuda")
     dst = torch.empty((nq, k), dtype=torch.float32, device="cuda")
     for _ in range(2):
         comm.sharded_search(seg, q, k, out=(ids, dst))
     before = comm.stats()
-    tdist.barrier()
+    ctx.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(reps):
         comm.sharded_search(seg, q, k, out=(ids, dst))
     torch.cuda.synchronize()
-    ms = _max_over_ranks((time.perf_counter() - t0) * 1e3 / reps)
+    ms = ctx.max((time.perf_counter() - t0) * 1e3 / reps)
     after = comm.stats()
-    mq_scan.set_batch_mode(1)
+    ctx.process_wide(lambda: mq_scan.set_batch_mode(1))
     try:
         ei, ed = comm.sharded_search(seg, q, k)
     finally:
-        mq_scan.set_batch_mode(0)
+        ctx.process_wide(lambda: mq_scan.set_batch_mode(0))
     same = bool(torch.equal(ids, ei)) and bool(torch.equal(dst.view(torch.int32), ed.view(torch.int32)))
-    all_same = _max_over_ranks(0.0 if same else 1.0) == 0.0
+    all_same = ctx.max(0.0 if same else 1.0) == 0.0
     return {"nq": nq, "ms_per_search": round(ms, 3), "qps": round(nq / (ms * 1e-3), 1),
             "fast_path_calls": after["fast_calls"] - before["fast_calls"],
             "redo_calls": after["redo_calls"] - before["redo_calls"],
             "exact": {"queries": nq, "ids_and_dist_bits_equal_on_every_rank": all_same}}
 
 
-def sharded_legs(mq, mq_scan, comm, seg, args, rank, world):
+def sharded_legs(ctx, mq, mq_scan, comm, seg, args):
     """N > 1, on every rank (collectives): the small batches of the configs[1]
     part through the sharded path, then BASELINE configs[3] -- FLAT IP over a
     1536-d part, 12.5M rows per GPU generated in HBM: the full 100M x 1536
     part at N >= 8, a 12.5M x N subset below (100M needs >= 8
-    shards of this size) -- at nq 1 / 16 / 1000, each point checked against
-    the exact path on every query."""
+    shards of this size; the loopback rehearsal uses --config3-rows per
+    virtual rank) -- at nq 1 / 16 / 1000, each point checked against the exact
+    path on every query.  A leg that fails on any rank is recorded as
+    {"error": ...} on every rank (step_all) and the next leg runs."""
     import torch
     from myscaledb_amd.sharded import shard_rows
     from myscaledb_amd.vector_scan import generate_device
+    rank, world = ctx.rank, ctx.world
     out = {}
-    pts = []
-    for nq in (1, 16):
-        q = torch.empty((nq, args.d), dtype=torch.float32, device="cuda")
-        generate_device(SEED_QUERY, args.mode, 0, nq, args.d, q)
-        e = sharded_point(comm, seg, q, args.k, 20, mq_scan)
-        plane = 2.0 * args.n * seg_dpad(args.d)
-        e["aggregate_plane_tb_s"] = round(plane / (e["ms_per_search"] * 1e-3) / 1e12, 3)
-        pts.append(e)
-    out["small_batch_sharded"] = pts
+
+    def small():
+        pts = []
+        for nq in (1, 16):
+            q = step_all(ctx, lambda: _queries(args.mode, nq, args.d), "small-batch queries")
+            e = step_all(ctx, lambda: sharded_point(ctx, comm, seg, q, args.k, 20, mq_scan), f"sharded nq {nq}")
+            plane = 2.0 * args.n * seg_dpad(args.d)
+            e["aggregate_plane_tb_s"] = round(plane / (e["ms_per_search"] * 1e-3) / 1e12, 3)
+            pts.append(e)
+        return pts
+
+    try:
+        out["small_batch_sharded"] = small()
+    except LegError as e:
+        out["small_batch_sharded"] = {"error": str(e)}
     if args.no_config3_sharded:
         return out
-    d3, per = 1536, 12_500_000
-    total = 100_000_000 if world >= 8 else per * world
+    d3 = 1536
+    per = args.config3_rows or 12_500_000
+    total = 100_000_000 if (world >= 8 and not args.config3_rows) else per * world
     r0, r1 = shard_rows(total, args.granule, rank, world)
-    seg3 = mq.VectorScanSegment.generate(SEED_BASE, 1, r1 - r0, d3, "IP", args.granule, row_offset=r0)
+    seg3 = None
+
+    def gen3():
+        if args.inject_leg_failure == f"config3:{rank}":
+            raise RuntimeError("injected failure (--inject-leg-failure)")
+        return mq.VectorScanSegment.generate(SEED_BASE, 1, r1 - r0, d3, "IP", args.granule, row_offset=r0)
+
     try:
+        seg3 = step_all(ctx, gen3, "config3 shard generation")
         pts = []
         for nq in (1, 16, 1000):
-            q = torch.empty((nq, d3), dtype=torch.float32, device="cuda")
-            generate_device(SEED_QUERY, 1, 0, nq, d3, q)
-            e = sharded_point(comm, seg3, q, 100, 5 if nq == 1000 else 10, mq_scan)
+            q = step_all(ctx, lambda: _queries(1, nq, d3), "config3 queries")
+            e = step_all(ctx, lambda: sharded_point(ctx, comm, seg3, q, 100, 5 if nq == 1000 else 10, mq_scan),
+                         f"config3 nq {nq}")
             plane = 2.0 * total * seg_dpad(d3)
             e["plane_bytes_read"] = plane
             e["aggregate_plane_tb_s"] = round(plane / (e["ms_per_search"] * 1e-3) / 1e12, 3)
             e["frac_of_n_x_8tbs"] = round(plane / (e["ms_per_search"] * 1e-3) / 1e9 / (HBM_PEAK_GBS * world), 4)
             pts.append(e)
+        out["config3_sharded"] = {
+            "workload": (f"FLAT IP {total / 1e6:g}M x {d3} (N(0,1)) over {world} ranks, top-100, "
+                         + ("BASELINE configs[3] at full size" if total == 100_000_000 else
+                            f"scaled subset of BASELINE configs[3]'s 100M rows: {per / 1e6:g}M rows per rank")),
+            "rows": total, "rows_per_rank0": r1 - r0 if rank == 0 else None, "full_size": total == 100_000_000,
+            "points": pts}
+    except LegError as e:
+        out["config3_sharded"] = {"error": str(e)}
     finally:
-        seg3.free()
+        if seg3 is not None:
+            seg3.free()
         torch.cuda.synchronize()
-        torch.cuda.empty_cache()
-    out["config3_sharded"] = {
-        "workload": (f"FLAT IP {total / 1e6:g}M x {d3} (N(0,1)) over {world} GPUs, top-100, "
-                     + ("BASELINE configs[3] at full size" if total == 100_000_000 else
-                        f"scaled subset of BASELINE configs[3]'s 100M rows: {per / 1e6:g}M rows per GPU")),
-        "rows": total, "rows_per_gpu_rank0": r1 - r0 if rank == 0 else None, "full_size": total == 100_000_000,
-        "points": pts}
     return out
+
+
+def _queries(mode, nq, d):
+    import torch
+    from myscaledb_amd.vector_scan import generate_device
+    q = torch.empty((nq, d), dtype=torch.float32, device="cuda")
+    generate_device(SEED_QUERY, mode, 0, nq, d, q)
+    return q
 
 
 def launch_ranks(args):
@@ -754,8 +860,359 @@ def launch_ranks(args):
     return subprocess.run(cmd, env=dict(os.environ)).returncode
 
 
+# keys of the line's `roofline` kept first (the driver's record keeps about
+# 20 keys of a nested dict): the north-star nq = 1 scalars right after the
+# contract's own; everything else goes to `roofline_detail`
+ROOF_KEYS = ("bound", "kernel", "achieved", "peak", "unit", "frac", "traffic",
+             "nq1_frac_8tbs", "nq1_frac_end_to_end_8tbs", "nq1_ms", "nq1_ms_end_to_end", "nq1_pmc_over_plane",
+             "nq1_exact", "traffic_over_plane", "pmc_mfma_busy_frac", "pmc_clock_ghz", "survey_t_star_over_t",
+             "l2_to_lds_tb_s", "traffic_source", "flop_definition")
+
+
+def split_roofline(roof):
+    """(roofline with at most 20 keys in ROOF_KEYS order, the rest)."""
+    head = {k: roof[k] for k in ROOF_KEYS if k in roof}
+    if "kernel" in head and isinstance(head["kernel"], str) and len(head["kernel"]) > 100:
+        head["kernel"] = head["kernel"][:97] + "..."
+    rest = {k: v for k, v in roof.items() if k not in head or k == "kernel"}
+    return head, rest
+
+
+def emit(result):
+    out = dict(result)
+    if "roofline" in out:
+        head, rest = split_roofline(out["roofline"])
+        out["roofline"] = head
+        out["roofline_detail"] = rest
+    print(json.dumps(out), flush=True)
+
+
+def run_leg(result, name, fn):
+    """An optional single-GPU leg: its failure is recorded in the line
+    instead of losing the line."""
+    try:
+        result[name] = fn()
+    except Exception as e:  # noqa: BLE001
+        result[name] = {"error": f"{type(e).__name__}: {e}"}
+        import torch
+        torch.cuda.synchronize()
+
+
+def headline(args, ms, st, roof, exact, n_ranks, exchange, world, extra_config=None):
+    n, d, nq, k, g = args.n, args.d, args.nq, args.k, args.granule
+    qps = nq / (ms / 1000.0)
+    pf = st.get("prefilter") if st["path"] == 2 else None
+    compute = ("bf16-hi MFMA pre-filter (one bf16 product, rigorous error bound from measured residual norms) + "
+               "exact f32 fma-chain re-rank of the survivors") if pf == 2 else (
+        "f32 MFMA fma chain" if st["path"] == 1 else "f32 VALU, product then add")
+    cfg = {"workload": f"FLAT {args.metric} {n // 1_000_000}M x {d} Float32, batch {nq}, "
+                       f"top-{k} (BASELINE configs[1])",
+           "n": n, "d": d, "nq": nq, "k": k, "metric": args.metric, "generator_mode": args.mode,
+           "granule_rows": g, "parallelism": f"row-range shards x{world}", "exchange": exchange}
+    cfg.update(extra_config or {})
+    return {
+        "metric": "QPS (FLAT brute force, batch top-k)",
+        "value": round(qps, 2),
+        "unit": "queries/s",
+        "n_gpus": n_ranks,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 3),
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "roofline": roof,
+        "compute": compute,
+        "data": "synthetic (counter-based %s, generated in HBM)" % {
+            0: "exact integers in [-8, 8]", 1: "N(0,1)", 2: "gaussian mixture, 4096 centres",
+            3: "gaussian mixture, 65536 centres, unit noise"}[args.mode],
+        "config": cfg,
+        "mdist_per_s": round(nq * n / (ms / 1000.0) / 1e6, 1),
+        "recall_at_10": exact["recall_at_10"] if exact and "recall_at_10" in exact else None,
+        "exact_check": exact,
+        "stats_last_step": {kk: (round(v, 3) if isinstance(v, float) else v) for kk, v in st.items()},
+    }
+
+
+def rank_main(ctx, args, comm, exchange, loopback=0):
+    """N > 1 (processes over RCCL, or threads over the loopback transport):
+    each rank searches its granule-aligned row-range shard of the configs[1]
+    part, the per-shard top-k are exchanged and merged inside libmqvs.  Rank
+    0 prints the headline line as soon as it is measured, then the line again
+    with the optional legs (a leg failing on any rank is recorded, not fatal)."""
+    import torch
+    import myscaledb_amd as mq
+    import myscaledb_amd.vector_scan as mq_scan
+    from myscaledb_amd import _lib
+    from myscaledb_amd.sharded import shard_rows
+    from myscaledb_amd.vector_scan import merge_shards
+    rank, world = ctx.rank, ctx.world
+    n, d, nq, k, g = args.n, args.d, args.nq, args.k, args.granule
+    r0, r1 = shard_rows(n, g, rank, world)
+    seg = mq.VectorScanSegment.generate(SEED_BASE, args.mode, r1 - r0, d, args.metric, g, row_offset=r0)
+    q = _queries(args.mode, nq, d)
+    f_ids = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+    f_dst = torch.empty((nq, k), dtype=torch.float32, device="cuda")
+    if comm is None:
+        # (torch.distributed fallback exchange: the library's communicator
+        # could not be set up)
+        import torch.distributed as tdist
+        ids = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+        dst = torch.empty((nq, k), dtype=torch.float32, device="cuda")
+        g_ids = torch.empty((world, nq, k), dtype=torch.int64, device="cuda")
+        g_dst = torch.empty((world, nq, k), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+
+    def step():
+        if comm is not None:
+            comm.sharded_search(seg, q, k, out=(f_ids, f_dst))
+            return
+        seg.search(q, k, out=(ids, dst))
+        tdist.all_gather_into_tensor(g_ids, ids)
+        tdist.all_gather_into_tensor(g_dst, dst)
+        merge_shards(g_ids, g_dst, args.metric, out=(f_ids, f_dst))
+
+    for _ in range(args.warmup):
+        step()
+    ctx.process_wide(lambda: mq_scan.set_timing(True))
+    before = comm.stats() if comm is not None else None
+    stats = []
+    ctx.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+        stats.append(_lib.last_search_stats())
+    torch.cuda.synchronize()
+    ctx.barrier()
+    ms = ctx.max((time.perf_counter() - t0) * 1000.0 / args.steps)
+    ctx.process_wide(lambda: mq_scan.set_timing(False))
+    after = comm.stats() if comm is not None else None
+
+    main_ms = float(np.mean([s["main_ms"] for s in stats]))
+    st = stats[-1]
+    roof = roofline(st, main_ms, nq, d, args)
+    t_star = max((4.0 * n * d + 4.0 * nq * d + 12.0 * nq * k) / (HBM_PEAK_GBS * 1e9),
+                 2.0 * nq * n * d / (FP32_MFMA_PEAK_TFLOPS * 1e12))
+    roof["survey_t_star_ms"] = round(t_star * 1e3, 3)
+    roof["survey_t_star_over_t"] = round(t_star * 1e3 / ms, 3)
+
+    # exactness at full size, outside the timed region: the timed (merged)
+    # output against the same sharded search on every rank's exact fp32 path
+    exact = None
+    if not args.no_verify:
+        def check():
+            ctx.process_wide(lambda: mq_scan.set_batch_mode(1))
+            try:
+                if comm is not None:
+                    xi, xd = comm.sharded_search(seg, q, k)
+                else:
+                    ei, ed = seg.search(q, k)
+                    tdist.all_gather_into_tensor(g_ids, ei)
+                    tdist.all_gather_into_tensor(g_dst, ed)
+                    xi, xd = merge_shards(g_ids, g_dst, args.metric)
+            finally:
+                ctx.process_wide(lambda: mq_scan.set_batch_mode(0))
+            gi, gd, xi, xd = f_ids.cpu().numpy(), f_dst.cpu().numpy(), xi.cpu().numpy(), xd.cpu().numpy()
+            k10 = min(10, k)
+            return {"queries": nq, "ids_equal": bool(np.array_equal(gi, xi)),
+                    "dist_bitwise_equal": bool(np.array_equal(gd.view(np.uint32), xd.view(np.uint32))),
+                    "recall_at_10": round(float(np.mean([len(set(gi[i, :k10]) & set(xi[i, :k10]))
+                                                         for i in range(nq)]) / k10), 6)}
+        try:
+            exact = step_all(ctx, check, "exact check")
+        except LegError as e:
+            exact = {"error": str(e)}
+
+    result = None
+    if rank == 0:
+        extra = {"loopback_virtual_ranks": loopback} if loopback else {}
+        result = headline(args, ms, st, roof, exact, 1 if loopback else world, exchange, world, extra)
+        if loopback:
+            result["metric"] = "QPS (FLAT brute force, batch top-k) -- loopback rehearsal of the N-rank path on 1 GPU"
+            result["note"] = (f"{loopback} virtual ranks (threads) share ONE GPU: the value is not a scaling "
+                              "point; it exercises the sharded code path end to end")
+        if comm is not None:
+            result["fast_path_calls"] = after["fast_calls"] - before["fast_calls"]
+            result["redo_calls"] = after["redo_calls"] - before["redo_calls"]
+        emit(result)  # the headline first: a later leg cannot lose it
+    legs = sharded_legs(ctx, mq, mq_scan, comm, seg, args) if comm is not None else {}
+    if rank == 0:
+        result.update(legs)
+        emit(result)
+    ctx.barrier()
+    seg.free()
+    return 0
+
+
+def loopback_main(args):
+    """--loopback N: the N-rank sequence of `--gpus N` on ONE GPU -- one
+    process, mqvs_comm_init_loopback(N), one thread (and HIP stream) per
+    virtual rank, the exchange done as device copies by the same
+    mqvs_sharded_search code an RCCL communicator runs."""
+    import threading
+    import torch
+    torch.cuda.set_device(0)
+    import myscaledb_amd as mq
+    from myscaledb_amd import _lib
+    from myscaledb_amd.sharded import LoopbackComm
+    mq.init(0)
+    if not args.config3_rows:
+        args.config3_rows = 1_500_000  # (N virtual ranks share one GPU's HBM)
+    comms = LoopbackComm.group(args.loopback)
+    shared = LoopShared(args.loopback)
+    errs = []
+
+    def worker(r):
+        try:
+            mq.init(0)
+            with torch.cuda.stream(torch.cuda.Stream()):
+                rank_main(LoopCtx(shared, r), args, comms[r],
+                          f"mqvs_sharded_search over a {args.loopback}-rank loopback communicator "
+                          "(device copies between host barriers)", loopback=args.loopback)
+            _lib.check(_lib.lib.mqvs_thread_release())
+        except BaseException as e:  # noqa: BLE001
+            errs.append(f"rank {r}: {type(e).__name__}: {e}")
+            shared.bar.abort()
+
+    threads = [threading.Thread(target=worker, args=(r,)) for r in range(args.loopback)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    for c in comms:
+        c.free()
+    if errs:
+        print("\n".join(errs), file=sys.stderr, flush=True)
+        return 1
+    return 0
+
+
+def single_main(args):
+    import torch
+    import myscaledb_amd as mq
+    import myscaledb_amd.vector_scan as mq_scan
+    from myscaledb_amd import _lib
+    from myscaledb_amd.vector_scan import set_timing
+    n, d, nq, k, g = args.n, args.d, args.nq, args.k, args.granule
+    seg = mq.VectorScanSegment.generate(SEED_BASE, args.mode, n, d, args.metric, g)
+    q = _queries(args.mode, nq, d)
+    ids = torch.empty((nq, k), dtype=torch.int64, device="cuda")
+    dst = torch.empty((nq, k), dtype=torch.float32, device="cuda")
+    torch.cuda.synchronize()
+
+    for _ in range(args.warmup):
+        seg.search(q, k, out=(ids, dst))  # returns after its stream drained
+    set_timing(True)
+    stats = []
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        seg.search(q, k, out=(ids, dst))
+        stats.append(_lib.last_search_stats())
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    set_timing(False)
+    ms = (t1 - t0) * 1000.0 / args.steps
+
+    main_ms = float(np.mean([s["main_ms"] for s in stats]))
+    st = stats[-1]
+    roof = roofline(st, main_ms, nq, d, args)
+    # SURVEY.md 8(d): T* = max(bytes / HBM, flops / fp32 MFMA) for the whole step
+    t_star = max((4.0 * n * d + 4.0 * nq * d + 12.0 * nq * k) / (HBM_PEAK_GBS * 1e9),
+                 2.0 * nq * n * d / (FP32_MFMA_PEAK_TFLOPS * 1e12))
+    roof["survey_t_star_ms"] = round(t_star * 1e3, 3)
+    roof["survey_t_star_over_t"] = round(t_star * 1e3 / ms, 3)
+    # exactness at full size, outside the timed region: the timed path's
+    # output against the exact fp32 path on every query
+    exact = None if args.no_verify else exact_check(mq_scan, seg, q, k, ids, dst)
+    result = headline(args, ms, st, roof, exact, 1, None, 1)
+
+    if args.read_sweep_gib > 0:
+        # the measured HBM read peak of this device (same process, same GPU):
+        # the denominator of frac_measured_peak below
+        def sweep():
+            gbs, bms = mq_scan.measure_read_bandwidth(int(args.read_sweep_gib * (1 << 30)), 5)
+            return {"gbs": round(gbs, 1), "bytes": int(args.read_sweep_gib * (1 << 30)),
+                    "best_ms": round(bms, 3), "frac_of_8tbs": round(gbs / HBM_PEAK_GBS, 4),
+                    "kernel": "best of k_read_sweep (16 B per lane, 4 loads in flight, grid-stride, "
+                              "8 workgroups per CU) and k_read_slices (a contiguous slice per "
+                              "workgroup, 8 or 16 non-temporal 16-B loads in flight per lane, "
+                              "2-8 workgroups per CU)"}
+        run_leg(result, "hbm_read_sweep", sweep)
+    if not args.no_small:
+        run_leg(result, "small_batch", lambda: small_batch_leg(mq_scan, seg, args))
+        p1 = [x for x in result["small_batch"] if x.get("nq") == 1] if isinstance(result["small_batch"], list) else []
+        if p1:
+            # the north-star nq = 1 point (SURVEY 8(d)): HBM-bound scan of the
+            # bf16 plane, against 8 TB/s and the measured read peak
+            p1 = p1[0]
+            plane = p1["bytes_read"]
+            nq1 = {"ms": p1["main_ms"], "ms_end_to_end": p1["ms_per_search"], "plane_bytes": plane,
+                   "kernel": "k_scan_hi_reg (bf16 16x16x32, operands straight from HBM into registers)",
+                   "achieved_gbs": p1["main_gbs"], "frac_8tbs": p1["hbm_frac_main"],
+                   "frac_end_to_end_8tbs": p1["hbm_frac_end_to_end"], "exact": p1["exact"]["ids_equal"] and
+                   p1["exact"]["dist_bitwise_equal"]}
+            sw = result.get("hbm_read_sweep")
+            if isinstance(sw, dict) and "gbs" in sw:
+                nq1["measured_peak_gbs"] = sw["gbs"]
+                nq1["frac_measured_peak"] = round(p1["main_gbs"] / sw["gbs"], 4)
+            pm = _pmc_kernel(args.pmc_nq1 or os.path.join(ROOT, PMC_NQ1_DEFAULT), "k_scan_hi_reg", 1, sum_all=True)
+            if pm:
+                nq1["pmc_hbm_bytes"] = round(pm["hbm_bytes_per_search"])
+                nq1["pmc_over_plane"] = round(pm["hbm_bytes_per_search"] / plane, 4)
+                nq1["pmc_source"] = pm["source"]
+            result["roofline"]["nq1"] = nq1
+            # (scalars in the roofline dict: the driver's record keeps its
+            # first ~20 keys, ROOF_KEYS orders them)
+            for key, val in (("nq1_ms", nq1["ms"]), ("nq1_ms_end_to_end", nq1["ms_end_to_end"]),
+                             ("nq1_frac_8tbs", nq1["frac_8tbs"]),
+                             ("nq1_frac_end_to_end_8tbs", nq1["frac_end_to_end_8tbs"]),
+                             ("nq1_pmc_over_plane", nq1.get("pmc_over_plane")),
+                             ("nq1_frac_measured_peak", nq1.get("frac_measured_peak")),
+                             ("nq1_exact", nq1["exact"])):
+                result["roofline"][key] = val
+    if not args.no_cpu:
+        # the CPU leg: the oracle (the reference's CPU path restated) timed on
+        # the host cores, and -- as the checker only -- its formula on sampled
+        # rows of the timed output (pins the exact path)
+        def cpu():
+            O = _oracle()
+            cb = cpu_baseline(O, args)
+            cb["one_thread_qps"] = cb["one_thread"]["qps"]
+            if not args.no_verify:
+                ok, nchk = verify_sample(O, ids.cpu().numpy(), dst.cpu().numpy(), q.cpu().numpy(), args)
+                result["oracle_sample"] = {"queries": nchk, "bitwise_and_no_better_sample": ok}
+            return cb
+        run_leg(result, "cpu_baseline", cpu)
+    if not args.no_index:
+        run_leg(result, "index", lambda: index_leg(mq, seg, args))
+    risk = os.path.join(ROOT, BLAS_RISK_DEFAULT)
+    if os.path.exists(risk):
+        # parity risk of the unpinned BLAS-branch order (tools/blas_order_risk.py,
+        # committed run of this config): queries whose top-k would change if
+        # faiss's sgemm blocked K
+        with open(risk) as f:
+            rk = json.load(f)
+        result["blas_order_risk"] = dict(rk, source=os.path.relpath(risk, ROOT))
+    seg.free()  # (room for the next parts)
+    torch.cuda.synchronize()
+    torch.cuda.empty_cache()
+    if not args.no_config1_points:
+        run_leg(result, "config1_points", lambda: config1_points(mq, mq_scan, args))
+    if not args.no_configs:
+        run_leg(result, "configs", lambda: configs_leg(mq, mq_scan, args))
+    emit(result)
+
+
 def main():
     args = parse()
+    if args.loopback:
+        if args.dry_run:
+            print(json.dumps({"dry_run": True, "loopback": args.loopback}), flush=True)
+            return
+        sys.exit(loopback_main(args))
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(launch_ranks(args))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -767,217 +1224,30 @@ def main():
         return
     import torch
     torch.cuda.set_device(local)
-    dist_on = world > 1
-    if dist_on:
-        import torch.distributed as tdist
-        tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
     import myscaledb_amd as mq
-    from myscaledb_amd import _lib
-    from myscaledb_amd.vector_scan import generate_device, merge_shards, set_timing
-
+    if world == 1:
+        mq.init(local)
+        single_main(args)
+        return
+    import torch.distributed as tdist
+    tdist.init_process_group("nccl", device_id=torch.device("cuda", local))
     mq.init(local)
-    n, d, nq, k, g = args.n, args.d, args.nq, args.k, args.granule
-    from myscaledb_amd.sharded import shard_rows
-    r0, r1 = shard_rows(n, g, rank, world)
-    seg = mq.VectorScanSegment.generate(SEED_BASE, args.mode, r1 - r0, d, args.metric, g, row_offset=r0)
-    q = torch.empty((nq, d), dtype=torch.float32, device="cuda")
-    generate_device(SEED_QUERY, args.mode, 0, nq, d, q)
-    ids = torch.empty((nq, k), dtype=torch.int64, device="cuda")
-    dst = torch.empty((nq, k), dtype=torch.float32, device="cuda")
-    if dist_on:
-        g_ids = torch.empty((world, nq, k), dtype=torch.int64, device="cuda")
-        g_dst = torch.empty((world, nq, k), dtype=torch.float32, device="cuda")
-        f_ids = torch.empty((nq, k), dtype=torch.int64, device="cuda")
-        f_dst = torch.empty((nq, k), dtype=torch.float32, device="cuda")
-    torch.cuda.synchronize()
-    # N > 1: libmqvs's own exchange (mqvs_sharded_search: RCCL all-gather of
-    # the per-shard top-k + device merge); torch.distributed's all_gather +
+    # libmqvs's own exchange (mqvs_sharded_search: RCCL all-gather of the
+    # per-shard top-k + device merge); torch.distributed's all_gather +
     # mqvs_merge_shards if that communicator cannot be set up
     comm, exchange = None, None
-    if dist_on:
-        try:
-            from myscaledb_amd.sharded import RcclComm
-            comm = RcclComm.from_process_group()
-            exchange = (f"mqvs_sharded_search (libmqvs RCCL communicator of {comm.nranks} ranks: one all-gather "
-                        "of headers + per-rank top-k, device merge, one host sync per search)")
-        except Exception as e:  # noqa: BLE001
-            comm, exchange = None, f"torch.distributed all_gather + mqvs_merge_shards ({type(e).__name__})"
-
-    def step():
+    try:
+        from myscaledb_amd.sharded import RcclComm
+        comm = RcclComm.from_process_group()
+        exchange = (f"mqvs_sharded_search (libmqvs RCCL communicator of {comm.nranks} ranks: header all-gather + "
+                    "one group of per-rank top-k all-gathers, device merge, one host sync per search)")
+    except Exception as e:  # noqa: BLE001
+        comm, exchange = None, f"torch.distributed all_gather + mqvs_merge_shards ({type(e).__name__})"
+    try:
+        rank_main(DistCtx(rank, world), args, comm, exchange)
+    finally:
         if comm is not None:
-            comm.sharded_search(seg, q, k, out=(f_ids, f_dst))
-            return
-        seg.search(q, k, out=(ids, dst))  # returns after its stream drained
-        if dist_on:
-            tdist.all_gather_into_tensor(g_ids, ids)
-            tdist.all_gather_into_tensor(g_dst, dst)
-            merge_shards(g_ids, g_dst, args.metric, out=(f_ids, f_dst))
-
-    for _ in range(args.warmup):
-        step()
-    set_timing(True)
-    stats = []
-    if dist_on:
-        tdist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        step()
-        stats.append(_lib.last_search_stats())
-    torch.cuda.synchronize()
-    if dist_on:
-        tdist.barrier()
-    t1 = time.perf_counter()
-    set_timing(False)
-    ms = (t1 - t0) * 1000.0 / args.steps
-    if dist_on:
-        t = torch.tensor([ms], dtype=torch.float64, device="cuda")
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        ms = float(t.item())
-
-    main_ms = float(np.mean([s["main_ms"] for s in stats]))
-    st = stats[-1]
-    roof = roofline(st, main_ms, nq, d, args)
-    # T* = max(bytes / HBM, flops / fp32 MFMA) for the whole step
-    t_star = max((4.0 * n * d + 4.0 * nq * d + 12.0 * nq * k) / (HBM_PEAK_GBS * 1e9),
-                 2.0 * nq * n * d / (FP32_MFMA_PEAK_TFLOPS * 1e12))
-    roof["survey_t_star_ms"] = round(t_star * 1e3, 3)
-    roof["survey_t_star_over_t"] = round(t_star * 1e3 / ms, 3)
-
-    # exactness at full size, outside the timed region: the timed path's
-    # output (merged over ranks) against the exact fp32 path on every query
-    import myscaledb_amd.vector_scan as mq_scan
-    exact = None
-    if not args.no_verify:
-        if dist_on:
-            mq_scan.set_batch_mode(1)
-            ei, ed = seg.search(q, k)
-            mq_scan.set_batch_mode(0)
-            tdist.all_gather_into_tensor(g_ids, ei)
-            tdist.all_gather_into_tensor(g_dst, ed)
-            xi, xd = merge_shards(g_ids, g_dst, args.metric)
-            gi, gd, xi, xd = f_ids.cpu().numpy(), f_dst.cpu().numpy(), xi.cpu().numpy(), xd.cpu().numpy()
-            k10 = min(10, k)
-            exact = {"queries": nq, "ids_equal": bool(np.array_equal(gi, xi)),
-                     "dist_bitwise_equal": bool(np.array_equal(gd.view(np.uint32), xd.view(np.uint32))),
-                     "recall_at_10": round(float(np.mean([len(set(gi[i, :k10]) & set(xi[i, :k10]))
-                                                          for i in range(nq)]) / k10), 6)}
-        else:
-            exact = exact_check(mq_scan, seg, q, k, ids, dst)
-
-    extra = sharded_legs(mq, mq_scan, comm, seg, args, rank, world) if comm is not None and world > 1 else {}
-
-    result = None
-    if rank == 0:
-        qps = nq / (ms / 1000.0)
-        pf = st.get("prefilter") if st["path"] == 2 else None
-        compute = ("bf16-hi MFMA pre-filter (one bf16 product, rigorous error bound from measured residual norms) + "
-                   "exact f32 fma-chain re-rank of the survivors") if pf == 2 else (
-            "f32 MFMA fma chain" if st["path"] == 1 else "f32 VALU, product then add")
-        result = {
-            "metric": "QPS (FLAT brute force, batch top-k)",
-            "value": round(qps, 2),
-            "unit": "queries/s",
-            "n_gpus": comm.nranks if comm is not None else world,
-            "steps": args.steps,
-            "warmup": args.warmup,
-            "ms_per_step": round(ms, 3),
-            "higher_is_better": True,
-            "scaling": "strong",
-            "vs_baseline": None,
-            "dtype": "f32",
-            "compute": compute,
-            "data": "synthetic (counter-based %s, generated in HBM)" % {
-                0: "exact integers in [-8, 8]", 1: "N(0,1)", 2: "gaussian mixture, 4096 centres",
-                3: "gaussian mixture, 65536 centres, unit noise"}[args.mode],
-            "config": {"workload": f"FLAT {args.metric} {n // 1_000_000}M x {d} Float32, batch {nq}, "
-                                   f"top-{k} (BASELINE configs[1])",
-                       "n": n, "d": d, "nq": nq, "k": k, "metric": args.metric, "generator_mode": args.mode,
-                       "granule_rows": g, "parallelism": f"row-range shards x{world}",
-                       "exchange": exchange},
-            "mdist_per_s": round(nq * n / (ms / 1000.0) / 1e6, 1),
-            "recall_at_10": exact["recall_at_10"] if exact else None,
-            "exact_check": exact,
-            "stats_last_step": {kk: (round(v, 3) if isinstance(v, float) else v) for kk, v in st.items()},
-            "roofline": roof,
-        }
-        result.update(extra)
-        if args.read_sweep_gib > 0 and world == 1:
-            # the measured HBM read peak of this device (same process, same
-            # GPU): the denominator of frac_measured_peak below
-            gbs, bms = mq_scan.measure_read_bandwidth(int(args.read_sweep_gib * (1 << 30)), 5)
-            result["hbm_read_sweep"] = {"gbs": round(gbs, 1), "bytes": int(args.read_sweep_gib * (1 << 30)),
-                                        "best_ms": round(bms, 3), "frac_of_8tbs": round(gbs / HBM_PEAK_GBS, 4),
-                                        "kernel": "best of k_read_sweep (16 B per lane, 4 loads in flight, grid-stride, "
-                                                  "8 workgroups per CU) and k_read_slices (a contiguous slice per "
-                                                  "workgroup, 8 or 16 non-temporal 16-B loads in flight per lane, "
-                                                  "2-8 workgroups per CU)"}
-        if not args.no_small and world == 1:
-            result["small_batch"] = small_batch_leg(mq_scan, seg, args)
-            p1 = [x for x in result["small_batch"] if x["nq"] == 1]
-            if p1:
-                # the north-star nq = 1 point: HBM-bound scan of
-                # the bf16 plane, against 8 TB/s and the measured read peak
-                p1 = p1[0]
-                plane = p1["bytes_read"]
-                nq1 = {"ms": p1["main_ms"], "ms_end_to_end": p1["ms_per_search"], "plane_bytes": plane,
-                       "kernel": "k_scan_hi_reg (bf16 16x16x32, operands straight from HBM into registers)",
-                       "achieved_gbs": p1["main_gbs"], "frac_8tbs": p1["hbm_frac_main"],
-                       "frac_end_to_end_8tbs": p1["hbm_frac_end_to_end"], "exact": p1["exact"]["ids_equal"] and
-                       p1["exact"]["dist_bitwise_equal"]}
-                if "hbm_read_sweep" in result:
-                    nq1["measured_peak_gbs"] = result["hbm_read_sweep"]["gbs"]
-                    nq1["frac_measured_peak"] = round(p1["main_gbs"] / result["hbm_read_sweep"]["gbs"], 4)
-                pm = _pmc_kernel(args.pmc_nq1 or os.path.join(ROOT, PMC_NQ1_DEFAULT), "k_scan_hi_reg", 1, sum_all=True)
-                if pm:
-                    nq1["pmc_hbm_bytes"] = round(pm["hbm_bytes_per_search"])
-                    nq1["pmc_over_plane"] = round(pm["hbm_bytes_per_search"] / plane, 4)
-                    nq1["pmc_source"] = pm["source"]
-                result["roofline"]["nq1"] = nq1
-                # (scalars at the top level of roofline: the driver's record
-                # keeps those, not the nested dict)
-                for key, val in (("nq1_ms", nq1["ms"]), ("nq1_ms_end_to_end", nq1["ms_end_to_end"]),
-                                 ("nq1_frac_8tbs", nq1["frac_8tbs"]),
-                                 ("nq1_frac_end_to_end_8tbs", nq1["frac_end_to_end_8tbs"]),
-                                 ("nq1_pmc_over_plane", nq1.get("pmc_over_plane")),
-                                 ("nq1_frac_measured_peak", nq1.get("frac_measured_peak")),
-                                 ("nq1_exact", nq1["exact"])):
-                    result["roofline"][key] = val
-        if not args.no_cpu and world == 1:
-            # the CPU leg: the oracle (the reference's CPU path restated) timed
-            # on the host cores, and -- as the checker only -- its formula on
-            # sampled rows of the timed output (pins the exact path)
-            O = _oracle()
-            result["cpu_baseline"] = cpu_baseline(O, args)
-            result["cpu_baseline"]["one_thread_qps"] = result["cpu_baseline"]["one_thread"]["qps"]
-            if not args.no_verify:
-                ok, nchk = verify_sample(O, ids.cpu().numpy(), dst.cpu().numpy(), q.cpu().numpy(), args)
-                result["oracle_sample"] = {"queries": nchk, "bitwise_and_no_better_sample": ok}
-        if not args.no_index and world == 1:
-            result["index"] = index_leg(mq, seg, args)
-        risk = os.path.join(ROOT, BLAS_RISK_DEFAULT)
-        if os.path.exists(risk):
-            # parity risk of the unpinned BLAS-branch order (tools/blas_order_risk.py,
-            # committed run of this config): queries whose top-k would change
-            # if faiss's sgemm blocked K
-            with open(risk) as f:
-                rk = json.load(f)
-            result["blas_order_risk"] = dict(rk, source=os.path.relpath(risk, ROOT))
-        if (not args.no_configs or not args.no_config1_points) and world == 1:
-            seg.free()  # (room for the next parts)
-            seg = None
-            torch.cuda.synchronize()
-            torch.cuda.empty_cache()
-        if not args.no_config1_points and world == 1:
-            result["config1_points"] = config1_points(mq, mq_scan, args)
-        if not args.no_configs and world == 1:
-            result["configs"] = configs_leg(mq, mq_scan, args)
-        print(json.dumps(result), flush=True)
-    if comm is not None:
-        comm.free()
-    if seg is not None:
-        seg.free()
-    if dist_on:
+            comm.free()
         tdist.barrier()
         tdist.destroy_process_group()
 

@@ -522,8 +522,10 @@ size_t mqvs_set_scratch_budget(size_t bytes);
  * ends while others wait frees its workspace).  Only when every running
  * search is waiting does one go over the cap (counted in over_budget) instead
  * of deadlocking.  Default: a quarter of the device memory.  Returns the
- * previous value; 0 leaves it unchanged.  (Index-search buffers and segments
- * are not counted.) */
+ * previous value; 0 leaves it unchanged.  Index searches (mqvs_index_search,
+ * mqvs_decoupled_filter) pass the same gate: their scratch is counted in, and
+ * trimmed with, the calling thread's workspace.  (Segments, indexes and
+ * communicators are not counted.) */
 size_t mqvs_set_workspace_budget(size_t bytes);
 typedef struct {
     size_t budget;       /* the cap */
@@ -544,6 +546,14 @@ int mqvs_workspace_stats(mqvs_workspace_stats_t *out, int32_t reset_peak);
  * >= 4 GiB defeats the 256 MiB Infinity Cache), best of `reps` timed passes
  * after one warm-up: *gbs = bytes / best time (1e9 B/s), *best_ms (optional). */
 int mqvs_measure_read_bandwidth(size_t bytes, int32_t reps, double *gbs, double *best_ms);
+/* Fault drill for a caller's host fallback (on a device error the
+ * host runs its CPU path; include/mqvs_vector_index.hpp takes the fallback as
+ * a callable): the next `calls` search entry points made by THIS thread --
+ * mqvs_search, mqvs_search_ex, mqvs_knn_raw, mqvs_search_binary,
+ * mqvs_knn_binary_raw, mqvs_index_search -- return `status` (MQVS_ERR_DEVICE
+ * or MQVS_ERR_MEMORY_LIMIT) without touching the device or the outputs.
+ * calls = 0 disarms.  Other statuses are MQVS_ERR_BAD_ARGUMENTS. */
+int mqvs_inject_fault(int32_t status, int32_t calls);
 
 #ifdef __cplusplus
 }

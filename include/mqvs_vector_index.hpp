@@ -50,6 +50,7 @@
  */
 #pragma once
 
+#include <atomic>
 #include <cstddef>
 #include <cstdint>
 #include <functional>
@@ -143,25 +144,68 @@ int toMqvsMetric(const MetricEnum & metric)
     return -1;
 }
 
+/// Host fallback on a device failure ("on device error the host
+/// falls back to the CPU path").  The seams below take an optional callable
+/// that runs the reference's own CPU code in place of the GPU call when
+/// libmqvs returns MQVS_ERR_DEVICE or MQVS_ERR_MEMORY_LIMIT (a lost or
+/// exhausted device); every other status still throws.  In the ClickHouse
+/// tree the callable is the call the seam replaced, e.g. faiss::knn_L2sqr /
+/// knn_inner_product for tryBruteForceSearch (BruteForceSearch.h:80-87), the
+/// per-part CPU vectorScanWithoutIndex for PartScan, the CPU index for
+/// GpuIndex.  fallbackCount() counts the calls it served (a metric to export).
+inline bool isFallbackStatus(int status)
+{
+    return status == MQVS_ERR_DEVICE || status == MQVS_ERR_MEMORY_LIMIT;
+}
+
+inline std::atomic<uint64_t> & fallbackCount()
+{
+    static std::atomic<uint64_t> n{0};
+    return n;
+}
+
+/// status -> done (OK), `run` (a device failure and the caller gave a
+/// fallback), or DB::Exception
+template <typename F>
+void checkOrFallback(int status, bool have_fallback, const F & run)
+{
+    if (status != MQVS_OK && isFallbackStatus(status) && have_fallback)
+    {
+        run();
+        fallbackCount().fetch_add(1, std::memory_order_relaxed);
+        return;
+    }
+    check(status);
+}
+
+/// The CPU search tryBruteForceSearch replaces (faiss knn_L2sqr /
+/// knn_inner_product, BruteForceSearch.h:80-87), same arguments.
+using BruteForceFallback = std::function<void(const float * x, const float * y, size_t d, size_t k, size_t nx,
+                                              size_t ny, int64_t * result_id, float * distance, int mqvs_metric)>;
+
 /// tryBruteForceSearch<FloatVector> (BruteForceSearch.h:62-92): x nx*d
 /// queries, y ny*d base, result_id / distance nx*k in faiss layout.
+/// fallback: runs instead when the device fails (see isFallbackStatus).
 inline void tryBruteForceSearch(
     const float * x, const float * y, size_t d, size_t k, size_t nx, size_t ny,
-    int64_t * result_id, float * distance, int mqvs_metric)
+    int64_t * result_id, float * distance, int mqvs_metric, const BruteForceFallback & fallback = nullptr)
 {
     if (mqvs_metric != MQVS_METRIC_L2 && mqvs_metric != MQVS_METRIC_IP)
         throw DB::Exception(DB::ErrorCodes::NOT_IMPLEMENTED, "{}",
                             std::string("Metric not implemented in brute force search for Float32 Vector"));
-    check(mqvs_knn_raw(x, y, static_cast<int64_t>(d), static_cast<int64_t>(k), static_cast<int64_t>(nx),
-                       static_cast<int64_t>(ny), mqvs_metric, result_id, distance));
+    const int st = mqvs_knn_raw(x, y, static_cast<int64_t>(d), static_cast<int64_t>(k), static_cast<int64_t>(nx),
+                                static_cast<int64_t>(ny), mqvs_metric, result_id, distance);
+    checkOrFallback(st, static_cast<bool>(fallback),
+                    [&] { fallback(x, y, d, k, nx, ny, result_id, distance, mqvs_metric); });
 }
 
 template <typename MetricEnum>
 void tryBruteForceSearch(
     const float * x, const float * y, size_t d, size_t k, size_t nx, size_t ny,
-    int64_t * result_id, float * distance, const MetricEnum & metric_type)
+    int64_t * result_id, float * distance, const MetricEnum & metric_type,
+    const BruteForceFallback & fallback = nullptr)
 {
-    tryBruteForceSearch(x, y, d, k, nx, ny, result_id, distance, toMqvsMetric(metric_type));
+    tryBruteForceSearch(x, y, d, k, nx, ny, result_id, distance, toMqvsMetric(metric_type), fallback);
 }
 
 /// tryBruteForceSearch<BinaryVector> (BruteForceSearch.h:94-110): x nx*(d/8)
@@ -267,13 +311,22 @@ public:
     /// ~3x larger fits; same results) or back (mqvs_segment_set_rows_host).
     void setRowsHost(bool host) { check(mqvs_segment_set_rows_host(seg->h, host ? 1 : 0)); }
 
+    /// The CPU part scan PartScan replaces (vectorScanWithoutIndex over this
+    /// part, MergeTreeVSManager.cpp:960-1536), same arguments and outputs.
+    using ScanFallback = std::function<void(const float * queries, int32_t nq, int32_t k, const uint8_t * filter,
+                                            const uint8_t * row_exists, int64_t * ids, float * dist)>;
+
     /// Raw top-k: ids / dist nq*k (caller-owned), -1 / FLT_MAX (FLT_MIN for IP)
     /// padded.  filter: PREWHERE bitmap, row_exists: lightweight-delete mask
     /// (LSB-first, n bits, or nullptr).  flags: MQVS_F_* (per call).
+    /// fallback: runs instead when the device fails (isFallbackStatus).
     void search(const float * queries, int32_t nq, int32_t k, const uint8_t * filter,
-                const uint8_t * row_exists, int64_t * ids, float * dist, uint32_t flags = 0) const
+                const uint8_t * row_exists, int64_t * ids, float * dist, uint32_t flags = 0,
+                const ScanFallback & fallback = nullptr) const
     {
-        check(mqvs_search(seg->h, queries, nq, k, metric, filter, row_exists, ids, dist, flags, nullptr));
+        const int st = mqvs_search(seg->h, queries, nq, k, metric, filter, row_exists, ids, dist, flags, nullptr);
+        checkOrFallback(st, static_cast<bool>(fallback),
+                        [&] { fallback(queries, nq, k, filter, row_exists, ids, dist); });
     }
 
     /// Raw top-k of a row-range shard of a larger part: chunk_ord_base = chunks
@@ -299,10 +352,13 @@ public:
     /// As above, after the reference's dimension check (generateVectorDataset,
     /// MergeTreeVSManager.cpp:135-182 throws on a mismatch).
     ScanColumns scan(const float * queries, int32_t nq, int32_t query_dim, int32_t k, bool is_batch,
-                     const uint8_t * filter, const uint8_t * row_exists) const
+                     const uint8_t * filter, const uint8_t * row_exists, const ScanFallback & fallback = nullptr) const
     {
         checkDimension(query_dim);
-        return scan(queries, nq, k, is_batch, filter, row_exists);
+        std::vector<int64_t> ids(static_cast<size_t>(nq) * k);
+        std::vector<float> dist(ids.size());
+        search(queries, nq, k, filter, row_exists, ids.data(), dist.data(), 0, fallback);
+        return toColumns(ids, dist, k, is_batch);
     }
 
     /// computeTopDistanceSubset: exact distances to nq*ncand candidate rows.
@@ -389,13 +445,23 @@ public:
     /// padded; filter = the PREWHERE bitmap ANDed with the lightweight-delete
     /// bitmap by the library (row_exists).  With a row_ids_map registered, the
     /// ids are decoupled-part rows.  params: alpha / nprobe / num_reorder.
+    /// The CPU index search GpuIndex replaces (the part's Search::VectorIndex
+    /// search, VIWithDataPart.cpp:926), same arguments and outputs.
+    using SearchFallback = std::function<void(const float * queries, int32_t nq, int32_t k, const std::string & params,
+                                              const uint8_t * filter, const uint8_t * row_exists,
+                                              bool first_stage_only, int64_t * ids, float * dist)>;
+
+    /// fallback: runs instead when the device fails (isFallbackStatus).
     void search(const float * queries, int32_t nq, int32_t query_dim, int32_t k, const std::string & params,
                 const uint8_t * filter, const uint8_t * row_exists, bool first_stage_only, int64_t * ids,
-                float * dist) const
+                float * dist, const SearchFallback & fallback = nullptr) const
     {
         part.checkDimension(query_dim);
-        check(mqvs_index_search(idx->h, queries, nq, k, params.c_str(), filter, row_exists, ids, dist,
-                                first_stage_only ? MQVS_F_FIRST_STAGE : 0u, nullptr));
+        const int st = mqvs_index_search(idx->h, queries, nq, k, params.c_str(), filter, row_exists, ids, dist,
+                                         first_stage_only ? MQVS_F_FIRST_STAGE : 0u, nullptr);
+        checkOrFallback(st, static_cast<bool>(fallback), [&] {
+            fallback(queries, nq, k, params, filter, row_exists, first_stage_only, ids, dist);
+        });
     }
 
     /// computeTopDistanceSubset (VIWithDataPart.cpp:838-856): exact distances of

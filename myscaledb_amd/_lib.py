@@ -51,7 +51,7 @@ SYMBOLS = [
     "mqvs_comm_unique_id", "mqvs_comm_init", "mqvs_comm_init_loopback", "mqvs_comm_free", "mqvs_sharded_search", "mqvs_comm_stats",
     "mqvs_index_set_row_ids_map", "mqvs_decoupled_filter",
     "mqvs_cache_create", "mqvs_cache_free", "mqvs_cache_put", "mqvs_cache_acquire", "mqvs_cache_release",
-    "mqvs_cache_remove", "mqvs_cache_stats",
+    "mqvs_cache_remove", "mqvs_cache_stats", "mqvs_inject_fault",
 ]
 
 
@@ -149,6 +149,7 @@ def _load(path=LIB_PATH):
         "mqvs_workspace_stats": ([P, ctypes.c_int32], ctypes.c_int),
         "mqvs_measure_read_bandwidth": ([ctypes.c_size_t, ctypes.c_int32, P, P], ctypes.c_int),
         "mqvs_set_prefilter": ([ctypes.c_int], ctypes.c_int),
+        "mqvs_inject_fault": ([I32, I32], ctypes.c_int),
         "mqvs_index_build": ([P, ctypes.c_char_p, ctypes.c_char_p, P], ctypes.c_int),
         "mqvs_index_free": ([P], ctypes.c_int),
         "mqvs_index_info": ([P, P], ctypes.c_int),

@@ -81,24 +81,44 @@ constexpr int64_t kCoarseFlatLists = 16384;  // more lists: the coarse step is a
 
 // plan / scan / select buffers of one list pass
 struct ListBufs {
-    DevBuf lcount, lfill, lstart, lq, items, grp, chk, nitems, qbase, qstart, cand, stats, large;
-    void release() {
-        for (DevBuf *b : {&lcount, &lfill, &lstart, &lq, &items, &grp, &chk, &nitems, &qbase, &qstart, &cand, &stats,
-                          &large})
-            b->release();
+    GBuf lcount, lfill, lstart, lq, items, grp, chk, nitems, qbase, qstart, cand, stats, large;
+    size_t release() {
+        size_t b = 0;
+        for (GBuf *x : {&lcount, &lfill, &lstart, &lq, &items, &grp, &chk, &nitems, &qbase, &qstart, &cand, &stats,
+                        &large}) {
+            b += x->cap;
+            x->release();
+        }
+        return b;
     }
 };
 
-struct IndexWorkspace {
+// The scratch of a thread's index searches.  Every buffer is a GBuf: it grows
+// through the thread's FLAT workspace gate (WsScope in search_index_impl), so
+// concurrent index searches share the process-wide HBM budget with FLAT
+// scans, and an idle thread's index scratch is trimmed with its workspace.
+struct IndexWorkspace final : WsExt {
     hipEvent_t ev[6] = {};
     // the cosine variant chain runs on `side` between fork and join (created
     // on the workspace's device: index_workspace is called under its guard)
     hipEvent_t fork = nullptr, join = nullptr;
     hipStream_t side = nullptr;
     int64_t *host = nullptr;  // pinned: the search's stats [4] and status word (one sync, no staging copies)
-    DevBuf queries, qvars, qnorms, qmu, qlam, status, qhi, probes, cprobes, filter, exists, rows, out_ids, out_dist,
+    GBuf queries, qvars, qnorms, qmu, qlam, status, qhi, probes, cprobes, filter, exists, rows, out_ids, out_dist,
         ord, dmap, dwords, pdist, cqhi, gmax;
     ListBufs coarse, fine;
+    // WsExt: the owner is between calls (its workspace's `done` event passed:
+    // the main stream, which joins the side chain, has drained)
+    size_t free_scratch() override {
+        if (side) (void)hipStreamSynchronize(side);
+        size_t b = 0;
+        for (GBuf *x : {&queries, &qvars, &qnorms, &qmu, &qlam, &status, &qhi, &probes, &cprobes, &filter, &exists,
+                        &rows, &out_ids, &out_dist, &ord, &dmap, &dwords, &pdist, &cqhi, &gmax}) {
+            b += x->cap;
+            x->release();
+        }
+        return b + coarse.release() + fine.release();
+    }
     void init() {
         if (ev[0]) return;
         for (auto &e : ev) MQVS_HIP(hipEventCreate(&e));
@@ -109,15 +129,11 @@ struct IndexWorkspace {
     }
     // after the last search's kernels (ev[5] ends every search, ASYNC ones
     // included; the side stream's chain is joined before it)
+    // (the scratch is detached and freed first: ws_detach_ext)
     void release() {
         if (!ev[0]) return;
         (void)hipEventSynchronize(ev[5]);
         if (side) (void)hipStreamSynchronize(side);
-        for (DevBuf *b : {&queries, &qvars, &qnorms, &qmu, &qlam, &status, &qhi, &probes, &cprobes, &filter, &exists,
-                          &rows, &out_ids, &out_dist, &ord, &dmap, &dwords, &pdist, &cqhi, &gmax})
-            b->release();
-        coarse.release();
-        fine.release();
         for (auto &e : ev) {
             (void)hipEventDestroy(e);
             e = nullptr;
@@ -140,6 +156,7 @@ void index_thread_release() {
     if (!g_iws) return;
     for (auto &kv : *g_iws) {
         (void)hipSetDevice(kv.first);
+        ws_detach_ext(kv.first, &kv.second);
         kv.second.release();
     }
     g_iws->clear();
@@ -768,7 +785,24 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     mqvs_segment *seg = ix->seg;
     DeviceGuard guard(seg->device);
     IndexWorkspace &ws = index_workspace(seg->device);
+    // admission under the workspace budget; every scratch buffer below grows
+    // through its gate
+    WsScope scope(seg->device, &ws);
     hipStream_t s = user_stream ? user_stream : thread_stream(seg->device);
+    scope.set_stream(s);
+    // the side stream's variant chain is joined into s on EVERY exit after it
+    // forks (an exception between fork and the re-rank's wait included), so
+    // the next search on this thread -- whose prep rewrites qvars and status
+    // on s -- and a trimmer waiting for s's completion see it finished
+    bool forked = false;
+    struct JoinGuard {
+        hipStream_t s;
+        hipEvent_t ev;
+        bool &on;
+        ~JoinGuard() {
+            if (on) (void)hipStreamWaitEvent(s, ev, 0);
+        }
+    } join_guard{s, ws.join, forked};
     const bool dev = flags & MQVS_F_DEVICE_PTRS;
     const int d = seg->d;
     const bool cos = ix->metric == MQVS_METRIC_COSINE;
@@ -833,6 +867,7 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     auto fork_chain = [&]() {
         MQVS_HIP(hipEventRecord(ws.fork, s));
         MQVS_HIP(hipStreamWaitEvent(ws.side, ws.fork, 0));
+        forked = true;
         launch_query_prep(dq, nq, d, MQVS_METRIC_COSINE, false, qvars, maxv, qnorms, qmu, qlam, status, ws.side, 2);
         MQVS_HIP(hipGetLastError());
         MQVS_HIP(hipEventRecord(ws.join, ws.side));
@@ -921,7 +956,10 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
         list_pass(ws.fine, ix->plane, ix->perm, ix->pnorm, ix->list_off, ix->nlist, ix->npos, ix->max_list, ix->dpad,
                   ix->metric, qhi, qnorms, nq, probes, nprobe, dfilter, dexists, R, crow, 0, nullptr, ws.ev, s);
         // ---- exact re-rank (needs the whole variant chain)
-        if (split) MQVS_HIP(hipStreamWaitEvent(s, ws.join, 0));
+        if (split) {
+            MQVS_HIP(hipStreamWaitEvent(s, ws.join, 0));
+            forked = false;
+        }
         ScanParams rp{};
         rp.rows = seg->rows;
         rp.row_norms = seg->norms;
@@ -1040,6 +1078,7 @@ int mqvs_index_search(mqvs_index_t idx, const float *queries, int32_t nq, int32_
                       const uint8_t *filter, const uint8_t *row_exists, int64_t *out_ids, float *out_dist,
                       uint32_t flags, mqvs_stream_t stream) {
     return guarded([&] {
+        fault_point();
         search_index_impl(idx, queries, nq, k, params, filter, row_exists, out_ids, out_dist, flags,
                           (hipStream_t)stream, 0);
     });
@@ -1084,7 +1123,9 @@ int mqvs_decoupled_filter(const uint8_t *new_filter, int64_t new_rows, const uin
         int dev = 0;
         MQVS_HIP(hipGetDevice(&dev));
         IndexWorkspace &ws = index_workspace(dev);
+        WsScope scope(dev, &ws);
         hipStream_t s = stream ? (hipStream_t)stream : thread_stream(dev);
+        scope.set_stream(s);
         const bool devp = flags & MQVS_F_DEVICE_PTRS;
         const int64_t nb = (new_rows + 7) / 8, ob = (old_rows + 7) / 8;
         const uint8_t *df = new_filter;

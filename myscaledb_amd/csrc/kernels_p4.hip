@@ -140,6 +140,26 @@ __device__ inline f32x4 p4_aread4(float a, float b, float c, float d) {
     return f32x4{x, y, z, w};
 }
 
+// PROBE: values of rows that row_valid rejects (PREWHERE filter, empty array
+// under a filter, lightweight delete) become -inf.  Lane value v4[g][i] is
+// row r0 + rbl + GS g + i; rows at or past the item's end are already -inf.
+template <int GS>
+__device__ inline void p4_mask_invalid_t(const ScanParams &p, f32x4 (&v4)[4], int r0, int rbl, int ecrn) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int i = 0; i < 4; ++i) {
+            const int rl = rbl + GS * g + i;
+            if (rl < ecrn && !row_valid(p, (int64_t)r0 + rl)) v4[g][i] = -__builtin_inff();
+        }
+}
+__device__ inline void p4_mask_invalid(const ScanParams &p, f32x4 (&v4)[4], int r0, int rbl, int gs, int ecrn) {
+    if (gs == 16)
+        p4_mask_invalid_t<16>(p, v4, r0, rbl, ecrn);
+    else
+        p4_mask_invalid_t<8>(p, v4, r0, rbl, ecrn);
+}
+
 __device__ inline void p4_barrier() {
     __builtin_amdgcn_sched_barrier(0);
     asm volatile("s_barrier" ::: "memory");
@@ -449,6 +469,9 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
                 for (int r = 0; r < 16; ++r)
                     if (rbl + (r & 3) + 8 * (r >> 2) >= ecrn) v4[r >> 2][r & 3] = -__builtin_inff();
             }
+            // (filtered / deleted rows never define a group's best value, as
+            // in k_scan_p4m below)
+            if (p.filter || p.exists) p4_mask_invalid(p, v4, ecr0, wr * 128 + rb * 32 + 4 * h, 8, ecrn);
             float mx = v4[0][0];
 #pragma unroll
             for (int r = 1; r < 16; ++r) mx = __builtin_elementwise_maximum(mx, v4[r >> 2][r & 3]);
@@ -934,6 +957,13 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
                 for (int r = 0; r < 16; ++r)
                     if (rbl + 16 * (r >> 2) + (r & 3) >= ecrn) v4[r >> 2][r & 3] = -__builtin_inff();
             }
+            // rows the PREWHERE bitmap rejects or a lightweight delete
+            // removed never define a group's best value: each maximum must be
+            // one VALID row's approximate value, or the k-th of them is
+            // tighter than the k-th valid row's (true neighbours would then
+            // fail the append test).  (Uniform branch: probes without a
+            // filter or deletes skip it.)
+            if (p.filter || p.exists) p4_mask_invalid(p, v4, ecr0, rbl, 16, ecrn);
         }
         const int j = q0 + wq * 128 + jb * 16 + l16;
         if constexpr (PROBE && GRP == 16) {

@@ -99,6 +99,8 @@ struct Workspace {
     size_t held = 0;    // device bytes of the buffers (the gate's share of this workspace)
     size_t resv = 0;    // the current call's reservation left
     size_t call_peak = 0, recent = 0;  // most held during the current / the last call
+    WsExt *ext = nullptr;  // the thread's index workspace: its scratch is counted and trimmed with this one
+    bool trimming = false;  // picked by a trimmer, which waits and frees outside the gate mutex
     void init(int dev) {
         if (stream) return;
         device = dev;
@@ -125,18 +127,20 @@ struct Workspace {
         }
         return b;
     }
-    // free every buffer but the ASYNC sticky word, once the last call's work
-    // has drained -- on whichever stream it ran, the caller's included (an
-    // ASYNC call returns with its kernels in flight) -- (gate mutex held by
-    // the caller)
+    // free every buffer but the ASYNC sticky word (and the index scratch
+    // counted here), once the last call's work has drained -- on whichever
+    // stream it ran, the caller's included (an ASYNC call returns with its
+    // kernels in flight).  Called WITHOUT the gate mutex (GPU waits and frees
+    // must not stall every other thread's admission) by a thread that holds
+    // `use`; the caller updates `held` and the gate under the mutex.
     size_t trim() {
         int cur = -1;
         (void)hipGetDevice(&cur);
         (void)hipSetDevice(device);
         (void)hipEventSynchronize(done);
         (void)hipStreamSynchronize(stream);
-        const size_t b = free_buffers(true);
-        held = sticky.cap;
+        size_t b = free_buffers(true);
+        if (ext) b += ext->free_scratch();
         if (cur >= 0) (void)hipSetDevice(cur);
         return b;
     }
@@ -148,6 +152,8 @@ struct Workspace {
             g.held -= std::min(g.held, held);
             held = 0;
         }
+        if (ext) (void)ext->free_scratch();
+        ext = nullptr;
         (void)free_buffers(false);
         if (host_flags) (void)hipHostFree(host_flags);
         host_flags = nullptr;
@@ -163,17 +169,35 @@ struct Workspace {
     void *get(DevBuf &b, size_t bytes);
 };
 
-// gate mutex held: free idle workspaces of other threads until `need` more
-// bytes fit under the budget
-static void trim_idle(WsGate &g, Workspace *me, size_t need, size_t budget) {
+// lk holds the gate mutex: free idle workspaces of other threads until `need`
+// more bytes fit under the budget.  The victims are picked (their `use` taken,
+// marked) under the mutex; their GPU waits and frees run with it released, and
+// the accounting is updated once it is re-taken.  Returns whether anything was
+// trimmed (the caller re-checks its condition either way).
+static bool trim_idle(std::unique_lock<std::mutex> &lk, WsGate &g, Workspace *me, size_t need, size_t budget) {
+    std::vector<Workspace *> victims;
+    size_t expect = 0;
     for (Workspace *w : g.all) {
-        if (g.held + g.reserved + need <= budget) return;
-        if (w == me || w->held <= w->sticky.cap || !w->use.try_lock()) continue;
-        const size_t b = w->trim();
-        w->use.unlock();
-        g.held -= std::min(g.held, b);
-        ++g.trims;
+        if (g.held - std::min(g.held, expect) + g.reserved + need <= budget) break;
+        if (w == me || w->trimming || w->held <= w->sticky.cap || !w->use.try_lock()) continue;
+        w->trimming = true;
+        victims.push_back(w);
+        expect += w->held - w->sticky.cap;
     }
+    if (victims.empty()) return false;
+    lk.unlock();
+    for (Workspace *w : victims) (void)w->trim();
+    lk.lock();
+    for (Workspace *w : victims) {
+        // (the gate counted held - sticky of it: every gated buffer is gone)
+        g.held -= std::min(g.held, w->held - std::min(w->held, w->sticky.cap));
+        w->held = std::min(w->held, w->sticky.cap);
+        w->trimming = false;
+        ++g.trims;
+        w->use.unlock();
+    }
+    g.cv.notify_all();
+    return true;
 }
 
 void *Workspace::get(DevBuf &b, size_t bytes) {
@@ -194,7 +218,7 @@ void *Workspace::get(DevBuf &b, size_t bytes) {
             const size_t B = ws_budget();
             bool counted = false;
             while (g.held + g.reserved + rest > B) {
-                trim_idle(g, this, rest, B);
+                trim_idle(lk, g, this, rest, B);
                 if (g.held + g.reserved + rest <= B) break;
                 const int others = g.active - g.blocked - (depth > 0 ? 1 : 0);
                 if (others <= 0) {
@@ -243,7 +267,7 @@ struct WsCall {
         const size_t extra = need - ws.held;
         bool counted = false;
         while (g.held + g.reserved + extra > B) {
-            trim_idle(g, &ws, extra, B);
+            trim_idle(lk, g, &ws, extra, B);
             if (g.held + g.reserved + extra <= B || g.active == 0) break;  // (nobody to wait for)
             if (!counted) ++g.waits;
             counted = true;
@@ -261,6 +285,7 @@ struct WsCall {
         (void)hipEventRecord(ws.done, ws.last ? ws.last : ws.stream);
         ws.last = nullptr;
         WsGate &g = gate();
+        bool self_trim = false;
         {
             std::lock_guard<std::mutex> lk(g.mu);
             --g.active;
@@ -269,12 +294,18 @@ struct WsCall {
             ws.recent = ws.call_peak;
             g.typical = ws.call_peak;
             const size_t B = g_ws_budget.load(std::memory_order_relaxed);
-            if ((g.blocked > 0 || g.admitting > 0 || (B && g.held > B)) && ws.held > ws.sticky.cap &&
-                hipEventQuery(ws.done) == hipSuccess) {
-                const size_t b = ws.trim();
-                g.held -= std::min(g.held, b);
-                ++g.trims;
-            }
+            self_trim = (g.blocked > 0 || g.admitting > 0 || (B && g.held > B)) && ws.held > ws.sticky.cap &&
+                        hipEventQuery(ws.done) == hipSuccess;
+            g.cv.notify_all();
+        }
+        if (self_trim) {
+            // (the frees run outside the gate mutex; `use` is still held, so
+            // no trimmer picks this workspace meanwhile)
+            (void)ws.trim();
+            std::lock_guard<std::mutex> lk(g.mu);
+            g.held -= std::min(g.held, ws.held - std::min(ws.held, ws.sticky.cap));
+            ws.held = std::min(ws.held, ws.sticky.cap);
+            ++g.trims;
             g.cv.notify_all();
         }
         ws.use.unlock();
@@ -290,6 +321,58 @@ static Workspace &workspace(int device) {
     Workspace &w = (*g_ws)[device];
     w.init(device);
     return w;
+}
+
+// WsScope (mqvs_internal.h): a WsCall on the thread's workspace, made the
+// current one for GBuf growth
+struct WsScopeImpl {
+    Workspace &ws;
+    WsCall call;
+    explicit WsScopeImpl(Workspace &w) : ws(w), call(w) {}
+};
+static thread_local WsScopeImpl *t_scope = nullptr;
+
+WsScope::WsScope(int device, WsExt *ext) {
+    Workspace &w = workspace(device);
+    auto *im = new WsScopeImpl(w);  // admission (may wait for memory)
+    w.ext = ext;                    // (one ext per thread and device; `use` is held)
+    prev_ = t_scope;
+    t_scope = im;
+    impl_ = im;
+}
+WsScope::~WsScope() {
+    t_scope = static_cast<WsScopeImpl *>(prev_);
+    delete static_cast<WsScopeImpl *>(impl_);
+}
+void WsScope::set_stream(hipStream_t s) { static_cast<WsScopeImpl *>(impl_)->ws.last = s; }
+
+void *GBuf::get(size_t bytes) {
+    if (!t_scope) fail(MQVS_ERR_LOGICAL, "gated scratch grown outside a workspace scope");
+    return t_scope->ws.get(*this, bytes);
+}
+
+static thread_local int t_fault_status = MQVS_OK, t_fault_calls = 0;
+
+void fault_point() {
+    if (t_fault_calls <= 0) return;
+    --t_fault_calls;
+    fail(t_fault_status, "injected fault (mqvs_inject_fault)");
+}
+
+void ws_detach_ext(int device, WsExt *ext) {
+    if (!g_ws) return;
+    auto it = g_ws->find(device);
+    if (it == g_ws->end()) return;
+    Workspace &w = it->second;
+    std::lock_guard<std::mutex> u(w.use);
+    if (w.ext != ext) return;
+    const size_t b = ext->free_scratch();
+    WsGate &g = gate();
+    std::lock_guard<std::mutex> lk(g.mu);
+    g.held -= std::min(g.held, b);
+    w.held -= std::min(w.held, b);
+    w.ext = nullptr;
+    g.cv.notify_all();
 }
 
 
@@ -1660,6 +1743,16 @@ int mqvs_thread_release(void) {
 
 int mqvs_shutdown(void) { return mqvs_thread_release(); }
 
+int mqvs_inject_fault(int32_t status, int32_t calls) {
+    if (calls < 0 || (calls > 0 && status != MQVS_ERR_DEVICE && status != MQVS_ERR_MEMORY_LIMIT)) {
+        set_error("mqvs_inject_fault: status must be MQVS_ERR_DEVICE or MQVS_ERR_MEMORY_LIMIT, calls >= 0");
+        return MQVS_ERR_BAD_ARGUMENTS;
+    }
+    t_fault_status = status;
+    t_fault_calls = calls;
+    return MQVS_OK;
+}
+
 int mqvs_segment_create(const float *host_rows, int64_t n, int32_t d, int32_t metric,
                         int64_t granule_rows, const uint8_t *nonempty, int64_t row_offset,
                         mqvs_segment_t *out) {
@@ -1822,6 +1915,7 @@ int mqvs_search(mqvs_segment_t seg, const float *queries, int32_t nq, int32_t k,
                 const uint8_t *filter, const uint8_t *row_exists, int64_t *out_ids, float *out_dist,
                 uint32_t flags, mqvs_stream_t stream) {
     return guarded([&] {
+        fault_point();
         search_impl(seg, queries, nq, k, metric, filter, row_exists, out_ids, out_dist, flags,
                     (hipStream_t)stream);
     });
@@ -1831,6 +1925,7 @@ int mqvs_search_ex(mqvs_segment_t seg, const float *queries, int32_t nq, int32_t
                    const uint8_t *filter, const uint8_t *row_exists, int64_t chunk_ord_base,
                    int64_t *out_ids, float *out_dist, uint32_t flags, mqvs_stream_t stream) {
     return guarded([&] {
+        fault_point();
         if (chunk_ord_base > INT32_MAX) fail(MQVS_ERR_BAD_ARGUMENTS, "chunk_ord_base out of range");
         search_impl(seg, queries, nq, k, metric, filter, row_exists, out_ids, out_dist, flags,
                     (hipStream_t)stream, false, chunk_ord_base);
@@ -1842,6 +1937,7 @@ int mqvs_knn_raw(const float *x, const float *y, int64_t d, int64_t k, int64_t n
     return guarded([&] {
         if (metric != MQVS_METRIC_L2 && metric != MQVS_METRIC_IP)
             fail(MQVS_ERR_NOT_IMPLEMENTED, "Metric not implemented in brute force search for Float32 Vector");
+        fault_point();
         if (d <= 0 || d > INT32_MAX || k < 0 || k > INT32_MAX || nx < 0 || nx > INT32_MAX || ny < 0)
             fail(MQVS_ERR_BAD_ARGUMENTS, "bad sizes");
         if (nx == 0 || k == 0) return;
@@ -1905,6 +2001,7 @@ int mqvs_search_binary(mqvs_segment_t seg, const uint8_t *queries, int32_t nq, i
                        const uint8_t *filter, const uint8_t *row_exists, int64_t *out_ids, float *out_dist,
                        uint32_t flags, mqvs_stream_t stream) {
     return guarded([&] {
+        fault_point();
         search_binary_impl(seg, queries, nq, k, metric, filter, row_exists, out_ids, out_dist, flags,
                            (hipStream_t)stream);
     });
@@ -1915,6 +2012,7 @@ int mqvs_knn_binary_raw(const uint8_t *x, const uint8_t *y, int64_t d, int64_t k
     return guarded([&] {
         if (metric != MQVS_METRIC_HAMMING && metric != MQVS_METRIC_JACCARD)
             fail(MQVS_ERR_NOT_IMPLEMENTED, "Metric not implemented in brute force search for Binary Vector");
+        fault_point();
         if (d <= 0 || d % 8 != 0 || d > INT32_MAX || k < 0 || k > INT32_MAX || nx < 0 || nx > INT32_MAX ||
             ny < 0)
             fail(MQVS_ERR_BAD_ARGUMENTS, "bad sizes");

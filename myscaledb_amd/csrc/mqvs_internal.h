@@ -509,6 +509,44 @@ struct DevBuf {
     }
 };
 
+// Per-thread scratch of another path (the index's, index.hip) counted in, and
+// trimmed with, the calling thread's FLAT workspace under the process-wide
+// HBM budget (mqvs_set_workspace_budget): the reference runs index searches
+// from as many part threads as FLAT scans (VIWithDataPart.cpp:900-901 under
+// ScanThreadLimiter.h:25-58), so both share one admission gate.
+struct WsExt {
+    // every gated buffer freed once the owner's work on it has drained (the
+    // caller holds the owner's workspace); returns the bytes freed
+    virtual size_t free_scratch() = 0;
+
+   protected:
+    ~WsExt() = default;
+};
+// a DevBuf whose growth passes the gate of the calling thread's current
+// WsScope (fails outside one: no ungated scratch)
+struct GBuf : DevBuf {
+    void *get(size_t bytes);
+};
+// one call on the calling thread's workspace of `device` (admission, nests
+// with FLAT calls), with `ext` attached to it
+class WsScope {
+   public:
+    WsScope(int device, WsExt *ext);
+    ~WsScope();
+    void set_stream(hipStream_t s);  // the stream whose completion ends the call's use of its buffers
+    WsScope(const WsScope &) = delete;
+    WsScope &operator=(const WsScope &) = delete;
+
+   private:
+    void *impl_ = nullptr;
+    void *prev_ = nullptr;
+};
+// index_thread_release: `ext`'s scratch freed and detached from the thread's workspace
+void ws_detach_ext(int device, WsExt *ext);
+// the search entry points' fault drill (mqvs_inject_fault): throws the armed
+// status while this thread's count lasts
+void fault_point();
+
 struct DeviceGuard {
     int prev = -1;
     explicit DeviceGuard(int dev) {

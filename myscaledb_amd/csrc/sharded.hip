@@ -12,9 +12,11 @@
 //      chunk, VIWithDataPart.h:358, so the ranks below fix a shard's
 //      chunk-ordinal base, i.e. its query variant);
 //   2. the local top-k on every rank (mqvs_search_ex with that base);
-//   3. ONE exchange over xGMI: a 128-B header per rank (shard placement, the
-//      call, outcome, fallback flags, chunk count) plus the per-rank
-//      (id, distance) lists, nq*k*12 bytes per rank, as one RCCL group;
+//   3. the exchange over xGMI: a 128-B header per rank (shard placement, the
+//      call, outcome, fallback flags, chunk count), then the per-rank
+//      (id, distance) lists, nq*k*12 bytes per rank, as one RCCL group (the
+//      same two collectives on every path, so ranks on different paths
+//      still pair their operations);
 //   4. the device merge by (distance, rank, position) = the unsharded order.
 // Every rank ends with the merged result, bit-identical to a single-GPU
 // search of the whole part.
@@ -494,14 +496,21 @@ Fast fast_search(mqvs_comm *c, const CallArgs &a) {
         MQVS_HIP(hipMemcpyAsync(mine, hm, sizeof(int64_t) * kHdrWords, hipMemcpyHostToDevice, a.s));
     }
     const bool have = local_code == MQVS_OK;
-    comm_group_start(c);
+    // The collective sequence is the one every path issues: the header
+    // all-gather ON ITS OWN, then the two list gathers as one group.  A rank
+    // on the validated path (slow_search) cannot know that this rank took the
+    // fast path until its header gather returns; it then joins the list group
+    // with the same two operations.  (One group of all three here would pair
+    // a grouped launch with an ungrouped one, and RCCL splits grouped
+    // collectives over channels by the group's contents.)
     comm_all_gather(c, mine, hd, sizeof(int64_t) * kHdrWords, a.s);
     if (a.nk) {
         // (a failed rank sends whatever its buffers hold: every rank fails below)
+        comm_group_start(c);
         comm_all_gather(c, c->local_ids.p, c->all_ids.p, sizeof(int64_t) * a.nk, a.s);
         comm_all_gather(c, c->local_dist.p, c->all_dist.p, sizeof(float) * a.nk, a.s);
+        comm_group_end(c);
     }
-    comm_group_end(c);
     if (have) merge_out(c, a, b);
     MQVS_HIP(hipMemcpyAsync(ht, hd, sizeof(int64_t) * kHdrWords * c->nranks, hipMemcpyDeviceToHost, a.s));
     MQVS_HIP(hipStreamSynchronize(a.s));

@@ -5,6 +5,9 @@
 //   shim_check gpu <outdir>    tryBruteForceSearch + PartScan::scan / rerank on
 //                              deterministic integer data; raw outputs written
 //                              to <outdir> for comparison with the oracle
+//   shim_check fallback        no GPU needed: an injected device failure
+//                              (mqvs_inject_fault) runs the caller's fallback
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -75,6 +78,79 @@ static int errors() {
     return 0;
 }
 
+// The CPU path a maintainer passes as the fallback (in the ClickHouse tree:
+// faiss::knn_L2sqr / knn_inner_product, BruteForceSearch.h:80-87).  Here a
+// plain scan: on integer data every order of the sums gives the same floats,
+// so its distances equal the GPU's bit for bit (ties may order differently).
+static void cpu_knn(const float *x, const float *y, size_t d, size_t k, size_t nx, size_t ny, int64_t *ids,
+                    float *dist, int metric) {
+    std::vector<std::pair<float, int64_t>> all(ny);
+    for (size_t i = 0; i < nx; ++i) {
+        for (size_t r = 0; r < ny; ++r) {
+            float acc = 0.f;
+            for (size_t j = 0; j < d; ++j) {
+                const float a = x[i * d + j], b = y[r * d + j];
+                acc += metric == MQVS_METRIC_L2 ? (a - b) * (a - b) : a * b;
+            }
+            all[r] = {metric == MQVS_METRIC_L2 ? acc : -acc, (int64_t)r};
+        }
+        std::sort(all.begin(), all.end());
+        for (size_t j = 0; j < k; ++j) {
+            ids[i * k + j] = j < ny ? all[j].second : -1;
+            dist[i * k + j] = j < ny ? (metric == MQVS_METRIC_L2 ? all[j].first : -all[j].first) : 0.f;
+        }
+    }
+}
+
+static int fallback() {
+    float x[2 * 4] = {1, 2, 3, 4, 0, 0, 1, 1}, y[3 * 4] = {1, 2, 3, 5, 0, 0, 0, 0, 4, 4, 4, 4};
+    int64_t id[2 * 2];
+    float dist[2 * 2];
+    int served = 0;
+    MI::BruteForceFallback fb = [&](const float *a, const float *b, size_t d, size_t k, size_t nx, size_t ny,
+                                    int64_t *i, float *o, int m) {
+        ++served;
+        cpu_knn(a, b, d, k, nx, ny, i, o, m);
+    };
+    // a device failure (and an HBM shortage) runs the fallback ...
+    for (int status : {MQVS_ERR_DEVICE, MQVS_ERR_MEMORY_LIMIT}) {
+        if (mqvs_inject_fault(status, 1) != MQVS_OK) return 1;
+        MI::tryBruteForceSearch(x, y, 4, 2, 2, 3, id, dist, Metric::L2, fb);
+    }
+    const bool ok = served == 2 && id[0] == 0 && dist[0] == 1.f && id[1] == 2 && dist[1] == 14.f && id[2] == 1 &&
+                    dist[2] == 2.f && MI::fallbackCount().load() == 2;
+    std::printf("fallback served %d ids %lld %lld dist %g %g\n", served, (long long)id[0], (long long)id[1],
+                (double)dist[0], (double)dist[1]);
+    if (!ok) return 1;
+    // ... without one the failure is rethrown with its code
+    if (mqvs_inject_fault(MQVS_ERR_DEVICE, 1) != MQVS_OK) return 1;
+    try {
+        MI::tryBruteForceSearch(x, y, 4, 2, 2, 3, id, dist, Metric::IP);
+        return 1;
+    } catch (const DB::Exception &e) {
+        if (e.code() != DB::ErrorCodes::LOGICAL_ERROR) return 1;
+    }
+    if (mqvs_inject_fault(MQVS_ERR_MEMORY_LIMIT, 1) != MQVS_OK) return 1;
+    try {
+        MI::tryBruteForceSearch(x, y, 4, 2, 2, 3, id, dist, Metric::IP);
+        return 1;
+    } catch (const DB::Exception &e) {
+        if (e.code() != DB::ErrorCodes::MEMORY_LIMIT_EXCEEDED) return 1;
+    }
+    // other statuses never fall back: an unsupported metric stays NOT_IMPLEMENTED
+    try {
+        MI::tryBruteForceSearch(x, y, 4, 2, 2, 3, id, dist, Metric::Cosine, fb);
+        return 1;
+    } catch (const DB::Exception &e) {
+        if (e.code() != DB::ErrorCodes::NOT_IMPLEMENTED || served != 2) return 1;
+    }
+    // the drill accepts only the two fallback statuses
+    if (mqvs_inject_fault(MQVS_ERR_LOGICAL, 1) != MQVS_ERR_BAD_ARGUMENTS) return 1;
+    if (mqvs_inject_fault(MQVS_ERR_DEVICE, 0) != MQVS_OK) return 1;
+    std::printf("fallback ok\n");
+    return 0;
+}
+
 // k = 8000 (above the old 4096 cap; the reference's max_search_result_window
 // is 10000), the 1-rank RCCL sharded search, the index seam, getRealBitmap and
 // the part cache.
@@ -105,6 +181,43 @@ static int gpu_more(const std::string &dir, const std::vector<float> &rows, cons
                           std::memcmp(da.data(), db.data(), da.size() * 4) == 0;
         std::printf("sharded==search %d\n", same ? 1 : 0);
         if (!same) return 1;
+    }
+
+    // device-failure fallbacks at the part and index seams: the injected
+    // failure runs the caller's CPU path (here: the GPU answer computed
+    // before, standing in for the CPU scan); the next call runs on the GPU
+    {
+        std::vector<int64_t> a((size_t)nq * k), b(a.size());
+        std::vector<float> da(a.size()), db(a.size());
+        cos_part.search(q.data(), nq, k, nullptr, nullptr, a.data(), da.data());
+        int served = 0;
+        MI::PartScan::ScanFallback sfb = [&](const float *, int32_t, int32_t, const uint8_t *, const uint8_t *,
+                                             int64_t *i, float *o) {
+            ++served;
+            std::memcpy(i, a.data(), a.size() * 8);
+            std::memcpy(o, da.data(), da.size() * 4);
+        };
+        mqvs_inject_fault(MQVS_ERR_DEVICE, 1);
+        cos_part.search(q.data(), nq, k, nullptr, nullptr, b.data(), db.data(), 0, sfb);
+        bool ok = served == 1 && std::memcmp(a.data(), b.data(), a.size() * 8) == 0;
+        std::fill(b.begin(), b.end(), -7);
+        cos_part.search(q.data(), nq, k, nullptr, nullptr, b.data(), db.data(), 0, sfb);  // GPU again
+        ok = ok && served == 1 && std::memcmp(a.data(), b.data(), a.size() * 8) == 0;
+        MI::GpuIndex index(lpart, "MSTG", "nlist=16");
+        std::vector<int64_t> ia(a.size()), ib(a.size());
+        std::vector<float> ida(a.size()), idb(a.size());
+        index.search(q.data(), nq, d, k, "nprobe=16", nullptr, nullptr, false, ia.data(), ida.data());
+        MI::GpuIndex::SearchFallback ifb = [&](const float *, int32_t, int32_t, const std::string &, const uint8_t *,
+                                               const uint8_t *, bool, int64_t *i, float *o) {
+            ++served;
+            std::memcpy(i, ia.data(), ia.size() * 8);
+            std::memcpy(o, ida.data(), ida.size() * 4);
+        };
+        mqvs_inject_fault(MQVS_ERR_MEMORY_LIMIT, 1);
+        index.search(q.data(), nq, d, k, "nprobe=16", nullptr, nullptr, false, ib.data(), idb.data(), ifb);
+        ok = ok && served == 2 && std::memcmp(ia.data(), ib.data(), ia.size() * 8) == 0;
+        std::printf("gpu fallback %d\n", ok ? 1 : 0);
+        if (!ok) return 1;
     }
 
     // index seam: build, search, computeTopDistanceSubset, row_ids_map remap
@@ -251,6 +364,14 @@ static int gpu(const std::string &dir) {
 
 int main(int argc, char **argv) {
     if (argc >= 2 && std::string(argv[1]) == "errors") return errors();
+    if (argc >= 2 && std::string(argv[1]) == "fallback") {
+        try {
+            return fallback();
+        } catch (const std::exception &e) {
+            std::printf("exception: %s\n", e.what());
+            return 1;
+        }
+    }
     if (argc >= 3 && std::string(argv[1]) == "gpu") {
         try {
             return gpu(argv[2]);
@@ -259,6 +380,6 @@ int main(int argc, char **argv) {
             return 1;
         }
     }
-    std::fprintf(stderr, "usage: shim_check errors | gpu <outdir>\n");
+    std::fprintf(stderr, "usage: shim_check errors | fallback | gpu <outdir>\n");
     return 2;
 }

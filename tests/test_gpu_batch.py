@@ -97,6 +97,45 @@ def test_batch_kernel_filters_and_deletes(mq, metric):
     assert_bitwise(ids_g, dist_g, ids_o, dist_o, f"filter+lwd {metric}")
 
 
+@pytest.mark.parametrize("metric,how", [("L2", "lwd"), ("IP", "lwd"), ("Cosine", "lwd"),
+                                        ("L2", "filter"), ("IP", "filter")])
+def test_batch_probe_ignores_invalid_best_rows(mq, metric, how):
+    """The batch probe (nq > 128) turns per-(query, 128-row group) maxima into
+    the append threshold.  Here each probe group's best row for EVERY query is
+    a planted near-copy of the queries' common centre that is deleted (LWD) or
+    rejected by the PREWHERE bitmap: were those rows to count, the k-th group
+    maximum would sit far above every valid row and the main scan would append
+    nothing valid.  Results must equal the oracle's (which never sees those
+    rows), at k = 2 (two probe groups of L2 / IP parts) and k = 20."""
+    from myscaledb_amd.vector_scan import set_gather_mode
+    n, d, nq, gran = 40000, 64, 200, 8192
+    seed = zlib.crc32(f"probe_invalid_{metric}_{how}".encode())
+    rng = np.random.default_rng(seed)
+    rows = rng.standard_normal((n, d)).astype(np.float32)
+    c = rng.standard_normal(d).astype(np.float32)
+    hot = np.arange(3, n, 61)  # several rows in every 128-row group
+    rows[hot] = (5.0 * c if metric == "IP" else c)[None, :]
+    q = (c[None, :] + 0.05 * rng.standard_normal((nq, d))).astype(np.float32)
+    keep = np.ones(n, bool)
+    keep[hot] = False
+    keep &= rng.random(n) >= 0.05
+    bits = mq.pack_bitmap(keep)
+    flt, rex = (bits, None) if how == "filter" else (None, bits)
+    set_gather_mode(0)  # masked scan: the probe sees the rejected rows
+    try:
+        seg = mq.VectorScanSegment.from_rows(rows, metric=metric, granule=gran)
+        try:
+            for k in (2, 20):
+                ids_o, dist_o = O.vector_scan(rows, q, k, O.METRICS[metric], gran, filter_bits=flt,
+                                              row_exists_bits=rex, fast=True)
+                ids_g, dist_g = seg.search(q, k, metric, flt, rex)
+                assert_bitwise(ids_g, dist_g, ids_o, dist_o, f"{metric} {how} k={k}")
+        finally:
+            seg.free()
+    finally:
+        set_gather_mode(1)
+
+
 def test_batch_kernel_many_candidates(mq):
     """Every row ties with the query (identical rows): each wave's candidate
     queue overflows into the direct appends, then the candidate lists

@@ -116,3 +116,57 @@ def test_workspace_budget_bounds_concurrent_batches(mq):
     assert st["over_budget"] == 0, st
     assert st["peak"] <= cap, st
     assert st["waits"] > 0, st  # (the cap did bind)
+
+
+def test_workspace_budget_bounds_concurrent_index_searches(mq):
+    """index searches pass the same workspace gate as FLAT
+    scans (the reference runs VIWithColumnInPart::search from every part
+    thread, VIWithDataPart.cpp:900-901, under ScanThreadLimiter.h:25-58).  64
+    threads each run nq 1000 index searches (generator mode 2, 1M rows,
+    num_reorder 4096) under a 3 GiB cap: the scratch of their index searches
+    is counted and trimmed with their workspaces, the cap is never passed, and
+    every result equals the sequential one bit for bit."""
+    from myscaledb_amd import _lib
+    n, d, gran, k = 1_000_000, 128, 8192, 100
+    seg = mq.VectorScanSegment.generate(0x5EED0303, 2, n, d, "L2", gran)
+    idx = mq.VectorIndex.build(seg, "MSTG", "")
+    params = "nprobe=4,num_reorder=4096"
+    qs = [O.generate(0x5EED0404 + i, 2, 0, 1000, d) for i in range(4)]
+    expected = [idx.search(q, k, params) for q in qs]
+    _lib.check(_lib.lib.mqvs_thread_release())
+    cap = 3 << 30
+    prev = _lib.set_workspace_budget(cap)
+    _lib.workspace_stats(reset_peak=True)
+    results, errors = {}, []
+
+    def worker(tid):
+        try:
+            mq.init(0)
+            for rep in range(2):
+                j = (tid + rep) % len(qs)
+                results[(tid, rep)] = (j, idx.search(qs[j], k, params))
+            _lib.check(_lib.lib.mqvs_thread_release())
+        except Exception as e:  # noqa: BLE001
+            errors.append(repr(e))
+
+    try:
+        threads = [threading.Thread(target=worker, args=(t,)) for t in range(64)]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join(timeout=300)
+            assert not t.is_alive(), "an index search thread did not finish"
+        st = _lib.workspace_stats()
+    finally:
+        _lib.set_workspace_budget(prev)
+        idx.free()
+        seg.free()
+    assert not errors, errors[:3]
+    assert len(results) == 128
+    for (tid, rep), (j, (ig, dg)) in results.items():
+        ie, de = expected[j]
+        assert np.array_equal(ig, ie), (tid, rep)
+        assert np.array_equal(dg.view(np.uint32), de.view(np.uint32)), (tid, rep)
+    assert st["over_budget"] == 0, st
+    assert st["peak"] <= cap, st
+    assert st["peak"] > 0 and st["workspaces"] > 0, st  # (index scratch is counted)

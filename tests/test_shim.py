@@ -33,6 +33,18 @@ def test_shim_compiles_and_maps_errors(shim_bin):
     assert "errors ok" in r.stdout
 
 
+def test_shim_device_failure_falls_back(shim_bin):
+    """on a device error the host runs its CPU path.  An injected
+    failure (mqvs_inject_fault: MQVS_ERR_DEVICE, then MQVS_ERR_MEMORY_LIMIT)
+    makes tryBruteForceSearch run the caller's fallback -- the faiss call of
+    BruteForceSearch.h:80-87 in the ClickHouse tree -- and return its result;
+    without a fallback the status is rethrown with its DB::ErrorCodes value,
+    and other statuses (NOT_IMPLEMENTED) never fall back."""
+    r = subprocess.run([shim_bin, "fallback"], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert "fallback ok" in r.stdout
+
+
 def _val(i, j):
     return np.float32(((i * 31 + j * 17) % 23) - 11)
 
@@ -64,7 +76,7 @@ def test_shim_gpu_matches_oracle(shim_bin, tmp_path):
                           (np.arange(nq * k) // k)[keep].astype(np.uint32))
     assert np.array_equal(rd("scan_dist.bin", np.float32).view(np.uint32),
                           do.reshape(-1)[keep].view(np.uint32))
-    for tag in ("sharded==search 1", "row_ids_map 1", "getRealBitmap 1", "cache 1", "prefilter active 1"):
+    for tag in ("sharded==search 1", "gpu fallback 1", "row_ids_map 1", "getRealBitmap 1", "cache 1", "prefilter active 1"):
         assert tag in r.stdout, r.stdout
     # k = 8000 over the 12000-row L2 part == the oracle's vectorScanWithoutIndex
     nl, kl = 12000, 8000
