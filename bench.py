@@ -681,6 +681,13 @@ class DistCtx:
     def all_ok(self, ok):
         return self.max(0.0 if ok else 1.0) == 0.0
 
+    def first_error(self, err):
+        """The lowest failing rank's error message (None when every rank is
+        fine), the same on every rank."""
+        objs = [None] * self.world
+        self.tdist.all_gather_object(objs, err)
+        return next((f"rank {r}: {e}" for r, e in enumerate(objs) if e), None)
+
     def process_wide(self, fn):
         fn()  # (every process holds its own library state)
 
@@ -691,6 +698,7 @@ class LoopShared:
         self.n = n
         self.bar = threading.Barrier(n, timeout=timeout)
         self.vals = [0.0] * n
+        self.errs = [None] * n
 
 
 class LoopCtx:
@@ -715,6 +723,13 @@ class LoopCtx:
     def all_ok(self, ok):
         return self.max(0.0 if ok else 1.0) == 0.0
 
+    def first_error(self, err):
+        self.sh.errs[self.rank] = err
+        self.sh.bar.wait()
+        e = next((f"rank {r}: {x}" for r, x in enumerate(self.sh.errs) if x), None)
+        self.sh.bar.wait()
+        return e
+
     def process_wide(self, fn):
         self.sh.bar.wait()
         if self.rank == 0:
@@ -730,8 +745,9 @@ def step_all(ctx, fn, what):
         r, err = fn(), None
     except Exception as e:  # noqa: BLE001
         r, err = None, f"{what}: {type(e).__name__}: {e}"
-    if not ctx.all_ok(err is None):
-        raise LegError(err or f"{what}: failed on another rank")
+    first = ctx.first_error(err)
+    if first is not None:
+        raise LegError(first)
     return r
 
 

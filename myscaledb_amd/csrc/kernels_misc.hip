@@ -145,9 +145,11 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
     }
     if (metric != MQVS_METRIC_COSINE) {
         if (phase == 2) return;
+        // (columns d .. qs: zeros; the table is not cleared beforehand and
+        // the padded readers take them)
 #pragma unroll
         for (int u = 0; u < J; ++u)
-            if (lane + 64 * u < d) v0[lane + 64 * u] = x[u];
+            if (lane + 64 * u < qs) v0[lane + 64 * u] = x[u];
         const float sum = blas ? seq_sq_sum<J>(x, d) : 0.0f;
         if (lane == 0) {
             if (qnorms) qnorms[j] = sum;
@@ -173,7 +175,7 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
             float *cur = v0 + (int64_t)v * qs;
 #pragma unroll
             for (int u = 0; u < J; ++u)
-                if (lane + 64 * u < d) cur[lane + 64 * u] = x[u];
+                if (lane + 64 * u < qs) cur[lane + 64 * u] = x[u];  // (x = 0 past d)
         }
         if (phase == 1) {
             if (lane == 0 && qnorms) qnorms[j] = 0.0f;
@@ -202,6 +204,13 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
                     qlam[j] = v - u;
                     if (qnorms) qnorms[j] = 0.0f;
                 }
+                // the variants past the chain are never selected, but the bf16
+                // plane and the bound read every stored one: zeros (the table
+                // is not cleared beforehand)
+                // (16-B stores: variants are 128-B aligned, qs a multiple of 32)
+                float4 *z = reinterpret_cast<float4 *>(v0 + (int64_t)v * qs);
+                const int64_t n4 = (int64_t)(maxv - v) * qs / 4;
+                for (int64_t i = lane; i < n4; i += 64) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
                 return;
             }
         }
@@ -244,7 +253,7 @@ __global__ __launch_bounds__(64) void k_query_prep_lds(const float *q, int nq, i
         return r;
     };
     if (metric != MQVS_METRIC_COSINE) {
-        for (int i = lane; i < d; i += 64) v0[i] = qbuf[i];
+        for (int i = lane; i < qs; i += 64) v0[i] = i < d ? qbuf[i] : 0.0f;
         const float sum = blas ? seqsum() : 0.0f;
         if (lane == 0) {
             if (qnorms) qnorms[j] = sum;
@@ -268,6 +277,8 @@ __global__ __launch_bounds__(64) void k_query_prep_lds(const float *q, int nq, i
                 qbuf[i] = x;
             }
         }
+        if (cur)
+            for (int i = d + lane; i < qs; i += 64) cur[i] = 0.0f;  // (padding columns)
         __syncthreads();
         for (int u = 0; u < v; ++u) {
             const float *o = v0 + (int64_t)u * qs;
@@ -280,6 +291,8 @@ __global__ __launch_bounds__(64) void k_query_prep_lds(const float *q, int nq, i
                     qlam[j] = v - u;
                     if (qnorms) qnorms[j] = 0.0f;
                 }
+                for (int w = v; w < maxv; ++w)  // (unused variants: zeros)
+                    for (int i = lane; i < qs; i += 64) v0[(int64_t)w * qs + i] = 0.0f;
                 return;
             }
         }
@@ -388,6 +401,27 @@ __global__ void k_pack(const uint8_t *bytes, int64_t n, uint8_t *bits) {
         }
         bits[b] = v;
     }
+}
+
+// Up to two 32-bit fills in one launch (the small status / counter / list-tail
+// fills of a search: a runtime memset is a ~4 us kernel of its own each)
+__global__ void k_fill2(uint32_t *a, int64_t na, uint32_t va, uint32_t *b, int64_t nb, uint32_t vb) {
+    const int64_t stride = (int64_t)gridDim.x * blockDim.x;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < na + nb; i += stride) {
+        if (i < na)
+            a[i] = va;
+        else
+            b[i - na] = vb;
+    }
+}
+
+void launch_fill2(uint32_t *a, int64_t na, uint32_t va, uint32_t *b, int64_t nb, uint32_t vb, hipStream_t s) {
+    if (!a) na = 0;
+    if (!b) nb = 0;
+    const int64_t n = na + nb;
+    if (n <= 0) return;
+    const int64_t blocks = std::min<int64_t>((n + 255) / 256, 4096);
+    hipLaunchKernelGGL(k_fill2, dim3((unsigned)blocks), dim3(256), 0, s, a, na, va, b, nb, vb);
 }
 
 void launch_pack_nonempty(const uint8_t *bytes, int64_t n, uint8_t *bits, hipStream_t s) {

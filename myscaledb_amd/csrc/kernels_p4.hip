@@ -41,8 +41,9 @@
 // make the wave wait for every LDS-DMA piece in flight; a full queue falls back
 // to exactly that (correct, slower).
 //
-// PROBE (p.p4_gmax set): the same scan over the probe rows, with no threshold
-// tests: per query and 128-row half tile (one wave's rows of an item) the
+// PROBE (p.p4_gmax set; searches without a PREWHERE filter or deletes, whose
+// group maxima could come from rows that do not count): the same scan over
+// the probe rows, with no threshold tests: per query and 128-row half tile (one wave's rows of an item) the
 // best approximate value is written to p4_gmax[q][2 t + wr] as a raw metric
 // value (L2: fl(qn - 2 acc)).  The k-th best of those maxima is the k-th best
 // of k actual rows, so k_probe_select_wide turns it into an append threshold
@@ -138,26 +139,6 @@ __device__ inline f32x4 p4_aread4(float a, float b, float c, float d) {
         : "=v"(x), "=v"(y), "=v"(z), "=v"(w)
         : "a"(a), "a"(b), "a"(c), "a"(d));
     return f32x4{x, y, z, w};
-}
-
-// PROBE: values of rows that row_valid rejects (PREWHERE filter, empty array
-// under a filter, lightweight delete) become -inf.  Lane value v4[g][i] is
-// row r0 + rbl + GS g + i; rows at or past the item's end are already -inf.
-template <int GS>
-__device__ inline void p4_mask_invalid_t(const ScanParams &p, f32x4 (&v4)[4], int r0, int rbl, int ecrn) {
-#pragma unroll
-    for (int g = 0; g < 4; ++g)
-#pragma unroll
-        for (int i = 0; i < 4; ++i) {
-            const int rl = rbl + GS * g + i;
-            if (rl < ecrn && !row_valid(p, (int64_t)r0 + rl)) v4[g][i] = -__builtin_inff();
-        }
-}
-__device__ inline void p4_mask_invalid(const ScanParams &p, f32x4 (&v4)[4], int r0, int rbl, int gs, int ecrn) {
-    if (gs == 16)
-        p4_mask_invalid_t<16>(p, v4, r0, rbl, ecrn);
-    else
-        p4_mask_invalid_t<8>(p, v4, r0, rbl, ecrn);
 }
 
 __device__ inline void p4_barrier() {
@@ -469,9 +450,6 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
                 for (int r = 0; r < 16; ++r)
                     if (rbl + (r & 3) + 8 * (r >> 2) >= ecrn) v4[r >> 2][r & 3] = -__builtin_inff();
             }
-            // (filtered / deleted rows never define a group's best value, as
-            // in k_scan_p4m below)
-            if (p.filter || p.exists) p4_mask_invalid(p, v4, ecr0, wr * 128 + rb * 32 + 4 * h, 8, ecrn);
             float mx = v4[0][0];
 #pragma unroll
             for (int r = 1; r < 16; ++r) mx = __builtin_elementwise_maximum(mx, v4[r >> 2][r & 3]);
@@ -549,7 +527,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
                     wq_base[slot_] = u32x4{__builtin_bit_cast(unsigned, raw), row, (unsigned)j, 0u};
                 else  // queue full: the direct append (its returned slot makes
                       // this wave wait for its LDS-DMA in flight: correct, slower)
-                    emit_approx<METRIC, false>(p, j, row, row, row_valid(p, row), raw);
+                    emit_approx<METRIC, false, false>(p, j, row, row, row_valid(p, row), raw);
             }
             qcnt += __popcll(m);
         }
@@ -709,7 +687,15 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
 // B fragment 7 read at the start of phase 0 instead of the end of phase 1,
 // +0.4..2.4 % main scan; waves 2 and 3 issuing their DMA pieces in phase 1,
 // +15 %.)
-template <int METRIC, int NBUF, bool PROBE = false, int GRP = 0>
+// DIAG (measurement builds only; wrong results, timing only): 1 = no stage
+// barrier, 2 = no DMA pieces issued, 4 = no threshold tests (the accumulators
+// kept live by one read per block)
+// PLM: where a stage's 8 DMA pieces (of stage s + D) go: 0 = phase 0 gaps
+// 8, 11, .., 29; 1 = phase 0 gaps 0, 4, .., 28; 2 = the 4 row pieces in phase
+// 0 (gaps 8, 14, 20, 26), the 4 query pieces in phase 1 (gaps 0, 8, 16, 24,
+// after the barrier: stage s + D's buffer was last read before barrier
+// s - 1); 3 = all 8 in phase 1 gaps 0, 4, .., 28
+template <int METRIC, int NBUF, bool PROBE = false, int GRP = 0, int DIAG = 0, int PLM = 0>
 __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u32x4 *queue, int qcap, int tmap) {
     constexpr bool L2 = METRIC == MQVS_METRIC_L2;
     constexpr int D = NBUF - 1;
@@ -867,6 +853,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
     int si = 0, issued = 0, ibuf = 0, items_issued = 0;
     bool live = true;
     auto issue_piece = [&](int x) __attribute__((always_inline)) {
+        if constexpr ((DIAG & 2) != 0) return;
         unsigned char *dst = lds + ibuf * kP4Stage;
         if (x < 4) {
             __builtin_amdgcn_global_load_lds((const void *)(rbase + plane_step_off((uint32_t)si) + roff[x]),
@@ -957,13 +944,6 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
                 for (int r = 0; r < 16; ++r)
                     if (rbl + 16 * (r >> 2) + (r & 3) >= ecrn) v4[r >> 2][r & 3] = -__builtin_inff();
             }
-            // rows the PREWHERE bitmap rejects or a lightweight delete
-            // removed never define a group's best value: each maximum must be
-            // one VALID row's approximate value, or the k-th of them is
-            // tighter than the k-th valid row's (true neighbours would then
-            // fail the append test).  (Uniform branch: probes without a
-            // filter or deletes skip it.)
-            if (p.filter || p.exists) p4_mask_invalid(p, v4, ecr0, rbl, 16, ecrn);
         }
         const int j = q0 + wq * 128 + jb * 16 + l16;
         if constexpr (PROBE && GRP == 16) {
@@ -981,6 +961,10 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
                     p.p4_gmax[(int64_t)j * p.p4_gld + 16 * eti + 8 * wr + 4 * hf + g] = raw;
                 }
             }
+            return;
+        }
+        if constexpr (!PROBE && (DIAG & 4) != 0) {
+            if (v4[0][0] == -1.2345e-30f) qcnt += 1;  // (diagnostic: keep the accumulators live)
             return;
         }
         float mx = v4[0][0];
@@ -1036,7 +1020,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
                 if (slot_ < qcap)
                     wq_base[slot_] = u32x4{__builtin_bit_cast(unsigned, raw), row, (unsigned)j, 0u};
                 else
-                    emit_approx<METRIC, false>(p, j, row, row, row_valid(p, row), raw);
+                    emit_approx<METRIC, false, false>(p, j, row, row, row_valid(p, row), raw);
             }
             qcnt += __popcll(m);
         }
@@ -1072,8 +1056,12 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
                 acc[rb][jb] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[rb], b[jb], acc[rb][jb], 0, 0, 0);
             if constexpr (x >= 2 && x < 6)
                 a[2 + x] = frag(st, rowA + (2 + x) * 16 * 64 + offm);
-            else if constexpr (x >= 8 && (x - 8) % 3 == 0 && (x - 8) / 3 < 8)
+            if constexpr (PLM == 0 && x >= 8 && (x - 8) % 3 == 0 && (x - 8) / 3 < 8)
                 issue_piece((x - 8) / 3);
+            else if constexpr (PLM == 1 && (x & 3) == 0)
+                issue_piece(x >> 2);
+            else if constexpr (PLM == 2 && x >= 8 && (x - 8) % 6 == 0)
+                issue_piece((x - 8) / 6);
             __builtin_amdgcn_sched_barrier(0);
         });
     };
@@ -1100,6 +1088,10 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
                 a[x >> 2] = frag(sn, rowA + (x >> 2) * 16 * 64 + offm);
             if constexpr (LAST && (x & 3) == 2)
                 check(std::integral_constant<int, 0>{}, std::integral_constant<int, jb>{}, cr0, crn, ti_c);
+            if constexpr (PLM == 2 && (x & 7) == 0)
+                issue_piece(4 + (x >> 3));
+            else if constexpr (PLM == 3 && (x & 3) == 0)
+                issue_piece(x >> 2);
             __builtin_amdgcn_sched_barrier(0);
         });
     };
@@ -1108,13 +1100,21 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
         const unsigned char *st = lds + cbuf * kP4Stage;
         const int nbuf_next = cbuf + 1 == NBUF ? 0 : cbuf + 1;
         phase0(st, first_tag, epi_tag);
-        if (L2 && si == 0 && live) issue_piece(8);
-        issue_advance();
+        if constexpr (PLM < 2) {
+            if (L2 && si == 0 && live) issue_piece(8);
+            issue_advance();
+        }
         const bool has_next = gc + 1 < issued;
-        p4_wait_vm<NPW>(issued - gc - 2, has_next);
+        // (PLM 2: the row half of stage gc + D is issued and younger than
+        // stage gc + 1's pieces; PLM 3: none of it yet)
+        p4_wait_vm<NPW, PLM == 2 ? NPW / 2 : 0>(issued - gc - 2, has_next);
         asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        p4_barrier();
+        if constexpr ((DIAG & 1) == 0) p4_barrier();
         phase1(lds + nbuf_next * kP4Stage, first_tag, last_tag, cr1 - cr0);
+        if constexpr (PLM >= 2) {
+            if (L2 && si == 0 && live) issue_piece(8);
+            issue_advance();
+        }
         ++gc;
         cbuf = nbuf_next;
     };
@@ -1347,6 +1347,23 @@ static bool launch_p4_any(const ScanParams &p, hipStream_t s) {
     const dim3 grid((unsigned)(8 * per_xcd));
     auto *qq = reinterpret_cast<u32x4 *>(c.p4_queue);
     const int tmap = tune_int("MQVS_P4_MAP", 1);
+    if constexpr (kDebugTuning) {
+        // measurement builds: decomposition variants (wrong results)
+        const int diag = tune_int("MQVS_P4M_DIAG", 0);
+        const int plm = tune_int("MQVS_P4M_PL", 0);
+#define MQVS_P4M(DG_, PL_)                                                                                          \
+    hipLaunchKernelGGL((k_scan_p4m<METRIC, 4, false, 0, DG_, PL_>), grid, dim3(256), 0, s, c, slots, qq, kP4QueueCap, \
+                       tmap)
+        if (diag == 1) MQVS_P4M(1, 0);
+        else if (diag == 4) MQVS_P4M(4, 0);
+        else if (diag == 6) MQVS_P4M(6, 0);
+        else if (plm == 1) MQVS_P4M(0, 1);
+        else if (plm == 2) MQVS_P4M(0, 2);
+        else if (plm == 3) MQVS_P4M(0, 3);
+        else MQVS_P4M(0, 0);
+#undef MQVS_P4M
+        return true;
+    }
     hipLaunchKernelGGL((k_scan_p4m<METRIC, 4>), grid, dim3(256), 0, s, c, slots, qq, kP4QueueCap, tmap);
     return true;
 }
@@ -1355,6 +1372,12 @@ static bool launch_p4_any(const ScanParams &p, hipStream_t s) {
 // probe rows cannot take the batch kernel (the caller runs the dense probe)
 template <int METRIC>
 static bool launch_p4_probe_t(ScanParams p, hipStream_t s) {
+    // Group maxima are taken over every row of a group: with a PREWHERE
+    // filter or lightweight deletes the best row of a group may be one that
+    // row_valid rejects, and the k-th maximum would then be tighter than the
+    // k-th VALID row's value (true neighbours would fail the append test).
+    // Such searches keep the dense probe, which masks invalid rows.
+    if (p.filter || p.exists) return false;
     if (!p.p4_gmax || p.p4_gld < 2 * p.tiles || !p4_ok(p, false)) return false;
     if (METRIC == MQVS_METRIC_L2 && !p.row_norms) return false;
     int dev = 0, cus = 0;

@@ -62,6 +62,7 @@ struct WsGate {
     int active = 0;             // threads inside a call
     int blocked = 0;            // of them, waiting for memory
     int admitting = 0;          // threads waiting to start a call
+    int trimming = 0;           // workspaces being freed outside the mutex (their bytes still in held)
     int64_t waits = 0, trims = 0, over = 0;
     std::vector<Workspace *> all;
 };
@@ -185,6 +186,7 @@ static bool trim_idle(std::unique_lock<std::mutex> &lk, WsGate &g, Workspace *me
         expect += w->held - w->sticky.cap;
     }
     if (victims.empty()) return false;
+    g.trimming += (int)victims.size();
     lk.unlock();
     for (Workspace *w : victims) (void)w->trim();
     lk.lock();
@@ -194,6 +196,7 @@ static bool trim_idle(std::unique_lock<std::mutex> &lk, WsGate &g, Workspace *me
         w->held = std::min(w->held, w->sticky.cap);
         w->trimming = false;
         ++g.trims;
+        --g.trimming;
         w->use.unlock();
     }
     g.cv.notify_all();
@@ -220,8 +223,9 @@ void *Workspace::get(DevBuf &b, size_t bytes) {
             while (g.held + g.reserved + rest > B) {
                 trim_idle(lk, g, this, rest, B);
                 if (g.held + g.reserved + rest <= B) break;
+                // (memory being freed outside the mutex comes back: wait for it)
                 const int others = g.active - g.blocked - (depth > 0 ? 1 : 0);
-                if (others <= 0) {
+                if (others <= 0 && g.trimming == 0) {
                     ++g.over;  // every running call waits: go over rather than deadlock
                     break;
                 }
@@ -268,7 +272,8 @@ struct WsCall {
         bool counted = false;
         while (g.held + g.reserved + extra > B) {
             trim_idle(lk, g, &ws, extra, B);
-            if (g.held + g.reserved + extra <= B || g.active == 0) break;  // (nobody to wait for)
+            // (nobody to wait for: no running call, no trim in flight)
+            if (g.held + g.reserved + extra <= B || (g.active == 0 && g.trimming == 0)) break;
             if (!counted) ++g.waits;
             counted = true;
             ++g.admitting;
@@ -296,6 +301,7 @@ struct WsCall {
             const size_t B = g_ws_budget.load(std::memory_order_relaxed);
             self_trim = (g.blocked > 0 || g.admitting > 0 || (B && g.held > B)) && ws.held > ws.sticky.cap &&
                         hipEventQuery(ws.done) == hipSuccess;
+            if (self_trim) ++g.trimming;  // (waiters wait for these bytes instead of going over)
             g.cv.notify_all();
         }
         if (self_trim) {
@@ -306,6 +312,7 @@ struct WsCall {
             g.held -= std::min(g.held, ws.held - std::min(ws.held, ws.sticky.cap));
             ws.held = std::min(ws.held, ws.sticky.cap);
             ++g.trims;
+            --g.trimming;
             g.cv.notify_all();
         }
         ws.use.unlock();
@@ -543,9 +550,10 @@ static int prep_variants(Workspace &ws, const float *dq, int nq, int d, bool cos
     int maxv = cos ? (maxv_override > 0 ? maxv_override : kMaxVariants) : 1;
     for (int pass = 0; pass < 2; ++pass) {
         const size_t bytes = sizeof(float) * (size_t)nq * maxv * qstride;
+        // (no clear of the table: the prep writes every stored variant,
+        // zeros past a query's chain)
         qvars = (float *)ws.get(ws.qvars, bytes);
-        MQVS_HIP(hipMemsetAsync(qvars, 0, bytes, s));
-        if (pass > 0 || !zeroed_status) MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
+        if (pass > 0 || !zeroed_status) launch_fill2((uint32_t *)status, 4, 0u, nullptr, 0, 0u, s);
         launch_query_prep(dq, nq, d, cos ? MQVS_METRIC_COSINE : MQVS_METRIC_L2, l2norms, qvars, maxv, qnorms, qmu,
                           qlam, status, s);
         MQVS_HIP(hipGetLastError());
@@ -793,7 +801,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     int *qmu = nullptr, *qlam = nullptr, *status = nullptr;
     // one zeroed block for the status words: [overflow 4][status 4][count nq]
     int *fl = (int *)ws.get(ws.flags, sizeof(int) * (8 + (size_t)nq));
-    MQVS_HIP(hipMemsetAsync(fl, 0, sizeof(int) * (8 + (size_t)nq), s));
+    launch_fill2((uint32_t *)fl, 8 + (int64_t)nq, 0u, nullptr, 0, 0u, s);
     // The query-variant table starts at kMaxVariants per query without a host
     // round trip; a chain that does not repeat within it on a part of more
     // chunk ordinals (rare: small-integer data) is caught from the status word
@@ -852,7 +860,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         launch_gather_list(dfilter, seg->nonempty_bits, dexists, n, seg->granule, gtile, gcount, goff, list, s);
         MQVS_HIP(hipGetLastError());
         if (gpadded > selected && gtile == 1)  // the dense list's tail: -1 entries up to a whole tile
-            MQVS_HIP(hipMemsetAsync(list + selected, 0xFF, sizeof(int32_t) * (size_t)(gpadded - selected), s));
+            launch_fill2((uint32_t *)(list + selected), gpadded - selected, 0xFFFFFFFFu, nullptr, 0, 0u, s);
         row_list = list;
         scan_n = gpadded;
         st.gather = 1;
@@ -878,6 +886,13 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         // waves of the first segments down the append path: measured net
         // loss at nq = 1000 with a 64 MB cap on the probe matrix)
         P = std::max<int64_t>(P, 8 * (int64_t)k);
+        // A gathered scan's appends take the per-row path (list lookup,
+        // bitmap tests, norms), so a loose first threshold is costly there:
+        // at 1 % of 50M rows a 1024-position probe left ~10 % of the first
+        // segment's rows passing (110 us for 66k positions, then a 45 us
+        // refinement).  A probe of scan_n / 16 positions (<= 16384) costs
+        // about the same launch and cuts the first segment's appends ~16x.
+        if (row_list) P = std::max<int64_t>(P, std::min<int64_t>(scan_n / 16, 16384));
         P = round_up(P, aligned ? seg->granule : tile_rows);
         if (P > scan_n) P = scan_n;
     }
@@ -1117,9 +1132,8 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
                 fail(MQVS_ERR_LOGICAL, "candidate overflow: more than " + std::to_string(cap) +
                                            " rows tie at the k-th distance");
             launch_cand_tau(cand, count, cap, nq, k, metric, tau, nullptr, s);
-            MQVS_HIP(hipMemsetAsync(count, 0, sizeof(int) * nq, s));
+            launch_fill2((uint32_t *)count, nq, 0u, (uint32_t *)overflow, 4, 0u, s);
             run_scan(p, make_range(0, scan_n, tile_rows, seg->granule, aligned), kind, metric, false, s);
-            MQVS_HIP(hipMemsetAsync(overflow, 0, sizeof(int) * 4, s));
             launch_final_select(cand, count, cap, nq, k, metric, seg->granule, seg->row_offset, dids,
                                 ddist, overflow, large, s);
             MQVS_HIP(hipGetLastError());
@@ -1443,7 +1457,7 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[5], s));
     scan(0, P, true, false);
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[1], s));
-    MQVS_HIP(hipMemsetAsync(count, 0, sizeof(int) * nq, s));
+    launch_fill2((uint32_t *)count, nq, 0u, nullptr, 0, 0u, s);
     launch_probe_select(p.probe, P, P, nq, k, kOrder, tau, count, cand, cap, 0, nullptr, s);
     MQVS_HIP(hipGetLastError());
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[2], s));
@@ -1472,7 +1486,7 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
         st.segments = segs;
     }
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[3], s));
-    MQVS_HIP(hipMemsetAsync(overflow, 0, sizeof(int) * 4, s));
+    launch_fill2((uint32_t *)overflow, 4, 0u, nullptr, 0, 0u, s);
     launch_final_select(cand, count, cap, nq, k, kOrder, 0, seg->row_offset, dids, ddist, overflow, large, s);
     MQVS_HIP(hipGetLastError());
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[4], s));
@@ -1498,9 +1512,8 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
                 fail(MQVS_ERR_LOGICAL, "candidate overflow: more than " + std::to_string(cap) +
                                            " rows tie at the k-th distance");
             launch_cand_tau(cand, count, cap, nq, k, kOrder, tau, nullptr, s);
-            MQVS_HIP(hipMemsetAsync(count, 0, sizeof(int) * nq, s));
+            launch_fill2((uint32_t *)count, nq, 0u, (uint32_t *)overflow, 4, 0u, s);
             scan(0, n, false, false);
-            MQVS_HIP(hipMemsetAsync(overflow, 0, sizeof(int) * 4, s));
             launch_final_select(cand, count, cap, nq, k, kOrder, 0, seg->row_offset, dids, ddist, overflow, large,
                                 s);
             MQVS_HIP(hipGetLastError());

@@ -312,6 +312,8 @@ void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, flo
 void launch_generate(uint64_t seed, int mode, int64_t row0, int64_t n, int d, float *out,
                      hipStream_t s);
 void launch_pack_nonempty(const uint8_t *bytes, int64_t n, uint8_t *bits, hipStream_t s);
+// up to two 32-bit fills (a: na words of va, b: nb words of vb) in one launch
+void launch_fill2(uint32_t *a, int64_t na, uint32_t va, uint32_t *b, int64_t nb, uint32_t vb, hipStream_t s);
 void launch_chunk_ordinals(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists,
                            int64_t n, int64_t chunk_rows, int require_filter, int *ord,
                            hipStream_t s);
