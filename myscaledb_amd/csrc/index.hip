@@ -105,7 +105,7 @@ struct IndexWorkspace final : WsExt {
     hipStream_t side = nullptr;
     int64_t *host = nullptr;  // pinned: the search's stats [4] and status word (one sync, no staging copies)
     GBuf queries, qvars, qnorms, qmu, qlam, status, qhi, probes, cprobes, filter, exists, rows, out_ids, out_dist,
-        ord, dmap, dwords, pdist, cqhi, gmax;
+        ord, dmap, dwords, pdist, cqhi, gmax, crec, cbq;
     ListBufs coarse, fine;
     // WsExt: the owner is between calls (its workspace's `done` event passed:
     // the main stream, which joins the side chain, has drained)
@@ -113,7 +113,7 @@ struct IndexWorkspace final : WsExt {
         if (side) (void)hipStreamSynchronize(side);
         size_t b = 0;
         for (GBuf *x : {&queries, &qvars, &qnorms, &qmu, &qlam, &status, &qhi, &probes, &cprobes, &filter, &exists,
-                        &rows, &out_ids, &out_dist, &ord, &dmap, &dwords, &pdist, &cqhi, &gmax}) {
+                        &rows, &out_ids, &out_dist, &ord, &dmap, &dwords, &pdist, &cqhi, &gmax, &crec, &cbq}) {
             b += x->cap;
             x->release();
         }
@@ -901,7 +901,9 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
         // (variant 0 of every query: the raw query, or the normalised one for
         // cosine -- centroids of cosine parts are normalised: same ranking as
         // the raw inner product)
-        launch_to_hi(qvars, nq, d, (int64_t)maxv * qstride, cs->dpad, 1, vpad, cq, nullptr, nullptr, s);
+        // (with the variants' norm records: the pick's bf16 bound)
+        float *crec = (float *)ws.crec.get(sizeof(float) * kMxRec * (size_t)nq);
+        launch_to_hi(qvars, nq, d, (int64_t)maxv * qstride, cs->dpad, 1, vpad, cq, crec, nullptr, s);
         MQVS_HIP(hipGetLastError());
         ScanParams cp{};
         cp.rows_hi = cs->rows_hi;
@@ -925,8 +927,15 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
         cp.p4_gld = gld;
         if (launch_scan_p4_groups(cp, ix->coarse_metric, s)) {
             MQVS_HIP(hipGetLastError());
+            // each query's bound on |bf16 group value - exact| (the direct
+            // formula's rounding terms: the larger of the two)
+            float *cbq = (float *)ws.cbq.get(sizeof(float) * (size_t)nq);
+            ScanParams bp = cp;
+            bp.blas_nq = 1;
+            launch_query_bound(bp, ix->coarse_metric, cs->ynorm_max, crec, cs->ynorm_max + 4, cbq, s);
+            MQVS_HIP(hipGetLastError());
             launch_coarse_pick(cp.p4_gmax, gld, 16 * cp.tiles, nprobe + 2, nprobe, ix->coarse_metric, qvars,
-                               (int64_t)maxv * qstride, cs->rows, cs->norms, cs->n, d, nq, probes, s);
+                               (int64_t)maxv * qstride, cs->rows, cs->norms, cs->n, d, cbq, nq, probes, s);
             MQVS_HIP(hipGetLastError());
             picked = true;
         }

@@ -1017,10 +1017,17 @@ void launch_centroid_mean(const float *rows, int d, const int32_t *order, const 
 // ---------------------------------------------------------------------------
 // The coarse step's pick (index.hip): per query, from the batch probe's best
 // approximate value of every 16-centroid group (kernels_p4.hip, GRP 16), the
-// T best groups -- every centroid among the query's T best lies in one of
-// them (a group outside holds nothing better than the T-th group maximum) --
-// then the exact fp32 value of each centroid of those groups and the nprobe
-// best.  One workgroup per query; T <= kCoarsePickMaxT.
+// T best groups, then the exact fp32 value of each centroid of those groups
+// and the nprobe best.  The group maxima are bf16 values within bq (the
+// query's bound on |approx - exact|, k_query_bound) of the exact ones: a
+// centroid of a group left out has exact value <= its group maximum + bq <=
+// the T-th maximum + bq, while the T taken groups hold T >= nprobe
+// centroids of exact value >= the T-th maximum - bq; so every group whose
+// maximum is within 2 bq of the T-th (widen) is taken as well -- up to Tcap
+// groups in all, beyond which near-ties among more than Tcap groups are cut
+// (counted nowhere: the probes are then approximate, as any IVF's).  The
+// probes are the exact top-nprobe of the centroids (in this pick's fp32 dot
+// order).  One workgroup per query; Tcap <= kCoarsePickMaxT.
 //
 // The group keys are staged in LDS once (up to kPickStage groups: 131072
 // lists), so the four radix passes read LDS, not L2.  The exact values are
@@ -1033,9 +1040,9 @@ constexpr int kPickU = 4;
 
 template <int METRIC, bool STAGED>  // METRIC: MQVS_METRIC_L2 or kMetricIpRaw (the coarse metric)
 __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T,
-                                                             int nprobe, const float *q, int64_t qld,
+                                                             int Tcap, int nprobe, const float *q, int64_t qld,
                                                              const float *cent, const float *cnorm, int64_t ncent,
-                                                             int d, int64_t *probes) {
+                                                             int d, const float *bq, int64_t *probes) {
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh[4];
     __shared__ int s_grp[kCoarsePickMaxT];
@@ -1045,7 +1052,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
     extern __shared__ uint4 dyn[];
     uint4 *recs = dyn;
     int NR = 1;
-    while (NR < 16 * T) NR <<= 1;
+    while (NR < 16 * Tcap) NR <<= 1;
     uint32_t *keys = reinterpret_cast<uint32_t *>(dyn + NR);
     const int qi = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const float *row = gmax + (int64_t)qi * gld;
@@ -1060,19 +1067,26 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
         s_valid = 0;
     }
     __syncthreads();
-    // the groups strictly better than the T-th, then its ties up to T
+    // the groups strictly better than the T-th, then those within 2 bq of it
+    // (its ties included), up to Tcap
+    uint32_t kthr = th;
+    if (th < 0xFFFFFFFEu && bq) {
+        const float w = widen<METRIC>(okey_value<METRIC>(th), bq[qi]);
+        const uint32_t kw = okey<METRIC>(w);
+        kthr = w == w && kw > th ? kw : th;
+    }
     for (int pass = 0; pass < 2; ++pass) {
         for (int64_t i = t; i < ngroups; i += SEL_THREADS) {
             const uint32_t k = keyof(i);
             if (k == 0xFFFFFFFFu) continue;
-            const bool take = th == 0xFFFFFFFEu ? pass == 0 : (pass == 0 ? k < th : k == th);
+            const bool take = th == 0xFFFFFFFEu ? pass == 0 : (pass == 0 ? k < th : k <= kthr && k >= th);
             if (!take) continue;
             const int slot = atomicAdd(&s_ng, 1);
-            if (slot < T) s_grp[slot] = (int)i;
+            if (slot < Tcap) s_grp[slot] = (int)i;
         }
         __syncthreads();
     }
-    const int ng = min(s_ng, T);
+    const int ng = min(s_ng, Tcap);
     const int M = 16 * ng;
     // exact values: wave wv scores centroids c0 .. c0 + kPickU - 1, lanes over
     // float4 columns (scalar columns when d or the rows are not 16-B aligned)
@@ -1175,14 +1189,16 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
 
 void launch_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T, int nprobe, int metric,
                         const float *q, int64_t qld, const float *cent, const float *cnorm, int64_t ncent, int d,
-                        int nq, int64_t *probes, hipStream_t s) {
+                        const float *bq, int nq, int64_t *probes, hipStream_t s) {
     if (nq <= 0) return;
-#define MQVS_PICK(M, ST)                                                                                             \
-    hipLaunchKernelGGL((k_coarse_pick<M, ST>), dim3(nq), dim3(SEL_THREADS), lds, s, gmax, gld, ngroups, T, nprobe, q, \
-                       qld, cent, cnorm, ncent, d, probes)
+    // room for the groups within the bound of the T-th (near-ties)
+    const int Tcap = std::min(kCoarsePickMaxT, T + std::max(T, 8));
+#define MQVS_PICK(M, ST)                                                                                         \
+    hipLaunchKernelGGL((k_coarse_pick<M, ST>), dim3(nq), dim3(SEL_THREADS), lds, s, gmax, gld, ngroups, T, Tcap, \
+                       nprobe, q, qld, cent, cnorm, ncent, d, bq, probes)
     const bool staged = ngroups <= kPickStage;
     size_t nr = 1;
-    while (nr < (size_t)16 * T) nr <<= 1;
+    while (nr < (size_t)16 * Tcap) nr <<= 1;
     const size_t lds = nr * sizeof(uint4) + (staged ? sizeof(uint32_t) * (size_t)ngroups : 0);
     if (metric == MQVS_METRIC_L2) {
         if (staged) MQVS_PICK(MQVS_METRIC_L2, true); else MQVS_PICK(MQVS_METRIC_L2, false);

@@ -122,16 +122,51 @@ __device__ __forceinline__ float seq_sq_sum(const float (&x)[J], int d) {
     return acc;
 }
 
+// The same sum through LDS: the rounded products are stored once, and every
+// lane walks them in order from 16-B broadcast reads (4 elements per read;
+// the reads run ahead of the dependent adds).  Same order, same bits.
+template <int J>
+__device__ __forceinline__ float seq_sq_sum_lds(const float (&x)[J], float *prod) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int u = 0; u < J; ++u) prod[lane + 64 * u] = x[u] * x[u];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the stores landed (one wave)
+    __builtin_amdgcn_wave_barrier();
+    float acc = 0.0f;
+    const float4 *p4 = reinterpret_cast<const float4 *>(prod);
+#pragma unroll 8
+    for (int i = 0; i < 16 * J; ++i) {
+        const float4 v = p4[i];
+        acc = acc + v.x;
+        acc = acc + v.y;
+        acc = acc + v.z;
+        acc = acc + v.w;
+    }
+    __builtin_amdgcn_wave_barrier();  // (the next step rewrites prod)
+    return acc;
+}
+
 // J > 0: d <= 64 J, the query in registers.
 // phase 0: everything.  Cosine searches whose first consumers need only
 // variant 0 split the work: phase 1 writes variant 0 (and |q|^2 = 0); phase 2,
 // launched after it (on a side stream, concurrent with the coarse step and the
 // list scan), walks the rest of the chain -- it compares against the stored
 // variant 0 but does not rewrite it -- and writes mu, lambda and the status.
-template <int J>
+// SUMV: 0 = readlane walk (seq_sq_sum), 1 = LDS broadcast walk
+// (seq_sq_sum_lds; the launcher's: 39.0 -> 35.5 us at nq 1, 72.5 -> 65.7 us
+// at nq 1000 for d = 768, bit-identical tables, tools/qprep_sum_ab.hip,
+// profiles/r05/qprep_sum_ab.jsonl)
+template <int J, int SUMV = 0>
 __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d, int metric, int blas, float *qvars,
                                                    int maxv, float *qnorms, int *qmu, int *qlam, int *status,
                                                    int phase) {
+    __shared__ __attribute__((aligned(16))) float prod[SUMV ? 64 * J : 1];
+    auto sqsum = [&](const float(&xx)[J]) -> float {
+        if constexpr (SUMV == 1)
+            return seq_sq_sum_lds<J>(xx, prod);
+        else
+            return seq_sq_sum<J>(xx, 0);
+    };
     const int j = blockIdx.x;
     const int lane = threadIdx.x;
     const int64_t qs = (int64_t)((d + 31) / 32 * 32);
@@ -150,7 +185,7 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
 #pragma unroll
         for (int u = 0; u < J; ++u)
             if (lane + 64 * u < qs) v0[lane + 64 * u] = x[u];
-        const float sum = blas ? seq_sq_sum<J>(x, d) : 0.0f;
+        const float sum = blas ? sqsum(x) : 0.0f;
         if (lane == 0) {
             if (qnorms) qnorms[j] = sum;
             qmu[j] = 0;
@@ -165,7 +200,7 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
     // registers); only a signature match is confirmed element by element.
     extern __shared__ uint64_t sig[];  // maxv + 1 signatures
     for (int v = 0; v <= maxv; ++v) {
-        const float sum = seq_sq_sum<J>(x, d);
+        const float sum = sqsum(x);
         if (!(sum < eps)) {
             const float sr = sqrtf(sum);
 #pragma unroll
@@ -311,7 +346,7 @@ void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, flo
     const size_t lds = (size_t)((d + 31) / 32 * 32 + 4) * sizeof(float);
     const size_t sig = (size_t)(maxv + 1) * sizeof(uint64_t);
 #define MQVS_QP(J)                                                                                               \
-    hipLaunchKernelGGL(k_query_prep<J>, dim3(nq), dim3(64), sig, s, q, nq, d, metric, blas ? 1 : 0, qvars, maxv, \
+    hipLaunchKernelGGL((k_query_prep<J, 1>), dim3(nq), dim3(64), sig, s, q, nq, d, metric, blas ? 1 : 0, qvars, maxv, \
                        qnorms, qmu, qlam, status, phase)
     if (d <= 128)
         MQVS_QP(2);

@@ -454,13 +454,14 @@ void launch_gather_rows(const float *src, int64_t src_ld, int d, const int64_t *
                         hipStream_t s);
 constexpr int kCoarsePickMaxT = 64;  // groups a coarse pick may take per query
 // the coarse step's pick from the batch probe's 16-centroid group maxima
-// (kernels_ivf.hip): per query the T best groups (T <= 64), the exact values
-// of their centroids (coarse metric: L2 or kMetricIpRaw), the nprobe best ->
-// probes[q][0, nprobe) (-1 when fewer)
+// (kernels_ivf.hip): per query the T best groups (T <= 64) and every group
+// within 2 bq[q] of the T-th (bq: the query's bf16 bound, k_query_bound;
+// null = none), the exact values of their centroids (coarse metric: L2 or
+// kMetricIpRaw), the nprobe best -> probes[q][0, nprobe) (-1 when fewer)
 void index_thread_release();  // index.hip: the calling thread's index workspaces
 void launch_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T, int nprobe, int metric,
                         const float *q, int64_t qld, const float *cent, const float *cnorm, int64_t ncent, int d,
-                        int nq, int64_t *probes, hipStream_t s);
+                        const float *bq, int nq, int64_t *probes, hipStream_t s);
 // the batch probe by 16-row groups (kernels_p4.hip): p.p4_gmax[q][16 t + r]
 // = the best value of rows [16 r, 16 r + 16) of tile t (p.p4_gld >= 16
 // p.tiles); false when the rows cannot take the batch kernel

@@ -35,6 +35,8 @@ for f in ('$O/seg_ab_nq1.jsonl','$O/seg_ab_nq16.jsonl'):
     for l in open(f):
         d=json.loads(l); print(d['tune'], d['nq'], 'wall', d['wall_ms'], 'med', d.get('wall_med_ms'), 'main', d['main_ms'], 'segs', d['segments'], 'eq', d['bitwise_eq_exact'])
 " ;;
+    qprep_ab) timeout -k 10 120 ./tools/bin/qprep_sum_ab > $O/qprep_sum_ab.jsonl 2> $O/qprep_sum_ab.err || exit 1
+              cat $O/qprep_sum_ab.jsonl ;;
     *) echo "unknown step $step"; exit 2 ;;
   esac
   echo "step $step ok"

@@ -1,0 +1,57 @@
+// A/B of the cosine query prep's sequential square sum (kernels_misc.hip
+// k_query_prep): SUMV 0 = v_readlane walk, 1 = LDS broadcast walk.  Both must
+// write bit-identical variant tables; prints the best of 20 launches at
+// nq = 1 and nq = 1000 (generator mode 1, d = 768, maxv 32).
+//   hipcc -O3 -std=c++17 --offload-arch=gfx950 -ffp-contract=off tools/qprep_sum_ab.hip -o tools/bin/qprep_sum_ab
+#include "../myscaledb_amd/csrc/kernels_misc.hip"
+
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+using namespace mqvs;
+
+template <int V>
+static float run(const float *q, int nq, int d, int maxv, float *qv, float *qn, int *mu, int *lam, int *st) {
+    hipEvent_t a, b;
+    (void)hipEventCreate(&a);
+    (void)hipEventCreate(&b);
+    float best = 1e9f;
+    const size_t sig = (size_t)(maxv + 1) * sizeof(uint64_t);
+    for (int it = 0; it < 20; ++it) {
+        (void)hipMemset(st, 0, 16);
+        (void)hipEventRecord(a);
+        hipLaunchKernelGGL((k_query_prep<12, V>), dim3(nq), dim3(64), sig, 0, q, nq, d, MQVS_METRIC_COSINE, 0, qv, maxv,
+                           qn, mu, lam, st, 0);
+        (void)hipEventRecord(b);
+        (void)hipEventSynchronize(b);
+        float ms;
+        (void)hipEventElapsedTime(&ms, a, b);
+        if (ms < best) best = ms;
+    }
+    return best * 1e3f;
+}
+
+int main() {
+    const int d = 768, maxv = 32;
+    for (int nq : {1, 1000}) {
+        float *q, *qv[2], *qn;
+        int *mu, *lam, *st;
+        (void)hipMalloc(&q, sizeof(float) * nq * d);
+        for (auto &p : qv) (void)hipMalloc(&p, sizeof(float) * (size_t)nq * maxv * d);
+        (void)hipMalloc(&qn, sizeof(float) * nq);
+        (void)hipMalloc(&mu, sizeof(int) * nq);
+        (void)hipMalloc(&lam, sizeof(int) * nq);
+        (void)hipMalloc(&st, sizeof(int) * 4);
+        launch_generate(0x5EED0002ull, 1, 0, nq, d, q, 0);
+        const float t0 = run<0>(q, nq, d, maxv, qv[0], qn, mu, lam, st);
+        const float t1 = run<1>(q, nq, d, maxv, qv[1], qn, mu, lam, st);
+        std::vector<float> h0((size_t)nq * maxv * d), h1(h0.size());
+        (void)hipMemcpy(h0.data(), qv[0], h0.size() * 4, hipMemcpyDeviceToHost);
+        (void)hipMemcpy(h1.data(), qv[1], h1.size() * 4, hipMemcpyDeviceToHost);
+        const bool same = std::memcmp(h0.data(), h1.data(), h0.size() * 4) == 0;
+        std::printf("{\"nq\": %d, \"readlane_us\": %.2f, \"lds_us\": %.2f, \"bitwise_equal\": %s}\n", nq, t0, t1,
+                    same ? "true" : "false");
+    }
+    return 0;
+}
