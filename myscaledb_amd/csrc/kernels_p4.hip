@@ -660,7 +660,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
     for (int e = lane; e < nqueue; e += 64) {
         const u32x4 en = __builtin_nontemporal_load(wq_base + e);  // (bypasses L1)
         const uint32_t row = en[1];
-        emit_approx<METRIC, false>(p, (int)en[2], row, row, row_valid(p, row), __builtin_bit_cast(float, en[0]));
+        emit_approx<METRIC, false, false>(p, (int)en[2], row, row, row_valid(p, row), __builtin_bit_cast(float, en[0]));
     }
 }
 
@@ -1157,7 +1157,7 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
     for (int e = lane; e < nqueue; e += 64) {
         const u32x4 en = __builtin_nontemporal_load(wq_base + e);
         const uint32_t row = en[1];
-        emit_approx<METRIC, false>(p, (int)en[2], row, row, row_valid(p, row), __builtin_bit_cast(float, en[0]));
+        emit_approx<METRIC, false, false>(p, (int)en[2], row, row, row_valid(p, row), __builtin_bit_cast(float, en[0]));
     }
 }
 

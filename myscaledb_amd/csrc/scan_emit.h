@@ -6,8 +6,11 @@
 
 namespace mqvs {
 
-// AGG = false: one atomic per taker (for call sites inside register-bound
-// MFMA loops, where the appends are a rare fallback)
+// AGG = false: one atomic per taker -- the batch kernels (kernels_p4.hip),
+// whose appends are rare and spread over many queries: the aggregated form
+// there made the whole nq 1000 main scan 7 % slower (12.6 -> 13.5 ms, same-box
+// library A/B, profiles/r05/emit_agg_ab.txt: its end-of-launch queue flush
+// walks up to 64 queries per ballot round)
 template <int METRIC, bool PROBE, bool AGG = true>
 __device__ inline void emit_approx(const ScanParams &p, int j, int64_t pos, int64_t row, bool valid,
                                    float raw) {
