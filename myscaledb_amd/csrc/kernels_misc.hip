@@ -146,6 +146,44 @@ __device__ __forceinline__ float seq_sq_sum_lds(const float (&x)[J], float *prod
     return acc;
 }
 
+// The same walk software-pipelined: the 16-B reads of block b + 1 are issued
+// before the adds of block b, so the dependent add chain never waits on LDS
+// latency (the plain loop above issues a block's reads only after the previous
+// block's adds).  Same order, same bits.
+template <int J>
+__device__ __forceinline__ float seq_sq_sum_lds_pipe(const float (&x)[J], float *prod) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int u = 0; u < J; ++u) prod[lane + 64 * u] = x[u] * x[u];
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_wave_barrier();
+    constexpr int B = 4;              // float4 reads per block
+    constexpr int NB = 16 * J / B;    // blocks
+    const float4 *p4 = reinterpret_cast<const float4 *>(prod);
+    float4 cur[B], nxt[B];
+#pragma unroll
+    for (int i = 0; i < B; ++i) cur[i] = p4[i];
+    float acc = 0.0f;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+        if (b + 1 < NB) {
+#pragma unroll
+            for (int i = 0; i < B; ++i) nxt[i] = p4[(b + 1) * B + i];
+        }
+#pragma unroll
+        for (int i = 0; i < B; ++i) {
+            acc = acc + cur[i].x;
+            acc = acc + cur[i].y;
+            acc = acc + cur[i].z;
+            acc = acc + cur[i].w;
+        }
+#pragma unroll
+        for (int i = 0; i < B; ++i) cur[i] = nxt[i];
+    }
+    __builtin_amdgcn_wave_barrier();
+    return acc;
+}
+
 // J > 0: d <= 64 J, the query in registers.
 // phase 0: everything.  Cosine searches whose first consumers need only
 // variant 0 split the work: phase 1 writes variant 0 (and |q|^2 = 0); phase 2,
@@ -162,7 +200,9 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
                                                    int phase) {
     __shared__ __attribute__((aligned(16))) float prod[SUMV ? 64 * J : 1];
     auto sqsum = [&](const float(&xx)[J]) -> float {
-        if constexpr (SUMV == 1)
+        if constexpr (SUMV == 2)
+            return seq_sq_sum_lds_pipe<J>(xx, prod);
+        else if constexpr (SUMV == 1)
             return seq_sq_sum_lds<J>(xx, prod);
         else
             return seq_sq_sum<J>(xx, 0);
