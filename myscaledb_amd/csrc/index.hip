@@ -888,9 +888,9 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     // fixed stages dominate; profiles/r03/index)
     // Default (nprobe <= 62 and the centroid plane present): the batch kernel
     // scores every (query, centroid) on bf16 and keeps the best of each
-    // 16-centroid group; the nprobe + 2 best groups per query then get exact
-    // fp32 values and the nprobe best of those are the probes
-    // (k_coarse_pick).  65536 or 39063 lists at nq 1000: one batch-kernel
+    // 16-centroid group; the nprobe + 2 best groups per query (and any other
+    // group the bf16 bound cannot rule out) then get exact fp32 values and
+    // the nprobe best of those are the probes (k_coarse_pick).  65536 or 39063 lists at nq 1000: one batch-kernel
     // launch and one pick instead of mqvs_search's whole pipeline.
     bool picked = false;
     const int cmode = tune_int("MQVS_IVF_COARSE", 2);
@@ -935,7 +935,7 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
             launch_query_bound(bp, ix->coarse_metric, cs->ynorm_max, crec, cs->ynorm_max + 4, cbq, s);
             MQVS_HIP(hipGetLastError());
             launch_coarse_pick(cp.p4_gmax, gld, 16 * cp.tiles, nprobe + 2, nprobe, ix->coarse_metric, qvars,
-                               (int64_t)maxv * qstride, cs->rows, cs->norms, cs->n, d, cbq, nq, probes, s);
+                               (int64_t)maxv * qstride, cs->rows, cs->norms, cs->n, d, cbq, qnorms, nq, probes, s);
             MQVS_HIP(hipGetLastError());
             picked = true;
         }

@@ -1017,17 +1017,25 @@ void launch_centroid_mean(const float *rows, int d, const int32_t *order, const 
 // ---------------------------------------------------------------------------
 // The coarse step's pick (index.hip): per query, from the batch probe's best
 // approximate value of every 16-centroid group (kernels_p4.hip, GRP 16), the
-// T best groups, then the exact fp32 value of each centroid of those groups
-// and the nprobe best.  The group maxima are bf16 values within bq (the
-// query's bound on |approx - exact|, k_query_bound) of the exact ones: a
-// centroid of a group left out has exact value <= its group maximum + bq <=
-// the T-th maximum + bq, while the T taken groups hold T >= nprobe
-// centroids of exact value >= the T-th maximum - bq; so every group whose
-// maximum is within 2 bq of the T-th (widen) is taken as well -- up to Tcap
-// groups in all, beyond which near-ties among more than Tcap groups are cut
-// (counted nowhere: the probes are then approximate, as any IVF's).  The
-// probes are the exact top-nprobe of the centroids (in this pick's fp32 dot
-// order).  One workgroup per query; Tcap <= kCoarsePickMaxT.
+// exact fp32 value of each centroid of a few groups and the nprobe best.
+// The group maxima are bf16 values within bq (the query's bound on |approx -
+// exact|, k_query_bound) of the exact ones.
+//  1. core: the T best groups (by (key, group); large T: its ties included,
+//     up to Tcap), scored exactly;
+//     they hold T >= nprobe centroids, so the nprobe-th best exact value of
+//     the core, v, is a bound the final nprobe-th best cannot be worse than.
+//  2. extras: a group outside the core can hold a centroid better than v only
+//     if its maximum is within bq of v (its centroids' exact values are at
+//     most maximum + bq); those groups are scored too, up to Tcap groups in
+//     all, beyond which near-ties among more than Tcap groups are cut (counted
+//     nowhere: the probes are then approximate, as any IVF's).
+// Step 2 compares with the core's exact v, not with the T-th approximate
+// maximum: usually no group passes (round 5 first took every group within
+// 2 bq of the T-th maximum -- 8 more groups per query at nprobe 1, the pick
+// 50 -> ~100 us at 39063 lists).  The probes are the exact top-nprobe of the
+// centroids (in this pick's fp32 dot order).  One workgroup per query;
+// Tcap <= kCoarsePickMaxT.  qn: L2 only, |q|^2 (the group values are full
+// distances, the records |y|^2 - 2 ip).
 //
 // The group keys are staged in LDS once (up to kPickStage groups: 131072
 // lists), so the four radix passes read LDS, not L2.  The exact values are
@@ -1042,11 +1050,14 @@ template <int METRIC, bool STAGED>  // METRIC: MQVS_METRIC_L2 or kMetricIpRaw (t
 __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T,
                                                              int Tcap, int nprobe, const float *q, int64_t qld,
                                                              const float *cent, const float *cnorm, int64_t ncent,
-                                                             int d, const float *bq, int64_t *probes) {
+                                                             int d, const float *bq, const float *qnorms,
+                                                             int64_t *probes) {
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh[4];
     __shared__ int s_grp[kCoarsePickMaxT];
     __shared__ int s_ng, s_valid;
+    __shared__ uint32_t s_knp;
+    __shared__ uint64_t s_red[2 * (SEL_THREADS / 64)];
     // dynamic LDS: recs [pow2 >= 16 T] then (STAGED) keys [ngroups], sized per
     // launch so small pickups keep many workgroups per CU
     extern __shared__ uint4 dyn[];
@@ -1061,106 +1072,161 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
         __syncthreads();
     }
     auto keyof = [&](int64_t i) { return STAGED ? keys[i] : okey<METRIC>(row[i]); };
-    const uint32_t th = block_radix_select_mlp(keyof, ngroups, T, hist, sh);
+    // (the core's T groups come straight from the select for T <= kSelSmallK)
+    uint64_t tpair = ~0ull;  // the T-th (key << 32 | group)
+    int ncore = 0;
+    uint32_t th = 0xFFFFFFFEu;
+    if (T <= kSelSmallK) {
+        ncore = block_topk_small(keyof, ngroups, T, s_red, s_grp, &tpair);
+        th = tpair == ~0ull ? 0xFFFFFFFEu : (uint32_t)(tpair >> 32);
+    } else {
+        th = block_radix_select_mlp(keyof, ngroups, T, hist, sh);
+    }
     if (t == 0) {
-        s_ng = 0;
+        s_ng = ncore;
         s_valid = 0;
+        s_knp = 0xFFFFFFFFu;
     }
     __syncthreads();
-    // the groups strictly better than the T-th, then those within 2 bq of it
-    // (its ties included), up to Tcap
-    uint32_t kthr = th;
-    if (th < 0xFFFFFFFEu && bq) {
-        const float w = widen<METRIC>(okey_value<METRIC>(th), bq[qi]);
-        const uint32_t kw = okey<METRIC>(w);
-        kthr = w == w && kw > th ? kw : th;
-    }
-    for (int pass = 0; pass < 2; ++pass) {
+    // the groups whose key passes take(key, group), appended to s_grp (up to Tcap)
+    auto collect = [&](auto take) {
         for (int64_t i = t; i < ngroups; i += SEL_THREADS) {
             const uint32_t k = keyof(i);
-            if (k == 0xFFFFFFFFu) continue;
-            const bool take = th == 0xFFFFFFFEu ? pass == 0 : (pass == 0 ? k < th : k <= kthr && k >= th);
-            if (!take) continue;
+            if (k == 0xFFFFFFFFu || !take(k, i)) continue;
             const int slot = atomicAdd(&s_ng, 1);
             if (slot < Tcap) s_grp[slot] = (int)i;
         }
         __syncthreads();
-    }
-    const int ng = min(s_ng, Tcap);
-    const int M = 16 * ng;
-    // exact values: wave wv scores centroids c0 .. c0 + kPickU - 1, lanes over
-    // float4 columns (scalar columns when d or the rows are not 16-B aligned)
+    };
+    // exact values of centroids c in [cb, ce) (16 per taken group): wave wv
+    // scores centroids c0 .. c0 + kPickU - 1, lanes over float4 columns
+    // (scalar columns when d or the rows are not 16-B aligned)
     const float *qv = q + (int64_t)qi * qld;
     const bool v4 = (d & 3) == 0 && (((uintptr_t)cent | (uintptr_t)qv) & 15) == 0;
-    for (int c0 = wv * kPickU; c0 < M; c0 += (SEL_THREADS / 64) * kPickU) {
-        int64_t r[kPickU];
-        float dot[kPickU];
+    auto score = [&](int cb, int ce) {
+        for (int c0 = cb + wv * kPickU; c0 < ce; c0 += (SEL_THREADS / 64) * kPickU) {
+            int64_t r[kPickU];
+            float dot[kPickU];
 #pragma unroll
-        for (int u = 0; u < kPickU; ++u) {
-            const int c = c0 + u;
-            r[u] = c < M ? (int64_t)s_grp[c >> 4] * 16 + (c & 15) : ncent;
-            if (r[u] >= ncent) r[u] = -1;
-            dot[u] = 0.f;
-        }
-        if (v4) {
-            const float4 *q4 = reinterpret_cast<const float4 *>(qv);
-            // three column steps per round: 3 kPickU independent 16-B loads
-            // per lane in flight (d = 768 is one round)
-            const int n4 = d >> 2;
-            for (int j0 = lane; j0 < n4; j0 += 3 * 64) {
-                float4 x[3], y[3][kPickU];
+            for (int u = 0; u < kPickU; ++u) {
+                const int c = c0 + u;
+                r[u] = c < ce ? (int64_t)s_grp[c >> 4] * 16 + (c & 15) : ncent;
+                if (r[u] >= ncent) r[u] = -1;
+                dot[u] = 0.f;
+            }
+            if (v4) {
+                const float4 *q4 = reinterpret_cast<const float4 *>(qv);
+                // three column steps per round: 3 kPickU independent 16-B loads
+                // per lane in flight (d = 768 is one round)
+                const int n4 = d >> 2;
+                for (int j0 = lane; j0 < n4; j0 += 3 * 64) {
+                    float4 x[3], y[3][kPickU];
 #pragma unroll
-                for (int t = 0; t < 3; ++t) {
-                    const int j = j0 + 64 * t;
-                    const bool in = j < n4;
-                    x[t] = in ? q4[j] : float4{0.f, 0.f, 0.f, 0.f};
+                    for (int tt = 0; tt < 3; ++tt) {
+                        const int j = j0 + 64 * tt;
+                        const bool in = j < n4;
+                        x[tt] = in ? q4[j] : float4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+                        for (int u = 0; u < kPickU; ++u)
+                            y[tt][u] = in && r[u] >= 0 ? reinterpret_cast<const float4 *>(cent + r[u] * d)[j]
+                                                       : float4{0.f, 0.f, 0.f, 0.f};
+                    }
+#pragma unroll
+                    for (int tt = 0; tt < 3; ++tt)
+#pragma unroll
+                        for (int u = 0; u < kPickU; ++u) {
+                            dot[u] = fmaf(x[tt].x, y[tt][u].x, dot[u]);
+                            dot[u] = fmaf(x[tt].y, y[tt][u].y, dot[u]);
+                            dot[u] = fmaf(x[tt].z, y[tt][u].z, dot[u]);
+                            dot[u] = fmaf(x[tt].w, y[tt][u].w, dot[u]);
+                        }
+                }
+            } else {
+                for (int e = lane; e < d; e += 64) {
+                    const float x = qv[e];
 #pragma unroll
                     for (int u = 0; u < kPickU; ++u)
-                        y[t][u] = in && r[u] >= 0 ? reinterpret_cast<const float4 *>(cent + r[u] * d)[j]
-                                                  : float4{0.f, 0.f, 0.f, 0.f};
+                        if (r[u] >= 0) dot[u] = fmaf(x, cent[r[u] * d + e], dot[u]);
                 }
+            }
 #pragma unroll
-                for (int t = 0; t < 3; ++t)
+            for (int u = 0; u < kPickU; ++u) {
+                float v = dot[u];
+                for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+                dot[u] = v;
+            }
+            if (lane < kPickU) {
+                float dv = dot[0];
+                int64_t rv = r[0];
 #pragma unroll
-                    for (int u = 0; u < kPickU; ++u) {
-                        dot[u] = fmaf(x[t].x, y[t][u].x, dot[u]);
-                        dot[u] = fmaf(x[t].y, y[t][u].y, dot[u]);
-                        dot[u] = fmaf(x[t].z, y[t][u].z, dot[u]);
-                        dot[u] = fmaf(x[t].w, y[t][u].w, dot[u]);
+                for (int u = 1; u < kPickU; ++u)
+                    if (lane == u) {
+                        dv = dot[u];
+                        rv = r[u];
                     }
-            }
-        } else {
-            for (int e = lane; e < d; e += 64) {
-                const float x = qv[e];
-#pragma unroll
-                for (int u = 0; u < kPickU; ++u)
-                    if (r[u] >= 0) dot[u] = fmaf(x, cent[r[u] * d + e], dot[u]);
-            }
-        }
-#pragma unroll
-        for (int u = 0; u < kPickU; ++u) {
-            float v = dot[u];
-            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-            dot[u] = v;
-        }
-        if (lane < kPickU) {
-            float dv = dot[0];
-            int64_t rv = r[0];
-#pragma unroll
-            for (int u = 1; u < kPickU; ++u)
-                if (lane == u) {
-                    dv = dot[u];
-                    rv = r[u];
+                const int c = c0 + lane;
+                if (c < ce) {
+                    uint32_t key = 0xFFFFFFFFu;
+                    if (rv >= 0) key = okey<METRIC>(METRIC == MQVS_METRIC_L2 ? cnorm[rv] - 2.0f * dv : dv);
+                    recs[c] = uint4{key, (uint32_t)(rv >= 0 ? rv : 0xFFFFFFFFu), 0u, 0u};
+                    if (key != 0xFFFFFFFFu) atomicAdd(&s_valid, 1);
                 }
-            const int c = c0 + lane;
-            if (c < M) {
-                uint32_t key = 0xFFFFFFFFu;
-                if (rv >= 0) key = okey<METRIC>(METRIC == MQVS_METRIC_L2 ? cnorm[rv] - 2.0f * dv : dv);
-                recs[c] = uint4{key, (uint32_t)(rv >= 0 ? rv : 0xFFFFFFFFu), 0u, 0u};
-                if (key != 0xFFFFFFFFu) atomicAdd(&s_valid, 1);
             }
         }
+        __syncthreads();
+    };
+    // 1. core: the T best (key, group) pairs (large T: the groups better than
+    // the T-th key, then its ties)
+    if (T > kSelSmallK) {
+        collect([&](uint32_t k, int64_t) { return th == 0xFFFFFFFEu || k < th; });
+        if (th != 0xFFFFFFFEu) collect([&](uint32_t k, int64_t) { return k == th; });
+        tpair = th == 0xFFFFFFFEu ? ~0ull : ((uint64_t)th << 32) | 0xFFFFFFFFull;  // (every tie is in)
     }
+    const int ng0 = min(s_ng, Tcap);
+    score(0, 16 * ng0);
+    int ng = ng0;
+    // 2. extras (needs the bound and a full core; fewer than T valid groups:
+    // every group is in the core already)
+    if (bq && tpair != ~0ull && s_ng < Tcap) {
+        const int M0 = 16 * ng0;
+        for (int c = t; c < M0; c += SEL_THREADS) {
+            const uint4 e = recs[c];
+            if (e.x == 0xFFFFFFFFu) continue;
+            int rank = 0;
+            for (int o = 0; o < M0; ++o) rank += rec_less(recs[o], e) ? 1 : 0;
+            if (rank == nprobe - 1) s_knp = e.x;
+        }
+        __syncthreads();
+        uint32_t kx;
+        if (s_knp != 0xFFFFFFFFu) {
+            // the approximate maximum a group needs: v -/+ bq (rounding slack
+            // as widen's), v a full distance for L2
+            float v = okey_value<METRIC>(s_knp);
+            if (METRIC == MQVS_METRIC_L2) v = qnorms[qi] + v;
+            const float b = bq[qi];
+            float w;
+            if (METRIC == MQVS_METRIC_L2) {
+                w = v + b;
+                w = w + fabsf(w) * 2.4e-7f + 1e-30f;
+            } else {
+                w = v - b;
+                w = w - fabsf(w) * 2.4e-7f - 1e-30f;
+            }
+            kx = w == w ? okey<METRIC>(w) : th;
+        } else {
+            // fewer than nprobe valid centroids in the core: every group
+            // within 2 bq of the T-th maximum
+            const float w = widen<METRIC>(okey_value<METRIC>(th), bq[qi]);
+            kx = w == w ? okey<METRIC>(w) : th;
+        }
+        if (kx >= th)
+            collect([&](uint32_t k, int64_t i) {
+                return k <= kx && (((uint64_t)k << 32) | (uint64_t)(uint32_t)i) > tpair;
+            });
+        ng = min(s_ng, Tcap);
+        if (ng > ng0) score(M0, 16 * ng);
+    }
+    const int M = 16 * ng;
     __syncthreads();
     const int nvalid = s_valid;
     if (M <= 256) {
@@ -1189,13 +1255,13 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
 
 void launch_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T, int nprobe, int metric,
                         const float *q, int64_t qld, const float *cent, const float *cnorm, int64_t ncent, int d,
-                        const float *bq, int nq, int64_t *probes, hipStream_t s) {
+                        const float *bq, const float *qnorms, int nq, int64_t *probes, hipStream_t s) {
     if (nq <= 0) return;
     // room for the groups within the bound of the T-th (near-ties)
     const int Tcap = std::min(kCoarsePickMaxT, T + std::max(T, 8));
 #define MQVS_PICK(M, ST)                                                                                         \
     hipLaunchKernelGGL((k_coarse_pick<M, ST>), dim3(nq), dim3(SEL_THREADS), lds, s, gmax, gld, ngroups, T, Tcap, \
-                       nprobe, q, qld, cent, cnorm, ncent, d, bq, probes)
+                       nprobe, q, qld, cent, cnorm, ncent, d, bq, qnorms, probes)
     const bool staged = ngroups <= kPickStage;
     size_t nr = 1;
     while (nr < (size_t)16 * Tcap) nr <<= 1;

@@ -461,7 +461,7 @@ constexpr int kCoarsePickMaxT = 64;  // groups a coarse pick may take per query
 void index_thread_release();  // index.hip: the calling thread's index workspaces
 void launch_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T, int nprobe, int metric,
                         const float *q, int64_t qld, const float *cent, const float *cnorm, int64_t ncent, int d,
-                        const float *bq, int nq, int64_t *probes, hipStream_t s);
+                        const float *bq, const float *qnorms, int nq, int64_t *probes, hipStream_t s);
 // the batch probe by 16-row groups (kernels_p4.hip): p.p4_gmax[q][16 t + r]
 // = the best value of rows [16 r, 16 r + 16) of tile t (p.p4_gld >= 16
 // p.tiles); false when the rows cannot take the batch kernel

@@ -147,6 +147,69 @@ __device__ inline uint32_t block_radix_select_mlp(KeyFn keyof, int64_t count, in
     return prefix;
 }
 
+// The k smallest valid keys for small k (k <= kSelSmallK): each thread keeps
+// its k smallest (key, index) pairs (insertion into registers), then k rounds
+// of a block minimum over the threads' heads (wave shuffles + one LDS
+// exchange), the owner popping its head.  Writes the popped indices in order
+// to idx_out[0 ..) and returns their count (< k: fewer valid keys);
+// *kth_out = the k-th pair (key << 32 | index), or ~0 when fewer than k.
+// 0xFFFFFFFF keys are never taken; indices < 2^32.  No histogram passes.
+// red: 2 * (NT / 64) words of LDS.
+constexpr int kSelSmallK = 8;
+template <int NT = SEL_THREADS, typename KeyFn>
+__device__ inline int block_topk_small(KeyFn keyof, int64_t count, int k, uint64_t *red, int *idx_out,
+                                       uint64_t *kth_out) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    uint64_t loc[kSelSmallK];  // (key << 32 | index), ascending
+#pragma unroll
+    for (int j = 0; j < kSelSmallK; ++j) loc[j] = ~0ull;
+    uint64_t worst = ~0ull;  // loc[k - 1]
+    for (int64_t i = t; i < count; i += NT) {
+        const uint32_t key = keyof(i);
+        if (key == 0xFFFFFFFFu) continue;
+        uint64_t v = ((uint64_t)key << 32) | (uint64_t)(uint32_t)i;
+        if (v >= worst) continue;
+#pragma unroll
+        for (int j = 0; j < kSelSmallK; ++j) {  // sorted insertion; the largest falls off
+            if (j < k && v < loc[j]) {
+                const uint64_t o = loc[j];
+                loc[j] = v;
+                v = o;
+            }
+        }
+#pragma unroll
+        for (int j = 0; j < kSelSmallK; ++j)
+            if (j == k - 1) worst = loc[j];
+    }
+    int head = 0, n = 0;
+    uint64_t last = ~0ull;
+    for (int r = 0; r < k; ++r) {
+        uint64_t h = ~0ull;
+#pragma unroll
+        for (int j = 0; j < kSelSmallK; ++j)
+            if (j == head) h = loc[j];
+        uint64_t m = h;
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint64_t o = __shfl_xor(m, off);
+            m = o < m ? o : m;
+        }
+        uint64_t *slot = red + (r & 1) * (NT / 64);
+        if (lane == 0) slot[wv] = m;
+        __syncthreads();
+        m = slot[0];
+#pragma unroll
+        for (int w = 1; w < NT / 64; ++w) m = slot[w] < m ? slot[w] : m;
+        if (m == ~0ull) break;  // fewer than k valid keys
+        if (h == m) ++head;     // (pairs are unique: one owner)
+        if (t == 0) idx_out[r] = (int)(uint32_t)m;
+        last = m;
+        ++n;
+    }
+    __syncthreads();  // (idx_out and red are read / reused by the caller)
+    *kth_out = n == k ? last : ~0ull;
+    return n;
+}
+
 // Visit every element of a float row: float4 loads, 4 in flight per thread
 // (the probe rows are megabytes; a scalar loop leaves HBM idle).
 template <int NT = SEL_THREADS, typename F>

@@ -19,6 +19,12 @@ for step in "$@"; do
              python3 tools/timeline.py $O/tr_sel1/run_kernel_trace.csv --start k_chunk_count --nth -1 ;;
     tl_nq1) trace tr_nq1 --nq 1 --searches 4 || exit 1
             python3 tools/timeline.py $O/tr_nq1/run_kernel_trace.csv --start k_query_prep --nth -1 ;;
+    tl_idx3|tl_idx2)  # one index search (mode 3 nprobe 1 / mode 2 nprobe 1), last of 3
+            m=${step#tl_idx}
+            ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$GRAFT_REPO_ROOT/$O/tr_idx$m" -o run --output-format csv \
+                -- python3 "$GRAFT_REPO_ROOT/tools/index_search_run.py" --mode $m --search nprobe=1 --searches 3 \
+                > "$GRAFT_REPO_ROOT/$O/tr_idx$m.log" 2>&1 ) || exit 1
+            python3 tools/timeline.py $O/tr_idx$m/run_kernel_trace.csv --start k_to_bf16 --nth -1 ;;
     bench_quick) timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-index --no-configs --no-config1-points --no-cpu > $O/bench_quick.json 2> $O/bench_quick.err || exit 1
                  python3 -c "import json;d=json.loads(open('$O/bench_quick.json').readlines()[-1]);print(d['value'],d['ms_per_step'],d['roofline']);print([ (x['nq'],x['ms_per_search'],x['hbm_frac_end_to_end']) for x in d['small_batch']])" ;;
     bench) timeout -k 10 900 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || exit 1 ;;
