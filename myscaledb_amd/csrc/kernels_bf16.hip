@@ -157,7 +157,9 @@ __global__ __launch_bounds__(kPsThreads) void k_probe_select_wide(const float *p
     const float *row = probe + (int64_t)q * ld;
     uint32_t prefix = 0, mask = 0, kk = (uint32_t)k;
     bool none = false;
-    for (int pass = 0; pass < 4; ++pass) {
+    // three passes: the top 24 bits of the k-th key; the bound below takes the
+    // low byte set (an upper bound on the k-th key, as block_radix_select<3>)
+    for (int pass = 0; pass < 3; ++pass) {
         const int shift = 24 - 8 * pass;
         if (t < 256) hist[t] = 0;
         __syncthreads();
@@ -183,7 +185,7 @@ __global__ __launch_bounds__(kPsThreads) void k_probe_select_wide(const float *p
     if (none)
         tt = (METRIC == MQVS_METRIC_L2) ? __builtin_inff() : -__builtin_inff();
     else
-        tt = widen<METRIC>(okey_value<METRIC>(prefix), bq[q]);
+        tt = widen<METRIC>(okey_bound_value<METRIC>(prefix | 0xFFu), bq[q]);
     if (t == 0) thr[q] = tt;
     if (!cand) return;  // (the batch probe's maxima: threshold only)
     for_each_f4<kPsThreads>(row, P, [&](int64_t i, float raw) {
@@ -239,12 +241,14 @@ __global__ __launch_bounds__(SEL_THREADS) void k_survivors(ScanParams p, const f
         n = p.cand_cap;
     }
     const Cand *c = p.cand + (int64_t)q * p.cand_cap;
-    const uint32_t th = block_radix_select_mlp([&](int64_t i) { return okey<METRIC>(c[i].raw); }, n, k, hist, sh);
+    // (a bound on the k-th key is enough: 3 radix passes, block_radix_select)
+    const uint32_t th =
+        block_radix_select_mlp<SEL_THREADS, 3>([&](int64_t i) { return okey<METRIC>(c[i].raw); }, n, k, hist, sh);
     float t;
     if (th == 0xFFFFFFFEu)
         t = (METRIC == MQVS_METRIC_L2) ? __builtin_inff() : -__builtin_inff();
     else
-        t = widen<METRIC>(okey_value<METRIC>(th), bq[q]);
+        t = widen<METRIC>(okey_bound_value<METRIC>(th), bq[q]);
     if (threadIdx.x == 0) s_cnt = 0;
     __syncthreads();
     uint32_t *out = surv + (int64_t)q * rs;

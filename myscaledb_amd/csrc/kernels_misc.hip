@@ -184,6 +184,44 @@ __device__ __forceinline__ float seq_sq_sum_lds_pipe(const float (&x)[J], float 
     return acc;
 }
 
+// The same sum from registers: the rounded products go through LDS once and
+// lane L < 8 loads elements [8 J L, 8 J (L + 1)) into its registers (2 J
+// 16-B reads, all issued up front); then eight phases of 8 J dependent adds,
+// phase L continuing the running sum of phase L - 1 (readlane broadcast) with
+// lane L's elements.  The add chain never waits on LDS (the walk above
+// re-reads LDS for every 4 elements); same order, same bits.
+template <int J>
+__device__ __forceinline__ float seq_sq_sum_lanes(const float (&x)[J], float *prod) {
+    constexpr int NL = 8, PL = 8 * J;  // lanes, elements per lane (64 J = NL PL)
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int u = 0; u < J; ++u) prod[lane + 64 * u] = x[u] * x[u];
+    __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the stores landed (one wave)
+    __builtin_amdgcn_wave_barrier();
+    const float4 *p4 = reinterpret_cast<const float4 *>(prod + (lane < NL ? lane : 0) * PL);
+    float v[PL];
+#pragma unroll
+    for (int j = 0; j < PL / 4; ++j) {
+        const float4 t = p4[j];
+        v[4 * j] = t.x;
+        v[4 * j + 1] = t.y;
+        v[4 * j + 2] = t.z;
+        v[4 * j + 3] = t.w;
+    }
+    // (every read issued before the first add: left to itself the compiler
+    // sinks the reads into phase 0, two at a time, each pair waited for)
+    __builtin_amdgcn_sched_barrier(0);
+    float acc = 0.0f;
+#pragma unroll
+    for (int L = 0; L < NL; ++L) {
+#pragma unroll
+        for (int i = 0; i < PL; ++i) acc = acc + v[i];
+        acc = __builtin_bit_cast(float, __builtin_amdgcn_readlane(__builtin_bit_cast(int, acc), L));
+    }
+    __builtin_amdgcn_wave_barrier();  // (the next step rewrites prod)
+    return acc;
+}
+
 // J > 0: d <= 64 J, the query in registers.
 // phase 0: everything.  Cosine searches whose first consumers need only
 // variant 0 split the work: phase 1 writes variant 0 (and |q|^2 = 0); phase 2,
@@ -191,16 +229,20 @@ __device__ __forceinline__ float seq_sq_sum_lds_pipe(const float (&x)[J], float 
 // list scan), walks the rest of the chain -- it compares against the stored
 // variant 0 but does not rewrite it -- and writes mu, lambda and the status.
 // SUMV: 0 = readlane walk (seq_sq_sum), 1 = LDS broadcast walk
-// (seq_sq_sum_lds; the launcher's: 39.0 -> 35.5 us at nq 1, 72.5 -> 65.7 us
-// at nq 1000 for d = 768, bit-identical tables, tools/qprep_sum_ab.hip,
-// profiles/r05/qprep_sum_ab.jsonl)
-template <int J, int SUMV = 0>
+// (seq_sq_sum_lds: 39.0 -> 35.5 us at nq 1, 72.5 -> 65.7 us at nq 1000 for
+// d = 768), 2 = that walk software-pipelined (slower: 45 us), 3 = register
+// phases (seq_sq_sum_lanes, the launcher's); bit-identical tables,
+// tools/qprep_sum_ab.hip, profiles/r05/qprep_sum_ab.jsonl
+constexpr int kLaneSigMax = 32;  // variants whose per-lane signatures fit LDS (33 x 256 B)
+template <int J, int SUMV = 0, bool LANESIG = false>
 __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d, int metric, int blas, float *qvars,
                                                    int maxv, float *qnorms, int *qmu, int *qlam, int *status,
                                                    int phase) {
     __shared__ __attribute__((aligned(16))) float prod[SUMV ? 64 * J : 1];
     auto sqsum = [&](const float(&xx)[J]) -> float {
-        if constexpr (SUMV == 2)
+        if constexpr (SUMV == 3)
+            return seq_sq_sum_lanes<J>(xx, prod);
+        else if constexpr (SUMV == 2)
             return seq_sq_sum_lds_pipe<J>(xx, prod);
         else if constexpr (SUMV == 1)
             return seq_sq_sum_lds<J>(xx, prod);
@@ -236,9 +278,13 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
     const float eps = 1.1920929e-07f;
     // variants 0..maxv-1 are stored; normalisation maxv is only compared, so a
     // fixed point reached at the last stored variant is still detected.  A
-    // repeat is found by a 64-bit signature of each variant (wave-reduced in
-    // registers); only a signature match is confirmed element by element.
-    extern __shared__ uint64_t sig[];  // maxv + 1 signatures
+    // repeat is found by a signature of each variant; only a signature match
+    // is confirmed element by element.  LANESIG (maxv <= kLaneSigMax): a 32-bit
+    // hash per lane, kept per variant in LDS and matched with one vote (no
+    // cross-lane reduction: 0.3 -> ~0.05 us per normalisation); else one 64-bit
+    // hash per variant, wave-reduced.
+    extern __shared__ uint64_t sig[];  // LANESIG: [maxv + 1][64] uint32; else maxv + 1 uint64
+    uint32_t *lsig = reinterpret_cast<uint32_t *>(sig);
     for (int v = 0; v <= maxv; ++v) {
         const float sum = sqsum(x);
         if (!(sum < eps)) {
@@ -248,25 +294,49 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
         }
         if (v < maxv && (phase != 2 || v > 0)) {
             float *cur = v0 + (int64_t)v * qs;
+            if (64 * J == qs) {
+                // every slot in range: one address, immediate offsets (the
+                // per-slot predicate below makes the compiler rebuild the
+                // address before each store and wait for the previous store:
+                // ~1 us per normalisation)
 #pragma unroll
-            for (int u = 0; u < J; ++u)
-                if (lane + 64 * u < qs) cur[lane + 64 * u] = x[u];  // (x = 0 past d)
+                for (int u = 0; u < J; ++u) cur[lane + 64 * u] = x[u];
+            } else {
+#pragma unroll
+                for (int u = 0; u < J; ++u)
+                    if (lane + 64 * u < qs) cur[lane + 64 * u] = x[u];  // (x = 0 past d)
+            }
         }
         if (phase == 1) {
             if (lane == 0 && qnorms) qnorms[j] = 0.0f;
             return;
         }
         uint64_t h = 0;
+        uint32_t hl = 0x811C9DC5u;
+        if constexpr (LANESIG) {
 #pragma unroll
-        for (int u = 0; u < J; ++u) {
-            const uint64_t b = __builtin_bit_cast(uint32_t, x[u]);
-            h += (b + 0x9E3779B97F4A7C15ull * (uint64_t)(u + 1)) * (b | 1ull) ^ (b << 29);
+            for (int u = 0; u < J; ++u) {
+                const uint32_t b = __builtin_bit_cast(uint32_t, x[u]);
+                hl = ((hl << 5) | (hl >> 27)) ^ (b + 0x9E3779B9u * (uint32_t)(u + 1));
+            }
+            if (v < maxv) lsig[v * 64 + lane] = hl;
+            __builtin_amdgcn_wave_barrier();  // (one wave: its LDS ops complete in order)
+        } else {
+#pragma unroll
+            for (int u = 0; u < J; ++u) {
+                const uint64_t b = __builtin_bit_cast(uint32_t, x[u]);
+                h += (b + 0x9E3779B97F4A7C15ull * (uint64_t)(u + 1)) * (b | 1ull) ^ (b << 29);
+            }
+            for (int off = 32; off > 0; off >>= 1) h += __shfl_xor(h, off);
+            if (v < maxv && lane == 0) sig[v] = h;
+            __syncthreads();
         }
-        for (int off = 32; off > 0; off >>= 1) h += __shfl_xor(h, off);
-        if (v < maxv && lane == 0) sig[v] = h;
-        __syncthreads();
         for (int u = 0; u < v; ++u) {
-            if (sig[u] != h) continue;
+            if constexpr (LANESIG) {
+                if (!__all(lsig[u * 64 + lane] == hl)) continue;
+            } else if (sig[u] != h) {
+                continue;
+            }
             const float *o = v0 + (int64_t)u * qs;
             bool eq = true;
 #pragma unroll
@@ -384,10 +454,17 @@ void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, flo
                        float *qnorms, int *qmu, int *qlam, int *status, hipStream_t s, int phase) {
     if (metric != MQVS_METRIC_COSINE) maxv = 1;
     const size_t lds = (size_t)((d + 31) / 32 * 32 + 4) * sizeof(float);
-    const size_t sig = (size_t)(maxv + 1) * sizeof(uint64_t);
-#define MQVS_QP(J)                                                                                               \
-    hipLaunchKernelGGL((k_query_prep<J, 1>), dim3(nq), dim3(64), sig, s, q, nq, d, metric, blas ? 1 : 0, qvars, maxv, \
-                       qnorms, qmu, qlam, status, phase)
+    const bool lanesig = maxv <= kLaneSigMax;
+    const size_t sig = lanesig ? (size_t)(maxv + 1) * 64 * sizeof(uint32_t) : (size_t)(maxv + 1) * sizeof(uint64_t);
+#define MQVS_QP(J)                                                                                                   \
+    do {                                                                                                             \
+        if (lanesig)                                                                                                 \
+            hipLaunchKernelGGL((k_query_prep<J, 3, true>), dim3(nq), dim3(64), sig, s, q, nq, d, metric, blas ? 1 : 0, \
+                               qvars, maxv, qnorms, qmu, qlam, status, phase);                                       \
+        else                                                                                                         \
+            hipLaunchKernelGGL((k_query_prep<J, 3, false>), dim3(nq), dim3(64), sig, s, q, nq, d, metric,             \
+                               blas ? 1 : 0, qvars, maxv, qnorms, qmu, qlam, status, phase);                         \
+    } while (0)
     if (d <= 128)
         MQVS_QP(2);
     else if (d <= 256)

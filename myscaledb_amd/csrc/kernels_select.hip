@@ -355,15 +355,15 @@ __global__ __launch_bounds__(SEL_THREADS) void k_refine(const Cand *cin, const i
     float tf = 0.f;
     if (APPROX) {
         auto keyof = [&](int64_t i) { return okey<METRIC>(c[i].raw); };
-        const uint32_t th = block_radix_select(keyof, n, k, hist, sh);
+        const uint32_t th = block_radix_select<3>(keyof, n, k, hist, sh);  // (a bound: 3 passes)
         tf = thr[q];
         if (th != 0xFFFFFFFEu) {
-            const float w = widen<METRIC>(okey_value<METRIC>(th), bq[q]);
+            const float w = widen<METRIC>(okey_bound_value<METRIC>(th), bq[q]);
             tf = (METRIC == MQVS_METRIC_L2) ? fminf(tf, w) : fmaxf(tf, w);
         }
     } else {
         auto keyof = [&](int64_t i) { return key32<METRIC>(c[i].raw); };
-        const uint32_t th = block_radix_select(keyof, n, k, hist, sh);
+        const uint32_t th = block_radix_select<3>(keyof, n, k, hist, sh);
         tk = tau[q];
         if (th < tk) tk = th;
     }

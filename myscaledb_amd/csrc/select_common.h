@@ -74,12 +74,16 @@ __device__ inline void hist_pick(const uint32_t *hist, uint32_t kk, bool first, 
 
 // k-th smallest valid key (1-based rank k) among `count` values produced by
 // load(i); 0xFFFFFFFE when fewer than k values are valid.  Block-wide.
-template <typename KeyFn>
+// PASSES = 3 (thresholds only): the top 24 bits of the k-th key, the low byte
+// set -- an upper bound on the k-th key (every key <= it passes a "<= bound"
+// test, so a threshold built from it keeps every row the exact one keeps;
+// 2^-16 relative looser) without the fourth histogram pass.
+template <int PASSES = 4, typename KeyFn>
 __device__ inline uint32_t block_radix_select(KeyFn keyof, int64_t count, int k, uint32_t *hist,
                                        uint32_t *sh) {
     const int t = threadIdx.x;
     uint32_t prefix = 0, mask = 0, kk = (uint32_t)k;
-    for (int pass = 0; pass < 4; ++pass) {
+    for (int pass = 0; pass < PASSES; ++pass) {
         const int shift = 24 - 8 * pass;
         for (int i = t; i < 256; i += SEL_THREADS) hist[i] = 0;
         __syncthreads();
@@ -103,17 +107,17 @@ __device__ inline uint32_t block_radix_select(KeyFn keyof, int64_t count, int k,
         kk -= sh[2];
         __syncthreads();
     }
-    return prefix;
+    return PASSES == 4 ? prefix : prefix | (0xFFFFFFFFu >> (8 * PASSES));
 }
 
 // block_radix_select with the bucket search in parallel and 4 keys in
 // flight per thread (keyof(i) may read global memory).
-template <int NT = SEL_THREADS, typename KeyFn>
+template <int NT = SEL_THREADS, int PASSES = 4, typename KeyFn>
 __device__ inline uint32_t block_radix_select_mlp(KeyFn keyof, int64_t count, int k, uint32_t *hist, uint32_t *sh) {
     constexpr int SEL_THREADS = NT;  // block size of the caller
     const int t = threadIdx.x;
     uint32_t prefix = 0, mask = 0, kk = (uint32_t)k;
-    for (int pass = 0; pass < 4; ++pass) {
+    for (int pass = 0; pass < PASSES; ++pass) {
         const int shift = 24 - 8 * pass;
         for (int i = t; i < 256; i += SEL_THREADS) hist[i] = 0;
         __syncthreads();
@@ -144,7 +148,7 @@ __device__ inline uint32_t block_radix_select_mlp(KeyFn keyof, int64_t count, in
         kk -= sh[2];
         __syncthreads();
     }
-    return prefix;
+    return PASSES == 4 ? prefix : prefix | (0xFFFFFFFFu >> (8 * PASSES));
 }
 
 // The k smallest valid keys for small k (k <= kSelSmallK): each thread keeps
@@ -375,6 +379,16 @@ __device__ inline float okey_value(uint32_t k) {
     uint32_t u = (METRIC == MQVS_METRIC_L2) ? k : ~k;
     u = (u & 0x80000000u) ? (u & 0x7FFFFFFFu) : ~u;
     return __builtin_bit_cast(float, u);
+}
+
+// the value of an upper bound on a k-th key (block_radix_select<3>: its low
+// byte set): past the worst infinity the bound's bits decode to a NaN, which
+// would fail every test -- the k-th value was that infinity, so use it
+template <int METRIC>
+__device__ inline float okey_bound_value(uint32_t k) {
+    const float v = okey_value<METRIC>(k);
+    if (v == v) return v;
+    return METRIC == MQVS_METRIC_L2 ? __builtin_inff() : -__builtin_inff();
 }
 
 // threshold on the approximate value that keeps every row of the exact top-k
