@@ -665,8 +665,9 @@ __global__ __launch_bounds__(256) void k_chunk_active(const uint8_t *filter,
 // One workgroup of kScanThreads: thread t owns a contiguous run of chunks;
 // the run sums are scanned by waves, then over the wave totals.
 constexpr int kScanThreads = 1024;
-template <class Val, class Out>
+template <int NT = kScanThreads, class Val, class Out>
 __device__ void run_scan(int64_t nchunks, Val val, Out out, int64_t *sh, int64_t &grand) {
+    constexpr int kScanThreads = NT;  // block size of the caller
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const int64_t per = (nchunks + kScanThreads - 1) / kScanThreads;
     const int64_t b = t * per, e = b + per < nchunks ? b + per : nchunks;
@@ -703,35 +704,63 @@ __global__ __launch_bounds__(kScanThreads) void k_exclusive_ord(int *flag_ord, i
 // Gather list of a selective PREWHERE scan: the rows that pass the filter,
 // are non-empty and not deleted, chunk by chunk in row order, each chunk's
 // run padded with -1 to a multiple of `tile` entries.
-__global__ __launch_bounds__(256) void k_chunk_count(const uint8_t *filter, const uint8_t *nonempty,
-                                                      const uint8_t *exists, int64_t n, int64_t chunk_rows,
-                                                      int64_t nchunks, int *count) {
-    const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
-    const int lane = threadIdx.x & 63;
-    if (c >= nchunks) return;
-    const int64_t r0 = c * chunk_rows;
-    const int64_t r1 = r0 + chunk_rows < n ? r0 + chunk_rows : n;
-    int cnt = 0;
-    for (int64_t w = (r0 >> 5) + lane; w < ((r1 + 31) >> 5); w += 64)
-        cnt += __popc(sel_word(filter, nonempty, exists, n, w) & range_mask(w, r0, r1));
-    for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
-    if (lane == 0) count[c] = cnt;
-}
-
-// offsets[c] = sum of padded counts before c; totals[0] = padded list
-// length, totals[1] = selected rows
-__global__ __launch_bounds__(kScanThreads) void k_pad_scan(const int *count, int64_t nchunks, int tile,
-                                                            int64_t *offsets, int64_t *totals) {
+// k_chunk_count: per chunk its selected rows (one wave per chunk); the last
+// workgroup to finish (an agent-scope ticket, zeroed with the search's status
+// words) then scans the counts: offsets[c] = sum of padded counts before c,
+// totals[0] = padded list length, totals[1] = selected rows.  host_totals
+// (pinned host memory, may be null): the same two values, [0] then [1] behind
+// a system-scope fence, so the host can act on them as soon as [1] changes
+// from its -1 sentinel instead of draining the stream for a copy.  (One
+// launch: the separate single-workgroup scan cost ~8 us plus a launch gap.)
+__global__ __launch_bounds__(kScanThreads) void k_chunk_count(const uint8_t *filter, const uint8_t *nonempty,
+                                                               const uint8_t *exists, int64_t n, int64_t chunk_rows,
+                                                               int64_t nchunks, int *count, int tile,
+                                                               int64_t *offsets, int64_t *totals,
+                                                               int64_t *host_totals, int *ticket) {
     __shared__ int64_t sh[kScanThreads / 64];
+    __shared__ int s_last;
+    const int64_t c = (int64_t)blockIdx.x * (kScanThreads / 64) + (threadIdx.x >> 6);
+    const int lane = threadIdx.x & 63;
+    if (c < nchunks) {
+        const int64_t r0 = c * chunk_rows;
+        const int64_t r1 = r0 + chunk_rows < n ? r0 + chunk_rows : n;
+        int cnt = 0;
+        for (int64_t w = (r0 >> 5) + lane; w < ((r1 + 31) >> 5); w += 64)
+            cnt += __popc(sel_word(filter, nonempty, exists, n, w) & range_mask(w, r0, r1));
+        for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
+        // (write-through: the count reaches the device-coherent level
+        // without an agent-scope release, which writes back the whole L2 --
+        // one per workgroup cost ~50 us at 1526 workgroups)
+        if (lane == 0) __hip_atomic_store(count + c, cnt, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // last workgroup in: every count stored and drained before the ticket
+    __builtin_amdgcn_s_waitcnt(0x0F70);  // vmcnt(0)
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const int prev = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        s_last = prev == (int)gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!s_last) return;
+    // (coherent loads of the other workgroups' counts, no acquire fence)
+    auto cnt_of = [&](int64_t i) -> int64_t {
+        return (int64_t)__hip_atomic_load(count + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    };
     int64_t padded_total = 0, selected = 0;
     run_scan(
-        nchunks, [&](int64_t i) -> int64_t { return (int64_t)(count[i] + tile - 1) / tile * tile; },
+        nchunks, [&](int64_t i) -> int64_t { return (cnt_of(i) + tile - 1) / tile * tile; },
         [&](int64_t i, int64_t before, int64_t) { offsets[i] = before; }, sh, padded_total);
-    run_scan(
-        nchunks, [&](int64_t i) -> int64_t { return count[i]; }, [&](int64_t, int64_t, int64_t) {}, sh, selected);
+    run_scan(nchunks, cnt_of, [&](int64_t, int64_t, int64_t) {}, sh, selected);
     if (threadIdx.x == 0) {
         totals[0] = padded_total;
         totals[1] = selected;
+        *ticket = 0;
+        if (host_totals) {
+            *reinterpret_cast<volatile int64_t *>(host_totals) = padded_total;
+            __threadfence_system();
+            *reinterpret_cast<volatile int64_t *>(host_totals + 1) = selected;
+            __threadfence_system();
+        }
     }
 }
 
@@ -740,7 +769,7 @@ __global__ __launch_bounds__(kScanThreads) void k_pad_scan(const int *count, int
 __global__ __launch_bounds__(256) void k_compact_rows(const uint8_t *filter, const uint8_t *nonempty,
                                                        const uint8_t *exists, int64_t n, int64_t chunk_rows,
                                                        int64_t nchunks, const int *count, const int64_t *offsets,
-                                                       int tile, int32_t *list) {
+                                                       int tile, int32_t *list, int64_t list_end) {
     const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (c >= nchunks) return;
@@ -775,25 +804,29 @@ __global__ __launch_bounds__(256) void k_compact_rows(const uint8_t *filter, con
     const int cnt = count[c];
     const int padded = (cnt + tile - 1) / tile * tile;
     for (int i = cnt + lane; i < padded; i += 64) out[i] = -1;
+    // the last chunk also pads the list's end up to list_end (whole tiles of
+    // the scan; -1 entries)
+    if (c == nchunks - 1)
+        for (int64_t i = offsets[c] + padded + lane; i < list_end; i += 64) list[i] = -1;
 }
 
 void launch_gather_count(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists, int64_t n,
                          int64_t chunk_rows, int tile, int *count, int64_t *offsets, int64_t *totals,
-                         hipStream_t s) {
+                         int64_t *host_totals, int *ticket, hipStream_t s) {
     const int64_t nchunks = (n + chunk_rows - 1) / chunk_rows;
     if (nchunks < 1) return;
-    hipLaunchKernelGGL(k_chunk_count, dim3((unsigned)((nchunks + 3) / 4)), dim3(256), 0, s, filter, nonempty, exists,
-                       n, chunk_rows, nchunks, count);
-    hipLaunchKernelGGL(k_pad_scan, dim3(1), dim3(kScanThreads), 0, s, count, nchunks, tile, offsets, totals);
+    constexpr int wpb = kScanThreads / 64;  // chunks (waves) per workgroup
+    hipLaunchKernelGGL(k_chunk_count, dim3((unsigned)((nchunks + wpb - 1) / wpb)), dim3(kScanThreads), 0, s, filter,
+                       nonempty, exists, n, chunk_rows, nchunks, count, tile, offsets, totals, host_totals, ticket);
 }
 
 void launch_gather_list(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists, int64_t n,
                         int64_t chunk_rows, int tile, const int *count, const int64_t *offsets, int32_t *list,
-                        hipStream_t s) {
+                        int64_t list_end, hipStream_t s) {
     const int64_t nchunks = (n + chunk_rows - 1) / chunk_rows;
     if (nchunks < 1) return;
     hipLaunchKernelGGL(k_compact_rows, dim3((unsigned)((nchunks + 3) / 4)), dim3(256), 0, s, filter, nonempty, exists,
-                       n, chunk_rows, nchunks, count, offsets, tile, list);
+                       n, chunk_rows, nchunks, count, offsets, tile, list, list_end);
 }
 
 void launch_chunk_ordinals(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists,

@@ -13,6 +13,7 @@
 
 #include <algorithm>
 #include <atomic>
+#include <chrono>
 #include <condition_variable>
 #include <cstring>
 #include <map>
@@ -778,16 +779,24 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     // its end is padded (at 1 % selectivity per-chunk padding made the list
     // 3x the selected rows: 82 rows per 8192-row chunk, padded to 256)
     const int gtile = cos ? (int)kSmallRows : 1;
+    // one zeroed block for the status words: [overflow 4][status 4][count nq]
+    // [gather-count ticket 1]
+    int *fl = (int *)ws.get(ws.flags, sizeof(int) * (9 + (size_t)nq));
+    launch_fill2((uint32_t *)fl, 9 + (int64_t)nq, 0u, nullptr, 0, 0u, s);
     if (dfilter && gather_mode != 0 && n > 0) {
         const int64_t nch = (n + seg->granule - 1) / seg->granule;
         gcount = (int *)ws.get(ws.gcount, sizeof(int) * nch);
         goff = (int64_t *)ws.get(ws.goff, sizeof(int64_t) * (nch + 2));
+        // the totals also land in pinned host memory (k_chunk_count), read once
+        // the query prep, chunk ordinals and bf16 query planes are queued: the
+        // host waits for this kernel only, not for a drained stream
+        auto *htot = reinterpret_cast<int64_t *>(ws.host_flags + 8);
+        htot[0] = -1;
+        htot[1] = -1;
+        std::atomic_thread_fence(std::memory_order_seq_cst);
         launch_gather_count(dfilter, seg->nonempty_bits, dexists, n, seg->granule, gtile, gcount, goff, goff + nch,
-                            s);
+                            htot, fl + 8 + nq, s);
         MQVS_HIP(hipGetLastError());
-        // read back after the query prep and chunk ordinals are queued (the
-        // host round trip overlaps them)
-        MQVS_HIP(hipMemcpyAsync(ws.host_flags + 8, goff + nch, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
         selected = 0;
     }
     const bool mfma = fnq >= kBlasThreshold;
@@ -799,9 +808,6 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     const int64_t qstride = round_up(d, 32);
     float *qvars = nullptr, *qnorms = nullptr;
     int *qmu = nullptr, *qlam = nullptr, *status = nullptr;
-    // one zeroed block for the status words: [overflow 4][status 4][count nq]
-    int *fl = (int *)ws.get(ws.flags, sizeof(int) * (8 + (size_t)nq));
-    launch_fill2((uint32_t *)fl, 8 + (int64_t)nq, 0u, nullptr, 0, 0u, s);
     // The query-variant table starts at kMaxVariants per query without a host
     // round trip; a chain that does not repeat within it on a part of more
     // chunk ordinals (rare: small-integer data) is caught from the status word
@@ -823,13 +829,6 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     } else {
         chunk_ord = seg->chunk_ord;
     }
-    if (selected >= 0) {
-        MQVS_HIP(hipStreamSynchronize(s));
-        const int64_t *htot = reinterpret_cast<const int64_t *>(ws.host_flags + 8);
-        gpadded = round_up(htot[0], kSmallRows);
-        selected = htot[1];
-    }
-
     // ---- kernel choice
     // faiss's formula branch is set by nq (kBlasThreshold); the bf16
     // pre-filter serves both branches (its exact re-rank uses the branch's
@@ -840,62 +839,14 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     // below ~30% (tools/sweep.py --sels, profiles/r01)
     // (the bf16 plane streams half the bytes of the fp32 rows, so it serves
     // every batch size)
-    bool bf16 = bf16_ok;
-    bool gather = false;
-    if (selected >= 0) {
-        if (gather_mode == 2)
-            gather = bf16 || !mfma;
-        else if (bf16_ok && 10 * selected <= 6 * n)
-            gather = bf16 = true;
-        else if (!bf16 && !mfma && 10 * selected <= 3 * n)
-            gather = true;
-    }
+    // (the gather decision below never changes bf16 from bf16_ok, so the kind
+    // and the bf16 query planes are set before the selected count is known)
+    const bool bf16 = bf16_ok;
     const int kind = bf16 ? kScanBf16 : !mfma ? kScanSmall : kScanMfma32;
 
-    // ---- gather list of the selected rows
-    const int32_t *row_list = nullptr;
-    int64_t scan_n = n;  // scan positions: rows, or gather-list entries
-    if (gather) {
-        int32_t *list = (int32_t *)ws.get(ws.glist, sizeof(int32_t) * std::max<int64_t>(gpadded, 1));
-        launch_gather_list(dfilter, seg->nonempty_bits, dexists, n, seg->granule, gtile, gcount, goff, list, s);
-        MQVS_HIP(hipGetLastError());
-        if (gpadded > selected && gtile == 1)  // the dense list's tail: -1 entries up to a whole tile
-            launch_fill2((uint32_t *)(list + selected), gpadded - selected, 0xFFFFFFFFu, nullptr, 0, 0u, s);
-        row_list = list;
-        scan_n = gpadded;
-        st.gather = 1;
-    }
-    const bool aligned = !row_list && (cos || chunk_ord != nullptr);
-    const int64_t tile_rows = kind == kScanBf16 ? kBfRows : !mfma ? kSmallRows : kMfmaRows;
-
-    // ---- candidate capacity per query (a fixed budget spread over the
-    // batch) and probe size: expected candidates ~ k*n/P; aim at cap/3
+    // ---- candidate capacity per query (a fixed budget spread over the batch)
     int cap = (int)std::min<int64_t>(kCandMax, kCandBudget / std::max(nq, 1));
     cap = std::max(cap, k > kSortCap ? large_k_cap(k) : kSortCap) / 256 * 256;
-    // (more candidates = more appends from the scan; 16k keeps them cheap)
-    const SegTune tune = seg_tune(nq);
-    const int64_t target_cands = std::min<int64_t>(cap / 3, std::max<int64_t>(tune.target, 2 * (int64_t)k));
-    uint4 *large = k > kSortCap ? (uint4 *)ws.get(ws.large, sizeof(uint4) * 2 * kLargeCap * (size_t)nq) : nullptr;
-    int64_t P = scan_n;
-    // (small k over a part much larger than k -- e.g. the index build's
-    // top-1 k-means assignment against 10^4 centroids -- also takes a short
-    // probe: a dense probe of every row would dominate the search)
-    if (scan_n > 32768 || (k <= 16 && scan_n > 16 * tile_rows)) {
-        P = (int64_t)(((double)k * (double)scan_n) / target_cands) + 1;
-        // (a shorter probe is cheaper but its looser threshold sends more
-        // waves of the first segments down the append path: measured net
-        // loss at nq = 1000 with a 64 MB cap on the probe matrix)
-        P = std::max<int64_t>(P, 8 * (int64_t)k);
-        // A gathered scan's appends take the per-row path (list lookup,
-        // bitmap tests, norms), so a loose first threshold is costly there:
-        // at 1 % of 50M rows a 1024-position probe left ~10 % of the first
-        // segment's rows passing (110 us for 66k positions, then a 45 us
-        // refinement).  A probe of scan_n / 16 positions (<= 16384) costs
-        // about the same launch and cuts the first segment's appends ~16x.
-        if (row_list) P = std::max<int64_t>(P, std::min<int64_t>(scan_n / 16, 16384));
-        P = round_up(P, aligned ? seg->granule : tile_rows);
-        if (P > scan_n) P = scan_n;
-    }
 
     ScanParams p{};
     p.rows = seg->rows;
@@ -916,7 +867,6 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     p.filter = dfilter;
     p.exists = dexists;
     p.nonempty = seg->nonempty_bits;
-    p.row_list = row_list;
     p.num_qblocks = (nq + kMfmaQ - 1) / kMfmaQ;
     p.blas_nq = fnq;
     uint32_t *tau = (uint32_t *)ws.get(ws.tau, sizeof(uint32_t) * nq);
@@ -966,6 +916,83 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
             }
         }
         MQVS_HIP(hipGetLastError());
+    }
+
+    // ---- the selected count (k_chunk_count's pinned copy; past ~200 us of
+    // spinning -- earlier work queued on the caller's stream -- a stream sync)
+    if (selected >= 0) {
+        volatile int64_t *htot = reinterpret_cast<volatile int64_t *>(ws.host_flags + 8);
+        const auto t0 = std::chrono::steady_clock::now();
+        while (htot[1] < 0) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
+                MQVS_HIP(hipStreamSynchronize(s));
+                break;
+            }
+        }
+        std::atomic_thread_fence(std::memory_order_acquire);
+        if (htot[1] < 0) {
+            // (the pinned copy never showed: read the device totals)
+            const int64_t nch = (n + seg->granule - 1) / seg->granule;
+            int64_t dt[2];
+            MQVS_HIP(hipMemcpy(dt, goff + nch, sizeof(dt), hipMemcpyDeviceToHost));
+            htot[0] = dt[0];
+            htot[1] = dt[1];
+        }
+        gpadded = round_up(htot[0], kSmallRows);
+        selected = htot[1];
+    }
+    bool gather = false;
+    if (selected >= 0) {
+        if (gather_mode == 2)
+            gather = bf16 || !mfma;
+        else if (bf16_ok && 10 * selected <= 6 * n)
+            gather = true;
+        else if (!bf16 && !mfma && 10 * selected <= 3 * n)
+            gather = true;
+    }
+
+    // ---- gather list of the selected rows
+    const int32_t *row_list = nullptr;
+    int64_t scan_n = n;  // scan positions: rows, or gather-list entries
+    if (gather) {
+        int32_t *list = (int32_t *)ws.get(ws.glist, sizeof(int32_t) * std::max<int64_t>(gpadded, 1));
+        // (the list's tail up to gpadded: -1 entries, written by the last chunk)
+        launch_gather_list(dfilter, seg->nonempty_bits, dexists, n, seg->granule, gtile, gcount, goff, list, gpadded,
+                           s);
+        MQVS_HIP(hipGetLastError());
+        row_list = list;
+        scan_n = gpadded;
+        st.gather = 1;
+    }
+    const bool aligned = !row_list && (cos || chunk_ord != nullptr);
+    const int64_t tile_rows = kind == kScanBf16 ? kBfRows : !mfma ? kSmallRows : kMfmaRows;
+
+    p.row_list = row_list;
+
+    // ---- probe size: expected candidates ~ k*n/P; aim at cap/3
+    // (more candidates = more appends from the scan; 16k keeps them cheap)
+    const SegTune tune = seg_tune(nq);
+    const int64_t target_cands = std::min<int64_t>(cap / 3, std::max<int64_t>(tune.target, 2 * (int64_t)k));
+    uint4 *large = k > kSortCap ? (uint4 *)ws.get(ws.large, sizeof(uint4) * 2 * kLargeCap * (size_t)nq) : nullptr;
+    int64_t P = scan_n;
+    // (small k over a part much larger than k -- e.g. the index build's
+    // top-1 k-means assignment against 10^4 centroids -- also takes a short
+    // probe: a dense probe of every row would dominate the search)
+    if (scan_n > 32768 || (k <= 16 && scan_n > 16 * tile_rows)) {
+        P = (int64_t)(((double)k * (double)scan_n) / target_cands) + 1;
+        // (a shorter probe is cheaper but its looser threshold sends more
+        // waves of the first segments down the append path: measured net
+        // loss at nq = 1000 with a 64 MB cap on the probe matrix)
+        P = std::max<int64_t>(P, 8 * (int64_t)k);
+        // A gathered scan's appends take the per-row path (list lookup,
+        // bitmap tests, norms), so a loose first threshold is costly there:
+        // at 1 % of 50M rows a 1024-position probe left ~10 % of the first
+        // segment's rows passing (110 us for 66k positions, then a 45 us
+        // refinement).  A probe of scan_n / 16 positions (<= 16384) costs
+        // about the same launch and cuts the first segment's appends ~16x.
+        if (row_list) P = std::max<int64_t>(P, std::min<int64_t>(scan_n / 16, 16384));
+        P = round_up(P, aligned ? seg->granule : tile_rows);
+        if (P > scan_n) P = scan_n;
     }
 
     const Range pr = make_range(0, P, tile_rows, seg->granule, aligned);

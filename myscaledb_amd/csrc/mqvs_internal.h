@@ -249,9 +249,9 @@ __device__ inline bool row_valid(const ScanParams &p, int64_t r) {
 void launch_scan_small(const ScanParams &p, int metric, bool probe, hipStream_t s);
 void launch_gather_count(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists, int64_t n,
                          int64_t chunk_rows, int tile, int *count, int64_t *offsets, int64_t *totals,
-                         hipStream_t s);
+                         int64_t *host_totals, int *ticket, hipStream_t s);
 void launch_gather_list(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists, int64_t n,
-                        int64_t chunk_rows, int tile, const int *count, const int64_t *offsets, int32_t *list,
+                        int64_t chunk_rows, int tile, const int *count, const int64_t *offsets, int32_t *list, int64_t list_end,
                         hipStream_t s);
 void launch_rerank_ids(const ScanParams &p, int metric, const int64_t *cand, int ncand, int k,
                        int64_t id_offset, int64_t *out_ids, float *out_dist, uint4 *scratch, hipStream_t s);
