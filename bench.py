@@ -32,8 +32,8 @@ FP32_MFMA_PEAK_TFLOPS = 157.3   # MI355X_MICROARCH.md, f32 MFMA (= VALU) dense p
 BF16_MFMA_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md, bf16 MFMA dense peak (no sparsity)
 HBM_PEAK_GBS = 8000.0           # MI355X_MICROARCH.md, HBM3E spec peak
 ROOT = os.path.dirname(os.path.abspath(__file__))
-PMC_DEFAULT = "profiles/r04/pmc_traffic.json"
-PMC_NQ1_DEFAULT = "profiles/r04/pmc_nq1.json"
+PMC_DEFAULT = "profiles/r05/pmc_traffic.json"
+PMC_NQ1_DEFAULT = "profiles/r05/pmc_nq1.json"
 BLAS_RISK_DEFAULT = "profiles/r03/blas_order_risk.json"
 
 
@@ -266,7 +266,7 @@ def cpu_baseline(O, args):
     }
 
 
-INDEX_PMC_DEFAULT = os.path.join(ROOT, "profiles", "r04", "index_pmc.json")
+INDEX_PMC_DEFAULT = os.path.join(ROOT, "profiles", "r05", "index_pmc.json")
 
 
 def index_points(mq, seg, mode, settings, args):
