@@ -806,7 +806,10 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     const bool dev = flags & MQVS_F_DEVICE_PTRS;
     const int d = seg->d;
     const bool cos = ix->metric == MQVS_METRIC_COSINE;
-    MQVS_HIP(hipEventRecord(ws.ev[0], s));
+    // per-stage timing events only when asked (MQVS_F_TIMING / mqvs_set_timing:
+    // ev[0..4]); ev[5] ends every search (the workspace trim waits on it)
+    const bool tev = timing_on(flags);
+    if (tev) MQVS_HIP(hipEventRecord(ws.ev[0], s));
 
     const float *dq = queries;
     const uint8_t *dfilter = filter, *dexists = exists;
@@ -849,7 +852,7 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     int *qmu = (int *)ws.qmu.get(sizeof(int) * nq);
     int *qlam = (int *)ws.qlam.get(sizeof(int) * nq);
     int *status = (int *)ws.status.get(sizeof(int) * 4);
-    MQVS_HIP(hipMemsetAsync(status, 0, sizeof(int) * 4, s));
+    launch_fill2(reinterpret_cast<uint32_t *>(status), 4, 0u, nullptr, 0, 0u, s);
     // Cosine: only variant 0 is needed before the exact re-rank (coarse step,
     // list scan), so the rest of the chain -- a sequential fp32 sum per
     // normalisation, up to kMaxVariants of them: 60-130 us at nq 1000 -- runs
@@ -922,10 +925,13 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
         cp.tile_rows = 256;
         cp.tiles = (cs->n + 255) / 256;
         cp.tiles_per_chunk = 0;
-        const int64_t gld = rup(16 * cp.tiles, 4);
+        // groups of 8 centroids (round 5; 16 before): the pick scores half the
+        // centroids per group it takes
+        const int grp = tune_int("MQVS_IVF_GRP", 8) == 16 ? 16 : 8;
+        const int64_t gld = rup((256 / grp) * cp.tiles, 4);
         cp.p4_gmax = (float *)ws.gmax.get(sizeof(float) * (size_t)nq * gld);
         cp.p4_gld = gld;
-        if (launch_scan_p4_groups(cp, ix->coarse_metric, s)) {
+        if (launch_scan_p4_groups(cp, ix->coarse_metric, grp, s)) {
             MQVS_HIP(hipGetLastError());
             // each query's bound on |bf16 group value - exact| (the direct
             // formula's rounding terms: the larger of the two)
@@ -934,8 +940,9 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
             bp.blas_nq = 1;
             launch_query_bound(bp, ix->coarse_metric, cs->ynorm_max, crec, cs->ynorm_max + 4, cbq, s);
             MQVS_HIP(hipGetLastError());
-            launch_coarse_pick(cp.p4_gmax, gld, 16 * cp.tiles, nprobe + 2, nprobe, ix->coarse_metric, qvars,
-                               (int64_t)maxv * qstride, cs->rows, cs->norms, cs->n, d, cbq, qnorms, nq, probes, s);
+            launch_coarse_pick(cp.p4_gmax, gld, (256 / grp) * cp.tiles, nprobe + 2, nprobe, ix->coarse_metric, qvars,
+                               (int64_t)maxv * qstride, cs->rows, cs->norms, cs->n, d, cbq, qnorms, grp == 8 ? 3 : 4,
+                               nq, probes, s);
             MQVS_HIP(hipGetLastError());
             picked = true;
         }
@@ -950,7 +957,7 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
                   ix->dpad, ix->metric, qhi, qnorms, nq, cprobes, (int)ix->cnl, nullptr, nullptr, nprobe, probes, 0,
                   nullptr, nullptr, s, true);
     }
-    MQVS_HIP(hipEventRecord(ws.ev[1], s));
+    if (tev) MQVS_HIP(hipEventRecord(ws.ev[1], s));
     if (split && late_fork) fork_chain();
 
     // ---- fine: the probed lists
@@ -958,12 +965,13 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     if (first_stage) {
         list_pass(ws.fine, ix->plane, ix->perm, ix->pnorm, ix->list_off, ix->nlist, ix->npos, ix->max_list, ix->dpad,
                   ix->metric, qhi, qnorms, nq, probes, nprobe, dfilter, dexists, R, dids, seg->row_offset, ddist,
-                  ws.ev, s);
+                  tev ? ws.ev : nullptr, s);
         MQVS_HIP(hipEventRecord(ws.ev[5], s));
     } else {
         int64_t *crow = (int64_t *)ws.rows.get(sizeof(int64_t) * (size_t)nq * R);
         list_pass(ws.fine, ix->plane, ix->perm, ix->pnorm, ix->list_off, ix->nlist, ix->npos, ix->max_list, ix->dpad,
-                  ix->metric, qhi, qnorms, nq, probes, nprobe, dfilter, dexists, R, crow, 0, nullptr, ws.ev, s);
+                  ix->metric, qhi, qnorms, nq, probes, nprobe, dfilter, dexists, R, crow, 0, nullptr,
+                  tev ? ws.ev : nullptr, s);
         // ---- exact re-rank (needs the whole variant chain)
         if (split) {
             MQVS_HIP(hipStreamWaitEvent(s, ws.join, 0));
@@ -1015,8 +1023,8 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     }
     int64_t *hs = ws.host;
     int *hst = reinterpret_cast<int *>(ws.host + 4);
-    MQVS_HIP(hipMemcpyAsync(hs, dstats, sizeof(int64_t) * 4, hipMemcpyDeviceToHost, s));
-    MQVS_HIP(hipMemcpyAsync(hst, status, sizeof(int), hipMemcpyDeviceToHost, s));
+    launch_words_to_host(dstats, 4, status, 1, hs, hst, s);
+    MQVS_HIP(hipGetLastError());
     MQVS_HIP(hipStreamSynchronize(s));
     const int hstatus = *hst;
     if (hstatus && !first_stage && ords > maxv) {
@@ -1040,8 +1048,10 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     st.plane_bytes = hs[2];
     st.pairs = hs[3];
     float t[5] = {0, 0, 0, 0, 0}, tot = 0;
-    for (int i = 0; i < 5; ++i) MQVS_HIP(hipEventElapsedTime(&t[i], ws.ev[i], ws.ev[i + 1]));
-    MQVS_HIP(hipEventElapsedTime(&tot, ws.ev[0], ws.ev[5]));
+    if (tev) {
+        for (int i = 0; i < 5; ++i) MQVS_HIP(hipEventElapsedTime(&t[i], ws.ev[i], ws.ev[i + 1]));
+        MQVS_HIP(hipEventElapsedTime(&tot, ws.ev[0], ws.ev[5]));
+    }
     st.coarse_ms = t[0];
     st.plan_ms = t[1];
     st.scan_ms = t[2];

@@ -888,7 +888,9 @@ void launch_iota_probes(int64_t *probes, int nq, int np, hipStream_t s) {
 }
 
 void launch_ivf_plan(const IvfParams &p, hipStream_t s) {
-    MQVS_HIP(hipMemsetAsync(p.lcount, 0, sizeof(int) * p.nlist, s));  // (lfill: zeroed by the list pass)
+    // (lfill: zeroed by the list pass; a fill kernel, not hipMemsetAsync: the
+    // runtime's fill took two launches)
+    launch_fill2(reinterpret_cast<uint32_t *>(p.lcount), p.nlist, 0u, nullptr, 0, 0u, s);
     const int64_t E = (int64_t)p.nq * p.nprobe;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((std::max(E, (int64_t)p.nq) + 255) / 256, 2048));
     hipLaunchKernelGGL(k_plan_count, dim3(grid), dim3(256), 0, s, p);
@@ -1016,7 +1018,8 @@ void launch_centroid_mean(const float *rows, int d, const int32_t *order, const 
 
 // ---------------------------------------------------------------------------
 // The coarse step's pick (index.hip): per query, from the batch probe's best
-// approximate value of every 16-centroid group (kernels_p4.hip, GRP 16), the
+// approximate value of every group of 2^gs_log2 centroids (kernels_p4.hip,
+// GRP 16 or 8), the
 // exact fp32 value of each centroid of a few groups and the nprobe best.
 // The group maxima are bf16 values within bq (the query's bound on |approx -
 // exact|, k_query_bound) of the exact ones.
@@ -1051,7 +1054,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
                                                              int Tcap, int nprobe, const float *q, int64_t qld,
                                                              const float *cent, const float *cnorm, int64_t ncent,
                                                              int d, const float *bq, const float *qnorms,
-                                                             int64_t *probes) {
+                                                             int gs_log2, int64_t *probes) {
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh[4];
     __shared__ int s_grp[kCoarsePickMaxT];
@@ -1063,7 +1066,8 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
     extern __shared__ uint4 dyn[];
     uint4 *recs = dyn;
     int NR = 1;
-    while (NR < 16 * Tcap) NR <<= 1;
+    const int GS = 1 << gs_log2;  // centroids per group
+    while (NR < GS * Tcap) NR <<= 1;
     uint32_t *keys = reinterpret_cast<uint32_t *>(dyn + NR);
     const int qi = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const float *row = gmax + (int64_t)qi * gld;
@@ -1110,7 +1114,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
 #pragma unroll
             for (int u = 0; u < kPickU; ++u) {
                 const int c = c0 + u;
-                r[u] = c < ce ? (int64_t)s_grp[c >> 4] * 16 + (c & 15) : ncent;
+                r[u] = c < ce ? ((int64_t)s_grp[c >> gs_log2] << gs_log2) + (c & (GS - 1)) : ncent;
                 if (r[u] >= ncent) r[u] = -1;
                 dot[u] = 0.f;
             }
@@ -1183,12 +1187,12 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
         tpair = th == 0xFFFFFFFEu ? ~0ull : ((uint64_t)th << 32) | 0xFFFFFFFFull;  // (every tie is in)
     }
     const int ng0 = min(s_ng, Tcap);
-    score(0, 16 * ng0);
+    score(0, GS * ng0);
     int ng = ng0;
     // 2. extras (needs the bound and a full core; fewer than T valid groups:
     // every group is in the core already)
     if (bq && tpair != ~0ull && s_ng < Tcap) {
-        const int M0 = 16 * ng0;
+        const int M0 = GS * ng0;
         for (int c = t; c < M0; c += SEL_THREADS) {
             const uint4 e = recs[c];
             if (e.x == 0xFFFFFFFFu) continue;
@@ -1224,9 +1228,9 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
                 return k <= kx && (((uint64_t)k << 32) | (uint64_t)(uint32_t)i) > tpair;
             });
         ng = min(s_ng, Tcap);
-        if (ng > ng0) score(M0, 16 * ng);
+        if (ng > ng0) score(M0, GS * ng);
     }
-    const int M = 16 * ng;
+    const int M = GS * ng;
     __syncthreads();
     const int nvalid = s_valid;
     if (M <= 256) {
@@ -1255,16 +1259,16 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
 
 void launch_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T, int nprobe, int metric,
                         const float *q, int64_t qld, const float *cent, const float *cnorm, int64_t ncent, int d,
-                        const float *bq, const float *qnorms, int nq, int64_t *probes, hipStream_t s) {
+                        const float *bq, const float *qnorms, int gs_log2, int nq, int64_t *probes, hipStream_t s) {
     if (nq <= 0) return;
     // room for the groups within the bound of the T-th (near-ties)
     const int Tcap = std::min(kCoarsePickMaxT, T + std::max(T, 8));
 #define MQVS_PICK(M, ST)                                                                                         \
     hipLaunchKernelGGL((k_coarse_pick<M, ST>), dim3(nq), dim3(SEL_THREADS), lds, s, gmax, gld, ngroups, T, Tcap, \
-                       nprobe, q, qld, cent, cnorm, ncent, d, bq, qnorms, probes)
+                       nprobe, q, qld, cent, cnorm, ncent, d, bq, qnorms, gs_log2, probes)
     const bool staged = ngroups <= kPickStage;
     size_t nr = 1;
-    while (nr < (size_t)16 * Tcap) nr <<= 1;
+    while (nr < ((size_t)1 << gs_log2) * Tcap) nr <<= 1;
     const size_t lds = nr * sizeof(uint4) + (staged ? sizeof(uint32_t) * (size_t)ngroups : 0);
     if (metric == MQVS_METRIC_L2) {
         if (staged) MQVS_PICK(MQVS_METRIC_L2, true); else MQVS_PICK(MQVS_METRIC_L2, false);

@@ -839,6 +839,18 @@ void launch_chunk_ordinals(const uint8_t *filter, const uint8_t *nonempty, const
     hipLaunchKernelGGL(k_exclusive_ord, dim3(1), dim3(kScanThreads), 0, s, ord, nchunks);
 }
 
+__global__ void k_words_to_host(const int64_t *a, int na, const int *b, int nb, int64_t *ha, int *hb) {
+    const int t = threadIdx.x;
+    if (t < na) *reinterpret_cast<volatile int64_t *>(ha + t) = a[t];
+    if (t < nb) *reinterpret_cast<volatile int *>(hb + t) = b[t];
+    __threadfence_system();
+}
+
+void launch_words_to_host(const int64_t *a, int na, const int *b, int nb, int64_t *host_a, int *host_b,
+                          hipStream_t s) {
+    hipLaunchKernelGGL(k_words_to_host, dim3(1), dim3(64), 0, s, a, na, b, nb, host_a, host_b);
+}
+
 // ---------------------------------------------------------------------------
 // ASYNC outcome of a search, OR-ed into the thread's sticky word
 // (mqvs_async_check)

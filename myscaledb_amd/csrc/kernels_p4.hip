@@ -681,7 +681,8 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
 // (row blocks 0..3 in the last stage's phase 1, 4..7 in the next item's first
 // phase 0, before their first MFMA overwrites them).
 // GRP (PROBE only): 0 = one value per (query, 128-row half tile) as k_scan_p4's
-// probe; 16 = one per (query, 16-row block), p4_gmax[q][16 t + 8 wr + rb]
+// probe; 16 = one per (query, 16-row block), p4_gmax[q][16 t + 8 wr + rb];
+// 8 = one per (query, 8-row half block), p4_gmax[q][2 (16 t + 8 wr + rb) + h]
 // (the index's coarse step, kernels_ivf.hip k_coarse_pick)
 // (Measured and dropped, profiles/r04/p4m_l7_stg_ab.jsonl: the next stage's
 // B fragment 7 read at the start of phase 0 instead of the end of phase 1,
@@ -946,19 +947,21 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
             }
         }
         const int j = q0 + wq * 128 + jb * 16 + l16;
-        if constexpr (PROBE && GRP == 16) {
-            // the four lanes of query l16 hold the block's 16 rows
+        if constexpr (PROBE && (GRP == 16 || GRP == 8)) {
+            // the four lanes of query l16 hold the block's 16 rows (lanes
+            // g4 = 0, 1: rows 0..7; g4 = 2, 3: rows 8..15)
 #pragma unroll
             for (int g = 0; g < 4; ++g) {
                 float m = __builtin_elementwise_maximum(__builtin_elementwise_maximum(v4[g][0], v4[g][1]),
                                                         __builtin_elementwise_maximum(v4[g][2], v4[g][3]));
                 m = __builtin_elementwise_maximum(m, __shfl_xor(m, 16));
-                m = __builtin_elementwise_maximum(m, __shfl_xor(m, 32));
-                if (g4 == 0 && j < p.nq) {
+                if constexpr (GRP == 16) m = __builtin_elementwise_maximum(m, __shfl_xor(m, 32));
+                if ((GRP == 16 ? g4 == 0 : (g4 & 1) == 0) && j < p.nq) {
                     float raw = m;
                     if constexpr (L2) raw = qtab[2 * (j - q0) + 1] - 2.0f * m;
                     if (m == -__builtin_inff()) raw = __builtin_nanf("");
-                    p.p4_gmax[(int64_t)j * p.p4_gld + 16 * eti + 8 * wr + 4 * hf + g] = raw;
+                    const int64_t blk = 16 * eti + 8 * wr + 4 * hf + g;  // 16-row block of the part
+                    p.p4_gmax[(int64_t)j * p.p4_gld + (GRP == 16 ? blk : 2 * blk + (g4 >> 1))] = raw;
                 }
             }
             return;
@@ -1394,22 +1397,27 @@ static bool launch_p4_probe_t(ScanParams p, hipStream_t s) {
     return true;
 }
 
-template <int METRIC>
+template <int METRIC, int GRP>
 static bool launch_p4_groups_t(ScanParams p, hipStream_t s) {
-    if (!p.p4_gmax || p.p4_gld < 16 * p.tiles || !p4_ok(p, false)) return false;
+    if (!p.p4_gmax || p.p4_gld < (256 / GRP) * p.tiles || !p4_ok(p, false)) return false;
     if (METRIC == MQVS_METRIC_L2 && !p.row_norms) return false;
     int dev = 0, cus = 0;
     MQVS_HIP(hipGetDevice(&dev));
     MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
     const int per_xcd = cus / 8;
     const int slots = per_xcd / p.num_qblocks * p.num_qblocks;
-    hipLaunchKernelGGL((k_scan_p4m<METRIC, 4, true, 16>), dim3((unsigned)(8 * per_xcd)), dim3(256), 0, s, p, slots,
+    hipLaunchKernelGGL((k_scan_p4m<METRIC, 4, true, GRP>), dim3((unsigned)(8 * per_xcd)), dim3(256), 0, s, p, slots,
                        nullptr, kP4QueueCap, 1);
     return true;
 }
 
-bool launch_scan_p4_groups(const ScanParams &p, int metric, hipStream_t s) {
-    return metric == MQVS_METRIC_L2 ? launch_p4_groups_t<MQVS_METRIC_L2>(p, s) : launch_p4_groups_t<kMetricIpRaw>(p, s);
+// grp: centroids per group, 16 or 8 (p4_gmax[q][tiles * 256 / grp])
+bool launch_scan_p4_groups(const ScanParams &p, int metric, int grp, hipStream_t s) {
+    if (grp == 8)
+        return metric == MQVS_METRIC_L2 ? launch_p4_groups_t<MQVS_METRIC_L2, 8>(p, s)
+                                        : launch_p4_groups_t<kMetricIpRaw, 8>(p, s);
+    return metric == MQVS_METRIC_L2 ? launch_p4_groups_t<MQVS_METRIC_L2, 16>(p, s)
+                                    : launch_p4_groups_t<kMetricIpRaw, 16>(p, s);
 }
 
 bool launch_scan_p4_probe(const ScanParams &p, int metric, hipStream_t s) {

@@ -582,6 +582,7 @@ static int call_gather_mode(uint32_t flags) {
 static bool call_timing(uint32_t flags) {
     return (flags & MQVS_F_TIMING) || g_timing.load(std::memory_order_relaxed) != 0;
 }
+bool timing_on(uint32_t flags) { return call_timing(flags); }
 
 // ASYNC searches cannot run the host-driven fallbacks (exact re-scan after a
 // pre-filter overflow, tightened re-scan, the cosine variant check): their

@@ -461,11 +461,17 @@ constexpr int kCoarsePickMaxT = 64;  // groups a coarse pick may take per query
 void index_thread_release();  // index.hip: the calling thread's index workspaces
 void launch_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T, int nprobe, int metric,
                         const float *q, int64_t qld, const float *cent, const float *cnorm, int64_t ncent, int d,
-                        const float *bq, const float *qnorms, int nq, int64_t *probes, hipStream_t s);
+                        const float *bq, const float *qnorms, int gs_log2, int nq, int64_t *probes, hipStream_t s);
 // the batch probe by 16-row groups (kernels_p4.hip): p.p4_gmax[q][16 t + r]
 // = the best value of rows [16 r, 16 r + 16) of tile t (p.p4_gld >= 16
 // p.tiles); false when the rows cannot take the batch kernel
-bool launch_scan_p4_groups(const ScanParams &p, int metric, hipStream_t s);
+// the call's per-kernel timing events (MQVS_F_TIMING or mqvs_set_timing)
+bool timing_on(uint32_t flags);
+// a[0, na) and b[0, nb) into pinned host memory (system-scope stores; one
+// launch instead of two copy kernels before the caller's stream sync)
+void launch_words_to_host(const int64_t *a, int na, const int *b, int nb, int64_t *host_a, int *host_b,
+                          hipStream_t s);
+bool launch_scan_p4_groups(const ScanParams &p, int metric, int grp, hipStream_t s);
 void launch_centroid_mean(const float *rows, int d, const int32_t *order, const int64_t *off, int nlist, float *cent,
                           hipStream_t s);
 
