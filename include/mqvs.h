@@ -390,6 +390,22 @@ int mqvs_index_info(mqvs_index_t idx, mqvs_index_info_t *out);
 int mqvs_index_search(mqvs_index_t idx, const float *queries, int32_t nq, int32_t k, const char *params,
                       const uint8_t *filter, const uint8_t *row_exists, int64_t *out_ids, float *out_dist,
                       uint32_t flags, mqvs_stream_t stream);
+/* Introspection of the coarse step (no reference counterpart: the MSTG
+ * library's quantizer is not exposed through VectorIndex; these let a caller
+ * or a test check the probes against its own exact top-nprobe):
+ * mqvs_index_centroids: the nlist x dim fp32 centroid table (normalised for
+ *   cosine indexes) into host memory; cap = floats out holds.
+ * mqvs_index_probes: for each of nq host queries the list ids the search with
+ *   `params` (alpha / nprobe as mqvs_index_search) would probe, in no
+ *   guaranteed order, into out_probes[nq][nprobe] (host; nprobe as
+ *   mqvs_index_last_stats then reports it; nq x nlist always suffices).
+ *   For nprobe <= 62 (the coarse pick) and for indexes of more than 16384
+ *   lists (a FLAT search of the centroids) the lists are the exact top nprobe
+ *   by the coarse metric (L2; the raw inner product for IP and cosine parts),
+ *   up to fp32 rounding of near ties; otherwise they are ranked by the bf16
+ *   approximate value (the centroid list pass). */
+int mqvs_index_centroids(mqvs_index_t idx, float *out, int64_t cap);
+int mqvs_index_probes(mqvs_index_t idx, const float *queries, int32_t nq, const char *params, int64_t *out_probes);
 /* Decoupled parts: a part merged from several source parts whose index still
  * serves the source part's rows (the reference's VIWithMeta row_ids_map /
  * inverted maps, VICacheObject.h:50-64).

@@ -46,6 +46,7 @@ SYMBOLS = [
     "mqvs_last_search_stats", "mqvs_set_timing", "mqvs_set_batch_mode", "mqvs_set_gather_mode", "mqvs_set_prefilter",
     "mqvs_set_scratch_budget", "mqvs_measure_read_bandwidth", "mqvs_set_workspace_budget", "mqvs_workspace_stats",
     "mqvs_index_build", "mqvs_index_free", "mqvs_index_info", "mqvs_index_search", "mqvs_index_last_stats",
+    "mqvs_index_centroids", "mqvs_index_probes",
     "mqvs_segment_create_binary", "mqvs_search_binary", "mqvs_knn_binary_raw",
     "mqvs_segment_create_from_column", "mqvs_async_check",
     "mqvs_comm_unique_id", "mqvs_comm_init", "mqvs_comm_init_loopback", "mqvs_comm_free", "mqvs_sharded_search", "mqvs_comm_stats",
@@ -155,6 +156,8 @@ def _load(path=LIB_PATH):
         "mqvs_index_info": ([P, P], ctypes.c_int),
         "mqvs_index_search": ([P, P, I32, I32, ctypes.c_char_p, P, P, P, P, U32, P], ctypes.c_int),
         "mqvs_index_last_stats": ([P], ctypes.c_int),
+        "mqvs_index_centroids": ([P, P, I64], ctypes.c_int),
+        "mqvs_index_probes": ([P, P, I32, ctypes.c_char_p, P], ctypes.c_int),
         "mqvs_segment_create_binary": ([P, I64, I32, I32, I64, I64, U32, P], ctypes.c_int),
         "mqvs_search_binary": ([P, P, I32, I32, I32, P, P, P, P, U32, P], ctypes.c_int),
         "mqvs_knn_binary_raw": ([P, P, I64, I64, I64, I64, I32, P, P], ctypes.c_int),

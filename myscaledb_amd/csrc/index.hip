@@ -735,6 +735,10 @@ static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, c
     if (ev) MQVS_HIP(hipEventRecord(ev[4], s));
 }
 
+// mqvs_index_probes sets this for the duration of one search: the coarse
+// step's probes[nq][nprobe] are copied there and the search ends
+static thread_local int64_t *t_probes_out = nullptr;
+
 // formula_nq: the call's batch size, which selects the exact re-rank's
 // distance formula (0: nq; query sub-batches keep the call's, see mqvs.hip)
 static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int k, const char *params,
@@ -958,6 +962,12 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
                   nullptr, nullptr, s, true);
     }
     if (tev) MQVS_HIP(hipEventRecord(ws.ev[1], s));
+    if (t_probes_out) {
+        // mqvs_index_probes: the coarse step's lists, nothing after it
+        MQVS_HIP(hipMemcpyAsync(t_probes_out, probes, sizeof(int64_t) * (size_t)nq * nprobe, hipMemcpyDeviceToHost, s));
+        MQVS_HIP(hipStreamSynchronize(s));
+        return;
+    }
     if (split && late_fork) fork_chain();
 
     // ---- fine: the probed lists
@@ -1100,6 +1110,34 @@ int mqvs_index_search(mqvs_index_t idx, const float *queries, int32_t nq, int32_
         fault_point();
         search_index_impl(idx, queries, nq, k, params, filter, row_exists, out_ids, out_dist, flags,
                           (hipStream_t)stream, 0);
+    });
+}
+
+int mqvs_index_centroids(mqvs_index_t idx, float *out, int64_t cap) {
+    return guarded([&] {
+        if (!idx || !out) fail(MQVS_ERR_BAD_ARGUMENTS, "null argument");
+        if (!idx->cent) fail(MQVS_ERR_LOGICAL, "index has no centroid table");
+        const int64_t need = idx->cent->n * (int64_t)idx->cent->d;
+        if (cap < need) fail(MQVS_ERR_BAD_ARGUMENTS, "output holds " + std::to_string(cap) + " floats, " +
+                                                         std::to_string(need) + " needed");
+        DeviceGuard guard(idx->cent->device);
+        MQVS_HIP(hipMemcpy(out, idx->cent->rows, sizeof(float) * (size_t)need, hipMemcpyDeviceToHost));
+    });
+}
+
+int mqvs_index_probes(mqvs_index_t idx, const float *queries, int32_t nq, const char *params, int64_t *out_probes) {
+    return guarded([&] {
+        if (!idx || (nq > 0 && (!queries || !out_probes))) fail(MQVS_ERR_BAD_ARGUMENTS, "null argument");
+        if (nq < 0) fail(MQVS_ERR_BAD_ARGUMENTS, "nq must be non-negative");
+        if (nq == 0) return;
+        struct Reset {
+            ~Reset() { t_probes_out = nullptr; }
+        } reset;
+        t_probes_out = out_probes;
+        // k 1: the coarse step does not depend on k; the search stops after it
+        std::vector<int64_t> ids((size_t)nq);
+        std::vector<float> dd((size_t)nq);
+        search_index_impl(idx, queries, nq, 1, params, nullptr, nullptr, ids.data(), dd.data(), 0, nullptr, 0);
     });
 }
 

@@ -66,6 +66,28 @@ class VectorIndex:
         check(lib.mqvs_index_info(self._h, ctypes.byref(st)))
         return {f: getattr(st, f) for f, _ in _lib.IndexInfo._fields_}
 
+    def centroids(self):
+        """The coarse step's centroid table, float32[nlist, dim]."""
+        info = self.info()
+        c = np.empty((info["nlist"], info["dim"]), np.float32)
+        check(lib.mqvs_index_centroids(self._h, _ptr(c), c.size))
+        return c
+
+    def probes(self, queries, params=None):
+        """The lists a search with `params` probes, int64[nq, nprobe] (no order)."""
+        q = _host_f32(queries)
+        if q.ndim == 1:
+            q = q[None, :]
+        nq = q.shape[0]
+        pr = _params(params)
+        info = self.info()
+        # nprobe as the search resolves it: run the coarse step into a buffer
+        # of every list, then trim to the count the stats report
+        buf = np.full((nq, info["nlist"]), -1, np.int64)
+        check(lib.mqvs_index_probes(self._h, _ptr(q), nq, pr, _ptr(buf)))
+        npb = _lib.last_index_stats()["nprobe"]
+        return buf.reshape(-1)[: nq * npb].reshape(nq, npb).copy()
+
     def search(self, queries, k, params=None, filter_bitmap=None, row_exists=None, first_stage_only=False,
                out=None, async_=False, stream=None):
         """(ids[nq,k] int64, dist[nq,k] float32), reference order, -1 padded.

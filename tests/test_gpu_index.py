@@ -309,3 +309,61 @@ def test_index_many_lists(mq):
     assert recall >= 0.9, recall
     assert np.array_equal(ids_r, ids_i)
     assert np.array_equal(dist_r.view(np.uint32), dist_i.view(np.uint32))
+
+
+@pytest.mark.parametrize("metric,d,nlist", [("L2", 128, 96), ("IP", 64, 64), ("Cosine", 768, 48)])
+def test_index_coarse_probes_are_exact_top_nprobe(mq, metric, d, nlist):
+    """The coarse pick (nprobe <= 62: bf16 group maxima of the centroid scan,
+    then exact fp32 values for every group the bf16 bound cannot rule out)
+    returns the exact top-nprobe centroids.  Queries sit between two centroids
+    at a relative offset of 1e-2 .. 1e-4 -- near ties the bf16 values cannot
+    order -- and at random points.  Checked against float64 scores of the
+    index's own centroid table: no unpicked centroid is better than a picked
+    one by more than fp32 rounding of the score (parity unpinned: the MSTG
+    quantizer is absent from the reference snapshot)."""
+    n = 40000
+    rows = O.generate(0x5EED0011, 2, 0, n, d)
+    seg = mq.VectorScanSegment.from_rows(rows, metric=metric, granule=1024)
+    idx = mq.VectorIndex.build(seg, "MSTG", {"nlist": nlist})
+    try:
+        C = idx.centroids().astype(np.float64)
+        assert C.shape == (nlist, d) and np.all(np.isfinite(C))
+        rng = np.random.default_rng(d)
+        a = rng.integers(0, nlist, 96)
+        b = (a + 1 + rng.integers(0, nlist - 1, 96)) % nlist
+        eps = 10.0 ** -rng.integers(2, 5, 96)[:, None]
+        m, v = (C[a] + C[b]) / 2, C[a] - C[b]
+        if metric == "IP":  # equal inner products with a and b (centroid norms differ)
+            m = m - np.sum(m * v, axis=1, keepdims=True) / np.sum(v * v, axis=1, keepdims=True) * v
+        q = np.concatenate([m + eps * v,
+                            O.generate(0x5EED0012, 2, 0, 32, d).astype(np.float64)]).astype(np.float32)
+        got = {}
+        for nprobe in (1, 2, 5, 17, 60):
+            got[nprobe] = idx.probes(q, {"nprobe": nprobe})
+    finally:
+        idx.free()
+        seg.free()
+    q64 = q.astype(np.float64)
+    if metric == "Cosine":
+        q64 /= np.linalg.norm(q64, axis=1, keepdims=True)
+    qn = np.sum(q64 * q64, axis=1)[:, None]
+    cn = np.sum(C * C, axis=1)[None, :]
+    if metric == "L2":
+        score = qn + cn - 2 * q64 @ C.T          # smaller is better
+        tol = 4e-6 * (qn + cn).max(axis=1)
+    else:
+        score = -(q64 @ C.T)                      # raw inner product, larger is better
+        tol = 4e-6 * np.sqrt(qn[:, 0] * cn.max())
+    near_ties = 0
+    for nprobe, pr in got.items():
+        assert pr.shape == (len(q), nprobe)
+        for i in range(len(q)):
+            s = set(pr[i].tolist())
+            assert len(s) == nprobe and min(s) >= 0 and max(s) < nlist, (nprobe, i, pr[i])
+            picked = score[i, pr[i]]
+            rest = np.delete(score[i], pr[i])
+            if rest.size:
+                assert picked.max() <= rest.min() + tol[i], (metric, nprobe, i, picked.max() - rest.min(), tol[i])
+                srt = np.sort(score[i])
+                near_ties += int(srt[nprobe] - srt[nprobe - 1] < 1e3 * tol[i])
+    assert near_ties > 0  # the set holds boundaries bf16 alone cannot order
