@@ -338,7 +338,7 @@ def test_index_coarse_probes_are_exact_top_nprobe(mq, metric, d, nlist):
         q = np.concatenate([m + eps * v,
                             O.generate(0x5EED0012, 2, 0, 32, d).astype(np.float64)]).astype(np.float32)
         got = {}
-        for nprobe in (1, 2, 5, 17, 60):
+        for nprobe in (1, 2, 5, 17, min(60, nlist - 2)):
             got[nprobe] = idx.probes(q, {"nprobe": nprobe})
     finally:
         idx.free()
