@@ -705,7 +705,13 @@ static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, c
         if (!dense && (v == 16 || v == 32 || v == 64)) p.qg = v;
     }
     // work items = sum over probed lists of groups x 512-position slices
-    const int64_t max_items = (E / p.qg + std::min<int64_t>(E, nlist)) * (max_list / 512 + 1);
+    // list positions per work item (a multiple of 64): 8 x the item's queries,
+    // so the query tile stays a fixed share of the bytes an item reads (round
+    // 5: 128 for 16-query items, 512 before -- the item setup's chain of
+    // dependent loads was a large part of a 256-position list's scan; mode 3
+    // nprobe 1 scan 0.139 -> 0.117 ms, profiles/r05/index_scan/)
+    p.chunk = dense ? kIvfChunk : std::max(64, tune_int("MQVS_IVF_CHUNK", 8 * p.qg) / 64 * 64);
+    const int64_t max_items = (E / p.qg + std::min<int64_t>(E, nlist)) * (max_list / p.chunk + 1);
     p.item_list = (int *)b.items.get(sizeof(int) * max_items);
     p.item_grp = (int *)b.grp.get(sizeof(int) * max_items);
     p.item_chk = (int *)b.chk.get(sizeof(int) * max_items);
@@ -724,7 +730,8 @@ static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, c
         launch_ivf_plan(p, s);
     MQVS_HIP(hipGetLastError());
     if (ev) MQVS_HIP(hipEventRecord(ev[2], s));
-    launch_ivf_scan(p, metric, 1024, s);
+    // (a workgroup per work item up to 4096: ~2900 items at nq 1000, nprobe 1)
+    launch_ivf_scan(p, metric, dense ? 1024 : tune_int("MQVS_IVF_GRID", 4096), s);
     MQVS_HIP(hipGetLastError());
     if (ev) MQVS_HIP(hipEventRecord(ev[3], s));
     const int64_t expect = dense ? npos : (int64_t)((double)nprobe * npos / std::max<int64_t>(nlist, 1) * 1.5);

@@ -30,7 +30,6 @@ typedef float ivf_f32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int kPlanThreads = 1024;
 constexpr int kIvfWin = 4;      // 64-column windows loaded per group in the scan
-constexpr int kIvfChunk = 512;  // list positions per scan work item (balances long and short lists)
 
 // Exclusive scan of `n` int64 values produced by val(i) into out(i, prefix);
 // returns the total.  One workgroup of kPlanThreads; each thread owns a
@@ -112,7 +111,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_lists_reg(IvfParams p) {
         cnt[u] = in ? p.lcount[base + i] : 0;
         len[u] = in ? (int)(p.list_off[base + i + 1] - p.list_off[base + i]) : 0;
     }
-    auto items_of = [&](int u) { return (int64_t)((cnt[u] + p.qg - 1) >> qs) * ((len[u] + kIvfChunk - 1) / kIvfChunk); };
+    auto items_of = [&](int u) { return (int64_t)((cnt[u] + p.qg - 1) >> qs) * ((len[u] + p.chunk - 1) / p.chunk); };
     auto rows_of = [&](int u) { return (int64_t)((cnt[u] + p.qg - 1) >> qs) * len[u]; };
     int64_t w0 = 0, w1 = 0, w2 = 0;
 #pragma unroll
@@ -178,7 +177,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_lists_reg(IvfParams p) {
             p.lfill[base + i] = 0;  // the scatter's cursors (no memset of their own)
             int64_t r1 = c1 + i1 - v1;
             const int g = (cnt[u] + p.qg - 1) >> qs;
-            const int nc = (len[u] + kIvfChunk - 1) / kIvfChunk;
+            const int nc = (len[u] + p.chunk - 1) / p.chunk;
             for (int j = 0; j < g; ++j)
                 for (int cc = 0; cc < nc; ++cc) {
                     p.item_list[r1] = base + i;
@@ -236,7 +235,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_lists_blk(IvfParams p) {
         const int c = s_cnt[kPlanPer * t + r], l = s_len[kPlanPer * t + r];
         const int64_t g = (c + p.qg - 1) >> qs;
         a0 += c;
-        a1 += g * ((l + kIvfChunk - 1) / kIvfChunk);
+        a1 += g * ((l + p.chunk - 1) / p.chunk);
         a2 += g * l;
     }
     const int64_t i0 = wave_incl_scan(a0), i1 = wave_incl_scan(a1), i2 = wave_incl_scan(a2);
@@ -280,7 +279,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_lists_blk(IvfParams p) {
         if (li >= L) break;
         const int c = s_cnt[li], l = s_len[li];
         const int g = (c + p.qg - 1) >> qs;
-        const int nc = (l + kIvfChunk - 1) / kIvfChunk;
+        const int nc = (l + p.chunk - 1) / p.chunk;
         p.lstart[base + li] = c0;
         p.lfill[base + li] = 0;  // the scatter's cursors (no memset of their own)
         for (int j = 0; j < g; ++j)
@@ -320,7 +319,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_lists(IvfParams p) {
         len = in ? (int)(p.list_off[i + 1] - p.list_off[i]) : 0;
     };
     auto items_of = [&](int cnt, int len) {
-        return (int64_t)((cnt + p.qg - 1) >> qs) * ((len + kIvfChunk - 1) / kIvfChunk);
+        return (int64_t)((cnt + p.qg - 1) >> qs) * ((len + p.chunk - 1) / p.chunk);
     };
     int64_t w0 = 0, w1 = 0, w2 = 0;
     const int steps = S / 64;
@@ -370,7 +369,7 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_lists(IvfParams p) {
             p.lfill[i] = 0;
             int64_t r1 = c1 + i1 - v1;
             const int g = (cnt + p.qg - 1) >> qs;
-            const int nc = (len + kIvfChunk - 1) / kIvfChunk;
+            const int nc = (len + p.chunk - 1) / p.chunk;
             for (int j = 0; j < g; ++j)
                 for (int cc = 0; cc < nc; ++cc) {
                     p.item_list[r1] = i;
@@ -439,7 +438,7 @@ __global__ __launch_bounds__(256) void k_plan_dense(IvfParams p, int64_t npos) {
     }
     // items (list, group, slice): lists here are centroid chunks of equal
     // length, so every list has the same slices
-    const int NC = (int)((p.list_off[1] - p.list_off[0] + kIvfChunk - 1) / kIvfChunk);
+    const int NC = (int)((p.list_off[1] - p.list_off[0] + p.chunk - 1) / p.chunk);
     for (int64_t i = gt; i < (int64_t)L * G * NC; i += gs) {
         p.item_list[i] = (int)(i / ((int64_t)G * NC));
         p.item_grp[i] = (int)((i / NC) % G);
@@ -482,6 +481,36 @@ __global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
     const int ngrp = (int)((p.dpad / 64 + kIvfWin - 1) / kIvfWin);
     for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
         const int l = p.item_list[it], g = p.item_grp[it], chk = p.item_chk[it];
+        const int64_t pos0 = p.list_off[l];
+        const int cb = p.chunk / 16;  // 16-position blocks per work item
+        const int nb = (int)min<int64_t>((p.list_off[l + 1] - pos0) / 16, (int64_t)(chk + 1) * cb);
+        // the wave's blocks b0, b0 + 4, ... as one sequence of (block, window
+        // group) steps: the next step's loads -- the next block's first group
+        // included -- are in flight while a step feeds the MFMAs
+        const int b0 = chk * cb + w;
+        const int nsteps = b0 < nb ? (nb - b0 + 3) / 4 * ngrp : 0;
+        // the plane is blocked like the FLAT pre-filter plane: 16 positions x
+        // 32 columns = 1 KiB per piece (k_ivf_pack), so each fragment load of a
+        // wave reads one contiguous KiB (8 whole 128-B lines)
+        const uint16_t *rp0 = p.plane + ((pos0 >> 4) + (int64_t)b0) * 16 * p.dpad + l16 * 32 + c * 8;
+        const int64_t bstride = 4 * 16 * p.dpad;  // 4 blocks on
+        auto load = [&](int st, ivf_bf16x8 *dst) {
+            const int bi = st / ngrp, grp = st - bi * ngrp;
+            const uint16_t *rp = rp0 + bi * bstride;
+#pragma unroll
+            for (int u = 0; u < kIvfWin; ++u) {
+                const int64_t kw = ((int64_t)grp * kIvfWin + u) * 64;
+                if (kw < p.dpad) {
+                    dst[2 * u] = *reinterpret_cast<const ivf_bf16x8 *>(rp + (kw >> 5) * 512);
+                    dst[2 * u + 1] = *reinterpret_cast<const ivf_bf16x8 *>(rp + ((kw >> 5) + 1) * 512);
+                }
+            }
+        };
+        // the first step's rows are requested before the query tile is staged
+        // (its chain of dependent loads: pairs, regions, query rows): at ~256
+        // positions per list the item setup is a large part of an item
+        ivf_bf16x8 cur[2 * kIvfWin], nxt[2 * kIvfWin];
+        if (nsteps > 0) load(0, cur);
         const int cnt = min(QG, p.lcount[l] - g * QG);
         __syncthreads();  // the previous item's readers are done with qtile
         if (threadIdx.x < QG) {
@@ -500,65 +529,52 @@ __global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
             *reinterpret_cast<uint4 *>(qtile + j * qstr + cc * 16) = v;
         }
         __syncthreads();
-        const int64_t pos0 = p.list_off[l];
-        const int nb = (int)min<int64_t>((p.list_off[l + 1] - pos0) / 16, (int64_t)(chk + 1) * (kIvfChunk / 16));
         const unsigned char *qp = qtile + l16 * qstr + c * 16;
         int ent[QB];
 #pragma unroll
         for (int j = 0; j < QB; ++j) ent[j] = s_ent[16 * j + l16];
-        for (int b = chk * (kIvfChunk / 16) + w; b < nb; b += 4) {
-            // the plane is blocked like the FLAT pre-filter plane: 16 positions
-            // x 32 columns = 1 KiB per piece (k_ivf_pack), so each fragment
-            // load of a wave reads one contiguous KiB (8 whole 128-B lines);
-            // round 3's row-major plane made it 16 half lines (measured
-            // neutral: configs[2] mode 2 scan 0.68 ms either way)
-            const uint16_t *rp = p.plane + ((pos0 >> 4) + (int64_t)b) * 16 * p.dpad + l16 * 32 + c * 8;
-            ivf_f32x4 acc[QB];
+        ivf_f32x4 acc[QB];
+        int32_t rows[4];
+        float pn[4];
+        for (int st = 0; st < nsteps; ++st) {
+            const int bi = st / ngrp, grp = st - bi * ngrp;
+            const int64_t lp = (int64_t)(b0 + 4 * bi) * 16 + 4 * c;
+            if (grp == 0) {
 #pragma unroll
-            for (int j = 0; j < QB; ++j) acc[j] = ivf_f32x4{0.f, 0.f, 0.f, 0.f};
-            ivf_bf16x8 cur[2 * kIvfWin], nxt[2 * kIvfWin];
-            auto load = [&](int grp, ivf_bf16x8 *dst) {
+                for (int j = 0; j < QB; ++j) acc[j] = ivf_f32x4{0.f, 0.f, 0.f, 0.f};
+                // the block's position records, ahead of the next step's loads
 #pragma unroll
-                for (int u = 0; u < kIvfWin; ++u) {
-                    const int64_t kw = ((int64_t)grp * kIvfWin + u) * 64;
-                    if (kw < p.dpad) {
-                        dst[2 * u] = *reinterpret_cast<const ivf_bf16x8 *>(rp + (kw >> 5) * 512);
-                        dst[2 * u + 1] = *reinterpret_cast<const ivf_bf16x8 *>(rp + ((kw >> 5) + 1) * 512);
-                    }
+                for (int r = 0; r < 4; ++r) {
+                    rows[r] = p.perm[pos0 + lp + r];
+                    pn[r] = METRIC == MQVS_METRIC_L2 ? p.pnorm[pos0 + lp + r] : 0.f;
                 }
-            };
-            load(0, cur);
-            for (int grp = 0; grp < ngrp; ++grp) {
-                if (grp + 1 < ngrp) load(grp + 1, nxt);
-#pragma unroll
-                for (int u = 0; u < kIvfWin; ++u) {
-                    const int64_t kw = ((int64_t)grp * kIvfWin + u) * 64;
-                    if (kw < p.dpad) {
-#pragma unroll
-                        for (int j = 0; j < QB; ++j) {
-                            const unsigned char *qj = qp + 16 * j * qstr + 2 * kw;
-                            const ivf_bf16x8 b0 = *reinterpret_cast<const ivf_bf16x8 *>(qj);
-                            const ivf_bf16x8 b1 = *reinterpret_cast<const ivf_bf16x8 *>(qj + 64);
-                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[2 * u], b0, acc[j], 0, 0, 0);
-                            acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[2 * u + 1], b1, acc[j], 0, 0, 0);
-                        }
-                    }
-                }
-#pragma unroll
-                for (int u = 0; u < 2 * kIvfWin; ++u) cur[u] = nxt[u];
             }
+            if (st + 1 < nsteps) load(st + 1, nxt);
+#pragma unroll
+            for (int u = 0; u < kIvfWin; ++u) {
+                const int64_t kw = ((int64_t)grp * kIvfWin + u) * 64;
+                if (kw < p.dpad) {
+#pragma unroll
+                    for (int j = 0; j < QB; ++j) {
+                        const unsigned char *qj = qp + 16 * j * qstr + 2 * kw;
+                        const ivf_bf16x8 q0 = *reinterpret_cast<const ivf_bf16x8 *>(qj);
+                        const ivf_bf16x8 q1 = *reinterpret_cast<const ivf_bf16x8 *>(qj + 64);
+                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[2 * u], q0, acc[j], 0, 0, 0);
+                        acc[j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(cur[2 * u + 1], q1, acc[j], 0, 0, 0);
+                    }
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 2 * kIvfWin; ++u) cur[u] = nxt[u];
+            if (grp != ngrp - 1) continue;
             // C: lane (l16, c) holds rows 4c..4c+3 of the block for query slot 16 j + l16
-            const int64_t lp = (int64_t)b * 16 + 4 * c;
-            int32_t rows[4];
-            float pn[4];
+            int32_t rr[4];
 #pragma unroll
             for (int r = 0; r < 4; ++r) {
-                const int64_t gpos = pos0 + lp + r;
-                int32_t row = p.perm[gpos];
+                int32_t row = rows[r];
                 if (row >= 0 && p.filter && !bit_test(p.filter, row)) row = -1;
                 if (row >= 0 && p.exists && !bit_test(p.exists, row)) row = -1;
-                rows[r] = row;
-                pn[r] = METRIC == MQVS_METRIC_L2 ? p.pnorm[gpos] : 0.f;
+                rr[r] = row;
             }
 #pragma unroll
             for (int j = 0; j < QB; ++j) {
@@ -568,8 +584,8 @@ __global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
                 for (int r = 0; r < 4; ++r) {
                     float raw = acc[j][r];
                     if (METRIC == MQVS_METRIC_L2) raw = (s_qn[16 * j + l16] + pn[r]) - 2.0f * raw;
-                    out[r].raw = rows[r] >= 0 ? raw : __builtin_nanf("");
-                    out[r].row = rows[r] >= 0 ? (uint32_t)rows[r] : 0xFFFFFFFFu;
+                    out[r].raw = rr[r] >= 0 ? raw : __builtin_nanf("");
+                    out[r].row = rr[r] >= 0 ? (uint32_t)rr[r] : 0xFFFFFFFFu;
                 }
                 uint4 *dst = reinterpret_cast<uint4 *>(p.cand + s_base[16 * j + l16] + lp);
                 dst[0] = *reinterpret_cast<const uint4 *>(&out[0]);

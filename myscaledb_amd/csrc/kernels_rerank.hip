@@ -230,6 +230,104 @@ __device__ inline float wave_exact(const ScanParams &p, int q, int64_t row, floa
     return raw;
 }
 
+// d = 32 NT (NT a compile-time tile count; the common d = 768 is NT = 24):
+// the same chain and staging, the tile loop fully unrolled and the row
+// slices of kRrPF tiles in flight in a register ring.  Every load is
+// unconditional (a lane without a candidate streams row 0, its result is
+// discarded; the ring's refills past the last tile re-read it), so the
+// compiler counts each wait exactly: wave_exact waits a full random-row load
+// latency per tile (one tile ahead), ~24 latencies per wave at d = 768.
+constexpr int kRrPF = 3;
+
+template <int METRIC, bool DIRECT, int NT>
+__device__ inline float wave_exact_nt(const ScanParams &p, int q, int64_t row, float *tile) {
+    constexpr int d = 32 * NT;
+    const int lane = threadIdx.x & 63;
+    const float *x = p.qvars;
+    if (row >= 0) {
+        const int64_t chunk = p.chunk_rows > 0 ? row / p.chunk_rows : 0;
+        const int ord = chunk_ordinal(p, chunk);
+        const int v = variant_of(p, q, ord < 0 ? 0 : ord);
+        x = p.qvars + ((int64_t)q * p.maxv + v) * d;
+    }
+    float acc = 0.0f;
+    if (__ballot(row >= 0)) {
+        // rows this lane loads: slot j*8 + lane/8, float4 column lane%8
+        const float *base[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+            const int64_t r = __shfl(row, j * 8 + (lane >> 3));
+            base[j] = p.rows + (r >= 0 ? r : 0) * d + (lane & 7) * 4;
+        }
+        float4 ry[kRrPF][8], rx[8];
+        auto load_y = [&](int t, float4(&dst)[8]) __attribute__((always_inline)) {
+            const int tt = t < NT ? t : NT - 1;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) dst[j] = *reinterpret_cast<const float4 *>(base[j] + tt * 32);
+        };
+        auto load_x = [&](int t) __attribute__((always_inline)) {
+            const int tt = t < NT ? t : NT - 1;
+#pragma unroll
+            for (int j = 0; j < 8; ++j) rx[j] = *reinterpret_cast<const float4 *>(x + tt * 32 + 4 * j);
+        };
+#pragma unroll
+        for (int sl = 0; sl < kRrPF; ++sl) load_y(sl, ry[sl]);
+        load_x(0);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+            float4(&cur)[8] = ry[t % kRrPF];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                float *dst = tile + (j * 8 + (lane >> 3)) * kRrStride + (lane & 7) * 4;
+                dst[0] = cur[j].x;
+                dst[1] = cur[j].y;
+                dst[2] = cur[j].z;
+                dst[3] = cur[j].w;
+            }
+            float xt[32];
+#pragma unroll
+            for (int j = 0; j < 8; ++j) {
+                xt[4 * j] = rx[j].x;
+                xt[4 * j + 1] = rx[j].y;
+                xt[4 * j + 2] = rx[j].z;
+                xt[4 * j + 3] = rx[j].w;
+            }
+            load_y(t + kRrPF, cur);
+            load_x(t + 1);
+            __builtin_amdgcn_wave_barrier();
+            const float *mine = tile + lane * kRrStride;
+#pragma unroll
+            for (int cc = 0; cc < 32; ++cc) {
+                const float a = mine[cc], b = xt[cc];
+                if (DIRECT) {
+                    if (METRIC == MQVS_METRIC_L2) {
+                        const float e = a - b;
+                        acc = acc + e * e;
+                    } else {
+                        acc = acc + a * b;
+                    }
+                } else {
+                    acc = fmaf(b, a, acc);
+                }
+            }
+            __builtin_amdgcn_wave_barrier();
+        }
+    }
+    float raw = acc;
+    if (!DIRECT && METRIC == MQVS_METRIC_L2 && row >= 0) {
+        raw = (p.qnorms[q] + p.row_norms[row]) - 2.0f * acc;
+        if (raw < 0) raw = 0;
+    }
+    return raw;
+}
+
+// wave_exact_nt for d = 768, wave_exact otherwise
+template <int METRIC, bool DIRECT>
+__device__ inline float wave_exact_any(const ScanParams &p, int q, int64_t row, float *tile) {
+    if (p.d == 768) return wave_exact_nt<METRIC, DIRECT, 24>(p, q, row, tile);
+    return wave_exact<METRIC, DIRECT>(p, q, row, tile);
+}
+
 template <int METRIC, bool DIRECT>
 __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids_tiled(ScanParams p, const int64_t *cand, int ncand,
                                                                  int k, int64_t id_offset, int64_t *out_ids,
@@ -249,7 +347,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids_tiled(ScanParams p, 
             row = c[i];
             if (!(row >= 0 && row < p.n && row_valid(p, row))) row = -1;
         }
-        const float raw = wave_exact<METRIC, DIRECT>(p, q, row, tile);
+        const float raw = wave_exact_any<METRIC, DIRECT>(p, q, row, tile);
         if (i < ncand) dst[i] = rerank_rec<METRIC>(p, row, raw);
     }
     rerank_emit<METRIC>(recs, g, ncand, k, q, id_offset, out_ids, out_dist);
@@ -274,7 +372,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_exact_records(ScanParams p, con
         const int64_t row = i < m ? (int64_t)surv[(int64_t)q * rs + i] : -1;
         float raw;
         if ((p.d & 3) == 0)
-            raw = wave_exact<METRIC, DIRECT>(p, q, row, tile);
+            raw = wave_exact_any<METRIC, DIRECT>(p, q, row, tile);
         else
             raw = row >= 0 ? cand_value<METRIC, DIRECT>(p, q, row) : 0.f;
         if (i < m) recs[(int64_t)q * rs + i] = rerank_rec<METRIC>(p, row, raw);

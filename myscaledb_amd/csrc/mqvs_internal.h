@@ -412,6 +412,8 @@ void launch_exact_rerank(const ScanParams &p, int metric, const uint32_t *surv, 
 // Index path (kernels_ivf.hip, index.hip)
 constexpr int kIvfPad = 16;  // list lengths padded to this many positions
 
+constexpr int kIvfChunk = 512;  // default list positions per scan work item (balances long and short lists)
+
 struct IvfParams {
     const uint16_t *plane;    // [npos][dpad] bf16 rows in list order
     const int32_t *perm;      // [npos] segment row of each position, -1 = padding
@@ -421,6 +423,7 @@ struct IvfParams {
     int64_t dpad;
     int nq, nprobe;
     int qg;                   // queries per scan work item: 16 or 32 (MFMA B blocks x 16)
+    int chunk;                // list positions per scan work item (multiple of 64)
     const int64_t *probes;    // [nq][nprobe] list ids (-1 = none)
     const uint16_t *q_hi;     // [nq][dpad] bf16 query (cosine: normalised)
     const float *qnorm;       // [nq] |q|^2 (L2)

@@ -5,6 +5,7 @@
 cd "$GRAFT_REPO_ROOT" || exit 1
 export TMPDIR=/tmp
 O=gpurun_out/$1; shift
+IDX_TUNES=${IDX_TUNES:-";MQVS_IVF_CHUNK=256;MQVS_IVF_CHUNK=128;MQVS_IVF_CHUNK=256,MQVS_IVF_GRID=2048;MQVS_IVF_CHUNK=128,MQVS_IVF_GRID=4096"}
 mkdir -p $O
 trace() {  # name, args...
   local name=$1; shift
@@ -25,6 +26,10 @@ for step in "$@"; do
                 -- python3 "$GRAFT_REPO_ROOT/tools/index_search_run.py" --mode $m --search nprobe=1 --searches 3 \
                 > "$GRAFT_REPO_ROOT/$O/tr_idx$m.log" 2>&1 ) || exit 1
             python3 tools/timeline.py $O/tr_idx$m/run_kernel_trace.csv --start k_to_bf16 --nth -1 ;;
+    idx_ab) for m in 3 2; do
+              timeout -k 10 400 python -u tools/index_scan_ab.py --mode $m --search "${IDX_SEARCH:-nprobe=1}" --tunes "$IDX_TUNES" > $O/idx_ab$m.jsonl 2> $O/idx_ab$m.err || exit 1
+              cat $O/idx_ab$m.jsonl
+            done ;;
     bench_quick) timeout -k 10 300 python bench.py --steps 5 --warmup 2 --no-index --no-configs --no-config1-points --no-cpu > $O/bench_quick.json 2> $O/bench_quick.err || exit 1
                  python3 -c "import json;d=json.loads(open('$O/bench_quick.json').readlines()[-1]);print(d['value'],d['ms_per_step'],d['roofline']);print([ (x['nq'],x['ms_per_search'],x['hbm_frac_end_to_end']) for x in d['small_batch']])" ;;
     bench) timeout -k 10 900 python bench.py --steps 20 --warmup 5 > $O/bench.json 2> $O/bench.err || exit 1 ;;
