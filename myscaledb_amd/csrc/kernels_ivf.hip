@@ -466,9 +466,17 @@ __global__ __launch_bounds__(256) void k_plan_dense(IvfParams p, int64_t npos) {
 // one load instruction covers a contiguous 64-B half-window of 16 rows.
 // kIvfWin windows are in flight per lane and the next group is prefetched
 // while the current one feeds the MFMAs; every A fragment serves QB MFMAs.
-template <int METRIC, int QB>
+template <int METRIC, int QB, bool NTL>
 __global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
     constexpr int QG = 16 * QB;
+    // plane reads: each probed list's rows are read once per query group
+    // (NTL: non-temporal, kept out of the caches' retention)
+    auto ldp = [](const uint16_t *a) __attribute__((always_inline)) {
+        typedef uint32_t u32x4_t __attribute__((ext_vector_type(4)));
+        if (NTL)
+            return __builtin_bit_cast(ivf_bf16x8, __builtin_nontemporal_load(reinterpret_cast<const u32x4_t *>(a)));
+        return *reinterpret_cast<const ivf_bf16x8 *>(a);
+    };
     extern __shared__ __attribute__((aligned(16))) unsigned char qtile[];  // QG x (2 dpad + 16) B
     __shared__ int s_ent[QG];
     __shared__ int64_t s_base[QG];
@@ -501,8 +509,8 @@ __global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
             for (int u = 0; u < kIvfWin; ++u) {
                 const int64_t kw = ((int64_t)grp * kIvfWin + u) * 64;
                 if (kw < p.dpad) {
-                    dst[2 * u] = *reinterpret_cast<const ivf_bf16x8 *>(rp + (kw >> 5) * 512);
-                    dst[2 * u + 1] = *reinterpret_cast<const ivf_bf16x8 *>(rp + ((kw >> 5) + 1) * 512);
+                    dst[2 * u] = ldp(rp + (kw >> 5) * 512);
+                    dst[2 * u + 1] = ldp(rp + ((kw >> 5) + 1) * 512);
                 }
             }
         };
@@ -926,37 +934,45 @@ void launch_ivf_plan(const IvfParams &p, hipStream_t s) {
     hipLaunchKernelGGL(k_plan_queries, dim3(1), dim3(kPlanThreads), 0, s, p);
 }
 
-template <int QB>
+template <int QB, bool NTL>
 static void ivf_scan_t(const IvfParams &p, int metric, int grid, hipStream_t s) {
     const size_t lds = (size_t)16 * QB * (2 * p.dpad + 16);
     if (lds > 65536) {  // 64-query tiles of wide rows: opt in to more than 64 KiB of LDS
-        MQVS_HIP(hipFuncSetAttribute((const void *)k_ivf_scan<MQVS_METRIC_L2, QB>,
+        MQVS_HIP(hipFuncSetAttribute((const void *)k_ivf_scan<MQVS_METRIC_L2, QB, NTL>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        MQVS_HIP(hipFuncSetAttribute((const void *)k_ivf_scan<MQVS_METRIC_IP, QB>,
+        MQVS_HIP(hipFuncSetAttribute((const void *)k_ivf_scan<MQVS_METRIC_IP, QB, NTL>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-        MQVS_HIP(hipFuncSetAttribute((const void *)k_ivf_scan<MQVS_METRIC_COSINE, QB>,
+        MQVS_HIP(hipFuncSetAttribute((const void *)k_ivf_scan<MQVS_METRIC_COSINE, QB, NTL>,
                                      hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
     }
     switch (metric) {
         case MQVS_METRIC_L2:
-            hipLaunchKernelGGL((k_ivf_scan<MQVS_METRIC_L2, QB>), dim3(grid), dim3(256), lds, s, p);
+            hipLaunchKernelGGL((k_ivf_scan<MQVS_METRIC_L2, QB, NTL>), dim3(grid), dim3(256), lds, s, p);
             break;
         case MQVS_METRIC_IP:
-            hipLaunchKernelGGL((k_ivf_scan<MQVS_METRIC_IP, QB>), dim3(grid), dim3(256), lds, s, p);
+            hipLaunchKernelGGL((k_ivf_scan<MQVS_METRIC_IP, QB, NTL>), dim3(grid), dim3(256), lds, s, p);
             break;
         default:
-            hipLaunchKernelGGL((k_ivf_scan<MQVS_METRIC_COSINE, QB>), dim3(grid), dim3(256), lds, s, p);
+            hipLaunchKernelGGL((k_ivf_scan<MQVS_METRIC_COSINE, QB, NTL>), dim3(grid), dim3(256), lds, s, p);
             break;
     }
 }
 
-void launch_ivf_scan(const IvfParams &p, int metric, int grid, hipStream_t s) {
+template <bool NTL>
+static void ivf_scan_nt(const IvfParams &p, int metric, int grid, hipStream_t s) {
     if (p.qg == 64)
-        ivf_scan_t<4>(p, metric, grid, s);
+        ivf_scan_t<4, NTL>(p, metric, grid, s);
     else if (p.qg == 32)
-        ivf_scan_t<2>(p, metric, grid, s);
+        ivf_scan_t<2, NTL>(p, metric, grid, s);
     else
-        ivf_scan_t<1>(p, metric, grid, s);
+        ivf_scan_t<1, NTL>(p, metric, grid, s);
+}
+
+void launch_ivf_scan(const IvfParams &p, int metric, int grid, hipStream_t s) {
+    if (tune_int("MQVS_IVF_NT", 1) == 1)
+        ivf_scan_nt<true>(p, metric, grid, s);
+    else
+        ivf_scan_nt<false>(p, metric, grid, s);
 }
 
 void launch_ivf_select(const Cand *cand, const int64_t *qstart, int nq, int R, int metric, int64_t *out_rows,
