@@ -1086,7 +1086,12 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
                                                              int Tcap, int nprobe, const float *q, int64_t qld,
                                                              const float *cent, const float *cnorm, int64_t ncent,
                                                              int d, const float *bq, const float *qnorms,
-                                                             int gs_log2, int64_t *probes) {
+                                                             int gs_log2, int64_t *probes, int trace) {
+    // (measurement build: trace = 1 prints phase timestamps of three workgroups)
+    const bool tr = kDebugTuning && trace && threadIdx.x == 0 &&
+                    (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2 || blockIdx.x == gridDim.x - 1);
+    uint64_t ts[6] = {0, 0, 0, 0, 0, 0};
+    if (tr) ts[0] = wall_clock64();
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh[4];
     __shared__ int s_grp[kCoarsePickMaxT];
@@ -1107,6 +1112,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
         for_each_f4(row, ngroups, [&](int64_t i, float v) { keys[i] = okey<METRIC>(v); });
         __syncthreads();
     }
+    if (tr) ts[1] = wall_clock64();
     auto keyof = [&](int64_t i) { return STAGED ? keys[i] : okey<METRIC>(row[i]); };
     // (the core's T groups come straight from the select for T <= kSelSmallK)
     uint64_t tpair = ~0ull;  // the T-th (key << 32 | group)
@@ -1124,6 +1130,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
         s_knp = 0xFFFFFFFFu;
     }
     __syncthreads();
+    if (tr) ts[2] = wall_clock64();
     // the groups whose key passes take(key, group), appended to s_grp (up to Tcap)
     auto collect = [&](auto take) {
         for (int64_t i = t; i < ngroups; i += SEL_THREADS) {
@@ -1220,6 +1227,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
     }
     const int ng0 = min(s_ng, Tcap);
     score(0, GS * ng0);
+    if (tr) ts[3] = wall_clock64();
     int ng = ng0;
     // 2. extras (needs the bound and a full core; fewer than T valid groups:
     // every group is in the core already)
@@ -1264,6 +1272,14 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
     }
     const int M = GS * ng;
     __syncthreads();
+    if (tr) ts[4] = wall_clock64();
+    auto trace_out = [&]() {
+        if (tr)
+            printf("pick q %d ng0 %d ng %d stage %llu select %llu core %llu extras %llu place %llu (x10ns)\n", qi,
+                   ng0, ng, (unsigned long long)(ts[1] - ts[0]), (unsigned long long)(ts[2] - ts[1]),
+                   (unsigned long long)(ts[3] - ts[2]), (unsigned long long)(ts[4] - ts[3]),
+                   (unsigned long long)(wall_clock64() - ts[4]));
+    };
     const int nvalid = s_valid;
     if (M <= 256) {
         // rank counting: valid records are unique (key, centroid), so each
@@ -1276,6 +1292,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
             if (rank < nprobe) probes[(int64_t)qi * nprobe + rank] = (int64_t)e.y;
         }
         for (int j = nvalid + t; j < nprobe; j += SEL_THREADS) probes[(int64_t)qi * nprobe + j] = -1;
+        trace_out();
         return;
     }
     int N = 1;
@@ -1287,6 +1304,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
         const uint4 e = j < M ? recs[j] : uint4{0xFFFFFFFFu, 0xFFFFFFFFu, 0u, 0u};
         probes[(int64_t)qi * nprobe + j] = e.x == 0xFFFFFFFFu ? -1 : (int64_t)e.y;
     }
+    trace_out();
 }
 
 void launch_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T, int nprobe, int metric,
@@ -1295,9 +1313,10 @@ void launch_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T, 
     if (nq <= 0) return;
     // room for the groups within the bound of the T-th (near-ties)
     const int Tcap = std::min(kCoarsePickMaxT, T + std::max(T, 8));
+    const int trace = tune_int("MQVS_PICK_TRACE", 0);
 #define MQVS_PICK(M, ST)                                                                                         \
     hipLaunchKernelGGL((k_coarse_pick<M, ST>), dim3(nq), dim3(SEL_THREADS), lds, s, gmax, gld, ngroups, T, Tcap, \
-                       nprobe, q, qld, cent, cnorm, ncent, d, bq, qnorms, gs_log2, probes)
+                       nprobe, q, qld, cent, cnorm, ncent, d, bq, qnorms, gs_log2, probes, trace)
     const bool staged = ngroups <= kPickStage;
     size_t nr = 1;
     while (nr < ((size_t)1 << gs_log2) * Tcap) nr <<= 1;
