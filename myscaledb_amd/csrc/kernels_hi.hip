@@ -388,16 +388,21 @@ __global__ __launch_bounds__(256 * WQ) void k_scan_hi(ScanParams p) {
 // into the fragment; a block's whole row (nst loads, 24 KiB at d = 768) is in
 // flight while the previous block feeds the MFMAs.  The query tile (NQB blocks
 // of 16 queries, every stage's B fragment: 4 VGPRs each) stays in registers.
-template <int METRIC, bool PROBE, int NQB, int NST, bool NT = false>
+// NBLK: row blocks per wave -- 4 (256-row tiles), or 1 (kBfRowsSmall-row
+// tiles: short scans such as a few queries' probe, where 256-row tiles leave
+// most CUs idle and each wave's four blocks in a row set the time)
+template <int METRIC, bool PROBE, int NQB, int NST, bool NT = false, int NBLK = 4>
 __global__ __launch_bounds__(256) void k_scan_hi_reg(ScanParams p) {
-    constexpr int RT = kBfRows;
+    constexpr int RT = 64 * NBLK;
     const int64_t ti = blockIdx.x / p.num_qblocks;
     const int qb = (int)(blockIdx.x % p.num_qblocks);
     if (ti >= p.tiles) return;
     int64_t r0, r1, chunk;
     tile_range(p, ti, r0, r1, chunk);
     if (r0 >= r1) return;
-    const int ord = chunk_ordinal(p, chunk);
+    // (a gathered chunk run is padded to whole 256-row tiles: a shorter tile
+    // may hold padding only -- no row, as an unsearched chunk)
+    const int ord = (NBLK < 4 && p.row_list && p.row_list[r0] < 0) ? -1 : chunk_ordinal(p, chunk);
     const int t = threadIdx.x, lane = t & 63, w = t >> 6;
     const int l16 = lane & 15, c = lane >> 4;
     const int q0 = qb * 16 * NQB;
@@ -447,9 +452,9 @@ __global__ __launch_bounds__(256) void k_scan_hi_reg(ScanParams p) {
     };
     load(0, w);
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < NBLK; ++i) {
         const int rb = w + 4 * i;
-        if (i + 1 < 4) load((i + 1) & 1, rb + 4);
+        if (i + 1 < NBLK) load((i + 1) & 1, rb + 4);
         f32x4 acc[NQB];
 #pragma unroll
         for (int jb = 0; jb < NQB; ++jb) acc[jb] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -486,7 +491,10 @@ static void launch_hi_reg(ScanParams p, hipStream_t s) {
     switch (p.dpad / HI_K) {
 #define MQVS_HI_REG(N_)                                                                                        \
     case N_:                                                                                                   \
-        if (nt)                                                                                                \
+        if (p.tile_rows == kBfRowsSmall)                                                                       \
+            hipLaunchKernelGGL((k_scan_hi_reg<METRIC, PROBE, NQB, N_, true, 1>), dim3((unsigned)grid), dim3(256), \
+                               0, s, p);                                                                       \
+        else if (nt)                                                                                           \
             hipLaunchKernelGGL((k_scan_hi_reg<METRIC, PROBE, NQB, N_, true>), dim3((unsigned)grid), dim3(256), 0, s, \
                                p);                                                                             \
         else                                                                                                   \
@@ -502,6 +510,16 @@ static void launch_hi_reg(ScanParams p, hipStream_t s) {
 
 // dpad (d rounded to 64) of the register kernel's builds
 constexpr int kHiRegMaxDpad = 24 * HI_K;
+
+// A scan of nq queries that launch_scan_hi runs with k_scan_hi_reg<NQB = 1>,
+// which also takes kBfRowsSmall-row tiles (PROBE scans always reach it; main
+// scans when no tuned or batch kernel takes them first)
+bool scan_hi_small_tiles_ok(int nq, int64_t dpad) {
+    const char *reg = tune_env("MQVS_HI_REG");
+    const bool use_reg = !(reg && reg[0] == '0');
+    return use_reg && tune_int("MQVS_HI_SMALL_TILES", 1) == 1 && nq <= 16 && dpad <= kHiRegMaxDpad &&
+           dpad % (2 * HI_K) == 0 && dpad >= 2 * HI_K;
+}
 
 template <int METRIC, bool PROBE, int WQ, int QB, int NBUF, int PP = 0, int DIAG = 0>
 static void launch_hi_shape(ScanParams p, hipStream_t s) {

@@ -510,13 +510,16 @@ static Range make_range(int64_t b, int64_t e, int64_t tile_rows, int64_t chunk_r
 
 enum ScanKind { kScanSmall = 0, kScanMfma32 = 1, kScanBf16 = 2 };
 
-static void run_scan(ScanParams p, const Range &r, int kind, int metric, bool probe, hipStream_t st) {
+// tile_rows: the range's tile length when not the kind's (kBfRowsSmall: a
+// bf16 scan that scan_hi_small_tiles_ok admits)
+static void run_scan(ScanParams p, const Range &r, int kind, int metric, bool probe, hipStream_t st,
+                     int64_t tile_rows = 0) {
     if (r.tiles <= 0) return;
     p.row_begin = r.begin;
     p.row_end = r.end;
     p.tiles = r.tiles;
     p.tiles_per_chunk = r.tiles_per_chunk;
-    p.tile_rows = kind == kScanSmall ? kSmallRows : kind == kScanBf16 ? kBfRows : kMfmaRows;
+    p.tile_rows = tile_rows > 0 ? tile_rows : kind == kScanSmall ? kSmallRows : kind == kScanBf16 ? kBfRows : kMfmaRows;
     if (kind == kScanMfma32)
         launch_scan_mfma(p, metric, probe, st);
     else if (kind == kScanBf16)
@@ -996,7 +999,16 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         if (P > scan_n) P = scan_n;
     }
 
-    const Range pr = make_range(0, P, tile_rows, seg->granule, aligned);
+    // the dense probe of a few queries in kBfRowsSmall-row tiles: 4x the
+    // workgroups (a 16384-position probe is 64 tiles of 256 -- a quarter of
+    // the CUs, each wave walking four blocks in a row).  Gathered probes at
+    // nq <= 16: 34 -> 17 us (1 % of 50M rows, nq 1: 0.447 -> 0.431 ms wall);
+    // contiguous ones only at nq <= 2 (cosine 10M, nq 1: 15 -> 12 us; nq 16:
+    // 23 -> 27 us), profiles/r05/small_tiles/
+    const int64_t ptile =
+        (kind == kScanBf16 && (row_list || nq <= 2) && scan_hi_small_tiles_ok(nq, seg->dpad)) ? kBfRowsSmall
+                                                                                             : tile_rows;
+    const Range pr = make_range(0, P, ptile, seg->granule, aligned);
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[5], s));
     (void)take_batch_kernel_flag();
     // The batch probe (kernels_p4.hip PROBE): the batch kernel over the probe
@@ -1030,7 +1042,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         probe = (float *)ws.get(ws.probe, sizeof(float) * (size_t)nq * P);
         p.probe = probe;
         p.probe_ld = P;
-        run_scan(p, pr, kind, metric, true, s);
+        run_scan(p, pr, kind, metric, true, s, ptile);
     }
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[1], s));
     if (kind == kScanBf16)

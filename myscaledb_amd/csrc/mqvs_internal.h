@@ -53,6 +53,7 @@ constexpr int kSmallRows = 256;      // rows per tile, VALU scan
 constexpr int kMfmaRows = 128;       // rows per tile, MFMA scan
 constexpr int kMfmaQ = 128;          // queries per tile, MFMA scan
 constexpr int kBfRows = 256;         // rows per tile, bf16 pre-filter scans (kernels_hi.hip)
+constexpr int kBfRowsSmall = 64;     // short tiles of k_scan_hi_reg (scan_hi_small_tiles_ok)
 // Internal metric id: raw faiss inner product (knn_inner_product: every
 // ip > -FLT_MAX enters the heap), used by mqvs_knn_raw only.  The operator
 // path (mqvs_search) applies searchWrapper's FLT_MIN cut instead.
@@ -380,6 +381,7 @@ void launch_query_bound(const ScanParams &p, int metric, const float *ynorm_max,
 void launch_to_hi(const float *src, int64_t rows, int d, int64_t src_stride, int64_t dpad, int64_t vgroup,
                   int64_t vpad, uint16_t *hi, float *rec, float *maxrec, hipStream_t s);
 void launch_scan_hi(const ScanParams &p, int metric, bool probe, hipStream_t s);
+bool scan_hi_small_tiles_ok(int nq, int64_t dpad);
 // batch APPEND scan at one wave per SIMD (kernels_p4.hip): false when the
 // scan's shape is not served (gather lists, chunk-ordinal tables, no queue)
 bool launch_scan_p4(const ScanParams &p, int metric, hipStream_t s);
