@@ -1068,11 +1068,21 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         // at k = nprobe, used to run 7 segments of 2..64 tiles)
         int64_t b = bprobe ? 0 : P, seg_rows = std::max<int64_t>({tune.first * P, align, kMinSegRows});
         int segs = 0;
+        // dense gathered lists (L2 / IP) at nq <= 16: segments of at most
+        // 2^19 positions in kBfRowsSmall-row tiles too (a gathered row costs
+        // a list lookup before its loads; 4x the waves in flight hide it):
+        // 1 % of 50M rows, nq 1: 0.420 -> 0.404 ms.  Not for cosine lists,
+        // padded per chunk to whole 256-row tiles (4x the workgroups, most
+        // of them padding: 1 %, nq 1 0.50 -> 0.68 ms), nor long segments
+        // (L2 50 %, nq 16: 8.79 -> 9.01 ms); profiles/r05/small_tiles/main_ab.jsonl
+        const bool small_main = kind == kScanBf16 && row_list && !cos &&
+                                tune_int("MQVS_HI_SMALL_MAIN", 1) == 1 && scan_hi_small_tiles_ok(nq, seg->dpad);
         while (b < scan_n) {
             const int64_t e = std::min(scan_n, round_up(b + seg_rows + (segs == 0 && bprobe ? P : 0), align));
             const bool tev = timing && 2 * segs + 1 < Workspace::kSegEv;
             if (tev) MQVS_HIP(hipEventRecord(ws.seg_ev[2 * segs], s));
-            run_scan(p, make_range(b, e, tile_rows, seg->granule, aligned), kind, metric, false, s);
+            const int64_t mtile = (small_main && e - b <= (int64_t)1 << 19) ? kBfRowsSmall : tile_rows;
+            run_scan(p, make_range(b, e, mtile, seg->granule, aligned), kind, metric, false, s, mtile);
             if (tev) MQVS_HIP(hipEventRecord(ws.seg_ev[2 * segs + 1], s));
             b = e;
             seg_rows *= tune.growth;
