@@ -188,10 +188,19 @@ __global__ __launch_bounds__(kPsThreads) void k_probe_select_wide(const float *p
         tt = widen<METRIC>(okey_bound_value<METRIC>(prefix | 0xFFu), bq[q]);
     if (t == 0) thr[q] = tt;
     if (!cand) return;  // (the batch probe's maxima: threshold only)
+    const int lane = t & 63;
     for_each_f4<kPsThreads>(row, P, [&](int64_t i, float raw) {
         const bool take = (METRIC == MQVS_METRIC_L2) ? (raw <= tt) : (raw >= tt);
+        // one counter atomic per wave and value step (the lanes that take
+        // get consecutive slots)
+        const uint64_t m = __ballot(take);
+        if (m == 0) return;
+        const int leader = __ffsll((long long)m) - 1;
+        int base = 0;
+        if (lane == leader) base = atomicAdd(&cand_count[q], __popcll(m));
+        base = __shfl(base, leader);
         if (take) {
-            const int pos = atomicAdd(&cand_count[q], 1);
+            const int pos = base + __popcll(m & ((1ull << lane) - 1));
             if (pos < cap) {
                 Cand c;
                 c.raw = raw;
