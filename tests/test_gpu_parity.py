@@ -130,6 +130,12 @@ FILTERED = [c for c in PARITY if c[8] is not None] + [
     ("cos_filter_sparse_nq3", 50000, 64, 3, 50, "Cosine", 2, 2048, 0.003, 0.2, 0.1),
     ("ip_filter_sparse_nq30", 50000, 64, 30, 50, "IP", 1, 1000, 0.01, None, 0.0),
     ("l2_filter_mid_nq12", 40000, 96, 12, 100, "L2", 2, 4096, 0.08, 0.1, 0.05),
+    # gathered scans long enough for a probe and several segments: 64-row
+    # tiles for the probe and the short L2 segments, and (cosine) short tiles
+    # that hold chunk padding only
+    ("l2_filter_segments_nq1", 400000, 32, 1, 100, "L2", 1, 8192, 0.3, None, 0.0),
+    ("ip_filter_segments_nq16", 300000, 32, 16, 50, "IP", 1, 4096, 0.2, 0.1, 0.0),
+    ("cos_filter_pad_tiles_nq2", 400000, 32, 2, 50, "Cosine", 1, 8192, 0.1, None, 0.0),
 ]
 
 
