@@ -399,7 +399,7 @@ int mqvs_index_search(mqvs_index_t idx, const float *queries, int32_t nq, int32_
  *   `params` (alpha / nprobe as mqvs_index_search) would probe, in no
  *   guaranteed order, into out_probes[nq][nprobe] (host; nprobe as
  *   mqvs_index_last_stats then reports it; nq x nlist always suffices).
- *   For nprobe <= 62 (the coarse pick) and for indexes of more than 16384
+ *   For nprobe <= 64 (the coarse pick) and for indexes of more than 16384
  *   lists (a FLAT search of the centroids) the lists are the exact top nprobe
  *   by the coarse metric (L2; the raw inner product for IP and cosine parts),
  *   up to fp32 rounding of near ties; otherwise they are ranked by the bf16

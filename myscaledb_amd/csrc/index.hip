@@ -900,15 +900,20 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     // 65536 lists, nq 1000: 1.26 -> 0.67 ms; few lists: the list pass over
     // the centroid chunks (10000 lists: 0.28 ms vs 0.50, the FLAT path's
     // fixed stages dominate; profiles/r03/index)
-    // Default (nprobe <= 62 and the centroid plane present): the batch kernel
+    // Default (nprobe <= 64 and the centroid plane present): the batch kernel
     // scores every (query, centroid) on bf16 and keeps the best of each
-    // 16-centroid group; the nprobe + 2 best groups per query (and any other
+    // 8-centroid group; the nprobe best groups per query (and any other
     // group the bf16 bound cannot rule out) then get exact fp32 values and
     // the nprobe best of those are the probes (k_coarse_pick).  65536 or 39063 lists at nq 1000: one batch-kernel
     // launch and one pick instead of mqvs_search's whole pipeline.
     bool picked = false;
     const int cmode = tune_int("MQVS_IVF_COARSE", 2);
-    if (cmode == 2 && nprobe + 2 <= kCoarsePickMaxT && ix->cent && ix->cent->rows_hi && ix->cent->rows) {
+    // core groups of the pick: nprobe (any T keeps the probes exact; nprobe
+    // + 2 before: the core's 8 (nprobe + 2) centroids scored exactly, vs 8
+    // nprobe now -- mode 3 nprobe 1: 0.505 -> 0.499 ms per batch,
+    // profiles/r05/pick/core_t_ab.jsonl)
+    const int pick_t = std::max(1, nprobe + tune_int("MQVS_PICK_TX", 0));
+    if (cmode == 2 && pick_t <= kCoarsePickMaxT && ix->cent && ix->cent->rows_hi && ix->cent->rows) {
         mqvs_segment *cs = ix->cent;
         const int64_t vpad = rup(nq, 16);
         auto *cq = (uint16_t *)ws.cqhi.get(sizeof(uint16_t) * (size_t)vpad * cs->dpad);
@@ -951,7 +956,7 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
             bp.blas_nq = 1;
             launch_query_bound(bp, ix->coarse_metric, cs->ynorm_max, crec, cs->ynorm_max + 4, cbq, s);
             MQVS_HIP(hipGetLastError());
-            launch_coarse_pick(cp.p4_gmax, gld, (256 / grp) * cp.tiles, nprobe + 2, nprobe, ix->coarse_metric, qvars,
+            launch_coarse_pick(cp.p4_gmax, gld, (256 / grp) * cp.tiles, pick_t, nprobe, ix->coarse_metric, qvars,
                                (int64_t)maxv * qstride, cs->rows, cs->norms, cs->n, d, cbq, qnorms, grp == 8 ? 3 : 4,
                                nq, probes, s);
             MQVS_HIP(hipGetLastError());

@@ -1311,8 +1311,10 @@ void launch_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T, 
                         const float *q, int64_t qld, const float *cent, const float *cnorm, int64_t ncent, int d,
                         const float *bq, const float *qnorms, int gs_log2, int nq, int64_t *probes, hipStream_t s) {
     if (nq <= 0) return;
-    // room for the groups within the bound of the T-th (near-ties)
-    const int Tcap = std::min(kCoarsePickMaxT, T + std::max(T, 8));
+    // room for the groups within the bound of the core's nprobe-th value
+    // (near-ties): as many as a core of nprobe + 2 groups had (a smaller core
+    // leaves more of the near groups to the extras)
+    const int Tcap = std::min(kCoarsePickMaxT, std::max(T, nprobe + 2) + std::max(std::max(T, nprobe + 2), 8));
     const int trace = tune_int("MQVS_PICK_TRACE", 0);
 #define MQVS_PICK(M, ST)                                                                                         \
     hipLaunchKernelGGL((k_coarse_pick<M, ST>), dim3(nq), dim3(SEL_THREADS), lds, s, gmax, gld, ngroups, T, Tcap, \
