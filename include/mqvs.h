@@ -40,7 +40,7 @@
 extern "C" {
 #endif
 
-#define MQVS_ABI_VERSION 3
+#define MQVS_ABI_VERSION 4
 
 /* Metric ids (VICommon.h VIMetric).  L2 / IP / Cosine: Float32 vectors;
  * Hamming / Jaccard: binary vectors (FixedString(N) columns, mqvs_*_binary). */
@@ -387,6 +387,12 @@ int mqvs_index_info(mqvs_index_t idx, mqvs_index_info_t *out);
  * by the approximate bf16 distance (approximate distances), to be re-ranked
  * by mqvs_rerank (the reference's two-stage search). */
 #define MQVS_F_FIRST_STAGE 0x8u
+/* Re-rank every one of the num_reorder candidates.  By default a candidate
+ * whose approximate value is more than twice the query's bf16 bound past the
+ * k-th best approximate value is not re-ranked: its exact value cannot reach
+ * the top k, so the results are the same either way (the flag is for tests
+ * and measurements). */
+#define MQVS_F_RERANK_ALL 0x200u
 int mqvs_index_search(mqvs_index_t idx, const float *queries, int32_t nq, int32_t k, const char *params,
                       const uint8_t *filter, const uint8_t *row_exists, int64_t *out_ids, float *out_dist,
                       uint32_t flags, mqvs_stream_t stream);
@@ -439,6 +445,11 @@ typedef struct {
     int64_t plane_bytes;  /* bf16 plane bytes streamed by the scan */
     int64_t pairs;        /* (query, list) pairs */
     int32_t nq, k, nprobe, num_reorder;
+    int64_t reranked;     /* candidates re-ranked exactly (sum over queries, <= nq x num_reorder): the bf16
+                             bound prunes those that cannot reach the top k (MQVS_F_RERANK_ALL: none) */
+    int32_t pick_overflow;/* queries whose coarse pick found more near-tie centroid groups than its
+                             working set holds and scored them in batches (the probes stay exact) */
+    int32_t reserved;
 } mqvs_index_search_stats;
 int mqvs_index_last_stats(mqvs_index_search_stats *out);
 
@@ -562,13 +573,33 @@ int mqvs_workspace_stats(mqvs_workspace_stats_t *out, int32_t reset_peak);
  * >= 4 GiB defeats the 256 MiB Infinity Cache), best of `reps` timed passes
  * after one warm-up: *gbs = bytes / best time (1e9 B/s), *best_ms (optional). */
 int mqvs_measure_read_bandwidth(size_t bytes, int32_t reps, double *gbs, double *best_ms);
+/* How a calling thread waits for its GPU work (every synchronous call ends
+ * with a wait; a selective PREWHERE search also waits for its selected-row
+ * count).  The reference runs up to 2 x physical cores scans at once
+ * (ScanThreadLimiter.h:25-58, MergeTreeVSManager.cpp:974-975): a thread that
+ * spins for the length of its search holds a host core meanwhile.
+ *   MQVS_WAIT_RUNTIME  hipStreamSynchronize (the HIP runtime's own policy)
+ *   MQVS_WAIT_HYBRID   poll for up to spin_us, then sleep on a blocking-sync
+ *                      event until the work completes (default, 50 us)
+ *   MQVS_WAIT_BLOCK    sleep at once
+ * Results are identical in every mode.  Returns the previous mode;
+ * spin_us < 0 leaves the poll budget unchanged; other modes are
+ * MQVS_ERR_BAD_ARGUMENTS (returned as a negative value: -4). */
+#define MQVS_WAIT_RUNTIME 0
+#define MQVS_WAIT_HYBRID 1
+#define MQVS_WAIT_BLOCK 2
+int mqvs_set_wait_mode(int mode, int spin_us);
 /* Fault drill for a caller's host fallback (on a device error the
  * host runs its CPU path; include/mqvs_vector_index.hpp takes the fallback as
  * a callable): the next `calls` search entry points made by THIS thread --
  * mqvs_search, mqvs_search_ex, mqvs_knn_raw, mqvs_search_binary,
  * mqvs_knn_binary_raw, mqvs_index_search -- return `status` (MQVS_ERR_DEVICE
  * or MQVS_ERR_MEMORY_LIMIT) without touching the device or the outputs.
- * calls = 0 disarms.  Other statuses are MQVS_ERR_BAD_ARGUMENTS. */
+ * calls = 0 disarms.  Other statuses are MQVS_ERR_BAD_ARGUMENTS.
+ * status | MQVS_FAULT_MID_CALL: the fault fires inside a filtered mqvs_search
+ * instead, right after its selected-row count kernel is queued (a device
+ * failure after launches; the next call must not see that call's work). */
+#define MQVS_FAULT_MID_CALL 0x100
 int mqvs_inject_fault(int32_t status, int32_t calls);
 
 #ifdef __cplusplus

@@ -35,6 +35,8 @@ F_EXACT = 0x20
 F_GATHER_NEVER = 0x40
 F_GATHER_ALWAYS = 0x80
 F_TIMING = 0x100
+F_RERANK_ALL = 0x200
+WAIT_RUNTIME, WAIT_HYBRID, WAIT_BLOCK = 0, 1, 2
 
 # Exported C symbols: every one of these is declared in include/mqvs.h.
 SYMBOLS = [
@@ -52,7 +54,7 @@ SYMBOLS = [
     "mqvs_comm_unique_id", "mqvs_comm_init", "mqvs_comm_init_loopback", "mqvs_comm_free", "mqvs_sharded_search", "mqvs_comm_stats",
     "mqvs_index_set_row_ids_map", "mqvs_decoupled_filter",
     "mqvs_cache_create", "mqvs_cache_free", "mqvs_cache_put", "mqvs_cache_acquire", "mqvs_cache_release",
-    "mqvs_cache_remove", "mqvs_cache_stats", "mqvs_inject_fault",
+    "mqvs_cache_remove", "mqvs_cache_stats", "mqvs_inject_fault", "mqvs_set_wait_mode",
 ]
 
 
@@ -95,7 +97,9 @@ class IndexSearchStats(ctypes.Structure):
                 ("values", ctypes.c_int64), ("items", ctypes.c_int64),
                 ("plane_bytes", ctypes.c_int64), ("pairs", ctypes.c_int64),
                 ("nq", ctypes.c_int32), ("k", ctypes.c_int32),
-                ("nprobe", ctypes.c_int32), ("num_reorder", ctypes.c_int32)]
+                ("nprobe", ctypes.c_int32), ("num_reorder", ctypes.c_int32),
+                ("reranked", ctypes.c_int64), ("pick_overflow", ctypes.c_int32),
+                ("reserved", ctypes.c_int32)]
 
 
 def _share_hip_runtime_with_torch():
@@ -151,6 +155,7 @@ def _load(path=LIB_PATH):
         "mqvs_measure_read_bandwidth": ([ctypes.c_size_t, ctypes.c_int32, P, P], ctypes.c_int),
         "mqvs_set_prefilter": ([ctypes.c_int], ctypes.c_int),
         "mqvs_inject_fault": ([I32, I32], ctypes.c_int),
+        "mqvs_set_wait_mode": ([ctypes.c_int, ctypes.c_int], ctypes.c_int),
         "mqvs_index_build": ([P, ctypes.c_char_p, ctypes.c_char_p, P], ctypes.c_int),
         "mqvs_index_free": ([P], ctypes.c_int),
         "mqvs_index_info": ([P, P], ctypes.c_int),
@@ -250,6 +255,15 @@ def workspace_stats(reset_peak=False):
     st = WorkspaceStats()
     check(lib.mqvs_workspace_stats(ctypes.byref(st), 1 if reset_peak else 0))
     return {f: getattr(st, f) for f, _ in WorkspaceStats._fields_}
+
+
+def set_wait_mode(mode, spin_us=-1):
+    """mqvs_set_wait_mode: how calling threads wait for their GPU work
+    (WAIT_RUNTIME / WAIT_HYBRID / WAIT_BLOCK); returns the previous mode."""
+    rc = lib.mqvs_set_wait_mode(int(mode), int(spin_us))
+    if rc < 0:
+        check(-rc)
+    return rc
 
 
 def set_workspace_budget(nbytes):

@@ -53,6 +53,8 @@ struct mqvs_index {
     int32_t *perm = nullptr;       // [npos] row of each position, -1 = padding
     float *pnorm = nullptr;        // [npos] |y|^2
     int64_t *list_off = nullptr;   // [nlist+1]
+    float *yrec = nullptr;         // [kMxRec] maxima over the rows of |bf16(y)|, |y - bf16(y)|, |y| (the
+                                   // re-rank's bound pruning: k_query_bound's segment record)
     // coarse quantizer in the same list layout: the centroids in chunks of
     // kCoarseChunk (every query probes every chunk), bf16 plane + |c|^2
     int64_t cnl = 0, cnpos = 0, cmax = 0;
@@ -105,7 +107,7 @@ struct IndexWorkspace final : WsExt {
     hipStream_t side = nullptr;
     int64_t *host = nullptr;  // pinned: the search's stats [4] and status word (one sync, no staging copies)
     GBuf queries, qvars, qnorms, qmu, qlam, status, qhi, probes, cprobes, filter, exists, rows, out_ids, out_dist,
-        ord, dmap, dwords, pdist, cqhi, gmax, crec, cbq;
+        ord, dmap, dwords, pdist, cqhi, gmax, crec, cbq, craw, ibq;
     ListBufs coarse, fine;
     // WsExt: the owner is between calls (its workspace's `done` event passed:
     // the main stream, which joins the side chain, has drained)
@@ -113,7 +115,8 @@ struct IndexWorkspace final : WsExt {
         if (side) (void)hipStreamSynchronize(side);
         size_t b = 0;
         for (GBuf *x : {&queries, &qvars, &qnorms, &qmu, &qlam, &status, &qhi, &probes, &cprobes, &filter, &exists,
-                        &rows, &out_ids, &out_dist, &ord, &dmap, &dwords, &pdist, &cqhi, &gmax, &crec, &cbq}) {
+                        &rows, &out_ids, &out_dist, &ord, &dmap, &dwords, &pdist, &cqhi, &gmax, &crec, &cbq, &craw,
+                        &ibq}) {
             b += x->cap;
             x->release();
         }
@@ -275,7 +278,8 @@ static void free_index(mqvs_index *ix) {
     if (ix->seg) (void)hipSetDevice(ix->seg->device);
     if (ix->cent) segment_release(ix->cent);
     for (void *q : {(void *)ix->plane, (void *)ix->perm, (void *)ix->pnorm, (void *)ix->list_off, (void *)ix->cplane,
-                    (void *)ix->cperm, (void *)ix->cpnorm, (void *)ix->clist_off, (void *)ix->row_ids_map})
+                    (void *)ix->cperm, (void *)ix->cpnorm, (void *)ix->clist_off, (void *)ix->row_ids_map,
+                    (void *)ix->yrec})
         if (q) (void)hipFree(q);
     if (cur >= 0) (void)hipSetDevice(cur);
     delete ix;
@@ -463,6 +467,13 @@ static mqvs_index *build_impl(mqvs_segment *seg, const char *index_type, const c
             MQVS_HIP(hipMemcpyAsync(ix->perm, order.data(), sizeof(int32_t) * ix->npos, hipMemcpyHostToDevice, s));
         MQVS_HIP(hipMemcpyAsync(ix->list_off, off.data(), sizeof(int64_t) * (Lc + 1), hipMemcpyHostToDevice, s));
         launch_ivf_pack(seg->rows, seg->norms, d, ix->perm, ix->npos, ix->dpad, ix->plane, ix->pnorm, s);
+        MQVS_HIP(hipGetLastError());
+        // the plane's norm maxima (the same bf16 rounding as k_ivf_pack; empty
+        // arrays' FLT_MAX rows make them infinite, which turns the re-rank's
+        // bound pruning off)
+        ix->yrec = dalloc<float>(ix, kMxRec);
+        MQVS_HIP(hipMemsetAsync(ix->yrec, 0, sizeof(float) * kMxRec, s));
+        launch_to_hi(seg->rows, n, d, d, ix->dpad, 1, rup(n, 16), nullptr, nullptr, ix->yrec, s);
         MQVS_HIP(hipGetLastError());
         // ---- coarse quantizer as lists of kCoarseChunk centroids
         {
@@ -671,7 +682,8 @@ static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, c
                       const int64_t *list_off, int64_t nlist, int64_t npos, int64_t max_list, int64_t dpad, int metric,
                       const uint16_t *qhi, const float *qnorm, int nq, const int64_t *probes, int nprobe,
                       const uint8_t *filter, const uint8_t *exists, int R, int64_t *out_rows, int64_t id_offset,
-                      float *out_approx, hipEvent_t *ev, hipStream_t s, bool dense = false) {
+                      float *out_approx, hipEvent_t *ev, hipStream_t s, bool dense = false,
+                      float *out_raw = nullptr) {
     const int64_t E = (int64_t)nq * nprobe;
     IvfParams p{};
     p.plane = plane;
@@ -737,7 +749,7 @@ static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, c
     const int64_t expect = dense ? npos : (int64_t)((double)nprobe * npos / std::max<int64_t>(nlist, 1) * 1.5);
     // R above kSortCap: the select sorts through 2 R records of scratch per query
     uint4 *gscr = R > kSortCap ? (uint4 *)b.large.get(sizeof(uint4) * 2 * (size_t)R * nq) : nullptr;
-    launch_ivf_select(p.cand, p.qstart, nq, R, metric, out_rows, id_offset, out_approx, expect, s, gscr);
+    launch_ivf_select(p.cand, p.qstart, nq, R, metric, out_rows, id_offset, out_approx, expect, s, gscr, out_raw);
     MQVS_HIP(hipGetLastError());
     if (ev) MQVS_HIP(hipEventRecord(ev[4], s));
 }
@@ -862,8 +874,10 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     float *qnorms = (float *)ws.qnorms.get(sizeof(float) * nq);
     int *qmu = (int *)ws.qmu.get(sizeof(int) * nq);
     int *qlam = (int *)ws.qlam.get(sizeof(int) * nq);
-    int *status = (int *)ws.status.get(sizeof(int) * 4);
-    launch_fill2(reinterpret_cast<uint32_t *>(status), 4, 0u, nullptr, 0, 0u, s);
+    // [status 4 ints][pick overflow queries, candidates re-ranked: 2 x u64]
+    int *status = (int *)ws.status.get(sizeof(int) * 8);
+    launch_fill2(reinterpret_cast<uint32_t *>(status), 8, 0u, nullptr, 0, 0u, s);
+    auto *istat = reinterpret_cast<unsigned long long *>(status + 4);
     // Cosine: only variant 0 is needed before the exact re-rank (coarse step,
     // list scan), so the rest of the chain -- a sequential fp32 sum per
     // normalisation, up to kMaxVariants of them: 60-130 us at nq 1000 -- runs
@@ -913,7 +927,9 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     // nprobe now -- mode 3 nprobe 1: 0.505 -> 0.499 ms per batch,
     // profiles/r05/pick/core_t_ab.jsonl)
     const int pick_t = std::max(1, nprobe + tune_int("MQVS_PICK_TX", 0));
-    if (cmode == 2 && pick_t <= kCoarsePickMaxT && ix->cent && ix->cent->rows_hi && ix->cent->rows) {
+    float *qrec0 = nullptr;  // variant 0's norm records (the pick's bound; the re-rank pruning's)
+    if (cmode == 2 && pick_t <= kCoarsePickMaxT && nprobe <= kCoarsePickMaxT && ix->cent && ix->cent->rows_hi &&
+        ix->cent->rows) {
         mqvs_segment *cs = ix->cent;
         const int64_t vpad = rup(nq, 16);
         auto *cq = (uint16_t *)ws.cqhi.get(sizeof(uint16_t) * (size_t)vpad * cs->dpad);
@@ -923,6 +939,7 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
         // (with the variants' norm records: the pick's bf16 bound)
         float *crec = (float *)ws.crec.get(sizeof(float) * kMxRec * (size_t)nq);
         launch_to_hi(qvars, nq, d, (int64_t)maxv * qstride, cs->dpad, 1, vpad, cq, crec, nullptr, s);
+        qrec0 = crec;
         MQVS_HIP(hipGetLastError());
         ScanParams cp{};
         cp.rows_hi = cs->rows_hi;
@@ -958,7 +975,7 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
             MQVS_HIP(hipGetLastError());
             launch_coarse_pick(cp.p4_gmax, gld, (256 / grp) * cp.tiles, pick_t, nprobe, ix->coarse_metric, qvars,
                                (int64_t)maxv * qstride, cs->rows, cs->norms, cs->n, d, cbq, qnorms, grp == 8 ? 3 : 4,
-                               nq, probes, s);
+                               nq, probes, istat, s);
             MQVS_HIP(hipGetLastError());
             picked = true;
         }
@@ -977,8 +994,31 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     if (t_probes_out) {
         // mqvs_index_probes: the coarse step's lists, nothing after it
         MQVS_HIP(hipMemcpyAsync(t_probes_out, probes, sizeof(int64_t) * (size_t)nq * nprobe, hipMemcpyDeviceToHost, s));
-        MQVS_HIP(hipStreamSynchronize(s));
+        MQVS_HIP(hipMemcpyAsync(ws.host + 6, istat, 2 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
+        host_wait(s);
+        g_istats.pick_overflow = (int32_t)ws.host[6];
         return;
+    }
+    // ---- the re-rank's bound pruning (the candidates that cannot reach the
+    // exact top k are not re-ranked; same output): per query, the bound on
+    // |bf16 list-scan value - exact value| for query variant 0
+    const bool prune = !first_stage && !(flags & MQVS_F_RERANK_ALL) && ix->yrec && k < R;
+    float *craw = nullptr, *ibq = nullptr;
+    if (prune) {
+        craw = (float *)ws.craw.get(sizeof(float) * (size_t)nq * R);
+        ibq = (float *)ws.ibq.get(sizeof(float) * (size_t)nq);
+        if (!qrec0) {
+            qrec0 = (float *)ws.crec.get(sizeof(float) * kMxRec * (size_t)nq);
+            launch_to_hi(qvars, nq, d, (int64_t)maxv * qstride, ix->dpad, 1, rup(nq, 16), nullptr, qrec0, nullptr, s);
+        }
+        ScanParams bp{};
+        bp.nq = nq;
+        bp.d = d;
+        bp.maxv = 1;
+        bp.qnorms = qnorms;
+        bp.blas_nq = fnq;
+        launch_query_bound(bp, ix->metric, seg->ynorm_max, qrec0, ix->yrec, ibq, s);
+        MQVS_HIP(hipGetLastError());
     }
     if (split && late_fork) fork_chain();
 
@@ -993,7 +1033,7 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
         int64_t *crow = (int64_t *)ws.rows.get(sizeof(int64_t) * (size_t)nq * R);
         list_pass(ws.fine, ix->plane, ix->perm, ix->pnorm, ix->list_off, ix->nlist, ix->npos, ix->max_list, ix->dpad,
                   ix->metric, qhi, qnorms, nq, probes, nprobe, dfilter, dexists, R, crow, 0, nullptr,
-                  tev ? ws.ev : nullptr, s);
+                  tev ? ws.ev : nullptr, s, false, craw);
         // ---- exact re-rank (needs the whole variant chain)
         if (split) {
             MQVS_HIP(hipStreamWaitEvent(s, ws.join, 0));
@@ -1028,7 +1068,14 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
         rp.filter = nullptr;  // the scan applied the filter; candidates pass it
         rp.nonempty = seg->nonempty_bits;
         uint4 *rscr = R > kSortCap ? (uint4 *)ws.fine.large.get(sizeof(uint4) * 2 * (size_t)R * nq) : nullptr;
-        launch_rerank_ids(rp, ix->metric, crow, R, k, seg->row_offset, dids, ddist, rscr, s);
+        RerankPrune pr{};
+        pr.count = istat + 1;
+        if (prune) {
+            pr.raw = craw;
+            pr.bq = ibq;
+            pr.ymax = seg->ynorm_max;
+        }
+        launch_rerank_ids(rp, ix->metric, crow, R, k, seg->row_offset, dids, ddist, rscr, s, pr);
         MQVS_HIP(hipGetLastError());
         MQVS_HIP(hipEventRecord(ws.ev[5], s));
     }
@@ -1045,9 +1092,9 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     }
     int64_t *hs = ws.host;
     int *hst = reinterpret_cast<int *>(ws.host + 4);
-    launch_words_to_host(dstats, 4, status, 1, hs, hst, s);
+    launch_words_to_host(dstats, 4, status, 8, hs, hst, s);
     MQVS_HIP(hipGetLastError());
-    MQVS_HIP(hipStreamSynchronize(s));
+    host_wait(s);
     const int hstatus = *hst;
     if (hstatus && !first_stage && ords > maxv) {
         const int want = (int)std::min<int64_t>(ords, kMaxVariantsCap);
@@ -1063,12 +1110,14 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
         if (ix->row_ids_map) launch_map_ids(dids, (int64_t)nq * k, ix->row_ids_map, s);
         MQVS_HIP(hipMemcpyAsync(out_ids, dids, sizeof(int64_t) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
         MQVS_HIP(hipMemcpyAsync(out_dist, ddist, sizeof(float) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
-        MQVS_HIP(hipStreamSynchronize(s));
+        host_wait(s);
     }
     st.values = hs[0];
     st.items = hs[1];
     st.plane_bytes = hs[2];
     st.pairs = hs[3];
+    st.pick_overflow = (int32_t)hs[6];  // (istat, copied with the status words)
+    st.reranked = hs[7];
     float t[5] = {0, 0, 0, 0, 0}, tot = 0;
     if (tev) {
         for (int i = 0; i < 5; ++i) MQVS_HIP(hipEventElapsedTime(&t[i], ws.ev[i], ws.ev[i + 1]));
@@ -1218,7 +1267,7 @@ int mqvs_decoupled_filter(const uint8_t *new_filter, int64_t new_rows, const uin
                                 old_rows, s);
         MQVS_HIP(hipGetLastError());
         MQVS_HIP(hipMemcpyAsync(old_filter, words, ob, devp ? hipMemcpyDeviceToDevice : hipMemcpyDeviceToHost, s));
-        if (!(devp && (flags & MQVS_F_ASYNC))) MQVS_HIP(hipStreamSynchronize(s));
+        if (!(devp && (flags & MQVS_F_ASYNC))) host_wait(s);
     });
 }
 

@@ -65,14 +65,14 @@ __global__ __launch_bounds__(256) void k_to_hi(const float *src, int64_t rows, i
     for (int64_t v = (int64_t)blockIdx.x * 4 + w; v < rows; v += (int64_t)gridDim.x * 4) {
         const float *x = src + v * sstride;
         const int64_t u = (v % vgroup) * vpad + v / vgroup;
-        uint16_t *hu = hi + (u >> 4) * nb * 512 + plane_vec_off((uint32_t)(u & 15)) / 2;
+        uint16_t *hu = hi ? hi + (u >> 4) * nb * 512 + plane_vec_off((uint32_t)(u & 15)) / 2 : nullptr;  // (null: records only)
         double nx = 0, nh = 0, nr = 0;
         for (int64_t i = lane; i < dpad; i += 64) {
             const float xv = i < d ? x[i] : 0.f;
             const uint16_t hb = f32_to_bf16_rn(xv);
             const float hv = __builtin_bit_cast(float, (uint32_t)hb << 16);
             const float rv = xv - hv;  // exact
-            hu[plane_step_off((uint32_t)(i >> 5)) / 2 + (i & 31)] = hb;
+            if (hi) hu[plane_step_off((uint32_t)(i >> 5)) / 2 + (i & 31)] = hb;
             nx += (double)xv * xv;
             nh += (double)hv * hv;
             nr += (double)rv * rv;

@@ -620,7 +620,7 @@ constexpr int kTieCap = 64;  // <= every NT the kernel is launched with
 template <int METRIC, int NT, bool LARGE = false>
 __global__ __launch_bounds__(NT) void k_ivf_select(const Cand *cand, const int64_t *qstart, int R,
                                                    int64_t *out_rows, int64_t id_offset, float *out_approx,
-                                                   int keycap, uint4 *gscr) {
+                                                   int keycap, uint4 *gscr, float *out_raw) {
     // pow2 >= R records (LARGE: kSortCap, the sort runs), then the key cache
     extern __shared__ __attribute__((aligned(16))) uint4 recs[];
     __shared__ uint4 ties[kTieCap];
@@ -772,6 +772,8 @@ __global__ __launch_bounds__(NT) void k_ivf_select(const Cand *cand, const int64
         } else {
             out_rows[(int64_t)q * R + i] = ok ? (int64_t)r.y : -1;
         }
+        // (the re-rank's bound pruning: the raw approximate values, NaN past the valid ones)
+        if (out_raw) out_raw[(int64_t)q * R + i] = ok ? __builtin_bit_cast(float, r.z) : __builtin_nanf("");
     }
 }
 
@@ -976,8 +978,9 @@ void launch_ivf_scan(const IvfParams &p, int metric, int grid, hipStream_t s) {
 }
 
 void launch_ivf_select(const Cand *cand, const int64_t *qstart, int nq, int R, int metric, int64_t *out_rows,
-                       int64_t id_offset, float *out_approx, int64_t expect_len, hipStream_t s, uint4 *gscr) {
-    if (R <= 16 && !out_approx) {
+                       int64_t id_offset, float *out_approx, int64_t expect_len, hipStream_t s, uint4 *gscr,
+                       float *out_raw) {
+    if (R <= 16 && !out_approx && !out_raw) {
         const dim3 grid((unsigned)((nq + 3) / 4));
 #define MQVS_SMALL(M, RM_) \
     hipLaunchKernelGGL((k_ivf_select_small<M, RM_>), grid, dim3(256), 0, s, cand, qstart, nq, R, out_rows, id_offset, \
@@ -1013,13 +1016,13 @@ void launch_ivf_select(const Cand *cand, const int64_t *qstart, int nq, int R, i
     do {                                                                                                            \
         if (large)                                                                                                  \
             hipLaunchKernelGGL((k_ivf_select<M, SEL_THREADS, true>), dim3(nq), dim3(SEL_THREADS), lds, s, cand,     \
-                               qstart, R, out_rows, id_offset, out_approx, keycap, gscr);                           \
+                               qstart, R, out_rows, id_offset, out_approx, keycap, gscr, out_raw);                  \
         else if (wide)                                                                                              \
             hipLaunchKernelGGL((k_ivf_select<M, 1024>), dim3(nq), dim3(1024), lds, s, cand, qstart, R, out_rows,    \
-                               id_offset, out_approx, keycap, nullptr);                                             \
+                               id_offset, out_approx, keycap, nullptr, out_raw);                                    \
         else                                                                                                        \
             hipLaunchKernelGGL((k_ivf_select<M, SEL_THREADS>), dim3(nq), dim3(SEL_THREADS), lds, s, cand, qstart, R, \
-                               out_rows, id_offset, out_approx, keycap, nullptr);                                   \
+                               out_rows, id_offset, out_approx, keycap, nullptr, out_raw);                          \
     } while (0)
     switch (metric) {
         case MQVS_METRIC_L2: MQVS_SEL(MQVS_METRIC_L2); break;
@@ -1062,8 +1065,13 @@ void launch_centroid_mean(const float *rows, int d, const int32_t *order, const 
 //  2. extras: a group outside the core can hold a centroid better than v only
 //     if its maximum is within bq of v (its centroids' exact values are at
 //     most maximum + bq); those groups are scored too, up to Tcap groups in
-//     all, beyond which near-ties among more than Tcap groups are cut (counted
-//     nowhere: the probes are then approximate, as any IVF's).
+//     all.
+//  3. overflow (more than Tcap groups in the core's ties or within bq of v:
+//     near-ties, e.g. a query about equidistant from many centroids): every
+//     group that passes is scored, in batches of Tcap taken in group order by
+//     an ordered compaction, each batch merged into a running top-nprobe; the
+//     query is counted in *ovf (mqvs_index_search_stats.pick_overflow).  The
+//     probes stay the exact top-nprobe; only the time grows.
 // Step 2 compares with the core's exact v, not with the T-th approximate
 // maximum: usually no group passes (round 5 first took every group within
 // 2 bq of the T-th maximum -- 8 more groups per query at nprobe 1, the pick
@@ -1080,13 +1088,15 @@ void launch_centroid_mean(const float *rows, int d, const int32_t *order, const 
 // placed by rank counting (M <= 256) or the LDS bitonic sort.
 constexpr int kPickStage = 8192;
 constexpr int kPickU = 4;
+constexpr int kPickBest = kCoarsePickMaxT;  // running top-nprobe records of an overflowing pick (nprobe <= it)
 
 template <int METRIC, bool STAGED>  // METRIC: MQVS_METRIC_L2 or kMetricIpRaw (the coarse metric)
 __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T,
                                                              int Tcap, int nprobe, const float *q, int64_t qld,
                                                              const float *cent, const float *cnorm, int64_t ncent,
                                                              int d, const float *bq, const float *qnorms,
-                                                             int gs_log2, int64_t *probes, int trace) {
+                                                             int gs_log2, int64_t *probes,
+                                                             unsigned long long *ovf, int trace) {
     // (measurement build: trace = 1 prints phase timestamps of three workgroups)
     const bool tr = kDebugTuning && trace && threadIdx.x == 0 &&
                     (blockIdx.x == 0 || blockIdx.x == gridDim.x / 2 || blockIdx.x == gridDim.x - 1);
@@ -1094,17 +1104,18 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
     if (tr) ts[0] = wall_clock64();
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh[4];
-    __shared__ int s_grp[kCoarsePickMaxT];
-    __shared__ int s_ng, s_valid;
+    __shared__ int s_grp[kCoarsePickCap];
+    __shared__ int s_wc[SEL_THREADS / 64];
+    __shared__ int s_ng, s_valid, s_cur;
     __shared__ uint32_t s_knp;
     __shared__ uint64_t s_red[2 * (SEL_THREADS / 64)];
-    // dynamic LDS: recs [pow2 >= 16 T] then (STAGED) keys [ngroups], sized per
-    // launch so small pickups keep many workgroups per CU
+    // dynamic LDS: recs [pow2 >= kPickBest + GS Tcap] then (STAGED) keys
+    // [ngroups], sized per launch so small pickups keep many workgroups per CU
     extern __shared__ uint4 dyn[];
     uint4 *recs = dyn;
     int NR = 1;
     const int GS = 1 << gs_log2;  // centroids per group
-    while (NR < GS * Tcap) NR <<= 1;
+    while (NR < kPickBest + GS * Tcap) NR <<= 1;
     uint32_t *keys = reinterpret_cast<uint32_t *>(dyn + NR);
     const int qi = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const float *row = gmax + (int64_t)qi * gld;
@@ -1141,12 +1152,12 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
         }
         __syncthreads();
     };
-    // exact values of centroids c in [cb, ce) (16 per taken group): wave wv
-    // scores centroids c0 .. c0 + kPickU - 1, lanes over float4 columns
-    // (scalar columns when d or the rows are not 16-B aligned)
+    // exact values of centroids c in [cb, ce) (GS per taken group) into
+    // recs[ro + c]: wave wv scores centroids c0 .. c0 + kPickU - 1, lanes over
+    // float4 columns (scalar columns when d or the rows are not 16-B aligned)
     const float *qv = q + (int64_t)qi * qld;
     const bool v4 = (d & 3) == 0 && (((uintptr_t)cent | (uintptr_t)qv) & 15) == 0;
-    auto score = [&](int cb, int ce) {
+    auto score = [&](int cb, int ce, int ro) {
         for (int c0 = cb + wv * kPickU; c0 < ce; c0 += (SEL_THREADS / 64) * kPickU) {
             int64_t r[kPickU];
             float dot[kPickU];
@@ -1211,7 +1222,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
                 if (c < ce) {
                     uint32_t key = 0xFFFFFFFFu;
                     if (rv >= 0) key = okey<METRIC>(METRIC == MQVS_METRIC_L2 ? cnorm[rv] - 2.0f * dv : dv);
-                    recs[c] = uint4{key, (uint32_t)(rv >= 0 ? rv : 0xFFFFFFFFu), 0u, 0u};
+                    recs[ro + c] = uint4{key, (uint32_t)(rv >= 0 ? rv : 0xFFFFFFFFu), 0u, 0u};
                     if (key != 0xFFFFFFFFu) atomicAdd(&s_valid, 1);
                 }
             }
@@ -1226,12 +1237,16 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
         tpair = th == 0xFFFFFFFEu ? ~0ull : ((uint64_t)th << 32) | 0xFFFFFFFFull;  // (every tie is in)
     }
     const int ng0 = min(s_ng, Tcap);
-    score(0, GS * ng0);
+    // (a core with more ties than Tcap groups: overflow)
+    bool over = s_ng > Tcap;
+    score(0, GS * ng0, 0);
     if (tr) ts[3] = wall_clock64();
     int ng = ng0;
+    uint32_t kx = th;  // every group that can hold a top-nprobe centroid has key <= max(kx, th)
     // 2. extras (needs the bound and a full core; fewer than T valid groups:
-    // every group is in the core already)
-    if (bq && tpair != ~0ull && s_ng < Tcap) {
+    // every group is in the core already).  The collect counts every group
+    // that passes, so a working set that cannot hold them shows as s_ng > Tcap.
+    if (bq && tpair != ~0ull) {
         const int M0 = GS * ng0;
         for (int c = t; c < M0; c += SEL_THREADS) {
             const uint4 e = recs[c];
@@ -1241,7 +1256,6 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
             if (rank == nprobe - 1) s_knp = e.x;
         }
         __syncthreads();
-        uint32_t kx;
         if (s_knp != 0xFFFFFFFFu) {
             // the approximate maximum a group needs: v -/+ bq (rounding slack
             // as widen's), v a full distance for L2
@@ -1263,12 +1277,73 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
             const float w = widen<METRIC>(okey_value<METRIC>(th), bq[qi]);
             kx = w == w ? okey<METRIC>(w) : th;
         }
-        if (kx >= th)
+        if (kx >= th && !over) {
             collect([&](uint32_t k, int64_t i) {
                 return k <= kx && (((uint64_t)k << 32) | (uint64_t)(uint32_t)i) > tpair;
             });
-        ng = min(s_ng, Tcap);
-        if (ng > ng0) score(M0, GS * ng);
+            over = s_ng > Tcap;
+            ng = min(s_ng, Tcap);
+            if (!over && ng > ng0) score(M0, GS * ng, 0);
+        }
+    }
+    if (over) {
+        // 3. every group with key <= max(kx, th), Tcap groups at a time in
+        // group order; recs[0, nprobe) keeps the best so far (sorted), the
+        // batch's records follow at kPickBest
+        if (t == 0 && ovf) atomicAdd(ovf, 1ull);
+        const uint32_t kall = kx > th ? kx : th;
+        for (int c = t; c < kPickBest; c += SEL_THREADS) recs[c] = uint4{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+        int64_t cursor = 0;
+        while (cursor < ngroups) {
+            // ordered compaction of the next Tcap passing groups from `cursor`
+            int nb = 0;
+            int64_t i0 = cursor;
+            while (i0 < ngroups && nb < Tcap) {
+                const int64_t i = i0 + t;
+                bool pass = false;
+                if (i < ngroups) {
+                    const uint32_t kk = keyof(i);
+                    pass = kk != 0xFFFFFFFFu && kk <= kall;
+                }
+                const uint64_t bal = __ballot(pass);
+                if (lane == 0) s_wc[wv] = __popcll(bal);
+                __syncthreads();
+                int before = 0, tot = 0;
+                for (int x = 0; x < SEL_THREADS / 64; ++x) {
+                    before += x < wv ? s_wc[x] : 0;
+                    tot += s_wc[x];
+                }
+                const int pos = nb + before + __popcll(bal & ((1ull << lane) - 1ull));
+                if (pass && pos < Tcap) s_grp[pos] = (int)i;
+                if (pass && pos == Tcap - 1) s_cur = (int)(i + 1);
+                __syncthreads();
+                if (nb + tot >= Tcap) {
+                    i0 = s_cur;
+                    nb = Tcap;
+                } else {
+                    nb += tot;
+                    i0 += SEL_THREADS;
+                }
+                __syncthreads();  // (s_wc, s_cur reused)
+            }
+            cursor = i0;
+            if (nb == 0) break;
+            score(0, GS * nb, kPickBest);
+            int N = 1;
+            while (N < kPickBest + GS * nb) N <<= 1;
+            for (int c = kPickBest + GS * nb + t; c < N; c += SEL_THREADS)
+                recs[c] = uint4{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+            __syncthreads();
+            block_bitonic_sort(recs, N);
+            for (int c = nprobe + t; c < kPickBest; c += SEL_THREADS)
+                recs[c] = uint4{0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu, 0xFFFFFFFFu};
+            __syncthreads();
+        }
+        for (int j = t; j < nprobe; j += SEL_THREADS) {
+            const uint4 e = recs[j];
+            probes[(int64_t)qi * nprobe + j] = e.x == 0xFFFFFFFFu ? -1 : (int64_t)e.y;
+        }
+        return;
     }
     const int M = GS * ng;
     __syncthreads();
@@ -1309,19 +1384,22 @@ __global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, 
 
 void launch_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T, int nprobe, int metric,
                         const float *q, int64_t qld, const float *cent, const float *cnorm, int64_t ncent, int d,
-                        const float *bq, const float *qnorms, int gs_log2, int nq, int64_t *probes, hipStream_t s) {
+                        const float *bq, const float *qnorms, int gs_log2, int nq, int64_t *probes,
+                        unsigned long long *ovf, hipStream_t s) {
     if (nq <= 0) return;
+    if (T > kCoarsePickMaxT || nprobe > kPickBest) fail(MQVS_ERR_LOGICAL, "coarse pick: nprobe above its cap");
     // room for the groups within the bound of the core's nprobe-th value
     // (near-ties): as many as a core of nprobe + 2 groups had (a smaller core
-    // leaves more of the near groups to the extras)
-    const int Tcap = std::min(kCoarsePickMaxT, std::max(T, nprobe + 2) + std::max(std::max(T, nprobe + 2), 8));
+    // leaves more of the near groups to the extras); more are the overflow
+    // path's (exact, batched)
+    const int Tcap = std::min(kCoarsePickCap, std::max(T, nprobe + 2) + std::max(std::max(T, nprobe + 2), 8));
     const int trace = tune_int("MQVS_PICK_TRACE", 0);
 #define MQVS_PICK(M, ST)                                                                                         \
     hipLaunchKernelGGL((k_coarse_pick<M, ST>), dim3(nq), dim3(SEL_THREADS), lds, s, gmax, gld, ngroups, T, Tcap, \
-                       nprobe, q, qld, cent, cnorm, ncent, d, bq, qnorms, gs_log2, probes, trace)
+                       nprobe, q, qld, cent, cnorm, ncent, d, bq, qnorms, gs_log2, probes, ovf, trace)
     const bool staged = ngroups <= kPickStage;
     size_t nr = 1;
-    while (nr < ((size_t)1 << gs_log2) * Tcap) nr <<= 1;
+    while (nr < kPickBest + ((size_t)1 << gs_log2) * Tcap) nr <<= 1;
     const size_t lds = nr * sizeof(uint4) + (staged ? sizeof(uint32_t) * (size_t)ngroups : 0);
     if (metric == MQVS_METRIC_L2) {
         if (staged) MQVS_PICK(MQVS_METRIC_L2, true); else MQVS_PICK(MQVS_METRIC_L2, false);

@@ -708,15 +708,26 @@ __global__ __launch_bounds__(kScanThreads) void k_exclusive_ord(int *flag_ord, i
 // workgroup to finish (an agent-scope ticket, zeroed with the search's status
 // words) then scans the counts: offsets[c] = sum of padded counts before c,
 // totals[0] = padded list length, totals[1] = selected rows.  host_totals
-// (pinned host memory, may be null): the same two values, [0] then [1] behind
-// a system-scope fence, so the host can act on them as soon as [1] changes
-// from its -1 sentinel instead of draining the stream for a copy.  (One
-// launch: the separate single-workgroup scan cost ~8 us plus a launch gap.)
+// (pinned host memory, may be null): the same two values, then host_gen in
+// [2] behind a system-scope fence, so the host can act on them as soon as [2]
+// shows its call's generation instead of draining the stream for a copy (a
+// record left by another call's kernel never carries this call's number).
+// (One launch: the separate single-workgroup scan cost ~8 us plus a launch
+// gap.)
+// The ticket relies on gfx9-family memory ordering (gfx950 here): stores with
+// the agent-scope write-through and vmcnt counting stores, so a workgroup's
+// counts have left it when its s_waitcnt vmcnt(0) (the 0x0F70 encoding: gfx9's
+// field layout) retires, before its ticket; other ISA families order stores
+// differently and would need release/acquire fences on the ticket.
 __global__ __launch_bounds__(kScanThreads) void k_chunk_count(const uint8_t *filter, const uint8_t *nonempty,
                                                                const uint8_t *exists, int64_t n, int64_t chunk_rows,
                                                                int64_t nchunks, int *count, int tile,
                                                                int64_t *offsets, int64_t *totals,
-                                                               int64_t *host_totals, int *ticket) {
+                                                               int64_t *host_totals, int64_t host_gen,
+                                                               int *ticket) {
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__) && !defined(__gfx942__)
+#error "k_chunk_count's ticket assumes gfx94x/gfx950 store ordering (see above)"
+#endif
     __shared__ int64_t sh[kScanThreads / 64];
     __shared__ int s_last;
     const int64_t c = (int64_t)blockIdx.x * (kScanThreads / 64) + (threadIdx.x >> 6);
@@ -757,8 +768,9 @@ __global__ __launch_bounds__(kScanThreads) void k_chunk_count(const uint8_t *fil
         *ticket = 0;
         if (host_totals) {
             *reinterpret_cast<volatile int64_t *>(host_totals) = padded_total;
-            __threadfence_system();
             *reinterpret_cast<volatile int64_t *>(host_totals + 1) = selected;
+            __threadfence_system();
+            *reinterpret_cast<volatile int64_t *>(host_totals + 2) = host_gen;
             __threadfence_system();
         }
     }
@@ -812,12 +824,13 @@ __global__ __launch_bounds__(256) void k_compact_rows(const uint8_t *filter, con
 
 void launch_gather_count(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists, int64_t n,
                          int64_t chunk_rows, int tile, int *count, int64_t *offsets, int64_t *totals,
-                         int64_t *host_totals, int *ticket, hipStream_t s) {
+                         int64_t *host_totals, int64_t host_gen, int *ticket, hipStream_t s) {
     const int64_t nchunks = (n + chunk_rows - 1) / chunk_rows;
     if (nchunks < 1) return;
     constexpr int wpb = kScanThreads / 64;  // chunks (waves) per workgroup
     hipLaunchKernelGGL(k_chunk_count, dim3((unsigned)((nchunks + wpb - 1) / wpb)), dim3(kScanThreads), 0, s, filter,
-                       nonempty, exists, n, chunk_rows, nchunks, count, tile, offsets, totals, host_totals, ticket);
+                       nonempty, exists, n, chunk_rows, nchunks, count, tile, offsets, totals, host_totals, host_gen,
+                       ticket);
 }
 
 void launch_gather_list(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists, int64_t n,

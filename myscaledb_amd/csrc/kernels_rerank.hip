@@ -109,18 +109,102 @@ __device__ inline void rerank_emit(uint4 *recs, uint4 *g, int ncand, int k, int 
     }
 }
 
+// Bound pruning (index re-rank; RerankPrune in mqvs_internal.h): how many of
+// query q's candidates -- sorted by their approximate value a -- can reach the
+// exact top k.  With B the bound on |a - exact| (k_query_bound for query
+// variant 0, plus |x_v - x_0| |y|max for the cosine variant x_v the exact
+// value of a row uses), the k best candidates have exact values within B of
+// a_k, the k-th approximate value, so the k-th exact value is at most a_k + B
+// (L2; at least a_k - B for IP / cosine, larger better); a candidate with a >
+// a_k + 2B has an exact value strictly worse, and so has every later one.
+// The output is the same as re-ranking all of them.  No pruning (m = ncand)
+// when a_k is not a valid value, B is not finite, or for IP the k best could
+// fall under the FLT_MIN cut (searchWrapper's init) and leave fewer than k.
+// Block-uniform result; s_m: one int of LDS.
+template <int METRIC>
+__device__ inline int rerank_keep(const ScanParams &p, const RerankPrune &pr, int q, int ncand, int k, int *s_m) {
+    if (!pr.raw || k >= ncand) return ncand;
+    const float *raw = pr.raw + (int64_t)q * ncand;
+    const int t = threadIdx.x, lane = t & 63;
+    if (t == 0) *s_m = ncand;
+    __syncthreads();
+    __shared__ float s_cut;
+    __shared__ int s_ok;
+    if (t < 64) {
+        // cosine: the largest distance of a used variant from variant 0, in fp64
+        double dmax = 0.0;
+        if (METRIC == MQVS_METRIC_COSINE && p.maxv > 1) {
+            const int mu = p.qmu[q], lam = p.qlam[q];
+            const int nv = (lam >= 1 && mu >= 0 && mu + lam <= p.maxv) ? mu + lam : p.maxv;
+            const int64_t qs = (int64_t)((p.d + 31) / 32 * 32);
+            const float *x0 = p.qvars + (int64_t)q * p.maxv * qs;
+            for (int v = 1; v < nv; ++v) {
+                const float *xv = x0 + (int64_t)v * qs;
+                double ss = 0.0;
+                for (int i = lane; i < p.d; i += 64) {
+                    const double e = (double)xv[i] - (double)x0[i];
+                    ss += e * e;
+                }
+                for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
+                dmax = ss > dmax ? ss : dmax;
+            }
+        }
+        if (lane == 0) {
+            const float ak = raw[k - 1];
+            const float ym = *pr.ymax;
+            const float dv = dmax > 0.0 ? (float)(sqrt(dmax) * (1.0 + 1e-6)) * ym * 1.0001f : 0.f;
+            const float b = pr.bq[q] + dv + 1e-30f;
+            float w;
+            bool ok = ak == ak && b < 1e30f && ym < 1e30f;
+            if (METRIC == MQVS_METRIC_L2) {
+                w = ak + 2.0f * b;
+                w = w + fabsf(w) * 2.4e-7f + 1e-30f;
+            } else {
+                w = ak - 2.0f * b;
+                w = w - fabsf(w) * 2.4e-7f - 1e-30f;
+                if (METRIC == MQVS_METRIC_IP) {
+                    float lo = ak - b;
+                    lo = lo - fabsf(lo) * 2.4e-7f;
+                    ok = ok && lo > 1.17549435e-38f;
+                }
+            }
+            s_cut = w;
+            s_ok = ok && w == w ? 1 : 0;
+        }
+    }
+    __syncthreads();
+    if (s_ok) {
+        const float w = s_cut;
+        // the first candidate past the cut (NaN: no candidate) ends the prefix
+        for (int i = t; i < ncand; i += SEL_THREADS) {
+            const float a = raw[i];
+            const bool keep = METRIC == MQVS_METRIC_L2 ? a <= w : a >= w;
+            if (!keep) {
+                atomicMin(s_m, i);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    const int m = *s_m;
+    if (t == 0 && pr.count) atomicAdd(pr.count, (unsigned long long)m);
+    return m;
+}
+
 // Generic form (any d): one thread per candidate walks its row.
 template <int METRIC, bool DIRECT>
 __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids(ScanParams p, const int64_t *cand, int ncand,
                                                            int k, int64_t id_offset, int64_t *out_ids,
-                                                           float *out_dist, uint4 *scratch) {
+                                                           float *out_dist, uint4 *scratch, RerankPrune pr) {
     extern __shared__ __attribute__((aligned(16))) uint4 recs[];  // pow2 >= ncand (or kSortCap) records
+    __shared__ int s_m;
     const int q = blockIdx.x;
     const int64_t *c = cand + (int64_t)q * ncand;
     uint4 *g = scratch ? scratch + (int64_t)q * 2 * ncand : nullptr;
     uint4 *dst = g ? g : recs;
+    const int m = rerank_keep<METRIC>(p, pr, q, ncand, k, &s_m);
     for (int i = threadIdx.x; i < ncand; i += SEL_THREADS) {
-        int64_t row = c[i];
+        int64_t row = i < m ? c[i] : -1;
         if (!(row >= 0 && row < p.n && row_valid(p, row))) row = -1;
         dst[i] = rerank_rec<METRIC>(p, row, row >= 0 ? cand_value<METRIC, DIRECT>(p, q, row) : 0.f);
     }
@@ -331,8 +415,10 @@ __device__ inline float wave_exact_any(const ScanParams &p, int q, int64_t row, 
 template <int METRIC, bool DIRECT>
 __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids_tiled(ScanParams p, const int64_t *cand, int ncand,
                                                                  int k, int64_t id_offset, int64_t *out_ids,
-                                                                 float *out_dist, int nrec, uint4 *scratch) {
+                                                                 float *out_dist, int nrec, uint4 *scratch,
+                                                                 RerankPrune pr) {
     extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ int s_m;
     uint4 *recs = reinterpret_cast<uint4 *>(smem);
     uint4 *g = scratch ? scratch + (int64_t)blockIdx.x * 2 * ncand : nullptr;
     uint4 *dst = g ? g : recs;
@@ -340,10 +426,11 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids_tiled(ScanParams p, 
     float *tile = reinterpret_cast<float *>(smem + (size_t)nrec * sizeof(uint4)) + wv * 64 * kRrStride;
     const int q = blockIdx.x;
     const int64_t *c = cand + (int64_t)q * ncand;
+    const int m = rerank_keep<METRIC>(p, pr, q, ncand, k, &s_m);
     for (int cb = 0; cb < ncand; cb += SEL_THREADS) {
         const int i = cb + threadIdx.x;
         int64_t row = -1;
-        if (i < ncand) {
+        if (i < m) {
             row = c[i];
             if (!(row >= 0 && row < p.n && row_valid(p, row))) row = -1;
         }
@@ -475,26 +562,27 @@ void launch_exact_rerank(const ScanParams &p, int metric, const uint32_t *surv, 
 
 template <int M, bool DIRECT>
 static void rerank_ids_t(const ScanParams &p, const int64_t *cand, int ncand, int k, int64_t id_offset,
-                         int64_t *ids, float *dist, uint4 *scratch, hipStream_t s) {
+                         int64_t *ids, float *dist, uint4 *scratch, hipStream_t s, const RerankPrune &pr) {
     int N = 1;
     while (N < ncand) N <<= 1;
     if (scratch) N = kSortCap;  // LDS records of global_sort
     if ((p.d & 3) == 0) {
         const size_t lds = N * sizeof(uint4) + (SEL_THREADS / 64) * 64 * kRrStride * sizeof(float);
         hipLaunchKernelGGL((k_rerank_ids_tiled<M, DIRECT>), dim3(p.nq), dim3(SEL_THREADS), lds, s, p, cand, ncand, k,
-                           id_offset, ids, dist, N, scratch);
+                           id_offset, ids, dist, N, scratch, pr);
     } else {
         hipLaunchKernelGGL((k_rerank_ids<M, DIRECT>), dim3(p.nq), dim3(SEL_THREADS), N * sizeof(uint4), s, p, cand,
-                           ncand, k, id_offset, ids, dist, scratch);
+                           ncand, k, id_offset, ids, dist, scratch, pr);
     }
 }
 
 void launch_rerank_ids(const ScanParams &p, int metric, const int64_t *cand, int ncand, int k,
-                       int64_t id_offset, int64_t *out_ids, float *out_dist, uint4 *scratch, hipStream_t s) {
+                       int64_t id_offset, int64_t *out_ids, float *out_dist, uint4 *scratch, hipStream_t s,
+                       const RerankPrune &pr) {
     const bool direct = !blas_formula(p);
-#define MQVS_RR(M)                                                                           \
-    direct ? rerank_ids_t<M, true>(p, cand, ncand, k, id_offset, out_ids, out_dist, scratch, s) \
-           : rerank_ids_t<M, false>(p, cand, ncand, k, id_offset, out_ids, out_dist, scratch, s)
+#define MQVS_RR(M)                                                                                   \
+    direct ? rerank_ids_t<M, true>(p, cand, ncand, k, id_offset, out_ids, out_dist, scratch, s, pr) \
+           : rerank_ids_t<M, false>(p, cand, ncand, k, id_offset, out_ids, out_dist, scratch, s, pr)
     switch (metric) {
         case MQVS_METRIC_L2: MQVS_RR(MQVS_METRIC_L2); break;
         case MQVS_METRIC_IP: MQVS_RR(MQVS_METRIC_IP); break;

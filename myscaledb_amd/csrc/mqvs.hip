@@ -53,6 +53,11 @@ void set_error(const std::string &msg) { g_error = msg; }
 // Growth beyond the reservation passes the same gate inside the call; only
 // if every running call is then waiting does it go over the budget (counted)
 // rather than deadlock.
+// the pinned record [padded, selected, generation] of k_chunk_count (int64
+// words at host_flags + kCountRec), and how long a filtered search polls it
+constexpr int kCountRec = 32;
+constexpr int kCountSpinUs = 200;
+
 struct Workspace;
 struct WsGate {
     std::mutex mu;
@@ -91,7 +96,8 @@ struct Workspace {
     DevBuf queries, qvars, qnorms, qmu, qlam, status, filter, exists, ord, probe, tau, count, cand,
         overflow, out_ids, out_dist, misc, qhi, bq, thr, cand2, count2, gcount, goff, glist, large, sticky, surv,
         recs, flags, p4q, qord;
-    int *host_flags = nullptr;  // pinned
+    int *host_flags = nullptr;  // pinned (64 ints; the selected-row count record at kCountRec)
+    int64_t count_gen = 0;      // generation of the last selected-row count record asked for
     bool pending_timing = false, pending_bf16 = false;  // search_collect_stats
     int device = 0;
     std::mutex use;     // held by the owning thread during a call (WsCall); trimmers only try_lock it
@@ -360,11 +366,79 @@ void *GBuf::get(size_t bytes) {
 }
 
 static thread_local int t_fault_status = MQVS_OK, t_fault_calls = 0;
+static thread_local bool t_fault_mid = false;  // MQVS_FAULT_MID_CALL: fire inside the call instead
 
 void fault_point() {
-    if (t_fault_calls <= 0) return;
+    if (t_fault_calls <= 0 || t_fault_mid) return;
     --t_fault_calls;
     fail(t_fault_status, "injected fault (mqvs_inject_fault)");
+}
+
+// the mid-call drill point: a filtered mqvs_search right after its
+// selected-row count is queued (the count kernel is then still in flight)
+static void fault_point_mid() {
+    if (t_fault_calls <= 0 || !t_fault_mid) return;
+    --t_fault_calls;
+    fail(t_fault_status, "injected fault (mqvs_inject_fault, mid-call)");
+}
+
+// ---------------------------------------------------------------------------
+// Host waits (mqvs_set_wait_mode).  The reference admits up to 2 x physical
+// cores concurrent scans (ScanThreadLimiter.h:25-58, MergeTreeVSManager.cpp:
+// 974-975); here each of them waits for its GPU work, and a waiting thread
+// that spins holds a host core for the whole search.  HYBRID polls the
+// completion of a blocking-sync event for up to spin_us (a short search
+// returns without a wake-up) and then sleeps in hipEventSynchronize on it.
+static std::atomic<int> g_wait_mode{MQVS_WAIT_HYBRID};
+static std::atomic<int> g_wait_spin_us{50};
+
+void cpu_relax() {
+#if defined(__x86_64__) || defined(__i386__)
+    __builtin_ia32_pause();
+#endif
+}
+
+int wait_spin_us() {
+    const int m = g_wait_mode.load(std::memory_order_relaxed);
+    return m == MQVS_WAIT_RUNTIME ? -1 : m == MQVS_WAIT_BLOCK ? 0 : g_wait_spin_us.load(std::memory_order_relaxed);
+}
+
+// one blocking-sync event per thread and device (the current one)
+static hipEvent_t blocking_event() {
+    struct Events {
+        std::map<int, hipEvent_t> ev;
+        ~Events() {
+            for (auto &e : ev) (void)hipEventDestroy(e.second);
+        }
+    };
+    static thread_local Events t_ev;
+    int dev = 0;
+    MQVS_HIP(hipGetDevice(&dev));
+    hipEvent_t &e = t_ev.ev[dev];
+    if (!e) MQVS_HIP(hipEventCreateWithFlags(&e, hipEventBlockingSync | hipEventDisableTiming));
+    return e;
+}
+
+void host_wait(hipStream_t s) {
+    const int spin = wait_spin_us();
+    if (spin < 0) {
+        MQVS_HIP(hipStreamSynchronize(s));
+        return;
+    }
+    hipEvent_t e = blocking_event();
+    MQVS_HIP(hipEventRecord(e, s));
+    if (spin > 0) {
+        const auto t0 = std::chrono::steady_clock::now();
+        const auto lim = std::chrono::microseconds(spin);
+        while (true) {
+            const hipError_t q = hipEventQuery(e);
+            if (q == hipSuccess) return;
+            if (q != hipErrorNotReady) MQVS_HIP(q);
+            if (std::chrono::steady_clock::now() - t0 > lim) break;
+            for (int i = 0; i < 32; ++i) cpu_relax();
+        }
+    }
+    MQVS_HIP(hipEventSynchronize(e));
 }
 
 void ws_detach_ext(int device, WsExt *ext) {
@@ -563,7 +637,7 @@ static int prep_variants(Workspace &ws, const float *dq, int nq, int d, bool cos
         MQVS_HIP(hipGetLastError());
         if (pass > 0 || !cos || ords <= maxv || !may_sync || maxv_override > 0) break;
         MQVS_HIP(hipMemcpyAsync(ws.host_flags + 12, status, sizeof(int), hipMemcpyDeviceToHost, s));
-        MQVS_HIP(hipStreamSynchronize(s));
+        host_wait(s);
         if (!ws.host_flags[12]) break;
         maxv = (int)std::min<int64_t>(ords, kMaxVariantsCap);
     }
@@ -736,6 +810,10 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     WsCall ws_call(ws);
     hipStream_t s = user_stream ? (hipStream_t)user_stream : ws.stream;
     ws.last = s;
+    // a filtered search waits for its selected-row count mid-call: behind
+    // earlier work on the caller's stream (e.g. ASYNC searches) it sleeps
+    // instead of spinning (below)
+    const bool queued_on_entry = filter && hipStreamQuery(s) == hipErrorNotReady;
     const bool dev = flags & MQVS_F_DEVICE_PTRS;
     const int64_t n = seg->n;
     const int d = seg->d;
@@ -787,21 +865,37 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     // [gather-count ticket 1]
     int *fl = (int *)ws.get(ws.flags, sizeof(int) * (9 + (size_t)nq));
     launch_fill2((uint32_t *)fl, 9 + (int64_t)nq, 0u, nullptr, 0, 0u, s);
+    // (armed between the count launch and the host's read of its totals: an
+    // exception in between drains the stream, so that no count kernel of this
+    // call is still in flight when the next call on this workspace rearms the
+    // pinned record)
+    struct CountDrain {
+        hipStream_t s = nullptr;
+        ~CountDrain() {
+            if (s) (void)hipStreamSynchronize(s);
+        }
+    } count_drain;
+    int64_t count_gen = 0;
     if (dfilter && gather_mode != 0 && n > 0) {
         const int64_t nch = (n + seg->granule - 1) / seg->granule;
         gcount = (int *)ws.get(ws.gcount, sizeof(int) * nch);
         goff = (int64_t *)ws.get(ws.goff, sizeof(int64_t) * (nch + 2));
         // the totals also land in pinned host memory (k_chunk_count), read once
         // the query prep, chunk ordinals and bf16 query planes are queued: the
-        // host waits for this kernel only, not for a drained stream
-        auto *htot = reinterpret_cast<int64_t *>(ws.host_flags + 8);
-        htot[0] = -1;
-        htot[1] = -1;
+        // host waits for this kernel only, not for a drained stream.  The
+        // record [padded, selected, generation] is this call's once its
+        // generation word (written last, behind a system-scope fence) shows
+        // this call's number.
+        auto *htot = reinterpret_cast<int64_t *>(ws.host_flags + kCountRec);
+        count_gen = ++ws.count_gen;
+        htot[2] = 0;
         std::atomic_thread_fence(std::memory_order_seq_cst);
         launch_gather_count(dfilter, seg->nonempty_bits, dexists, n, seg->granule, gtile, gcount, goff, goff + nch,
-                            htot, fl + 8 + nq, s);
+                            htot, count_gen, fl + 8 + nq, s);
         MQVS_HIP(hipGetLastError());
+        count_drain.s = s;
         selected = 0;
+        fault_point_mid();
     }
     const bool mfma = fnq >= kBlasThreshold;
     const bool bf16_ok = seg->approx_ok && !force_exact && batch_mode == 0;
@@ -922,28 +1016,31 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         MQVS_HIP(hipGetLastError());
     }
 
-    // ---- the selected count (k_chunk_count's pinned copy; past ~200 us of
-    // spinning -- earlier work queued on the caller's stream -- a stream sync)
+    // ---- the selected count (k_chunk_count's pinned record, polled with a
+    // pause for up to kCountSpinUs; then -- or at once behind earlier work on
+    // the caller's stream, or in MQVS_WAIT_BLOCK -- the host's wait)
     if (selected >= 0) {
-        volatile int64_t *htot = reinterpret_cast<volatile int64_t *>(ws.host_flags + 8);
+        volatile int64_t *htot = reinterpret_cast<volatile int64_t *>(ws.host_flags + kCountRec);
+        const int spin = queued_on_entry || wait_spin_us() == 0 ? 0 : kCountSpinUs;
         const auto t0 = std::chrono::steady_clock::now();
-        while (htot[1] < 0) {
-            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(200)) {
-                MQVS_HIP(hipStreamSynchronize(s));
+        while (htot[2] != count_gen) {
+            if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(spin)) {
+                host_wait(s);
                 break;
             }
+            for (int i = 0; i < 8; ++i) cpu_relax();
         }
         std::atomic_thread_fence(std::memory_order_acquire);
-        if (htot[1] < 0) {
-            // (the pinned copy never showed: read the device totals)
+        int64_t tot[2] = {htot[0], htot[1]};
+        if (htot[2] != count_gen) {
+            // (the pinned record never showed: the device totals, the stream drained)
             const int64_t nch = (n + seg->granule - 1) / seg->granule;
-            int64_t dt[2];
-            MQVS_HIP(hipMemcpy(dt, goff + nch, sizeof(dt), hipMemcpyDeviceToHost));
-            htot[0] = dt[0];
-            htot[1] = dt[1];
+            MQVS_HIP(hipMemcpyAsync(tot, goff + nch, sizeof(tot), hipMemcpyDeviceToHost, s));
+            host_wait(s);
         }
-        gpadded = round_up(htot[0], kSmallRows);
-        selected = htot[1];
+        count_drain.s = nullptr;
+        gpadded = round_up(tot[0], kSmallRows);
+        selected = tot[1];
     }
     bool gather = false;
     if (selected >= 0) {
@@ -1145,7 +1242,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         // [overflow 4][status 4] in one copy -> host_flags[0] overflow bits,
         // [1] status, [4..6] survivor / candidate stats
         MQVS_HIP(hipMemcpyAsync(ws.host_flags + 16, fl, 8 * sizeof(int), hipMemcpyDeviceToHost, s));
-        MQVS_HIP(hipStreamSynchronize(s));
+        host_wait(s);
         ws.host_flags[0] = ws.host_flags[16];
         ws.host_flags[1] = ws.host_flags[20];
         ws.host_flags[4] = ws.host_flags[17];
@@ -1188,13 +1285,13 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
                                 ddist, overflow, large, s);
             MQVS_HIP(hipGetLastError());
             MQVS_HIP(hipMemcpyAsync(ws.host_flags, overflow, sizeof(int), hipMemcpyDeviceToHost, s));
-            MQVS_HIP(hipStreamSynchronize(s));
+            host_wait(s);
         }
         st.rescans = rescans;
         if (!dev) {
             MQVS_HIP(hipMemcpyAsync(out_ids, dids, sizeof(int64_t) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
             MQVS_HIP(hipMemcpyAsync(out_dist, ddist, sizeof(float) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
-            MQVS_HIP(hipStreamSynchronize(s));
+            host_wait(s);
         }
         if (timing) read_search_times(ws, st);
     }
@@ -1335,14 +1432,14 @@ static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const i
         return;
     }
     MQVS_HIP(hipMemcpyAsync(ws.host_flags, status, sizeof(int), hipMemcpyDeviceToHost, s));
-    MQVS_HIP(hipStreamSynchronize(s));
+    host_wait(s);
     if (ws.host_flags[0] && ords > maxv)
         fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not repeat within " + std::to_string(maxv) +
                                    " steps on a part of more chunks");
     if (!dev) {
         MQVS_HIP(hipMemcpyAsync(out_ids, dids, sizeof(int64_t) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
         MQVS_HIP(hipMemcpyAsync(out_dist, ddist, sizeof(float) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
-        MQVS_HIP(hipStreamSynchronize(s));
+        host_wait(s);
     }
 }
 
@@ -1552,7 +1649,7 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
         MQVS_HIP(hipGetLastError());
     } else {
         MQVS_HIP(hipMemcpyAsync(ws.host_flags, overflow, sizeof(int), hipMemcpyDeviceToHost, s));
-        MQVS_HIP(hipStreamSynchronize(s));
+        host_wait(s);
         int rescans = 0;
         while (ws.host_flags[0]) {
             // a list overflowed its capacity: tighten tau from what was kept and
@@ -1568,13 +1665,13 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
                                 s);
             MQVS_HIP(hipGetLastError());
             MQVS_HIP(hipMemcpyAsync(ws.host_flags, overflow, sizeof(int), hipMemcpyDeviceToHost, s));
-            MQVS_HIP(hipStreamSynchronize(s));
+            host_wait(s);
         }
         st.rescans = rescans;
         if (!dev) {
             MQVS_HIP(hipMemcpyAsync(out_ids, dids, sizeof(int64_t) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
             MQVS_HIP(hipMemcpyAsync(out_dist, ddist, sizeof(float) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
-            MQVS_HIP(hipStreamSynchronize(s));
+            host_wait(s);
         }
         if (timing) {
             float a = 0, b = 0, c = 0, e = 0, f = 0;
@@ -1632,7 +1729,7 @@ static std::pair<int64_t, int64_t> stream_table(IngestTmp &tmp, const uint8_t *d
     launch_block_table(dsrc, n, *tab, maxb, dout, s);
     MQVS_HIP(hipGetLastError());
     MQVS_HIP(hipMemcpyAsync(hbuf, dout, 3 * sizeof(int64_t), hipMemcpyDeviceToHost, s));
-    MQVS_HIP(hipStreamSynchronize(s));
+    host_wait(s);
     if (hbuf[2] == 2)
         fail(MQVS_ERR_NOT_IMPLEMENTED, std::string(what) + ": compression method other than LZ4 / NONE");
     if (hbuf[2])
@@ -1705,7 +1802,7 @@ static mqvs_segment *ingest_column(const uint8_t *data_bin, int64_t data_bytes, 
         int *hstatus = reinterpret_cast<int *>(h + 2);
         if (verify) MQVS_HIP(hipStreamWaitEvent(s, tmp.join, 0));
         MQVS_HIP(hipMemcpyAsync(hstatus, status, sizeof(int), hipMemcpyDeviceToHost, s));
-        MQVS_HIP(hipStreamSynchronize(s));
+        host_wait(s);
         if (*hstatus & (kBadSizesChecksum | kBadDataChecksum))
             fail(MQVS_ERR_CHECKSUM, std::string("Checksum doesn't match: corrupted data (") +
                                         (*hstatus & kBadSizesChecksum ? "array sizes stream" : "vector data stream") +
@@ -1807,12 +1904,15 @@ int mqvs_thread_release(void) {
 int mqvs_shutdown(void) { return mqvs_thread_release(); }
 
 int mqvs_inject_fault(int32_t status, int32_t calls) {
+    const bool mid = (status & MQVS_FAULT_MID_CALL) != 0;
+    status &= ~MQVS_FAULT_MID_CALL;
     if (calls < 0 || (calls > 0 && status != MQVS_ERR_DEVICE && status != MQVS_ERR_MEMORY_LIMIT)) {
         set_error("mqvs_inject_fault: status must be MQVS_ERR_DEVICE or MQVS_ERR_MEMORY_LIMIT, calls >= 0");
         return MQVS_ERR_BAD_ARGUMENTS;
     }
     t_fault_status = status;
     t_fault_calls = calls;
+    t_fault_mid = mid;
     return MQVS_OK;
 }
 
@@ -2157,7 +2257,7 @@ int mqvs_merge_shards(int32_t nshards, int32_t nq, int32_t k, int32_t metric, co
             MQVS_HIP(hipMemcpyAsync(out_ids, oi, nout * 8, hipMemcpyDeviceToHost, s));
             MQVS_HIP(hipMemcpyAsync(out_dist, od, nout * 4, hipMemcpyDeviceToHost, s));
         }
-        if (!(devp && (flags & MQVS_F_ASYNC))) MQVS_HIP(hipStreamSynchronize(s));
+        if (!(devp && (flags & MQVS_F_ASYNC))) host_wait(s);
     });
 }
 
@@ -2173,7 +2273,7 @@ int mqvs_generate_device(uint64_t seed, int32_t mode, int64_t row0, int64_t n, i
         ws.last = s;
         launch_generate(seed, mode, row0, n, d, dev_out, s);
         MQVS_HIP(hipGetLastError());
-        MQVS_HIP(hipStreamSynchronize(s));
+        host_wait(s);
     });
 }
 
@@ -2267,6 +2367,15 @@ int mqvs_set_timing(int enabled) {
     return MQVS_OK;
 }
 
+int mqvs_set_wait_mode(int mode, int spin_us) {
+    if (mode < MQVS_WAIT_RUNTIME || mode > MQVS_WAIT_BLOCK) {
+        set_error("mqvs_set_wait_mode: mode must be MQVS_WAIT_RUNTIME, MQVS_WAIT_HYBRID or MQVS_WAIT_BLOCK");
+        return -MQVS_ERR_BAD_ARGUMENTS;
+    }
+    if (spin_us >= 0) g_wait_spin_us.store(spin_us);
+    return g_wait_mode.exchange(mode);
+}
+
 int mqvs_async_check(mqvs_stream_t stream) {
     return guarded([&] {
         int dev = 0;
@@ -2275,7 +2384,7 @@ int mqvs_async_check(mqvs_stream_t stream) {
         WsCall ws_call(ws);
         hipStream_t s = stream ? (hipStream_t)stream : ws.stream;
         ws.last = s;
-        MQVS_HIP(hipStreamSynchronize(s));
+        host_wait(s);
         if (!ws.sticky.p) return;
         int word = 0;
         MQVS_HIP(hipMemcpy(&word, ws.sticky.p, sizeof(int), hipMemcpyDeviceToHost));

@@ -250,12 +250,23 @@ __device__ inline bool row_valid(const ScanParams &p, int64_t r) {
 void launch_scan_small(const ScanParams &p, int metric, bool probe, hipStream_t s);
 void launch_gather_count(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists, int64_t n,
                          int64_t chunk_rows, int tile, int *count, int64_t *offsets, int64_t *totals,
-                         int64_t *host_totals, int *ticket, hipStream_t s);
+                         int64_t *host_totals, int64_t host_gen, int *ticket, hipStream_t s);
 void launch_gather_list(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists, int64_t n,
                         int64_t chunk_rows, int tile, const int *count, const int64_t *offsets, int32_t *list, int64_t list_end,
                         hipStream_t s);
+// Bound pruning of an index re-rank (kernels_rerank.hip): the candidates come
+// sorted by their approximate value; those more than 2 B past the k-th
+// approximate value cannot reach the exact top k and are not re-ranked (same
+// output).  raw = null: every candidate is re-ranked.
+struct RerankPrune {
+    const float *raw = nullptr;           // [nq][ncand] approximate raw values in candidate order (NaN: none)
+    const float *bq = nullptr;            // [nq] bound on |approx - exact| for query variant 0 (k_query_bound)
+    const float *ymax = nullptr;          // device scalar: max |y| over the rows (cosine variant term)
+    unsigned long long *count = nullptr;  // += candidates re-ranked (may be null)
+};
 void launch_rerank_ids(const ScanParams &p, int metric, const int64_t *cand, int ncand, int k,
-                       int64_t id_offset, int64_t *out_ids, float *out_dist, uint4 *scratch, hipStream_t s);
+                       int64_t id_offset, int64_t *out_ids, float *out_dist, uint4 *scratch, hipStream_t s,
+                       const RerankPrune &prune = RerankPrune{});
 void launch_scan_mfma(const ScanParams &p, int metric, bool probe, hipStream_t s);
 void launch_probe_select(const float *probe, int64_t P, int64_t ld, int nq, int k, int metric,
                          uint32_t *tau, int *cand_count, Cand *cand, int cand_cap,
@@ -452,12 +463,14 @@ void launch_ivf_plan_dense(const IvfParams &p, int64_t npos, hipStream_t s);
 void launch_ivf_scan(const IvfParams &p, int metric, int grid, hipStream_t s);
 // expect_len: typical per-query region length (sizes the LDS key cache)
 void launch_ivf_select(const Cand *cand, const int64_t *qstart, int nq, int R, int metric, int64_t *out_rows,
-                       int64_t id_offset, float *out_approx, int64_t expect_len, hipStream_t s, uint4 *gscr = nullptr);
+                       int64_t id_offset, float *out_approx, int64_t expect_len, hipStream_t s, uint4 *gscr = nullptr,
+                       float *out_raw = nullptr);
 void launch_ivf_pack(const float *rows, const float *norms, int d, const int32_t *perm, int64_t npos, int64_t dpad,
                      uint16_t *plane, float *pnorm, hipStream_t s);
 void launch_gather_rows(const float *src, int64_t src_ld, int d, const int64_t *idx, int64_t m, float *dst,
                         hipStream_t s);
-constexpr int kCoarsePickMaxT = 64;  // groups a coarse pick may take per query
+constexpr int kCoarsePickMaxT = 64;  // core groups (and nprobe) of a coarse pick
+constexpr int kCoarsePickCap = 128;  // groups a pick's working set holds (more: its batched overflow path)
 // the coarse step's pick from the batch probe's 16-centroid group maxima
 // (kernels_ivf.hip): per query the T best groups (T <= 64) and every group
 // within 2 bq[q] of the T-th (bq: the query's bf16 bound, k_query_bound;
@@ -466,7 +479,8 @@ constexpr int kCoarsePickMaxT = 64;  // groups a coarse pick may take per query
 void index_thread_release();  // index.hip: the calling thread's index workspaces
 void launch_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T, int nprobe, int metric,
                         const float *q, int64_t qld, const float *cent, const float *cnorm, int64_t ncent, int d,
-                        const float *bq, const float *qnorms, int gs_log2, int nq, int64_t *probes, hipStream_t s);
+                        const float *bq, const float *qnorms, int gs_log2, int nq, int64_t *probes,
+                        unsigned long long *ovf, hipStream_t s);
 // the batch probe by 16-row groups (kernels_p4.hip): p.p4_gmax[q][16 t + r]
 // = the best value of rows [16 r, 16 r + 16) of tile t (p.p4_gld >= 16
 // p.tiles); false when the rows cannot take the batch kernel
@@ -594,6 +608,19 @@ static int guarded(F &&f) {
 
 // mqvs.hip services used by the index path
 hipStream_t thread_stream(int device);
+// The host's wait for the work queued on `s` (every synchronous call ends with
+// one): the policy of mqvs_set_wait_mode -- the runtime's own
+// hipStreamSynchronize, or a short poll of a blocking-sync event's completion
+// followed by a blocking wait on it (the calling thread sleeps instead of
+// holding a core for the length of the search).  The current device must be
+// s's.
+void host_wait(hipStream_t s);
+// poll budget of the hybrid wait (microseconds; 0 in MQVS_WAIT_BLOCK, -1 in
+// MQVS_WAIT_RUNTIME): also bounds the spin on a pinned-memory word
+int wait_spin_us();
+// one pause of a host spin loop (x86 PAUSE: the core yields to its sibling
+// hyper-thread and saves power while polling)
+void cpu_relax();
 double measure_read_sweep(size_t bytes, int reps, hipStream_t s, double *best_ms);
 size_t scratch_budget();  // bytes per scratch buffer of one call (mqvs_set_scratch_budget)
 // FLAT search of a segment (MergeTreeVSManager::vectorScanWithoutIndex);

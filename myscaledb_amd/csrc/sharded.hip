@@ -94,9 +94,15 @@ static Rccl &rccl() {
     } while (0)
 
 // Loopback transport: N virtual ranks of one process on one device (a thread
-// per rank), the all-gathers done as device copies through a shared buffer
-// between host barriers.  It runs exactly the code of mqvs_sharded_search that
-// an RCCL communicator runs, so the multi-rank path is tested on one GPU.
+// per rank), the all-gathers done as device copies through a shared buffer.
+// It runs exactly the code of mqvs_sharded_search that an RCCL communicator
+// runs, so the multi-rank path is tested on one GPU.  Like an RCCL
+// collective, a gather is only ENQUEUED: the ranks meet at host barriers to
+// publish their events, but no rank synchronises its stream -- each stream
+// waits on device for the other ranks' copy-in events before its copy-out
+// (and, before overwriting the buffer, for their copy-outs of the last
+// gather).  A caller that read a result before its stream got there would
+// see it here as it would on RCCL.
 struct LoopGroup {
     int nranks = 0;
     int device = 0;
@@ -107,6 +113,7 @@ struct LoopGroup {
     void *buf = nullptr;  // shared device buffer, nranks * bytes of the current gather
     size_t cap = 0;
     int refs = 0;
+    std::vector<hipEvent_t> in_ev, out_ev;  // per rank: its copy into buf done; its copy out of buf done
     int err_code = MQVS_OK;  // failure of the `last` step of generation err_gen
     std::string err_msg;
     uint64_t err_gen = ~(uint64_t)0;
@@ -184,6 +191,9 @@ void comm_all_gather(mqvs_comm *c, const void *send, void *recv, size_t bytes, h
     const size_t need = bytes * (size_t)g.nranks;
     g.barrier([&] {
         if (g.cap < need) {
+            // (a larger buffer: the last gather's copies out of the old one
+            // finish first -- the only host wait of the transport)
+            for (hipEvent_t e : g.out_ev) MQVS_HIP(hipEventSynchronize(e));
             if (g.buf) (void)hipFree(g.buf);
             g.buf = nullptr;
             g.cap = 0;
@@ -191,12 +201,17 @@ void comm_all_gather(mqvs_comm *c, const void *send, void *recv, size_t bytes, h
             g.cap = need;
         }
     });
+    // every rank has recorded its copy-out of the last gather (before this
+    // barrier): the buffer is free once the streams pass those events
+    for (int r = 0; r < g.nranks; ++r)
+        if (r != c->rank) MQVS_HIP(hipStreamWaitEvent(s, g.out_ev[r], 0));
     if (bytes) MQVS_HIP(hipMemcpyAsync((char *)g.buf + bytes * c->rank, send, bytes, hipMemcpyDeviceToDevice, s));
-    MQVS_HIP(hipStreamSynchronize(s));
+    MQVS_HIP(hipEventRecord(g.in_ev[c->rank], s));
     g.barrier([] {});
+    for (int r = 0; r < g.nranks; ++r)
+        if (r != c->rank) MQVS_HIP(hipStreamWaitEvent(s, g.in_ev[r], 0));
     if (bytes) MQVS_HIP(hipMemcpyAsync(recv, g.buf, need, hipMemcpyDeviceToDevice, s));
-    MQVS_HIP(hipStreamSynchronize(s));
-    g.barrier([] {});
+    MQVS_HIP(hipEventRecord(g.out_ev[c->rank], s));
 }
 
 void comm_group_start(mqvs_comm *c) {
@@ -278,6 +293,12 @@ int mqvs_comm_init_loopback(int32_t nranks, mqvs_comm_t *out) {
         g->nranks = nranks;
         MQVS_HIP(hipGetDevice(&g->device));
         g->refs = nranks;
+        g->in_ev.assign(nranks, nullptr);
+        g->out_ev.assign(nranks, nullptr);
+        for (int r = 0; r < nranks; ++r) {
+            MQVS_HIP(hipEventCreateWithFlags(&g->in_ev[r], hipEventDisableTiming));
+            MQVS_HIP(hipEventCreateWithFlags(&g->out_ev[r], hipEventDisableTiming));
+        }
         for (int r = 0; r < nranks; ++r) {
             auto *c = new mqvs_comm();
             c->nranks = nranks;
@@ -312,7 +333,12 @@ int mqvs_comm_free(mqvs_comm_t c) {
                 last = --g->refs == 0;
             }
             if (last) {
+                for (hipEvent_t e : g->out_ev)
+                    if (e) (void)hipEventSynchronize(e);
                 if (g->buf) (void)hipFree(g->buf);
+                for (auto *v : {&g->in_ev, &g->out_ev})
+                    for (hipEvent_t e : *v)
+                        if (e) (void)hipEventDestroy(e);
                 delete g;
             }
         }
@@ -513,7 +539,7 @@ Fast fast_search(mqvs_comm *c, const CallArgs &a) {
     }
     if (have) merge_out(c, a, b);
     MQVS_HIP(hipMemcpyAsync(ht, hd, sizeof(int64_t) * kHdrWords * c->nranks, hipMemcpyDeviceToHost, a.s));
-    MQVS_HIP(hipStreamSynchronize(a.s));
+    host_wait(a.s);
     if (have && a.nk) search_collect_stats(c->device);
     try {
         for (int r = 0; r < c->nranks; ++r)
@@ -570,7 +596,7 @@ void slow_search(mqvs_comm *c, const CallArgs &a, const ShardCall &call) {
                                    mine + kHdrChunks, a.s);
     comm_all_gather(c, mine, hd, sizeof(int64_t) * kHdrWords, a.s);
     MQVS_HIP(hipMemcpyAsync(ht, hd, sizeof(int64_t) * kHdrWords * c->nranks, hipMemcpyDeviceToHost, a.s));
-    MQVS_HIP(hipStreamSynchronize(a.s));
+    host_wait(a.s);
     for (int r = 0; r < c->nranks; ++r) {
         if (!row(ht, r)[kHdrFast]) continue;
         // A rank on the fast path (its call equals the last validated one)
@@ -586,7 +612,7 @@ void slow_search(mqvs_comm *c, const CallArgs &a, const ShardCall &call) {
             comm_all_gather(c, li, ai, sizeof(int64_t) * nkf, a.s);
             comm_all_gather(c, ld, ad, sizeof(float) * nkf, a.s);
             comm_group_end(c);
-            MQVS_HIP(hipStreamSynchronize(a.s));
+            host_wait(a.s);
         }
         fail(MQVS_ERR_BAD_ARGUMENTS, "ranks disagree on the call: rank " + std::to_string(r) +
                                          " repeated the last sharded search, this rank did not");
@@ -617,7 +643,7 @@ void slow_search(mqvs_comm *c, const CallArgs &a, const ShardCall &call) {
         comm_group_end(c);
         if (local_code == MQVS_OK) merge_out(c, a, b);
         MQVS_HIP(hipMemcpyAsync(ht, hd, sizeof(int64_t) * kHdrWords * c->nranks, hipMemcpyDeviceToHost, a.s));
-        MQVS_HIP(hipStreamSynchronize(a.s));
+        host_wait(a.s);
         for (int r = 0; r < c->nranks; ++r)
             if (!row(ht, r)[kHdrOk])
                 fail(r == c->rank ? local_code : (int)row(ht, r)[kHdrCode],

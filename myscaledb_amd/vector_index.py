@@ -23,7 +23,7 @@ import ctypes
 import numpy as np
 
 from . import _lib
-from ._lib import F_ASYNC, F_DEVICE_PTRS, F_FIRST_STAGE, check, lib
+from ._lib import F_ASYNC, F_DEVICE_PTRS, F_FIRST_STAGE, F_RERANK_ALL, check, lib
 from .vector_scan import VectorScanSegment, _host_f32, _host_u8, _is_torch, _ptr
 
 
@@ -89,11 +89,13 @@ class VectorIndex:
         return buf.reshape(-1)[: nq * npb].reshape(nq, npb).copy()
 
     def search(self, queries, k, params=None, filter_bitmap=None, row_exists=None, first_stage_only=False,
-               out=None, async_=False, stream=None):
+               out=None, async_=False, stream=None, rerank_all=False):
         """(ids[nq,k] int64, dist[nq,k] float32), reference order, -1 padded.
         first_stage_only: the k best rows by the approximate distance (stage 1
-        of a two-stage search; re-rank with compute_top_distance_subset)."""
-        fs = F_FIRST_STAGE if first_stage_only else 0
+        of a two-stage search; re-rank with compute_top_distance_subset).
+        rerank_all: re-rank every num_reorder candidate (MQVS_F_RERANK_ALL; the
+        default bound pruning gives the same results)."""
+        fs = (F_FIRST_STAGE if first_stage_only else 0) | (F_RERANK_ALL if rerank_all else 0)
         pr = _params(params)
         if _is_torch(queries):
             import torch

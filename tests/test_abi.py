@@ -29,7 +29,7 @@ def test_library_exports_every_declared_symbol():
 
 def test_abi_version():
     from myscaledb_amd import _lib
-    assert _lib.lib.mqvs_abi_version() == 3
+    assert _lib.lib.mqvs_abi_version() == 4
 
 
 def test_library_is_gfx950_code_object():

@@ -170,3 +170,76 @@ def test_workspace_budget_bounds_concurrent_index_searches(mq):
     assert st["over_budget"] == 0, st
     assert st["peak"] <= cap, st
     assert st["peak"] > 0, st  # (index scratch is counted)
+
+
+def test_filtered_search_after_mid_call_fault(mq):
+    """a filtered search that fails after queuing its selected-row
+    count (a device failure, or an allocation failure before the host reads
+    the count) must not leak that count into the thread's next filtered
+    search.  The count record carries its call's generation, and the failing
+    call drains its stream.  Drill: mqvs_inject_fault(... | MQVS_FAULT_MID_CALL)
+    fires right after the count launch; the next search -- another filter,
+    another selectivity, so another list length -- returns the same bits as
+    before the fault."""
+    from myscaledb_amd import _lib
+    n, d, nq, k = 300000, 96, 4, 20
+    seg = mq.VectorScanSegment.generate(0x5EED0003, 1, n, d, metric="L2", granule=8192)
+    q = O.generate(0x5EED0004, 1, 0, nq, d)
+    rng = np.random.default_rng(11)
+    fa = mq.pack_bitmap(rng.random(n) < 0.02)
+    fb = mq.pack_bitmap(rng.random(n) < 0.3)
+    try:
+        exp_a = seg.search(q, k, filter_bitmap=fa)
+        exp_b = seg.search(q, k, filter_bitmap=fb)
+        for first, second, exp in ((fa, fb, exp_b), (fb, fa, exp_a)):
+            _lib.check(_lib.lib.mqvs_inject_fault(_lib.ERR_DEVICE | 0x100, 1))
+            with pytest.raises(_lib.MqvsError, match="mid-call"):
+                seg.search(q, k, filter_bitmap=first)
+            ids, dist = seg.search(q, k, filter_bitmap=second)
+            assert np.array_equal(ids, exp[0])
+            assert np.array_equal(dist.view(np.uint32), exp[1].view(np.uint32))
+    finally:
+        _lib.check(_lib.lib.mqvs_inject_fault(0, 0))
+        seg.free()
+
+
+@pytest.mark.parametrize("mode,spin", [(0, -1), (1, 0), (1, 50), (1, 2000), (2, -1)])
+def test_wait_modes_same_results(mq, mode, spin):
+    """mqvs_set_wait_mode (runtime sync, poll-then-sleep with several poll
+    budgets, sleep at once): FLAT searches at nq 1 and 64, a selective
+    PREWHERE search (its mid-call wait for the selected count) and an index
+    search return the same bits in every mode, from several threads at once."""
+    from myscaledb_amd import _lib
+    n, d = 120000, 64
+    seg = mq.VectorScanSegment.generate(0x5EED0005, 2, n, d, metric="Cosine", granule=4096)
+    idx = mq.VectorIndex.build(seg, "MSTG", {"nlist": 64})
+    rng = np.random.default_rng(3)
+    flt = mq.pack_bitmap(rng.random(n) < 0.05)
+    jobs = [(O.generate(50 + i, 2, n, nq, d), nq) for i, nq in enumerate((1, 64, 3, 200))]
+    expected = [(seg.search(q, 20), seg.search(q, 20, filter_bitmap=flt), idx.search(q, 20, {"nprobe": 4}))
+                for q, _ in jobs]
+    prev = _lib.set_wait_mode(mode, spin)
+    errors, results = [], [None] * len(jobs)
+    try:
+        def worker(j):
+            try:
+                mq.init(0)
+                q, _ = jobs[j]
+                results[j] = (seg.search(q, 20), seg.search(q, 20, filter_bitmap=flt), idx.search(q, 20, {"nprobe": 4}))
+                _lib.check(_lib.lib.mqvs_thread_release())
+            except Exception as e:  # noqa: BLE001
+                errors.append(repr(e))
+        threads = [threading.Thread(target=worker, args=(j,)) for j in range(len(jobs))]
+        for t in threads:
+            t.start()
+        for t in threads:
+            t.join()
+    finally:
+        _lib.set_wait_mode(prev, 50)
+        idx.free()
+        seg.free()
+    assert not errors, errors
+    for j, (got, exp) in enumerate(zip(results, expected)):
+        for (gi, gd), (ei, ed) in zip(got, exp):
+            assert np.array_equal(gi, ei), j
+            assert np.array_equal(gd.view(np.uint32), ed.view(np.uint32)), j

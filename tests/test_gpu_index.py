@@ -367,3 +367,71 @@ def test_index_coarse_probes_are_exact_top_nprobe(mq, metric, d, nlist):
                 srt = np.sort(score[i])
                 near_ties += int(srt[nprobe] - srt[nprobe - 1] < 1e3 * tol[i])
     assert near_ties > 0  # the set holds boundaries bf16 alone cannot order
+
+
+@pytest.mark.parametrize("n,nprobe", [(2048, 8), (4096, 60), (4096, 64)])
+def test_index_coarse_pick_overflow_is_exact(mq, n, nprobe):
+    """More near-tie centroid groups than the coarse pick's working set holds
+    (groups past Tcap were cut silently).  With nlist = n and no
+    k-means iteration the centroids are the rows themselves (evenly spaced
+    initial centroids = every row), so they are built to tie: every row holds
+    two ones (inner product 2 with the all-ones query, exactly, in bf16 too),
+    and four rows at the end of the table hold 1 + 2^-12 in place of one of
+    them -- an exact fp32 inner product of 2 + 2^-12 that the bf16 values
+    (both 2) cannot see.  Every one of the n / 8 groups is then within the
+    bound of the nprobe-th value; the pick must score them all (its batched
+    overflow path, counted in the stats) and return the four rows plus the
+    lowest-numbered ties (the (value, centroid) order)."""
+    d = 128
+    rows = np.zeros((n, d), np.float32)
+    i = np.arange(n)
+    rows[i, i % d] = 1.0
+    rows[i, (i // d + 1 + i) % d] = 1.0   # a second column, never the first one
+    special = np.arange(n - 4, n)
+    rows[special, (special // d + 1 + special) % d] = np.float32(1 + 2.0 ** -12)
+    seg = mq.VectorScanSegment.from_rows(rows, metric="IP", granule=1024)
+    idx = mq.VectorIndex.build(seg, "MSTG", {"nlist": n, "kmeans_iters": 0})
+    try:
+        C = idx.centroids()
+        assert np.array_equal(C, rows)   # the construction the test relies on
+        q = np.ones((3, d), np.float32)
+        pr = idx.probes(q, {"nprobe": nprobe})
+        st = mq.vector_index.last_index_stats()
+    finally:
+        idx.free()
+        seg.free()
+    expect = set(special.tolist()) | set(range(nprobe - 4))
+    for r in range(len(q)):
+        assert set(pr[r].tolist()) == expect, (nprobe, sorted(set(pr[r].tolist()) ^ expect)[:8])
+    assert st["pick_overflow"] == len(q), st
+
+
+@pytest.mark.parametrize("metric,nq,fsel,lwd", [("L2", 200, None, None), ("IP", 64, 0.4, None),
+                                                 ("Cosine", 300, 0.5, 0.2), ("L2", 7, None, 0.3),
+                                                 ("Cosine", 12, None, None)])
+def test_index_pruned_rerank_equals_full(mq, metric, nq, fsel, lwd):
+    """The re-rank's bound pruning (candidates more than 2 B past
+    the k-th approximate value cannot reach the exact top k) returns the same
+    ids and distance bits as re-ranking all num_reorder candidates, on both
+    distance formulas (nq < 20: faiss's sequential one), with a PREWHERE
+    filter and deletes, and re-ranks fewer candidates."""
+    n, d, k, R = 40000, 768 if metric == "Cosine" else 128, 50, 400
+    seg = mq.VectorScanSegment.generate(0x5EED0001, 2, n, d, metric=metric, granule=1024)
+    q = O.generate(0x5EED0001, 2, n, nq, d)
+    rng = np.random.default_rng(nq)
+    flt = np.packbits((rng.random(n) < fsel).astype(np.uint8), bitorder="little") if fsel else None
+    ex = np.packbits((rng.random(n) >= lwd).astype(np.uint8), bitorder="little") if lwd else None
+    idx = mq.VectorIndex.build(seg, "MSTG", {"nlist": 64})
+    try:
+        params = {"nprobe": 6, "num_reorder": R}
+        ids_a, dist_a = idx.search(q, k, params, filter_bitmap=flt, row_exists=ex, rerank_all=True)
+        st_a = mq.vector_index.last_index_stats()
+        ids_p, dist_p = idx.search(q, k, params, filter_bitmap=flt, row_exists=ex)
+        st_p = mq.vector_index.last_index_stats()
+    finally:
+        idx.free()
+        seg.free()
+    assert np.array_equal(ids_p, ids_a)
+    assert np.array_equal(dist_p.view(np.uint32), dist_a.view(np.uint32))
+    assert st_a["reranked"] == nq * R
+    assert 0 < st_p["reranked"] < nq * R, st_p

@@ -26,6 +26,8 @@ def main():
                     help="';'-separated search param strings")
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--query-seed", type=lambda x: int(x, 0), default=0x5EED0001)
+    ap.add_argument("--rerank-all", action="store_true",
+                    help="re-rank every num_reorder candidate (MQVS_F_RERANK_ALL: no bound pruning)")
     ap.add_argument("--dbg", action="store_true",
                     help="load the measurement build libmqvs_dbg.so (reads MQVS_* A/B switches)")
     args = ap.parse_args()
@@ -58,18 +60,18 @@ def main():
     dist = torch.empty((args.nq, args.k), dtype=torch.float32, device="cuda")
     from myscaledb_amd.vector_scan import set_timing
     for sp in [s for s in args.search.split(";") if s is not None]:
-        idx.search(q, args.k, sp, out=(ids, dist))
+        idx.search(q, args.k, sp, out=(ids, dist), rerank_all=args.rerank_all)
         walls, sts = [], []
         # stage times from searches with the timing events on; walls without
         set_timing(True)
         for _ in range(3):
-            idx.search(q, args.k, sp, out=(ids, dist))
+            idx.search(q, args.k, sp, out=(ids, dist), rerank_all=args.rerank_all)
             sts.append(last_index_stats())
         set_timing(False)
         for _ in range(args.reps):
             torch.cuda.synchronize()
             t0 = time.perf_counter()
-            idx.search(q, args.k, sp, out=(ids, dist))
+            idx.search(q, args.k, sp, out=(ids, dist), rerank_all=args.rerank_all)
             torch.cuda.synchronize()
             walls.append((time.perf_counter() - t0) * 1e3)
         got = ids.cpu().numpy()
@@ -78,7 +80,7 @@ def main():
         st = min(sts, key=lambda s: s["total_ms"])
         w = min(walls)
         print(json.dumps({
-            "search": sp, "nq": args.nq, "k": args.k, "wall_ms": round(w, 3),
+            "search": sp, "rerank_all": args.rerank_all, "nq": args.nq, "k": args.k, "wall_ms": round(w, 3),
             "qps": round(args.nq / (w / 1e3), 1), "recall_at_10": round(r10, 4),
             "recall_at_100": round(r100, 4),
             **{key: (round(v, 4) if isinstance(v, float) else v) for key, v in st.items()},
