@@ -107,7 +107,7 @@ struct IndexWorkspace final : WsExt {
     hipStream_t side = nullptr;
     int64_t *host = nullptr;  // pinned: the search's stats [4] and status word (one sync, no staging copies)
     GBuf queries, qvars, qnorms, qmu, qlam, status, qhi, probes, cprobes, filter, exists, rows, out_ids, out_dist,
-        ord, dmap, dwords, pdist, cqhi, gmax, crec, cbq, craw, ibq;
+        ord, dmap, dwords, pdist, cqhi, gmax, crec, cbq, craw, ibq, rsurv, rcnt, rrecs, qdelta, pstats;
     ListBufs coarse, fine;
     // WsExt: the owner is between calls (its workspace's `done` event passed:
     // the main stream, which joins the side chain, has drained)
@@ -116,7 +116,7 @@ struct IndexWorkspace final : WsExt {
         size_t b = 0;
         for (GBuf *x : {&queries, &qvars, &qnorms, &qmu, &qlam, &status, &qhi, &probes, &cprobes, &filter, &exists,
                         &rows, &out_ids, &out_dist, &ord, &dmap, &dwords, &pdist, &cqhi, &gmax, &crec, &cbq, &craw,
-                        &ibq}) {
+                        &ibq, &rsurv, &rcnt, &rrecs, &qdelta, &pstats}) {
             b += x->cap;
             x->release();
         }
@@ -677,13 +677,17 @@ static mqvs_index *build_auto(mqvs_segment *seg, const char *index_type, const c
 // probes[nq][nprobe] are list ids; out: the R best rows per query by the
 // approximate distance (+ id_offset; with out_approx, ids and approximate
 // distances for a first-stage result).  ev (optional): events 2..4 after
-// plan, scan and select.
-static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, const float *pnorm,
-                      const int64_t *list_off, int64_t nlist, int64_t npos, int64_t max_list, int64_t dpad, int metric,
-                      const uint16_t *qhi, const float *qnorm, int nq, const int64_t *probes, int nprobe,
-                      const uint8_t *filter, const uint8_t *exists, int R, int64_t *out_rows, int64_t id_offset,
-                      float *out_approx, hipEvent_t *ev, hipStream_t s, bool dense = false,
-                      float *out_raw = nullptr) {
+// plan, scan and select.  pair_stats ([nq][4] words; null: no pair mode):
+// few pairs per list take pair mode (no plan; the select writes each query's
+// stats there).  Returns the stats words of the pass; *per_query: whether
+// they are pair mode's per-query rows.
+static int64_t *list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, const float *pnorm,
+                          const int64_t *list_off, int64_t nlist, int64_t npos, int64_t max_list, int64_t dpad,
+                          int metric, const uint16_t *qhi, const float *qnorm, int nq, const int64_t *probes,
+                          int nprobe, const uint8_t *filter, const uint8_t *exists, int R, int64_t *out_rows,
+                          int64_t id_offset, float *out_approx, hipEvent_t *ev, hipStream_t s, bool dense = false,
+                          float *out_raw = nullptr, int64_t *pair_stats = nullptr, bool *per_query = nullptr) {
+    if (per_query) *per_query = false;
     const int64_t E = (int64_t)nq * nprobe;
     IvfParams p{};
     p.plane = plane;
@@ -723,6 +727,40 @@ static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, c
     // dependent loads was a large part of a 256-position list's scan; mode 3
     // nprobe 1 scan 0.139 -> 0.117 ms, profiles/r05/index_scan/)
     p.chunk = dense ? kIvfChunk : std::max(64, tune_int("MQVS_IVF_CHUNK", 8 * p.qg) / 64 * 64);
+    // Pair mode: with about one query per probed list the plan groups
+    // nothing; it only orders the pairs (six launches over every list: ~43 us
+    // at 39063 lists, nq 1000, nprobe 1).  Instead every (pair, slice) is a
+    // work item of its own, each query's region a fixed stride.  Lists probed
+    // by several queries are then read once per query (mode 2 at nprobe 1:
+    // ~10 % of its list bytes twice).
+    const bool pairs = pair_stats && !dense && p.qg == 16 && 16 * E <= nlist && max_list > 0 &&
+                       (double)nq * nprobe * (max_list / p.chunk + 1) < 2e9 && tune_int("MQVS_IVF_PAIR", 1) == 1;
+    if (pairs) {
+        p.pair_stride = (int64_t)nprobe * max_list;
+        p.pair_nch = (int)((max_list + p.chunk - 1) / p.chunk);
+        p.stats = pair_stats;
+        p.cand = (Cand *)b.cand.get(sizeof(Cand) * (size_t)std::max<int64_t>((int64_t)nq * p.pair_stride, 1));
+        if (ev) MQVS_HIP(hipEventRecord(ev[2], s));
+        launch_ivf_scan(p, metric, tune_int("MQVS_IVF_GRID", 4096), s);
+        MQVS_HIP(hipGetLastError());
+        if (ev) MQVS_HIP(hipEventRecord(ev[3], s));
+        IvfRegions rg;
+        rg.stride = p.pair_stride;
+        rg.nprobe = nprobe;
+        rg.nlist = (int)nlist;
+        rg.chunk = p.chunk;
+        rg.dpad = dpad;
+        rg.probes = probes;
+        rg.list_off = list_off;
+        rg.stats = pair_stats;
+        const int64_t expect = (int64_t)((double)nprobe * npos / std::max<int64_t>(nlist, 1) * 1.5);
+        uint4 *gscr = R > kSortCap ? (uint4 *)b.large.get(sizeof(uint4) * 2 * (size_t)R * nq) : nullptr;
+        launch_ivf_select(p.cand, rg, nq, R, metric, out_rows, id_offset, out_approx, expect, s, gscr, out_raw);
+        MQVS_HIP(hipGetLastError());
+        if (ev) MQVS_HIP(hipEventRecord(ev[4], s));
+        if (per_query) *per_query = true;
+        return pair_stats;
+    }
     const int64_t max_items = (E / p.qg + std::min<int64_t>(E, nlist)) * (max_list / p.chunk + 1);
     p.item_list = (int *)b.items.get(sizeof(int) * max_items);
     p.item_grp = (int *)b.grp.get(sizeof(int) * max_items);
@@ -749,9 +787,12 @@ static void list_pass(ListBufs &b, const uint16_t *plane, const int32_t *perm, c
     const int64_t expect = dense ? npos : (int64_t)((double)nprobe * npos / std::max<int64_t>(nlist, 1) * 1.5);
     // R above kSortCap: the select sorts through 2 R records of scratch per query
     uint4 *gscr = R > kSortCap ? (uint4 *)b.large.get(sizeof(uint4) * 2 * (size_t)R * nq) : nullptr;
-    launch_ivf_select(p.cand, p.qstart, nq, R, metric, out_rows, id_offset, out_approx, expect, s, gscr, out_raw);
+    IvfRegions rg;
+    rg.qstart = p.qstart;
+    launch_ivf_select(p.cand, rg, nq, R, metric, out_rows, id_offset, out_approx, expect, s, gscr, out_raw);
     MQVS_HIP(hipGetLastError());
     if (ev) MQVS_HIP(hipEventRecord(ev[4], s));
+    return p.stats;
 }
 
 // mqvs_index_probes sets this for the duration of one search: the coarse
@@ -878,6 +919,9 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     int *status = (int *)ws.status.get(sizeof(int) * 8);
     launch_fill2(reinterpret_cast<uint32_t *>(status), 8, 0u, nullptr, 0, 0u, s);
     auto *istat = reinterpret_cast<unsigned long long *>(status + 4);
+    // the fine pass's per-query stats in pair mode
+    auto *pstats = (int64_t *)ws.pstats.get(sizeof(int64_t) * 4 * (size_t)nq);
+    bool stats_per_query = false;
     // Cosine: only variant 0 is needed before the exact re-rank (coarse step,
     // list scan), so the rest of the chain -- a sequential fp32 sum per
     // normalisation, up to kMaxVariants of them: 60-130 us at nq 1000 -- runs
@@ -892,11 +936,13 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     // profiles/r04/index/fork_ab.jsonl).  MQVS_IVF_FORK=0 (measurement build):
     // start it right after variant 0.
     const bool late_fork = tune_int("MQVS_IVF_FORK", 1) == 1;
+    float *qdelta = nullptr;  // cosine, pruned re-rank: the chain's variant spread (k_query_prep phase 2)
     auto fork_chain = [&]() {
         MQVS_HIP(hipEventRecord(ws.fork, s));
         MQVS_HIP(hipStreamWaitEvent(ws.side, ws.fork, 0));
         forked = true;
-        launch_query_prep(dq, nq, d, MQVS_METRIC_COSINE, false, qvars, maxv, qnorms, qmu, qlam, status, ws.side, 2);
+        launch_query_prep(dq, nq, d, MQVS_METRIC_COSINE, false, qvars, maxv, qnorms, qmu, qlam, status, ws.side, 2,
+                          qdelta);
         MQVS_HIP(hipGetLastError());
         MQVS_HIP(hipEventRecord(ws.join, ws.side));
     };
@@ -1007,6 +1053,7 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     if (prune) {
         craw = (float *)ws.craw.get(sizeof(float) * (size_t)nq * R);
         ibq = (float *)ws.ibq.get(sizeof(float) * (size_t)nq);
+        if (split && late_fork) qdelta = (float *)ws.qdelta.get(sizeof(float) * (size_t)nq);
         if (!qrec0) {
             qrec0 = (float *)ws.crec.get(sizeof(float) * kMxRec * (size_t)nq);
             launch_to_hi(qvars, nq, d, (int64_t)maxv * qstride, ix->dpad, 1, rup(nq, 16), nullptr, qrec0, nullptr, s);
@@ -1025,15 +1072,16 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     // ---- fine: the probed lists
     int64_t *dstats = nullptr;
     if (first_stage) {
-        list_pass(ws.fine, ix->plane, ix->perm, ix->pnorm, ix->list_off, ix->nlist, ix->npos, ix->max_list, ix->dpad,
-                  ix->metric, qhi, qnorms, nq, probes, nprobe, dfilter, dexists, R, dids, seg->row_offset, ddist,
-                  tev ? ws.ev : nullptr, s);
+        dstats = list_pass(ws.fine, ix->plane, ix->perm, ix->pnorm, ix->list_off, ix->nlist, ix->npos, ix->max_list,
+                           ix->dpad, ix->metric, qhi, qnorms, nq, probes, nprobe, dfilter, dexists, R, dids,
+                           seg->row_offset, ddist, tev ? ws.ev : nullptr, s, false, nullptr, pstats,
+                           &stats_per_query);
         MQVS_HIP(hipEventRecord(ws.ev[5], s));
     } else {
         int64_t *crow = (int64_t *)ws.rows.get(sizeof(int64_t) * (size_t)nq * R);
-        list_pass(ws.fine, ix->plane, ix->perm, ix->pnorm, ix->list_off, ix->nlist, ix->npos, ix->max_list, ix->dpad,
-                  ix->metric, qhi, qnorms, nq, probes, nprobe, dfilter, dexists, R, crow, 0, nullptr,
-                  tev ? ws.ev : nullptr, s, false, craw);
+        dstats = list_pass(ws.fine, ix->plane, ix->perm, ix->pnorm, ix->list_off, ix->nlist, ix->npos, ix->max_list,
+                           ix->dpad, ix->metric, qhi, qnorms, nq, probes, nprobe, dfilter, dexists, R, crow, 0,
+                           nullptr, tev ? ws.ev : nullptr, s, false, craw, pstats, &stats_per_query);
         // ---- exact re-rank (needs the whole variant chain)
         if (split) {
             MQVS_HIP(hipStreamWaitEvent(s, ws.join, 0));
@@ -1074,12 +1122,23 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
             pr.raw = craw;
             pr.bq = ibq;
             pr.ymax = seg->ynorm_max;
+            pr.qdelta = qdelta;
         }
-        launch_rerank_ids(rp, ix->metric, crow, R, k, seg->row_offset, dids, ddist, rscr, s, pr);
+        // over waves (k_rerank_plan + k_exact_records_w + k_sort_emit): the
+        // pruned candidates of every query spread over the chip (mode 3,
+        // nprobe 1: see DESIGN 3.7); MQVS_IVF_RR=0 (measurement build): one
+        // workgroup per query
+        bool wide = false;
+        if (R <= kSortCap && tune_int("MQVS_IVF_RR", 0) == 1) {
+            auto *sv = (uint32_t *)ws.rsurv.get(sizeof(uint32_t) * (size_t)nq * R);
+            auto *sc = (int *)ws.rcnt.get(sizeof(int) * (size_t)nq);
+            auto *sr = (uint4 *)ws.rrecs.get(sizeof(uint4) * (size_t)nq * R);
+            wide = launch_rerank_ids_wide(rp, ix->metric, crow, R, k, seg->row_offset, dids, ddist, pr, sv, sc, sr, s);
+        }
+        if (!wide) launch_rerank_ids(rp, ix->metric, crow, R, k, seg->row_offset, dids, ddist, rscr, s, pr);
         MQVS_HIP(hipGetLastError());
         MQVS_HIP(hipEventRecord(ws.ev[5], s));
     }
-    dstats = (int64_t *)ws.fine.stats.get(sizeof(int64_t) * 8);
 
     // decoupled part: results in the new part's row ids (VIWithDataPart.cpp:938-943)
     if (dev && ix->row_ids_map) launch_map_ids(dids, (int64_t)nq * k, ix->row_ids_map, s);
@@ -1092,7 +1151,7 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     }
     int64_t *hs = ws.host;
     int *hst = reinterpret_cast<int *>(ws.host + 4);
-    launch_words_to_host(dstats, 4, status, 8, hs, hst, s);
+    launch_words_to_host(dstats, 4, status, 8, hs, hst, s, stats_per_query ? dstats : nullptr, nq);
     MQVS_HIP(hipGetLastError());
     host_wait(s);
     const int hstatus = *hst;

@@ -113,9 +113,7 @@ __global__ __launch_bounds__(256) void k_to_hi(const float *src, int64_t rows, i
 void launch_to_hi(const float *src, int64_t rows, int d, int64_t src_stride, int64_t dpad, int64_t vgroup,
                   int64_t vpad, uint16_t *hi, float *rec, float *maxrec, hipStream_t s) {
     if (rows <= 0) return;
-    int dev = 0, cus = 0;
-    MQVS_HIP(hipGetDevice(&dev));
-    MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int cus = device_cus();
     const int64_t blocks = std::min<int64_t>((rows + 3) / 4, (int64_t)cus * 16);
     hipLaunchKernelGGL(k_to_hi, dim3((unsigned)blocks), dim3(256), 0, s, src, rows, d, src_stride, dpad, vgroup, vpad,
                        hi, rec, maxrec);

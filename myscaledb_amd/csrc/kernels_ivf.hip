@@ -425,6 +425,114 @@ __global__ __launch_bounds__(kPlanThreads) void k_plan_queries(IvfParams p) {
     }
 }
 
+// Plan for few pairs (E = nq * nprobe <= kPlanSmallE; nprobe 1..4 at nq
+// 1000), in ONE workgroup: the (list, pair) keys are sorted in LDS, so the
+// lists a query batch actually probes are runs of the sorted keys -- the
+// general plan above scans every list of the index (39063: zero-fill, count,
+// two passes over the lists, scatter, query scan = six launches, ~43 us at
+// nq 1000, nprobe 1).  Outputs are the general plan's: lstart / lcount of the
+// probed lists (the scan reads no other), the pairs grouped by list in lq,
+// items in list order, the query regions (qbase, qstart) and the stats.
+constexpr int kPlanSmallE = 4096;
+__global__ __launch_bounds__(kPlanThreads) void k_plan_small(IvfParams p) {
+    __shared__ uint64_t key[kPlanSmallE];
+    __shared__ int64_t sh[kPlanThreads + 1];
+    __shared__ unsigned long long s_rows;
+    const int t = threadIdx.x;
+    const int E = p.nq * p.nprobe;
+    const int qs = p.qg == 64 ? 6 : p.qg == 32 ? 5 : 4;  // qg is 16, 32 or 64
+    int N = 1;
+    while (N < E) N <<= 1;
+    for (int i = t; i < N; i += kPlanThreads) {
+        uint64_t k = ~0ull;
+        if (i < E) {
+            const int64_t l = p.probes[i];
+            if (l >= 0 && l < p.nlist) k = ((uint64_t)l << 32) | (uint32_t)i;
+        }
+        key[i] = k;
+    }
+    if (t == 0) s_rows = 0;
+    __syncthreads();
+    for (int size = 2; size <= N; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = t; i < (N >> 1); i += kPlanThreads) {
+                const int lo = 2 * stride * (i / stride) + (i % stride), hi = lo + stride;
+                const bool up = (lo & size) == 0;
+                const uint64_t a = key[lo], b = key[hi];
+                if ((b < a) == up) {
+                    key[lo] = b;
+                    key[hi] = a;
+                }
+            }
+            __syncthreads();
+        }
+    // valid keys [0, Ev); a run of one list starts where the list changes
+    auto list_at = [&](int i) { return (int)(key[i] >> 32); };
+    auto valid = [&](int i) { return key[i] != ~0ull; };
+    auto head = [&](int i) { return valid(i) && (i == 0 || list_at(i - 1) != list_at(i)); };
+    // run length: the first position of a larger list (binary search)
+    auto run_len = [&](int i) {
+        const uint64_t bound = ((uint64_t)(uint32_t)list_at(i) + 1) << 32;
+        int lo = i + 1, hi = N;
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (key[mid] < bound) lo = mid + 1;
+            else hi = mid;
+        }
+        return lo - i;
+    };
+    auto list_len = [&](int l) { return (int)(p.list_off[l + 1] - p.list_off[l]); };
+    const int64_t nitems = block_exclusive_scan(
+        N,
+        [&](int64_t i) -> int64_t {
+            if (!head((int)i)) return 0;
+            const int g = (run_len((int)i) + p.qg - 1) >> qs;
+            return (int64_t)g * ((list_len(list_at((int)i)) + p.chunk - 1) / p.chunk);
+        },
+        [&](int64_t i, int64_t r1) {
+            if (!valid((int)i)) return;
+            const int l = list_at((int)i);
+            p.lq[i] = (int)(uint32_t)key[i];
+            if (!head((int)i)) return;
+            const int c = run_len((int)i), len = list_len(l);
+            const int g = (c + p.qg - 1) >> qs, nc = (len + p.chunk - 1) / p.chunk;
+            p.lstart[l] = i;
+            p.lcount[l] = c;
+            atomicAdd(&s_rows, (unsigned long long)g * (unsigned long long)len);
+            for (int j = 0; j < g; ++j)
+                for (int cc = 0; cc < nc; ++cc) {
+                    p.item_list[r1] = l;
+                    p.item_grp[r1] = j;
+                    p.item_chk[r1] = cc;
+                    ++r1;
+                }
+        },
+        sh);
+    // per query: its probes' regions back to back in probe order, then the
+    // exclusive scan of the query totals
+    for (int q = t; q < p.nq; q += kPlanThreads) {
+        int64_t tot = 0;
+        for (int r = 0; r < p.nprobe; ++r) {
+            const int64_t e = (int64_t)q * p.nprobe + r;
+            const int64_t l = p.probes[e];
+            p.qbase[e] = tot;
+            if (l >= 0 && l < p.nlist) tot += p.list_off[l + 1] - p.list_off[l];
+        }
+        p.qstart[q] = tot;
+    }
+    __syncthreads();
+    const int64_t total = block_exclusive_scan(
+        p.nq, [&](int64_t i) { return p.qstart[i]; }, [&](int64_t i, int64_t v) { p.qstart[i] = v; }, sh);
+    if (t == 0) {
+        p.qstart[p.nq] = total;
+        *p.nitems = (int)nitems;
+        p.stats[0] = total;
+        p.stats[1] = nitems;
+        p.stats[2] = (int64_t)s_rows * p.dpad * 2;
+        p.stats[3] = E;
+    }
+}
+
 // Plan for the dense case (every query probes every list, probe r = list r:
 // the coarse quantizer's centroid chunks), in one grid kernel.
 __global__ __launch_bounds__(256) void k_plan_dense(IvfParams p, int64_t npos) {
@@ -458,6 +566,41 @@ __global__ __launch_bounds__(256) void k_plan_dense(IvfParams p, int64_t npos) {
     }
 }
 
+// query q's candidate region (start, length)
+__device__ inline void ivf_region(const IvfRegions &g, int q, int64_t &start, int64_t &T) {
+    if (g.qstart) {
+        start = g.qstart[q];
+        T = g.qstart[q + 1] - start;
+        return;
+    }
+    start = (int64_t)q * g.stride;
+    T = 0;
+    for (int r = 0; r < g.nprobe; ++r) {
+        const int64_t l = g.probes[(int64_t)q * g.nprobe + r];
+        if (l >= 0 && l < g.nlist) T += g.list_off[l + 1] - g.list_off[l];
+    }
+}
+
+// pair mode's stats (the plan's in the grouped mode), by the select: query
+// q's [values, items, plane bytes, pairs] to stats[4 q ..] (summed by the
+// final copy, k_words_to_host: 4 atomics per query on the same 4 words
+// serialised the select, 26 -> 75 us at nq 1000)
+__device__ inline void ivf_pair_stats(const IvfRegions &g, int q, int64_t T, bool leader) {
+    if (g.qstart || !g.stats || !leader) return;
+    int64_t items = 0, pairs = 0;
+    for (int r = 0; r < g.nprobe; ++r) {
+        const int64_t l = g.probes[(int64_t)q * g.nprobe + r];
+        if (l < 0 || l >= g.nlist) continue;
+        items += (g.list_off[l + 1] - g.list_off[l] + g.chunk - 1) / g.chunk;
+        ++pairs;
+    }
+    int64_t *o = g.stats + 4 * (int64_t)q;
+    o[0] = T;
+    o[1] = items;
+    o[2] = T * g.dpad * 2;
+    o[3] = pairs;
+}
+
 // Scan work item = one list x up to 16 QB queries (QB MFMA B blocks).  The
 // query tile sits in LDS (row stride 2 dpad + 16 B: the 16 rows of a B block
 // hit distinct bank groups).  Each wave takes 16-row blocks of the list; lane
@@ -484,11 +627,29 @@ __global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
     const int64_t qstr = 2 * p.dpad + 16;
     const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
     const int l16 = lane & 15, c = lane >> 4;
-    const int nitems = *p.nitems;
+    const int nitems = p.pair_stride ? p.nq * p.nprobe * p.pair_nch : *p.nitems;
     const int cpr = (int)(p.dpad / 8);  // 16-B chunks per query row
     const int ngrp = (int)((p.dpad / 64 + kIvfWin - 1) / kIvfWin);
     for (int it = blockIdx.x; it < nitems; it += gridDim.x) {
-        const int l = p.item_list[it], g = p.item_grp[it], chk = p.item_chk[it];
+        int l, g, chk, pe = -1;
+        if (p.pair_stride) {
+            // pair mode: one query's probe; slices past its list's end are
+            // empty.  Slice-major (slice 0 of every pair first): pair-major
+            // gave the workgroups of the first slices two items each and the
+            // rest none (scan 82 -> 169 us at nq 1000, nprobe 1)
+            const int E = p.nq * p.nprobe;
+            chk = it / E;
+            pe = it - chk * E;
+            g = 0;
+            const int64_t ll = p.probes[pe];
+            if (ll < 0 || ll >= p.nlist) continue;  // (uniform over the workgroup)
+            l = (int)ll;
+            if ((int64_t)chk * p.chunk >= p.list_off[l + 1] - p.list_off[l]) continue;
+        } else {
+            l = p.item_list[it];
+            g = p.item_grp[it];
+            chk = p.item_chk[it];
+        }
         const int64_t pos0 = p.list_off[l];
         const int cb = p.chunk / 16;  // 16-position blocks per work item
         const int nb = (int)min<int64_t>((p.list_off[l + 1] - pos0) / 16, (int64_t)(chk + 1) * cb);
@@ -519,13 +680,30 @@ __global__ __launch_bounds__(256) void k_ivf_scan(IvfParams p) {
         // positions per list the item setup is a large part of an item
         ivf_bf16x8 cur[2 * kIvfWin], nxt[2 * kIvfWin];
         if (nsteps > 0) load(0, cur);
-        const int cnt = min(QG, p.lcount[l] - g * QG);
+        const int cnt = p.pair_stride ? 1 : min(QG, p.lcount[l] - g * QG);
         __syncthreads();  // the previous item's readers are done with qtile
         if (threadIdx.x < QG) {
             const int j = threadIdx.x;
-            const int e = j < cnt ? p.lq[p.lstart[l] + (int64_t)g * QG + j] : -1;
+            int e = -1;
+            int64_t base = 0;
+            if (p.pair_stride) {
+                // the pair's region: its query's stride, after the lists of
+                // the query's earlier probes
+                if (j == 0) {
+                    e = pe;
+                    const int q = e / p.nprobe, r = e - q * p.nprobe;
+                    base = (int64_t)q * p.pair_stride;
+                    for (int r2 = 0; r2 < r; ++r2) {
+                        const int64_t l2 = p.probes[(int64_t)q * p.nprobe + r2];
+                        if (l2 >= 0 && l2 < p.nlist) base += p.list_off[l2 + 1] - p.list_off[l2];
+                    }
+                }
+            } else {
+                e = j < cnt ? p.lq[p.lstart[l] + (int64_t)g * QG + j] : -1;
+                base = e >= 0 ? p.qstart[e / p.nprobe] + p.qbase[e] : 0;
+            }
             s_ent[j] = e;
-            s_base[j] = e >= 0 ? p.qstart[e / p.nprobe] + p.qbase[e] : 0;
+            s_base[j] = base;
             s_qn[j] = (e >= 0 && METRIC == MQVS_METRIC_L2) ? p.qnorm[e / p.nprobe] : 0.f;
         }
         __syncthreads();
@@ -618,7 +796,7 @@ constexpr int kTieCap = 64;  // <= every NT the kernel is launched with
 // 2 R records of global scratch per query (gscr) and are sorted there by
 // global_sort (LDS runs of kSortCap, then merge passes); NT = SEL_THREADS.
 template <int METRIC, int NT, bool LARGE = false>
-__global__ __launch_bounds__(NT) void k_ivf_select(const Cand *cand, const int64_t *qstart, int R,
+__global__ __launch_bounds__(NT) void k_ivf_select(const Cand *cand, IvfRegions rg, int R,
                                                    int64_t *out_rows, int64_t id_offset, float *out_approx,
                                                    int keycap, uint4 *gscr, float *out_raw) {
     // pow2 >= R records (LARGE: kSortCap, the sort runs), then the key cache
@@ -635,8 +813,10 @@ __global__ __launch_bounds__(NT) void k_ivf_select(const Cand *cand, const int64
     const int q = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     uint4 *rr = LARGE ? gscr + (int64_t)q * 2 * R : recs;  // the records (LARGE: [0, R); [R, 2R) sort scratch)
     const int mcap = LARGE ? R : N;                        // room for records below th + ties
-    const Cand *c = cand + qstart[q];
-    const int64_t T = qstart[q + 1] - qstart[q];
+    int64_t rs0 = 0, T = 0;
+    ivf_region(rg, q, rs0, T);
+    ivf_pair_stats(rg, q, T, threadIdx.x == 0);
+    const Cand *c = cand + rs0;
     auto gkey = [&](int64_t i) {
         const Cand e = c[i];
         return e.row == 0xFFFFFFFFu ? 0xFFFFFFFFu : okey<METRIC>(e.raw);
@@ -783,14 +963,16 @@ __global__ __launch_bounds__(NT) void k_ivf_select(const Cand *cand, const int64
 // min over the lanes per pop).  Order = (key, row), like k_ivf_select for a
 // monotone perm.
 template <int METRIC, int RM>
-__global__ __launch_bounds__(256) void k_ivf_select_small(const Cand *cand, const int64_t *qstart, int nq, int R,
+__global__ __launch_bounds__(256) void k_ivf_select_small(const Cand *cand, IvfRegions rg, int nq, int R,
                                                          int64_t *out_rows, int64_t id_offset, float *out_approx) {
     constexpr int U = 8;
     const int lane = threadIdx.x & 63;
     const int q = blockIdx.x * 4 + (threadIdx.x >> 6);
     if (q >= nq) return;  // wave-uniform
-    const Cand *c = cand + qstart[q];
-    const int64_t T = qstart[q + 1] - qstart[q];
+    int64_t rs0 = 0, T = 0;
+    ivf_region(rg, q, rs0, T);
+    ivf_pair_stats(rg, q, T, lane == 0);
+    const Cand *c = cand + rs0;
     uint64_t best[RM];
 #pragma unroll
     for (int i = 0; i < RM; ++i) best[i] = ~0ull;
@@ -914,13 +1096,19 @@ void launch_iota_probes(int64_t *probes, int nq, int np, hipStream_t s) {
 }
 
 void launch_ivf_plan(const IvfParams &p, hipStream_t s) {
+    const int64_t E = (int64_t)p.nq * p.nprobe;
+    if (E <= kPlanSmallE && tune_int("MQVS_IVF_PLAN", 0) == 0) {
+        hipLaunchKernelGGL(k_plan_small, dim3(1), dim3(kPlanThreads), 0, s, p);
+        return;
+    }
     // (lfill: zeroed by the list pass; a fill kernel, not hipMemsetAsync: the
     // runtime's fill took two launches)
     launch_fill2(reinterpret_cast<uint32_t *>(p.lcount), p.nlist, 0u, nullptr, 0, 0u, s);
-    const int64_t E = (int64_t)p.nq * p.nprobe;
     const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((std::max(E, (int64_t)p.nq) + 255) / 256, 2048));
     hipLaunchKernelGGL(k_plan_count, dim3(grid), dim3(256), 0, s, p);
-    const int plan = tune_int("MQVS_IVF_PLAN", 0);  // A/B (measurement build): 1 one workgroup, 2 register walk
+    // A/B (measurement build): 1 one workgroup, 2 register walk, 3 the list
+    // kernels even for few pairs (k_plan_small above otherwise)
+    const int plan = tune_int("MQVS_IVF_PLAN", 0);
     if (plan == 1) {
         hipLaunchKernelGGL(k_plan_lists, dim3(1), dim3(kPlanThreads), 0, s, p);
     } else if (plan == 2) {
@@ -977,13 +1165,13 @@ void launch_ivf_scan(const IvfParams &p, int metric, int grid, hipStream_t s) {
         ivf_scan_nt<false>(p, metric, grid, s);
 }
 
-void launch_ivf_select(const Cand *cand, const int64_t *qstart, int nq, int R, int metric, int64_t *out_rows,
+void launch_ivf_select(const Cand *cand, const IvfRegions &rg, int nq, int R, int metric, int64_t *out_rows,
                        int64_t id_offset, float *out_approx, int64_t expect_len, hipStream_t s, uint4 *gscr,
                        float *out_raw) {
     if (R <= 16 && !out_approx && !out_raw) {
         const dim3 grid((unsigned)((nq + 3) / 4));
 #define MQVS_SMALL(M, RM_) \
-    hipLaunchKernelGGL((k_ivf_select_small<M, RM_>), grid, dim3(256), 0, s, cand, qstart, nq, R, out_rows, id_offset, \
+    hipLaunchKernelGGL((k_ivf_select_small<M, RM_>), grid, dim3(256), 0, s, cand, rg, nq, R, out_rows, id_offset, \
                        out_approx)
 #define MQVS_SMALL_M(M)              \
     if (R <= 2) MQVS_SMALL(M, 2);      \
@@ -1016,12 +1204,12 @@ void launch_ivf_select(const Cand *cand, const int64_t *qstart, int nq, int R, i
     do {                                                                                                            \
         if (large)                                                                                                  \
             hipLaunchKernelGGL((k_ivf_select<M, SEL_THREADS, true>), dim3(nq), dim3(SEL_THREADS), lds, s, cand,     \
-                               qstart, R, out_rows, id_offset, out_approx, keycap, gscr, out_raw);                  \
+                               rg, R, out_rows, id_offset, out_approx, keycap, gscr, out_raw);                  \
         else if (wide)                                                                                              \
-            hipLaunchKernelGGL((k_ivf_select<M, 1024>), dim3(nq), dim3(1024), lds, s, cand, qstart, R, out_rows,    \
+            hipLaunchKernelGGL((k_ivf_select<M, 1024>), dim3(nq), dim3(1024), lds, s, cand, rg, R, out_rows,    \
                                id_offset, out_approx, keycap, nullptr, out_raw);                                    \
         else                                                                                                        \
-            hipLaunchKernelGGL((k_ivf_select<M, SEL_THREADS>), dim3(nq), dim3(SEL_THREADS), lds, s, cand, qstart, R, \
+            hipLaunchKernelGGL((k_ivf_select<M, SEL_THREADS>), dim3(nq), dim3(SEL_THREADS), lds, s, cand, rg, R, \
                                out_rows, id_offset, out_approx, keycap, nullptr, out_raw);                          \
     } while (0)
     switch (metric) {
@@ -1091,7 +1279,7 @@ constexpr int kPickU = 4;
 constexpr int kPickBest = kCoarsePickMaxT;  // running top-nprobe records of an overflowing pick (nprobe <= it)
 
 template <int METRIC, bool STAGED>  // METRIC: MQVS_METRIC_L2 or kMetricIpRaw (the coarse metric)
-__global__ __launch_bounds__(SEL_THREADS) void k_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T,
+__global__ __launch_bounds__(SEL_THREADS) __attribute__((amdgpu_waves_per_eu(4))) void k_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T,
                                                              int Tcap, int nprobe, const float *q, int64_t qld,
                                                              const float *cent, const float *cnorm, int64_t ncent,
                                                              int d, const float *bq, const float *qnorms,

@@ -234,10 +234,15 @@ __device__ __forceinline__ float seq_sq_sum_lanes(const float (&x)[J], float *pr
 // phases (seq_sq_sum_lanes, the launcher's); bit-identical tables,
 // tools/qprep_sum_ab.hip, profiles/r05/qprep_sum_ab.jsonl
 constexpr int kLaneSigMax = 32;  // variants whose per-lane signatures fit LDS (33 x 256 B)
+// qdelta (may be null; cosine): per query an upper bound on the largest
+// |x_v - x_0| over the variants the chain produces (the index re-rank's bound
+// pruning compares exact values of variant x_v with variant-0 approximations):
+// per lane the largest fp64 partial sum of squares over the variants, summed
+// over the lanes (a sum of maxima bounds the maximum of sums), rounded up.
 template <int J, int SUMV = 0, bool LANESIG = false>
 __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d, int metric, int blas, float *qvars,
                                                    int maxv, float *qnorms, int *qmu, int *qlam, int *status,
-                                                   int phase) {
+                                                   int phase, float *qdelta) {
     __shared__ __attribute__((aligned(16))) float prod[SUMV ? 64 * J : 1];
     auto sqsum = [&](const float(&xx)[J]) -> float {
         if constexpr (SUMV == 3)
@@ -262,6 +267,7 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
     }
     if (metric != MQVS_METRIC_COSINE) {
         if (phase == 2) return;
+        if (qdelta && lane == 0) qdelta[j] = 0.0f;
         // (columns d .. qs: zeros; the table is not cleared beforehand and
         // the padded readers take them)
 #pragma unroll
@@ -285,12 +291,34 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
     // hash per variant, wave-reduced.
     extern __shared__ uint64_t sig[];  // LANESIG: [maxv + 1][64] uint32; else maxv + 1 uint64
     uint32_t *lsig = reinterpret_cast<uint32_t *>(sig);
+    float x0[J];
+    double dl = 0.0;
+    auto put_delta = [&]() {
+        if (!qdelta) return;
+        double t = dl;
+        for (int off = 32; off > 0; off >>= 1) t += __shfl_xor(t, off);
+        if (lane == 0) qdelta[j] = (float)(sqrt(t) * (1.0 + 1e-6)) + 1e-30f;
+    };
     for (int v = 0; v <= maxv; ++v) {
         const float sum = sqsum(x);
         if (!(sum < eps)) {
             const float sr = sqrtf(sum);
 #pragma unroll
             for (int u = 0; u < J; ++u) x[u] = x[u] / sr;
+        }
+        if (qdelta) {
+            if (v == 0) {
+#pragma unroll
+                for (int u = 0; u < J; ++u) x0[u] = x[u];
+            } else {
+                double ss = 0.0;
+#pragma unroll
+                for (int u = 0; u < J; ++u) {
+                    const double e = (double)x[u] - (double)x0[u];
+                    ss += e * e;
+                }
+                dl = ss > dl ? ss : dl;
+            }
         }
         if (v < maxv && (phase != 2 || v > 0)) {
             float *cur = v0 + (int64_t)v * qs;
@@ -356,10 +384,12 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
                 float4 *z = reinterpret_cast<float4 *>(v0 + (int64_t)v * qs);
                 const int64_t n4 = (int64_t)(maxv - v) * qs / 4;
                 for (int64_t i = lane; i < n4; i += 64) z[i] = make_float4(0.f, 0.f, 0.f, 0.f);
+                put_delta();
                 return;
             }
         }
     }
+    put_delta();
     if (lane == 0) {
         // no repeat within maxv + 1 normalisations: variants 0..maxv-1 are
         // exact, later chunk ordinals are not (the host fails the search if
@@ -375,7 +405,7 @@ __global__ __launch_bounds__(64) void k_query_prep(const float *q, int nq, int d
 // (phase 1 does everything here, phase 2 nothing)
 __global__ __launch_bounds__(64) void k_query_prep_lds(const float *q, int nq, int d, int metric, int blas,
                                                        float *qvars, int maxv, float *qnorms, int *qmu, int *qlam,
-                                                       int *status, int phase) {
+                                                       int *status, int phase, float *qdelta) {
     if (phase == 2) return;
     extern __shared__ __attribute__((aligned(16))) float qbuf[];
     const int j = blockIdx.x;
@@ -385,6 +415,21 @@ __global__ __launch_bounds__(64) void k_query_prep_lds(const float *q, int nq, i
     float *v0 = qvars + (int64_t)j * maxv * qs;
     for (int i = lane; i < d; i += 64) qbuf[i] = src[i];
     __syncthreads();
+    // qdelta as k_query_prep's, from the stored variants [1, nv)
+    auto put_delta = [&](int nv) {
+        if (!qdelta) return;
+        double dl = 0.0;
+        for (int v = 1; v < nv; ++v) {
+            double ss = 0.0;
+            for (int i = lane; i < d; i += 64) {
+                const double e = (double)v0[(int64_t)v * qs + i] - (double)v0[i];
+                ss += e * e;
+            }
+            dl = ss > dl ? ss : dl;
+        }
+        for (int off = 32; off > 0; off >>= 1) dl += __shfl_xor(dl, off);
+        if (lane == 0) qdelta[j] = (float)(sqrt(dl) * (1.0 + 1e-6)) + 1e-30f;
+    };
     auto seqsum = [&]() -> float {
         if (lane == 0) {
             float s = 0.0f;
@@ -400,6 +445,7 @@ __global__ __launch_bounds__(64) void k_query_prep_lds(const float *q, int nq, i
     if (metric != MQVS_METRIC_COSINE) {
         for (int i = lane; i < qs; i += 64) v0[i] = i < d ? qbuf[i] : 0.0f;
         const float sum = blas ? seqsum() : 0.0f;
+        if (qdelta && lane == 0) qdelta[j] = 0.0f;
         if (lane == 0) {
             if (qnorms) qnorms[j] = sum;
             qmu[j] = 0;
@@ -438,10 +484,12 @@ __global__ __launch_bounds__(64) void k_query_prep_lds(const float *q, int nq, i
                 }
                 for (int w = v; w < maxv; ++w)  // (unused variants: zeros)
                     for (int i = lane; i < qs; i += 64) v0[(int64_t)w * qs + i] = 0.0f;
+                put_delta(v);
                 return;
             }
         }
     }
+    put_delta(maxv);
     if (lane == 0) {
         atomicOr(status, 1);
         qmu[j] = maxv - 1;
@@ -451,7 +499,7 @@ __global__ __launch_bounds__(64) void k_query_prep_lds(const float *q, int nq, i
 }
 
 void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, float *qvars, int maxv,
-                       float *qnorms, int *qmu, int *qlam, int *status, hipStream_t s, int phase) {
+                       float *qnorms, int *qmu, int *qlam, int *status, hipStream_t s, int phase, float *qdelta) {
     if (metric != MQVS_METRIC_COSINE) maxv = 1;
     const size_t lds = (size_t)((d + 31) / 32 * 32 + 4) * sizeof(float);
     const bool lanesig = maxv <= kLaneSigMax;
@@ -460,10 +508,10 @@ void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, flo
     do {                                                                                                             \
         if (lanesig)                                                                                                 \
             hipLaunchKernelGGL((k_query_prep<J, 3, true>), dim3(nq), dim3(64), sig, s, q, nq, d, metric, blas ? 1 : 0, \
-                               qvars, maxv, qnorms, qmu, qlam, status, phase);                                       \
+                               qvars, maxv, qnorms, qmu, qlam, status, phase, qdelta);                               \
         else                                                                                                         \
             hipLaunchKernelGGL((k_query_prep<J, 3, false>), dim3(nq), dim3(64), sig, s, q, nq, d, metric,             \
-                               blas ? 1 : 0, qvars, maxv, qnorms, qmu, qlam, status, phase);                         \
+                               blas ? 1 : 0, qvars, maxv, qnorms, qmu, qlam, status, phase, qdelta);                 \
     } while (0)
     if (d <= 128)
         MQVS_QP(2);
@@ -479,7 +527,7 @@ void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, flo
         MQVS_QP(24);
     else
         hipLaunchKernelGGL(k_query_prep_lds, dim3(nq), dim3(64), lds, s, q, nq, d, metric, blas ? 1 : 0, qvars, maxv,
-                           qnorms, qmu, qlam, status, phase);
+                           qnorms, qmu, qlam, status, phase, qdelta);
 #undef MQVS_QP
 }
 
@@ -852,16 +900,27 @@ void launch_chunk_ordinals(const uint8_t *filter, const uint8_t *nonempty, const
     hipLaunchKernelGGL(k_exclusive_ord, dim3(1), dim3(kScanThreads), 0, s, ord, nchunks);
 }
 
-__global__ void k_words_to_host(const int64_t *a, int na, const int *b, int nb, int64_t *ha, int *hb) {
+__global__ void k_words_to_host(const int64_t *a, int na, const int *b, int nb, int64_t *ha, int *hb,
+                                const int64_t *pq, int npq) {
     const int t = threadIdx.x;
-    if (t < na) *reinterpret_cast<volatile int64_t *>(ha + t) = a[t];
+    if (pq) {
+        // one wave: column sums of pq[npq][na]
+        for (int c = 0; c < na; ++c) {
+            int64_t v = 0;
+            for (int r = t; r < npq; r += 64) v += pq[(int64_t)r * na + c];
+            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+            if (t == 0) *reinterpret_cast<volatile int64_t *>(ha + c) = v;
+        }
+    } else if (t < na) {
+        *reinterpret_cast<volatile int64_t *>(ha + t) = a[t];
+    }
     if (t < nb) *reinterpret_cast<volatile int *>(hb + t) = b[t];
     __threadfence_system();
 }
 
 void launch_words_to_host(const int64_t *a, int na, const int *b, int nb, int64_t *host_a, int *host_b,
-                          hipStream_t s) {
-    hipLaunchKernelGGL(k_words_to_host, dim3(1), dim3(64), 0, s, a, na, b, nb, host_a, host_b);
+                          hipStream_t s, const int64_t *pq, int npq) {
+    hipLaunchKernelGGL(k_words_to_host, dim3(1), dim3(64), 0, s, a, na, b, nb, host_a, host_b, pq, npq);
 }
 
 // ---------------------------------------------------------------------------
@@ -1008,9 +1067,7 @@ __global__ __launch_bounds__(256) void k_read_slices(const rs_u32x4 *p, int64_t 
 // 8 workgroups per CU with 8 or 16 loads in flight): the best is the
 // achievable read rate the bench reports beside the plane scans
 double measure_read_sweep(size_t bytes, int reps, hipStream_t s, double *best_ms) {
-    int dev = 0, cus = 0;
-    MQVS_HIP(hipGetDevice(&dev));
-    MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int cus = device_cus();
     bytes = bytes / 16 * 16;
     void *buf = nullptr;
     MQVS_HIP(hipMalloc(&buf, bytes + 256));

@@ -688,9 +688,10 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4(ScanParams p, int slots, u32
 // B fragment 7 read at the start of phase 0 instead of the end of phase 1,
 // +0.4..2.4 % main scan; waves 2 and 3 issuing their DMA pieces in phase 1,
 // +15 %.)
-// DIAG (measurement builds only; wrong results, timing only): 1 = no stage
-// barrier, 2 = no DMA pieces issued, 4 = no threshold tests (the accumulators
-// kept live by one read per block)
+// DIAG (measurement builds only; 1, 2, 4: wrong results, timing only): 1 = no
+// stage barrier, 2 = no DMA pieces issued, 4 = no threshold tests (the
+// accumulators kept live by one read per block); 8 = the round-5 lane-major
+// walk scratch (correct results; the A/B of its bank conflicts)
 // PLM: where a stage's 8 DMA pieces (of stage s + D) go: 0 = phase 0 gaps
 // 8, 11, .., 29; 1 = phase 0 gaps 0, 4, .., 28; 2 = the 4 row pieces in phase
 // 0 (gaps 8, 14, 20, 26), the 4 query pieces in phase 1 (gaps 0, 8, 16, 24,
@@ -998,14 +999,23 @@ __global__ __launch_bounds__(256, 1) void k_scan_p4m(ScanParams p, int slots, u3
         unsigned m16 = 0;
 #pragma unroll
         for (int r = 0; r < 16; ++r) m16 |= (v4[r >> 2][r & 3] >= th ? 1u : 0u) << r;
+        // walk scratch value-major (value r of lane l at r 64 + l): the walk's
+        // reads of a per-lane value index hit 64 distinct banks; lane-major
+        // (DIAG 8, round 5: lane stride 64 B) put every fourth lane on the
+        // same bank -- 16-way conflicts on every read of the walk
+        if constexpr ((DIAG & 8) != 0) {
 #pragma unroll
-        for (int g = 0; g < 4; ++g) *reinterpret_cast<f32x4 *>(wscr + lane * 16 + 4 * g) = v4[g];
+            for (int g = 0; g < 4; ++g) *reinterpret_cast<f32x4 *>(wscr + lane * 16 + 4 * g) = v4[g];
+        } else {
+#pragma unroll
+            for (int r = 0; r < 16; ++r) wscr[r * 64 + lane] = v4[r >> 2][r & 3];
+        }
 #pragma unroll 1
         while (__ballot(m16 != 0u) != 0) {
             bool pass = m16 != 0u;
             const int r = pass ? __builtin_ctz(m16) : 0;
             m16 &= m16 - 1u;
-            const float x = wscr[lane * 16 + r];
+            const float x = (DIAG & 8) != 0 ? wscr[lane * 16 + r] : wscr[r * 64 + lane];
             float raw = x;
             if constexpr (L2) {
                 raw = qn - 2.0f * x;
@@ -1170,9 +1180,7 @@ constexpr int kP4QueueCap = 4096;
 // (the current device's CU count, queried per call: launch_p4 sizes its grid
 // from the same query, so the queue always covers blockIdx * 4 + wave)
 size_t p4_queue_bytes() {
-    int dev = 0, cus = 0;
-    MQVS_HIP(hipGetDevice(&dev));
-    MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int cus = device_cus();
     return (size_t)cus * 4 * kP4QueueCap * sizeof(u32x4);
 }
 
@@ -1259,9 +1267,7 @@ static bool p4_ok(ScanParams &p, bool need_queue = true) {
     if ((need_queue && !p.p4_queue) || p.row_list || p.chunk_ord || p.tiles < 1 || p.tile_rows != kP4Tile)
         return false;
     p.num_qblocks = (p.nq + kP4Tile - 1) / kP4Tile;
-    int dev = 0, cus = 0;
-    MQVS_HIP(hipGetDevice(&dev));
-    MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int cus = device_cus();
     if (p.num_qblocks > cus / 8 || p.dpad % kP4HiK) return false;
     if (p.row_begin % 16 || (p.tiles_per_chunk > 0 && p.chunk_rows % 16)) return false;
     if (p.row_begin < 0 || p.row_end + p.chunk_rows + p.tile_rows > 0x7FFFFFFF || p.tiles > 0x3FFFFFFF ||
@@ -1277,9 +1283,7 @@ template <int METRIC>
 static bool launch_p4_t(ScanParams p, hipStream_t s) {
     if (!p.p4_queue || p.row_list || p.chunk_ord || p.tiles < 1 || p.tile_rows != kP4Tile) return false;
     p.num_qblocks = (p.nq + kP4Tile - 1) / kP4Tile;
-    int dev = 0, cus = 0;
-    MQVS_HIP(hipGetDevice(&dev));
-    MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int cus = device_cus();
     const int per_xcd = cus / 8;
     if (p.num_qblocks > per_xcd) return false;
     if (p.dpad % kP4HiK) return false;
@@ -1342,9 +1346,7 @@ static bool launch_p4_any(const ScanParams &p, hipStream_t s) {
     ScanParams c = p;
     if (!p4_ok(c)) return false;
     if (METRIC == MQVS_METRIC_L2 && !c.row_norms) return false;
-    int dev = 0, cus = 0;
-    MQVS_HIP(hipGetDevice(&dev));
-    MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int cus = device_cus();
     const int per_xcd = cus / 8;
     const int slots = per_xcd / c.num_qblocks * c.num_qblocks;
     const dim3 grid((unsigned)(8 * per_xcd));
@@ -1359,6 +1361,7 @@ static bool launch_p4_any(const ScanParams &p, hipStream_t s) {
                        tmap)
         if (diag == 1) MQVS_P4M(1, 0);
         else if (diag == 4) MQVS_P4M(4, 0);
+        else if (diag == 8) MQVS_P4M(8, 0);
         else if (diag == 6) MQVS_P4M(6, 0);
         else if (plm == 1) MQVS_P4M(0, 1);
         else if (plm == 2) MQVS_P4M(0, 2);
@@ -1383,9 +1386,7 @@ static bool launch_p4_probe_t(ScanParams p, hipStream_t s) {
     if (p.filter || p.exists) return false;
     if (!p.p4_gmax || p.p4_gld < 2 * p.tiles || !p4_ok(p, false)) return false;
     if (METRIC == MQVS_METRIC_L2 && !p.row_norms) return false;
-    int dev = 0, cus = 0;
-    MQVS_HIP(hipGetDevice(&dev));
-    MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int cus = device_cus();
     const int per_xcd = cus / 8;
     const int slots = per_xcd / p.num_qblocks * p.num_qblocks;
     const dim3 grid((unsigned)(8 * per_xcd));
@@ -1401,9 +1402,7 @@ template <int METRIC, int GRP>
 static bool launch_p4_groups_t(ScanParams p, hipStream_t s) {
     if (!p.p4_gmax || p.p4_gld < (256 / GRP) * p.tiles || !p4_ok(p, false)) return false;
     if (METRIC == MQVS_METRIC_L2 && !p.row_norms) return false;
-    int dev = 0, cus = 0;
-    MQVS_HIP(hipGetDevice(&dev));
-    MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+    const int cus = device_cus();
     const int per_xcd = cus / 8;
     const int slots = per_xcd / p.num_qblocks * p.num_qblocks;
     hipLaunchKernelGGL((k_scan_p4m<METRIC, 4, true, GRP>), dim3((unsigned)(8 * per_xcd)), dim3(256), 0, s, p, slots,

@@ -120,56 +120,70 @@ __device__ inline void rerank_emit(uint4 *recs, uint4 *g, int ncand, int k, int 
 // The output is the same as re-ranking all of them.  No pruning (m = ncand)
 // when a_k is not a valid value, B is not finite, or for IP the k best could
 // fall under the FLT_MIN cut (searchWrapper's init) and leave fewer than k.
+// wave_prune_cut: the cut of query q, computed by one wave (its 64 lanes
+// share the cosine variant distances); returns whether pruning applies and
+// the cut w on the approximate raw value (keep a <= w for L2, a >= w else),
+// uniform over the wave.
+template <int METRIC>
+__device__ inline bool wave_prune_cut(const ScanParams &p, const RerankPrune &pr, int q, int ncand, int k, float &w) {
+    const int lane = threadIdx.x & 63;
+    // cosine: the largest distance of a used variant from variant 0, in fp64
+    // (from the query prep when it measured it)
+    double dmax = 0.0;
+    if (METRIC == MQVS_METRIC_COSINE && pr.qdelta) {
+        const double dq = (double)pr.qdelta[q];
+        dmax = dq * dq;
+    } else if (METRIC == MQVS_METRIC_COSINE && p.maxv > 1) {
+        const int mu = p.qmu[q], lam = p.qlam[q];
+        const int nv = (lam >= 1 && mu >= 0 && mu + lam <= p.maxv) ? mu + lam : p.maxv;
+        const int64_t qs = (int64_t)((p.d + 31) / 32 * 32);
+        const float *x0 = p.qvars + (int64_t)q * p.maxv * qs;
+        for (int v = 1; v < nv; ++v) {
+            const float *xv = x0 + (int64_t)v * qs;
+            double ss = 0.0;
+            for (int i = lane; i < p.d; i += 64) {
+                const double e = (double)xv[i] - (double)x0[i];
+                ss += e * e;
+            }
+            for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
+            dmax = ss > dmax ? ss : dmax;
+        }
+    }
+    const float ak = pr.raw[(int64_t)q * ncand + k - 1];
+    const float ym = *pr.ymax;
+    const float dv = dmax > 0.0 ? (float)(sqrt(dmax) * (1.0 + 1e-6)) * ym * 1.0001f : 0.f;
+    const float b = pr.bq[q] + dv + 1e-30f;
+    bool ok = ak == ak && b < 1e30f && ym < 1e30f;
+    if (METRIC == MQVS_METRIC_L2) {
+        w = ak + 2.0f * b;
+        w = w + fabsf(w) * 2.4e-7f + 1e-30f;
+    } else {
+        w = ak - 2.0f * b;
+        w = w - fabsf(w) * 2.4e-7f - 1e-30f;
+        if (METRIC == MQVS_METRIC_IP) {
+            float lo = ak - b;
+            lo = lo - fabsf(lo) * 2.4e-7f;
+            ok = ok && lo > 1.17549435e-38f;
+        }
+    }
+    return ok && w == w;
+}
+
 // Block-uniform result; s_m: one int of LDS.
 template <int METRIC>
 __device__ inline int rerank_keep(const ScanParams &p, const RerankPrune &pr, int q, int ncand, int k, int *s_m) {
     if (!pr.raw || k >= ncand) return ncand;
     const float *raw = pr.raw + (int64_t)q * ncand;
-    const int t = threadIdx.x, lane = t & 63;
+    const int t = threadIdx.x;
     if (t == 0) *s_m = ncand;
-    __syncthreads();
     __shared__ float s_cut;
     __shared__ int s_ok;
     if (t < 64) {
-        // cosine: the largest distance of a used variant from variant 0, in fp64
-        double dmax = 0.0;
-        if (METRIC == MQVS_METRIC_COSINE && p.maxv > 1) {
-            const int mu = p.qmu[q], lam = p.qlam[q];
-            const int nv = (lam >= 1 && mu >= 0 && mu + lam <= p.maxv) ? mu + lam : p.maxv;
-            const int64_t qs = (int64_t)((p.d + 31) / 32 * 32);
-            const float *x0 = p.qvars + (int64_t)q * p.maxv * qs;
-            for (int v = 1; v < nv; ++v) {
-                const float *xv = x0 + (int64_t)v * qs;
-                double ss = 0.0;
-                for (int i = lane; i < p.d; i += 64) {
-                    const double e = (double)xv[i] - (double)x0[i];
-                    ss += e * e;
-                }
-                for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off);
-                dmax = ss > dmax ? ss : dmax;
-            }
-        }
-        if (lane == 0) {
-            const float ak = raw[k - 1];
-            const float ym = *pr.ymax;
-            const float dv = dmax > 0.0 ? (float)(sqrt(dmax) * (1.0 + 1e-6)) * ym * 1.0001f : 0.f;
-            const float b = pr.bq[q] + dv + 1e-30f;
-            float w;
-            bool ok = ak == ak && b < 1e30f && ym < 1e30f;
-            if (METRIC == MQVS_METRIC_L2) {
-                w = ak + 2.0f * b;
-                w = w + fabsf(w) * 2.4e-7f + 1e-30f;
-            } else {
-                w = ak - 2.0f * b;
-                w = w - fabsf(w) * 2.4e-7f - 1e-30f;
-                if (METRIC == MQVS_METRIC_IP) {
-                    float lo = ak - b;
-                    lo = lo - fabsf(lo) * 2.4e-7f;
-                    ok = ok && lo > 1.17549435e-38f;
-                }
-            }
+        float w = 0.f;
+        const bool ok = wave_prune_cut<METRIC>(p, pr, q, ncand, k, w);
+        if (t == 0) {
             s_cut = w;
-            s_ok = ok && w == w ? 1 : 0;
+            s_ok = ok ? 1 : 0;
         }
     }
     __syncthreads();
@@ -186,9 +200,7 @@ __device__ inline int rerank_keep(const ScanParams &p, const RerankPrune &pr, in
         }
     }
     __syncthreads();
-    const int m = *s_m;
-    if (t == 0 && pr.count) atomicAdd(pr.count, (unsigned long long)m);
-    return m;
+    return *s_m;
 }
 
 // Generic form (any d): one thread per candidate walks its row.
@@ -203,6 +215,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids(ScanParams p, const 
     uint4 *g = scratch ? scratch + (int64_t)q * 2 * ncand : nullptr;
     uint4 *dst = g ? g : recs;
     const int m = rerank_keep<METRIC>(p, pr, q, ncand, k, &s_m);
+    if (threadIdx.x == 0 && pr.count) atomicAdd(pr.count, (unsigned long long)m);
     for (int i = threadIdx.x; i < ncand; i += SEL_THREADS) {
         int64_t row = i < m ? c[i] : -1;
         if (!(row >= 0 && row < p.n && row_valid(p, row))) row = -1;
@@ -427,6 +440,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids_tiled(ScanParams p, 
     const int q = blockIdx.x;
     const int64_t *c = cand + (int64_t)q * ncand;
     const int m = rerank_keep<METRIC>(p, pr, q, ncand, k, &s_m);
+    if (threadIdx.x == 0 && pr.count) atomicAdd(pr.count, (unsigned long long)m);
     for (int cb = 0; cb < ncand; cb += SEL_THREADS) {
         const int i = cb + threadIdx.x;
         int64_t row = -1;
@@ -476,21 +490,24 @@ __global__ __launch_bounds__(SEL_THREADS) void k_exact_records(ScanParams p, con
 // kSelCap records at <= X (mass ties): the bitonic sort of all of them.
 constexpr int kSelCap = SEL_THREADS;
 
+// rcap: the records' LDS room (a power of two <= kSortCap; kSortCap when a
+// query may hold more records -- the global_sort path needs all of it)
 template <int METRIC>
 __global__ __launch_bounds__(SEL_THREADS) void k_sort_emit(uint4 *recs, const int *cnt, int64_t rs, int k,
-                                                          int64_t id_offset, int64_t *out_ids, float *out_dist) {
-    extern __shared__ __attribute__((aligned(16))) uint4 lrec[];  // kSortCap + kSelCap records
+                                                          int64_t id_offset, int64_t *out_ids, float *out_dist,
+                                                          int rcap) {
+    extern __shared__ __attribute__((aligned(16))) uint4 lrec[];  // rcap + kSelCap records
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh[4];
     __shared__ int s_c;
     const int q = blockIdx.x;
     const int m = cnt[q];
     uint4 *g = recs + (int64_t)q * rs;
-    if (m > kSortCap) {
+    if (m > rcap) {
         rerank_emit<METRIC>(lrec, g, m, k, q, id_offset, out_ids, out_dist);
         return;
     }
-    uint4 *sel = lrec + kSortCap;
+    uint4 *sel = lrec + rcap;
     if (threadIdx.x == 0) s_c = 0;
     for (int i = threadIdx.x; i < m; i += SEL_THREADS) lrec[i] = g[i];
     __syncthreads();
@@ -548,8 +565,7 @@ void launch_exact_rerank(const ScanParams &p, int metric, const uint32_t *surv, 
             hipLaunchKernelGGL((k_exact_records<M, false>), dim3(grid), dim3(SEL_THREADS), 0, s, p, surv, cnt,    \
                                rs, chunks, recs);                                                                 \
         hipLaunchKernelGGL((k_sort_emit<M>), dim3(p.nq), dim3(SEL_THREADS), (kSortCap + kSelCap) * sizeof(uint4), s, \
-                           recs, cnt,                                                                             \
-                           rs, k, id_offset, out_ids, out_dist);                                                  \
+                           recs, cnt, rs, k, id_offset, out_ids, out_dist, kSortCap);                              \
     } while (0)
     switch (metric) {
         case MQVS_METRIC_L2: MQVS_ER(MQVS_METRIC_L2); break;
@@ -558,6 +574,108 @@ void launch_exact_rerank(const ScanParams &p, int metric, const uint32_t *surv, 
         default: MQVS_ER(kMetricIpRaw); break;
     }
 #undef MQVS_ER
+}
+
+// ---------------------------------------------------------------------------
+// The index re-rank spread over waves instead of one workgroup per query
+// (R <= kSortCap, d % 4 == 0).  k_rerank_ids_tiled keeps every query's
+// candidates in one 4-wave workgroup: at ~233 VGPRs two waves per SIMD fit,
+// so 1000 queries took two rounds of workgroups and a workgroup lasts as long
+// as its slowest wave's 24-tile chain whether the bound pruned half its
+// candidates or not.  Here:
+//   k_rerank_plan      one wave per query: the pruned prefix (wave_prune_cut)
+//                      and its valid rows, compacted in candidate order;
+//   k_exact_records_w  work items of (64 candidates, query), chunk-major over
+//                      the queries, one per wave (the waves of a workgroup
+//                      take 4 consecutive queries' same chunk);
+//   k_sort_emit        the top k of each query's records, as mqvs_search.
+// Records and order are the ones k_rerank_ids_tiled produces.
+template <int METRIC>
+__global__ __launch_bounds__(256) void k_rerank_plan(ScanParams p, const int64_t *cand, int ncand, int k,
+                                                     RerankPrune pr, uint32_t *surv, int *cnt) {
+    const int q = blockIdx.x * 4 + (threadIdx.x >> 6), lane = threadIdx.x & 63;
+    if (q >= p.nq) return;
+    float w = 0.f;
+    const bool ok = pr.raw && k < ncand && wave_prune_cut<METRIC>(p, pr, q, ncand, k, w);
+    const int64_t *c = cand + (int64_t)q * ncand;
+    const float *raw = pr.raw ? pr.raw + (int64_t)q * ncand : nullptr;
+    uint32_t *out = surv + (int64_t)q * ncand;
+    int n = 0, m = ncand;
+    for (int i0 = 0; i0 < ncand; i0 += 64) {
+        const int i = i0 + lane;
+        bool keep = i < ncand;
+        if (ok && keep) {
+            const float a = raw[i];
+            keep = METRIC == MQVS_METRIC_L2 ? a <= w : a >= w;
+        }
+        const uint64_t km = __ballot(keep);
+        // the sorted candidates: the first one past the cut ends the prefix
+        const int stop = km == ~0ull ? 64 : __builtin_ctzll(~km);
+        const int64_t row = (i < ncand && lane < stop) ? c[i] : -1;
+        const bool v = row >= 0 && row < p.n && row_valid(p, row);
+        const uint64_t vm = __ballot(v);
+        if (v) out[n + __popcll(vm & ((1ull << lane) - 1ull))] = (uint32_t)row;
+        n += __popcll(vm);
+        if (stop < 64) {
+            m = i0 + stop;
+            break;
+        }
+    }
+    if (lane == 0) {
+        cnt[q] = n;
+        if (pr.count) atomicAdd(pr.count, (unsigned long long)m);
+    }
+}
+
+template <int METRIC, bool DIRECT>
+__global__ __launch_bounds__(SEL_THREADS) void k_exact_records_w(ScanParams p, const uint32_t *surv, const int *cnt,
+                                                                int64_t rs, int chunks, uint4 *recs) {
+    __shared__ float tiles[(SEL_THREADS / 64) * 64 * kRrStride];
+    const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    float *tile = tiles + wv * 64 * kRrStride;
+    const int64_t items = (int64_t)p.nq * chunks;
+    const int64_t nw = (int64_t)gridDim.x * (SEL_THREADS / 64);
+    for (int64_t it = (int64_t)blockIdx.x * (SEL_THREADS / 64) + wv; it < items; it += nw) {
+        const int c = (int)(it / p.nq), q = (int)(it - (int64_t)c * p.nq);
+        const int m = cnt[q];
+        if (c * 64 >= m) continue;  // (uniform over the wave)
+        const int i = c * 64 + lane;
+        const int64_t row = i < m ? (int64_t)surv[(int64_t)q * rs + i] : -1;
+        const float raw = wave_exact_any<METRIC, DIRECT>(p, q, row, tile);
+        if (i < m) recs[(int64_t)q * rs + i] = rerank_rec<METRIC>(p, row, raw);
+    }
+}
+
+bool launch_rerank_ids_wide(const ScanParams &p, int metric, const int64_t *cand, int ncand, int k,
+                            int64_t id_offset, int64_t *out_ids, float *out_dist, const RerankPrune &pr,
+                            uint32_t *surv, int *cnt, uint4 *recs, hipStream_t s) {
+    if (ncand > kSortCap || (p.d & 3) || p.nq <= 0) return false;
+    const bool direct = !blas_formula(p);
+    const int chunks = (ncand + 63) / 64;
+    const int64_t items = (int64_t)p.nq * chunks;
+    const int grid = (int)std::max<int64_t>(1, std::min<int64_t>((items + 3) / 4, 8192));
+    int rcap = 1;  // (every query holds at most ncand records: LDS for that many)
+    while (rcap < ncand) rcap <<= 1;
+#define MQVS_RW(M)                                                                                                  \
+    do {                                                                                                            \
+        hipLaunchKernelGGL((k_rerank_plan<M>), dim3((p.nq + 3) / 4), dim3(256), 0, s, p, cand, ncand, k, pr, surv,  \
+                           cnt);                                                                                    \
+        if (direct)                                                                                                 \
+            hipLaunchKernelGGL((k_exact_records_w<M, true>), dim3(grid), dim3(SEL_THREADS), 0, s, p, surv, cnt,      \
+                               (int64_t)ncand, chunks, recs);                                                       \
+        else                                                                                                        \
+            hipLaunchKernelGGL((k_exact_records_w<M, false>), dim3(grid), dim3(SEL_THREADS), 0, s, p, surv, cnt,     \
+                               (int64_t)ncand, chunks, recs);                                                       \
+        hipLaunchKernelGGL((k_sort_emit<M>), dim3(p.nq), dim3(SEL_THREADS), (rcap + kSelCap) * sizeof(uint4), s,     \
+                           recs, cnt, (int64_t)ncand, k, id_offset, out_ids, out_dist, rcap);                       \
+    } while (0)
+    switch (metric) {
+        case MQVS_METRIC_L2: MQVS_RW(MQVS_METRIC_L2); break;
+        case MQVS_METRIC_IP: MQVS_RW(MQVS_METRIC_IP); break;
+        default: MQVS_RW(MQVS_METRIC_COSINE); break;
+    }
+#undef MQVS_RW
+    return true;
 }
 
 template <int M, bool DIRECT>

@@ -398,6 +398,23 @@ void cpu_relax() {
 #endif
 }
 
+int device_cus() {
+    static std::atomic<int> cache[64];
+    int dev = 0;
+    MQVS_HIP(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) {
+        int cus = 0;
+        MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        return cus;
+    }
+    int cus = cache[dev].load(std::memory_order_relaxed);
+    if (cus <= 0) {
+        MQVS_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+        cache[dev].store(cus, std::memory_order_relaxed);
+    }
+    return cus;
+}
+
 int wait_spin_us() {
     const int m = g_wait_mode.load(std::memory_order_relaxed);
     return m == MQVS_WAIT_RUNTIME ? -1 : m == MQVS_WAIT_BLOCK ? 0 : g_wait_spin_us.load(std::memory_order_relaxed);

@@ -262,11 +262,18 @@ struct RerankPrune {
     const float *raw = nullptr;           // [nq][ncand] approximate raw values in candidate order (NaN: none)
     const float *bq = nullptr;            // [nq] bound on |approx - exact| for query variant 0 (k_query_bound)
     const float *ymax = nullptr;          // device scalar: max |y| over the rows (cosine variant term)
+    const float *qdelta = nullptr;        // [nq] cosine: >= max_v |x_v - x_0| (k_query_prep); null: computed here
     unsigned long long *count = nullptr;  // += candidates re-ranked (may be null)
 };
 void launch_rerank_ids(const ScanParams &p, int metric, const int64_t *cand, int ncand, int k,
                        int64_t id_offset, int64_t *out_ids, float *out_dist, uint4 *scratch, hipStream_t s,
                        const RerankPrune &prune = RerankPrune{});
+// the same re-rank over waves (k_rerank_plan + k_exact_records_w +
+// k_sort_emit; ncand <= kSortCap, d % 4 == 0, else false and nothing runs):
+// scratch surv [nq][ncand] u32, cnt [nq], recs [nq][ncand]
+bool launch_rerank_ids_wide(const ScanParams &p, int metric, const int64_t *cand, int ncand, int k,
+                            int64_t id_offset, int64_t *out_ids, float *out_dist, const RerankPrune &pr,
+                            uint32_t *surv, int *cnt, uint4 *recs, hipStream_t s);
 void launch_scan_mfma(const ScanParams &p, int metric, bool probe, hipStream_t s);
 void launch_probe_select(const float *probe, int64_t P, int64_t ld, int nq, int k, int metric,
                          uint32_t *tau, int *cand_count, Cand *cand, int cand_cap,
@@ -320,7 +327,8 @@ void launch_row_norms(const float *rows, int64_t n, int d, float *norms, hipStre
 // maxv: variants stored per query (1 unless cosine)
 // phase: 0 everything; 1 variant 0 only; 2 the rest of the chain (after 1)
 void launch_query_prep(const float *q, int nq, int d, int metric, bool blas, float *qvars, int maxv,
-                       float *qnorms, int *qmu, int *qlam, int *status, hipStream_t s, int phase = 0);
+                       float *qnorms, int *qmu, int *qlam, int *status, hipStream_t s, int phase = 0,
+                       float *qdelta = nullptr);
 void launch_generate(uint64_t seed, int mode, int64_t row0, int64_t n, int d, float *out,
                      hipStream_t s);
 void launch_pack_nonempty(const uint8_t *bytes, int64_t n, uint8_t *bits, hipStream_t s);
@@ -455,6 +463,24 @@ struct IvfParams {
     Cand *cand;               // approximate values, one per (pair, list position)
     int64_t *stats;           // [4] values written, items, plane bytes, pairs
     int64_t *bsum;            // [3 * plan workgroups] per-workgroup list totals (k_plan_lists_reg)
+    // pair mode (pair_stride > 0; few pairs per list): no plan -- work item
+    // it is (pair it / pair_nch, slice it % pair_nch) of one query, query q's
+    // region starts at q * pair_stride and holds its probes' lists back to back
+    int64_t pair_stride;
+    int pair_nch;
+};
+
+// The per-query candidate regions of a list pass, as the select reads them:
+// the plan's qstart[nq + 1], or pair mode's fixed strides (regions filled by
+// the probed lists' lengths; the select then also sums the stats).
+struct IvfRegions {
+    const int64_t *qstart = nullptr;
+    int64_t stride = 0;
+    int nprobe = 0, nlist = 0, chunk = 0;
+    int64_t dpad = 0;
+    const int64_t *probes = nullptr;
+    const int64_t *list_off = nullptr;
+    int64_t *stats = nullptr;  // pair mode: [nq][4] values, items, plane bytes, pairs per query
 };
 
 void launch_ivf_plan(const IvfParams &p, hipStream_t s);
@@ -462,7 +488,7 @@ void launch_iota_probes(int64_t *probes, int nq, int np, hipStream_t s);
 void launch_ivf_plan_dense(const IvfParams &p, int64_t npos, hipStream_t s);
 void launch_ivf_scan(const IvfParams &p, int metric, int grid, hipStream_t s);
 // expect_len: typical per-query region length (sizes the LDS key cache)
-void launch_ivf_select(const Cand *cand, const int64_t *qstart, int nq, int R, int metric, int64_t *out_rows,
+void launch_ivf_select(const Cand *cand, const IvfRegions &rg, int nq, int R, int metric, int64_t *out_rows,
                        int64_t id_offset, float *out_approx, int64_t expect_len, hipStream_t s, uint4 *gscr = nullptr,
                        float *out_raw = nullptr);
 void launch_ivf_pack(const float *rows, const float *norms, int d, const int32_t *perm, int64_t npos, int64_t dpad,
@@ -488,8 +514,9 @@ void launch_coarse_pick(const float *gmax, int64_t gld, int64_t ngroups, int T, 
 bool timing_on(uint32_t flags);
 // a[0, na) and b[0, nb) into pinned host memory (system-scope stores; one
 // launch instead of two copy kernels before the caller's stream sync)
+// (pq: a's words are the sums over npq rows of pq[npq][na] instead)
 void launch_words_to_host(const int64_t *a, int na, const int *b, int nb, int64_t *host_a, int *host_b,
-                          hipStream_t s);
+                          hipStream_t s, const int64_t *pq = nullptr, int npq = 0);
 bool launch_scan_p4_groups(const ScanParams &p, int metric, int grp, hipStream_t s);
 void launch_centroid_mean(const float *rows, int d, const int32_t *order, const int64_t *off, int nlist, float *cent,
                           hipStream_t s);
@@ -608,6 +635,9 @@ static int guarded(F &&f) {
 
 // mqvs.hip services used by the index path
 hipStream_t thread_stream(int device);
+// compute units of the current device (cached per device: launchers size
+// their persistent grids from it on every call)
+int device_cus();
 // The host's wait for the work queued on `s` (every synchronous call ends with
 // one): the policy of mqvs_set_wait_mode -- the runtime's own
 // hipStreamSynchronize, or a short poll of a blocking-sync event's completion

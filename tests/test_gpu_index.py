@@ -435,3 +435,32 @@ def test_index_pruned_rerank_equals_full(mq, metric, nq, fsel, lwd):
     assert np.array_equal(dist_p.view(np.uint32), dist_a.view(np.uint32))
     assert st_a["reranked"] == nq * R
     assert 0 < st_p["reranked"] < nq * R, st_p
+
+
+@pytest.mark.parametrize("metric,fsel,lwd", [("L2", None, None), ("IP", 0.5, None), ("Cosine", 0.4, 0.2)])
+def test_index_pair_mode_equals_grouped_plan(mq, metric, fsel, lwd):
+    """Few (query, list) pairs per list (16 nq nprobe <= nlist) take pair
+    mode: no plan, one work item per (pair, list slice), fixed per-query
+    regions.  The same 40 queries searched alone (pair mode) and inside a
+    batch of 400 (the same queries ten times: the grouped plan) return the
+    same ids and distance bits (queries are independent; both batches use the
+    nq >= 20 formula), with a PREWHERE filter and deletes, and the stats count
+    the pairs and values of the pass."""
+    n, d, nq, k, nlist, nprobe = 120000, 64, 40, 50, 1600, 2
+    seg = mq.VectorScanSegment.generate(0x5EED0001, 2, n, d, metric=metric, granule=4096)
+    q = O.generate(0x5EED0001, 2, n, nq, d)
+    rng = np.random.default_rng(5)
+    flt = np.packbits((rng.random(n) < fsel).astype(np.uint8), bitorder="little") if fsel else None
+    ex = np.packbits((rng.random(n) >= lwd).astype(np.uint8), bitorder="little") if lwd else None
+    idx = mq.VectorIndex.build(seg, "MSTG", {"nlist": nlist})
+    try:
+        params = {"nprobe": nprobe}
+        ids_p, dist_p = idx.search(q, k, params, filter_bitmap=flt, row_exists=ex)
+        st = mq.vector_index.last_index_stats()
+        ids_g, dist_g = idx.search(np.concatenate([q] * 10), k, params, filter_bitmap=flt, row_exists=ex)
+    finally:
+        idx.free()
+        seg.free()
+    assert np.array_equal(ids_p, ids_g[:nq])
+    assert np.array_equal(dist_p.view(np.uint32), dist_g[:nq].view(np.uint32))
+    assert st["pairs"] == nq * nprobe and st["values"] > 0 and st["plane_bytes"] == st["values"] * 2 * 64, st

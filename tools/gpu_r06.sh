@@ -25,6 +25,28 @@ for step in "$@"; do
         done
       done
       cut -c1-600 $O/isweep.jsonl ;;
+    ab)
+      timeout -k 10 600 python -u tools/ab_split.py --dbg --nqs 1000 --splits 2 --modes 1 --metrics Cosine,L2 \
+        --tunes 'MQVS_P4M_DIAG=0;MQVS_P4M_DIAG=8;MQVS_P4M_DIAG=0;MQVS_P4M_DIAG=8' --reps 5 \
+        > $O/ab_walk.jsonl 2> $O/ab_walk.err || { echo "ab failed"; tail -20 $O/ab_walk.err; exit 1; }
+      cut -c1-400 $O/ab_walk.jsonl ;;
+    rr)
+      # index A/B arms of the measurement build: IDX_ARMS="ENV=V,ENV=V;..." ('-' = defaults)
+      IFS=';' read -ra ARMS <<< "${IDX_ARMS:--;MQVS_IVF_PAIR=0}"
+      for arm in "${ARMS[@]}"; do
+        ( [ "$arm" != "-" ] && for kv in ${arm//,/ }; do export "$kv"; done
+          timeout -k 10 300 python -u tools/index_sweep.py --dbg --mode ${IDX_MODE:-3} --search "${IDX_SEARCH:-nprobe=1}" --reps 7 \
+            | sed "s/^{/{\"arm\": \"$arm\", /" ) >> $O/rr_ab.jsonl 2>> $O/rr_ab.err || { echo "rr failed"; tail -20 $O/rr_ab.err; exit 1; }
+      done
+      grep search $O/rr_ab.jsonl | cut -c1-460 ;;
+    itl)
+      # kernel timeline of one mode-3 nprobe=1 index search (k_to_bf16 opens a search)
+      ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --output-format csv -d "$GRAFT_REPO_ROOT/$O/itl" -o run \
+          -- python "$GRAFT_REPO_ROOT/tools/index_search_run.py" --mode 3 --search nprobe=1 --searches 3 \
+          > "$GRAFT_REPO_ROOT/$O/itl.log" 2>&1 ) || { echo "itl failed"; tail -5 $O/itl.log; exit 1; }
+      python3 tools/timeline.py $O/itl/run_kernel_trace.csv --start k_to_bf16 --nth -1 | tee $O/index_m3_nprobe1_timeline.txt ;;
+    lds)
+      bash tools/gpu_lds_pmc.sh 0 8 4 6 || exit 1 ;;
     cpu)
       timeout -k 10 600 python -u tools/host_cpu_wait.py > $O/host_cpu_wait.jsonl 2> $O/host_cpu_wait.err \
         || { echo "cpu wait failed"; tail -20 $O/host_cpu_wait.err; exit 1; }

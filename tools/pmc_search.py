@@ -28,9 +28,14 @@ def main():
     ap.add_argument("--searches", type=int, default=2)
     ap.add_argument("--selectivity", type=int, default=None,
                     help="PREWHERE attr < T over a uniform attr in [0, 100) (configs[4] shape)")
+    ap.add_argument("--dbg", action="store_true",
+                    help="load the measurement build libmqvs_dbg.so (reads MQVS_* A/B switches)")
     args = ap.parse_args()
     import torch
     import myscaledb_amd as mq
+    if args.dbg:
+        from myscaledb_amd import _lib as _mq_lib
+        _mq_lib.use_measurement_build()
     from myscaledb_amd.vector_scan import generate_device, pack_bitmap
     mq.init(0)
     seg = mq.VectorScanSegment.generate(SEED_BASE, args.mode, args.n, args.d, args.metric, args.granule)
