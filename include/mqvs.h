@@ -578,10 +578,12 @@ int mqvs_measure_read_bandwidth(size_t bytes, int32_t reps, double *gbs, double 
  * count).  The reference runs up to 2 x physical cores scans at once
  * (ScanThreadLimiter.h:25-58, MergeTreeVSManager.cpp:974-975): a thread that
  * spins for the length of its search holds a host core meanwhile.
- *   MQVS_WAIT_RUNTIME  hipStreamSynchronize (the HIP runtime's own policy)
- *   MQVS_WAIT_HYBRID   poll for up to spin_us, then sleep on a blocking-sync
- *                      event until the work completes (default, 50 us)
- *   MQVS_WAIT_BLOCK    sleep at once
+ *   MQVS_WAIT_RUNTIME  hipStreamSynchronize (the HIP runtime's own policy;
+ *                      on ROCm it spins, also with BlockingSync events)
+ *   MQVS_WAIT_HYBRID   poll for up to spin_us, then sleep: most of the time
+ *                      this thread's recent waits took, then short
+ *                      sleep-polls (default, 50 us)
+ *   MQVS_WAIT_BLOCK    the same without the first poll
  * Results are identical in every mode.  Returns the previous mode;
  * spin_us < 0 leaves the poll budget unchanged; other modes are
  * MQVS_ERR_BAD_ARGUMENTS (returned as a negative value: -4). */

@@ -106,6 +106,7 @@ struct IndexWorkspace final : WsExt {
     hipEvent_t fork = nullptr, join = nullptr;
     hipStream_t side = nullptr;
     int64_t *host = nullptr;  // pinned: the search's stats [4] and status word (one sync, no staging copies)
+    HostBuf pin_q, pin_f, pin_e, pin_o;  // pinned staging of host-pointer searches
     GBuf queries, qvars, qnorms, qmu, qlam, status, qhi, probes, cprobes, filter, exists, rows, out_ids, out_dist,
         ord, dmap, dwords, pdist, cqhi, gmax, crec, cbq, craw, ibq, rsurv, rcnt, rrecs, qdelta, pstats;
     ListBufs coarse, fine;
@@ -114,6 +115,7 @@ struct IndexWorkspace final : WsExt {
     size_t free_scratch() override {
         if (side) (void)hipStreamSynchronize(side);
         size_t b = 0;
+        for (HostBuf *x : {&pin_q, &pin_f, &pin_e, &pin_o}) x->release();  // (host memory: not counted)
         for (GBuf *x : {&queries, &qvars, &qnorms, &qmu, &qlam, &status, &qhi, &probes, &cprobes, &filter, &exists,
                         &rows, &out_ids, &out_dist, &ord, &dmap, &dwords, &pdist, &cqhi, &gmax, &crec, &cbq, &craw,
                         &ibq, &rsurv, &rcnt, &rrecs, &qdelta, &pstats}) {
@@ -880,16 +882,16 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     const int64_t bm = (seg->n + 7) / 8;
     if (!dev) {
         float *q = (float *)ws.queries.get(sizeof(float) * (size_t)nq * d);
-        MQVS_HIP(hipMemcpyAsync(q, queries, sizeof(float) * (size_t)nq * d, hipMemcpyHostToDevice, s));
+        stage_in(ws.pin_q, q, queries, sizeof(float) * (size_t)nq * d, s);
         dq = q;
         if (filter) {
             auto *f = (uint8_t *)ws.filter.get(bm);
-            MQVS_HIP(hipMemcpyAsync(f, filter, bm, hipMemcpyHostToDevice, s));
+            stage_in(ws.pin_f, f, filter, bm, s);
             dfilter = f;
         }
         if (exists) {
             auto *f = (uint8_t *)ws.exists.get(bm);
-            MQVS_HIP(hipMemcpyAsync(f, exists, bm, hipMemcpyHostToDevice, s));
+            stage_in(ws.pin_e, f, exists, bm, s);
             dexists = f;
         }
     }
@@ -1151,6 +1153,11 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
     }
     int64_t *hs = ws.host;
     int *hst = reinterpret_cast<int *>(ws.host + 4);
+    if (!dev) {
+        // (host outputs: copied before the final wait)
+        if (ix->row_ids_map) launch_map_ids(dids, (int64_t)nq * k, ix->row_ids_map, s);
+        stage_out_begin(ws.pin_o, dids, ddist, (size_t)nq * k, s);
+    }
     launch_words_to_host(dstats, 4, status, 8, hs, hst, s, stats_per_query ? dstats : nullptr, nq);
     MQVS_HIP(hipGetLastError());
     host_wait(s);
@@ -1165,12 +1172,7 @@ static void search_index_impl(mqvs_index *ix, const float *queries, int nq, int 
         fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not repeat within " + std::to_string(maxv) +
                                    " steps on a part of more chunks");
     }
-    if (!dev) {
-        if (ix->row_ids_map) launch_map_ids(dids, (int64_t)nq * k, ix->row_ids_map, s);
-        MQVS_HIP(hipMemcpyAsync(out_ids, dids, sizeof(int64_t) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
-        MQVS_HIP(hipMemcpyAsync(out_dist, ddist, sizeof(float) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
-        host_wait(s);
-    }
+    if (!dev) stage_out_end(ws.pin_o, out_ids, out_dist, (size_t)nq * k);
     st.values = hs[0];
     st.items = hs[1];
     st.plane_bytes = hs[2];

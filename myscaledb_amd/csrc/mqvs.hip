@@ -19,6 +19,7 @@
 #include <map>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "mqvs_internal.h"
@@ -97,6 +98,7 @@ struct Workspace {
         overflow, out_ids, out_dist, misc, qhi, bq, thr, cand2, count2, gcount, goff, glist, large, sticky, surv,
         recs, flags, p4q, qord;
     int *host_flags = nullptr;  // pinned (64 ints; the selected-row count record at kCountRec)
+    HostBuf pin_q, pin_f, pin_e, pin_o;  // pinned staging of host-pointer calls (stage_in / stage_out_results)
     int64_t count_gen = 0;      // generation of the last selected-row count record asked for
     bool pending_timing = false, pending_bf16 = false;  // search_collect_stats
     int device = 0;
@@ -133,6 +135,7 @@ struct Workspace {
             b += x->cap;
             x->release();
         }
+        for (HostBuf *x : {&pin_q, &pin_f, &pin_e, &pin_o}) x->release();  // (host memory: not counted)
         return b;
     }
     // free every buffer but the ASYNC sticky word (and the index scratch
@@ -386,9 +389,23 @@ static void fault_point_mid() {
 // Host waits (mqvs_set_wait_mode).  The reference admits up to 2 x physical
 // cores concurrent scans (ScanThreadLimiter.h:25-58, MergeTreeVSManager.cpp:
 // 974-975); here each of them waits for its GPU work, and a waiting thread
-// that spins holds a host core for the whole search.  HYBRID polls the
-// completion of a blocking-sync event for up to spin_us (a short search
-// returns without a wake-up) and then sleeps in hipEventSynchronize on it.
+// that spins holds a host core for the whole search.  On ROCm neither
+// hipStreamSynchronize nor hipEventSynchronize on a hipEventBlockingSync
+// event sleeps (the runtime documents BlockingSync as a synonym of Yield;
+// measured: thread CPU time = wall time in every runtime mode,
+// profiles/r06/host_cpu_wait_runtime.jsonl), so the library sleeps itself:
+// HYBRID polls the work's completion event for up to spin_us (a short
+// search returns without a wake-up), then sleeps most of the time this
+// thread's recent waits took (the shorter of the last two: searches of one
+// thread are alike, and a shorter one must not wait behind a longer one's
+// estimate): to 97 % of it, then polls through its end (at most a tenth of
+// it), then -- a first wait, or a longer one -- polls with sleeps of 1/32 of
+// the time waited so far (10-200 us: the overshoot stays a few per cent of
+// the wait).  Sleeps are shortened by how late this thread's wake-ups have
+// landed; a wait found done on waking shrinks the estimate by 10 %, so the
+// estimate approaches the work's length from above without learning the
+// sleep's overshoot; an expected wait under 3 wake-up latenesses is polled
+// through (a sleep cannot save much of it).  BLOCK skips both polls.
 static std::atomic<int> g_wait_mode{MQVS_WAIT_HYBRID};
 static std::atomic<int> g_wait_spin_us{50};
 
@@ -420,8 +437,8 @@ int wait_spin_us() {
     return m == MQVS_WAIT_RUNTIME ? -1 : m == MQVS_WAIT_BLOCK ? 0 : g_wait_spin_us.load(std::memory_order_relaxed);
 }
 
-// one blocking-sync event per thread and device (the current one)
-static hipEvent_t blocking_event() {
+// one completion event per thread and device (the current one)
+static hipEvent_t wait_event() {
     struct Events {
         std::map<int, hipEvent_t> ev;
         ~Events() {
@@ -432,7 +449,7 @@ static hipEvent_t blocking_event() {
     int dev = 0;
     MQVS_HIP(hipGetDevice(&dev));
     hipEvent_t &e = t_ev.ev[dev];
-    if (!e) MQVS_HIP(hipEventCreateWithFlags(&e, hipEventBlockingSync | hipEventDisableTiming));
+    if (!e) MQVS_HIP(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     return e;
 }
 
@@ -442,20 +459,86 @@ void host_wait(hipStream_t s) {
         MQVS_HIP(hipStreamSynchronize(s));
         return;
     }
-    hipEvent_t e = blocking_event();
+    using clk = std::chrono::steady_clock;
+    static thread_local double t_hist[2] = {0.0, 0.0};  // this thread's last two waits (us)
+    static thread_local double t_late = 60.0;            // how late this thread's sleeps wake (us)
+    hipEvent_t e = wait_event();
     MQVS_HIP(hipEventRecord(e, s));
-    if (spin > 0) {
-        const auto t0 = std::chrono::steady_clock::now();
-        const auto lim = std::chrono::microseconds(spin);
-        while (true) {
-            const hipError_t q = hipEventQuery(e);
-            if (q == hipSuccess) return;
-            if (q != hipErrorNotReady) MQVS_HIP(q);
-            if (std::chrono::steady_clock::now() - t0 > lim) break;
+    const auto t0 = clk::now();
+    auto since = [](clk::time_point a) { return std::chrono::duration<double, std::micro>(clk::now() - a).count(); };
+    auto done = [&]() {
+        const hipError_t q = hipEventQuery(e);
+        if (q == hipSuccess) return true;
+        if (q != hipErrorNotReady) MQVS_HIP(q);
+        return false;
+    };
+    bool fin = done();
+    auto poll_to = [&](double stop_us) {
+        while (!fin && since(t0) < stop_us) {
             for (int i = 0; i < 32; ++i) cpu_relax();
+            fin = done();
+        }
+    };
+    auto nap = [&](double us) {  // sleep, learning how late the wake-up lands
+        const auto a = clk::now();
+        std::this_thread::sleep_for(std::chrono::microseconds((int64_t)us));
+        t_late = 0.8 * t_late + 0.2 * std::min(1000.0, std::max(0.0, since(a) - us));
+        fin = done();
+    };
+    // 1. poll (HYBRID)
+    poll_to(spin);
+    const double hint = std::min(t_hist[0], t_hist[1]);
+    // what this wait tells the next one: the time waited, except when the
+    // work was found done on waking from step 2 -- it ended somewhere before,
+    // and recording the wake-up time would ratchet the estimate up by the
+    // sleep's overshoot every search; shrink the estimate instead, until a
+    // wake-up lands before the end and step 3's poll times it
+    double learned = -1;
+    if (!fin && hint > 0) {
+        if (spin > 0 && hint < 3 * t_late) {
+            // (HYBRID, a wait too short for a sleep to pay: poll it through)
+            poll_to(2 * hint + spin);
+        } else {
+            // 2. sleep to 97 % of the expected time, less the wake-up's lateness
+            const double until = 0.97 * hint - t_late, now_us = since(t0);
+            if (until > now_us + 20) {
+                nap(until - now_us);
+                if (fin) learned = std::min(since(t0), 0.9 * hint);
+            }
+            // 3. poll through the expected end (at most a tenth of the expected time)
+            poll_to(std::min(1.1 * hint, since(t0) + 0.1 * hint));
         }
     }
-    MQVS_HIP(hipEventSynchronize(e));
+    // 4. sleep-poll (a first wait, or one longer than expected)
+    while (!fin) nap(std::min(200.0, std::max(10.0, since(t0) / 32)));
+    // (a wait the first poll covers -- a status copy after the work, say --
+    // says nothing about the next search's length)
+    const double w = learned > 0 ? learned : since(t0);
+    if (w > 50.0) {
+        t_hist[1] = t_hist[0];
+        t_hist[0] = w;
+    }
+}
+
+void stage_out_begin(HostBuf &pin, const int64_t *dids, const float *ddist, size_t m, hipStream_t s) {
+    auto *h = (unsigned char *)pin.get(12 * m);
+    if (!m) return;
+    MQVS_HIP(hipMemcpyAsync(h, dids, 8 * m, hipMemcpyDeviceToHost, s));
+    MQVS_HIP(hipMemcpyAsync(h + 8 * m, ddist, 4 * m, hipMemcpyDeviceToHost, s));
+}
+
+void stage_out_end(const HostBuf &pin, int64_t *ids, float *dist, size_t m) {
+    if (!m) return;
+    const auto *h = (const unsigned char *)pin.p;
+    std::memcpy(ids, h, 8 * m);
+    std::memcpy(dist, h + 8 * m, 4 * m);
+}
+
+void stage_out_results(HostBuf &pin, int64_t *ids, float *dist, const int64_t *dids, const float *ddist, size_t m,
+                       hipStream_t s) {
+    stage_out_begin(pin, dids, ddist, m, s);
+    host_wait(s);
+    stage_out_end(pin, ids, dist, m);
 }
 
 void ws_detach_ext(int device, WsExt *ext) {
@@ -845,16 +928,16 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     const uint8_t *dfilter = filter, *dexists = exists;
     if (!dev) {
         float *q = (float *)ws.get(ws.queries, sizeof(float) * (size_t)nq * d);
-        MQVS_HIP(hipMemcpyAsync(q, queries, sizeof(float) * (size_t)nq * d, hipMemcpyHostToDevice, s));
+        stage_in(ws.pin_q, q, queries, sizeof(float) * (size_t)nq * d, s);
         dq = q;
         if (filter) {
             auto *f = (uint8_t *)ws.get(ws.filter, bm_bytes);
-            MQVS_HIP(hipMemcpyAsync(f, filter, bm_bytes, hipMemcpyHostToDevice, s));
+            stage_in(ws.pin_f, f, filter, bm_bytes, s);
             dfilter = f;
         }
         if (exists) {
             auto *f = (uint8_t *)ws.get(ws.exists, bm_bytes);
-            MQVS_HIP(hipMemcpyAsync(f, exists, bm_bytes, hipMemcpyHostToDevice, s));
+            stage_in(ws.pin_e, f, exists, bm_bytes, s);
             dexists = f;
         }
     }
@@ -1258,6 +1341,8 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     } else {
         // [overflow 4][status 4] in one copy -> host_flags[0] overflow bits,
         // [1] status, [4..6] survivor / candidate stats
+        // (host outputs: copied with the status words, one wait)
+        if (!dev) stage_out_begin(ws.pin_o, dids, ddist, (size_t)nq * k, s);
         MQVS_HIP(hipMemcpyAsync(ws.host_flags + 16, fl, 8 * sizeof(int), hipMemcpyDeviceToHost, s));
         host_wait(s);
         ws.host_flags[0] = ws.host_flags[16];
@@ -1305,11 +1390,10 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
             host_wait(s);
         }
         st.rescans = rescans;
-        if (!dev) {
-            MQVS_HIP(hipMemcpyAsync(out_ids, dids, sizeof(int64_t) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
-            MQVS_HIP(hipMemcpyAsync(out_dist, ddist, sizeof(float) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
-            host_wait(s);
-        }
+        if (!dev && rescans)
+            stage_out_results(ws.pin_o, out_ids, out_dist, dids, ddist, (size_t)nq * k, s);
+        else if (!dev)
+            stage_out_end(ws.pin_o, out_ids, out_dist, (size_t)nq * k);
         if (timing) read_search_times(ws, st);
     }
     g_stats = st;
@@ -1401,16 +1485,15 @@ static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const i
     float *ddist = out_dist;
     if (!dev) {
         float *q = (float *)ws.get(ws.queries, sizeof(float) * (size_t)nq * d);
-        MQVS_HIP(hipMemcpyAsync(q, queries, sizeof(float) * (size_t)nq * d, hipMemcpyHostToDevice, s));
+        stage_in(ws.pin_q, q, queries, sizeof(float) * (size_t)nq * d, s);
         dq = q;
         int64_t *c = (int64_t *)ws.get(ws.misc, sizeof(int64_t) * std::max<size_t>((size_t)nq * ncand, 1));
-        if (ncand > 0)
-            MQVS_HIP(hipMemcpyAsync(c, cand, sizeof(int64_t) * (size_t)nq * ncand, hipMemcpyHostToDevice, s));
+        if (ncand > 0) stage_in(ws.pin_f, c, cand, sizeof(int64_t) * (size_t)nq * ncand, s);
         dc = c;
         if (exists) {
             const int64_t bm = (seg->n + 7) / 8;
             auto *f = (uint8_t *)ws.get(ws.exists, bm);
-            MQVS_HIP(hipMemcpyAsync(f, exists, bm, hipMemcpyHostToDevice, s));
+            stage_in(ws.pin_e, f, exists, bm, s);
             dexists = f;
         }
         dids = (int64_t *)ws.get(ws.out_ids, sizeof(int64_t) * (size_t)nq * k);
@@ -1448,16 +1531,13 @@ static void rerank_impl(mqvs_segment *seg, const float *queries, int nq, const i
         MQVS_HIP(hipGetLastError());
         return;
     }
+    if (!dev) stage_out_begin(ws.pin_o, dids, ddist, (size_t)nq * k, s);
     MQVS_HIP(hipMemcpyAsync(ws.host_flags, status, sizeof(int), hipMemcpyDeviceToHost, s));
     host_wait(s);
     if (ws.host_flags[0] && ords > maxv)
         fail(MQVS_ERR_LOGICAL, "cosine query normalisation did not repeat within " + std::to_string(maxv) +
                                    " steps on a part of more chunks");
-    if (!dev) {
-        MQVS_HIP(hipMemcpyAsync(out_ids, dids, sizeof(int64_t) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
-        MQVS_HIP(hipMemcpyAsync(out_dist, ddist, sizeof(float) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
-        host_wait(s);
-    }
+    if (!dev) stage_out_end(ws.pin_o, out_ids, out_dist, (size_t)nq * k);
 }
 
 
@@ -1552,12 +1632,12 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
     if (!dev) {
         if (filter) {
             auto *f = (uint8_t *)ws.get(ws.filter, bm_bytes);
-            MQVS_HIP(hipMemcpyAsync(f, filter, bm_bytes, hipMemcpyHostToDevice, s));
+            stage_in(ws.pin_f, f, filter, bm_bytes, s);
             dfilter = f;
         }
         if (exists) {
             auto *f = (uint8_t *)ws.get(ws.exists, bm_bytes);
-            MQVS_HIP(hipMemcpyAsync(f, exists, bm_bytes, hipMemcpyHostToDevice, s));
+            stage_in(ws.pin_e, f, exists, bm_bytes, s);
             dexists = f;
         }
     }
@@ -1665,6 +1745,7 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
         launch_async_flags(overflow, nullptr, 0, sticky_word(ws, s), s);
         MQVS_HIP(hipGetLastError());
     } else {
+        if (!dev) stage_out_begin(ws.pin_o, dids, ddist, (size_t)nq * k, s);
         MQVS_HIP(hipMemcpyAsync(ws.host_flags, overflow, sizeof(int), hipMemcpyDeviceToHost, s));
         host_wait(s);
         int rescans = 0;
@@ -1685,11 +1766,10 @@ static void search_binary_impl(mqvs_segment *seg, const uint8_t *queries, int nq
             host_wait(s);
         }
         st.rescans = rescans;
-        if (!dev) {
-            MQVS_HIP(hipMemcpyAsync(out_ids, dids, sizeof(int64_t) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
-            MQVS_HIP(hipMemcpyAsync(out_dist, ddist, sizeof(float) * (size_t)nq * k, hipMemcpyDeviceToHost, s));
-            host_wait(s);
-        }
+        if (!dev && rescans)
+            stage_out_results(ws.pin_o, out_ids, out_dist, dids, ddist, (size_t)nq * k, s);
+        else if (!dev)
+            stage_out_end(ws.pin_o, out_ids, out_dist, (size_t)nq * k);
         if (timing) {
             float a = 0, b = 0, c = 0, e = 0, f = 0;
             MQVS_HIP(hipEventElapsedTime(&a, ws.ev[5], ws.ev[1]));

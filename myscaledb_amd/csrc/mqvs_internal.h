@@ -4,6 +4,7 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include <cstring>
 #include <string>
 #include <stdexcept>
 #include <algorithm>
@@ -564,6 +565,40 @@ struct DevBuf {
     }
 };
 
+// Pinned host staging of a synchronous call's host inputs and outputs: the
+// caller's (pageable) arrays are copied by the CPU into it and DMA'd from it,
+// so the HIP runtime never stages a pageable copy itself (it waits for those
+// by spinning: with 16 threads searching 10M x 768 at nq 1000 from host
+// arrays, 18 % of each thread's wall time was CPU time, profiles/r06).
+// Reused across calls (each synchronous call ends after its copies).
+struct HostBuf {
+    void *p = nullptr;
+    size_t cap = 0;
+    void *get(size_t bytes) {
+        if (bytes == 0) bytes = 16;
+        if (bytes > cap) {
+            if (p) (void)hipHostFree(p);
+            p = nullptr;
+            cap = 0;
+            MQVS_HIP(hipHostMalloc(&p, bytes, hipHostMallocDefault));
+            cap = bytes;
+        }
+        return p;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+// host -> device through `pin` (the CPU copy now, the DMA queued on s)
+inline void stage_in(HostBuf &pin, void *dst, const void *src, size_t bytes, hipStream_t s) {
+    if (!bytes) return;
+    void *h = pin.get(bytes);
+    std::memcpy(h, src, bytes);
+    MQVS_HIP(hipMemcpyAsync(dst, h, bytes, hipMemcpyHostToDevice, s));
+}
+
 // Per-thread scratch of another path (the index's, index.hip) counted in, and
 // trimmed with, the calling thread's FLAT workspace under the process-wide
 // HBM budget (mqvs_set_workspace_budget): the reference runs index searches
@@ -645,6 +680,16 @@ int device_cus();
 // holding a core for the length of the search).  The current device must be
 // s's.
 void host_wait(hipStream_t s);
+// the ids and distances of a synchronous host-pointer call: device ->
+// pinned `pin` -> the caller's arrays (m results each), after the work queued
+// on s (one host_wait)
+void stage_out_results(HostBuf &pin, int64_t *ids, float *dist, const int64_t *dids, const float *ddist, size_t m,
+                       hipStream_t s);
+// the same in two halves, so the call's last host_wait covers the copies:
+// begin queues the device -> pinned copies on s, end (after that wait)
+// copies pinned -> the caller's arrays
+void stage_out_begin(HostBuf &pin, const int64_t *dids, const float *ddist, size_t m, hipStream_t s);
+void stage_out_end(const HostBuf &pin, int64_t *ids, float *dist, size_t m);
 // poll budget of the hybrid wait (microseconds; 0 in MQVS_WAIT_BLOCK, -1 in
 // MQVS_WAIT_RUNTIME): also bounds the spin on a pinned-memory word
 int wait_spin_us();
