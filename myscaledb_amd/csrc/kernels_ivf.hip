@@ -1307,8 +1307,16 @@ __global__ __launch_bounds__(SEL_THREADS) __attribute__((amdgpu_waves_per_eu(4))
     uint32_t *keys = reinterpret_cast<uint32_t *>(dyn + NR);
     const int qi = blockIdx.x, t = threadIdx.x, lane = t & 63, wv = t >> 6;
     const float *row = gmax + (int64_t)qi * gld;
+    // T = 1 (nprobe 1): the best (key, group) kept while staging -- one pass
+    // and a block minimum instead of a second pass over the keys
+    uint64_t best = ~0ull;
     if (STAGED) {
-        for_each_f4(row, ngroups, [&](int64_t i, float v) { keys[i] = okey<METRIC>(v); });
+        for_each_f4(row, ngroups, [&](int64_t i, float v) {
+            const uint32_t k = okey<METRIC>(v);
+            keys[i] = k;
+            const uint64_t pr = ((uint64_t)k << 32) | (uint64_t)(uint32_t)i;
+            if (k != 0xFFFFFFFFu && pr < best) best = pr;
+        });
         __syncthreads();
     }
     if (tr) ts[1] = wall_clock64();
@@ -1317,7 +1325,30 @@ __global__ __launch_bounds__(SEL_THREADS) __attribute__((amdgpu_waves_per_eu(4))
     uint64_t tpair = ~0ull;  // the T-th (key << 32 | group)
     int ncore = 0;
     uint32_t th = 0xFFFFFFFEu;
-    if (T <= kSelSmallK) {
+    if (T == 1 && STAGED) {
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint64_t o = __shfl_xor(best, off);
+            best = o < best ? o : best;
+        }
+        if (lane == 0) s_red[wv] = best;
+        __syncthreads();
+        best = s_red[0];
+#pragma unroll
+        for (int w = 1; w < SEL_THREADS / 64; ++w) best = s_red[w] < best ? s_red[w] : best;
+        if (best != ~0ull) {
+            ncore = 1;
+            tpair = best;
+            if (t == 0) s_grp[0] = (int)(uint32_t)best;
+        }
+        th = tpair == ~0ull ? 0xFFFFFFFEu : (uint32_t)(tpair >> 32);
+        __syncthreads();  // (s_red, s_grp)
+    } else if (T <= 2) {
+        ncore = block_topk_small<SEL_THREADS, 2>(keyof, ngroups, T, s_red, s_grp, &tpair);
+        th = tpair == ~0ull ? 0xFFFFFFFEu : (uint32_t)(tpair >> 32);
+    } else if (T <= 4) {
+        ncore = block_topk_small<SEL_THREADS, 4>(keyof, ngroups, T, s_red, s_grp, &tpair);
+        th = tpair == ~0ull ? 0xFFFFFFFEu : (uint32_t)(tpair >> 32);
+    } else if (T <= kSelSmallK) {
         ncore = block_topk_small(keyof, ngroups, T, s_red, s_grp, &tpair);
         th = tpair == ~0ull ? 0xFFFFFFFEu : (uint32_t)(tpair >> 32);
     } else {

@@ -900,17 +900,26 @@ void launch_chunk_ordinals(const uint8_t *filter, const uint8_t *nonempty, const
     hipLaunchKernelGGL(k_exclusive_ord, dim3(1), dim3(kScanThreads), 0, s, ord, nchunks);
 }
 
-__global__ void k_words_to_host(const int64_t *a, int na, const int *b, int nb, int64_t *ha, int *hb,
-                                const int64_t *pq, int npq) {
-    const int t = threadIdx.x;
+__global__ __launch_bounds__(256) void k_words_to_host(const int64_t *a, int na, const int *b, int nb, int64_t *ha,
+                                                      int *hb, const int64_t *pq, int npq) {
+    const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
     if (pq) {
-        // one wave: column sums of pq[npq][na]
-        for (int c = 0; c < na; ++c) {
-            int64_t v = 0;
-            for (int r = t; r < npq; r += 64) v += pq[(int64_t)r * na + c];
-            for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
-            if (t == 0) *reinterpret_cast<volatile int64_t *>(ha + c) = v;
+        // column sums of pq[npq][na] (na <= 4): each thread its rows' na
+        // words (independent loads, 4 rows in flight), then the block sum
+        __shared__ int64_t part[4][4];
+        int64_t v[4] = {0, 0, 0, 0};
+#pragma unroll 4
+        for (int r = t; r < npq; r += 256)
+#pragma unroll
+            for (int c = 0; c < 4; ++c)
+                if (c < na) v[c] += pq[(int64_t)r * na + c];
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+            for (int off = 32; off > 0; off >>= 1) v[c] += __shfl_xor(v[c], off);
+            if (lane == 0) part[wv][c] = v[c];
         }
+        __syncthreads();
+        if (t < na) *reinterpret_cast<volatile int64_t *>(ha + t) = part[0][t] + part[1][t] + part[2][t] + part[3][t];
     } else if (t < na) {
         *reinterpret_cast<volatile int64_t *>(ha + t) = a[t];
     }
@@ -920,7 +929,8 @@ __global__ void k_words_to_host(const int64_t *a, int na, const int *b, int nb, 
 
 void launch_words_to_host(const int64_t *a, int na, const int *b, int nb, int64_t *host_a, int *host_b,
                           hipStream_t s, const int64_t *pq, int npq) {
-    hipLaunchKernelGGL(k_words_to_host, dim3(1), dim3(64), 0, s, a, na, b, nb, host_a, host_b, pq, npq);
+    if (pq && na > 4) fail(MQVS_ERR_LOGICAL, "words_to_host: more than 4 summed columns");
+    hipLaunchKernelGGL(k_words_to_host, dim3(1), dim3(pq ? 256 : 64), 0, s, a, na, b, nb, host_a, host_b, pq, npq);
 }
 
 // ---------------------------------------------------------------------------

@@ -454,6 +454,102 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids_tiled(ScanParams p, 
     rerank_emit<METRIC>(recs, g, ncand, k, q, id_offset, out_ids, out_dist);
 }
 
+// Two queries per workgroup (waves 0-1: query 2 b, waves 2-3: query 2 b + 1),
+// for up to kRrPairMax candidates: k_rerank_ids_tiled's chain and records,
+// each query's candidates 128 at a time over its two waves.  At ~233 VGPRs
+// two waves per SIMD fit -- two workgroups per CU: one query per workgroup
+// took two rounds of 1000 workgroups at nq 1000, each as long as a 24-tile
+// random-row chain, and after pruning (~120 of 200 candidates kept) half of
+// its waves had no rows; here 500 workgroups are one round.  The top k is
+// placed by rank counting over the kept prefix (records are unique: key, then
+// row; equal records -- a row listed twice -- rank by position, as a stable
+// sort), the same output as rerank_emit's sort.
+constexpr int kRrPairMax = 512;
+
+template <int METRIC, bool DIRECT>
+__global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids_pair(ScanParams p, const int64_t *cand, int ncand,
+                                                                int k, int64_t id_offset, int64_t *out_ids,
+                                                                float *out_dist, RerankPrune pr) {
+    extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+    __shared__ int s_m[2], s_ok[2], s_nv[2];
+    __shared__ float s_cut[2];
+    const int h = threadIdx.x >> 7, ht = threadIdx.x & 127, wv = threadIdx.x >> 6;
+    const int q = blockIdx.x * 2 + h;
+    const bool act = q < p.nq;
+    const int qq = act ? q : 0;
+    uint4 *recs = reinterpret_cast<uint4 *>(smem) + (size_t)h * ncand;
+    float *tile = reinterpret_cast<float *>(smem + 2 * (size_t)ncand * sizeof(uint4)) + wv * 64 * kRrStride;
+    if (ht == 0) {
+        s_m[h] = act ? ncand : 0;
+        s_ok[h] = 0;
+        s_nv[h] = 0;
+    }
+    // the cut (rerank_keep, per half): its first wave
+    if (act && pr.raw && k < ncand && ht < 64) {
+        float w = 0.f;
+        const bool ok = wave_prune_cut<METRIC>(p, pr, q, ncand, k, w);
+        if (ht == 0) {
+            s_cut[h] = w;
+            s_ok[h] = ok ? 1 : 0;
+        }
+    }
+    __syncthreads();
+    if (act && s_ok[h]) {
+        const float w = s_cut[h];
+        const float *raw = pr.raw + (int64_t)q * ncand;
+        for (int i = ht; i < ncand; i += 128) {
+            const float a = raw[i];
+            const bool keep = METRIC == MQVS_METRIC_L2 ? a <= w : a >= w;
+            if (!keep) {
+                atomicMin(&s_m[h], i);
+                break;
+            }
+        }
+    }
+    __syncthreads();
+    const int m = s_m[h];
+    if (act && ht == 0 && pr.count) atomicAdd(pr.count, (unsigned long long)m);
+    const int64_t *c = cand + (int64_t)qq * ncand;
+    for (int cb = 0; cb < ncand; cb += 128) {
+        const int i = cb + ht;
+        int64_t row = -1;
+        if (i < m) {
+            row = c[i];
+            if (!(row >= 0 && row < p.n && row_valid(p, row))) row = -1;
+        }
+        const float raw = cb < m ? wave_exact_any<METRIC, DIRECT>(p, qq, row, tile) : 0.f;
+        if (i < ncand) recs[i] = rerank_rec<METRIC>(p, row, raw);
+    }
+    __syncthreads();
+    // records at m and later are invalid (all ones: never less than a valid one)
+    if (act) {
+        for (int i = ht; i < m; i += 128) {
+            const uint4 e = recs[i];
+            if (e.x == 0xFFFFFFFFu) continue;
+            int rank = 0;
+            for (int o = 0; o < m; ++o) {
+                const uint4 f = recs[o];
+                rank += (rec_less(f, e) || (o < i && f.x == e.x && f.y == e.y && f.z == e.z && f.w == e.w)) ? 1 : 0;
+            }
+            atomicAdd(&s_nv[h], 1);
+            if (rank < k) {
+                out_ids[(int64_t)q * k + rank] = (int64_t)e.w + id_offset;
+                out_dist[(int64_t)q * k + rank] = key_to_value(METRIC, e.x);
+            }
+        }
+    }
+    __syncthreads();
+    if (act) {
+        const float pad = (METRIC == MQVS_METRIC_IP) ? 1.17549435e-38f
+                          : (METRIC == kMetricIpRaw) ? -3.40282347e+38f
+                                                     : 3.40282347e+38f;
+        for (int i = s_nv[h] + ht; i < k; i += 128) {
+            out_ids[(int64_t)q * k + i] = -1;
+            out_dist[(int64_t)q * k + i] = pad;
+        }
+    }
+}
+
 // ---------------------------------------------------------------------------
 // Exact re-rank of the pre-filter's survivors, spread over the whole chip
 // (mqvs_search path 2): query q's cnt[q] survivor rows are surv[q * rs + i];
@@ -684,7 +780,11 @@ static void rerank_ids_t(const ScanParams &p, const int64_t *cand, int ncand, in
     int N = 1;
     while (N < ncand) N <<= 1;
     if (scratch) N = kSortCap;  // LDS records of global_sort
-    if ((p.d & 3) == 0) {
+    if ((p.d & 3) == 0 && !scratch && ncand <= kRrPairMax && tune_int("MQVS_RR_PAIR", 1) == 1) {
+        const size_t lds = 2 * (size_t)ncand * sizeof(uint4) + (SEL_THREADS / 64) * 64 * kRrStride * sizeof(float);
+        hipLaunchKernelGGL((k_rerank_ids_pair<M, DIRECT>), dim3((p.nq + 1) / 2), dim3(SEL_THREADS), lds, s, p, cand,
+                           ncand, k, id_offset, ids, dist, pr);
+    } else if ((p.d & 3) == 0) {
         const size_t lds = N * sizeof(uint4) + (SEL_THREADS / 64) * 64 * kRrStride * sizeof(float);
         hipLaunchKernelGGL((k_rerank_ids_tiled<M, DIRECT>), dim3(p.nq), dim3(SEL_THREADS), lds, s, p, cand, ncand, k,
                            id_offset, ids, dist, N, scratch, pr);

@@ -159,14 +159,19 @@ __device__ inline uint32_t block_radix_select_mlp(KeyFn keyof, int64_t count, in
 // *kth_out = the k-th pair (key << 32 | index), or ~0 when fewer than k.
 // 0xFFFFFFFF keys are never taken; indices < 2^32.  No histogram passes.
 // red: 2 * (NT / 64) words of LDS.
+// KMAX (>= k): the registers kept per thread -- the insertion costs KMAX
+// compare-and-swaps per key, so a k = 1 pick with KMAX 8 spent ~8x the VALU
+// instructions of a minimum (the coarse pick runs 4 workgroups per CU: VALU-
+// bound there, 7-15 us of ~25 per query).
 constexpr int kSelSmallK = 8;
-template <int NT = SEL_THREADS, typename KeyFn>
+template <int NT = SEL_THREADS, int KMAX = kSelSmallK, typename KeyFn>
 __device__ inline int block_topk_small(KeyFn keyof, int64_t count, int k, uint64_t *red, int *idx_out,
                                        uint64_t *kth_out) {
+    static_assert(KMAX >= 1 && KMAX <= kSelSmallK, "KMAX");
     const int t = threadIdx.x, lane = t & 63, wv = t >> 6;
-    uint64_t loc[kSelSmallK];  // (key << 32 | index), ascending
+    uint64_t loc[KMAX];  // (key << 32 | index), ascending
 #pragma unroll
-    for (int j = 0; j < kSelSmallK; ++j) loc[j] = ~0ull;
+    for (int j = 0; j < KMAX; ++j) loc[j] = ~0ull;
     uint64_t worst = ~0ull;  // loc[k - 1]
     for (int64_t i = t; i < count; i += NT) {
         const uint32_t key = keyof(i);
@@ -174,7 +179,7 @@ __device__ inline int block_topk_small(KeyFn keyof, int64_t count, int k, uint64
         uint64_t v = ((uint64_t)key << 32) | (uint64_t)(uint32_t)i;
         if (v >= worst) continue;
 #pragma unroll
-        for (int j = 0; j < kSelSmallK; ++j) {  // sorted insertion; the largest falls off
+        for (int j = 0; j < KMAX; ++j) {  // sorted insertion; the largest falls off
             if (j < k && v < loc[j]) {
                 const uint64_t o = loc[j];
                 loc[j] = v;
@@ -182,7 +187,7 @@ __device__ inline int block_topk_small(KeyFn keyof, int64_t count, int k, uint64
             }
         }
 #pragma unroll
-        for (int j = 0; j < kSelSmallK; ++j)
+        for (int j = 0; j < KMAX; ++j)
             if (j == k - 1) worst = loc[j];
     }
     int head = 0, n = 0;
@@ -190,7 +195,7 @@ __device__ inline int block_topk_small(KeyFn keyof, int64_t count, int k, uint64
     for (int r = 0; r < k; ++r) {
         uint64_t h = ~0ull;
 #pragma unroll
-        for (int j = 0; j < kSelSmallK; ++j)
+        for (int j = 0; j < KMAX; ++j)
             if (j == head) h = loc[j];
         uint64_t m = h;
         for (int off = 32; off > 0; off >>= 1) {

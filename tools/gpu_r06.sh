@@ -91,6 +91,17 @@ for step in "$@"; do
           -- python "$GRAFT_REPO_ROOT/tools/index_search_run.py" --mode 3 --search nprobe=1 --searches 3 \
           > "$GRAFT_REPO_ROOT/$O/itl.log" 2>&1 ) || { echo "itl failed"; tail -5 $O/itl.log; exit 1; }
       python3 tools/timeline.py $O/itl/run_kernel_trace.csv --start k_to_bf16 --nth -1 | tee $O/index_m3_nprobe1_timeline.txt ;;
+    api)
+      # kernel + host HIP-call timelines: one mode-3 nprobe=1 index search, one nq 1 FLAT search
+      ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d "$GRAFT_REPO_ROOT/$O/api_idx" -o run \
+          -- python "$GRAFT_REPO_ROOT/tools/index_search_run.py" --mode 3 --search nprobe=1 --searches 3 \
+          > "$GRAFT_REPO_ROOT/$O/api_idx.log" 2>&1 ) || { echo "api idx failed"; tail -5 $O/api_idx.log; exit 1; }
+      python3 tools/timeline.py $O/api_idx/run_kernel_trace.csv --api $O/api_idx/run_hip_api_trace.csv --start k_to_bf16 --nth -1 > $O/api_idx.txt
+      ( cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --hip-runtime-trace --output-format csv -d "$GRAFT_REPO_ROOT/$O/api_nq1" -o run \
+          -- python3 "$GRAFT_REPO_ROOT/tools/pmc_search.py" --nq 1 --searches 4 > "$GRAFT_REPO_ROOT/$O/api_nq1.log" 2>&1 ) \
+        || { echo "api nq1 failed"; tail -5 $O/api_nq1.log; exit 1; }
+      python3 tools/timeline.py $O/api_nq1/run_kernel_trace.csv --api $O/api_nq1/run_hip_api_trace.csv --start k_query_prep --nth -1 > $O/api_nq1.txt
+      head -30 $O/api_idx.txt ;;
     lds)
       bash tools/gpu_lds_pmc.sh 0 8 4 6 || exit 1 ;;
     cpu)
