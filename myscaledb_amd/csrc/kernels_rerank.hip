@@ -780,7 +780,7 @@ static void rerank_ids_t(const ScanParams &p, const int64_t *cand, int ncand, in
     int N = 1;
     while (N < ncand) N <<= 1;
     if (scratch) N = kSortCap;  // LDS records of global_sort
-    if ((p.d & 3) == 0 && !scratch && ncand <= kRrPairMax && tune_int("MQVS_RR_PAIR", 1) == 1) {
+    if ((p.d & 3) == 0 && !scratch && ncand <= kRrPairMax && tune_int("MQVS_RR_PAIR", 0) == 1) {
         const size_t lds = 2 * (size_t)ncand * sizeof(uint4) + (SEL_THREADS / 64) * 64 * kRrStride * sizeof(float);
         hipLaunchKernelGGL((k_rerank_ids_pair<M, DIRECT>), dim3((p.nq + 1) / 2), dim3(SEL_THREADS), lds, s, p, cand,
                            ncand, k, id_offset, ids, dist, pr);
