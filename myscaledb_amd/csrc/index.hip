@@ -1230,6 +1230,8 @@ int mqvs_index_search(mqvs_index_t idx, const float *queries, int32_t nq, int32_
                       uint32_t flags, mqvs_stream_t stream) {
     return guarded([&] {
         fault_point();
+        WaitScope wsc{4, (uint64_t)(uintptr_t)idx, (uint64_t)nq, (uint64_t)k, wait_str_hash(params), filter != nullptr,
+                      row_exists != nullptr, flags};
         search_index_impl(idx, queries, nq, k, params, filter, row_exists, out_ids, out_dist, flags,
                           (hipStream_t)stream, 0);
     });
@@ -1256,6 +1258,7 @@ int mqvs_index_probes(mqvs_index_t idx, const float *queries, int32_t nq, const 
             ~Reset() { t_probes_out = nullptr; }
         } reset;
         t_probes_out = out_probes;
+        WaitScope wsc{5, (uint64_t)(uintptr_t)idx, (uint64_t)nq, wait_str_hash(params)};
         // k 1: the coarse step does not depend on k; the search stops after it
         std::vector<int64_t> ids((size_t)nq);
         std::vector<float> dd((size_t)nq);

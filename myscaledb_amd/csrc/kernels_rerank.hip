@@ -463,7 +463,11 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids_tiled(ScanParams p, 
 // its waves had no rows; here 500 workgroups are one round.  The top k is
 // placed by rank counting over the kept prefix (records are unique: key, then
 // row; equal records -- a row listed twice -- rank by position, as a stable
-// sort), the same output as rerank_emit's sort.
+// sort), the same output as rerank_emit's sort.  Measured slower (mode 3,
+// nprobe 1, k 100: re-rank 127 -> 140 us; the rows arrive at ~2.9 TB/s either
+// way -- a torch index_select of the same rows runs at 2.5-2.8 TB/s,
+// tools/gather_tlb_probe.py -- so the random-row read rate bounds it, not the
+// rounds): MQVS_RR_PAIR=1, measurement build only.
 constexpr int kRrPairMax = 512;
 
 template <int METRIC, bool DIRECT>

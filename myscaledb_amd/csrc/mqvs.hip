@@ -402,10 +402,13 @@ static void fault_point_mid() {
 // it), then -- a first wait, or a longer one -- polls with sleeps of 1/32 of
 // the time waited so far (10-200 us: the overshoot stays a few per cent of
 // the wait).  Sleeps are shortened by how late this thread's wake-ups have
-// landed; a wait found done on waking shrinks the estimate by 10 %, so the
-// estimate approaches the work's length from above without learning the
-// sleep's overshoot; an expected wait under 3 wake-up latenesses is polled
-// through (a sleep cannot save much of it).  BLOCK skips both polls.
+// landed; a wait found done on waking halves the estimate, so the estimate
+// never learns the sleep's overshoot; an expected wait under 3 wake-up
+// latenesses is polled through (a sleep cannot save much of it), and in
+// HYBRID so is one under 10 spin_us.  The history
+// is kept per call shape and wait position (WaitScope): one history for every
+// call made nq 1 searches after nq 1000 ones sleep 13 ms for 2.4 ms of work.
+// BLOCK skips both polls.
 static std::atomic<int> g_wait_mode{MQVS_WAIT_HYBRID};
 static std::atomic<int> g_wait_spin_us{50};
 
@@ -453,6 +456,26 @@ static hipEvent_t wait_event() {
     return e;
 }
 
+static thread_local uint64_t t_wait_key = 0;  // the current API call's shape (0: none)
+static thread_local int t_wait_ord = 0;        // waits so far in that call
+
+static uint64_t wait_mix(uint64_t h, uint64_t v) {
+    h ^= v + 0x9E3779B97F4A7C15ull + (h << 6) + (h >> 2);
+    return h * 0xFF51AFD7ED558CCDull;
+}
+
+WaitScope::WaitScope(std::initializer_list<uint64_t> parts) : prev_key(t_wait_key), prev_ord(t_wait_ord) {
+    uint64_t h = 0x6A09E667F3BCC909ull;
+    for (uint64_t v : parts) h = wait_mix(h, v);
+    t_wait_key = h | 1;
+    t_wait_ord = 0;
+}
+
+WaitScope::~WaitScope() {
+    t_wait_key = prev_key;
+    t_wait_ord = prev_ord;
+}
+
 void host_wait(hipStream_t s) {
     const int spin = wait_spin_us();
     if (spin < 0) {
@@ -460,8 +483,27 @@ void host_wait(hipStream_t s) {
         return;
     }
     using clk = std::chrono::steady_clock;
-    static thread_local double t_hist[2] = {0.0, 0.0};  // this thread's last two waits (us)
-    static thread_local double t_late = 60.0;            // how late this thread's sleeps wake (us)
+    // this thread's last two waits (us) per wait key: (call shape, position in
+    // the call), 16 keys, least recently used out
+    struct Hist {
+        uint64_t key;
+        double h[2];
+        uint64_t used;
+    };
+    static thread_local Hist t_tab[16];
+    static thread_local uint64_t t_use = 0;
+    static thread_local double t_late = 60.0;  // how late this thread's sleeps wake (us)
+    const uint64_t key = t_wait_key ? wait_mix(t_wait_key, (uint64_t)t_wait_ord++) | 1 : 1;
+    Hist *hs = nullptr;
+    for (Hist &e : t_tab)
+        if (e.key == key) hs = &e;
+    if (!hs) {
+        hs = &t_tab[0];
+        for (Hist &e : t_tab)
+            if (e.used < hs->used) hs = &e;
+        *hs = Hist{key, {0.0, 0.0}, 0};
+    }
+    hs->used = ++t_use;
     hipEvent_t e = wait_event();
     MQVS_HIP(hipEventRecord(e, s));
     const auto t0 = clk::now();
@@ -487,23 +529,28 @@ void host_wait(hipStream_t s) {
     };
     // 1. poll (HYBRID)
     poll_to(spin);
-    const double hint = std::min(t_hist[0], t_hist[1]);
+    const double hint = std::min(hs->h[0], hs->h[1]);
     // what this wait tells the next one: the time waited, except when the
     // work was found done on waking from step 2 -- it ended somewhere before,
     // and recording the wake-up time would ratchet the estimate up by the
-    // sleep's overshoot every search; shrink the estimate instead, until a
-    // wake-up lands before the end and step 3's poll times it
+    // sleep's overshoot every search; halve the estimate instead (a shorter
+    // search than the history's is then re-timed within two waits), and the
+    // next wait's step 3 or 4 times it again
     double learned = -1;
     if (!fin && hint > 0) {
-        if (spin > 0 && hint < 3 * t_late) {
-            // (HYBRID, a wait too short for a sleep to pay: poll it through)
+        if (spin > 0 && hint < std::max(3 * t_late, 10.0 * spin)) {
+            // (HYBRID, a short wait -- under 10 spin_us, 500 us by default, or
+            // 3 wake-up latenesses: polled through.  A sleep there saves
+            // little CPU and its wake-up jitter is a large share of the wait:
+            // 1 % of 50M rows at nq 1, 0.420 ms polled vs 0.457 ms with the
+            // sleep, tools/wait_ab.py.  Under load waits grow past it.)
             poll_to(2 * hint + spin);
         } else {
             // 2. sleep to 97 % of the expected time, less the wake-up's lateness
             const double until = 0.97 * hint - t_late, now_us = since(t0);
             if (until > now_us + 20) {
                 nap(until - now_us);
-                if (fin) learned = std::min(since(t0), 0.9 * hint);
+                if (fin) learned = std::min(since(t0), 0.5 * hint);
             }
             // 3. poll through the expected end (at most a tenth of the expected time)
             poll_to(std::min(1.1 * hint, since(t0) + 0.1 * hint));
@@ -515,8 +562,8 @@ void host_wait(hipStream_t s) {
     // says nothing about the next search's length)
     const double w = learned > 0 ? learned : since(t0);
     if (w > 50.0) {
-        t_hist[1] = t_hist[0];
-        t_hist[0] = w;
+        hs->h[1] = hs->h[0];
+        hs->h[0] = w;
     }
 }
 
@@ -2176,6 +2223,8 @@ int mqvs_search(mqvs_segment_t seg, const float *queries, int32_t nq, int32_t k,
                 uint32_t flags, mqvs_stream_t stream) {
     return guarded([&] {
         fault_point();
+        WaitScope wsc{1, (uint64_t)(uintptr_t)seg, (uint64_t)nq, (uint64_t)k, (uint64_t)metric, filter != nullptr,
+                      row_exists != nullptr, flags};
         search_impl(seg, queries, nq, k, metric, filter, row_exists, out_ids, out_dist, flags,
                     (hipStream_t)stream);
     });
@@ -2187,6 +2236,8 @@ int mqvs_search_ex(mqvs_segment_t seg, const float *queries, int32_t nq, int32_t
     return guarded([&] {
         fault_point();
         if (chunk_ord_base > INT32_MAX) fail(MQVS_ERR_BAD_ARGUMENTS, "chunk_ord_base out of range");
+        WaitScope wsc{1, (uint64_t)(uintptr_t)seg, (uint64_t)nq, (uint64_t)k, (uint64_t)metric, filter != nullptr,
+                      row_exists != nullptr, flags};
         search_impl(seg, queries, nq, k, metric, filter, row_exists, out_ids, out_dist, flags,
                     (hipStream_t)stream, false, chunk_ord_base);
     });
@@ -2262,6 +2313,8 @@ int mqvs_search_binary(mqvs_segment_t seg, const uint8_t *queries, int32_t nq, i
                        uint32_t flags, mqvs_stream_t stream) {
     return guarded([&] {
         fault_point();
+        WaitScope wsc{2, (uint64_t)(uintptr_t)seg, (uint64_t)nq, (uint64_t)k, (uint64_t)metric, filter != nullptr,
+                      row_exists != nullptr, flags};
         search_binary_impl(seg, queries, nq, k, metric, filter, row_exists, out_ids, out_dist, flags,
                            (hipStream_t)stream);
     });
@@ -2378,6 +2431,8 @@ int mqvs_rerank(mqvs_segment_t seg, const float *queries, int32_t nq, const int6
                 int32_t ncand, int32_t k, int32_t metric, const uint8_t *row_exists, int64_t *out_ids,
                 float *out_dist, uint32_t flags, mqvs_stream_t stream) {
     return guarded([&] {
+        WaitScope wsc{3, (uint64_t)(uintptr_t)seg, (uint64_t)nq, (uint64_t)ncand, (uint64_t)k, (uint64_t)metric,
+                      row_exists != nullptr, flags};
         rerank_impl(seg, queries, nq, cand, ncand, k, metric, row_exists, out_ids, out_dist, flags,
                     (hipStream_t)stream);
     });

@@ -5,6 +5,7 @@
 #include <stdint.h>
 
 #include <cstring>
+#include <initializer_list>
 #include <string>
 #include <stdexcept>
 #include <algorithm>
@@ -680,6 +681,23 @@ int device_cus();
 // holding a core for the length of the search).  The current device must be
 // s's.
 void host_wait(hipStream_t s);
+// The wait history's key for the host_waits of one API call: set by the
+// entry points from the call's shape (function, segment, nq, k, filter,
+// flags); each wait position within the call keeps its own history, so a
+// thread alternating nq 1000 and nq 1 searches sleeps each for its own length.
+struct WaitScope {
+    uint64_t prev_key;
+    int prev_ord;
+    explicit WaitScope(std::initializer_list<uint64_t> parts);
+    ~WaitScope();
+    WaitScope(const WaitScope &) = delete;
+    WaitScope &operator=(const WaitScope &) = delete;
+};
+inline uint64_t wait_str_hash(const char *p) {  // (a parameter string's part of a wait key)
+    uint64_t h = 1469598103934665603ull;
+    for (; p && *p; ++p) h = (h ^ (unsigned char)*p) * 1099511628211ull;
+    return h;
+}
 // the ids and distances of a synchronous host-pointer call: device ->
 // pinned `pin` -> the caller's arrays (m results each), after the work queued
 // on s (one host_wait)

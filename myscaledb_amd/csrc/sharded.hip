@@ -668,6 +668,8 @@ int mqvs_sharded_search(mqvs_comm_t c, mqvs_segment_t shard, const float *querie
         if (shard->device != c->device) fail(MQVS_ERR_BAD_ARGUMENTS, "shard and communicator on different devices");
         std::lock_guard<std::mutex> lock(c->mu);
         DeviceGuard guard(c->device);
+        WaitScope wsc{6, (uint64_t)(uintptr_t)c, (uint64_t)(uintptr_t)shard, (uint64_t)nq, (uint64_t)k,
+                      (uint64_t)metric, filter != nullptr, row_exists != nullptr, flags};
         CallArgs a{shard, queries, nq, k, metric, filter, row_exists, out_ids, out_dist,
                    flags & ~(MQVS_F_ASYNC | MQVS_F_DEVICE_PTRS), (flags & MQVS_F_DEVICE_PTRS) != 0,
                    stream ? (hipStream_t)stream : c->stream,

@@ -102,6 +102,10 @@ for step in "$@"; do
         || { echo "api nq1 failed"; tail -5 $O/api_nq1.log; exit 1; }
       python3 tools/timeline.py $O/api_nq1/run_kernel_trace.csv --api $O/api_nq1/run_hip_api_trace.csv --start k_query_prep --nth -1 > $O/api_nq1.txt
       head -30 $O/api_idx.txt ;;
+    wab)
+      timeout -k 10 400 python -u tools/wait_ab.py > $O/wait_ab.jsonl 2> $O/wait_ab.err \
+        || { echo "wait ab failed"; tail -20 $O/wait_ab.err; exit 1; }
+      cat $O/wait_ab.jsonl ;;
     lds)
       bash tools/gpu_lds_pmc.sh 0 8 4 6 || exit 1 ;;
     cpu)
