@@ -767,6 +767,8 @@ __global__ __launch_bounds__(kScanThreads) void k_exclusive_ord(int *flag_ord, i
 // counts have left it when its s_waitcnt vmcnt(0) (the 0x0F70 encoding: gfx9's
 // field layout) retires, before its ticket; other ISA families order stores
 // differently and would need release/acquire fences on the ticket.
+constexpr int kCountStage = 16384;  // chunks whose counts k_chunk_count's scan stages in LDS
+
 __global__ __launch_bounds__(kScanThreads) void k_chunk_count(const uint8_t *filter, const uint8_t *nonempty,
                                                                const uint8_t *exists, int64_t n, int64_t chunk_rows,
                                                                int64_t nchunks, int *count, int tile,
@@ -784,6 +786,9 @@ __global__ __launch_bounds__(kScanThreads) void k_chunk_count(const uint8_t *fil
         const int64_t r0 = c * chunk_rows;
         const int64_t r1 = r0 + chunk_rows < n ? r0 + chunk_rows : n;
         int cnt = 0;
+        // (unrolled: a chunk of 8192 rows is 4 words per lane, their loads in
+        // flight together)
+#pragma unroll 4
         for (int64_t w = (r0 >> 5) + lane; w < ((r1 + 31) >> 5); w += 64)
             cnt += __popc(sel_word(filter, nonempty, exists, n, w) & range_mask(w, r0, r1));
         for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o);
@@ -802,7 +807,30 @@ __global__ __launch_bounds__(kScanThreads) void k_chunk_count(const uint8_t *fil
     __syncthreads();
     if (!s_last) return;
     // (coherent loads of the other workgroups' counts, no acquire fence)
+    // Up to kCountStage chunks: staged in LDS first, 8 independent loads in
+    // flight per thread -- the two scans below read each count twice, and
+    // reading them from memory there serialised ~18 coherent loads per thread
+    // (k_chunk_count 21 us at 6104 chunks)
+    extern __shared__ int s_cnt[];
+    const bool staged = nchunks <= kCountStage;
+    if (staged) {
+        for (int64_t i0 = threadIdx.x; i0 < nchunks; i0 += 8 * kScanThreads) {
+            int v[8];
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t i = i0 + (int64_t)u * kScanThreads;
+                v[u] = i < nchunks ? __hip_atomic_load(count + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; ++u) {
+                const int64_t i = i0 + (int64_t)u * kScanThreads;
+                if (i < nchunks) s_cnt[i] = v[u];
+            }
+        }
+        __syncthreads();
+    }
     auto cnt_of = [&](int64_t i) -> int64_t {
+        if (staged) return (int64_t)s_cnt[i];
         return (int64_t)__hip_atomic_load(count + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     };
     int64_t padded_total = 0, selected = 0;
@@ -876,7 +904,8 @@ void launch_gather_count(const uint8_t *filter, const uint8_t *nonempty, const u
     const int64_t nchunks = (n + chunk_rows - 1) / chunk_rows;
     if (nchunks < 1) return;
     constexpr int wpb = kScanThreads / 64;  // chunks (waves) per workgroup
-    hipLaunchKernelGGL(k_chunk_count, dim3((unsigned)((nchunks + wpb - 1) / wpb)), dim3(kScanThreads), 0, s, filter,
+    const size_t lds = sizeof(int) * (size_t)(nchunks <= kCountStage ? nchunks : 0);
+    hipLaunchKernelGGL(k_chunk_count, dim3((unsigned)((nchunks + wpb - 1) / wpb)), dim3(kScanThreads), lds, s, filter,
                        nonempty, exists, n, chunk_rows, nchunks, count, tile, offsets, totals, host_totals, host_gen,
                        ticket);
 }

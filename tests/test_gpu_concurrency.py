@@ -243,3 +243,47 @@ def test_wait_modes_same_results(mq, mode, spin):
         for (gi, gd), (ei, ed) in zip(got, exp):
             assert np.array_equal(gi, ei), j
             assert np.array_equal(gd.view(np.uint32), ed.view(np.uint32)), j
+
+
+def test_hybrid_wait_alternating_shapes_latency(mq):
+    """The HYBRID wait's sleep estimate is kept per call shape: a thread that
+    alternates long (nq 1000) and short (nq 1) searches must not sleep the
+    long search's time on the short one (the round-6 bench's nq 1 end to end
+    read 6.0 ms for 2.4 ms of work while one history served every call).
+    Medians over interleaved repetitions; the bound is loose (timing on a
+    shared box): the short search under HYBRID within 1.5x + 0.3 ms of its
+    RUNTIME time."""
+    import time
+    import torch
+    from myscaledb_amd import _lib
+    from myscaledb_amd.vector_scan import generate_device
+    n, d = 2_000_000, 768
+    seg = mq.VectorScanSegment.generate(0x5EED0007, 1, n, d, metric="Cosine", granule=8192)
+    qs = {}
+    for nq in (1000, 1):
+        t = torch.empty((nq, d), dtype=torch.float32, device="cuda")
+        generate_device(0x5EED0008, 1, 0, nq, d, t)
+        qs[nq] = (t, torch.empty((nq, 10), dtype=torch.int64, device="cuda"),
+                  torch.empty((nq, 10), dtype=torch.float32, device="cuda"))
+    prev = _lib.set_wait_mode(_lib.WAIT_HYBRID, 50)
+    times = {_lib.WAIT_RUNTIME: [], _lib.WAIT_HYBRID: []}
+    try:
+        for q, ids, dst in qs.values():
+            seg.search(q, 10, out=(ids, dst))
+        for _ in range(6):
+            for mode in times:
+                _lib.set_wait_mode(mode, 50)
+                for nq in (1000, 1, 1000, 1):
+                    q, ids, dst = qs[nq]
+                    torch.cuda.synchronize()
+                    t0 = time.perf_counter()
+                    seg.search(q, 10, out=(ids, dst))
+                    torch.cuda.synchronize()
+                    if nq == 1:
+                        times[mode].append(time.perf_counter() - t0)
+    finally:
+        _lib.set_wait_mode(prev, 50)
+        seg.free()
+    rt = float(np.median(times[_lib.WAIT_RUNTIME]))
+    hy = float(np.median(times[_lib.WAIT_HYBRID]))
+    assert hy <= 1.5 * rt + 3e-4, (hy, rt)
