@@ -335,8 +335,11 @@ __device__ inline float wave_exact(const ScanParams &p, int q, int64_t row, floa
 // compiler counts each wait exactly: wave_exact waits a full random-row load
 // latency per tile (one tile ahead), ~24 latencies per wave at d = 768.
 constexpr int kRrPF = 3;
-
-template <int METRIC, bool DIRECT, int NT>
+// XPF: tiles of the query slice in flight.  1 (the index re-rank: registers
+// are its occupancy) waits an L2 round trip for the query slice every tile --
+// the whole chain at small nq, where one workgroup's 24 tiles are the exact
+// stage (k_exact_records at nq 1: ~23 us); 3 keeps it in a ring like the rows.
+template <int METRIC, bool DIRECT, int NT, int XPF = 1>
 __device__ inline float wave_exact_nt(const ScanParams &p, int q, int64_t row, float *tile) {
     constexpr int d = 32 * NT;
     const int lane = threadIdx.x & 63;
@@ -356,23 +359,25 @@ __device__ inline float wave_exact_nt(const ScanParams &p, int q, int64_t row, f
             const int64_t r = __shfl(row, j * 8 + (lane >> 3));
             base[j] = p.rows + (r >= 0 ? r : 0) * d + (lane & 7) * 4;
         }
-        float4 ry[kRrPF][8], rx[8];
+        float4 ry[kRrPF][8], rx[XPF][8];
         auto load_y = [&](int t, float4(&dst)[8]) __attribute__((always_inline)) {
             const int tt = t < NT ? t : NT - 1;
 #pragma unroll
             for (int j = 0; j < 8; ++j) dst[j] = *reinterpret_cast<const float4 *>(base[j] + tt * 32);
         };
-        auto load_x = [&](int t) __attribute__((always_inline)) {
+        auto load_x = [&](int t, float4(&dst)[8]) __attribute__((always_inline)) {
             const int tt = t < NT ? t : NT - 1;
 #pragma unroll
-            for (int j = 0; j < 8; ++j) rx[j] = *reinterpret_cast<const float4 *>(x + tt * 32 + 4 * j);
+            for (int j = 0; j < 8; ++j) dst[j] = *reinterpret_cast<const float4 *>(x + tt * 32 + 4 * j);
         };
 #pragma unroll
         for (int sl = 0; sl < kRrPF; ++sl) load_y(sl, ry[sl]);
-        load_x(0);
+#pragma unroll
+        for (int sl = 0; sl < XPF; ++sl) load_x(sl, rx[sl]);
 #pragma unroll
         for (int t = 0; t < NT; ++t) {
             float4(&cur)[8] = ry[t % kRrPF];
+            float4(&curx)[8] = rx[t % XPF];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
                 float *dst = tile + (j * 8 + (lane >> 3)) * kRrStride + (lane & 7) * 4;
@@ -384,13 +389,13 @@ __device__ inline float wave_exact_nt(const ScanParams &p, int q, int64_t row, f
             float xt[32];
 #pragma unroll
             for (int j = 0; j < 8; ++j) {
-                xt[4 * j] = rx[j].x;
-                xt[4 * j + 1] = rx[j].y;
-                xt[4 * j + 2] = rx[j].z;
-                xt[4 * j + 3] = rx[j].w;
+                xt[4 * j] = curx[j].x;
+                xt[4 * j + 1] = curx[j].y;
+                xt[4 * j + 2] = curx[j].z;
+                xt[4 * j + 3] = curx[j].w;
             }
             load_y(t + kRrPF, cur);
-            load_x(t + 1);
+            load_x(t + XPF, curx);
             __builtin_amdgcn_wave_barrier();
             const float *mine = tile + lane * kRrStride;
 #pragma unroll
@@ -419,13 +424,13 @@ __device__ inline float wave_exact_nt(const ScanParams &p, int q, int64_t row, f
 }
 
 // wave_exact_nt for d = 768, wave_exact otherwise
-template <int METRIC, bool DIRECT>
+template <int METRIC, bool DIRECT, int XPF = 1>
 __device__ inline float wave_exact_any(const ScanParams &p, int q, int64_t row, float *tile) {
-    if (p.d == 768) return wave_exact_nt<METRIC, DIRECT, 24>(p, q, row, tile);
+    if (p.d == 768) return wave_exact_nt<METRIC, DIRECT, 24, XPF>(p, q, row, tile);
     return wave_exact<METRIC, DIRECT>(p, q, row, tile);
 }
 
-template <int METRIC, bool DIRECT>
+template <int METRIC, bool DIRECT, int XPF = 1>
 __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids_tiled(ScanParams p, const int64_t *cand, int ncand,
                                                                  int k, int64_t id_offset, int64_t *out_ids,
                                                                  float *out_dist, int nrec, uint4 *scratch,
@@ -448,7 +453,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids_tiled(ScanParams p, 
             row = c[i];
             if (!(row >= 0 && row < p.n && row_valid(p, row))) row = -1;
         }
-        const float raw = wave_exact_any<METRIC, DIRECT>(p, q, row, tile);
+        const float raw = wave_exact_any<METRIC, DIRECT, XPF>(p, q, row, tile);
         if (i < ncand) dst[i] = rerank_rec<METRIC>(p, row, raw);
     }
     rerank_emit<METRIC>(recs, g, ncand, k, q, id_offset, out_ids, out_dist);
@@ -559,7 +564,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_rerank_ids_pair(ScanParams p, c
 // (mqvs_search path 2): query q's cnt[q] survivor rows are surv[q * rs + i];
 // their records go to recs[q * rs + i].  Work items (chunk of 256
 // survivors, query), chunk-major, walked grid-stride.
-template <int METRIC, bool DIRECT>
+template <int METRIC, bool DIRECT, bool XPF3 = true>
 __global__ __launch_bounds__(SEL_THREADS) void k_exact_records(ScanParams p, const uint32_t *surv, const int *cnt,
                                                               int64_t rs, int chunks, uint4 *recs) {
     __shared__ float tiles[(SEL_THREADS / 64) * 64 * kRrStride];
@@ -573,9 +578,31 @@ __global__ __launch_bounds__(SEL_THREADS) void k_exact_records(ScanParams p, con
         const int64_t row = i < m ? (int64_t)surv[(int64_t)q * rs + i] : -1;
         float raw;
         if ((p.d & 3) == 0)
-            raw = wave_exact_any<METRIC, DIRECT>(p, q, row, tile);
+            raw = XPF3 ? wave_exact_any<METRIC, DIRECT, 3>(p, q, row, tile) : wave_exact_any<METRIC, DIRECT>(p, q, row, tile);
         else
             raw = row >= 0 ? cand_value<METRIC, DIRECT>(p, q, row) : 0.f;
+        if (i < m) recs[(int64_t)q * rs + i] = rerank_rec<METRIC>(p, row, raw);
+    }
+}
+
+// Small batches: one wave per workgroup, work items of (64 survivors, query).
+// At nq 1 the ~240 survivors of k_exact_records's one 256-thread workgroup
+// were 24 tiles of random rows pulled through ONE CU (~780 KB at the per-CU
+// read rate: ~23 us; a deeper query-slice prefetch did not help); here their
+// 4 waves run on 4 CUs.  Same chain, same records.
+template <int METRIC, bool DIRECT>
+__global__ __launch_bounds__(64) void k_exact_records_1w(ScanParams p, const uint32_t *surv, const int *cnt,
+                                                         int64_t rs, int chunks, uint4 *recs) {
+    __shared__ float tile[64 * kRrStride];
+    const int lane = threadIdx.x;
+    const int64_t items = (int64_t)p.nq * chunks;
+    for (int64_t it = blockIdx.x; it < items; it += gridDim.x) {
+        const int c = (int)(it / p.nq), q = (int)(it - (int64_t)c * p.nq);
+        const int m = cnt[q];
+        if (c * 64 >= m) continue;  // (uniform over the wave)
+        const int i = c * 64 + lane;
+        const int64_t row = i < m ? (int64_t)surv[(int64_t)q * rs + i] : -1;
+        const float raw = wave_exact_any<METRIC, DIRECT>(p, q, row, tile);
         if (i < m) recs[(int64_t)q * rs + i] = rerank_rec<METRIC>(p, row, raw);
     }
 }
@@ -656,9 +683,29 @@ void launch_exact_rerank(const ScanParams &p, int metric, const uint32_t *surv, 
     const int items = p.nq * chunks;
     const int grid = std::max(1, std::min(items, 4096));
     const bool direct = !blas_formula(p);
+    // small batches (d % 4 == 0): one wave per workgroup over 64-survivor items
+    const bool one_wave = (p.d & 3) == 0 && p.nq <= tune_int("MQVS_RR_1W_NQ", 16);
+    const int chunks64 = (cap + 63) / 64;
+    const int grid64 = std::max(1, std::min(p.nq * chunks64, 16384));
+    // (measurement build A/B: MQVS_RR_XPF=1, the query slice one tile ahead)
+    // (query slice three tiles ahead measured slower: nq 1 23.2 -> 25.2 us,
+    // the index re-rank 124 -> 167 us)
+    const bool xpf1 = tune_int("MQVS_RR_XPF", 1) == 1;
 #define MQVS_ER(M)                                                                                                \
     do {                                                                                                          \
-        if (direct)                                                                                               \
+        if (one_wave && direct)                                                                                   \
+            hipLaunchKernelGGL((k_exact_records_1w<M, true>), dim3(grid64), dim3(64), 0, s, p, surv, cnt, rs,      \
+                               chunks64, recs);                                                                   \
+        else if (one_wave)                                                                                        \
+            hipLaunchKernelGGL((k_exact_records_1w<M, false>), dim3(grid64), dim3(64), 0, s, p, surv, cnt, rs,     \
+                               chunks64, recs);                                                                   \
+        else if (xpf1 && direct)                                                                                  \
+            hipLaunchKernelGGL((k_exact_records<M, true, false>), dim3(grid), dim3(SEL_THREADS), 0, s, p, surv, cnt, \
+                               rs, chunks, recs);                                                                 \
+        else if (xpf1)                                                                                            \
+            hipLaunchKernelGGL((k_exact_records<M, false, false>), dim3(grid), dim3(SEL_THREADS), 0, s, p, surv,  \
+                               cnt, rs, chunks, recs);                                                            \
+        else if (direct)                                                                                          \
             hipLaunchKernelGGL((k_exact_records<M, true>), dim3(grid), dim3(SEL_THREADS), 0, s, p, surv, cnt, rs, \
                                chunks, recs);                                                                     \
         else                                                                                                      \
@@ -790,8 +837,13 @@ static void rerank_ids_t(const ScanParams &p, const int64_t *cand, int ncand, in
                            ncand, k, id_offset, ids, dist, pr);
     } else if ((p.d & 3) == 0) {
         const size_t lds = N * sizeof(uint4) + (SEL_THREADS / 64) * 64 * kRrStride * sizeof(float);
-        hipLaunchKernelGGL((k_rerank_ids_tiled<M, DIRECT>), dim3(p.nq), dim3(SEL_THREADS), lds, s, p, cand, ncand, k,
-                           id_offset, ids, dist, N, scratch, pr);
+        // (measurement build A/B: MQVS_IDX_XPF=3, the query slice three tiles ahead)
+        if (tune_int("MQVS_IDX_XPF", 1) == 3)
+            hipLaunchKernelGGL((k_rerank_ids_tiled<M, DIRECT, 3>), dim3(p.nq), dim3(SEL_THREADS), lds, s, p, cand,
+                               ncand, k, id_offset, ids, dist, N, scratch, pr);
+        else
+            hipLaunchKernelGGL((k_rerank_ids_tiled<M, DIRECT>), dim3(p.nq), dim3(SEL_THREADS), lds, s, p, cand,
+                               ncand, k, id_offset, ids, dist, N, scratch, pr);
     } else {
         hipLaunchKernelGGL((k_rerank_ids<M, DIRECT>), dim3(p.nq), dim3(SEL_THREADS), N * sizeof(uint4), s, p, cand,
                            ncand, k, id_offset, ids, dist, scratch, pr);
