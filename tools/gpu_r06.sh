@@ -106,6 +106,12 @@ for step in "$@"; do
       timeout -k 10 400 python -u tools/wait_ab.py > $O/wait_ab.jsonl 2> $O/wait_ab.err \
         || { echo "wait ab failed"; tail -20 $O/wait_ab.err; exit 1; }
       cat $O/wait_ab.jsonl ;;
+    seg)
+      # nq 1 segmentation A/B (measurement build): SEG_TUNES="MQVS_SEG=a,b,c;..."
+      timeout -k 10 600 python -u tools/ab_split.py --dbg --nqs 1 --splits 2 --modes 1 --metrics Cosine \
+        --tunes "${SEG_TUNES:-MQVS_SEG=8,4,65536;MQVS_SEG=32,4,65536}" --reps 15 \
+        > $O/seg_ab.jsonl 2> $O/seg_ab.err || { echo "seg ab failed"; tail -20 $O/seg_ab.err; exit 1; }
+      cut -c1-400 $O/seg_ab.jsonl ;;
     lds)
       bash tools/gpu_lds_pmc.sh 0 8 4 6 || exit 1 ;;
     cpu)
