@@ -876,8 +876,14 @@ static SegTune seg_tune(int nq) {
         v.growth = 4;
         // one or two queries: a 4x shorter probe (its single-workgroup select
         // 53 -> 21 us at 10M x 768; one more segment; wall median 2.80 ->
-        // 2.75 ms at nq 1, no gain at nq 4, profiles/r02/smallnq/seg_ab.jsonl)
-        if (nq <= 2) v.target = 65536;
+        // 2.75 ms at nq 1, no gain at nq 4, profiles/r02/smallnq/seg_ab.jsonl);
+        // round 6: half that probe and a first segment of 16 probe lengths
+        // (3 segments, 2 refinements): kernels 2.386 -> 2.365 ms, wall median
+        // 2.418-2.439 -> 2.394-2.404 ms (profiles/r06/seg_ab_nq1.jsonl)
+        if (nq <= 2) {
+            v.first = 16;
+            v.target = 32768;
+        }
     } else if (nq < 256) {
         v.first = 4;
         v.growth = 4;
