@@ -146,6 +146,8 @@ void launch_query_bound(const ScanParams &p, int metric, const float *ynorm_max,
 // in the append: the probe row (L2-resident) is read five times, never with
 // one dependent load in flight per thread.
 constexpr int kPsThreads = 1024;
+constexpr int kPsKeep = 4;        // keys kept per thread for the threshold select
+constexpr int kPsKeepMaxK = 256;  // k up to which the kept keys are selected (else full passes)
 
 template <int METRIC>
 __global__ __launch_bounds__(kPsThreads) void k_probe_select_wide(const float *probe, int64_t P, int64_t ld, int k,
@@ -153,33 +155,67 @@ __global__ __launch_bounds__(kPsThreads) void k_probe_select_wide(const float *p
                                                                   Cand *cand, int cap, const int32_t *row_list) {
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh[4];
+    __shared__ uint32_t skeys[kPsKeep * kPsThreads];
     const int q = blockIdx.x, t = threadIdx.x;
     const float *row = probe + (int64_t)q * ld;
-    uint32_t prefix = 0, mask = 0, kk = (uint32_t)k;
+    // Each thread keeps its kPsKeep smallest keys in registers (one read of
+    // the row), and the radix passes run over those 4096 keys in LDS: the
+    // k-th smallest of a subset of the keys is an upper bound on the k-th of
+    // all of them -- all a threshold needs -- and equal to it unless one
+    // thread held more than kPsKeep of the k best (k 100 of 32768 values:
+    // ~0.1 per thread).  Three passes over the row with an LDS atomic per
+    // value took 17-27 us at nq 1.
     bool none = false;
-    // three passes: the top 24 bits of the k-th key; the bound below takes the
-    // low byte set (an upper bound on the k-th key, as block_radix_select<3>)
-    for (int pass = 0; pass < 3; ++pass) {
-        const int shift = 24 - 8 * pass;
-        if (t < 256) hist[t] = 0;
-        __syncthreads();
-        RunHist rh;
+    uint32_t prefix = 0;
+    if (k <= kPsKeepMaxK) {
+        uint32_t best[kPsKeep];
+#pragma unroll
+        for (int j = 0; j < kPsKeep; ++j) best[j] = 0xFFFFFFFFu;
         for_each_f4<kPsThreads>(row, P, [&](int64_t, float raw) {
-            const uint32_t key = okey<METRIC>(raw);
-            if (key != 0xFFFFFFFFu && (key & mask) == prefix) rh.add(hist, (key >> shift) & 255u);
+            uint32_t key = okey<METRIC>(raw);
+            if (key >= best[kPsKeep - 1]) return;
+#pragma unroll
+            for (int j = 0; j < kPsKeep; ++j) {  // sorted insertion; the largest falls off
+                if (key < best[j]) {
+                    const uint32_t o = best[j];
+                    best[j] = key;
+                    key = o;
+                }
+            }
         });
-        rh.flush(hist);
+#pragma unroll
+        for (int j = 0; j < kPsKeep; ++j) skeys[j * kPsThreads + t] = best[j];
         __syncthreads();
-        hist_pick(hist, kk, pass == 0, sh);
-        __syncthreads();
-        if (sh[0]) {
-            none = true;
-            break;
+        const uint32_t sel = block_radix_select_mlp<kPsThreads, 3>([&](int64_t i) { return skeys[i]; },
+                                                                  (int64_t)kPsKeep * kPsThreads, k, hist, sh);
+        none = sel == 0xFFFFFFFEu;
+        prefix = sel & ~0xFFu;
+    } else {
+        // large k: three passes over the row; the bound takes the low byte set
+        // (an upper bound on the k-th key, as block_radix_select<3>)
+        uint32_t mask = 0, kk = (uint32_t)k;
+        for (int pass = 0; pass < 3; ++pass) {
+            const int shift = 24 - 8 * pass;
+            if (t < 256) hist[t] = 0;
+            __syncthreads();
+            RunHist rh;
+            for_each_f4<kPsThreads>(row, P, [&](int64_t, float raw) {
+                const uint32_t key = okey<METRIC>(raw);
+                if (key != 0xFFFFFFFFu && (key & mask) == prefix) rh.add(hist, (key >> shift) & 255u);
+            });
+            rh.flush(hist);
+            __syncthreads();
+            hist_pick(hist, kk, pass == 0, sh);
+            __syncthreads();
+            if (sh[0]) {
+                none = true;
+                break;
+            }
+            prefix |= sh[1] << shift;
+            mask |= 255u << shift;
+            kk -= sh[2];
+            __syncthreads();
         }
-        prefix |= sh[1] << shift;
-        mask |= 255u << shift;
-        kk -= sh[2];
-        __syncthreads();
     }
     float tt;
     if (none)
