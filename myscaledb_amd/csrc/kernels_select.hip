@@ -340,22 +340,46 @@ void launch_merge_shards(int nshards, int nq, int k, int metric, const int64_t *
 //   approx (bf16):          thr = tighter(thr, widen(k-th approximate value))
 // Every row of the exact top-k seen so far passes the new threshold (same
 // argument as the probe threshold), so nothing the final select needs is lost.
+// Up to `stage` candidates (the launch's LDS) are first copied into LDS with
+// four loads in flight per thread, and the three radix passes and the
+// compaction read them there: from global memory each pass waited one load
+// per 256 candidates in turn (nq 1: ~3000 candidates, 9-16 us per refine).
+constexpr int kRefineStage = 8192;
+
 template <int METRIC, bool APPROX>
 __global__ __launch_bounds__(SEL_THREADS) void k_refine(const Cand *cin, const int *cnt_in, int cap,
                                                        int k, const float *bq, uint32_t *tau,
-                                                       float *thr, Cand *cout, int *cnt_out) {
+                                                       float *thr, Cand *cout, int *cnt_out, int stage) {
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh[4];
     __shared__ int s_cnt;
+    extern __shared__ Cand s_cand[];
     const int q = blockIdx.x;
     int n = cnt_in[q];
     if (n > cap) n = cap;  // overflowed lists keep their overflow: count stays > cap
     const Cand *c = cin + (int64_t)q * cap;
+    if (n <= stage) {
+        int i = threadIdx.x;
+        for (; i + 3 * SEL_THREADS < n; i += 4 * SEL_THREADS) {
+            const Cand a = c[i], b = c[i + SEL_THREADS], d = c[i + 2 * SEL_THREADS], e = c[i + 3 * SEL_THREADS];
+            s_cand[i] = a;
+            s_cand[i + SEL_THREADS] = b;
+            s_cand[i + 2 * SEL_THREADS] = d;
+            s_cand[i + 3 * SEL_THREADS] = e;
+        }
+        for (; i < n; i += SEL_THREADS) s_cand[i] = c[i];
+        __syncthreads();
+        c = s_cand;
+    }
     uint32_t tk = 0;
     float tf = 0.f;
+    // (k <= 256: the bound from the threads' 4 smallest keys, kept_kth_bound)
+    __shared__ uint32_t skeys[4 * SEL_THREADS];
+    const bool kept = k <= SEL_THREADS;
     if (APPROX) {
         auto keyof = [&](int64_t i) { return okey<METRIC>(c[i].raw); };
-        const uint32_t th = block_radix_select<3>(keyof, n, k, hist, sh);  // (a bound: 3 passes)
+        const uint32_t th = kept ? kept_kth_bound<SEL_THREADS, 4>(keyof, n, k, skeys, hist, sh)
+                                 : block_radix_select<3>(keyof, n, k, hist, sh);  // (a bound: 3 passes)
         tf = thr[q];
         if (th != 0xFFFFFFFEu) {
             const float w = widen<METRIC>(okey_bound_value<METRIC>(th), bq[q]);
@@ -363,7 +387,8 @@ __global__ __launch_bounds__(SEL_THREADS) void k_refine(const Cand *cin, const i
         }
     } else {
         auto keyof = [&](int64_t i) { return key32<METRIC>(c[i].raw); };
-        const uint32_t th = block_radix_select<3>(keyof, n, k, hist, sh);
+        const uint32_t th = kept ? kept_kth_bound<SEL_THREADS, 4>(keyof, n, k, skeys, hist, sh)
+                                 : block_radix_select<3>(keyof, n, k, hist, sh);
         tk = tau[q];
         if (th < tk) tk = th;
     }
@@ -393,8 +418,11 @@ __global__ __launch_bounds__(SEL_THREADS) void k_refine(const Cand *cin, const i
 template <int M, bool A>
 static void refine_t(const Cand *cin, const int *cnt_in, int cap, int nq, int k, const float *bq,
                      uint32_t *tau, float *thr, Cand *cout, int *cnt_out, hipStream_t s) {
-    hipLaunchKernelGGL((k_refine<M, A>), dim3(nq), dim3(SEL_THREADS), 0, s, cin, cnt_in, cap, k, bq, tau,
-                       thr, cout, cnt_out);
+    // (small batches stage up to 8192 candidates; a batch, whose thousand
+    // workgroups need occupancy more, 2048: ~2k appends per segment)
+    const int stage = std::min(cap, nq <= 16 ? kRefineStage : kRefineStage / 4);
+    hipLaunchKernelGGL((k_refine<M, A>), dim3(nq), dim3(SEL_THREADS), sizeof(Cand) * (size_t)stage, s, cin, cnt_in,
+                       cap, k, bq, tau, thr, cout, cnt_out, stage);
 }
 
 void launch_refine(const Cand *cin, const int *cnt_in, int cap, int nq, int k, int metric,

@@ -151,6 +151,48 @@ __device__ inline uint32_t block_radix_select_mlp(KeyFn keyof, int64_t count, in
     return PASSES == 4 ? prefix : prefix | (0xFFFFFFFFu >> (8 * PASSES));
 }
 
+// An upper bound on the k-th smallest valid key of count keys: each thread
+// keeps its KEEP smallest in registers, and block_radix_select_mlp's three
+// passes (the low byte set) run over those NT * KEEP keys in LDS (skeys).
+// The k-th smallest of a subset is >= the k-th of all, and equal unless a
+// thread held more than KEEP of the k best -- a threshold needs no more.
+// 0xFFFFFFFE when the subset holds fewer than k valid keys (then the caller
+// keeps its threshold: every row passes it).  One pass over the keys with no
+// LDS atomics per key (the full radix passes serialised on the few buckets
+// clustered keys share).
+template <int NT, int KEEP, typename KeyFn>
+__device__ inline uint32_t kept_kth_bound(KeyFn keyof, int64_t count, int k, uint32_t *skeys, uint32_t *hist,
+                                          uint32_t *sh) {
+    const int t = threadIdx.x;
+    uint32_t best[KEEP];
+#pragma unroll
+    for (int j = 0; j < KEEP; ++j) best[j] = 0xFFFFFFFFu;
+    auto insert = [&](uint32_t key) {
+        if (key >= best[KEEP - 1]) return;
+#pragma unroll
+        for (int j = 0; j < KEEP; ++j) {
+            if (key < best[j]) {
+                const uint32_t o = best[j];
+                best[j] = key;
+                key = o;
+            }
+        }
+    };
+    int64_t i = t;
+    for (; i + 3 * NT < count; i += 4 * NT) {
+        const uint32_t k0 = keyof(i), k1 = keyof(i + NT), k2 = keyof(i + 2 * NT), k3 = keyof(i + 3 * NT);
+        insert(k0);
+        insert(k1);
+        insert(k2);
+        insert(k3);
+    }
+    for (; i < count; i += NT) insert(keyof(i));
+#pragma unroll
+    for (int j = 0; j < KEEP; ++j) skeys[j * NT + t] = best[j];
+    __syncthreads();
+    return block_radix_select_mlp<NT, 3>([&](int64_t x) { return skeys[x]; }, (int64_t)KEEP * NT, k, hist, sh);
+}
+
 // The k smallest valid keys for small k (k <= kSelSmallK): each thread keeps
 // its k smallest (key, index) pairs (insertion into registers), then k rounds
 // of a block minimum over the threads' heads (wave shuffles + one LDS
