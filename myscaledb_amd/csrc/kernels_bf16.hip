@@ -286,9 +286,12 @@ __global__ __launch_bounds__(SEL_THREADS) void k_survivors(ScanParams p, const f
         n = p.cand_cap;
     }
     const Cand *c = p.cand + (int64_t)q * p.cand_cap;
-    // (a bound on the k-th key is enough: 3 radix passes, block_radix_select)
-    const uint32_t th =
-        block_radix_select_mlp<SEL_THREADS, 3>([&](int64_t i) { return okey<METRIC>(c[i].raw); }, n, k, hist, sh);
+    // (a bound on the k-th key is enough: 3 radix passes, block_radix_select;
+    // k <= 256: over the threads' 4 smallest keys, kept_kth_bound)
+    __shared__ uint32_t skeys[4 * SEL_THREADS];
+    auto keyof = [&](int64_t i) { return okey<METRIC>(c[i].raw); };
+    const uint32_t th = k <= SEL_THREADS ? kept_kth_bound<SEL_THREADS, 4>(keyof, n, k, skeys, hist, sh)
+                                         : block_radix_select_mlp<SEL_THREADS, 3>(keyof, n, k, hist, sh);
     float t;
     if (th == 0xFFFFFFFEu)
         t = (METRIC == MQVS_METRIC_L2) ? __builtin_inff() : -__builtin_inff();

@@ -638,7 +638,13 @@ __global__ __launch_bounds__(SEL_THREADS) void k_sort_emit(uint4 *recs, const in
     if (threadIdx.x == 0) s_c = 0;
     for (int i = threadIdx.x; i < m; i += SEL_THREADS) lrec[i] = g[i];
     __syncthreads();
-    const uint32_t X = block_radix_select([&](int64_t i) { return lrec[i].x; }, m, k, hist, sh);
+    // X: the k-th key, or (k <= 256) an upper bound on it from the threads'
+    // 4 smallest keys (kept_kth_bound: one pass, no per-key LDS atomics) --
+    // the records <= X still hold the top k, and are placed by rank below
+    __shared__ uint32_t skeys[4 * SEL_THREADS];
+    const uint32_t X = k <= SEL_THREADS
+                           ? kept_kth_bound<SEL_THREADS, 4>([&](int64_t i) { return lrec[i].x; }, m, k, skeys, hist, sh)
+                           : block_radix_select([&](int64_t i) { return lrec[i].x; }, m, k, hist, sh);
     // (0xFFFFFFFE: fewer than k valid records -- all valid ones qualify)
     for (int i = threadIdx.x; i < m; i += SEL_THREADS) {
         const uint4 r = lrec[i];
