@@ -324,7 +324,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_survivors(ScanParams p, const f
 // slots per query (2 lcap when lcap > kSortCap: global_sort's second buffer).
 void launch_rerank_select(const ScanParams &p, int metric, const float *bq, int k, int64_t id_offset,
                           int64_t *out_ids, float *out_dist, int *overflow, uint32_t *surv, int *scnt,
-                          uint4 *recs, int lcap, int64_t rs, hipStream_t s) {
+                          uint4 *recs, int lcap, int64_t rs, hipStream_t s, const int *fl, int *host_fl) {
     switch (metric) {
         case MQVS_METRIC_L2:
             hipLaunchKernelGGL(k_survivors<MQVS_METRIC_L2>, dim3(p.nq), dim3(SEL_THREADS), 0, s, p, bq, k, overflow,
@@ -343,7 +343,7 @@ void launch_rerank_select(const ScanParams &p, int metric, const float *bq, int 
                                surv, scnt, lcap, rs);
             break;
     }
-    launch_exact_rerank(p, metric, surv, scnt, rs, lcap, recs, k, id_offset, out_ids, out_dist, s);
+    launch_exact_rerank(p, metric, surv, scnt, rs, lcap, recs, k, id_offset, out_ids, out_dist, s, fl, host_fl);
 }
 
 }  // namespace mqvs

@@ -622,12 +622,17 @@ constexpr int kSelCap = SEL_THREADS;
 template <int METRIC>
 __global__ __launch_bounds__(SEL_THREADS) void k_sort_emit(uint4 *recs, const int *cnt, int64_t rs, int k,
                                                           int64_t id_offset, int64_t *out_ids, float *out_dist,
-                                                          int rcap) {
+                                                          int rcap, const int *fl, int *host_fl) {
     extern __shared__ __attribute__((aligned(16))) uint4 lrec[];  // rcap + kSelCap records
     __shared__ uint32_t hist[256];
     __shared__ uint32_t sh[4];
     __shared__ int s_c;
     const int q = blockIdx.x;
+    if (host_fl && q == 0 && threadIdx.x < 8) {
+        // the search's status words (final: written by earlier kernels)
+        *reinterpret_cast<volatile int *>(host_fl + threadIdx.x) = fl[threadIdx.x];
+        __threadfence_system();
+    }
     const int m = cnt[q];
     uint4 *g = recs + (int64_t)q * rs;
     if (m > rcap) {
@@ -684,7 +689,7 @@ __global__ __launch_bounds__(SEL_THREADS) void k_sort_emit(uint4 *recs, const in
 
 void launch_exact_rerank(const ScanParams &p, int metric, const uint32_t *surv, const int *cnt, int64_t rs,
                          int cap, uint4 *recs, int k, int64_t id_offset, int64_t *out_ids, float *out_dist,
-                         hipStream_t s) {
+                         hipStream_t s, const int *fl, int *host_fl) {
     const int chunks = (cap + SEL_THREADS - 1) / SEL_THREADS;
     const int items = p.nq * chunks;
     const int grid = std::max(1, std::min(items, 4096));
@@ -718,7 +723,7 @@ void launch_exact_rerank(const ScanParams &p, int metric, const uint32_t *surv, 
             hipLaunchKernelGGL((k_exact_records<M, false>), dim3(grid), dim3(SEL_THREADS), 0, s, p, surv, cnt,    \
                                rs, chunks, recs);                                                                 \
         hipLaunchKernelGGL((k_sort_emit<M>), dim3(p.nq), dim3(SEL_THREADS), (kSortCap + kSelCap) * sizeof(uint4), s, \
-                           recs, cnt, rs, k, id_offset, out_ids, out_dist, kSortCap);                              \
+                           recs, cnt, rs, k, id_offset, out_ids, out_dist, kSortCap, fl, host_fl);                 \
     } while (0)
     switch (metric) {
         case MQVS_METRIC_L2: MQVS_ER(MQVS_METRIC_L2); break;
@@ -820,7 +825,7 @@ bool launch_rerank_ids_wide(const ScanParams &p, int metric, const int64_t *cand
             hipLaunchKernelGGL((k_exact_records_w<M, false>), dim3(grid), dim3(SEL_THREADS), 0, s, p, surv, cnt,     \
                                (int64_t)ncand, chunks, recs);                                                       \
         hipLaunchKernelGGL((k_sort_emit<M>), dim3(p.nq), dim3(SEL_THREADS), (rcap + kSelCap) * sizeof(uint4), s,     \
-                           recs, cnt, (int64_t)ncand, k, id_offset, out_ids, out_dist, rcap);                       \
+                           recs, cnt, (int64_t)ncand, k, id_offset, out_ids, out_dist, rcap, nullptr, nullptr);     \
     } while (0)
     switch (metric) {
         case MQVS_METRIC_L2: MQVS_RW(MQVS_METRIC_L2); break;

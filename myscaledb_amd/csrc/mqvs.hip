@@ -1350,6 +1350,7 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         st.segments = segs;
     }
     if (timing) MQVS_HIP(hipEventRecord(ws.ev[3], s));
+    bool flags_folded = false;  // the status words stored by the final select (k_sort_emit)
     if (kind == kScanBf16) {
         // survivors of the bound: up to kSortCap per query (kLargeCap with
         // the global-scratch sort for k > kSortCap)
@@ -1358,8 +1359,12 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         auto *surv = (uint32_t *)ws.get(ws.surv, sizeof(uint32_t) * (size_t)nq * rs + sizeof(int) * nq);
         int *scnt = (int *)(surv + (size_t)nq * rs);
         uint4 *recs = large ? large : (uint4 *)ws.get(ws.recs, sizeof(uint4) * (size_t)nq * rs);
+        // (a synchronous call: the final select also stores the status words
+        // into the pinned record the host reads after its wait)
+        const bool fold = !(dev && (flags & MQVS_F_ASYNC));
         launch_rerank_select(p, metric, bq, k, seg->row_offset, dids, ddist, overflow, surv, scnt, recs, lcap, rs,
-                             s);
+                             s, fold ? fl : nullptr, fold ? ws.host_flags + 16 : nullptr);
+        flags_folded = fold;
     } else
         launch_final_select(cand, count, cap, nq, k, metric, seg->granule, seg->row_offset, dids, ddist,
                             overflow, large, s);
@@ -1396,7 +1401,13 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         // [1] status, [4..6] survivor / candidate stats
         // (host outputs: copied with the status words, one wait)
         if (!dev) stage_out_begin(ws.pin_o, dids, ddist, (size_t)nq * k, s);
-        MQVS_HIP(hipMemcpyAsync(ws.host_flags + 16, fl, 8 * sizeof(int), hipMemcpyDeviceToHost, s));
+        // (stored by the final select when it could; else a one-wave kernel
+        // storing into the pinned words -- the runtime's device-to-host copy
+        // is a 4.4 us blit kernel at the end of every search)
+        if (!flags_folded) {
+            launch_words_to_host(nullptr, 0, fl, 8, nullptr, ws.host_flags + 16, s);
+            MQVS_HIP(hipGetLastError());
+        }
         host_wait(s);
         ws.host_flags[0] = ws.host_flags[16];
         ws.host_flags[1] = ws.host_flags[20];

@@ -424,12 +424,16 @@ void launch_refine(const Cand *cin, const int *cnt_in, int cap, int nq, int k, i
                    hipStream_t s);
 // the segment an index was built over (cache.hip validates put pairs)
 mqvs_segment *index_segment(mqvs_index *idx);
+// fl / host_fl (optional): the final select's first workgroup also stores the
+// 8 words fl (written by earlier kernels of the stream) into pinned host_fl --
+// the search's status copy without a kernel of its own
 void launch_rerank_select(const ScanParams &p, int metric, const float *bq, int k, int64_t id_offset,
                           int64_t *out_ids, float *out_dist, int *overflow, uint32_t *surv, int *scnt,
-                          uint4 *recs, int lcap, int64_t rs, hipStream_t s);
+                          uint4 *recs, int lcap, int64_t rs, hipStream_t s, const int *fl = nullptr,
+                          int *host_fl = nullptr);
 void launch_exact_rerank(const ScanParams &p, int metric, const uint32_t *surv, const int *cnt, int64_t rs,
                          int cap, uint4 *recs, int k, int64_t id_offset, int64_t *out_ids, float *out_dist,
-                         hipStream_t s);
+                         hipStream_t s, const int *fl = nullptr, int *host_fl = nullptr);
 
 // ---------------------------------------------------------------------------
 // Index path (kernels_ivf.hip, index.hip)
