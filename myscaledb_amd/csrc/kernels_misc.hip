@@ -857,7 +857,8 @@ __global__ __launch_bounds__(kScanThreads) void k_chunk_count(const uint8_t *fil
 __global__ __launch_bounds__(256) void k_compact_rows(const uint8_t *filter, const uint8_t *nonempty,
                                                        const uint8_t *exists, int64_t n, int64_t chunk_rows,
                                                        int64_t nchunks, const int *count, const int64_t *offsets,
-                                                       int tile, int32_t *list, int64_t list_end) {
+                                                       int tile, int32_t *list, int64_t list_end,
+                                                       const int64_t *dev_total, int64_t round) {
     const int64_t c = (int64_t)blockIdx.x * 4 + (threadIdx.x >> 6);
     const int lane = threadIdx.x & 63;
     if (c >= nchunks) return;
@@ -893,7 +894,10 @@ __global__ __launch_bounds__(256) void k_compact_rows(const uint8_t *filter, con
     const int padded = (cnt + tile - 1) / tile * tile;
     for (int i = cnt + lane; i < padded; i += 64) out[i] = -1;
     // the last chunk also pads the list's end up to list_end (whole tiles of
-    // the scan; -1 entries)
+    // the scan; -1 entries); list_end < 0: the padded total k_chunk_count
+    // left in device memory, rounded up to `round` (a list launched before
+    // the host read the count)
+    if (list_end < 0) list_end = (*dev_total + round - 1) / round * round;
     if (c == nchunks - 1)
         for (int64_t i = offsets[c] + padded + lane; i < list_end; i += 64) list[i] = -1;
 }
@@ -912,11 +916,11 @@ void launch_gather_count(const uint8_t *filter, const uint8_t *nonempty, const u
 
 void launch_gather_list(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists, int64_t n,
                         int64_t chunk_rows, int tile, const int *count, const int64_t *offsets, int32_t *list,
-                        int64_t list_end, hipStream_t s) {
+                        int64_t list_end, hipStream_t s, const int64_t *dev_total, int64_t round) {
     const int64_t nchunks = (n + chunk_rows - 1) / chunk_rows;
     if (nchunks < 1) return;
     hipLaunchKernelGGL(k_compact_rows, dim3((unsigned)((nchunks + 3) / 4)), dim3(256), 0, s, filter, nonempty, exists,
-                       n, chunk_rows, nchunks, count, offsets, tile, list, list_end);
+                       n, chunk_rows, nchunks, count, offsets, tile, list, list_end, dev_total, round);
 }
 
 void launch_chunk_ordinals(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists,

@@ -1169,6 +1169,22 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
         MQVS_HIP(hipGetLastError());
     }
 
+    // ---- the gather list, launched before the host reads the count (when
+    // the call may gather): k_compact_rows needs only the device offsets, and
+    // pads the list's end from the device totals, so the host's round trip
+    // for the count overlaps it.  Sized for every row (n entries plus the
+    // chunks' tile padding); a search the count then sends to the mask scan
+    // wasted one compaction beside a scan of >= 60 % of the part.
+    int32_t *spec_list = nullptr;
+    if (selected >= 0 && (gather_mode == 2 || bf16_ok || (!bf16 && !mfma))) {
+        const int64_t nch = (n + seg->granule - 1) / seg->granule;
+        const int64_t worst = round_up(n + nch * (int64_t)(gtile - 1), kSmallRows);
+        spec_list = (int32_t *)ws.get(ws.glist, sizeof(int32_t) * (size_t)std::max<int64_t>(worst, 1));
+        launch_gather_list(dfilter, seg->nonempty_bits, dexists, n, seg->granule, gtile, gcount, goff, spec_list, -1, s,
+                           goff + nch, kSmallRows);
+        MQVS_HIP(hipGetLastError());
+    }
+
     // ---- the selected count (k_chunk_count's pinned record, polled with a
     // pause for up to kCountSpinUs; then -- or at once behind earlier work on
     // the caller's stream, or in MQVS_WAIT_BLOCK -- the host's wait)
@@ -1209,11 +1225,14 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     const int32_t *row_list = nullptr;
     int64_t scan_n = n;  // scan positions: rows, or gather-list entries
     if (gather) {
-        int32_t *list = (int32_t *)ws.get(ws.glist, sizeof(int32_t) * std::max<int64_t>(gpadded, 1));
-        // (the list's tail up to gpadded: -1 entries, written by the last chunk)
-        launch_gather_list(dfilter, seg->nonempty_bits, dexists, n, seg->granule, gtile, gcount, goff, list, gpadded,
-                           s);
-        MQVS_HIP(hipGetLastError());
+        int32_t *list = spec_list;
+        if (!list) {
+            list = (int32_t *)ws.get(ws.glist, sizeof(int32_t) * std::max<int64_t>(gpadded, 1));
+            // (the list's tail up to gpadded: -1 entries, written by the last chunk)
+            launch_gather_list(dfilter, seg->nonempty_bits, dexists, n, seg->granule, gtile, gcount, goff, list,
+                               gpadded, s);
+            MQVS_HIP(hipGetLastError());
+        }
         row_list = list;
         scan_n = gpadded;
         st.gather = 1;

@@ -255,7 +255,7 @@ void launch_gather_count(const uint8_t *filter, const uint8_t *nonempty, const u
                          int64_t *host_totals, int64_t host_gen, int *ticket, hipStream_t s);
 void launch_gather_list(const uint8_t *filter, const uint8_t *nonempty, const uint8_t *exists, int64_t n,
                         int64_t chunk_rows, int tile, const int *count, const int64_t *offsets, int32_t *list, int64_t list_end,
-                        hipStream_t s);
+                        hipStream_t s, const int64_t *dev_total = nullptr, int64_t round = 1);
 // Bound pruning of an index re-rank (kernels_rerank.hip): the candidates come
 // sorted by their approximate value; those more than 2 B past the k-th
 // approximate value cannot reach the exact top k and are not re-ranked (same
