@@ -859,6 +859,10 @@ static int large_k_batch(int64_t n, int k) {
     return (int)std::max<int64_t>(1, std::min(by_cand, by_probe));
 }
 
+// the gather list launched before the selected count is read (search_impl)
+// is sized for every row: up to 64M rows' worth
+constexpr size_t kSpecListBytes = (size_t)256 << 20;
+
 // Main-scan segmentation: the first segment is `first` probe lengths, each
 // next one `growth` times the previous; the probe aims at `target`
 // candidates.  Few queries: fewer, longer segments (each refinement is a
@@ -1175,10 +1179,15 @@ static void search_impl(mqvs_segment *seg, const float *queries, int nq, int k, 
     // for the count overlaps it.  Sized for every row (n entries plus the
     // chunks' tile padding); a search the count then sends to the mask scan
     // wasted one compaction beside a scan of >= 60 % of the part.
+    // (Parts whose worst-case list passes kSpecListBytes -- 64M rows -- keep
+    // the list sized by the count: the workspace peak is what admission
+    // reserves for the thread's next call.)
     int32_t *spec_list = nullptr;
-    if (selected >= 0 && (gather_mode == 2 || bf16_ok || (!bf16 && !mfma))) {
-        const int64_t nch = (n + seg->granule - 1) / seg->granule;
-        const int64_t worst = round_up(n + nch * (int64_t)(gtile - 1), kSmallRows);
+    const int64_t nch_all = (n + seg->granule - 1) / seg->granule;
+    const int64_t worst = round_up(n + nch_all * (int64_t)(gtile - 1), kSmallRows);
+    if (selected >= 0 && (gather_mode == 2 || bf16_ok || (!bf16 && !mfma)) &&
+        (size_t)worst * sizeof(int32_t) <= kSpecListBytes) {
+        const int64_t nch = nch_all;
         spec_list = (int32_t *)ws.get(ws.glist, sizeof(int32_t) * (size_t)std::max<int64_t>(worst, 1));
         launch_gather_list(dfilter, seg->nonempty_bits, dexists, n, seg->granule, gtile, gcount, goff, spec_list, -1, s,
                            goff + nch, kSmallRows);

@@ -130,6 +130,44 @@ def test_config1_flat_cosine_10M_x768_batch1000(mq, mode):
         seg.free()
 
 
+def test_config1_nq2_full_part_vs_oracle(mq):
+    """configs[1] at full size against the ORACLE, not the exact HIP path:
+    two queries (nq 2: the faiss sequential formula, with the per-chunk
+    cosine re-normalisation chain) over the whole 10M x 768 cosine part,
+    scanned by the C restatement of vectorScanWithoutIndex
+    (oracle/mqvs_oracle.c orc_vector_scan_fast) on the host -- ids and
+    distance bits equal.  The rows are the device generator's (copied to the
+    host: the C generator would take minutes single-threaded); the searched
+    segment generates them itself in HBM."""
+    import torch
+    from myscaledb_amd.vector_scan import generate_device
+    n, d, k, mode = 10_000_000, 768, 100, 1
+    seg = mq.VectorScanSegment.generate(SEED_BASE, mode, n, d, "Cosine", 8192)
+    try:
+        q = _dev_queries(SEED_QUERY, mode, 0, 2, d)
+        gi, gd = seg.search(q, k)
+        gi, gd = _np(gi), _np(gd)
+    finally:
+        seg.free()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    rows = np.empty((n, d), np.float32)
+    step = 1 << 20
+    t = torch.empty((step, d), dtype=torch.float32, device="cuda")
+    for r0 in range(0, n, step):
+        m = min(step, n - r0)
+        generate_device(SEED_BASE, mode, r0, m, d, t[:m])
+        rows[r0:r0 + m] = t[:m].cpu().numpy()
+    del t
+    # (spot check of the copied rows against the C generator)
+    for r in (0, 4_999_999, n - 1):
+        assert np.array_equal(rows[r], O.generate(SEED_BASE, mode, r, 1, d)[0])
+    oi, od = O.vector_scan(rows, q.cpu().numpy(), k, O.COSINE, 8192, fast=True)
+    del rows
+    assert np.array_equal(gi, oi), np.argwhere(gi != oi)[:4]
+    assert np.array_equal(_bits(gd), _bits(od)), np.argwhere(_bits(gd) != _bits(od))[:4]
+
+
 def test_config1_exact_variant_l2_10M_x768(mq):
     """configs[1] exact variant: L2 on exact integers, where
     every reduction order gives the same value -- bit-identical ids decided
