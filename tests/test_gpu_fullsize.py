@@ -168,6 +168,39 @@ def test_config1_nq2_full_part_vs_oracle(mq):
     assert np.array_equal(_bits(gd), _bits(od)), np.argwhere(_bits(gd) != _bits(od))[:4]
 
 
+def test_config1_full_part_l2_nq20_vs_oracle(mq):
+    """The same part under L2 at nq 20: the BLAS-branch formula (|q|^2 +
+    |y|^2 - 2 ip, the inner product one fma chain as the oracle assumes,
+    DESIGN 5) against the oracle's scan of 16 row-range parts on 16 threads,
+    merged by the reference's cross-part merge (one L2 variant: the parts'
+    union is the part) -- ids and distance bits equal
+    (tools/fullsize_l2_nq20_oracle.py as a test)."""
+    import torch
+    from myscaledb_amd.vector_scan import generate_device
+    n, d, k, mode, nq = 10_000_000, 768, 100, 1, 20
+    seg = mq.VectorScanSegment.generate(SEED_BASE, mode, n, d, "L2", 8192)
+    try:
+        q = _dev_queries(SEED_QUERY, mode, 0, nq, d)
+        gi, gd = seg.search(q, k)
+        gi, gd = _np(gi), _np(gd)
+    finally:
+        seg.free()
+        torch.cuda.synchronize()
+        torch.cuda.empty_cache()
+    rows = np.empty((n, d), np.float32)
+    step = 1 << 20
+    t = torch.empty((step, d), dtype=torch.float32, device="cuda")
+    for r0 in range(0, n, step):
+        m = min(step, n - r0)
+        generate_device(SEED_BASE, mode, r0, m, d, t[:m])
+        rows[r0:r0 + m] = t[:m].cpu().numpy()
+    del t
+    oi, od = O.scan_parts(rows, q.cpu().numpy(), k, O.L2, 8192, 16, 16)
+    del rows
+    assert np.array_equal(gi, oi), np.argwhere(gi != oi)[:4]
+    assert np.array_equal(_bits(gd), _bits(od)), np.argwhere(_bits(gd) != _bits(od))[:4]
+
+
 def test_config1_exact_variant_l2_10M_x768(mq):
     """configs[1] exact variant: L2 on exact integers, where
     every reduction order gives the same value -- bit-identical ids decided
